@@ -1,0 +1,218 @@
+"""Benchmark: V-cycles/sec of the MI355X AMG V-cycle on the 3D 7-point Laplace 216^3 (C4).
+
+One step = one multilevel weighted-Jacobi V(1,1)-cycle (the MLAMG.amg_2_v cycle of
+ns/preconditioner/MLAMG.py:189-195, applied recursively) over the whole 10,077,696-DoF problem,
+including the end-of-cycle residual norm (MLAMG.py:194). Setup (aggregation, lambda_max, SA
+prolongators, Galerkin, dense coarse inverse) runs on the GPU before timing and is reported
+separately.
+
+  python bench.py [--gpus N --steps K --warmup W] [--n 216] [--no-cpu-baseline]
+
+N > 1: launched by torch.distributed.run, one process per GPU; the fine level is row-partitioned
+(contiguous z-slabs) with an RCCL halo exchange, coarse levels are replicated (mlamg.distributed).
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "ml-amg_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "V-cycles/sec + fine-level SpMV GB/s (%HBM peak), 3D Laplace 10M DoF"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def spmv_bytes(n_rows, n_cols, nnz):
+    """12*nnz + 4*(n+1) + 8*n_cols (x) + 8*n (y)."""
+    return 12.0 * nnz + 4.0 * (n_rows + 1) + 8.0 * n_cols + 8.0 * n_rows
+
+
+def time_kernel(fn, reps=50):
+    """Average device time of fn() (one kernel launch on torch's current stream) via HIP events."""
+    s = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / 1000.0 / reps
+
+
+def load_traffic(name):
+    """HBM bytes per launch of the dominant kernel measured with rocprofv3 --pmc
+    (profiles/*_pmc.json written by tools/pmc_traffic.py), or None."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as fh:
+            return json.load(fh)
+    except Exception:
+        return None
+
+
+def cpu_baseline(H, b_host, x_host, cycles):
+    """Oracle (scipy restatement of the reference cycle) on the same hierarchy, 1 thread."""
+    from threadpoolctl import threadpool_limits
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    from oracle import restated as orc
+
+    levels = []
+    for L in H.levels:
+        A = L.A.to_scipy()
+        levels.append({"A": A, "P": L.P.to_scipy(), "Dw": sp.diags(L.dinv.cpu().numpy())})
+    Ac = H.Ac.to_scipy()
+    with threadpool_limits(limits=1):
+        lu = spla.factorized(sp.csc_matrix(Ac))
+        # one untimed cycle (page in), then the timed sample
+        orc.vcycle_solve(levels, Ac, b_host, x_host, 1, lu=lu)
+        t0 = time.perf_counter()
+        _, hist = orc.vcycle_solve(levels, Ac, b_host, x_host, cycles, lu=lu)
+        dt = time.perf_counter() - t0
+    return cycles / dt, dt, hist
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=216, help="grid points per dimension (C4: 216)")
+    ap.add_argument("--alpha", type=float, default=0.1)
+    ap.add_argument("--max-coarse", type=int, default=2000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-cycles", type=int, default=3)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        return run_distributed(args, world, rank, local_rank)
+
+    from mlamg import problems
+    from mlamg.hierarchy import Hierarchy
+
+    n1 = args.n
+    t0 = time.perf_counter()
+    A = problems.poisson_3d_7pt(n1)
+    log(f"C4 matrix {A.shape[0]} rows, {A.nnz} nnz built in {time.perf_counter() - t0:.1f}s")
+    H = Hierarchy.build(A, alpha=args.alpha, strength_mode="invabs", max_coarse=args.max_coarse,
+                        verbose=args.verbose)
+    setup_s = H.timings["total"]
+    for row in H.describe():
+        log(row)
+    n = A.shape[0]
+    x0 = np.random.RandomState(0).randn(n)
+    x0 /= np.linalg.norm(x0)
+    b = torch.zeros(n, dtype=torch.float64, device="cuda")
+    x = torch.as_tensor(x0).cuda()
+    use_graph = not args.no_graph
+    # convergence sample (also warms the graph)
+    hist = H.cycle(b, x, 10, use_graph=use_graph)
+    conv = float((hist[-1] / hist[-4]) ** (1.0 / 3.0)) if len(hist) >= 4 else float("nan")
+    log(f"residual history (10 cycles): {hist[0]:.3e} -> {hist[-1]:.3e}, conv factor {conv:.4f}")
+    x.copy_(torch.as_tensor(x0))
+    H.cycle_async(b, x, args.warmup, use_graph=use_graph)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    H.cycle_async(b, x, args.steps, use_graph=use_graph)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    cycles_per_s = args.steps / dt
+    ms_per_step = dt / args.steps * 1e3
+
+    # dominant kernel: the fine-level CSR SpMV (headline unit 1)
+    A0 = H.levels[0].A
+    xs = torch.randn(n, dtype=torch.float64, device="cuda")
+    ys = torch.empty_like(xs)
+    t_spmv = time_kernel(lambda: A0.matvec(xs, out=ys), reps=50)
+    B = spmv_bytes(n, n, A0.nnz)
+    achieved = B / t_spmv / 1e9
+    pmc = load_traffic("spmv_c4_pmc.json")
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    cyc_bytes = H.cycle_bytes()
+    out = {
+        "metric": METRIC,
+        "value": round(cycles_per_s, 3),
+        "unit": "V-cycles/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"C4: 3D 7-point Laplace {n1}^3 ({n} DoF, nnz {A0.nnz}), SA-AMG "
+                        f"V(1,1) weighted Jacobi w=2/3, seeded Bellman-Ford aggregates "
+                        f"alpha={args.alpha}, {H.n_levels} levels, dense coarse n={H.Ac.shape[0]}",
+            "n": n, "nnz": A0.nnz, "levels": H.n_levels,
+            "operator_complexity": round(H.operator_complexity(), 4),
+            "parallelism": "single GPU",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "fine-level CSR-stream SpMV (k_csr_stream<AXPBY>)",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": B,
+            "avg_launch_us": round(t_spmv * 1e6, 2),
+        },
+        "cycle_algorithmic_GBps": round(cyc_bytes / (dt / args.steps) / 1e9, 1),
+        "setup_s": {k: round(v, 3) for k, v in H.timings.items()},
+        "conv_factor_10cycles": round(conv, 5),
+    }
+    if not args.no_cpu_baseline:
+        b_h = np.zeros(n)
+        v, dtc, hcpu = cpu_baseline(H, b_h, x0, args.cpu_cycles)
+        # the CPU port and the device agree on the residual history (fp64 tolerance)
+        agree = bool(np.allclose(hcpu[: min(3, len(hist))], hist[: min(3, len(hcpu))],
+                                 rtol=1e-8))
+        out["cpu_baseline"] = {
+            "value": round(v, 5), "unit": "V-cycles/s", "cores": 1, "kind": "port",
+            "sample": f"{args.cpu_cycles} V-cycles of the same C4 hierarchy with the scipy "
+                      f"oracle (oracle/restated.py vcycle_solve), 1 thread, {dtc:.1f}s; "
+                      f"host nproc={os.cpu_count()}; residuals agree with GPU: {agree}",
+        }
+    print(json.dumps(out), flush=True)
+
+
+def run_distributed(args, world, rank, local_rank):
+    from mlamg import distributed
+    return distributed.bench_main(args, world, rank, local_rank, METRIC, HBM_PEAK_GBPS)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,200 @@
+/*
+ * mlamg.h — C-ABI of libmlamg_hip.so, the MI355X (gfx950) implementation of ml-amg's AMG V-cycle
+ * solve path (nicknytko/ml-amg: ns/lib/multigrid.py, ns/lib/graph.py, ns/lib/sparse.py,
+ * ns/preconditioner/MLAMG.py).
+ *
+ * The reference is pure Python; its "FFI" is the set of Python calls into scipy sparsetools,
+ * SuperLU, ARPACK and pyamg amg_core that the hot path makes. Each entry point below names the
+ * reference call (file:line) it replaces. The Python side (ml-amg_amd/mlamg/_lib.py) binds these
+ * with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - plain pointers and sizes only; no torch types. int32 CSR indices, fp64 values.
+ *  - every vector argument is a DEVICE pointer (e.g. torch.Tensor.data_ptr()) unless named *_host.
+ *  - `stream` is a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = default.
+ *    Calls are asynchronous on it; calls that return a host-visible value synchronise it.
+ *  - return 0 on success, a negative MLAMG_E* code on failure; message via mlamg_last_error()
+ *    (thread-local). Numerical breakdown (NaN) is not an error: it flows through the results,
+ *    as in the reference (utils/common.py:78-81 maps NaN conv factors itself).
+ *  - handles own their device memory unless created with MLAMG_WRAP_DEVICE.
+ */
+#ifndef MLAMG_H_
+#define MLAMG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MLAMG_OK 0
+#define MLAMG_EINVAL -1
+#define MLAMG_EHIP -2
+#define MLAMG_ENCCL -3
+#define MLAMG_ENOMEM -4
+#define MLAMG_EUNSUPPORTED -5
+
+/* where the arrays passed to mlamg_csr_create live */
+#define MLAMG_COPY_HOST 0    /* host arrays, copied to the device               */
+#define MLAMG_COPY_DEVICE 1  /* device arrays, copied                            */
+#define MLAMG_WRAP_DEVICE 2  /* device arrays, wrapped (caller keeps them alive) */
+
+typedef struct mlamg_csr mlamg_csr;
+typedef struct mlamg_dense mlamg_dense;
+typedef struct mlamg_hier mlamg_hier;
+typedef struct mlamg_gs mlamg_gs;
+typedef struct mlamg_comm mlamg_comm;
+
+/* ---------------------------------------------------------------- runtime */
+int mlamg_version(void);
+const char* mlamg_last_error(void);
+int mlamg_set_device(int dev);
+int mlamg_get_device(int* dev);
+int mlamg_stream_sync(void* stream);
+
+/* ---------------------------------------------------------------- CSR handles
+ * Replaces the scipy.sparse.csr_matrix objects the reference passes around
+ * (ns/lib/multigrid.py:111 A,P; ns/preconditioner/MLAMG.py:103 self.A) and the torch COO
+ * conversions of ns/lib/sparse.py:20-32,105-106. */
+int mlamg_csr_create(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t* indptr,
+                     const int32_t* indices, const double* data, int where, mlamg_csr** out);
+int mlamg_csr_destroy(mlamg_csr* A);
+int mlamg_csr_shape(const mlamg_csr* A, int64_t* n_rows, int64_t* n_cols, int64_t* nnz);
+int mlamg_csr_device_arrays(const mlamg_csr* A, int32_t** indptr, int32_t** indices,
+                            double** data);
+/* copy the arrays back to host buffers (indptr n_rows+1, indices/data nnz); syncs */
+int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indices_host,
+                       double* data_host);
+
+/* ---------------------------------------------------------------- hot-path sparse ops
+ * Each sums a row left-to-right in stored order with separate multiply and add roundings,
+ * i.e. exactly scipy sparsetools csr_matvec, so results are bitwise identical to the CPU path. */
+
+/* y = alpha*A@x + beta*y.  A@x: ns/lib/multigrid.py:181,191; MLAMG.py:145,191,194.
+ * alpha==1 && beta==0 gives A@x bit for bit. */
+int mlamg_spmv(const mlamg_csr* A, const double* x, double* y, double alpha, double beta,
+               void* stream);
+
+/* r = b - A@x; if norm2 != NULL, *norm2 (DEVICE scalar) = ||r||_2 (deterministic order).
+ * ns/lib/multigrid.py:181,191 (b - A@x), :191 la.norm; MLAMG.py:191,194. */
+int mlamg_residual(const mlamg_csr* A, const double* b, const double* x, double* r,
+                   double* norm2, void* stream);
+
+/* nu weighted-Jacobi sweeps, MLAMG form: x += Dinv@(b - A@x), Dinv = diag(1/a_ii)*omega
+ * pre-scaled (ns/preconditioner/MLAMG.py:104,143-146). x_tmp: scratch of n. Result lands in x. */
+int mlamg_jacobi(const mlamg_csr* A, const double* dinv_w, const double* b, double* x,
+                 double* x_tmp, int nu, void* stream);
+
+/* nu sweeps of ns/lib/multigrid.py:15-45 form: x += (w*Dinv)@b - ((w*Dinv)@A)@x.
+ * M must be the explicit (w*Dinv)@A built by mlamg_csr_scale_rows(reverse=1). */
+int mlamg_jacobi_explicit(const mlamg_csr* M, const double* dinv_w, const double* b, double* x,
+                          double* x_tmp, int nu, void* stream);
+
+/* r_c = R@r with R = P^T held explicitly (mlamg_transpose). Bitwise equal to scipy's
+ * csc_matvec of P.T@r (ns/lib/multigrid.py:181; MLAMG.py:191). */
+int mlamg_restrict(const mlamg_csr* R, const double* r, double* r_c, void* stream);
+
+/* x += P@e_c (ns/lib/multigrid.py:181 `x += P @ ...`; MLAMG.py:191). */
+int mlamg_prolong_add(const mlamg_csr* P, const double* e_c, double* x, void* stream);
+
+/* dinv_w[i] = (1.0/a_ii)*omega (MLAMG.py:104; multigrid.py:41,104). Missing diagonal -> 1/0. */
+int mlamg_diag_inv(const mlamg_csr* A, double omega, double* dinv_w, void* stream);
+
+/* *out (DEVICE scalar) = ||x||_2 (multigrid.py:193 la.norm(x, 2)). */
+int mlamg_norm2(const double* x, int64_t n, double* out, void* stream);
+
+/* ---------------------------------------------------------------- setup kernels */
+/* R = A^T, columns sorted (used for P.T; multigrid.py:165,181). */
+int mlamg_transpose(const mlamg_csr* A, mlamg_csr** out, void* stream);
+
+/* C = A@B with scipy csr_matmat semantics (multigrid.py:107 `smoother @ Agg`):
+ * C_ij = 0 + A_ik1*B_k1j + ... over k in the stored order of A's row i, exact zeros dropped, and
+ * each output row's columns in csr_matmat's order (reverse order of first appearance), so a
+ * later C@x sums in the same order as scipy. */
+int mlamg_spgemm(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out, void* stream);
+
+/* A_c = (R@A)@P, left-associative like `P.T@A@P` (multigrid.py:165; MLAMG.py:121), with R = P^T
+ * from mlamg_transpose. Every entry is summed over k ascending, as scipy's CSC kernels do for
+ * this expression, so values are bitwise scipy's; output columns sorted ascending. */
+int mlamg_galerkin(const mlamg_csr* R, const mlamg_csr* A, const mlamg_csr* P, mlamg_csr** out,
+                   void* stream);
+
+/* S = I - (omega*Dinv)@A with scipy rounding/zero-dropping (multigrid.py:104-106). */
+int mlamg_sa_smoother(const mlamg_csr* A, double omega, mlamg_csr** out, void* stream);
+
+/* M = diag(d)@A (row scaling) with zeros dropped; reverse!=0 stores each row's columns in
+ * descending order — the order scipy's csr_matmat emits for dia@csr (multigrid.py:44). */
+int mlamg_csr_scale_rows(const mlamg_csr* A, const double* d, int reverse, mlamg_csr** out,
+                         void* stream);
+
+/* lambda_max of Dinv@A (ARPACK eigs k=1 'LM' in multigrid.py:105) by Lanczos on the similar
+ * symmetric D^-1/2 A D^-1/2 (A symmetric with positive diagonal). *lam_host written; syncs. */
+int mlamg_lambda_max_dinvA(const mlamg_csr* A, int max_iter, double tol, uint64_t seed,
+                           double* lam_host, int* iters_host, void* stream);
+
+/* strength-of-connection graph (utils/common.py:26,28,29): mode 0 abs, 1 invabs, 2 unit. */
+int mlamg_strength(const mlamg_csr* A, int mode, mlamg_csr** out, void* stream);
+
+/* Seeded Bellman-Ford (ns/lib/graph.py:7-53) on edge weights G (row i -> col j, weight g_ij,
+ * evaluated in fp32 like the torch reference). dist_f32[n], cluster[n] (node id of the nearest
+ * seed, -1 if unreachable). Ties broken deterministically by the smallest seed node id.
+ * *iters_host = number of synchronous sweeps. Syncs. */
+int mlamg_bellman_ford(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* dist_f32,
+                       int32_t* cluster, int32_t* iters_host, void* stream);
+
+/* Agg (n x k, values 1.0) from a per-node column assignment col[n] (-1 = no aggregate):
+ * graph.py:56-86 nearest_center_to_agg and graph.py:234-238 AggOp. */
+int mlamg_aggregate_op(const int32_t* col, int64_t n, int64_t k, mlamg_csr** out, void* stream);
+
+/* map node-id labels to aggregate columns: col[i] = pos[label[i]] (graph.py:76-84). */
+int mlamg_labels_to_columns(const int32_t* label, int64_t n, const int32_t* seeds, int32_t k,
+                            int32_t* col, void* stream);
+
+/* pyamg 4.x lloyd_cluster (called at ns/lib/graph.py:232): up to maxiter rounds of
+ * {outward Bellman-Ford, boundary detection, inward Bellman-Ford, recentre}, fp64 distances.
+ * seeds (DEVICE, k) updated in place; dist[n], cluster[n] (aggregate index, -1 none). Syncs. */
+int mlamg_lloyd_cluster(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxiter, double* dist,
+                        int32_t* cluster, int32_t* iters_host, void* stream);
+
+/* ---------------------------------------------------------------- Gauss-Seidel
+ * pyamg relaxation.gauss_seidel (forward lexicographic, in place) used by the reference driver
+ * (ns/lib/multigrid.py:175,184). Exact lexicographic order via level scheduling of the row
+ * dependency DAG: bitwise identical to the sequential sweep. */
+int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream);
+int mlamg_gs_destroy(mlamg_gs* G);
+int mlamg_gs_levels(const mlamg_gs* G, int32_t* n_levels);
+int mlamg_gs_sweep(const mlamg_gs* G, double* x, const double* b, int iterations, void* stream);
+
+/* ---------------------------------------------------------------- coarse direct solve
+ * Replaces spla.factorized/splu (multigrid.py:168; MLAMG.py:122): the coarse operator is
+ * inverted densely on the device (Gauss-Jordan, partial pivoting, fp64) once; each solve is a
+ * dense GEMV. Returns MLAMG_EINVAL if the matrix is numerically singular. */
+int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream);
+int mlamg_dense_destroy(mlamg_dense* D);
+int mlamg_dense_solve(const mlamg_dense* D, const double* b, double* x, void* stream);
+
+/* ---------------------------------------------------------------- V-cycle executor
+ * Multilevel weighted-Jacobi V(nu1,nu2) cycle: the two-level cycle of MLAMG.py:189-195 applied
+ * recursively (the multilevel solver the PyAMG PC runs, PyAMG.py:94,119), coarsest level solved
+ * with mlamg_dense. Levels are added fine to coarse; the hierarchy keeps references to the
+ * handles (caller keeps them alive). */
+int mlamg_hier_create(mlamg_hier** out);
+int mlamg_hier_destroy(mlamg_hier* H);
+/* level l: A, dinv_w (device, n), P (n x n_next), R = P^T */
+int mlamg_hier_add_level(mlamg_hier* H, const mlamg_csr* A, const double* dinv_w,
+                         const mlamg_csr* P, const mlamg_csr* R);
+int mlamg_hier_set_coarse(mlamg_hier* H, const mlamg_csr* A_coarse, const mlamg_dense* D);
+int mlamg_hier_set_smoothing(mlamg_hier* H, int nu_pre, int nu_post);
+/* run n_cycles V-cycles on (b, x) (x updated in place). After each cycle ||b - A x||_2 is
+ * written to res_hist[c] (DEVICE, may be NULL). If tol > 0 the cycle loop stops after the first
+ * cycle with ||r|| <= tol (MLAMG.py:194); *cycles_done_host (nullable) receives the count and
+ * the call syncs. use_graph != 0 replays one captured hipGraph per cycle. */
+int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, double tol,
+                      double* res_hist, int32_t* cycles_done_host, int use_graph, void* stream);
+/* bytes one V-cycle moves by the algorithmic model of SURVEY.md §8(d) (for roofline reports) */
+int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MLAMG_H_ */

@@ -1,0 +1,95 @@
+// Internal types and helpers of libmlamg_hip (gfx950 / MI355X).
+//
+// Device-resident CSR handle, error plumbing for the C-ABI (include/mlamg.h), launch helpers.
+// Every floating-point kernel is compiled with -ffp-contract=off so that each multiply and add
+// rounds exactly like scipy's sparsetools loops (no FMA contraction); this is what makes the
+// SpMV / residual / Jacobi / restriction / prolongation results bitwise identical to the reference
+// CPU path (ns/lib/multigrid.py:44,181,191; ns/preconditioner/MLAMG.py:145,191,194).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "../../include/mlamg.h"
+
+namespace mlamg {
+
+// ---------------------------------------------------------------- errors
+void set_error(const std::string& msg);
+const char* get_error();
+
+#define MLAMG_HIP(call)                                                              \
+  do {                                                                               \
+    hipError_t _e = (call);                                                          \
+    if (_e != hipSuccess) {                                                          \
+      ::mlamg::set_error(std::string(#call) + " failed: " + hipGetErrorString(_e) +  \
+                         " (" + __FILE__ + ":" + std::to_string(__LINE__) + ")");    \
+      return MLAMG_EHIP;                                                             \
+    }                                                                                \
+  } while (0)
+
+#define MLAMG_REQUIRE(cond, msg)                                                     \
+  do {                                                                               \
+    if (!(cond)) {                                                                   \
+      ::mlamg::set_error(std::string(__func__) + ": " + (msg));                      \
+      return MLAMG_EINVAL;                                                           \
+    }                                                                                \
+  } while (0)
+
+#define MLAMG_TRY(call)                                                              \
+  do {                                                                               \
+    int _rc = (call);                                                                \
+    if (_rc != MLAMG_OK) return _rc;                                                 \
+  } while (0)
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------- CSR-stream geometry
+// A row block = up to kBlockRows consecutive rows whose nonzeros (<= kBlockNnz) are staged
+// through LDS by one 256-thread workgroup; a row longer than kBlockNnz gets a block of its own
+// and is streamed in kBlockNnz chunks.
+constexpr int kThreads = 256;
+constexpr int kBlockRows = 256;
+constexpr int kBlockNnz = 2048;   // 16 KiB of fp64 products in LDS per workgroup
+
+}  // namespace mlamg
+
+// Device CSR matrix. int32 indptr/indices, fp64 values (scipy's choice for these sizes:
+// SURVEY.md §8a). Column indices are sorted within rows unless `sorted` is false.
+struct mlamg_csr {
+  int64_t n_rows = 0, n_cols = 0, nnz = 0;
+  int32_t* indptr = nullptr;
+  int32_t* indices = nullptr;
+  double* data = nullptr;
+  bool owns = true;
+  int device = 0;
+  // CSR-stream row-block partition (device + host copies)
+  int32_t n_blocks = 0;
+  int32_t* blk = nullptr;             // n_blocks+1 row boundaries
+  std::vector<int32_t> blk_host;
+  int32_t max_row_len = 0;
+  double avg_row_len = 0.0;
+};
+
+// Dense coarse-level inverse (dense.hip)
+struct mlamg_dense {
+  int64_t n = 0;
+  double* inv = nullptr;  // row-major n x n
+};
+
+namespace mlamg {
+// Allocate device arrays for an (n_rows x n_cols, nnz) CSR and the handle; no partition yet.
+int csr_alloc(int64_t n_rows, int64_t n_cols, int64_t nnz, mlamg_csr** out);
+// Build the CSR-stream row-block partition from the device indptr (syncs `stream`).
+int csr_finalize(mlamg_csr* A, hipStream_t stream);
+void csr_free(mlamg_csr* A);
+
+// scratch buffer cache (per device); grows monotonically, freed at destroy/exit.
+void* scratch(size_t bytes, int slot);
+
+// generic kernels shared across translation units
+int launch_spmv_plain(const mlamg_csr* A, const double* x, double* y, hipStream_t s);
+int exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s);  // out[n] = total
+int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, hipStream_t s);
+}  // namespace mlamg

@@ -1,0 +1,336 @@
+// Multilevel weighted-Jacobi V-cycle executor.
+//
+// Per level l < L (fine to coarse), one cycle is the reference two-level cycle
+// (ns/preconditioner/MLAMG.py:189-195) with the coarse solve replaced by the next level:
+//     x += Dinv_w (b - A x)          nu_pre times          MLAMG.py:143-146,190
+//     b_{l+1} = R (b - A x)                                 MLAMG.py:191 (P.T @ (b - A@x))
+//     x_{l+1} = cycle(l+1, x0 = 0)  / dense solve at L     MLAMG.py:191 (A_H_lu.solve)
+//     x += P x_{l+1}                                        MLAMG.py:191
+//     x += Dinv_w (b - A x)          nu_post times         MLAMG.py:192
+// and at the finest level ||b - A x||_2 ends the cycle (MLAMG.py:194). That end-of-cycle
+// residual is exactly what the next cycle's first pre-smoothing sweep recomputes, so it is kept
+// and reused (same kernel, same bits), and the first sweep from a zero guess on coarse levels is
+// x = Dinv_w b (0 + d*(b - A@0) bit for bit). The tolerance test runs on the device: the norm
+// kernel raises a flag and every later kernel of the call returns immediately, so a whole batch
+// of cycles is launched (or replayed from one captured hipGraph) without host round trips.
+#include "common.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace mlamg {
+int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
+                  double* hist, int32_t* counter, int32_t* done, double tol, double* copy_to,
+                  const double* copy_from, double* partial, hipStream_t s);
+int jacobi_sweep(const mlamg_csr* A, const double* dinv, const double* b, const double* xin,
+                 double* xout, bool explicit_form, const int32_t* done, hipStream_t s);
+int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
+int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
+int jacobi_from_residual(double* x, const double* dinv, const double* r, int64_t n,
+                         const int32_t* done, hipStream_t s);
+int jacobi_from_zero(double* x, const double* dinv, const double* b, int64_t n,
+                     const int32_t* done, hipStream_t s);
+int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int32_t* done,
+                     hipStream_t s);
+}  // namespace mlamg
+
+namespace {
+struct Level {
+  const mlamg_csr* A = nullptr;
+  const double* dinv = nullptr;
+  const mlamg_csr* P = nullptr;
+  const mlamg_csr* R = nullptr;
+  int64_t n = 0;
+  double* x = nullptr;    // l > 0: iterate
+  double* b = nullptr;    // l > 0: right-hand side
+  double* r = nullptr;    // residual
+  double* tmp = nullptr;  // ping-pong partner of x
+};
+}  // namespace
+
+struct mlamg_hier {
+  std::vector<Level> lv;
+  const mlamg_csr* Ac = nullptr;
+  const mlamg_dense* D = nullptr;
+  double* xc = nullptr;
+  double* bc = nullptr;
+  int nu_pre = 1, nu_post = 1;
+  void* mem = nullptr;
+  size_t mem_bytes = 0;
+  double* partial = nullptr;
+  int32_t* flags = nullptr;  // [0] counter, [1] done
+  bool ready = false;
+  // captured single cycle
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  const double* g_b = nullptr;
+  double* g_x = nullptr;
+  double* g_hist = nullptr;
+  double g_tol = -1.0;
+  hipStream_t cap_stream = nullptr;
+};
+
+using namespace mlamg;
+
+static void hier_free_graph(mlamg_hier* H) {
+  if (H->exec) (void)hipGraphExecDestroy(H->exec);
+  if (H->graph) (void)hipGraphDestroy(H->graph);
+  H->exec = nullptr;
+  H->graph = nullptr;
+}
+
+static int hier_prepare(mlamg_hier* H) {
+  if (H->ready) return MLAMG_OK;
+  MLAMG_REQUIRE(!H->lv.empty() || H->D, "empty hierarchy");
+  MLAMG_REQUIRE(H->D != nullptr, "coarse solver not set (mlamg_hier_set_coarse)");
+  size_t total = 0;
+  auto add = [&](int64_t n) {
+    size_t b = sizeof(double) * (size_t)std::max<int64_t>(n, 1);
+    b = (b + 255) & ~size_t(255);
+    total += b;
+    return b;
+  };
+  for (size_t l = 0; l < H->lv.size(); ++l) {
+    const int64_t n = H->lv[l].n;
+    if (l > 0) {
+      add(n);
+      add(n);
+    }
+    add(n);
+    add(n);
+  }
+  const int64_t nc = H->D->n;
+  add(nc);
+  add(nc);
+  int64_t maxblk = 1;
+  for (auto& L : H->lv) maxblk = std::max<int64_t>(maxblk, L.A->n_blocks);
+  add(maxblk);
+  total += 256;
+  MLAMG_HIP(hipMalloc(&H->mem, total));
+  H->mem_bytes = total;
+  char* p = static_cast<char*>(H->mem);
+  auto take = [&](int64_t n) {
+    double* q = reinterpret_cast<double*>(p);
+    size_t b = sizeof(double) * (size_t)std::max<int64_t>(n, 1);
+    p += (b + 255) & ~size_t(255);
+    return q;
+  };
+  for (size_t l = 0; l < H->lv.size(); ++l) {
+    Level& L = H->lv[l];
+    if (l > 0) {
+      L.x = take(L.n);
+      L.b = take(L.n);
+    }
+    L.r = take(L.n);
+    L.tmp = take(L.n);
+  }
+  H->xc = take(nc);
+  H->bc = take(nc);
+  H->partial = take(maxblk);
+  H->flags = reinterpret_cast<int32_t*>(p);
+  MLAMG_HIP(hipMemset(H->mem, 0, total));
+  H->ready = true;
+  return MLAMG_OK;
+}
+
+// smoothing sweeps starting from `cur` (x or tmp); returns buffer holding the result
+static int smooth(const Level& L, const double* b, double*& cur, double* other, int nu,
+                  const int32_t* done, hipStream_t s) {
+  for (int i = 0; i < nu; ++i) {
+    MLAMG_TRY(jacobi_sweep(L.A, L.dinv, b, cur, other, false, done, s));
+    std::swap(cur, other);
+  }
+  return MLAMG_OK;
+}
+
+// one V-cycle below the finest level; result pointer returned through `res`
+static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, hipStream_t s) {
+  const int32_t* done = H->flags + 1;
+  if (l == H->lv.size()) {
+    MLAMG_TRY(dense_solve_impl(H->D, b, H->xc, done, s));
+    *res = H->xc;
+    return MLAMG_OK;
+  }
+  Level& L = H->lv[l];
+  double* cur = L.x;
+  double* other = L.tmp;
+  if (H->nu_pre > 0) {
+    MLAMG_TRY(jacobi_from_zero(cur, L.dinv, b, L.n, done, s));
+    MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre - 1, done, s));
+    MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, const_cast<int32_t*>(done),
+                            0.0, nullptr, nullptr, nullptr, s));
+  } else {
+    MLAMG_HIP(hipMemsetAsync(cur, 0, sizeof(double) * L.n, s));
+    MLAMG_HIP(hipMemcpyAsync(L.r, b, sizeof(double) * L.n, hipMemcpyDeviceToDevice, s));
+  }
+  double* bn = (l + 1 == H->lv.size()) ? H->bc : H->lv[l + 1].b;
+  MLAMG_TRY(spmv_set(L.R, L.r, bn, done, s));
+  double* xn = nullptr;
+  MLAMG_TRY(cycle_coarse(H, l + 1, bn, &xn, s));
+  MLAMG_TRY(spmv_add(L.P, xn, cur, done, s));
+  other = (cur == L.x) ? L.tmp : L.x;
+  MLAMG_TRY(smooth(L, b, cur, other, H->nu_post, done, s));
+  *res = cur;
+  return MLAMG_OK;
+}
+
+// one finest-level cycle; requires L0.r == b - A x on entry, leaves it so on exit
+static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, double tol,
+                     hipStream_t s) {
+  int32_t* counter = H->flags;
+  int32_t* done = H->flags + 1;
+  if (H->lv.empty()) {  // coarse-only hierarchy: x = A^-1 b
+    MLAMG_TRY(dense_solve_impl(H->D, b, x, done, s));
+    return MLAMG_OK;
+  }
+  Level& L = H->lv[0];
+  double* cur = x;
+  double* other = L.tmp;
+  if (H->nu_pre > 0) {
+    MLAMG_TRY(jacobi_from_residual(cur, L.dinv, L.r, L.n, done, s));
+    MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre - 1, done, s));
+    MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, done, 0.0, nullptr,
+                            nullptr, nullptr, s));
+  }
+  double* bn = (H->lv.size() == 1) ? H->bc : H->lv[1].b;
+  MLAMG_TRY(spmv_set(L.R, L.r, bn, done, s));
+  double* xn = nullptr;
+  MLAMG_TRY(cycle_coarse(H, 1, bn, &xn, s));
+  MLAMG_TRY(spmv_add(L.P, xn, cur, done, s));
+  other = (cur == x) ? L.tmp : x;
+  MLAMG_TRY(smooth(L, b, cur, other, H->nu_post, done, s));
+  // end-of-cycle residual + norm (+ copy the iterate back into x when it sits in tmp)
+  MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, hist, counter, done, tol,
+                          cur != x ? x : nullptr, cur != x ? cur : nullptr, H->partial, s));
+  return MLAMG_OK;
+}
+
+extern "C" {
+
+int mlamg_hier_create(mlamg_hier** out) {
+  MLAMG_REQUIRE(out, "out is NULL");
+  *out = new mlamg_hier();
+  return MLAMG_OK;
+}
+
+int mlamg_hier_destroy(mlamg_hier* H) {
+  if (!H) return MLAMG_OK;
+  hier_free_graph(H);
+  if (H->cap_stream) (void)hipStreamDestroy(H->cap_stream);
+  if (H->mem) (void)hipFree(H->mem);
+  delete H;
+  return MLAMG_OK;
+}
+
+int mlamg_hier_add_level(mlamg_hier* H, const mlamg_csr* A, const double* dinv_w,
+                         const mlamg_csr* P, const mlamg_csr* R) {
+  MLAMG_REQUIRE(H && A && dinv_w && P && R, "NULL argument");
+  MLAMG_REQUIRE(!H->ready, "hierarchy already finalised");
+  MLAMG_REQUIRE(A->n_rows == A->n_cols, "A must be square");
+  MLAMG_REQUIRE(P->n_rows == A->n_rows, "P rows != A rows");
+  MLAMG_REQUIRE(R->n_cols == A->n_rows && R->n_rows == P->n_cols, "R must be P^T");
+  if (!H->lv.empty()) {
+    MLAMG_REQUIRE(H->lv.back().P->n_cols == A->n_rows, "level sizes do not chain");
+  }
+  Level L;
+  L.A = A;
+  L.dinv = dinv_w;
+  L.P = P;
+  L.R = R;
+  L.n = A->n_rows;
+  H->lv.push_back(L);
+  return MLAMG_OK;
+}
+
+int mlamg_hier_set_coarse(mlamg_hier* H, const mlamg_csr* A_coarse, const mlamg_dense* D) {
+  MLAMG_REQUIRE(H && D, "NULL argument");
+  MLAMG_REQUIRE(!H->ready, "hierarchy already finalised");
+  if (!H->lv.empty())
+    MLAMG_REQUIRE(H->lv.back().P->n_cols == D->n, "coarse size does not match last P");
+  H->Ac = A_coarse;
+  H->D = D;
+  return MLAMG_OK;
+}
+
+int mlamg_hier_set_smoothing(mlamg_hier* H, int nu_pre, int nu_post) {
+  MLAMG_REQUIRE(H && nu_pre >= 0 && nu_post >= 0, "invalid argument");
+  H->nu_pre = nu_pre;
+  H->nu_post = nu_post;
+  hier_free_graph(H);
+  return MLAMG_OK;
+}
+
+int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, double tol,
+                      double* res_hist, int32_t* cycles_done_host, int use_graph, void* stream) {
+  MLAMG_REQUIRE(H && b && x, "NULL argument");
+  MLAMG_REQUIRE(b != x, "b and x must differ");
+  MLAMG_REQUIRE(n_cycles >= 0, "n_cycles < 0");
+  MLAMG_TRY(hier_prepare(H));
+  hipStream_t s = S(stream);
+  MLAMG_HIP(hipMemsetAsync(H->flags, 0, 2 * sizeof(int32_t), s));
+  if (!H->lv.empty()) {
+    Level& L = H->lv[0];
+    // r = b - A x for the first cycle's pre-smoothing sweep
+    MLAMG_TRY(residual_impl(L.A, b, x, L.r, nullptr, nullptr, nullptr, nullptr, 0.0, nullptr,
+                            nullptr, nullptr, s));
+  }
+  if (use_graph && n_cycles > 0 && !H->lv.empty()) {
+    if (!(H->exec && H->g_b == b && H->g_x == x && H->g_hist == res_hist && H->g_tol == tol)) {
+      hier_free_graph(H);
+      if (!H->cap_stream) MLAMG_HIP(hipStreamCreateWithFlags(&H->cap_stream, hipStreamNonBlocking));
+      MLAMG_HIP(hipStreamBeginCapture(H->cap_stream, hipStreamCaptureModeThreadLocal));
+      int rc = cycle_top(H, b, x, res_hist, tol, H->cap_stream);
+      hipGraph_t g = nullptr;
+      hipError_t e = hipStreamEndCapture(H->cap_stream, &g);
+      if (rc != MLAMG_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+      }
+      MLAMG_HIP(e);
+      H->graph = g;
+      MLAMG_HIP(hipGraphInstantiate(&H->exec, g, nullptr, nullptr, 0));
+      H->g_b = b;
+      H->g_x = x;
+      H->g_hist = res_hist;
+      H->g_tol = tol;
+    }
+    for (int c = 0; c < n_cycles; ++c) MLAMG_HIP(hipGraphLaunch(H->exec, s));
+  } else {
+    for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(cycle_top(H, b, x, res_hist, tol, s));
+  }
+  MLAMG_HIP(hipGetLastError());
+  if (cycles_done_host) {
+    int32_t cnt = 0;
+    MLAMG_HIP(hipMemcpyAsync(&cnt, H->flags, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipStreamSynchronize(s));
+    *cycles_done_host = H->lv.empty() ? n_cycles : cnt;
+  }
+  return MLAMG_OK;
+}
+
+static double spmv_bytes(const mlamg_csr* A) {
+  return 12.0 * A->nnz + 4.0 * (A->n_rows + 1) + 8.0 * A->n_cols + 8.0 * A->n_rows;
+}
+
+int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes) {
+  MLAMG_REQUIRE(H && bytes, "NULL argument");
+  double t = 0.0;
+  for (size_t l = 0; l < H->lv.size(); ++l) {
+    const Level& L = H->lv[l];
+    const double n = (double)L.n;
+    const double jac = spmv_bytes(L.A) + 16.0 * n;  // + b, dinv
+    const double res = spmv_bytes(L.A) + 8.0 * n;   // + b
+    if (H->nu_pre > 0) {
+      t += (l == 0) ? 32.0 * n : 24.0 * n;  // first sweep: elementwise
+      t += (H->nu_pre - 1) * jac + res;
+    }
+    t += spmv_bytes(L.R);
+    t += spmv_bytes(L.P) + 8.0 * n;  // + read x before the add
+    t += H->nu_post * jac;
+    if (l == 0) t += res;  // end-of-cycle residual norm
+  }
+  if (H->D) t += 8.0 * H->D->n * H->D->n + 16.0 * H->D->n;
+  *bytes = t;
+  return MLAMG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,231 @@
+// Runtime pieces of libmlamg_hip: error state, device CSR handle lifecycle, CSR-stream
+// partitioning, scratch buffers. Host C++ compiled by hipcc; no torch dependency.
+#include "common.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+
+namespace mlamg {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+const char* get_error() { return g_last_error.c_str(); }
+
+// ---------------------------------------------------------------- scratch
+namespace {
+struct Scratch {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_scratch_mu;
+std::vector<std::vector<Scratch>> g_scratch;  // [device][slot]
+}  // namespace
+
+void* scratch(size_t bytes, int slot) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  if ((int)g_scratch.size() <= dev) g_scratch.resize(dev + 1);
+  auto& v = g_scratch[dev];
+  if ((int)v.size() <= slot) v.resize(slot + 1);
+  Scratch& s = v[slot];
+  if (s.bytes < bytes) {
+    if (s.p) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(s.p);
+    }
+    s.p = nullptr;
+    s.bytes = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    if (hipMalloc(&s.p, want) != hipSuccess) return nullptr;
+    s.bytes = want;
+  }
+  return s.p;
+}
+
+// ---------------------------------------------------------------- CSR handle
+int csr_alloc(int64_t n_rows, int64_t n_cols, int64_t nnz, mlamg_csr** out) {
+  MLAMG_REQUIRE(out != nullptr, "out is NULL");
+  MLAMG_REQUIRE(n_rows >= 0 && n_cols >= 0 && nnz >= 0, "negative size");
+  MLAMG_REQUIRE(n_rows < (int64_t(1) << 31) - 1 && n_cols < (int64_t(1) << 31) - 1,
+                "dimension exceeds int32 index range");
+  MLAMG_REQUIRE(nnz < (int64_t(1) << 31) - 1, "nnz exceeds int32 indptr range");
+  auto* A = new mlamg_csr();
+  A->n_rows = n_rows;
+  A->n_cols = n_cols;
+  A->nnz = nnz;
+  A->owns = true;
+  (void)hipGetDevice(&A->device);
+  if (hipMalloc(&A->indptr, sizeof(int32_t) * (n_rows + 1)) != hipSuccess ||
+      hipMalloc(&A->indices, sizeof(int32_t) * std::max<int64_t>(nnz, 1)) != hipSuccess ||
+      hipMalloc(&A->data, sizeof(double) * std::max<int64_t>(nnz, 1)) != hipSuccess) {
+    csr_free(A);
+    set_error("csr_alloc: hipMalloc failed (out of device memory?)");
+    return MLAMG_ENOMEM;
+  }
+  *out = A;
+  return MLAMG_OK;
+}
+
+void csr_free(mlamg_csr* A) {
+  if (!A) return;
+  if (A->owns) {
+    if (A->indptr) (void)hipFree(A->indptr);
+    if (A->indices) (void)hipFree(A->indices);
+    if (A->data) (void)hipFree(A->data);
+  }
+  if (A->blk) (void)hipFree(A->blk);
+  delete A;
+}
+
+// Greedy row-block partition for the CSR-stream kernels: consecutive rows while the block has
+// <= kBlockRows rows and <= kBlockNnz nonzeros; an over-long row gets a block of its own.
+int csr_finalize(mlamg_csr* A, hipStream_t stream) {
+  const int64_t n = A->n_rows;
+  std::vector<int32_t> ip(n + 1);
+  MLAMG_HIP(hipMemcpyAsync(ip.data(), A->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost,
+                           stream));
+  MLAMG_HIP(hipStreamSynchronize(stream));
+  MLAMG_REQUIRE(ip[0] == 0, "indptr[0] != 0");
+  MLAMG_REQUIRE(ip[n] == A->nnz, "indptr[n] != nnz");
+  std::vector<int32_t>& blk = A->blk_host;
+  blk.clear();
+  blk.reserve(n / 64 + 2);
+  blk.push_back(0);
+  int32_t maxlen = 0;
+  int64_t r = 0;
+  while (r < n) {
+    int32_t len = ip[r + 1] - ip[r];
+    MLAMG_REQUIRE(len >= 0, "indptr not monotone");
+    if (len > kBlockNnz) {
+      maxlen = std::max(maxlen, len);
+      ++r;
+      blk.push_back((int32_t)r);
+      continue;
+    }
+    int64_t start = r;
+    int64_t nz = 0;
+    while (r < n && r - start < kBlockRows) {
+      len = ip[r + 1] - ip[r];
+      MLAMG_REQUIRE(len >= 0, "indptr not monotone");
+      if (nz + len > kBlockNnz) break;
+      maxlen = std::max(maxlen, len);
+      nz += len;
+      ++r;
+    }
+    blk.push_back((int32_t)r);
+  }
+  A->n_blocks = (int32_t)(blk.size() - 1);
+  A->max_row_len = maxlen;
+  A->avg_row_len = n ? double(A->nnz) / double(n) : 0.0;
+  if (A->blk) (void)hipFree(A->blk);
+  A->blk = nullptr;
+  MLAMG_HIP(hipMalloc(&A->blk, sizeof(int32_t) * blk.size()));
+  MLAMG_HIP(hipMemcpyAsync(A->blk, blk.data(), sizeof(int32_t) * blk.size(),
+                           hipMemcpyHostToDevice, stream));
+  MLAMG_HIP(hipStreamSynchronize(stream));
+  return MLAMG_OK;
+}
+
+}  // namespace mlamg
+
+using namespace mlamg;
+
+extern "C" {
+
+int mlamg_version(void) { return 10000; /* 0.1.0 */ }
+const char* mlamg_last_error(void) { return get_error(); }
+
+int mlamg_set_device(int dev) {
+  MLAMG_HIP(hipSetDevice(dev));
+  return MLAMG_OK;
+}
+int mlamg_get_device(int* dev) {
+  MLAMG_REQUIRE(dev, "dev is NULL");
+  MLAMG_HIP(hipGetDevice(dev));
+  return MLAMG_OK;
+}
+int mlamg_stream_sync(void* stream) {
+  MLAMG_HIP(hipStreamSynchronize(S(stream)));
+  return MLAMG_OK;
+}
+
+int mlamg_csr_create(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t* indptr,
+                     const int32_t* indices, const double* data, int where, mlamg_csr** out) {
+  MLAMG_REQUIRE(out != nullptr, "out is NULL");
+  MLAMG_REQUIRE(indptr != nullptr, "indptr is NULL");
+  MLAMG_REQUIRE(nnz == 0 || (indices && data), "indices/data NULL with nnz > 0");
+  MLAMG_REQUIRE(where >= 0 && where <= 2, "where must be 0 (host), 1 (device copy), 2 (wrap)");
+  hipStream_t s = nullptr;
+  mlamg_csr* A = nullptr;
+  if (where == MLAMG_WRAP_DEVICE) {
+    MLAMG_REQUIRE(n_rows >= 0 && n_cols >= 0 && nnz >= 0, "negative size");
+    A = new mlamg_csr();
+    A->n_rows = n_rows;
+    A->n_cols = n_cols;
+    A->nnz = nnz;
+    A->owns = false;
+    (void)hipGetDevice(&A->device);
+    A->indptr = const_cast<int32_t*>(indptr);
+    A->indices = const_cast<int32_t*>(indices);
+    A->data = const_cast<double*>(data);
+  } else {
+    MLAMG_TRY(csr_alloc(n_rows, n_cols, nnz, &A));
+    hipMemcpyKind k = where == MLAMG_COPY_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+    hipError_t e = hipMemcpyAsync(A->indptr, indptr, sizeof(int32_t) * (n_rows + 1), k, s);
+    if (e == hipSuccess && nnz)
+      e = hipMemcpyAsync(A->indices, indices, sizeof(int32_t) * nnz, k, s);
+    if (e == hipSuccess && nnz) e = hipMemcpyAsync(A->data, data, sizeof(double) * nnz, k, s);
+    if (e != hipSuccess) {
+      csr_free(A);
+      set_error(std::string("mlamg_csr_create: copy failed: ") + hipGetErrorString(e));
+      return MLAMG_EHIP;
+    }
+  }
+  int rc = csr_finalize(A, s);
+  if (rc != MLAMG_OK) {
+    csr_free(A);
+    return rc;
+  }
+  *out = A;
+  return MLAMG_OK;
+}
+
+int mlamg_csr_destroy(mlamg_csr* A) {
+  csr_free(A);
+  return MLAMG_OK;
+}
+
+int mlamg_csr_shape(const mlamg_csr* A, int64_t* n_rows, int64_t* n_cols, int64_t* nnz) {
+  MLAMG_REQUIRE(A, "A is NULL");
+  if (n_rows) *n_rows = A->n_rows;
+  if (n_cols) *n_cols = A->n_cols;
+  if (nnz) *nnz = A->nnz;
+  return MLAMG_OK;
+}
+
+int mlamg_csr_device_arrays(const mlamg_csr* A, int32_t** indptr, int32_t** indices,
+                            double** data) {
+  MLAMG_REQUIRE(A, "A is NULL");
+  if (indptr) *indptr = A->indptr;
+  if (indices) *indices = A->indices;
+  if (data) *data = A->data;
+  return MLAMG_OK;
+}
+
+int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indices_host,
+                       double* data_host) {
+  MLAMG_REQUIRE(A, "A is NULL");
+  if (indptr_host)
+    MLAMG_HIP(hipMemcpy(indptr_host, A->indptr, sizeof(int32_t) * (A->n_rows + 1),
+                        hipMemcpyDeviceToHost));
+  if (indices_host && A->nnz)
+    MLAMG_HIP(hipMemcpy(indices_host, A->indices, sizeof(int32_t) * A->nnz,
+                        hipMemcpyDeviceToHost));
+  if (data_host && A->nnz)
+    MLAMG_HIP(hipMemcpy(data_host, A->data, sizeof(double) * A->nnz, hipMemcpyDeviceToHost));
+  return MLAMG_OK;
+}
+
+}  // extern "C"

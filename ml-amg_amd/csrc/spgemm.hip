@@ -1,0 +1,522 @@
+// Setup-phase sparse kernels: transpose, SpGEMM (expand-sort-compress), Galerkin (R@A)@P,
+// smoothed-aggregation smoother S = I - (w*Dinv)@A, row scaling, strength-of-connection maps.
+//
+// Bitwise contract with scipy sparsetools (scipy 1.15.3, the version in this image):
+//  * csr_matmat sums C_ij = 0 + A_ik1*B_k1j + A_ik2*B_k2j + ... with k in the stored order of A's
+//    row i, and drops entries whose sum is exactly zero. Expand writes the products of row i in
+//    exactly that order; the segmented sort key (col << idx_bits | product index) is unique, so
+//    equal columns stay in product order and the compress pass reproduces the sum bit for bit.
+//  * P.T@A@P (multigrid.py:165, MLAMG.py:121) runs through scipy's CSC kernels, whose per-entry
+//    accumulation order is ascending k; R = P^T built here has ascending columns, so (R@A)@P
+//    with this SpGEMM (sorted-order mode for the intermediate) gives the same values; the
+//    Galerkin output is sorted (scipy's is an unsorted CSC; values do not depend on that).
+//  * csr_matmat emits each row's columns in reverse order of first appearance; mlamg_spgemm
+//    reproduces that layout (order mode 1), because it is the summation order of a later C@x.
+//  * (w*Dinv)@A (multigrid.py:44,106) goes dia -> csr -> csr_matmat, which emits a row's columns
+//    in reverse stored order; I - that (multigrid.py:106) goes through csr_binop_csr_general,
+//    which emits A's stored order without the diagonal, then the diagonal. Both orders matter
+//    downstream (they are the summation orders of the next product) and are reproduced here.
+#include "common.hpp"
+
+#include <rocprim/rocprim.hpp>
+
+namespace mlamg {
+
+static int bits_for(int64_t v) {  // bits to represent values in [0, v)
+  int b = 1;
+  while ((int64_t(1) << b) < v) ++b;
+  return b;
+}
+
+// ---------------------------------------------------------------- transpose
+__global__ void k_entry_rows(const int32_t* __restrict__ indptr, int64_t n, int32_t* __restrict__ rows) {
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  for (int k = indptr[i]; k < indptr[i + 1]; ++k) rows[k] = (int32_t)i;
+}
+
+__global__ void k_transpose_keys(const int32_t* __restrict__ rows, const int32_t* __restrict__ cols,
+                                 int64_t nnz, int rbits, uint64_t* __restrict__ keys,
+                                 int32_t* __restrict__ perm, int32_t* __restrict__ colcnt) {
+  int64_t e = blockIdx.x * 256ll + threadIdx.x;
+  if (e >= nnz) return;
+  const uint64_t c = (uint32_t)cols[e];
+  keys[e] = (c << rbits) | (uint32_t)rows[e];
+  perm[e] = (int32_t)e;
+  atomicAdd(&colcnt[c], 1);
+}
+
+__global__ void k_transpose_fill(const uint64_t* __restrict__ skeys, const int32_t* __restrict__ sperm,
+                                 const double* __restrict__ vals, int64_t nnz, uint64_t rmask,
+                                 int32_t* __restrict__ out_idx, double* __restrict__ out_val) {
+  int64_t e = blockIdx.x * 256ll + threadIdx.x;
+  if (e >= nnz) return;
+  out_idx[e] = (int32_t)(skeys[e] & rmask);
+  out_val[e] = vals[sperm[e]];
+}
+
+int transpose_impl(const mlamg_csr* A, mlamg_csr** out, hipStream_t s) {
+  mlamg_csr* T = nullptr;
+  MLAMG_TRY(csr_alloc(A->n_cols, A->n_rows, A->nnz, &T));
+  const int64_t nnz = A->nnz;
+  int32_t* colcnt = nullptr;
+  int32_t* rows = nullptr;
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  int32_t *p0 = nullptr, *p1 = nullptr;
+  void* tmp = nullptr;
+  int rc = MLAMG_OK;
+  auto fail = [&](hipError_t e, const char* what) {
+    set_error(std::string("transpose: ") + what + ": " + hipGetErrorString(e));
+    rc = MLAMG_EHIP;
+  };
+  hipError_t e = hipMalloc(&colcnt, sizeof(int32_t) * (A->n_cols + 1));
+  if (e == hipSuccess) e = hipMemsetAsync(colcnt, 0, sizeof(int32_t) * (A->n_cols + 1), s);
+  if (e == hipSuccess && nnz) {
+    e = hipMalloc(&rows, sizeof(int32_t) * nnz);
+    if (e == hipSuccess) e = hipMalloc(&k0, sizeof(uint64_t) * nnz);
+    if (e == hipSuccess) e = hipMalloc(&k1, sizeof(uint64_t) * nnz);
+    if (e == hipSuccess) e = hipMalloc(&p0, sizeof(int32_t) * nnz);
+    if (e == hipSuccess) e = hipMalloc(&p1, sizeof(int32_t) * nnz);
+  }
+  if (e != hipSuccess) fail(e, "alloc");
+  if (rc == MLAMG_OK && nnz) {
+    const int rbits = bits_for(std::max<int64_t>(A->n_rows, 2));
+    const int cbits = bits_for(std::max<int64_t>(A->n_cols, 2));
+    hipLaunchKernelGGL(k_entry_rows, dim3((A->n_rows + 255) / 256), dim3(256), 0, s, A->indptr,
+                       A->n_rows, rows);
+    hipLaunchKernelGGL(k_transpose_keys, dim3((nnz + 255) / 256), dim3(256), 0, s, rows,
+                       A->indices, nnz, rbits, k0, p0, colcnt);
+    size_t tb = 0;
+    e = rocprim::radix_sort_pairs(nullptr, tb, k0, k1, p0, p1, (size_t)nnz, 0, rbits + cbits, s);
+    if (e == hipSuccess) e = hipMalloc(&tmp, tb + 16);
+    if (e == hipSuccess)
+      e = rocprim::radix_sort_pairs(tmp, tb, k0, k1, p0, p1, (size_t)nnz, 0, rbits + cbits, s);
+    if (e != hipSuccess) fail(e, "sort");
+    if (rc == MLAMG_OK) {
+      hipLaunchKernelGGL(k_transpose_fill, dim3((nnz + 255) / 256), dim3(256), 0, s, k1, p1,
+                         A->data, nnz, (uint64_t(1) << rbits) - 1, T->indices, T->data);
+    }
+  }
+  if (rc == MLAMG_OK) rc = exclusive_scan_i32(colcnt, T->indptr, A->n_cols, s);
+  if (rc == MLAMG_OK) rc = csr_finalize(T, s);  // syncs
+  else (void)hipStreamSynchronize(s);
+  for (void* p : {(void*)colcnt, (void*)rows, (void*)k0, (void*)k1, (void*)p0, (void*)p1, tmp})
+    if (p) (void)hipFree(p);
+  if (rc != MLAMG_OK) {
+    csr_free(T);
+    return rc;
+  }
+  *out = T;
+  return MLAMG_OK;
+}
+
+// ---------------------------------------------------------------- SpGEMM (ESC)
+__global__ void k_count_products(const int32_t* __restrict__ ap, const int32_t* __restrict__ aj,
+                                 const int32_t* __restrict__ bp, int64_t n,
+                                 int64_t* __restrict__ cnt) {
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  int64_t c = 0;
+  for (int k = ap[i]; k < ap[i + 1]; ++k) {
+    const int j = aj[k];
+    c += bp[j + 1] - bp[j];
+  }
+  cnt[i] = c;
+}
+
+__global__ void k_row_max(const int64_t* __restrict__ cnt, int64_t n, unsigned long long* mx) {
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  atomicMax(mx, (unsigned long long)cnt[i]);
+}
+
+// products of row i in csr_matmat order: A's stored order, then B row's stored order
+__global__ void k_expand(const int32_t* __restrict__ ap, const int32_t* __restrict__ aj,
+                         const double* __restrict__ ax, const int32_t* __restrict__ bp,
+                         const int32_t* __restrict__ bj, const double* __restrict__ bx, int64_t n,
+                         const int64_t* __restrict__ off, int ibits, uint64_t* __restrict__ keys,
+                         double* __restrict__ prods) {
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  int64_t o = off[i];
+  uint32_t t = 0;
+  for (int k = ap[i]; k < ap[i + 1]; ++k) {
+    const int j = aj[k];
+    const double v = ax[k];
+    for (int kk = bp[j]; kk < bp[j + 1]; ++kk) {
+      keys[o + t] = ((uint64_t)(uint32_t)bj[kk] << ibits) | t;
+      prods[o + t] = v * bx[kk];
+      ++t;
+    }
+  }
+}
+
+// walk the sorted keys of row i; sum runs of equal columns in product order; keep nonzeros.
+// order 0: output columns ascending. order 1: scipy csr_matmat order — columns in reverse order
+// of their first appearance in the product stream (its linked list pushes each new column at
+// the head). prods[] entries are read exactly once, so a finished run's sum can be parked in
+// the slot of its first product.
+__global__ void k_compress(const uint64_t* __restrict__ keys, double* __restrict__ prods,
+                           const int64_t* __restrict__ off, int64_t n, int ibits, int order,
+                           int32_t* __restrict__ mark, int32_t* __restrict__ tcol,
+                           double* __restrict__ tval, int32_t* __restrict__ rowcnt) {
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  const int64_t a = off[i], b = off[i + 1];
+  const uint64_t imask = (uint64_t(1) << ibits) - 1;
+  int32_t m = 0;
+  int64_t p = a;
+  while (p < b) {
+    const uint64_t col = keys[p] >> ibits;
+    const int64_t tf = (int64_t)(keys[p] & imask);
+    double sum = 0.0;
+    while (p < b && (keys[p] >> ibits) == col) {
+      sum += prods[a + (int64_t)(keys[p] & imask)];
+      ++p;
+    }
+    if (sum != 0.0) {
+      if (order == 0) {
+        tcol[a + m] = (int32_t)col;
+        tval[a + m] = sum;
+        ++m;
+      } else {
+        prods[a + tf] = sum;
+        mark[a + tf] = (int32_t)col;
+      }
+    }
+  }
+  if (order != 0) {
+    for (int64_t t = b - 1; t >= a; --t) {
+      const int32_t c = mark[t];
+      if (c >= 0) {
+        tcol[a + m] = c;
+        tval[a + m] = prods[t];
+        ++m;
+      }
+    }
+  }
+  rowcnt[i] = m;
+}
+
+__global__ void k_scatter_rows(const int64_t* __restrict__ off, const int32_t* __restrict__ cip,
+                               const int32_t* __restrict__ tcol, const double* __restrict__ tval,
+                               int64_t n, int32_t* __restrict__ cj, double* __restrict__ cx) {
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  const int64_t a = off[i];
+  const int32_t o = cip[i];
+  const int32_t m = cip[i + 1] - o;
+  for (int32_t t = 0; t < m; ++t) {
+    cj[o + t] = tcol[a + t];
+    cx[o + t] = tval[a + t];
+  }
+}
+
+struct DevBuf {
+  std::vector<void*> ptrs;
+  ~DevBuf() {
+    for (void* p : ptrs)
+      if (p) (void)hipFree(p);
+  }
+  template <class T>
+  hipError_t get(T** p, size_t count) {
+    *p = nullptr;
+    hipError_t e = hipMalloc((void**)p, sizeof(T) * std::max<size_t>(count, 1));
+    if (e == hipSuccess) ptrs.push_back(*p);
+    return e;
+  }
+};
+
+#define DB_CHECK(expr)                                                          \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess) {                                                     \
+      set_error(std::string("spgemm: ") + #expr + ": " + hipGetErrorString(_e)); \
+      return MLAMG_EHIP;                                                        \
+    }                                                                           \
+  } while (0)
+
+int spgemm_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out, int order,
+                hipStream_t s) {
+  MLAMG_REQUIRE(A->n_cols == B->n_rows, "inner dimensions differ");
+  const int64_t n = A->n_rows;
+  DevBuf db;
+  int64_t* cnt = nullptr;
+  int64_t* off = nullptr;
+  unsigned long long* dmax = nullptr;
+  DB_CHECK(db.get(&cnt, n + 1));
+  DB_CHECK(db.get(&off, n + 1));
+  DB_CHECK(db.get(&dmax, 1));
+  DB_CHECK(hipMemsetAsync(dmax, 0, sizeof(unsigned long long), s));
+  if (n) {
+    hipLaunchKernelGGL(k_count_products, dim3((n + 255) / 256), dim3(256), 0, s, A->indptr,
+                       A->indices, B->indptr, n, cnt);
+    hipLaunchKernelGGL(k_row_max, dim3((n + 255) / 256), dim3(256), 0, s, cnt, n, dmax);
+  }
+  MLAMG_TRY(exclusive_scan_i64(cnt, off, n, s));
+  int64_t total = 0;
+  unsigned long long rmax = 0;
+  DB_CHECK(hipMemcpyAsync(&total, off + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  DB_CHECK(hipMemcpyAsync(&rmax, dmax, sizeof(rmax), hipMemcpyDeviceToHost, s));
+  DB_CHECK(hipStreamSynchronize(s));
+  MLAMG_REQUIRE(total < (int64_t(1) << 32) - 1, "too many intermediate products (>4G)");
+  const int ibits = bits_for(std::max<int64_t>((int64_t)rmax, 2));
+  const int cbits = bits_for(std::max<int64_t>(B->n_cols, 2));
+  MLAMG_REQUIRE(ibits + cbits <= 64, "key does not fit 64 bits");
+
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  double* prods = nullptr;
+  int32_t* tcol = nullptr;
+  double* tval = nullptr;
+  int32_t* rowcnt = nullptr;
+  DB_CHECK(db.get(&k0, total));
+  DB_CHECK(db.get(&k1, total));
+  DB_CHECK(db.get(&prods, total));
+  DB_CHECK(db.get(&tcol, total));
+  DB_CHECK(db.get(&tval, total));
+  DB_CHECK(db.get(&rowcnt, n + 1));
+  int32_t* mark = nullptr;
+  if (order != 0) {
+    DB_CHECK(db.get(&mark, total));
+    DB_CHECK(hipMemsetAsync(mark, 0xFF, sizeof(int32_t) * std::max<int64_t>(total, 1), s));
+  }
+  if (n) {
+    hipLaunchKernelGGL(k_expand, dim3((n + 255) / 256), dim3(256), 0, s, A->indptr, A->indices,
+                       A->data, B->indptr, B->indices, B->data, n, off, ibits, k0, prods);
+  }
+  if (total > 0) {
+    size_t tb = 0;
+    DB_CHECK(rocprim::segmented_radix_sort_keys(nullptr, tb, k0, k1, (unsigned)total, (unsigned)n,
+                                                off, off + 1, 0, ibits + cbits, s));
+    void* tmp = nullptr;
+    DB_CHECK(db.get((char**)&tmp, tb + 16));
+    DB_CHECK(rocprim::segmented_radix_sort_keys(tmp, tb, k0, k1, (unsigned)total, (unsigned)n,
+                                                off, off + 1, 0, ibits + cbits, s));
+  }
+  if (n) {
+    hipLaunchKernelGGL(k_compress, dim3((n + 255) / 256), dim3(256), 0, s, k1, prods, off, n,
+                       ibits, order, mark, tcol, tval, rowcnt);
+  }
+  int32_t* cip = nullptr;
+  DB_CHECK(db.get(&cip, n + 1));
+  MLAMG_TRY(exclusive_scan_i32(rowcnt, cip, n, s));
+  int32_t nnzc = 0;
+  DB_CHECK(hipMemcpyAsync(&nnzc, cip + n, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  DB_CHECK(hipStreamSynchronize(s));
+  mlamg_csr* C = nullptr;
+  MLAMG_TRY(csr_alloc(n, B->n_cols, nnzc, &C));
+  if (hipMemcpyAsync(C->indptr, cip, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToDevice, s) !=
+      hipSuccess) {
+    csr_free(C);
+    set_error("spgemm: indptr copy failed");
+    return MLAMG_EHIP;
+  }
+  if (n)
+    hipLaunchKernelGGL(k_scatter_rows, dim3((n + 255) / 256), dim3(256), 0, s, off, cip, tcol,
+                       tval, n, C->indices, C->data);
+  int rc = csr_finalize(C, s);  // syncs before DevBuf frees
+  if (rc != MLAMG_OK) {
+    csr_free(C);
+    return rc;
+  }
+  *out = C;
+  return MLAMG_OK;
+}
+
+// ---------------------------------------------------------------- row scaling / SA smoother
+// mode 0: M = diag(d)@A, reversed stored order, zeros dropped (csr_matmat of dia@csr)
+// mode 1: S = I - diag(d)@A in csr_binop_csr_general order (A's stored order sans diagonal,
+//         then the diagonal), zeros dropped
+__global__ void k_scale_count(const int32_t* __restrict__ ap, const int32_t* __restrict__ aj,
+                              const double* __restrict__ ax, const double* __restrict__ d,
+                              int64_t n, int mode, int32_t* __restrict__ cnt) {
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  const double di = d[i];
+  int32_t c = 0;
+  if (mode == 0) {
+    for (int k = ap[i]; k < ap[i + 1]; ++k) c += (di * ax[k] != 0.0);
+  } else {
+    double mdiag = 0.0;
+    for (int k = ap[i]; k < ap[i + 1]; ++k) {
+      const double m = di * ax[k];
+      if (aj[k] == (int32_t)i) {
+        mdiag = m;
+      } else {
+        c += (0.0 - m != 0.0);
+      }
+    }
+    c += (1.0 - mdiag != 0.0);
+  }
+  cnt[i] = c;
+}
+
+__global__ void k_scale_fill(const int32_t* __restrict__ ap, const int32_t* __restrict__ aj,
+                             const double* __restrict__ ax, const double* __restrict__ d,
+                             int64_t n, int mode, const int32_t* __restrict__ cp,
+                             int32_t* __restrict__ cj, double* __restrict__ cx) {
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  const double di = d[i];
+  int32_t o = cp[i];
+  if (mode == 0) {
+    for (int k = ap[i + 1] - 1; k >= ap[i]; --k) {
+      const double m = di * ax[k];
+      if (m != 0.0) {
+        cj[o] = aj[k];
+        cx[o] = m;
+        ++o;
+      }
+    }
+  } else {
+    double mdiag = 0.0;
+    for (int k = ap[i]; k < ap[i + 1]; ++k) {
+      const double m = di * ax[k];
+      if (aj[k] == (int32_t)i) {
+        mdiag = m;
+        continue;
+      }
+      const double v = 0.0 - m;
+      if (v != 0.0) {
+        cj[o] = aj[k];
+        cx[o] = v;
+        ++o;
+      }
+    }
+    const double v = 1.0 - mdiag;
+    if (v != 0.0) {
+      cj[o] = (int32_t)i;
+      cx[o] = v;
+    }
+  }
+}
+
+int scale_rows_impl(const mlamg_csr* A, const double* d, int mode, mlamg_csr** out,
+                    hipStream_t s) {
+  const int64_t n = A->n_rows;
+  DevBuf db;
+  int32_t* cnt = nullptr;
+  int32_t* cp = nullptr;
+  DB_CHECK(db.get(&cnt, n + 1));
+  DB_CHECK(db.get(&cp, n + 1));
+  if (n)
+    hipLaunchKernelGGL(k_scale_count, dim3((n + 255) / 256), dim3(256), 0, s, A->indptr,
+                       A->indices, A->data, d, n, mode, cnt);
+  MLAMG_TRY(exclusive_scan_i32(cnt, cp, n, s));
+  int32_t nnz = 0;
+  DB_CHECK(hipMemcpyAsync(&nnz, cp + n, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  DB_CHECK(hipStreamSynchronize(s));
+  mlamg_csr* C = nullptr;
+  MLAMG_TRY(csr_alloc(n, A->n_cols, nnz, &C));
+  if (hipMemcpyAsync(C->indptr, cp, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToDevice, s) !=
+      hipSuccess) {
+    csr_free(C);
+    set_error("scale_rows: copy failed");
+    return MLAMG_EHIP;
+  }
+  if (n)
+    hipLaunchKernelGGL(k_scale_fill, dim3((n + 255) / 256), dim3(256), 0, s, A->indptr,
+                       A->indices, A->data, d, n, mode, cp, C->indices, C->data);
+  int rc = csr_finalize(C, s);
+  if (rc != MLAMG_OK) {
+    csr_free(C);
+    return rc;
+  }
+  *out = C;
+  return MLAMG_OK;
+}
+
+int diag_inv_impl(const mlamg_csr* A, double omega, double* dinv, hipStream_t s);
+
+// ---------------------------------------------------------------- strength / distance maps
+// mode 0 abs |a| (common.py:26; graph.py:204), 1 inverse 1/|a| (common.py:28; graph.py:206),
+// 2 unit 1 (common.py:29; graph.py:202), 3 same a (graph.py:208)
+__global__ void k_strength(const double* __restrict__ x, int64_t nnz, int mode,
+                           double* __restrict__ y) {
+  int64_t e = blockIdx.x * 256ll + threadIdx.x;
+  if (e >= nnz) return;
+  const double v = x[e];
+  double r;
+  switch (mode) {
+    case 0: r = fabs(v); break;
+    case 1: r = 1.0 / fabs(v); break;
+    case 2: r = 1.0; break;
+    default: r = v; break;
+  }
+  y[e] = r;
+}
+
+}  // namespace mlamg
+
+using namespace mlamg;
+
+extern "C" {
+
+int mlamg_transpose(const mlamg_csr* A, mlamg_csr** out, void* stream) {
+  MLAMG_REQUIRE(A && out, "NULL argument");
+  return transpose_impl(A, out, S(stream));
+}
+
+int mlamg_spgemm(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out, void* stream) {
+  MLAMG_REQUIRE(A && B && out, "NULL argument");
+  return spgemm_impl(A, B, out, 1, S(stream));
+}
+
+int mlamg_galerkin(const mlamg_csr* R, const mlamg_csr* A, const mlamg_csr* P, mlamg_csr** out,
+                   void* stream) {
+  MLAMG_REQUIRE(R && A && P && out, "NULL argument");
+  MLAMG_REQUIRE(R->n_cols == A->n_rows && A->n_cols == P->n_rows, "shape mismatch");
+  mlamg_csr* M = nullptr;
+  MLAMG_TRY(spgemm_impl(R, A, &M, 0, S(stream)));
+  int rc = spgemm_impl(M, P, out, 0, S(stream));
+  csr_free(M);
+  return rc;
+}
+
+int mlamg_csr_scale_rows(const mlamg_csr* A, const double* d, int reverse, mlamg_csr** out,
+                         void* stream) {
+  MLAMG_REQUIRE(A && d && out, "NULL argument");
+  MLAMG_REQUIRE(reverse == 1, "only the scipy dia@csr (reverse=1) order is implemented");
+  return scale_rows_impl(A, d, 0, out, S(stream));
+}
+
+int mlamg_sa_smoother(const mlamg_csr* A, double omega, mlamg_csr** out, void* stream) {
+  MLAMG_REQUIRE(A && out, "NULL argument");
+  MLAMG_REQUIRE(A->n_rows == A->n_cols, "square matrix required");
+  double* d = nullptr;
+  MLAMG_HIP(hipMalloc(&d, sizeof(double) * std::max<int64_t>(A->n_rows, 1)));
+  int rc = mlamg_diag_inv(A, omega, d, stream);
+  if (rc == MLAMG_OK) rc = scale_rows_impl(A, d, 1, out, S(stream));
+  (void)hipStreamSynchronize(S(stream));
+  (void)hipFree(d);
+  return rc;
+}
+
+int mlamg_strength(const mlamg_csr* A, int mode, mlamg_csr** out, void* stream) {
+  MLAMG_REQUIRE(A && out, "NULL argument");
+  MLAMG_REQUIRE(mode >= 0 && mode <= 3, "mode must be 0 abs, 1 inv, 2 unit, 3 same");
+  hipStream_t s = S(stream);
+  mlamg_csr* C = nullptr;
+  MLAMG_TRY(csr_alloc(A->n_rows, A->n_cols, A->nnz, &C));
+  hipError_t e =
+      hipMemcpyAsync(C->indptr, A->indptr, sizeof(int32_t) * (A->n_rows + 1), hipMemcpyDeviceToDevice, s);
+  if (e == hipSuccess && A->nnz)
+    e = hipMemcpyAsync(C->indices, A->indices, sizeof(int32_t) * A->nnz, hipMemcpyDeviceToDevice, s);
+  if (e != hipSuccess) {
+    csr_free(C);
+    set_error("strength: copy failed");
+    return MLAMG_EHIP;
+  }
+  if (A->nnz)
+    hipLaunchKernelGGL(k_strength, dim3((A->nnz + 255) / 256), dim3(256), 0, s, A->data, A->nnz,
+                       mode, C->data);
+  int rc = csr_finalize(C, s);
+  if (rc != MLAMG_OK) {
+    csr_free(C);
+    return rc;
+  }
+  *out = C;
+  return MLAMG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,294 @@
+// CSR-stream SpMV family for gfx950 — the hot path of the V-cycle.
+//
+// One 256-thread workgroup per row block (<= 256 rows, <= 2048 nonzeros, built once per handle
+// in runtime.cpp). Phase 1 streams the block's contiguous column-index and value ranges with
+// fully coalesced loads (lane e reads nonzero e), gathers x[col] and writes the fp64 product
+// into LDS. Phase 2 gives each row to one lane, which sums its products left to right from LDS
+// and applies the fused epilogue. Summing in stored order with no FMA contraction
+// (-ffp-contract=off) reproduces scipy sparsetools csr_matvec bit for bit:
+//     sum = 0; for jj in row: sum += Ax[jj] * x[Aj[jj]]
+// Epilogues cover every use of A@x in the reference V-cycle:
+//   AXPBY   y = A@x (alpha=1,beta=0) or alpha*A@x + beta*y        multigrid.py:181 (P@e)
+//   RESID   r = b - A@x  (+ per-block sum of r^2)                  multigrid.py:181,191
+//   JACOBI  y = x + dinv_w*(b - A@x)                               MLAMG.py:145
+//   JACEXP  y = x + (dinv_w*b - M@x), M = (w*Dinv)@A explicit      multigrid.py:44
+//   ADD     y = y + A@x                                            multigrid.py:181 (x += P@e)
+// Roofline: HBM-bound. Algorithmic bytes per call = 12*nnz + 4*(n+1) + 8*n_cols + 8*n (+8n per
+// extra vector the epilogue reads/writes), SURVEY.md §8(d).
+#include "common.hpp"
+
+namespace mlamg {
+
+enum EpiOp : int { EPI_AXPBY = 0, EPI_RESID = 1, EPI_JACOBI = 2, EPI_JACEXP = 3, EPI_ADD = 4 };
+
+struct Epi {
+  double alpha, beta;
+  const double* b;
+  const double* xin;   // JACOBI/JACEXP: x (old iterate)
+  const double* dinv;  // JACOBI/JACEXP
+  double* y;           // output
+  double* copy_to;     // RESID: optional x copy-back (copy_to[i] = x[i]) — used by the V-cycle
+  const double* copy_from;
+  double* partial;     // RESID: per-block sum of r^2 (nullable)
+  const int32_t* done; // nullable: device flag; nonzero -> kernel is a no-op
+};
+
+template <int OP>
+__device__ __forceinline__ double epilogue(int row, double s, const Epi& e) {
+  if constexpr (OP == EPI_AXPBY) {
+    if (e.beta == 0.0) {
+      e.y[row] = (e.alpha == 1.0) ? s : e.alpha * s;
+    } else {
+      e.y[row] = e.alpha * s + e.beta * e.y[row];
+    }
+    return 0.0;
+  } else if constexpr (OP == EPI_RESID) {
+    const double r = e.b[row] - s;
+    e.y[row] = r;
+    if (e.copy_to) e.copy_to[row] = e.copy_from[row];
+    return r * r;
+  } else if constexpr (OP == EPI_JACOBI) {
+    const double r = e.b[row] - s;
+    e.y[row] = e.xin[row] + e.dinv[row] * r;
+    return 0.0;
+  } else if constexpr (OP == EPI_JACEXP) {
+    const double t1 = e.dinv[row] * e.b[row];
+    e.y[row] = e.xin[row] + (t1 - s);
+    return 0.0;
+  } else {  // EPI_ADD
+    e.y[row] = e.y[row] + s;
+    return 0.0;
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int OP, bool NORM>
+__global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restrict__ indptr,
+                                                         const int32_t* __restrict__ indices,
+                                                         const double* __restrict__ vals,
+                                                         const int32_t* __restrict__ blk,
+                                                         const double* __restrict__ x, Epi ep) {
+  __shared__ double prod[kBlockNnz];
+  __shared__ int32_t rp[kBlockRows + 1];
+  __shared__ double red[kThreads / 64];
+  if (ep.done && *ep.done) return;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int r0 = blk[b];
+  const int r1 = blk[b + 1];
+  const int nr = r1 - r0;
+  const int e0 = indptr[r0];
+  const int ne = indptr[r1] - e0;
+  double sq = 0.0;
+  if (ne <= kBlockNnz) {
+    for (int t = tid; t <= nr; t += kThreads) rp[t] = indptr[r0 + t] - e0;
+    const int32_t* ci = indices + e0;
+    const double* cv = vals + e0;
+    for (int e = tid; e < ne; e += kThreads) prod[e] = cv[e] * x[ci[e]];
+    __syncthreads();
+    for (int t = tid; t < nr; t += kThreads) {
+      double s = 0.0;
+      const int ka = rp[t], kb = rp[t + 1];
+      for (int k = ka; k < kb; ++k) s += prod[k];
+      sq += epilogue<OP>(r0 + t, s, ep);
+    }
+  } else {
+    // one over-long row: stream it through LDS in chunks, lane 0 keeps the ordered sum
+    double s = 0.0;
+    for (int c = 0; c < ne; c += kBlockNnz) {
+      const int m = min(kBlockNnz, ne - c);
+      for (int e = tid; e < m; e += kThreads) prod[e] = vals[e0 + c + e] * x[indices[e0 + c + e]];
+      __syncthreads();
+      if (tid == 0)
+        for (int k = 0; k < m; ++k) s += prod[k];
+      __syncthreads();
+    }
+    if (tid == 0) sq += epilogue<OP>(r0, s, ep);
+  }
+  if constexpr (NORM) {
+    // fixed-order block reduction -> deterministic partials
+    double w = wave_sum(sq);
+    if ((tid & 63) == 0) red[tid >> 6] = w;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+      for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+      ep.partial[b] = t;
+    }
+  }
+}
+
+// Sum `n` partials in a fixed order with one workgroup, write sqrt to out (device scalar),
+// optionally also to hist[*counter] and raise done flag when <= tol.
+__global__ __launch_bounds__(1024) void k_finalize_norm(const double* __restrict__ partial, int n,
+                                                        double* out, double* hist,
+                                                        int32_t* counter, int32_t* done,
+                                                        double tol) {
+  __shared__ double red[16];
+  if (done && *done) return;
+  const int tid = threadIdx.x;
+  double s = 0.0;
+  for (int i = tid; i < n; i += 1024) s += partial[i];
+  s = wave_sum(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0.0;
+    for (int i = 0; i < 16; ++i) t += red[i];
+    const double nrm = sqrt(t);
+    if (out) *out = nrm;
+    const int c = counter ? *counter : 0;
+    if (hist) hist[c] = nrm;
+    if (counter) *counter = c + 1;
+    if (done && tol > 0.0 && nrm <= tol) *done = 1;
+  }
+}
+
+// ---------------------------------------------------------------- launch helpers
+template <int OP, bool NORM>
+static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  if (A->n_blocks == 0) return MLAMG_OK;
+  hipLaunchKernelGGL((k_csr_stream<OP, NORM>), dim3(A->n_blocks), dim3(kThreads), 0, s,
+                     A->indptr, A->indices, A->data, A->blk, x, ep);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+int launch_spmv_plain(const mlamg_csr* A, const double* x, double* y, hipStream_t s) {
+  Epi ep{};
+  ep.alpha = 1.0;
+  ep.beta = 0.0;
+  ep.y = y;
+  return launch<EPI_AXPBY, false>(A, x, ep, s);
+}
+
+// per-handle partial buffer for residual norms (slot 0 of the scratch cache is shared:
+// callers on one stream only)
+static double* partial_buf(const mlamg_csr* A) {
+  return static_cast<double*>(scratch(sizeof(double) * (A->n_blocks + 1), 0));
+}
+
+int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
+                  double* hist, int32_t* counter, int32_t* done, double tol, double* copy_to,
+                  const double* copy_from, double* partial, hipStream_t s) {
+  Epi ep{};
+  ep.b = b;
+  ep.y = r;
+  ep.done = done;
+  ep.copy_to = copy_to;
+  ep.copy_from = copy_from;
+  const bool want = norm2 || hist || counter;
+  if (!want) return launch<EPI_RESID, false>(A, x, ep, s);
+  ep.partial = partial ? partial : partial_buf(A);
+  MLAMG_REQUIRE(ep.partial, "scratch allocation failed");
+  MLAMG_TRY((launch<EPI_RESID, true>(A, x, ep, s)));
+  hipLaunchKernelGGL(k_finalize_norm, dim3(1), dim3(1024), 0, s, ep.partial, A->n_blocks, norm2,
+                     hist, counter, done, tol);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+int jacobi_sweep(const mlamg_csr* A, const double* dinv, const double* b, const double* xin,
+                 double* xout, bool explicit_form, const int32_t* done, hipStream_t s) {
+  Epi ep{};
+  ep.b = b;
+  ep.xin = xin;
+  ep.dinv = dinv;
+  ep.y = xout;
+  ep.done = done;
+  if (explicit_form) return launch<EPI_JACEXP, false>(A, xin, ep, s);
+  return launch<EPI_JACOBI, false>(A, xin, ep, s);
+}
+
+int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s) {
+  Epi ep{};
+  ep.y = y;
+  ep.done = done;
+  return launch<EPI_ADD, false>(A, x, ep, s);
+}
+
+int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s) {
+  Epi ep{};
+  ep.alpha = 1.0;
+  ep.beta = 0.0;
+  ep.y = y;
+  ep.done = done;
+  return launch<EPI_AXPBY, false>(A, x, ep, s);
+}
+
+}  // namespace mlamg
+
+using namespace mlamg;
+
+extern "C" {
+
+int mlamg_spmv(const mlamg_csr* A, const double* x, double* y, double alpha, double beta,
+               void* stream) {
+  MLAMG_REQUIRE(A && (A->n_rows == 0 || (x && y)), "NULL argument");
+  Epi ep{};
+  ep.alpha = alpha;
+  ep.beta = beta;
+  ep.y = y;
+  return launch<EPI_AXPBY, false>(A, x, ep, S(stream));
+}
+
+int mlamg_residual(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
+                   void* stream) {
+  MLAMG_REQUIRE(A && (A->n_rows == 0 || (b && x && r)), "NULL argument");
+  MLAMG_REQUIRE(A->n_rows == A->n_cols, "residual needs a square matrix");
+  return residual_impl(A, b, x, r, norm2, nullptr, nullptr, nullptr, 0.0, nullptr, nullptr,
+                       nullptr, S(stream));
+}
+
+int mlamg_jacobi(const mlamg_csr* A, const double* dinv_w, const double* b, double* x,
+                 double* x_tmp, int nu, void* stream) {
+  MLAMG_REQUIRE(A && (A->n_rows == 0 || (dinv_w && b && x && x_tmp)), "NULL argument");
+  MLAMG_REQUIRE(A->n_rows == A->n_cols, "jacobi needs a square matrix");
+  MLAMG_REQUIRE(nu >= 0, "nu < 0");
+  MLAMG_REQUIRE(x != x_tmp, "x_tmp must differ from x");
+  hipStream_t s = S(stream);
+  double* cur = x;
+  double* nxt = x_tmp;
+  for (int i = 0; i < nu; ++i) {
+    MLAMG_TRY(jacobi_sweep(A, dinv_w, b, cur, nxt, false, nullptr, s));
+    std::swap(cur, nxt);
+  }
+  if (cur != x)
+    MLAMG_HIP(hipMemcpyAsync(x, cur, sizeof(double) * A->n_rows, hipMemcpyDeviceToDevice, s));
+  return MLAMG_OK;
+}
+
+int mlamg_jacobi_explicit(const mlamg_csr* M, const double* dinv_w, const double* b, double* x,
+                          double* x_tmp, int nu, void* stream) {
+  MLAMG_REQUIRE(M && (M->n_rows == 0 || (dinv_w && b && x && x_tmp)), "NULL argument");
+  MLAMG_REQUIRE(M->n_rows == M->n_cols, "jacobi needs a square matrix");
+  MLAMG_REQUIRE(nu >= 0, "nu < 0");
+  MLAMG_REQUIRE(x != x_tmp, "x_tmp must differ from x");
+  hipStream_t s = S(stream);
+  double* cur = x;
+  double* nxt = x_tmp;
+  for (int i = 0; i < nu; ++i) {
+    MLAMG_TRY(jacobi_sweep(M, dinv_w, b, cur, nxt, true, nullptr, s));
+    std::swap(cur, nxt);
+  }
+  if (cur != x)
+    MLAMG_HIP(hipMemcpyAsync(x, cur, sizeof(double) * M->n_rows, hipMemcpyDeviceToDevice, s));
+  return MLAMG_OK;
+}
+
+int mlamg_restrict(const mlamg_csr* R, const double* r, double* r_c, void* stream) {
+  MLAMG_REQUIRE(R && (R->n_rows == 0 || (r && r_c)), "NULL argument");
+  return spmv_set(R, r, r_c, nullptr, S(stream));
+}
+
+int mlamg_prolong_add(const mlamg_csr* P, const double* e_c, double* x, void* stream) {
+  MLAMG_REQUIRE(P && (P->n_rows == 0 || (e_c && x)), "NULL argument");
+  return spmv_add(P, e_c, x, nullptr, S(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,134 @@
+"""ctypes binding of libmlamg_hip.so (C-ABI declared in include/mlamg.h).
+
+torch is imported first on purpose: torch ships its own libamdhip64.so.7, and loading it before
+this library makes both share one HIP runtime (the .so resolves libamdhip64.so.7 by soname), so
+device pointers and streams from torch are valid here.
+
+There is no CPU fallback: if the library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before the HIP library, see module doc)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MLAMG_LIB", os.path.join(_HERE, "libmlamg_hip.so"))
+
+MLAMG_OK = 0
+MLAMG_EINVAL = -1
+MLAMG_EHIP = -2
+MLAMG_ENCCL = -3
+MLAMG_ENOMEM = -4
+MLAMG_EUNSUPPORTED = -5
+
+MLAMG_COPY_HOST = 0
+MLAMG_COPY_DEVICE = 1
+MLAMG_WRAP_DEVICE = 2
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"libmlamg_hip.so not found at {LIB_PATH}; build it with "
+        "`python ml-amg_amd/build_native.py` (or __graft_entry__.build()). "
+        "The MI355X path has no CPU fallback."
+    )
+
+lib = ctypes.CDLL(LIB_PATH)
+
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_int = ctypes.c_int
+c_dbl = ctypes.c_double
+c_vp = ctypes.c_void_p
+c_vpp = ctypes.POINTER(ctypes.c_void_p)
+P_i32 = ctypes.POINTER(ctypes.c_int32)
+P_i64 = ctypes.POINTER(ctypes.c_int64)
+P_dbl = ctypes.POINTER(ctypes.c_double)
+P_int = ctypes.POINTER(ctypes.c_int)
+
+# name -> (restype, argtypes); every symbol of include/mlamg.h
+SIGNATURES = {
+    "mlamg_version": (c_int, []),
+    "mlamg_last_error": (ctypes.c_char_p, []),
+    "mlamg_set_device": (c_int, [c_int]),
+    "mlamg_get_device": (c_int, [P_int]),
+    "mlamg_stream_sync": (c_int, [c_vp]),
+    "mlamg_csr_create": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vpp]),
+    "mlamg_csr_destroy": (c_int, [c_vp]),
+    "mlamg_csr_shape": (c_int, [c_vp, P_i64, P_i64, P_i64]),
+    "mlamg_csr_device_arrays": (c_int, [c_vp, c_vpp, c_vpp, c_vpp]),
+    "mlamg_csr_download": (c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_spmv": (c_int, [c_vp, c_vp, c_vp, c_dbl, c_dbl, c_vp]),
+    "mlamg_residual": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_jacobi": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "mlamg_jacobi_explicit": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "mlamg_restrict": (c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_prolong_add": (c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_diag_inv": (c_int, [c_vp, c_dbl, c_vp, c_vp]),
+    "mlamg_norm2": (c_int, [c_vp, c_i64, c_vp, c_vp]),
+    "mlamg_transpose": (c_int, [c_vp, c_vpp, c_vp]),
+    "mlamg_spgemm": (c_int, [c_vp, c_vp, c_vpp, c_vp]),
+    "mlamg_galerkin": (c_int, [c_vp, c_vp, c_vp, c_vpp, c_vp]),
+    "mlamg_sa_smoother": (c_int, [c_vp, c_dbl, c_vpp, c_vp]),
+    "mlamg_csr_scale_rows": (c_int, [c_vp, c_vp, c_int, c_vpp, c_vp]),
+    "mlamg_lambda_max_dinvA": (c_int, [c_vp, c_int, c_dbl, c_u64, P_dbl, P_int, c_vp]),
+    "mlamg_strength": (c_int, [c_vp, c_int, c_vpp, c_vp]),
+    "mlamg_bellman_ford": (c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, P_i32, c_vp]),
+    "mlamg_aggregate_op": (c_int, [c_vp, c_i64, c_i64, c_vpp, c_vp]),
+    "mlamg_labels_to_columns": (c_int, [c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "mlamg_lloyd_cluster": (c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp, P_i32, c_vp]),
+    "mlamg_gs_create": (c_int, [c_vp, c_vpp, c_vp]),
+    "mlamg_gs_destroy": (c_int, [c_vp]),
+    "mlamg_gs_levels": (c_int, [c_vp, P_i32]),
+    "mlamg_gs_sweep": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp]),
+    "mlamg_dense_create": (c_int, [c_vp, c_vpp, c_vp]),
+    "mlamg_dense_destroy": (c_int, [c_vp]),
+    "mlamg_dense_solve": (c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_hier_create": (c_int, [c_vpp]),
+    "mlamg_hier_destroy": (c_int, [c_vp]),
+    "mlamg_hier_add_level": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_hier_set_coarse": (c_int, [c_vp, c_vp, c_vp]),
+    "mlamg_hier_set_smoothing": (c_int, [c_vp, c_int, c_int]),
+    "mlamg_hier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_int, c_vp]),
+    "mlamg_hier_cycle_bytes": (c_int, [c_vp, P_dbl]),
+}
+
+for _name, (_res, _args) in SIGNATURES.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+class MlamgError(RuntimeError):
+    def __init__(self, code, where):
+        msg = lib.mlamg_last_error()
+        msg = msg.decode() if msg else ""
+        super().__init__(f"{where} failed ({code}): {msg}")
+        self.code = code
+
+
+def check(rc, where=""):
+    if rc != MLAMG_OK:
+        raise MlamgError(rc, where)
+    return rc
+
+
+def call(name, *args):
+    """Call a C-ABI entry point and raise MlamgError on a nonzero status."""
+    return check(getattr(lib, name)(*args), name)
+
+
+def stream_ptr(stream=None):
+    """hipStream_t of the given (or current) torch stream."""
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())

@@ -1,0 +1,164 @@
+"""Drop-in mirror of ns/lib/graph.py (aggregation) running on the MI355X.
+
+  modified_bellman_ford   ns/lib/graph.py:7-53     seeded Bellman-Ford, fp32 (torch) arithmetic
+  nearest_center_to_agg   ns/lib/graph.py:56-86    aggregate matrix from assignments
+  lloyd_aggregation       ns/lib/graph.py:156-239  seeds + pyamg 4.x lloyd_cluster + AggOp
+
+Distances are bit-exact with the reference for any input (order-independent fixed point, see
+csrc/graph.hip). Seed labels are bit-exact whenever shortest paths are unique; on exact ties the
+device uses the order-independent rule "smallest seed id among tight predecessors" where the
+reference keeps whichever its sequential sweep found first.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from ._lib import call, ptr, stream_ptr
+from .sparse import DeviceCSR, _device
+
+
+def _coo_to_device_csr(S_T):
+    """torch COO (coalesced, row-major) -> DeviceCSR with the fp32 values widened exactly."""
+    S_T = S_T.coalesce()
+    n, m = S_T.shape
+    idx = S_T.indices().cpu().numpy()
+    vals = S_T.values().detach().cpu().numpy().astype(np.float64)
+    A = sp.csr_matrix((vals, (idx[0], idx[1])), shape=(n, m))
+    # coalesced COO is sorted by (row, col); csr_matrix keeps that order
+    return DeviceCSR.from_scipy(A, check=False)
+
+
+def bellman_ford_device(G, seeds_dev):
+    """Device Bellman-Ford on G (push form: edge i -> j, weight G[i, j]).
+
+    Returns (distance fp32 tensor, label int32 tensor (seed node id, -1 unreachable), sweeps).
+    """
+    n = G.shape[0]
+    dev = _device()
+    dist = torch.empty(n, dtype=torch.float32, device=dev)
+    lab = torch.empty(n, dtype=torch.int32, device=dev)
+    sweeps = ctypes.c_int32()
+    call("mlamg_bellman_ford", G.handle, ptr(seeds_dev), int(seeds_dev.numel()), ptr(dist),
+         ptr(lab), ctypes.byref(sweeps), stream_ptr())
+    return dist, lab, int(sweeps.value)
+
+
+def modified_bellman_ford(S_T, centers):
+    """ns/lib/graph.py:7-53. S_T: torch sparse COO strength matrix; centers: 1-D int tensor.
+
+    Returns (distance, nearest_center) on centers.device, fp32 / int64 like the reference
+    (unreachable nodes: distance inf, nearest_center 0, as the reference's initial values).
+    """
+    G = _coo_to_device_csr(S_T)
+    seeds = torch.as_tensor(centers).to(device=_device(), dtype=torch.int32)
+    dist, lab, _ = bellman_ford_device(G, seeds)
+    nearest = lab.to(torch.int64)
+    nearest = torch.where(nearest < 0, torch.zeros_like(nearest), nearest)
+    dev = centers.device if isinstance(centers, torch.Tensor) else torch.device("cpu")
+    return dist.to(dev), nearest.to(dev)
+
+
+def aggregate_op_device(col_dev, k):
+    """Agg (n x k, ones) from per-node aggregate columns (-1 = none) on the device."""
+    h = ctypes.c_void_p()
+    call("mlamg_aggregate_op", ptr(col_dev), int(col_dev.numel()), int(k), ctypes.byref(h),
+         stream_ptr())
+    return DeviceCSR(h)
+
+
+def labels_to_columns(lab_dev, seeds_dev):
+    col = torch.empty_like(lab_dev)
+    call("mlamg_labels_to_columns", ptr(lab_dev), int(lab_dev.numel()), ptr(seeds_dev),
+         int(seeds_dev.numel()), ptr(col), stream_ptr())
+    return col
+
+
+def nearest_center_to_agg(top_k, nearest_center):
+    """ns/lib/graph.py:56-86: torch sparse COO (n x m) of fp32 ones, coalesced.
+
+    Raises KeyError for an assignment that is not one of top_k, like the reference's dict lookup.
+    """
+    dev = _device()
+    seeds = torch.as_tensor(top_k).to(device=dev, dtype=torch.int32)
+    lab = torch.as_tensor(nearest_center).to(device=dev, dtype=torch.int32)
+    col = labels_to_columns(lab, seeds)
+    if bool((col < 0).any()):
+        bad = int(lab[col < 0][0].item())
+        raise KeyError(bad)
+    Agg = aggregate_op_device(col, seeds.numel())
+    A = Agg.to_scipy().tocoo()
+    out_dev = top_k.device if isinstance(top_k, torch.Tensor) else torch.device("cpu")
+    T = torch.sparse_coo_tensor(
+        torch.as_tensor(np.vstack([A.row, A.col]).astype(np.int64)),
+        torch.ones(A.nnz, dtype=torch.float32), (lab.numel(), seeds.numel()), device=out_dev)
+    return T.coalesce()
+
+
+def lloyd_cluster_device(G, seeds_dev, maxiter=10):
+    """pyamg 4.x lloyd_cluster on the device. Returns (distances, clusters, seeds, iters)."""
+    n = G.shape[0]
+    dev = _device()
+    d = torch.empty(n, dtype=torch.float64, device=dev)
+    c = torch.empty(n, dtype=torch.int32, device=dev)
+    its = ctypes.c_int32()
+    call("mlamg_lloyd_cluster", G.handle, ptr(seeds_dev), int(seeds_dev.numel()), int(maxiter),
+         ptr(d), ptr(c), ctypes.byref(its), stream_ptr())
+    return d, c, seeds_dev, int(its.value)
+
+
+def distance_data(C, distance):
+    """Edge weights of lloyd_aggregation (ns/lib/graph.py:201-212)."""
+    if distance == 'unit':
+        data = np.ones_like(C.data).astype(float)
+    elif distance == 'abs':
+        data = abs(C.data)
+    elif distance == 'inv':
+        data = 1.0 / abs(C.data)
+    elif distance == 'same':
+        data = C.data
+    elif distance == 'min':
+        data = C.data - C.data.min()
+    else:
+        raise ValueError(f'Unrecognized value distance={distance}')
+    return data
+
+
+def lloyd_aggregation(C, ratio=0.03, distance='unit', maxiter=10, rand=None):
+    """ns/lib/graph.py:156-239 with pyamg.graph.lloyd_cluster run on the device.
+
+    Returns (AggOp CSR int8 N x num_seeds, roots, seeds) like the reference.
+    """
+    if ratio <= 0 or ratio > 1:
+        raise ValueError('ratio must be > 0.0 and <= 1.0')
+    if not (sp.isspmatrix_csr(C) or sp.isspmatrix_csc(C)):
+        raise TypeError('expected csr_matrix or csc_matrix')
+    data = distance_data(C, distance)
+    if rand is None:
+        rand = np.random
+    elif isinstance(rand, int):
+        rand = np.random.RandomState(rand)
+    elif not isinstance(rand, np.random.RandomState):
+        raise TypeError('rand should be an integer seed value or a random state')
+    if C.dtype == complex:
+        data = np.real(data)
+    assert data.min() >= 0
+    G = C.__class__((data, C.indices, C.indptr), shape=C.shape)
+    if sp.isspmatrix_csc(G):
+        # pyamg's amg_core reads G.indptr/G.indices as CSR arrays whatever the format, so a CSC
+        # graph is walked as its transpose; reproduce that
+        G = sp.csr_matrix((G.data, G.indices, G.indptr), shape=G.shape)
+    N = C.shape[0]
+    num_seeds = int(np.ceil(ratio * N))
+    seeds = rand.permutation(N)[:num_seeds]
+    Gd = DeviceCSR.from_scipy(G)
+    seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
+    _, clusters, roots_dev, _ = lloyd_cluster_device(Gd, seeds_dev, maxiter)
+    Agg = aggregate_op_device(clusters, num_seeds).to_scipy()
+    AggOp = sp.csr_matrix((Agg.data.astype(np.int8), Agg.indices, Agg.indptr),
+                          shape=(G.shape[0], num_seeds))
+    roots = roots_dev.cpu().numpy().astype(np.intc)
+    return AggOp, roots, seeds

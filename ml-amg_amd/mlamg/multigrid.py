@@ -1,0 +1,271 @@
+"""Drop-in mirror of ns/lib/multigrid.py running on the MI355X.
+
+Same names, argument meaning, return values and error behaviour as the reference; every sparse
+operation runs in libmlamg_hip (HIP kernels for gfx950). scipy matrices / numpy vectors go in and
+come out, like the reference; `DeviceCSR` operands and torch cuda tensors are also accepted.
+
+  jacobi                     ns/lib/multigrid.py:15-45
+  gauss_seidel               ns/lib/multigrid.py:58-90 (pyamg gauss_seidel order)
+  smoothed_aggregation_jacobi ns/lib/multigrid.py:102-108
+  amg_2_v                    ns/lib/multigrid.py:111-210
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr
+from .sparse import DeviceCSR, as_device, galerkin, to_device_vec
+
+
+def _as_numpy_out(x_dev, like):
+    out = x_dev.cpu().numpy()
+    if isinstance(like, np.ndarray):
+        like[...] = out
+        return like
+    return out
+
+
+def _dinv_vector(A_dev, Dinv):
+    """Diagonal of the reference's Dinv argument as a device vector (fl(1/a_ii))."""
+    if Dinv is None:
+        return A_dev.diag_inv(1.0)
+    if sp.issparse(Dinv):
+        d = np.asarray(Dinv.diagonal(), dtype=np.float64)
+    else:
+        d = np.asarray(Dinv, dtype=np.float64)
+        if d.ndim == 2:
+            d = np.diagonal(d).copy()
+    return to_device_vec(d)
+
+
+def _scale(d, omega):
+    # `omega * Dinv` scales the dia data: fl(omega * d)
+    return d * omega
+
+
+def jacobi(A, b, x, Dinv=None, omega=0.666, nu=2):
+    """Weighted Jacobi, ns/lib/multigrid.py:15-45:  x += w*Dinv@b - ((w*Dinv)@A)@x, nu times.
+
+    The explicit product (w*Dinv)@A is formed on the device with scipy's row order, so the
+    result is bitwise the reference's. x (numpy) is updated in place and returned.
+    """
+    A_dev = as_device(A)
+    d = _dinv_vector(A_dev, Dinv)
+    dw = _scale(d, omega)
+    h = ctypes.c_void_p()
+    call("mlamg_csr_scale_rows", A_dev.handle, ptr(dw), 1, ctypes.byref(h), stream_ptr())
+    M = DeviceCSR(h)
+    xd = to_device_vec(x)
+    bd = to_device_vec(b)
+    tmp = torch.empty_like(xd)
+    call("mlamg_jacobi_explicit", M.handle, ptr(dw), ptr(bd), ptr(xd), ptr(tmp), int(nu),
+         stream_ptr())
+    if isinstance(x, torch.Tensor):
+        x.copy_(xd)
+        return x
+    return _as_numpy_out(xd, x)
+
+
+class GaussSeidel:
+    """Level-scheduled forward Gauss-Seidel with pyamg relaxation.gauss_seidel semantics."""
+
+    def __init__(self, A_dev):
+        self.A = A_dev
+        h = ctypes.c_void_p()
+        call("mlamg_gs_create", A_dev.handle, ctypes.byref(h), stream_ptr())
+        self.handle = h
+        n = ctypes.c_int32()
+        call("mlamg_gs_levels", h, ctypes.byref(n))
+        self.n_levels = int(n.value)
+
+    def sweep(self, x, b, iterations=1):
+        call("mlamg_gs_sweep", self.handle, ptr(x), ptr(b), int(iterations), stream_ptr())
+        return x
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                _lib.lib.mlamg_gs_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+def gauss_seidel(A, b, x, L=None, U=None, nu=2):
+    """Gauss-Seidel, ns/lib/multigrid.py:58-90 (nu forward sweeps; L/U are ignored)."""
+    A_dev = as_device(A)
+    gs = GaussSeidel(A_dev)
+    xd = to_device_vec(x)
+    bd = to_device_vec(b)
+    gs.sweep(xd, bd, nu)
+    out = xd.cpu().numpy()
+    return out
+
+
+def lambda_max_dinv_a(A, max_iter=20000, tol=1e-15, seed=0):
+    """Largest eigenvalue of Dinv@A (ARPACK eigs k=1 'LM' at ns/lib/multigrid.py:105)."""
+    A_dev = as_device(A)
+    lam = ctypes.c_double()
+    its = ctypes.c_int()
+    call("mlamg_lambda_max_dinvA", A_dev.handle, int(max_iter), float(tol), int(seed),
+         ctypes.byref(lam), ctypes.byref(its), stream_ptr())
+    return float(lam.value), int(its.value)
+
+
+def sa_omega(A, **kw):
+    lam, _ = lambda_max_dinv_a(A, **kw)
+    return (4.0 / 3.0) / abs(lam)
+
+
+def smoothed_aggregation_jacobi_device(A_dev, Agg_dev, omega=None):
+    """P = (I - omega*Dinv@A) @ Agg on the device; omega = (4/3)/lambda_max(Dinv@A)."""
+    if omega is None:
+        omega = sa_omega(A_dev)
+    h = ctypes.c_void_p()
+    call("mlamg_sa_smoother", A_dev.handle, float(omega), ctypes.byref(h), stream_ptr())
+    S = DeviceCSR(h)
+    return S @ Agg_dev, omega
+
+
+def smoothed_aggregation_jacobi(A, Agg):
+    """ns/lib/multigrid.py:102-108; returns a scipy CSR like the reference."""
+    A_dev = as_device(A)
+    Agg_dev = as_device(sp.csr_matrix(Agg, dtype=np.float64) if sp.issparse(Agg) else Agg)
+    P, _ = smoothed_aggregation_jacobi_device(A_dev, Agg_dev)
+    return P.to_scipy()
+
+
+def conv_factor(err):
+    """Convergence-factor formula of ns/lib/multigrid.py:201-208, quirks included."""
+    if len(err) != 1:
+        try:
+            err_n = min(len(err) // 3, 10)
+            conv = (err[-1] / err[-err_n]) ** (1 / (err_n - 1))
+        except Exception:  # the reference's bare except: divide by zero, empty history
+            conv = 0
+    else:
+        conv = 0
+    return conv
+
+
+class TwoLevel:
+    """Device state of one amg_2_v call: A, P, R = P^T, A_H = (R@A)@P and its dense inverse."""
+
+    def __init__(self, A, P):
+        self.A = as_device(A)
+        self.P = as_device(P)
+        self.R = self.P.transpose()
+        self.A_H = galerkin(self.R, self.A, self.P)
+        h = ctypes.c_void_p()
+        call("mlamg_dense_create", self.A_H.handle, ctypes.byref(h), stream_ptr())
+        self.dense = h
+        self.n = self.A.shape[0]
+        self.nc = self.P.shape[1]
+
+    def coarse_correct(self, x, b, r, rc, ec):
+        """x += P @ A_H^-1 (P.T @ (b - A@x))  (ns/lib/multigrid.py:181)."""
+        s = stream_ptr()
+        call("mlamg_residual", self.A.handle, ptr(b), ptr(x), ptr(r), None, s)
+        call("mlamg_restrict", self.R.handle, ptr(r), ptr(rc), s)
+        call("mlamg_dense_solve", self.dense, ptr(rc), ptr(ec), s)
+        call("mlamg_prolong_add", self.P.handle, ptr(ec), ptr(x), s)
+
+    def __del__(self):
+        h = getattr(self, "dense", None)
+        if h:
+            try:
+                _lib.lib.mlamg_dense_destroy(h)
+            except Exception:
+                pass
+            self.dense = None
+
+
+def amg_2_v(A, P, b, x,
+            pre_smoothing_steps=1,
+            post_smoothing_steps=1,
+            jacobi_weight=0.666,
+            res_tol=None,
+            error_tol=None,
+            max_iter=500,
+            singular=False,
+            *, smoother="gauss_seidel"):
+    """Two-level AMG solver, ns/lib/multigrid.py:111-210, on the GPU.
+
+    smoother='gauss_seidel' (reference default: pyamg forward GS, :175,184) or 'jacobi'
+    (weighted Jacobi x += w*Dinv(b - A x) with w = jacobi_weight, the MLAMG.py:143-146 form).
+    Returns (x, conv_factor, err, num_iterations) exactly like the reference.
+    """
+    if res_tol is None and error_tol is None:
+        raise RuntimeError('One of res_tol or error_tol must be set!')
+    tol = res_tol if res_tol is not None else error_tol
+    if singular:
+        raise NotImplementedError("singular=True (lsqr coarse solve + mean removal, "
+                                  "multigrid.py:178-187) is not implemented on the GPU path")
+    if smoother not in ("gauss_seidel", "jacobi"):
+        raise ValueError(f"unknown smoother {smoother!r}")
+    err = np.zeros(max_iter)
+    try:
+        two = TwoLevel(A, P)
+    except _lib.MlamgError as e:
+        if e.code == _lib.MLAMG_EINVAL and "singular" in str(e):
+            return x, np.float64(1.), err, 0  # multigrid.py:167-170
+        raise
+    n = two.n
+    dev_x = to_device_vec(x).clone()  # x = x.copy()  (:171)
+    dev_b = to_device_vec(b)
+    r = torch.empty(n, dtype=torch.float64, device=dev_x.device)
+    tmp = torch.empty_like(r)
+    rc = torch.empty(two.nc, dtype=torch.float64, device=dev_x.device)
+    ec = torch.empty_like(rc)
+    nrm = torch.empty(1, dtype=torch.float64, device=dev_x.device)
+    s = stream_ptr()
+    if smoother == "gauss_seidel":
+        gs = GaussSeidel(two.A)
+
+        def smooth(nu):
+            if nu:
+                gs.sweep(dev_x, dev_b, nu)
+    else:
+        dinv_w = two.A.diag_inv(jacobi_weight)
+
+        def smooth(nu):
+            if nu:
+                call("mlamg_jacobi", two.A.handle, ptr(dinv_w), ptr(dev_b), ptr(dev_x), ptr(tmp),
+                     int(nu), s)
+
+    for i in range(max_iter):
+        smooth(pre_smoothing_steps)
+        two.coarse_correct(dev_x, dev_b, r, rc, ec)
+        smooth(post_smoothing_steps)
+        if res_tol is not None:
+            call("mlamg_residual", two.A.handle, ptr(dev_b), ptr(dev_x), ptr(r), ptr(nrm), s)
+        else:
+            call("mlamg_norm2", ptr(dev_x), n, ptr(nrm), s)
+        e = float(nrm.item())
+        err[i] = e
+        if e <= tol:
+            err = err[:i + 1]
+            break
+    return dev_x.cpu().numpy(), conv_factor(err), err, len(err)
+
+
+def amg_2_v_jacobi(A, P, b, x, dinv_w=None, omega=2. / 3., pre_smoothing_steps=1,
+                   post_smoothing_steps=1, max_iter=500, tol=1e-8, history=False):
+    """MLAMG.amg_2_v (ns/preconditioner/MLAMG.py:148-197) through the device V-cycle executor.
+
+    Stops after the first cycle with ||b - A x||_2 <= tol (absolute, :194). Returns x (numpy),
+    plus the residual history when history=True.
+    """
+    from .hierarchy import Hierarchy
+    H = Hierarchy.two_level(A, P, omega=omega, nu_pre=pre_smoothing_steps,
+                            nu_post=post_smoothing_steps, dinv_w=dinv_w)
+    xd = to_device_vec(x).clone()
+    hist = H.cycle(to_device_vec(b), xd, max_iter, tol=tol)
+    out = xd.cpu().numpy()
+    return (out, hist) if history else out

@@ -1,0 +1,224 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY. CPU restatement of the reference hot-path loops that
+ * live in compiled third-party code or in slow pure-Python loops, used by tests/ and by
+ * bench.py's cpu_baseline leg as the checker. Never linked into, or called by, the product
+ * (ml-amg_amd/mlamg). Built with -ffp-contract=off so every multiply and add rounds separately,
+ * like scipy/pyamg on x86-64.
+ *
+ *   ref_csr_matvec          scipy sparsetools csr_matvec (A@x at ns/lib/multigrid.py:181,191)
+ *   ref_gauss_seidel        pyamg 4.x amg_core gauss_seidel, forward sweep (multigrid.py:175,184)
+ *   ref_bellman_ford_torch  ns/lib/graph.py:28-53 modified_bellman_ford (fp32, sequential push
+ *                           over coalesced COO order, strict <)
+ *   canon_bellman_ford      same distances (order-independent fixed point) with the device's
+ *                           order-independent label rule (min seed id over tight edges)
+ *   ref_lloyd_cluster       pyamg 4.x amg_core lloyd_cluster + graph.lloyd_cluster driver loop
+ *                           (called at ns/lib/graph.py:232), sequential
+ *   canon_lloyd_cluster     same with the device's label rule (min cluster index over tight
+ *                           pull neighbours)
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+void ref_csr_matvec(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
+                    const double* x, double* y) {
+  for (int64_t i = 0; i < n; ++i) {
+    double s = 0.0; /* Yx zero-initialised by A@x */
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) s += ax[k] * x[ij[k]];
+    y[i] = s;
+  }
+}
+
+void ref_gauss_seidel(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
+                      double* x, const double* b, int iterations) {
+  for (int it = 0; it < iterations; ++it) {
+    for (int64_t i = 0; i < n; ++i) {
+      double rsum = 0.0, diag = 0.0;
+      for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
+        const int32_t j = ij[k];
+        if (j == i) diag = ax[k];
+        else rsum += ax[k] * x[j];
+      }
+      if (diag != 0.0) x[i] = (b[i] - rsum) / diag;
+    }
+  }
+}
+
+/* graph.py:28-53. dist fp32 [n], nearest int64 [n]; returns number of sweeps */
+int ref_bellman_ford_torch(int64_t n, const int32_t* ip, const int32_t* ij, const float* w,
+                           const int64_t* centers, int64_t k, float* dist, int64_t* nearest) {
+  for (int64_t i = 0; i < n; ++i) {
+    dist[i] = INFINITY;
+    nearest[i] = 0;
+  }
+  for (int64_t t = 0; t < k; ++t) {
+    dist[centers[t]] = 0.0f;
+    nearest[centers[t]] = centers[t];
+  }
+  int sweeps = 0;
+  for (;;) {
+    int finished = 1;
+    ++sweeps;
+    for (int64_t i = 0; i < n; ++i) {
+      for (int32_t e = ip[i]; e < ip[i + 1]; ++e) {
+        const int32_t j = ij[e];
+        const float cand = dist[i] + w[e];
+        if (cand < dist[j]) {
+          dist[j] = cand;
+          nearest[j] = nearest[i];
+          finished = 0;
+        }
+      }
+    }
+    if (finished) break;
+  }
+  return sweeps;
+}
+
+/* device rule: same fixed-point distances; label = min seed node id over tight in-edges */
+void canon_bellman_ford(int64_t n, const int32_t* ip, const int32_t* ij, const float* w,
+                        const int32_t* seeds, int64_t k, float* dist, int32_t* label) {
+  char* is_seed = (char*)calloc((size_t)n + 1, 1);
+  for (int64_t i = 0; i < n; ++i) {
+    dist[i] = INFINITY;
+    label[i] = INT32_MAX;
+  }
+  for (int64_t t = 0; t < k; ++t) {
+    dist[seeds[t]] = 0.0f;
+    label[seeds[t]] = seeds[t];
+    is_seed[seeds[t]] = 1;
+  }
+  int changed = 1;
+  while (changed) {
+    changed = 0;
+    for (int64_t i = 0; i < n; ++i)
+      for (int32_t e = ip[i]; e < ip[i + 1]; ++e) {
+        const float cand = dist[i] + w[e];
+        if (cand < dist[ij[e]]) {
+          dist[ij[e]] = cand;
+          changed = 1;
+        }
+      }
+  }
+  changed = 1;
+  while (changed) {
+    changed = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      if (!(dist[i] < INFINITY) || label[i] == INT32_MAX) continue;
+      for (int32_t e = ip[i]; e < ip[i + 1]; ++e) {
+        const int32_t j = ij[e];
+        if (is_seed[j]) continue;
+        if (dist[i] + w[e] == dist[j] && label[i] < label[j]) {
+          label[j] = label[i];
+          changed = 1;
+        }
+      }
+    }
+  }
+  for (int64_t i = 0; i < n; ++i)
+    if (label[i] == INT32_MAX) label[i] = -1;
+  free(is_seed);
+}
+
+/* pyamg amg_core bellman_ford (pull, in place); returns nonzero if anything changed */
+static int pyamg_bf(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax, double* x,
+                    int32_t* z, int update_z) {
+  int changed = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double xi = x[i];
+    int32_t zi = z[i];
+    for (int32_t jj = ip[i]; jj < ip[i + 1]; ++jj) {
+      const int32_t j = ij[jj];
+      const double d = ax[jj] + x[j];
+      if (d < xi) {
+        xi = d;
+        zi = z[j];
+      }
+    }
+    if (xi != x[i]) changed = 1;
+    x[i] = xi;
+    if (update_z) z[i] = zi;
+  }
+  return changed;
+}
+
+static void lloyd_boundary(int64_t n, const int32_t* ip, const int32_t* ij, const int32_t* c,
+                           double* d) {
+  for (int64_t i = 0; i < n; ++i) d[i] = DBL_MAX;
+  for (int64_t i = 0; i < n; ++i)
+    for (int32_t jj = ip[i]; jj < ip[i + 1]; ++jj)
+      if (c[i] != c[ij[jj]]) {
+        d[i] = 0.0;
+        break;
+      }
+}
+
+static void lloyd_recentre(int64_t n, const int32_t* c, const double* d, int32_t* s) {
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t seed = c[i];
+    if (seed == -1) continue;
+    if (d[s[seed]] < d[i]) s[seed] = (int32_t)i;
+  }
+}
+
+/* one amg_core lloyd_cluster call; canon != 0 uses the order-independent label rule */
+static void lloyd_once(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
+                       int32_t k, double* d, int32_t* c, int32_t* s, int canon, char* is_seed) {
+  for (int64_t i = 0; i < n; ++i) {
+    d[i] = DBL_MAX;
+    c[i] = -1;
+  }
+  for (int32_t t = 0; t < k; ++t) {
+    d[s[t]] = 0.0;
+    c[s[t]] = t;
+  }
+  if (!canon) {
+    while (pyamg_bf(n, ip, ij, ax, d, c, 1)) {
+    }
+  } else {
+    memset(is_seed, 0, (size_t)n);
+    for (int32_t t = 0; t < k; ++t) is_seed[s[t]] = 1;
+    while (pyamg_bf(n, ip, ij, ax, d, c, 0)) {
+    }
+    int changed = 1;
+    while (changed) {
+      changed = 0;
+      for (int64_t i = 0; i < n; ++i) {
+        if (is_seed[i] || !(d[i] < DBL_MAX)) continue;
+        int32_t best = c[i];
+        for (int32_t jj = ip[i]; jj < ip[i + 1]; ++jj) {
+          const int32_t j = ij[jj];
+          if (ax[jj] + d[j] == d[i] && c[j] >= 0 && (best < 0 || c[j] < best)) best = c[j];
+        }
+        if (best != c[i]) {
+          c[i] = best;
+          changed = 1;
+        }
+      }
+    }
+  }
+  lloyd_boundary(n, ip, ij, c, d);
+  while (pyamg_bf(n, ip, ij, ax, d, c, canon ? 0 : 1)) {
+  }
+  lloyd_recentre(n, c, d, s);
+}
+
+/* pyamg.graph.lloyd_cluster driver: up to maxiter calls, stop when seeds do not move.
+ * seeds updated in place; returns iterations run */
+int lloyd_cluster(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax, int32_t k,
+                  int32_t* seeds, int maxiter, double* d, int32_t* c, int canon) {
+  int32_t* last = (int32_t*)malloc(sizeof(int32_t) * (size_t)(k > 0 ? k : 1));
+  char* is_seed = (char*)malloc((size_t)n + 1);
+  int it = 0;
+  for (; it < maxiter;) {
+    memcpy(last, seeds, sizeof(int32_t) * (size_t)k);
+    lloyd_once(n, ip, ij, ax, k, d, c, seeds, canon, is_seed);
+    ++it;
+    if (memcmp(last, seeds, sizeof(int32_t) * (size_t)k) == 0) break;
+  }
+  free(last);
+  free(is_seed);
+  return it;
+}

@@ -1,0 +1,343 @@
+"""TEST INFRASTRUCTURE ONLY — numpy/scipy restatement of the reference hot path.
+
+Each function cites the reference lines it restates. scipy calls are the reference's own
+arithmetic (the reference is scipy code), so wherever the reference uses scipy this module uses
+the same scipy call. pyamg (absent here) is restated in oracle/oracle.c.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+
+import numpy as np
+import numpy.linalg as la
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+
+from . import build as _build
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = _build.OUT
+        if not os.path.exists(path):
+            path = _build.build()
+        L = ctypes.CDLL(path)
+        vp = ctypes.c_void_p
+        i64 = ctypes.c_int64
+        L.ref_csr_matvec.argtypes = [i64, vp, vp, vp, vp, vp]
+        L.ref_gauss_seidel.argtypes = [i64, vp, vp, vp, vp, vp, ctypes.c_int]
+        L.ref_bellman_ford_torch.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
+        L.ref_bellman_ford_torch.restype = ctypes.c_int
+        L.canon_bellman_ford.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
+        L.lloyd_cluster.argtypes = [i64, vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int, vp, vp,
+                                    ctypes.c_int]
+        L.lloyd_cluster.restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _csr_arrays(A):
+    A = A.tocsr()
+    return (np.ascontiguousarray(A.indptr, dtype=np.int32),
+            np.ascontiguousarray(A.indices, dtype=np.int32),
+            np.ascontiguousarray(A.data, dtype=np.float64))
+
+
+# ---------------------------------------------------------------- sparse primitives
+def csr_matvec(A, x):
+    """scipy csr_matvec (A@x), restated in C."""
+    ip, ij, ax = _csr_arrays(A)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty(A.shape[0])
+    lib().ref_csr_matvec(A.shape[0], _p(ip), _p(ij), _p(ax), _p(x), _p(y))
+    return y
+
+
+def gauss_seidel(A, x, b, iterations=1):
+    """pyamg.relaxation.relaxation.gauss_seidel(A, x, b, iterations) forward, in place
+    (called at ns/lib/multigrid.py:175,184)."""
+    ip, ij, ax = _csr_arrays(A)
+    assert x.dtype == np.float64 and x.flags.c_contiguous
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    lib().ref_gauss_seidel(A.shape[0], _p(ip), _p(ij), _p(ax), _p(x), _p(b), int(iterations))
+    return x
+
+
+def jacobi_mg(A, b, x, Dinv=None, omega=0.666, nu=2):
+    """ns/lib/multigrid.py:15-45."""
+    if Dinv is None:
+        Dinv = sp.diags(1.0 / A.diagonal())
+    for _ in range(nu):
+        x += omega * Dinv @ b - omega * Dinv @ A @ x
+    return x
+
+
+def jacobi_mlamg(A, Dinv_w, b, x, nu=2):
+    """ns/preconditioner/MLAMG.py:143-146 with Dinv_w = sp.diags(1/diag)*w (MLAMG.py:104)."""
+    for _ in range(nu):
+        x += Dinv_w @ (b - A @ x)
+    return x
+
+
+def mlamg_dinv(A, w=2.0 / 3.0):
+    """MLAMG.py:104."""
+    return sp.diags(1.0 / A.diagonal()) * w
+
+
+def smoothed_aggregation_jacobi(A, Agg, omega=None):
+    """ns/lib/multigrid.py:102-108 (omega from ARPACK unless given)."""
+    n = A.shape[0]
+    Dinv = sp.diags([1.0 / A.diagonal()], [0])
+    if omega is None:
+        omega = (4. / 3.) / np.abs(spla.eigs(Dinv @ A, k=1, return_eigenvectors=False)).item()
+    smoother = (sp.eye(n) - omega * Dinv @ A)
+    P = smoother @ Agg
+    return P, omega
+
+
+def arpack_lambda_max(A):
+    Dinv = sp.diags([1.0 / A.diagonal()], [0])
+    return float(np.abs(spla.eigs(Dinv @ A, k=1, return_eigenvectors=False)).item())
+
+
+def canonical(M):
+    """CSR with sorted indices (values untouched) for array-level comparison."""
+    M = sp.csr_matrix(M)
+    M = M.copy()
+    M.has_sorted_indices = False
+    M.sort_indices()
+    return M
+
+
+def galerkin(A, P):
+    """ns/lib/multigrid.py:165 `P.T@A@P` (scipy CSC path), as sorted CSR."""
+    return canonical((P.T @ A @ P).tocsr())
+
+
+# ---------------------------------------------------------------- drivers
+def conv_factor(err):
+    """ns/lib/multigrid.py:201-208."""
+    if len(err) != 1:
+        try:
+            err_n = min(len(err) // 3, 10)
+            conv_factor = (err[-1] / err[-err_n]) ** (1 / (err_n - 1))
+        except Exception:
+            conv_factor = 0
+    else:
+        conv_factor = 0
+    return conv_factor
+
+
+def amg_2_v(A, P, b, x, pre_smoothing_steps=1, post_smoothing_steps=1, jacobi_weight=0.666,
+            res_tol=None, error_tol=None, max_iter=500, smoother="gauss_seidel"):
+    """ns/lib/multigrid.py:111-210 (non-singular branch); smoother='jacobi' swaps in the
+    MLAMG.py:143-146 Jacobi form with weight jacobi_weight."""
+    if res_tol is None and error_tol is None:
+        raise RuntimeError('One of res_tol or error_tol must be set!')
+    tol = res_tol if res_tol is not None else error_tol
+    err = np.zeros(max_iter)
+    A_H = P.T @ A @ P
+    try:
+        A_H_LU = spla.factorized(A_H)
+    except Exception:
+        return x, np.float64(1.), err, 0
+    x = x.copy()
+    if smoother == "jacobi":
+        Dw = mlamg_dinv(A, jacobi_weight)
+
+        def smooth(nu):
+            jacobi_mlamg(A, Dw, b, x, nu)
+    else:
+        def smooth(nu):
+            gauss_seidel(A, x, b, iterations=nu)
+    for i in range(max_iter):
+        smooth(pre_smoothing_steps)
+        x += P @ A_H_LU(P.T @ (b - A @ x))
+        smooth(post_smoothing_steps)
+        if res_tol is not None:
+            e = la.norm(b - A @ x, 2)
+        else:
+            e = la.norm(x, 2)
+        err[i] = e
+        if e <= tol:
+            err = err[:i + 1]
+            break
+    return x, conv_factor(err), err, len(err)
+
+
+def mlamg_amg_2_v(A, P, Dinv_w, b, x, pre_smoothing_steps=1, post_smoothing_steps=1,
+                  max_iter=500, amg_rtol=1e-8):
+    """ns/preconditioner/MLAMG.py:148-197 (A_H_lu = splu(P^T A P, COLAMD), :121-122).
+    Returns (x, residual-norm history)."""
+    A_H = (P.T @ A @ P).tocsc()
+    lu = spla.splu(A_H, permc_spec='COLAMD')
+    hist = []
+    x = x.copy()
+    for i in range(max_iter):
+        x = jacobi_mlamg(A, Dinv_w, b, x, nu=pre_smoothing_steps)
+        x += P @ lu.solve(P.T @ (b - A @ x))
+        x = jacobi_mlamg(A, Dinv_w, b, x, nu=post_smoothing_steps)
+        r = la.norm(b - A @ x, 2)
+        hist.append(r)
+        if r <= amg_rtol:
+            break
+    return x, np.array(hist)
+
+
+# ---------------------------------------------------------------- aggregation
+def modified_bellman_ford(C, centers):
+    """ns/lib/graph.py:7-53 on S_T = scipy_to_torch(C): fp32 sequential push over the
+    coalesced COO (= sorted CSR) order. Returns (distance fp32, nearest_center int64, sweeps)."""
+    C = canonical(C)
+    ip, ij, _ = _csr_arrays(C)
+    w = np.ascontiguousarray(C.data, dtype=np.float32)
+    c = np.ascontiguousarray(centers, dtype=np.int64)
+    n = C.shape[0]
+    d = np.empty(n, dtype=np.float32)
+    nc = np.empty(n, dtype=np.int64)
+    sweeps = lib().ref_bellman_ford_torch(n, _p(ip), _p(ij), _p(w), _p(c), len(c), _p(d), _p(nc))
+    return d, nc, sweeps
+
+
+def canon_bellman_ford(C, seeds):
+    """Same distances with the device's order-independent label rule; label -1 unreachable."""
+    C = canonical(C)
+    ip, ij, _ = _csr_arrays(C)
+    w = np.ascontiguousarray(C.data, dtype=np.float32)
+    s = np.ascontiguousarray(seeds, dtype=np.int32)
+    n = C.shape[0]
+    d = np.empty(n, dtype=np.float32)
+    lab = np.empty(n, dtype=np.int32)
+    lib().canon_bellman_ford(n, _p(ip), _p(ij), _p(w), _p(s), len(s), _p(d), _p(lab))
+    return d, lab
+
+
+def nearest_center_to_agg(top_k, nearest_center):
+    """ns/lib/graph.py:56-86 as a scipy CSR of ones (n x m)."""
+    n, m = len(nearest_center), len(top_k)
+    inv = {int(k): i for i, k in enumerate(top_k)}
+    cols = np.array([inv[int(c)] for c in nearest_center], dtype=np.int64)
+    return sp.csr_matrix((np.ones(n), (np.arange(n), cols)), shape=(n, m))
+
+
+def lloyd_cluster(G, seeds, maxiter=10, canon=False):
+    """pyamg 4.x graph.lloyd_cluster (ns/lib/graph.py:232). Returns (distances, clusters, seeds)."""
+    ip, ij, ax = _csr_arrays(G)
+    s = np.array(seeds, dtype=np.int32)
+    n = G.shape[0]
+    d = np.empty(n)
+    c = np.empty(n, dtype=np.int32)
+    lib().lloyd_cluster(n, _p(ip), _p(ij), _p(ax), len(s), _p(s), int(maxiter), _p(d), _p(c),
+                        int(bool(canon)))
+    return d, c, s
+
+
+def lloyd_aggregation(C, ratio=0.03, distance='unit', maxiter=10, rand=None, canon=False):
+    """ns/lib/graph.py:156-239 with the lloyd_cluster restatement."""
+    if distance == 'unit':
+        data = np.ones_like(C.data).astype(float)
+    elif distance == 'abs':
+        data = abs(C.data)
+    elif distance == 'inv':
+        data = 1.0 / abs(C.data)
+    elif distance == 'same':
+        data = C.data
+    elif distance == 'min':
+        data = C.data - C.data.min()
+    else:
+        raise ValueError(distance)
+    if rand is None:
+        rand = np.random
+    elif isinstance(rand, int):
+        rand = np.random.RandomState(rand)
+    G = C.__class__((data, C.indices, C.indptr), shape=C.shape)
+    if sp.isspmatrix_csc(G):
+        G = sp.csr_matrix((G.data, G.indices, G.indptr), shape=G.shape)
+    N = C.shape[0]
+    num_seeds = int(np.ceil(ratio * N))
+    seeds = rand.permutation(N)[:num_seeds]
+    _, clusters, roots = lloyd_cluster(G, np.copy(seeds), maxiter=maxiter, canon=canon)
+    row = (clusters >= 0).nonzero()[0]
+    col = clusters[row]
+    AggOp = sp.coo_matrix((np.ones(len(row), dtype='int8'), (row, col)),
+                          shape=(G.shape[0], num_seeds)).tocsr()
+    return AggOp, roots, seeds
+
+
+# ---------------------------------------------------------------- multilevel (device recipe)
+STRENGTH = {
+    "abs": lambda A: abs(A),
+    "invabs": lambda A: sp.csr_matrix((1.0 / np.abs(A.data), A.indices, A.indptr), A.shape),
+    "unit": lambda A: sp.csr_matrix((np.ones_like(A.data), A.indices, A.indptr), A.shape),
+}
+
+
+def build_hierarchy(A, alpha=0.1, strength_mode="invabs", seed=0, sort_seeds=True,
+                    max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, omegas=None):
+    """CPU restatement of mlamg.hierarchy.Hierarchy.build (aggregation='bellman_ford').
+
+    omegas: per-level SA weights to use (e.g. the device's); None -> ARPACK (multigrid.py:105).
+    Returns a list of level dicts and the coarsest matrix.
+    """
+    levels = []
+    A = canonical(A)
+    while A.shape[0] > max_coarse and len(levels) + 1 < max_levels:
+        n = A.shape[0]
+        C = STRENGTH[strength_mode](A)
+        k = int(math.ceil(alpha * n))
+        seeds = np.random.RandomState(seed).permutation(n)[:k]
+        if sort_seeds:
+            seeds = np.sort(seeds)
+        _, lab = canon_bellman_ford(C, seeds)
+        pos = {int(s): t for t, s in enumerate(seeds)}
+        col = np.array([pos.get(int(l), -1) if l >= 0 else -1 for l in lab])
+        rows = np.nonzero(col >= 0)[0]
+        Agg = sp.csr_matrix((np.ones(len(rows)), (rows, col[rows])), shape=(n, k))
+        om = None if omegas is None else omegas[len(levels)]
+        P, om = smoothed_aggregation_jacobi(A, Agg, omega=om)
+        P = P.tocsr()
+        levels.append({"A": A, "P": P, "omega": om, "Dw": mlamg_dinv(A, jacobi_weight),
+                       "Agg": Agg, "seeds": seeds, "labels": lab})
+        A = galerkin(A, P)
+    return levels, A
+
+
+def vcycle_solve(levels, Ac, b, x, n_cycles, tol=0.0, nu_pre=1, nu_post=1, lu=None):
+    """Multilevel Jacobi V(nu_pre, nu_post) iteration in the device executor's order
+    (mlamg hier.hip; each level = MLAMG.py:189-195 with the coarse solve recursing).
+    Returns (x, residual history). lu: a pre-factorised coarse solve (spla.factorized)."""
+    if lu is None:
+        lu = spla.factorized(sp.csc_matrix(Ac))
+
+    def cycle(l, b, x):
+        if l == len(levels):
+            return lu(b)
+        L = levels[l]
+        A, P, Dw = L["A"], L["P"], L["Dw"]
+        if x is None:
+            x = np.zeros(A.shape[0])
+        x = jacobi_mlamg(A, Dw, b, x, nu_pre)
+        xc = cycle(l + 1, P.T @ (b - A @ x), None)
+        x += P @ xc
+        x = jacobi_mlamg(A, Dw, b, x, nu_post)
+        return x
+
+    x = x.copy()
+    hist = []
+    A0 = levels[0]["A"] if levels else Ac
+    for _ in range(n_cycles):
+        x = cycle(0, b, x) if levels else lu(b)
+        r = la.norm(b - A0 @ x, 2)
+        hist.append(r)
+        if tol > 0 and r <= tol:
+            break
+    return x, np.array(hist)
