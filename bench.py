@@ -102,9 +102,11 @@ def main():
     ap.add_argument("--alpha", type=float, default=0.1)
     ap.add_argument("--max-coarse", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-cycles", type=int, default=3)
+    ap.add_argument("--cpu-cycles", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--dist", action="store_true",
+                    help="use the distributed executor even at N=1 (tests the RCCL path)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,7 +115,7 @@ def main():
     if world != args.gpus:
         log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
     torch.cuda.set_device(local_rank)
-    if world > 1:
+    if world > 1 or args.dist:
         return run_distributed(args, world, rank, local_rank)
 
     from mlamg import problems

@@ -194,6 +194,37 @@ int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, d
 /* bytes one V-cycle moves by the algorithmic model of SURVEY.md §8(d) (for roofline reports) */
 int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes);
 
+/* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI)
+ * New relative to the reference, whose only parallelism is a process task farm over independent
+ * grids (ns/parallel/pool.py:139-186, pickled objects over pipes / mpi4py, no collectives).
+ * One process per GPU; the fine level is row-partitioned, coarse levels replicated
+ * (SURVEY.md §8e). The unique id (128 bytes) is created on rank 0 and broadcast by the caller. */
+typedef struct mlamg_halo mlamg_halo;
+typedef struct mlamg_dhier mlamg_dhier;
+int mlamg_comm_unique_id(void* id_out);
+int mlamg_comm_create(const void* id, int nranks, int rank, mlamg_comm** out);
+int mlamg_comm_destroy(mlamg_comm* c);
+int mlamg_comm_allreduce_sum(mlamg_comm* c, double* buf, int64_t n, void* stream);
+/* ghost layout of one rank: x_ext = [owned n_own | ghosts]; for neighbour q (ascending),
+ * send_cnt[q] owned entries (send_idx_host, concatenated) and recv_cnt[q] ghosts, stored
+ * contiguously in neighbour order. */
+int mlamg_halo_create(mlamg_comm* c, int64_t n_own, int32_t n_nbr, const int32_t* nbr,
+                      const int64_t* send_cnt, const int32_t* send_idx_host,
+                      const int64_t* recv_cnt, mlamg_halo** out);
+int mlamg_halo_destroy(mlamg_halo* h);
+int mlamg_halo_exchange(mlamg_halo* h, double* x_ext, void* stream);
+/* distributed V-cycle: A_loc (n_own x n_own+ghosts_x), P_loc (n_own x n_c), R_own (owned coarse
+ * rows x n_own+ghosts_r), coarse = hierarchy of the replicated levels 1..L, coarse segment
+ * bounds of every rank. Iterates on x_ext (owned part first). */
+int mlamg_dhier_create(mlamg_comm* c, const mlamg_csr* A_loc, const double* dinv_w,
+                       const mlamg_csr* P_loc, const mlamg_csr* R_own, mlamg_halo* halo_x,
+                       mlamg_halo* halo_r, mlamg_hier* coarse, const int64_t* c_lo_all,
+                       const int64_t* c_hi_all, mlamg_dhier** out);
+int mlamg_dhier_destroy(mlamg_dhier* D);
+int mlamg_dhier_set_coarse_graph(mlamg_dhier* D, int use_graph);
+int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cycles, double tol,
+                       double* res_hist, int32_t* cycles_done_host, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

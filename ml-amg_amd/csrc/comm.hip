@@ -1,0 +1,375 @@
+// Multi-GPU fine level: RCCL communicator, halo exchange and the distributed V-cycle.
+//
+// One process per GPU. The fine level is row-partitioned (mlamg/partition.py builds the maps);
+// coarse levels are replicated on every rank (their setup is deterministic). Per cycle:
+//   x += Dinv r                                    local
+//   halo(x); r = b - A_loc x_ext                   RCCL send/recv with the slab neighbours
+//   halo_r(r); b_c[own] = R_own r_ext              coarse rows owned by the rank of their seed
+//   allgatherv(b_c)                                grouped send/recv of the owned segments
+//   x_c = coarse V-cycle from zero (replicated)    mlamg_hier, optionally a captured hipGraph
+//   x += P_loc x_c                                 local
+//   halo(x); t = x + Dinv(b - A x)                 post-smoothing
+//   halo(t); r = b - A t, ||r||^2 -> allreduce     end-of-cycle residual (MLAMG.py:194)
+// Local rows keep their stored column order and coarse rows their owner's full sum, so the
+// iterate is bitwise the single-GPU iterate; only the norm's summation order differs.
+#include "common.hpp"
+
+#include <rccl/rccl.h>
+
+struct mlamg_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+struct mlamg_halo {
+  mlamg_comm* c = nullptr;
+  int64_t n_own = 0, n_ghost = 0;
+  std::vector<int> nbr;
+  std::vector<int64_t> send_off, send_cnt, recv_off, recv_cnt;
+  int32_t* send_idx = nullptr;  // device, concatenated per neighbour
+  double* send_buf = nullptr;   // device
+  int64_t n_send = 0;
+};
+
+#define MLAMG_NCCL(call)                                                            \
+  do {                                                                              \
+    ncclResult_t _r = (call);                                                       \
+    if (_r != ncclSuccess) {                                                        \
+      ::mlamg::set_error(std::string(#call) + " failed: " + ncclGetErrorString(_r)); \
+      return MLAMG_ENCCL;                                                           \
+    }                                                                               \
+  } while (0)
+
+namespace mlamg {
+
+__global__ void k_pack(const double* __restrict__ x, const int32_t* __restrict__ idx, int64_t n,
+                       double* __restrict__ out) {
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i < n) out[i] = x[idx[i]];
+}
+
+int halo_exchange_impl(mlamg_halo* h, double* x_ext, hipStream_t s) {
+  if (h->n_send) {
+    hipLaunchKernelGGL(k_pack, dim3((h->n_send + 255) / 256), dim3(256), 0, s, x_ext, h->send_idx,
+                       h->n_send, h->send_buf);
+    MLAMG_HIP(hipGetLastError());
+  }
+  if (h->nbr.empty()) return MLAMG_OK;
+  MLAMG_NCCL(ncclGroupStart());
+  for (size_t q = 0; q < h->nbr.size(); ++q) {
+    if (h->send_cnt[q])
+      MLAMG_NCCL(ncclSend(h->send_buf + h->send_off[q], (size_t)h->send_cnt[q], ncclFloat64,
+                          h->nbr[q], h->c->comm, s));
+    if (h->recv_cnt[q])
+      MLAMG_NCCL(ncclRecv(x_ext + h->n_own + h->recv_off[q], (size_t)h->recv_cnt[q], ncclFloat64,
+                          h->nbr[q], h->c->comm, s));
+  }
+  MLAMG_NCCL(ncclGroupEnd());
+  return MLAMG_OK;
+}
+
+// declared in other TUs
+int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
+                  double* hist, int32_t* counter, int32_t* done, double tol, double* copy_to,
+                  const double* copy_from, double* partial, hipStream_t s);
+int jacobi_sweep(const mlamg_csr* A, const double* dinv, const double* b, const double* xin,
+                 double* xout, bool explicit_form, const int32_t* done, hipStream_t s);
+int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
+int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
+int jacobi_from_residual(double* x, const double* dinv, const double* r, int64_t n,
+                         const int32_t* done, hipStream_t s);
+int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
+                      hipStream_t s);
+int residual_partials(const mlamg_csr* A, const double* b, const double* x, double* r,
+                      double* copy_to, const double* copy_from, double* partial,
+                      const int32_t* done, hipStream_t s);
+
+// sum the residual partials of this rank into partial[n] (fixed order)
+__global__ __launch_bounds__(1024) void k_local_sum(double* __restrict__ partial, int n) {
+  __shared__ double red[16];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) s += partial[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < 16; ++i) t += red[i];
+    partial[n] = t;
+  }
+}
+
+__global__ void k_norm_finish(const double* __restrict__ sum, double* hist, int32_t* counter,
+                              int32_t* done, double tol) {
+  const double nrm = sqrt(*sum);
+  const int c = *counter;
+  if (hist) hist[c] = nrm;
+  *counter = c + 1;
+  if (tol > 0.0 && nrm <= tol) *done = 1;
+}
+
+}  // namespace mlamg
+
+using namespace mlamg;
+
+struct mlamg_dhier {
+  mlamg_comm* c = nullptr;
+  const mlamg_csr* A = nullptr;  // n_own x (n_own + n_ghost_x)
+  const mlamg_csr* P = nullptr;  // n_own x nc
+  const mlamg_csr* R = nullptr;  // (c_hi - c_lo) x (n_own + n_ghost_r)
+  const double* dinv = nullptr;
+  mlamg_halo* hx = nullptr;
+  mlamg_halo* hr = nullptr;
+  mlamg_hier* coarse = nullptr;  // replicated levels 1..L
+  int64_t n_own = 0, nc = 0, c_lo = 0, c_hi = 0;
+  std::vector<int64_t> c_lo_all, c_hi_all;
+  // work
+  double* r_ext = nullptr;
+  double* t_ext = nullptr;
+  double* bc = nullptr;
+  double* partial = nullptr;
+  int32_t* flags = nullptr;  // counter, done
+  int coarse_graph = 1;
+};
+
+extern "C" {
+
+int mlamg_comm_unique_id(void* id_out) {
+  MLAMG_REQUIRE(id_out, "NULL argument");
+  ncclUniqueId id;
+  MLAMG_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, sizeof(id));
+  return MLAMG_OK;
+}
+
+int mlamg_comm_create(const void* id, int nranks, int rank, mlamg_comm** out) {
+  MLAMG_REQUIRE(id && out && nranks >= 1 && rank >= 0 && rank < nranks, "invalid argument");
+  auto* c = new mlamg_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    set_error(std::string("ncclCommInitRank failed: ") + ncclGetErrorString(r));
+    return MLAMG_ENCCL;
+  }
+  *out = c;
+  return MLAMG_OK;
+}
+
+int mlamg_comm_destroy(mlamg_comm* c) {
+  if (c) {
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    delete c;
+  }
+  return MLAMG_OK;
+}
+
+int mlamg_comm_allreduce_sum(mlamg_comm* c, double* buf, int64_t n, void* stream) {
+  MLAMG_REQUIRE(c && (n == 0 || buf), "NULL argument");
+  MLAMG_NCCL(ncclAllReduce(buf, buf, (size_t)n, ncclFloat64, ncclSum, c->comm, S(stream)));
+  return MLAMG_OK;
+}
+
+int mlamg_halo_create(mlamg_comm* c, int64_t n_own, int32_t n_nbr, const int32_t* nbr,
+                      const int64_t* send_cnt, const int32_t* send_idx_host,
+                      const int64_t* recv_cnt, mlamg_halo** out) {
+  MLAMG_REQUIRE(c && out && n_own >= 0 && n_nbr >= 0, "invalid argument");
+  MLAMG_REQUIRE(n_nbr == 0 || (nbr && send_cnt && recv_cnt), "NULL argument");
+  auto* h = new mlamg_halo();
+  h->c = c;
+  h->n_own = n_own;
+  int64_t so = 0, ro = 0;
+  for (int q = 0; q < n_nbr; ++q) {
+    if (nbr[q] < 0 || nbr[q] >= c->nranks || nbr[q] == c->rank || send_cnt[q] < 0 || recv_cnt[q] < 0) {
+      delete h;
+      set_error("mlamg_halo_create: invalid neighbour entry");
+      return MLAMG_EINVAL;
+    }
+    h->nbr.push_back(nbr[q]);
+    h->send_off.push_back(so);
+    h->send_cnt.push_back(send_cnt[q]);
+    h->recv_off.push_back(ro);
+    h->recv_cnt.push_back(recv_cnt[q]);
+    so += send_cnt[q];
+    ro += recv_cnt[q];
+  }
+  h->n_send = so;
+  h->n_ghost = ro;
+  for (int64_t i = 0; i < so; ++i)
+    if (send_idx_host[i] < 0 || send_idx_host[i] >= n_own) {
+      delete h;
+      set_error("mlamg_halo_create: send index out of range");
+      return MLAMG_EINVAL;
+    }
+  if (so) {
+    if (hipMalloc(&h->send_idx, sizeof(int32_t) * so) != hipSuccess ||
+        hipMalloc(&h->send_buf, sizeof(double) * so) != hipSuccess ||
+        hipMemcpy(h->send_idx, send_idx_host, sizeof(int32_t) * so, hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      if (h->send_idx) (void)hipFree(h->send_idx);
+      if (h->send_buf) (void)hipFree(h->send_buf);
+      delete h;
+      set_error("mlamg_halo_create: device allocation failed");
+      return MLAMG_ENOMEM;
+    }
+  }
+  *out = h;
+  return MLAMG_OK;
+}
+
+int mlamg_halo_destroy(mlamg_halo* h) {
+  if (h) {
+    if (h->send_idx) (void)hipFree(h->send_idx);
+    if (h->send_buf) (void)hipFree(h->send_buf);
+    delete h;
+  }
+  return MLAMG_OK;
+}
+
+int mlamg_halo_exchange(mlamg_halo* h, double* x_ext, void* stream) {
+  MLAMG_REQUIRE(h && (h->n_own + h->n_ghost == 0 || x_ext), "NULL argument");
+  return halo_exchange_impl(h, x_ext, S(stream));
+}
+
+int mlamg_dhier_create(mlamg_comm* c, const mlamg_csr* A_loc, const double* dinv_w,
+                       const mlamg_csr* P_loc, const mlamg_csr* R_own, mlamg_halo* halo_x,
+                       mlamg_halo* halo_r, mlamg_hier* coarse, const int64_t* c_lo_all,
+                       const int64_t* c_hi_all, mlamg_dhier** out) {
+  MLAMG_REQUIRE(c && A_loc && dinv_w && P_loc && R_own && halo_x && halo_r && coarse && c_lo_all &&
+                    c_hi_all && out,
+                "NULL argument");
+  auto* D = new mlamg_dhier();
+  D->c = c;
+  D->A = A_loc;
+  D->P = P_loc;
+  D->R = R_own;
+  D->dinv = dinv_w;
+  D->hx = halo_x;
+  D->hr = halo_r;
+  D->coarse = coarse;
+  D->n_own = A_loc->n_rows;
+  D->nc = P_loc->n_cols;
+  D->c_lo_all.assign(c_lo_all, c_lo_all + c->nranks);
+  D->c_hi_all.assign(c_hi_all, c_hi_all + c->nranks);
+  D->c_lo = D->c_lo_all[c->rank];
+  D->c_hi = D->c_hi_all[c->rank];
+  auto bad = [&](const char* m) {
+    delete D;
+    set_error(std::string("mlamg_dhier_create: ") + m);
+    return MLAMG_EINVAL;
+  };
+  if (A_loc->n_cols != D->n_own + halo_x->n_ghost) return bad("A_loc columns != n_own + x ghosts");
+  if (halo_x->n_own != D->n_own || halo_r->n_own != D->n_own) return bad("halo n_own mismatch");
+  if (P_loc->n_rows != D->n_own) return bad("P_loc rows != n_own");
+  if (R_own->n_rows != D->c_hi - D->c_lo) return bad("R_own rows != owned coarse rows");
+  if (R_own->n_cols != D->n_own + halo_r->n_ghost) return bad("R_own columns != n_own + r ghosts");
+  for (int q = 0; q < c->nranks; ++q)
+    if (D->c_lo_all[q] < 0 || D->c_hi_all[q] < D->c_lo_all[q] || D->c_hi_all[q] > D->nc)
+      return bad("coarse segment out of range");
+  const int64_t next = std::max(D->n_own + halo_r->n_ghost, D->n_own + halo_x->n_ghost);
+  const int64_t nb = std::max<int64_t>(A_loc->n_blocks, 1);
+  if (hipMalloc(&D->r_ext, sizeof(double) * std::max<int64_t>(next, 1)) != hipSuccess ||
+      hipMalloc(&D->t_ext, sizeof(double) * std::max<int64_t>(next, 1)) != hipSuccess ||
+      hipMalloc(&D->bc, sizeof(double) * std::max<int64_t>(D->nc, 1)) != hipSuccess ||
+      hipMalloc(&D->partial, sizeof(double) * (nb + 1)) != hipSuccess ||
+      hipMalloc(&D->flags, sizeof(int32_t) * 2) != hipSuccess) {
+    delete D;
+    set_error("mlamg_dhier_create: device allocation failed");
+    return MLAMG_ENOMEM;
+  }
+  (void)hipMemset(D->r_ext, 0, sizeof(double) * std::max<int64_t>(next, 1));
+  (void)hipMemset(D->t_ext, 0, sizeof(double) * std::max<int64_t>(next, 1));
+  *out = D;
+  return MLAMG_OK;
+}
+
+int mlamg_dhier_destroy(mlamg_dhier* D) {
+  if (D) {
+    for (void* p : {(void*)D->r_ext, (void*)D->t_ext, (void*)D->bc, (void*)D->partial,
+                    (void*)D->flags})
+      if (p) (void)hipFree(p);
+    delete D;
+  }
+  return MLAMG_OK;
+}
+
+int mlamg_dhier_set_coarse_graph(mlamg_dhier* D, int use_graph) {
+  MLAMG_REQUIRE(D, "NULL argument");
+  D->coarse_graph = use_graph;
+  return MLAMG_OK;
+}
+
+// allgatherv of the owned coarse segments into the replicated b_c
+static int allgather_segments(mlamg_dhier* D, hipStream_t s) {
+  const int P = D->c->nranks, me = D->c->rank;
+  if (P == 1) return MLAMG_OK;
+  MLAMG_NCCL(ncclGroupStart());
+  const size_t mine = (size_t)(D->c_hi - D->c_lo);
+  for (int q = 0; q < P; ++q) {
+    if (q == me) continue;
+    if (mine) MLAMG_NCCL(ncclSend(D->bc + D->c_lo, mine, ncclFloat64, q, D->c->comm, s));
+    const size_t theirs = (size_t)(D->c_hi_all[q] - D->c_lo_all[q]);
+    if (theirs)
+      MLAMG_NCCL(ncclRecv(D->bc + D->c_lo_all[q], theirs, ncclFloat64, q, D->c->comm, s));
+  }
+  MLAMG_NCCL(ncclGroupEnd());
+  return MLAMG_OK;
+}
+
+static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, double tol,
+                  hipStream_t s) {
+  int32_t* counter = D->flags;
+  int32_t* done = D->flags + 1;
+  const mlamg_csr* A = D->A;
+  // pre-smoothing from the end-of-cycle residual (bitwise a Jacobi sweep)
+  MLAMG_TRY(jacobi_from_residual(x_ext, D->dinv, D->r_ext, D->n_own, done, s));
+  MLAMG_TRY(halo_exchange_impl(D->hx, x_ext, s));
+  MLAMG_TRY(residual_impl(A, b, x_ext, D->r_ext, nullptr, nullptr, nullptr, done, 0.0, nullptr,
+                          nullptr, nullptr, s));
+  MLAMG_TRY(halo_exchange_impl(D->hr, D->r_ext, s));
+  MLAMG_TRY(spmv_set(D->R, D->r_ext, D->bc + D->c_lo, done, s));
+  MLAMG_TRY(allgather_segments(D, s));
+  double* xc = nullptr;
+  MLAMG_TRY(hier_coarse_cycle(D->coarse, D->bc, &xc, D->coarse_graph, s));
+  MLAMG_TRY(spmv_add(D->P, xc, x_ext, done, s));
+  MLAMG_TRY(halo_exchange_impl(D->hx, x_ext, s));
+  MLAMG_TRY(jacobi_sweep(A, D->dinv, b, x_ext, D->t_ext, false, done, s));
+  MLAMG_TRY(halo_exchange_impl(D->hx, D->t_ext, s));
+  // r = b - A t with per-block ||r||^2 partials, x <- t; then the global norm
+  MLAMG_TRY(residual_partials(A, b, D->t_ext, D->r_ext, x_ext, D->t_ext, D->partial, done, s));
+  const int nb = (int)A->n_blocks;
+  hipLaunchKernelGGL(k_local_sum, dim3(1), dim3(1024), 0, s, D->partial, nb);
+  MLAMG_HIP(hipGetLastError());
+  if (D->c->nranks > 1)
+    MLAMG_NCCL(ncclAllReduce(D->partial + nb, D->partial + nb, 1, ncclFloat64, ncclSum,
+                             D->c->comm, s));
+  hipLaunchKernelGGL(k_norm_finish, dim3(1), dim3(1), 0, s, D->partial + nb, hist, counter, done,
+                     tol);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cycles, double tol,
+                       double* res_hist, int32_t* cycles_done_host, void* stream) {
+  MLAMG_REQUIRE(D && b && x_ext, "NULL argument");
+  MLAMG_REQUIRE(n_cycles >= 0, "n_cycles < 0");
+  hipStream_t s = S(stream);
+  MLAMG_HIP(hipMemsetAsync(D->flags, 0, 2 * sizeof(int32_t), s));
+  MLAMG_TRY(halo_exchange_impl(D->hx, x_ext, s));
+  MLAMG_TRY(residual_impl(D->A, b, x_ext, D->r_ext, nullptr, nullptr, nullptr, nullptr, 0.0,
+                          nullptr, nullptr, nullptr, s));
+  for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(dcycle(D, b, x_ext, res_hist, tol, s));
+  if (cycles_done_host) {
+    int32_t cnt = 0;
+    MLAMG_HIP(hipMemcpyAsync(&cnt, D->flags, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipStreamSynchronize(s));
+    *cycles_done_host = cnt;
+  }
+  return MLAMG_OK;
+}
+
+}  // extern "C"

@@ -92,4 +92,7 @@ void* scratch(size_t bytes, int slot);
 int launch_spmv_plain(const mlamg_csr* A, const double* x, double* y, hipStream_t s);
 int exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s);  // out[n] = total
 int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, hipStream_t s);
+// entries of a[0..n) outside [lo, hi) (device check before any kernel indexes with them); syncs
+int count_out_of_range(const int32_t* a, int64_t n, int64_t lo, int64_t hi, hipStream_t s,
+                       int64_t* bad_out);
 }  // namespace mlamg

@@ -254,6 +254,9 @@ int mlamg_bellman_ford(const mlamg_csr* G, const int32_t* seeds, int32_t k, floa
   MLAMG_REQUIRE(G->n_rows == G->n_cols, "graph must be square");
   hipStream_t s = S(stream);
   const int64_t n = G->n_rows;
+  int64_t bad = 0;
+  MLAMG_TRY(count_out_of_range(seeds, k, 0, n, s, &bad));
+  MLAMG_REQUIRE(bad == 0, "seed index out of range [0, n)");
   float* w = nullptr;
   int32_t* flags = nullptr;
   MLAMG_HIP(hipMalloc(&w, sizeof(float) * std::max<int64_t>(G->nnz, 1)));
@@ -298,6 +301,11 @@ int mlamg_labels_to_columns(const int32_t* label, int64_t n, const int32_t* seed
                             int32_t* col, void* stream) {
   MLAMG_REQUIRE(label && col && (k == 0 || seeds), "NULL argument");
   hipStream_t s = S(stream);
+  int64_t bad = 0;
+  MLAMG_TRY(count_out_of_range(seeds, k, 0, n, s, &bad));
+  MLAMG_REQUIRE(bad == 0, "seed index out of range [0, n)");
+  MLAMG_TRY(count_out_of_range(label, n, -1, n, s, &bad));
+  MLAMG_REQUIRE(bad == 0, "label out of range [-1, n)");
   int32_t* pos = nullptr;
   MLAMG_HIP(hipMalloc(&pos, sizeof(int32_t) * std::max<int64_t>(n, 1)));
   if (n) hipLaunchKernelGGL(k_pos_init, g1(n), dim3(256), 0, s, pos, n);
@@ -312,6 +320,9 @@ int mlamg_labels_to_columns(const int32_t* label, int64_t n, const int32_t* seed
 int mlamg_aggregate_op(const int32_t* col, int64_t n, int64_t k, mlamg_csr** out, void* stream) {
   MLAMG_REQUIRE(out && (n == 0 || col), "NULL argument");
   hipStream_t s = S(stream);
+  int64_t bad = 0;
+  MLAMG_TRY(count_out_of_range(col, n, -1, k, s, &bad));
+  MLAMG_REQUIRE(bad == 0, "aggregate column out of range [-1, k)");
   int32_t* cnt = nullptr;
   MLAMG_HIP(hipMalloc(&cnt, sizeof(int32_t) * (n + 1)));
   int32_t* ip = nullptr;
@@ -354,6 +365,9 @@ int mlamg_lloyd_cluster(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxit
   MLAMG_REQUIRE(G->n_rows == G->n_cols, "graph must be square");
   hipStream_t s = S(stream);
   const int64_t n = G->n_rows;
+  int64_t bad = 0;
+  MLAMG_TRY(count_out_of_range(seeds, k, 0, n, s, &bad));
+  MLAMG_REQUIRE(bad == 0, "seed index out of range [0, n)");
   int32_t* iw = nullptr;
   unsigned long long* mx = nullptr;
   MLAMG_HIP(hipMalloc(&iw, sizeof(int32_t) * (n + k + 2)));

@@ -67,6 +67,11 @@ struct mlamg_hier {
   double* g_hist = nullptr;
   double g_tol = -1.0;
   hipStream_t cap_stream = nullptr;
+  // captured coarse cycle (distributed executor: this hierarchy = replicated levels 1..L)
+  hipGraph_t cgraph = nullptr;
+  hipGraphExec_t cexec = nullptr;
+  const double* cg_b = nullptr;
+  double* cg_res = nullptr;
 };
 
 using namespace mlamg;
@@ -76,6 +81,10 @@ static void hier_free_graph(mlamg_hier* H) {
   if (H->graph) (void)hipGraphDestroy(H->graph);
   H->exec = nullptr;
   H->graph = nullptr;
+  if (H->cexec) (void)hipGraphExecDestroy(H->cexec);
+  if (H->cgraph) (void)hipGraphDestroy(H->cgraph);
+  H->cexec = nullptr;
+  H->cgraph = nullptr;
 }
 
 static int hier_prepare(mlamg_hier* H) {
@@ -91,10 +100,8 @@ static int hier_prepare(mlamg_hier* H) {
   };
   for (size_t l = 0; l < H->lv.size(); ++l) {
     const int64_t n = H->lv[l].n;
-    if (l > 0) {
-      add(n);
-      add(n);
-    }
+    add(n);  // x: level 0 also needs it when this hierarchy serves as a coarse cycle
+    add(n);
     add(n);
     add(n);
   }
@@ -116,10 +123,8 @@ static int hier_prepare(mlamg_hier* H) {
   };
   for (size_t l = 0; l < H->lv.size(); ++l) {
     Level& L = H->lv[l];
-    if (l > 0) {
-      L.x = take(L.n);
-      L.b = take(L.n);
-    }
+    L.x = take(L.n);
+    L.b = take(L.n);
     L.r = take(L.n);
     L.tmp = take(L.n);
   }
@@ -203,6 +208,40 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
                           cur != x ? x : nullptr, cur != x ? cur : nullptr, H->partial, s));
   return MLAMG_OK;
 }
+
+namespace mlamg {
+// One cycle from a zero guess on (b -> *x_out) treating level 0 of H as a coarse level
+// (used by the distributed executor, whose H holds the replicated levels 1..L).
+int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
+                      hipStream_t s) {
+  MLAMG_TRY(hier_prepare(H));
+  if (!use_graph) return cycle_coarse(H, 0, b, x_out, s);
+  if (!(H->cexec && H->cg_b == b)) {
+    if (H->cexec) (void)hipGraphExecDestroy(H->cexec);
+    if (H->cgraph) (void)hipGraphDestroy(H->cgraph);
+    H->cexec = nullptr;
+    H->cgraph = nullptr;
+    if (!H->cap_stream) MLAMG_HIP(hipStreamCreateWithFlags(&H->cap_stream, hipStreamNonBlocking));
+    MLAMG_HIP(hipStreamBeginCapture(H->cap_stream, hipStreamCaptureModeThreadLocal));
+    double* res = nullptr;
+    int rc = cycle_coarse(H, 0, b, &res, H->cap_stream);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(H->cap_stream, &g);
+    if (rc != MLAMG_OK) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    MLAMG_HIP(e);
+    H->cgraph = g;
+    MLAMG_HIP(hipGraphInstantiate(&H->cexec, g, nullptr, nullptr, 0));
+    H->cg_b = b;
+    H->cg_res = res;
+  }
+  MLAMG_HIP(hipGraphLaunch(H->cexec, s));
+  *x_out = H->cg_res;
+  return MLAMG_OK;
+}
+}  // namespace mlamg
 
 extern "C" {
 

@@ -89,6 +89,9 @@ int csr_finalize(mlamg_csr* A, hipStream_t stream) {
   MLAMG_HIP(hipStreamSynchronize(stream));
   MLAMG_REQUIRE(ip[0] == 0, "indptr[0] != 0");
   MLAMG_REQUIRE(ip[n] == A->nnz, "indptr[n] != nnz");
+  int64_t bad = 0;
+  MLAMG_TRY(count_out_of_range(A->indices, A->nnz, 0, A->n_cols, stream, &bad));
+  MLAMG_REQUIRE(bad == 0, "column index out of range [0, n_cols)");
   std::vector<int32_t>& blk = A->blk_host;
   blk.clear();
   blk.reserve(n / 64 + 2);

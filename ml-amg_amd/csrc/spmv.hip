@@ -193,6 +193,20 @@ int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* 
   return MLAMG_OK;
 }
 
+// r = b - A x with per-block sums of r^2 in partial[0..n_blocks) (no finalize), optional copy
+int residual_partials(const mlamg_csr* A, const double* b, const double* x, double* r,
+                      double* copy_to, const double* copy_from, double* partial,
+                      const int32_t* done, hipStream_t s) {
+  Epi ep{};
+  ep.b = b;
+  ep.y = r;
+  ep.done = done;
+  ep.copy_to = copy_to;
+  ep.copy_from = copy_from;
+  ep.partial = partial;
+  return launch<EPI_RESID, true>(A, x, ep, s);
+}
+
 int jacobi_sweep(const mlamg_csr* A, const double* dinv, const double* b, const double* xin,
                  double* xout, bool explicit_form, const int32_t* done, hipStream_t s) {
   Epi ep{};

@@ -167,3 +167,34 @@ int mlamg_diag_inv(const mlamg_csr* A, double omega, double* dinv_w, void* strea
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- index validation
+namespace mlamg {
+__global__ void k_count_out_of_range(const int32_t* __restrict__ a, int64_t n, int64_t lo,
+                                     int64_t hi, unsigned long long* bad) {
+  unsigned long long c = 0;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t v = a[i];
+    c += (v < lo || v >= hi) ? 1ull : 0ull;
+  }
+  if (c) atomicAdd(bad, c);
+}
+
+// number of entries of a[0..n) outside [lo, hi); syncs `s`
+int count_out_of_range(const int32_t* a, int64_t n, int64_t lo, int64_t hi, hipStream_t s,
+                       int64_t* bad_out) {
+  *bad_out = 0;
+  if (n <= 0) return MLAMG_OK;
+  unsigned long long* d = static_cast<unsigned long long*>(scratch(sizeof(unsigned long long), 3));
+  MLAMG_REQUIRE(d, "scratch allocation failed");
+  MLAMG_HIP(hipMemsetAsync(d, 0, sizeof(unsigned long long), s));
+  const int nb = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(k_count_out_of_range, dim3(nb), dim3(256), 0, s, a, n, lo, hi, d);
+  MLAMG_HIP(hipGetLastError());
+  unsigned long long h = 0;
+  MLAMG_HIP(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  *bad_out = (int64_t)h;
+  return MLAMG_OK;
+}
+}  // namespace mlamg

@@ -93,6 +93,18 @@ SIGNATURES = {
     "mlamg_hier_set_smoothing": (c_int, [c_vp, c_int, c_int]),
     "mlamg_hier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_int, c_vp]),
     "mlamg_hier_cycle_bytes": (c_int, [c_vp, P_dbl]),
+    "mlamg_comm_unique_id": (c_int, [c_vp]),
+    "mlamg_comm_create": (c_int, [c_vp, c_int, c_int, c_vpp]),
+    "mlamg_comm_destroy": (c_int, [c_vp]),
+    "mlamg_comm_allreduce_sum": (c_int, [c_vp, c_vp, c_i64, c_vp]),
+    "mlamg_halo_create": (c_int, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vpp]),
+    "mlamg_halo_destroy": (c_int, [c_vp]),
+    "mlamg_halo_exchange": (c_int, [c_vp, c_vp, c_vp]),
+    "mlamg_dhier_create": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                   c_vpp]),
+    "mlamg_dhier_destroy": (c_int, [c_vp]),
+    "mlamg_dhier_set_coarse_graph": (c_int, [c_vp, c_int]),
+    "mlamg_dhier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_vp]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -1,0 +1,130 @@
+"""Row partition of the fine level across GPUs and the halo maps it needs (host logic, numpy).
+
+The reference has no domain decomposition (its only parallelism is a task farm over independent
+grids, ns/parallel/pool.py:139-186); this is the north star's fine-level row split (SURVEY.md
+§8e). Every rank holds the full hierarchy (setup is deterministic and replicated), so every rank
+can derive every other rank's needs locally and no setup communication is required.
+
+Per rank r (rows [lo_r, hi_r) of the fine level, contiguous, near-equal):
+  A_loc   rows lo..hi of A0, columns renumbered into x_ext = [owned (hi-lo) | ghosts]
+  P_loc   rows lo..hi of P0 (columns = full coarse index space, replicated coarse vector)
+  R_own   rows c_lo..c_hi of R0 = P0^T (coarse rows whose aggregate seed lies in [lo, hi)),
+          columns renumbered into r_ext = [owned | r-ghosts]
+  x halo  ghosts of A_loc: for each neighbour q, ascending global indices owned by q
+  r halo  ghosts of R_own, same layout
+Ghost order = ascending global index, which is also grouped by owner (owners are contiguous).
+Because local rows keep their stored column order, every local product sums exactly like the
+single-GPU kernel: the distributed iterate is bitwise the single-GPU iterate.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+
+def row_ranges(n, world):
+    """Contiguous near-equal row blocks [lo, hi) per rank."""
+    base, extra = divmod(n, world)
+    sizes = [base + (1 if r < extra else 0) for r in range(world)]
+    bounds = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    return [(int(bounds[r]), int(bounds[r + 1])) for r in range(world)]
+
+
+def owner_of(idx, bounds_hi):
+    """Rank owning each global index (bounds_hi = array of hi per rank)."""
+    return np.searchsorted(bounds_hi, idx, side="right")
+
+
+class Halo:
+    """Ghost layout of one rank: recv from neighbours into ext[n_own:], send owned entries."""
+
+    def __init__(self, n_own, ghosts, ghost_owner, sends):
+        self.n_own = n_own
+        self.ghosts = ghosts                # global ids, ascending
+        self.ghost_owner = ghost_owner
+        self.sends = sends                  # {q: local indices (into owned) to send to q}
+        nbrs = sorted(set(np.unique(ghost_owner).tolist()) | set(sends.keys()))
+        self.neighbors = nbrs
+        self.recv_counts = [int(np.sum(ghost_owner == q)) for q in nbrs]
+        self.send_counts = [len(sends.get(q, ())) for q in nbrs]
+        self.send_idx = (np.concatenate([np.asarray(sends.get(q, []), np.int32) for q in nbrs])
+                         if nbrs else np.zeros(0, np.int32)).astype(np.int32)
+
+    @property
+    def n_ghost(self):
+        return len(self.ghosts)
+
+
+def _ghost_sets(M_rows_cols, lo, hi):
+    cols = np.unique(M_rows_cols)
+    return cols[(cols < lo) | (cols >= hi)]
+
+
+def _remap(M, lo, hi, ghosts):
+    """Renumber columns: owned j -> j - lo, ghost g -> n_own + position(g). Stored order kept."""
+    n_own = hi - lo
+    cols = M.indices.astype(np.int64)
+    out = np.empty_like(cols)
+    own = (cols >= lo) & (cols < hi)
+    out[own] = cols[own] - lo
+    gi = np.searchsorted(ghosts, cols[~own])
+    out[~own] = n_own + gi
+    return sp.csr_matrix((M.data, out.astype(np.int32), M.indptr.copy()),
+                         shape=(M.shape[0], n_own + len(ghosts)))
+
+
+def build(A0, P0, seeds, world, rank=None):
+    """Partition maps for all ranks (or one rank). A0: n x n CSR, P0: n x nc CSR, seeds: sorted
+    seed node of each coarse unknown (aggregate j's seed is seeds[j]).
+
+    Returns a list (per rank) of dicts, or the dict of `rank`.
+    """
+    A0 = A0.tocsr()
+    P0 = P0.tocsr()
+    n = A0.shape[0]
+    nc = P0.shape[1]
+    seeds = np.asarray(seeds, dtype=np.int64)
+    if len(seeds) != nc or (len(seeds) > 1 and np.any(np.diff(seeds) <= 0)):
+        raise ValueError("coarse unknowns must be ordered by strictly increasing seed node")
+    R0 = P0.T.tocsr()
+    R0.sort_indices()
+    ranges = row_ranges(n, world)
+    his = np.array([h for _, h in ranges], dtype=np.int64)
+    # coarse ownership by seed owner: contiguous because seeds are sorted
+    c_bounds = [int(np.searchsorted(seeds, lo)) for lo, _ in ranges] + [nc]
+    c_ranges = [(c_bounds[r], c_bounds[r + 1]) for r in range(world)]
+    # ghost sets of every rank (needed to derive send lists)
+    xg, rg = [], []
+    for r, (lo, hi) in enumerate(ranges):
+        Ar = A0[lo:hi]
+        xg.append(_ghost_sets(Ar.indices, lo, hi))
+        clo, chi = c_ranges[r]
+        Rr = R0[clo:chi]
+        rg.append(_ghost_sets(Rr.indices, lo, hi))
+    out = []
+    for r, (lo, hi) in enumerate(ranges):
+        if rank is not None and r != rank:
+            out.append(None)
+            continue
+        clo, chi = c_ranges[r]
+        sends_x, sends_r = {}, {}
+        for q in range(world):
+            if q == r:
+                continue
+            need = xg[q][(xg[q] >= lo) & (xg[q] < hi)]
+            if len(need):
+                sends_x[q] = (need - lo).astype(np.int32)
+            need = rg[q][(rg[q] >= lo) & (rg[q] < hi)]
+            if len(need):
+                sends_r[q] = (need - lo).astype(np.int32)
+        hx = Halo(hi - lo, xg[r], owner_of(xg[r], his), sends_x)
+        hr = Halo(hi - lo, rg[r], owner_of(rg[r], his), sends_r)
+        A_loc = _remap(A0[lo:hi], lo, hi, xg[r])
+        R_own = _remap(R0[clo:chi], lo, hi, rg[r])
+        P_loc = P0[lo:hi].copy()
+        out.append({
+            "rank": r, "world": world, "lo": lo, "hi": hi, "n": n, "nc": nc,
+            "c_lo": clo, "c_hi": chi, "c_ranges": c_ranges, "ranges": ranges,
+            "A_loc": A_loc, "P_loc": P_loc, "R_own": R_own, "halo_x": hx, "halo_r": hr,
+        })
+    return out[rank] if rank is not None else out

@@ -311,12 +311,8 @@ def build_hierarchy(A, alpha=0.1, strength_mode="invabs", seed=0, sort_seeds=Tru
     return levels, A
 
 
-def vcycle_solve(levels, Ac, b, x, n_cycles, tol=0.0, nu_pre=1, nu_post=1, lu=None):
-    """Multilevel Jacobi V(nu_pre, nu_post) iteration in the device executor's order
-    (mlamg hier.hip; each level = MLAMG.py:189-195 with the coarse solve recursing).
-    Returns (x, residual history). lu: a pre-factorised coarse solve (spla.factorized)."""
-    if lu is None:
-        lu = spla.factorized(sp.csc_matrix(Ac))
+def make_cycle(levels, lu, nu_pre=1, nu_post=1):
+    """cycle(l, b, x): one V-cycle at level l (x=None: zero guess), coarsest solved by lu."""
 
     def cycle(l, b, x):
         if l == len(levels):
@@ -331,6 +327,16 @@ def vcycle_solve(levels, Ac, b, x, n_cycles, tol=0.0, nu_pre=1, nu_post=1, lu=No
         x = jacobi_mlamg(A, Dw, b, x, nu_post)
         return x
 
+    return cycle
+
+
+def vcycle_solve(levels, Ac, b, x, n_cycles, tol=0.0, nu_pre=1, nu_post=1, lu=None):
+    """Multilevel Jacobi V(nu_pre, nu_post) iteration in the device executor's order
+    (mlamg hier.hip; each level = MLAMG.py:189-195 with the coarse solve recursing).
+    Returns (x, residual history). lu: a pre-factorised coarse solve (spla.factorized)."""
+    if lu is None:
+        lu = spla.factorized(sp.csc_matrix(Ac))
+    cycle = make_cycle(levels, lu, nu_pre, nu_post)
     x = x.copy()
     hist = []
     A0 = levels[0]["A"] if levels else Ac

@@ -149,9 +149,9 @@ def test_spgemm_scipy_layout_random(ml, seed):
 def test_spgemm_drops_exact_zeros(ml):
     A = sp.csr_matrix(np.array([[1.0, 1.0], [1.0, -1.0]]))
     B = sp.csr_matrix(np.array([[1.0, 2.0], [-1.0, 2.0]]))
-    C = A @ B
+    C = A @ B  # [[1-1, 2+2], [1+1, 2-2]]: two entries cancel exactly and are dropped
     Cd = (ml.sparse.DeviceCSR.from_scipy(A) @ ml.sparse.DeviceCSR.from_scipy(B)).to_scipy()
-    assert C.nnz == Cd.nnz == 3
+    assert C.nnz == Cd.nnz == 2
     assert np.array_equal(Cd.toarray(), C.toarray())
 
 

@@ -1,0 +1,83 @@
+"""HBM traffic of the roofline kernel from rocprofv3 PMC counters (run on the GPU box).
+
+Two separate passes (FETCH_SIZE costs 3 TCC slots, WRITE_SIZE 2: they cannot share one pass),
+counters only, no tracing domains. Both report KiB per dispatch. gfx950 correction
+(/opt/skills/guides/MI355X_MICROARCH.md §HBM): FETCH_SIZE counts exactly half the bytes of a
+wide coalesced streaming read, so reads are doubled; WRITE_SIZE is exact for streaming stores.
+This parent process never touches the GPU (rocprofv3 runs the driver as a child).
+
+Writes gpurun_out/pmc/spmv_c4_pmc.json and the raw counter CSVs (only gpurun_out/ comes back
+from the GPU box); they are then committed as profiles/spmv_c4_pmc.json (read by bench.py as
+roofline.traffic) and profiles/<round>/.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out", "pmc")
+KERNEL = "k_csr_stream"
+
+
+def run_pass(counter):
+    d = os.path.join(OUT, counter)
+    shutil.rmtree(d, ignore_errors=True)
+    os.makedirs(d, exist_ok=True)
+    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
+           sys.executable, os.path.join(ROOT, "tools", "spmv_driver.py")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"rocprofv3 failed:\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}")
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise RuntimeError(f"no counter_collection.csv under {d}")
+    vals = []
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    vals.append(float(row["Counter_Value"]))
+    return vals, files
+
+
+def main():
+    round_tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    fetch, f1 = run_pass("FETCH_SIZE")
+    write, f2 = run_pass("WRITE_SIZE")
+    if not fetch or not write:
+        raise RuntimeError("no dispatches of the SpMV kernel found in the counter CSVs")
+    # skip the first (cold) dispatch
+    fk = sorted(fetch[1:] or fetch)
+    wk = sorted(write[1:] or write)
+    fetch_kib = fk[len(fk) // 2]
+    write_kib = wk[len(wk) // 2]
+    read_bytes = 2.0 * fetch_kib * 1024.0
+    write_bytes = write_kib * 1024.0
+    n = 216 ** 3
+    nnz = 70263936
+    algo = 12.0 * nnz + 4.0 * (n + 1) + 8.0 * n + 8.0 * n
+    res = {
+        "kernel": "k_csr_stream<EPI_AXPBY> (fine-level SpMV, C4 216^3)",
+        "fetch_size_kib_median": fetch_kib,
+        "write_size_kib_median": write_kib,
+        "correction": "reads = 2 x FETCH_SIZE (gfx950 wide-read under-count), writes = WRITE_SIZE",
+        "hbm_read_bytes_per_launch": read_bytes,
+        "hbm_write_bytes_per_launch": write_bytes,
+        "hbm_bytes_per_launch": read_bytes + write_bytes,
+        "algorithmic_bytes_per_launch": algo,
+        "traffic_over_algorithmic": (read_bytes + write_bytes) / algo,
+        "dispatches": len(fetch),
+    }
+    with open(os.path.join(OUT, "spmv_c4_pmc.json"), "w") as fh:
+        json.dump(res, fh, indent=1)
+    for f, tag in ((f1[0], "FETCH_SIZE"), (f2[0], "WRITE_SIZE")):
+        shutil.copy(f, os.path.join(OUT, f"spmv_c4_pmc_{tag}_{round_tag}.csv"))
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

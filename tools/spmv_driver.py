@@ -1,0 +1,28 @@
+"""Run only the fine-level C4 SpMV (the roofline kernel) `reps` times — the program profiled by
+tools/pmc_traffic.py and tools/profile.sh under rocprofv3."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "ml-amg_amd")):
+    sys.path.insert(0, p)
+
+
+def main():
+    import torch
+    from mlamg import problems
+    from mlamg.sparse import DeviceCSR
+
+    n1 = int(os.environ.get("MLAMG_N", "216"))
+    reps = int(os.environ.get("MLAMG_REPS", "20"))
+    A = DeviceCSR.from_scipy(problems.poisson_3d_7pt(n1), check=False)
+    x = torch.randn(A.shape[1], dtype=torch.float64, device="cuda")
+    y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
+    for _ in range(reps):
+        A.matvec(x, out=y)
+    torch.cuda.synchronize()
+    print(f"spmv_driver: n={A.shape[0]} nnz={A.nnz} reps={reps}")
+
+
+if __name__ == "__main__":
+    main()
