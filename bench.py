@@ -152,11 +152,21 @@ def main():
 
     # dominant kernel: the fine-level CSR SpMV (headline unit 1)
     A0 = H.levels[0].A
+    fmt0 = A0.get_format()[0]
     xs = torch.randn(n, dtype=torch.float64, device="cuda")
     ys = torch.empty_like(xs)
     t_spmv = time_kernel(lambda: A0.matvec(xs, out=ys), reps=50)
     B = spmv_bytes(n, n, A0.nnz)
     achieved = B / t_spmv / 1e9
+    # A/B of the exact-order SpMV kernels on a separate copy of A0 (same bits, different layout)
+    from mlamg.sparse import DeviceCSR
+    Ab = DeviceCSR.from_scipy(A, check=False)
+    ab = {}
+    for fmt in ("csr_stream", "sell"):
+        Ab.set_format(fmt)
+        t = time_kernel(lambda: Ab.matvec(xs, out=ys), reps=30)
+        ab[fmt] = {"us": round(t * 1e6, 2), "GBps": round(B / t / 1e9, 1)}
+    del Ab
     pmc = load_traffic("spmv_c4_pmc.json")
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     cyc_bytes = H.cycle_bytes()
@@ -183,7 +193,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "fine-level CSR-stream SpMV (k_csr_stream<AXPBY>)",
+            "kernel": f"fine-level CSR SpMV, y = A x ({fmt0} kernel, scipy summation order)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
@@ -193,6 +203,9 @@ def main():
             "avg_launch_us": round(t_spmv * 1e6, 2),
         },
         "cycle_algorithmic_GBps": round(cyc_bytes / (dt / args.steps) / 1e9, 1),
+        "fine_spmv_formats": ab,
+        "operator_formats": [{k: v[0] + (f"/{v[1]}" if v[1] else "") for k, v in f.items()}
+                             for f in H.formats()],
         "setup_s": {k: round(v, 3) for k, v in H.timings.items()},
         "conv_factor_10cycles": round(conv, 5),
     }

@@ -66,6 +66,20 @@ int mlamg_csr_device_arrays(const mlamg_csr* A, int32_t** indptr, int32_t** indi
 int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indices_host,
                        double* data_host);
 
+/* SpMV storage/kernel of a handle (the CSR arrays always stay; formats add a device copy):
+ *   CSR_STREAM  LDS-staged row blocks, lane-per-row sums in stored order (scipy's bits)
+ *   SELL        SELL-64 slices, lane-per-row sums in stored order (scipy's bits)
+ *   VECTOR      vec_width lanes per row (0 = auto from the mean row length), lane-strided
+ *               partial sums + xor butterfly: a different, fixed order (oracle vec_matvec),
+ *               for long-row coarse operators that have no scipy counterpart
+ *   AUTO_EXACT  SELL when its padding costs <= 15% extra entries, else CSR_STREAM */
+#define MLAMG_FMT_CSR_STREAM 0
+#define MLAMG_FMT_SELL 1
+#define MLAMG_FMT_VECTOR 2
+#define MLAMG_FMT_AUTO_EXACT 3
+int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream);
+int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored_entries);
+
 /* ---------------------------------------------------------------- hot-path sparse ops
  * Each sums a row left-to-right in stored order with separate multiply and add roundings,
  * i.e. exactly scipy sparsetools csr_matvec, so results are bitwise identical to the CPU path. */

@@ -271,7 +271,7 @@ int mlamg_dhier_create(mlamg_comm* c, const mlamg_csr* A_loc, const double* dinv
     if (D->c_lo_all[q] < 0 || D->c_hi_all[q] < D->c_lo_all[q] || D->c_hi_all[q] > D->nc)
       return bad("coarse segment out of range");
   const int64_t next = std::max(D->n_own + halo_r->n_ghost, D->n_own + halo_x->n_ghost);
-  const int64_t nb = std::max<int64_t>(A_loc->n_blocks, 1);
+  const int64_t nb = part_capacity(A_loc);
   if (hipMalloc(&D->r_ext, sizeof(double) * std::max<int64_t>(next, 1)) != hipSuccess ||
       hipMalloc(&D->t_ext, sizeof(double) * std::max<int64_t>(next, 1)) != hipSuccess ||
       hipMalloc(&D->bc, sizeof(double) * std::max<int64_t>(D->nc, 1)) != hipSuccess ||
@@ -341,7 +341,7 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
   MLAMG_TRY(halo_exchange_impl(D->hx, D->t_ext, s));
   // r = b - A t with per-block ||r||^2 partials, x <- t; then the global norm
   MLAMG_TRY(residual_partials(A, b, D->t_ext, D->r_ext, x_ext, D->t_ext, D->partial, done, s));
-  const int nb = (int)A->n_blocks;
+  const int nb = (int)A->n_part;
   hipLaunchKernelGGL(k_local_sum, dim3(1), dim3(1024), 0, s, D->partial, nb);
   MLAMG_HIP(hipGetLastError());
   if (D->c->nranks > 1)

@@ -7,6 +7,7 @@
 // CPU path (ns/lib/multigrid.py:44,181,191; ns/preconditioner/MLAMG.py:145,191,194).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -70,6 +71,18 @@ struct mlamg_csr {
   std::vector<int32_t> blk_host;
   int32_t max_row_len = 0;
   double avg_row_len = 0.0;
+  // optional SELL-64 copy (slices of 64 consecutive rows stored column-major, padded to the
+  // slice's longest row with col = -1); used by the SpMV family when present
+  int64_t n_slices = 0;
+  int64_t* sell_ptr = nullptr;  // element offset of each slice (n_slices+1)
+  int32_t* sell_col = nullptr;
+  double* sell_val = nullptr;
+  int64_t sell_elems = 0;
+  // CSR-vector format (lane-strided partial sums + butterfly, NOT scipy's order): 0 = off,
+  // else the number of lanes per row (4..64)
+  int32_t vec_width = 0;
+  // number of per-block partial sums a NORM launch writes with the active format
+  int32_t n_part = 0;
 };
 
 // Dense coarse-level inverse (dense.hip)
@@ -79,6 +92,11 @@ struct mlamg_dense {
 };
 
 namespace mlamg {
+// Upper bound on the per-block partial sums a NORM launch of A can write, whatever format is
+// active (CSR-stream: n_blocks; SELL-64: n/256; CSR-vector: n*VW/256 <= n/4), plus one slot.
+inline int64_t part_capacity(const mlamg_csr* A) {
+  return std::max<int64_t>(A->n_blocks, (A->n_rows + 3) / 4) + 2;
+}
 // Allocate device arrays for an (n_rows x n_cols, nnz) CSR and the handle; no partition yet.
 int csr_alloc(int64_t n_rows, int64_t n_cols, int64_t nnz, mlamg_csr** out);
 // Build the CSR-stream row-block partition from the device indptr (syncs `stream`).

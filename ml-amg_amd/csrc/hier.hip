@@ -109,7 +109,7 @@ static int hier_prepare(mlamg_hier* H) {
   add(nc);
   add(nc);
   int64_t maxblk = 1;
-  for (auto& L : H->lv) maxblk = std::max<int64_t>(maxblk, L.A->n_blocks);
+  for (auto& L : H->lv) maxblk = std::max<int64_t>(maxblk, part_capacity(L.A));
   add(maxblk);
   total += 256;
   MLAMG_HIP(hipMalloc(&H->mem, total));

@@ -76,6 +76,9 @@ void csr_free(mlamg_csr* A) {
     if (A->data) (void)hipFree(A->data);
   }
   if (A->blk) (void)hipFree(A->blk);
+  if (A->sell_ptr) (void)hipFree(A->sell_ptr);
+  if (A->sell_col) (void)hipFree(A->sell_col);
+  if (A->sell_val) (void)hipFree(A->sell_val);
   delete A;
 }
 
@@ -120,6 +123,7 @@ int csr_finalize(mlamg_csr* A, hipStream_t stream) {
     blk.push_back((int32_t)r);
   }
   A->n_blocks = (int32_t)(blk.size() - 1);
+  A->n_part = A->n_blocks;
   A->max_row_len = maxlen;
   A->avg_row_len = n ? double(A->nnz) / double(n) : 0.0;
   if (A->blk) (void)hipFree(A->blk);

@@ -149,13 +149,220 @@ __global__ __launch_bounds__(1024) void k_finalize_norm(const double* __restrict
   }
 }
 
+// ---------------------------------------------------------------- SELL-64 variant
+// One wave per slice of 64 consecutive rows, one lane per row; entry k of the slice's rows is
+// stored contiguously for the 64 lanes (col-major), so every load instruction of the wave reads
+// 256 B of indices / 512 B of values with no LDS round trip and no row pointers. Lane i sums
+// its row in stored order, skipping the col = -1 padding: the same bits as csr_matvec.
+template <int OP, bool NORM>
+__global__ __launch_bounds__(kThreads) void k_sell(const int64_t* __restrict__ sp,
+                                                   const int32_t* __restrict__ cols,
+                                                   const double* __restrict__ vals,
+                                                   int64_t n_rows, int64_t n_slices,
+                                                   const double* __restrict__ x, Epi ep) {
+  __shared__ double red[kThreads / 64];
+  if (ep.done && *ep.done) return;
+  const int64_t slice = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  double sq = 0.0;
+  if (slice < n_slices) {
+    const int64_t base = sp[slice];
+    const int w = (int)((sp[slice + 1] - base) >> 6);
+    const int32_t* c = cols + base + lane;
+    const double* v = vals + base + lane;
+    double s = 0.0;
+    int k = 0;
+    for (; k + 4 <= w; k += 4) {
+      int32_t cc[4];
+      double vv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        cc[u] = __builtin_nontemporal_load(c + (int64_t)(k + u) * 64);
+        vv[u] = __builtin_nontemporal_load(v + (int64_t)(k + u) * 64);
+      }
+      double xv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (cc[u] >= 0) s += vv[u] * xv[u];
+    }
+    for (; k < w; ++k) {
+      const int32_t cc = __builtin_nontemporal_load(c + (int64_t)k * 64);
+      const double vv = __builtin_nontemporal_load(v + (int64_t)k * 64);
+      if (cc >= 0) s += vv * x[cc];
+    }
+    const int64_t row = slice * 64 + lane;
+    if (row < n_rows) sq = epilogue<OP>((int)row, s, ep);
+  }
+  if constexpr (NORM) {
+    double w = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+      ep.partial[blockIdx.x] = t;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- CSR-vector variant
+// VW lanes per row (long rows of coarse Galerkin operators). Lane l sums entries l, l+VW, ...
+// in order, then the VW partials are combined by an xor butterfly (off = VW/2 .. 1). This is a
+// DIFFERENT summation order from scipy's, restated exactly by the oracle (oracle.c
+// vec_matvec); it is only selected explicitly (mlamg_csr_set_format) for operators that have no
+// scipy counterpart in the reference (coarse levels of the multilevel hierarchy).
+template <int VW, int OP, bool NORM>
+__global__ __launch_bounds__(kThreads) void k_csr_vec(const int32_t* __restrict__ indptr,
+                                                      const int32_t* __restrict__ indices,
+                                                      const double* __restrict__ vals,
+                                                      int64_t n_rows,
+                                                      const double* __restrict__ x, Epi ep) {
+  __shared__ double red[kThreads / 64];
+  if (ep.done && *ep.done) return;
+  const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t row = gid / VW;
+  const int l = threadIdx.x & (VW - 1);
+  double s = 0.0;
+  if (row < n_rows) {
+    const int a = indptr[row], b = indptr[row + 1];
+    for (int k = a + l; k < b; k += VW) s += vals[k] * x[indices[k]];
+  }
+#pragma unroll
+  for (int off = VW / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, VW);
+  double sq = 0.0;
+  if (l == 0 && row < n_rows) sq = epilogue<OP>((int)row, s, ep);
+  if constexpr (NORM) {
+    double w = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+      ep.partial[blockIdx.x] = t;
+    }
+  }
+}
+
+template <int OP, bool NORM, int VW>
+static int launch_vec_w(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  const int64_t threads = A->n_rows * VW;
+  const unsigned nb = (unsigned)std::max<int64_t>(1, (threads + kThreads - 1) / kThreads);
+  hipLaunchKernelGGL((k_csr_vec<VW, OP, NORM>), dim3(nb), dim3(kThreads), 0, s, A->indptr,
+                     A->indices, A->data, A->n_rows, x, ep);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+template <int OP, bool NORM>
+static int launch_vec(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  if (A->n_rows == 0) return MLAMG_OK;
+  switch (A->vec_width) {
+    case 4: return launch_vec_w<OP, NORM, 4>(A, x, ep, s);
+    case 8: return launch_vec_w<OP, NORM, 8>(A, x, ep, s);
+    case 16: return launch_vec_w<OP, NORM, 16>(A, x, ep, s);
+    case 32: return launch_vec_w<OP, NORM, 32>(A, x, ep, s);
+    default: return launch_vec_w<OP, NORM, 64>(A, x, ep, s);
+  }
+}
+
 // ---------------------------------------------------------------- launch helpers
 template <int OP, bool NORM>
 static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  if (A->vec_width) return launch_vec<OP, NORM>(A, x, ep, s);
+  if (A->sell_ptr) {
+    if (A->n_slices == 0) return MLAMG_OK;
+    const unsigned nb = (unsigned)((A->n_slices + kThreads / 64 - 1) / (kThreads / 64));
+    hipLaunchKernelGGL((k_sell<OP, NORM>), dim3(nb), dim3(kThreads), 0, s, A->sell_ptr,
+                       A->sell_col, A->sell_val, A->n_rows, A->n_slices, x, ep);
+    MLAMG_HIP(hipGetLastError());
+    return MLAMG_OK;
+  }
   if (A->n_blocks == 0) return MLAMG_OK;
   hipLaunchKernelGGL((k_csr_stream<OP, NORM>), dim3(A->n_blocks), dim3(kThreads), 0, s,
                      A->indptr, A->indices, A->data, A->blk, x, ep);
   MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+// ---------------------------------------------------------------- SELL-64 construction
+__global__ void k_slice_width(const int32_t* __restrict__ ip, int64_t n, int64_t n_slices,
+                              int64_t* __restrict__ w64) {
+  const int64_t sl = blockIdx.x * 4ll + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (sl >= n_slices) return;
+  const int64_t row = sl * 64 + lane;
+  int len = row < n ? ip[row + 1] - ip[row] : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) len = max(len, __shfl_xor(len, off, 64));
+  if (lane == 0) w64[sl] = (int64_t)len * 64;
+}
+
+__global__ void k_sell_fill(const int32_t* __restrict__ ip, const int32_t* __restrict__ ij,
+                            const double* __restrict__ ax, int64_t n, int64_t n_slices,
+                            const int64_t* __restrict__ sp, int32_t* __restrict__ cols,
+                            double* __restrict__ vals) {
+  const int64_t sl = blockIdx.x * 4ll + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (sl >= n_slices) return;
+  const int64_t base = sp[sl];
+  const int w = (int)((sp[sl + 1] - base) >> 6);
+  const int64_t row = sl * 64 + lane;
+  const int a = row < n ? ip[row] : 0;
+  const int len = row < n ? ip[row + 1] - a : 0;
+  for (int k = 0; k < w; ++k) {
+    const int64_t o = base + (int64_t)k * 64 + lane;
+    cols[o] = k < len ? ij[a + k] : -1;
+    vals[o] = k < len ? ax[a + k] : 0.0;
+  }
+}
+
+static void drop_sell(mlamg_csr* A) {
+  if (A->sell_ptr) (void)hipFree(A->sell_ptr);
+  if (A->sell_col) (void)hipFree(A->sell_col);
+  if (A->sell_val) (void)hipFree(A->sell_val);
+  A->sell_ptr = nullptr;
+  A->sell_col = nullptr;
+  A->sell_val = nullptr;
+  A->n_slices = 0;
+  A->sell_elems = 0;
+  A->n_part = A->n_blocks;
+}
+
+int build_sell(mlamg_csr* A, hipStream_t s) {
+  drop_sell(A);
+  const int64_t n = A->n_rows;
+  const int64_t ns = (n + 63) / 64;
+  int64_t* w64 = nullptr;
+  MLAMG_HIP(hipMalloc(&A->sell_ptr, sizeof(int64_t) * (ns + 1)));
+  MLAMG_HIP(hipMalloc(&w64, sizeof(int64_t) * (ns + 1)));
+  if (ns) hipLaunchKernelGGL(k_slice_width, dim3((ns + 3) / 4), dim3(256), 0, s, A->indptr, n, ns, w64);
+  int rc = exclusive_scan_i64(w64, A->sell_ptr, ns, s);
+  int64_t total = 0;
+  if (rc == MLAMG_OK) {
+    (void)hipMemcpyAsync(&total, A->sell_ptr + ns, sizeof(int64_t), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+  }
+  (void)hipFree(w64);
+  if (rc != MLAMG_OK) {
+    drop_sell(A);
+    return rc;
+  }
+  if (hipMalloc(&A->sell_col, sizeof(int32_t) * std::max<int64_t>(total, 1)) != hipSuccess ||
+      hipMalloc(&A->sell_val, sizeof(double) * std::max<int64_t>(total, 1)) != hipSuccess) {
+    drop_sell(A);
+    set_error("build_sell: out of device memory");
+    return MLAMG_ENOMEM;
+  }
+  if (ns)
+    hipLaunchKernelGGL(k_sell_fill, dim3((ns + 3) / 4), dim3(256), 0, s, A->indptr, A->indices,
+                       A->data, n, ns, A->sell_ptr, A->sell_col, A->sell_val);
+  MLAMG_HIP(hipGetLastError());
+  MLAMG_HIP(hipStreamSynchronize(s));
+  A->n_slices = ns;
+  A->sell_elems = total;
+  A->n_part = (int32_t)std::max<int64_t>(1, (ns + 3) / 4);
   return MLAMG_OK;
 }
 
@@ -170,7 +377,7 @@ int launch_spmv_plain(const mlamg_csr* A, const double* x, double* y, hipStream_
 // per-handle partial buffer for residual norms (slot 0 of the scratch cache is shared:
 // callers on one stream only)
 static double* partial_buf(const mlamg_csr* A) {
-  return static_cast<double*>(scratch(sizeof(double) * (A->n_blocks + 1), 0));
+  return static_cast<double*>(scratch(sizeof(double) * part_capacity(A), 0));
 }
 
 int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
@@ -187,7 +394,7 @@ int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* 
   ep.partial = partial ? partial : partial_buf(A);
   MLAMG_REQUIRE(ep.partial, "scratch allocation failed");
   MLAMG_TRY((launch<EPI_RESID, true>(A, x, ep, s)));
-  hipLaunchKernelGGL(k_finalize_norm, dim3(1), dim3(1024), 0, s, ep.partial, A->n_blocks, norm2,
+  hipLaunchKernelGGL(k_finalize_norm, dim3(1), dim3(1024), 0, s, ep.partial, A->n_part, norm2,
                      hist, counter, done, tol);
   MLAMG_HIP(hipGetLastError());
   return MLAMG_OK;
@@ -292,6 +499,52 @@ int mlamg_jacobi_explicit(const mlamg_csr* M, const double* dinv_w, const double
   }
   if (cur != x)
     MLAMG_HIP(hipMemcpyAsync(x, cur, sizeof(double) * M->n_rows, hipMemcpyDeviceToDevice, s));
+  return MLAMG_OK;
+}
+
+int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
+  MLAMG_REQUIRE(A, "NULL argument");
+  hipStream_t s = S(stream);
+  switch (fmt) {
+    case MLAMG_FMT_CSR_STREAM:
+      drop_sell(A);
+      A->vec_width = 0;
+      return MLAMG_OK;
+    case MLAMG_FMT_SELL:
+      A->vec_width = 0;
+      return build_sell(A, s);
+    case MLAMG_FMT_VECTOR: {
+      drop_sell(A);
+      int vw = vec_width;
+      if (vw == 0) {
+        vw = 4;
+        while (vw < 64 && 2.0 * vw <= A->avg_row_len) vw *= 2;
+      }
+      MLAMG_REQUIRE(vw == 4 || vw == 8 || vw == 16 || vw == 32 || vw == 64,
+                    "vec_width must be 0 (auto), 4, 8, 16, 32 or 64");
+      A->vec_width = vw;
+      A->n_part = (int32_t)std::max<int64_t>(1, (A->n_rows * vw + kThreads - 1) / kThreads);
+      return MLAMG_OK;
+    }
+    case MLAMG_FMT_AUTO_EXACT: {
+      A->vec_width = 0;
+      MLAMG_TRY(build_sell(A, s));
+      // keep SELL only if padding costs <= 15% more stored entries than CSR
+      if (A->nnz == 0 || (double)A->sell_elems > 1.15 * (double)A->nnz) drop_sell(A);
+      return MLAMG_OK;
+    }
+    default:
+      MLAMG_REQUIRE(false, "unknown format");
+  }
+  return MLAMG_OK;
+}
+
+int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored) {
+  MLAMG_REQUIRE(A, "NULL argument");
+  const int f = A->vec_width ? MLAMG_FMT_VECTOR : (A->sell_ptr ? MLAMG_FMT_SELL : MLAMG_FMT_CSR_STREAM);
+  if (fmt) *fmt = f;
+  if (vec_width) *vec_width = A->vec_width;
+  if (stored) *stored = A->sell_ptr ? A->sell_elems : A->nnz;
   return MLAMG_OK;
 }
 

@@ -60,6 +60,8 @@ SIGNATURES = {
     "mlamg_csr_shape": (c_int, [c_vp, P_i64, P_i64, P_i64]),
     "mlamg_csr_device_arrays": (c_int, [c_vp, c_vpp, c_vpp, c_vpp]),
     "mlamg_csr_download": (c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_csr_set_format": (c_int, [c_vp, c_int, c_int, c_vp]),
+    "mlamg_csr_get_format": (c_int, [c_vp, P_int, P_int, P_i64]),
     "mlamg_spmv": (c_int, [c_vp, c_vp, c_vp, c_dbl, c_dbl, c_vp]),
     "mlamg_residual": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mlamg_jacobi": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),

@@ -77,7 +77,7 @@ class Halo:
 class DistributedHierarchy:
     """Fine level of a (replicated) Hierarchy split over `world` GPUs."""
 
-    def __init__(self, H, A_host, comm):
+    def __init__(self, H, A_host, comm, fine_format="auto_exact"):
         """H: mlamg.hierarchy.Hierarchy built identically on every rank (sorted seeds);
         A_host: the fine matrix as scipy CSR (same arrays as H.levels[0].A)."""
         if not H.levels:
@@ -92,9 +92,10 @@ class DistributedHierarchy:
         self.part = p = partition.build(A_host, P0, L0.seeds, world, rank)
         self.lo, self.hi = p["lo"], p["hi"]
         self.n_own = self.hi - self.lo
-        self.A_loc = DeviceCSR.from_scipy(p["A_loc"], check=False)
-        self.P_loc = DeviceCSR.from_scipy(p["P_loc"], check=False)
-        self.R_own = DeviceCSR.from_scipy(p["R_own"], check=False)
+        # level-0 operators keep scipy's summation order (same formats as H.apply_formats)
+        self.A_loc = DeviceCSR.from_scipy(p["A_loc"], check=False).set_format(fine_format)
+        self.P_loc = DeviceCSR.from_scipy(p["P_loc"], check=False).set_format(fine_format)
+        self.R_own = DeviceCSR.from_scipy(p["R_own"], check=False).set_format(fine_format)
         self.dinv = L0.dinv[self.lo:self.hi].clone()
         self.hx = Halo(comm, p["halo_x"])
         self.hr = Halo(comm, p["halo_r"])

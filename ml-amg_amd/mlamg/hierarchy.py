@@ -81,11 +81,34 @@ class Hierarchy:
         H._finalize(nu_pre, nu_post)
         return H
 
+    def apply_formats(self, fine_format="auto_exact", coarse_format="vector", vec_min_row=16):
+        """Choose the SpMV kernel of every operator.
+
+        Level 0 (A0, P0, R0 — operators with a scipy counterpart in the reference cycle) always
+        keeps scipy's summation order ('auto_exact': SELL-64 when its padding is small, else
+        CSR-stream). Coarser levels (the multilevel extension, no reference counterpart) use the
+        CSR-vector kernel for A_l and R_l when coarse_format='vector' and their mean row length
+        is >= vec_min_row; its fixed order is restated by the oracle (oracle.c vec_matvec)."""
+        for i, L in enumerate(self.levels):
+            for M in (L.A, L.P, L.R):
+                M.set_format(fine_format if fine_format != "vector" else "auto_exact")
+            if i > 0 and coarse_format == "vector":
+                for M in (L.A, L.R):
+                    if M.nnz >= vec_min_row * M.shape[0]:
+                        M.set_format("vector")
+            elif i > 0:
+                for M in (L.A, L.R):
+                    M.set_format("auto_exact")
+
+    def formats(self):
+        return [{"A": L.A.get_format(), "P": L.P.get_format(), "R": L.R.get_format()}
+                for L in self.levels]
+
     @classmethod
     def build(cls, A, *, alpha=0.1, strength_mode="invabs", aggregation="bellman_ford",
               max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, seed=0, sort_seeds=True,
               lanczos_tol=1e-15, lanczos_iter=20000, lloyd_maxiter=10, nu_pre=1, nu_post=1,
-              verbose=False):
+              fine_format="auto_exact", coarse_format="vector", verbose=False):
         H = cls()
         H.jacobi_weight = jacobi_weight
         t_all = time.perf_counter()
@@ -147,6 +170,7 @@ class Hierarchy:
             A_dev = A_next
         H.Ac = A_dev
         t5 = time.perf_counter()
+        H.apply_formats(fine_format, coarse_format)
         H._finalize(nu_pre, nu_post)
         torch.cuda.synchronize()
         tm["dense"] = time.perf_counter() - t5

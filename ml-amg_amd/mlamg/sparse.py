@@ -134,6 +134,21 @@ class DeviceCSR:
             return self.matvec(other)
         return NotImplemented
 
+    FORMATS = {"csr_stream": 0, "sell": 1, "vector": 2, "auto_exact": 3}
+
+    def set_format(self, fmt, vec_width=0):
+        """SpMV kernel/storage: 'csr_stream' | 'sell' | 'auto_exact' (scipy summation order)
+        or 'vector' (lane-strided order, see include/mlamg.h)."""
+        call("mlamg_csr_set_format", self.handle, self.FORMATS[fmt], int(vec_width), stream_ptr())
+        return self
+
+    def get_format(self):
+        f, vw, st = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+        call("mlamg_csr_get_format", self.handle, ctypes.byref(f), ctypes.byref(vw),
+             ctypes.byref(st))
+        name = {v: k for k, v in self.FORMATS.items()}[f.value]
+        return name, int(vw.value), int(st.value)
+
     def diag_inv(self, omega=1.0):
         d = torch.empty(self.shape[0], dtype=torch.float64, device=_device())
         call("mlamg_diag_inv", self.handle, omega, ptr(d), stream_ptr())

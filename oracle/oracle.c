@@ -31,6 +31,25 @@ void ref_csr_matvec(int64_t n, const int32_t* ip, const int32_t* ij, const doubl
   }
 }
 
+/* The device CSR-vector order (mlamg_csr_set_format VECTOR): lane l of vw sums entries
+ * l, l+vw, ... of the row in order, then partials combine by an xor butterfly off=vw/2..1. */
+void vec_matvec(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
+                const double* x, double* y, int vw) {
+  double part[64], nxt[64];
+  for (int64_t i = 0; i < n; ++i) {
+    for (int l = 0; l < vw; ++l) {
+      double s = 0.0;
+      for (int32_t k = ip[i] + l; k < ip[i + 1]; k += vw) s += ax[k] * x[ij[k]];
+      part[l] = s;
+    }
+    for (int off = vw / 2; off > 0; off >>= 1) {
+      for (int l = 0; l < vw; ++l) nxt[l] = part[l] + part[l ^ off];
+      for (int l = 0; l < vw; ++l) part[l] = nxt[l];
+    }
+    y[i] = part[0];
+  }
+}
+
 void ref_gauss_seidel(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
                       double* x, const double* b, int iterations) {
   for (int it = 0; it < iterations; ++it) {

@@ -34,6 +34,7 @@ def lib():
         L.ref_bellman_ford_torch.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
         L.ref_bellman_ford_torch.restype = ctypes.c_int
         L.canon_bellman_ford.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
+        L.vec_matvec.argtypes = [i64, vp, vp, vp, vp, vp, ctypes.c_int]
         L.lloyd_cluster.argtypes = [i64, vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int, vp, vp,
                                     ctypes.c_int]
         L.lloyd_cluster.restype = ctypes.c_int
@@ -60,6 +61,20 @@ def csr_matvec(A, x):
     y = np.empty(A.shape[0])
     lib().ref_csr_matvec(A.shape[0], _p(ip), _p(ij), _p(ax), _p(x), _p(y))
     return y
+
+
+def vec_matvec(A, x, vw):
+    """The device CSR-vector summation order (oracle.c vec_matvec)."""
+    ip, ij, ax = _csr_arrays(A)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty(A.shape[0])
+    lib().vec_matvec(A.shape[0], _p(ip), _p(ij), _p(ax), _p(x), _p(y), int(vw))
+    return y
+
+
+def mv(M, x, vw=0):
+    """M@x in scipy's order (vw == 0) or the device vector order (vw > 0)."""
+    return M @ x if not vw else vec_matvec(M, x, vw)
 
 
 def gauss_seidel(A, x, b, iterations=1):
@@ -319,12 +334,26 @@ def make_cycle(levels, lu, nu_pre=1, nu_post=1):
             return lu(b)
         L = levels[l]
         A, P, Dw = L["A"], L["P"], L["Dw"]
+        avw, pvw, rvw = L.get("A_vw", 0), L.get("P_vw", 0), L.get("R_vw", 0)
+        if not (avw or pvw or rvw):
+            if x is None:
+                x = np.zeros(A.shape[0])
+            x = jacobi_mlamg(A, Dw, b, x, nu_pre)
+            xc = cycle(l + 1, P.T @ (b - A @ x), None)
+            x += P @ xc
+            x = jacobi_mlamg(A, Dw, b, x, nu_post)
+            return x
+        # device vector-order operators (coarse levels): same cycle, explicit R = P^T
+        d = Dw.diagonal()
+        R = L["R"]
         if x is None:
             x = np.zeros(A.shape[0])
-        x = jacobi_mlamg(A, Dw, b, x, nu_pre)
-        xc = cycle(l + 1, P.T @ (b - A @ x), None)
-        x += P @ xc
-        x = jacobi_mlamg(A, Dw, b, x, nu_post)
+        for _ in range(nu_pre):
+            x = x + d * (b - mv(A, x, avw))
+        xc = cycle(l + 1, mv(R, b - mv(A, x, avw), rvw), None)
+        x = x + mv(P, xc, pvw)
+        for _ in range(nu_post):
+            x = x + d * (b - mv(A, x, avw))
         return x
 
     return cycle
