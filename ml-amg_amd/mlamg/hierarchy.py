@@ -108,7 +108,7 @@ class Hierarchy:
     def build(cls, A, *, alpha=0.1, strength_mode="invabs", aggregation="bellman_ford",
               max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, seed=0, sort_seeds=True,
               lanczos_tol=1e-15, lanczos_iter=20000, lloyd_maxiter=10, nu_pre=1, nu_post=1,
-              fine_format="auto_exact", coarse_format="vector", verbose=False):
+              fine_format="auto_exact", coarse_format="vector", verbose=False, finalize=True):
         H = cls()
         H.jacobi_weight = jacobi_weight
         t_all = time.perf_counter()
@@ -169,6 +169,8 @@ class Hierarchy:
                       flush=True)
             A_dev = A_next
         H.Ac = A_dev
+        if not finalize:  # setup only (e.g. to take P for a two-level cycle)
+            return H
         t5 = time.perf_counter()
         H.apply_formats(fine_format, coarse_format)
         H._finalize(nu_pre, nu_post)

@@ -1,0 +1,168 @@
+"""PETSc python-PC mirror of ns/preconditioner/MLAMG.py (and the multilevel PyAMG PC), plus the
+package-level precondition()/solve() entry points.
+
+Reference surface (ns/preconditioner/MLAMG.py):
+  class MLAMG(PCBase): initialize(pc) :30, update(pc) :126, apply(pc, X, Y) :199,
+  applyTranspose :214, view :218; options '<prefix>mlamg_amg_rtol' (1e-8, :64),
+  'mlamg_jacobi_weight' (2/3, :66); apply runs amg_2_v (:148-197) from x0 = np.random.normal
+  (:209) with the weighted-Jacobi smoother until ||b - A x||_2 <= amg_rtol, at most 500 cycles.
+
+What differs: the reference builds P with a learned GNN (InterpolationNetwork + greedy C/F
+splitting, :105-120), which needs torch_geometric and trained weights that are not shipped. Here P
+is the smoothed-aggregation prolongator of seeded Bellman-Ford aggregates, built on the GPU
+(option 'mlamg_alpha', default 0.1), or any P handed in via `MLAMG.set_prolongator`. The cycle,
+stopping rule and I/O contract are the reference's. The PC works with petsc4py when present and
+with any duck-typed object offering getOperators()/getOptionsPrefix() otherwise (no PETSc here).
+"""
+from __future__ import annotations
+
+import traceback
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from .hierarchy import Hierarchy
+from .sparse import to_device_vec
+
+
+class _Options:
+    """PETSc.Options stand-in: a dict; petsc4py's Options is used when importable."""
+
+    store = {}
+
+    def __init__(self):
+        try:  # pragma: no cover - petsc4py is not installed in this image
+            from petsc4py import PETSc
+            self._petsc = PETSc.Options()
+        except Exception:
+            self._petsc = None
+
+    def getScalar(self, key, default):
+        if self._petsc is not None:  # pragma: no cover
+            return self._petsc.getScalar(key, default)
+        return float(self.store.get(key, default))
+
+    def getInt(self, key, default):
+        if self._petsc is not None:  # pragma: no cover
+            return self._petsc.getInt(key, default)
+        return int(self.store.get(key, default))
+
+
+def _csr_from_pc(pc):
+    _, P = pc.getOperators()
+    if hasattr(P, "getValuesCSR"):
+        row, col, val = P.getValuesCSR()
+        return sp.csr_matrix((val, col, row))
+    return sp.csr_matrix(P)
+
+
+class MLAMG:
+    """Two-level weighted-Jacobi AMG preconditioner (MLAMG.py:27-222) on the MI355X."""
+
+    _prefix = "mlamg_"
+
+    def __init__(self):
+        self._P_user = None
+
+    # ------------------------------------------------------------------ PCBase protocol
+    def initialize(self, pc):
+        try:
+            self._initialize(pc)
+        except Exception as e:
+            traceback.print_exc()
+            raise e
+
+    def _initialize(self, pc):
+        prefix = pc.getOptionsPrefix() if hasattr(pc, "getOptionsPrefix") else ""
+        prefix = (prefix or "") + self._prefix
+        opts = _Options()
+        self.amg_rtol = opts.getScalar(f"{prefix}amg_rtol", 1e-8)
+        self.jacobi_weight = opts.getScalar(f"{prefix}jacobi_weight", 2.0 / 3.0)
+        self.alpha = opts.getScalar(f"{prefix}alpha", 0.1)
+        self.max_iter = opts.getInt(f"{prefix}max_iter", 500)
+        self.update(pc)
+
+    def set_prolongator(self, P):
+        """Use a given interpolation operator (e.g. a learned P) instead of SA-on-BF."""
+        self._P_user = P
+
+    def update(self, pc):
+        try:
+            self._createAmgSolver(pc)
+        except Exception as e:
+            traceback.print_exc()
+            raise e
+
+    def _createAmgSolver(self, pc):
+        A = _csr_from_pc(pc)
+        self.A = A
+        if self._P_user is not None:
+            P = self._P_user
+        else:
+            H = Hierarchy.build(A, alpha=self.alpha, max_levels=2, max_coarse=0,
+                                jacobi_weight=self.jacobi_weight, finalize=False)
+            P = H.levels[0].P
+        self.H = Hierarchy.two_level(A, P, omega=self.jacobi_weight)
+
+    def apply(self, pc, X, Y):
+        try:
+            self._apply(pc, X, Y)
+        except Exception as e:
+            traceback.print_exc()
+            raise e
+
+    def _apply(self, pc, X, Y):
+        b = X.array_r if hasattr(X, "array_r") else np.asarray(X)
+        x = np.random.normal(size=self.A.shape[1])  # MLAMG.py:209 (global RNG, unseeded)
+        bd = to_device_vec(b)
+        xd = to_device_vec(x).clone()
+        self.H.cycle(bd, xd, self.max_iter, tol=self.amg_rtol)
+        out = xd.cpu().numpy()
+        if hasattr(Y, "setArray"):
+            Y.setArray(out)
+        else:
+            Y[...] = out
+
+    def applyTranspose(self, pc, X, Y):
+        print('PyAMG applyTranspose!')  # reference behaviour: a no-op (MLAMG.py:214-216)
+
+    def view(self, pc, viewer=None):
+        if viewer is not None:
+            viewer.printfASCII('MLAMG (MI355X) Solver:\n')
+            viewer.printfASCII(f' levels: {self.H.n_levels}\n')
+            viewer.printfASCII(f' amg rtol: {self.amg_rtol}\n')
+
+
+class MultilevelPC(MLAMG):
+    """Multilevel variant (the role of ns/preconditioner/PyAMG.py: pyamg SA solver, :94,119),
+    SA prolongators on Bellman-Ford aggregates down to a dense coarse level; stationary V-cycles
+    (no GMRES acceleration)."""
+
+    _prefix = "pyamg_"
+
+    def _createAmgSolver(self, pc):
+        A = _csr_from_pc(pc)
+        self.A = A
+        opts = _Options()
+        prefix = ((pc.getOptionsPrefix() if hasattr(pc, "getOptionsPrefix") else "") or "")
+        levels = opts.getInt(f"{prefix}{self._prefix}amg_max_levels", 10)
+        self.H = Hierarchy.build(A, alpha=self.alpha, max_levels=levels,
+                                 jacobi_weight=self.jacobi_weight)
+
+
+# ---------------------------------------------------------------------- package-level API
+def setup(A, **kw):
+    """Build the device hierarchy once (Hierarchy.build keywords)."""
+    return Hierarchy.build(A, **kw)
+
+
+def precondition(H, b):
+    """Action of one V-cycle from x = 0 on b (numpy in -> numpy out, tensor in -> tensor out)."""
+    return H.precondition(b)
+
+
+def solve(A_or_H, b, x0=None, tol=1e-8, maxiter=500, return_history=False, **kw):
+    """V-cycle iteration until ||b - A x||_2 <= tol (absolute, MLAMG.py:194)."""
+    H = A_or_H if isinstance(A_or_H, Hierarchy) else Hierarchy.build(A_or_H, **kw)
+    return H.solve(b, x0=x0, tol=tol, maxiter=maxiter, return_history=return_history)
