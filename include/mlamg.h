@@ -68,7 +68,9 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
 
 /* SpMV storage/kernel of a handle (the CSR arrays always stay; formats add a device copy):
  *   CSR_STREAM  LDS-staged row blocks, lane-per-row sums in stored order (scipy's bits)
- *   SELL        SELL-64 slices, lane-per-row sums in stored order (scipy's bits)
+ *   SELL        SELL-64 slices, lane-per-row sums in stored order (scipy's bits); vec_width > 1
+ *               is read as sigma: rows sorted by length inside windows of sigma rows
+ *               (SELL-C-sigma; get_format reports sigma in vec_width)
  *   VECTOR      vec_width lanes per row (0 = auto from the mean row length), lane-strided
  *               partial sums + xor butterfly: a different, fixed order (oracle vec_matvec),
  *               for long-row coarse operators that have no scipy counterpart

@@ -77,6 +77,8 @@ struct mlamg_csr {
   int64_t* sell_ptr = nullptr;  // element offset of each slice (n_slices+1)
   int32_t* sell_col = nullptr;
   double* sell_val = nullptr;
+  int32_t* sell_perm = nullptr;  // SELL-C-sigma row order (nullptr: natural order)
+  int32_t sell_sigma = 0;
   int64_t sell_elems = 0;
   // CSR-vector format (lane-strided partial sums + butterfly, NOT scipy's order): 0 = off,
   // else the number of lanes per row (4..64)

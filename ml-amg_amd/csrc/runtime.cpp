@@ -79,6 +79,7 @@ void csr_free(mlamg_csr* A) {
   if (A->sell_ptr) (void)hipFree(A->sell_ptr);
   if (A->sell_col) (void)hipFree(A->sell_col);
   if (A->sell_val) (void)hipFree(A->sell_val);
+  if (A->sell_perm) (void)hipFree(A->sell_perm);
   delete A;
 }
 

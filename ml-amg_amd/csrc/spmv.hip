@@ -158,6 +158,7 @@ template <int OP, bool NORM>
 __global__ __launch_bounds__(kThreads) void k_sell(const int64_t* __restrict__ sp,
                                                    const int32_t* __restrict__ cols,
                                                    const double* __restrict__ vals,
+                                                   const int32_t* __restrict__ perm,
                                                    int64_t n_rows, int64_t n_slices,
                                                    const double* __restrict__ x, Epi ep) {
   __shared__ double red[kThreads / 64];
@@ -192,8 +193,8 @@ __global__ __launch_bounds__(kThreads) void k_sell(const int64_t* __restrict__ s
       const double vv = __builtin_nontemporal_load(v + (int64_t)k * 64);
       if (cc >= 0) s += vv * x[cc];
     }
-    const int64_t row = slice * 64 + lane;
-    if (row < n_rows) sq = epilogue<OP>((int)row, s, ep);
+    const int64_t srow = slice * 64 + lane;
+    if (srow < n_rows) sq = epilogue<OP>(perm ? perm[srow] : (int)srow, s, ep);
   }
   if constexpr (NORM) {
     double w = wave_sum(sq);
@@ -275,7 +276,7 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_
     if (A->n_slices == 0) return MLAMG_OK;
     const unsigned nb = (unsigned)((A->n_slices + kThreads / 64 - 1) / (kThreads / 64));
     hipLaunchKernelGGL((k_sell<OP, NORM>), dim3(nb), dim3(kThreads), 0, s, A->sell_ptr,
-                       A->sell_col, A->sell_val, A->n_rows, A->n_slices, x, ep);
+                       A->sell_col, A->sell_val, A->sell_perm, A->n_rows, A->n_slices, x, ep);
     MLAMG_HIP(hipGetLastError());
     return MLAMG_OK;
   }
@@ -287,28 +288,17 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_
 }
 
 // ---------------------------------------------------------------- SELL-64 construction
-__global__ void k_slice_width(const int32_t* __restrict__ ip, int64_t n, int64_t n_slices,
-                              int64_t* __restrict__ w64) {
-  const int64_t sl = blockIdx.x * 4ll + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (sl >= n_slices) return;
-  const int64_t row = sl * 64 + lane;
-  int len = row < n ? ip[row + 1] - ip[row] : 0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) len = max(len, __shfl_xor(len, off, 64));
-  if (lane == 0) w64[sl] = (int64_t)len * 64;
-}
-
 __global__ void k_sell_fill(const int32_t* __restrict__ ip, const int32_t* __restrict__ ij,
                             const double* __restrict__ ax, int64_t n, int64_t n_slices,
-                            const int64_t* __restrict__ sp, int32_t* __restrict__ cols,
-                            double* __restrict__ vals) {
+                            const int64_t* __restrict__ sp, const int32_t* __restrict__ perm,
+                            int32_t* __restrict__ cols, double* __restrict__ vals) {
   const int64_t sl = blockIdx.x * 4ll + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (sl >= n_slices) return;
   const int64_t base = sp[sl];
   const int w = (int)((sp[sl + 1] - base) >> 6);
-  const int64_t row = sl * 64 + lane;
+  const int64_t srow = sl * 64 + lane;
+  const int64_t row = (perm && srow < n) ? perm[srow] : srow;
   const int a = row < n ? ip[row] : 0;
   const int len = row < n ? ip[row + 1] - a : 0;
   for (int k = 0; k < w; ++k) {
@@ -322,46 +312,68 @@ static void drop_sell(mlamg_csr* A) {
   if (A->sell_ptr) (void)hipFree(A->sell_ptr);
   if (A->sell_col) (void)hipFree(A->sell_col);
   if (A->sell_val) (void)hipFree(A->sell_val);
+  if (A->sell_perm) (void)hipFree(A->sell_perm);
   A->sell_ptr = nullptr;
   A->sell_col = nullptr;
   A->sell_val = nullptr;
+  A->sell_perm = nullptr;
+  A->sell_sigma = 0;
   A->n_slices = 0;
   A->sell_elems = 0;
   A->n_part = A->n_blocks;
 }
 
-int build_sell(mlamg_csr* A, hipStream_t s) {
+// Layout on the host from the row lengths: with sigma > 1 the rows of each window of sigma rows
+// are ordered by decreasing length (stable), so a slice's rows have similar lengths and little
+// padding (SELL-C-sigma); perm[k] = original row of sorted position k. Each row keeps its own
+// entry order, so sums are unchanged; only which lane computes which row moves.
+int build_sell(mlamg_csr* A, hipStream_t s, int sigma) {
   drop_sell(A);
   const int64_t n = A->n_rows;
   const int64_t ns = (n + 63) / 64;
-  int64_t* w64 = nullptr;
-  MLAMG_HIP(hipMalloc(&A->sell_ptr, sizeof(int64_t) * (ns + 1)));
-  MLAMG_HIP(hipMalloc(&w64, sizeof(int64_t) * (ns + 1)));
-  if (ns) hipLaunchKernelGGL(k_slice_width, dim3((ns + 3) / 4), dim3(256), 0, s, A->indptr, n, ns, w64);
-  int rc = exclusive_scan_i64(w64, A->sell_ptr, ns, s);
-  int64_t total = 0;
-  if (rc == MLAMG_OK) {
-    (void)hipMemcpyAsync(&total, A->sell_ptr + ns, sizeof(int64_t), hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
+  std::vector<int32_t> ip(n + 1);
+  MLAMG_HIP(hipMemcpyAsync(ip.data(), A->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  std::vector<int32_t> perm;
+  if (sigma > 1) {
+    perm.resize(n);
+    for (int64_t i = 0; i < n; ++i) perm[i] = (int32_t)i;
+    for (int64_t w0 = 0; w0 < n; w0 += sigma) {
+      const int64_t w1 = std::min<int64_t>(n, w0 + sigma);
+      std::stable_sort(perm.begin() + w0, perm.begin() + w1, [&](int32_t a, int32_t b) {
+        return (ip[a + 1] - ip[a]) > (ip[b + 1] - ip[b]);
+      });
+    }
   }
-  (void)hipFree(w64);
-  if (rc != MLAMG_OK) {
-    drop_sell(A);
-    return rc;
+  std::vector<int64_t> sp(ns + 1, 0);
+  for (int64_t sl = 0; sl < ns; ++sl) {
+    int32_t w = 0;
+    for (int64_t k = sl * 64; k < std::min<int64_t>(n, sl * 64 + 64); ++k) {
+      const int32_t r = perm.empty() ? (int32_t)k : perm[k];
+      w = std::max(w, ip[r + 1] - ip[r]);
+    }
+    sp[sl + 1] = sp[sl] + 64ll * w;
   }
-  if (hipMalloc(&A->sell_col, sizeof(int32_t) * std::max<int64_t>(total, 1)) != hipSuccess ||
-      hipMalloc(&A->sell_val, sizeof(double) * std::max<int64_t>(total, 1)) != hipSuccess) {
+  const int64_t total = sp[ns];
+  if (hipMalloc(&A->sell_ptr, sizeof(int64_t) * (ns + 1)) != hipSuccess ||
+      hipMalloc(&A->sell_col, sizeof(int32_t) * std::max<int64_t>(total, 1)) != hipSuccess ||
+      hipMalloc(&A->sell_val, sizeof(double) * std::max<int64_t>(total, 1)) != hipSuccess ||
+      (!perm.empty() && hipMalloc(&A->sell_perm, sizeof(int32_t) * n) != hipSuccess)) {
     drop_sell(A);
     set_error("build_sell: out of device memory");
     return MLAMG_ENOMEM;
   }
+  MLAMG_HIP(hipMemcpyAsync(A->sell_ptr, sp.data(), sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice, s));
+  if (!perm.empty())
+    MLAMG_HIP(hipMemcpyAsync(A->sell_perm, perm.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
   if (ns)
     hipLaunchKernelGGL(k_sell_fill, dim3((ns + 3) / 4), dim3(256), 0, s, A->indptr, A->indices,
-                       A->data, n, ns, A->sell_ptr, A->sell_col, A->sell_val);
+                       A->data, n, ns, A->sell_ptr, A->sell_perm, A->sell_col, A->sell_val);
   MLAMG_HIP(hipGetLastError());
   MLAMG_HIP(hipStreamSynchronize(s));
   A->n_slices = ns;
   A->sell_elems = total;
+  A->sell_sigma = std::max(sigma, 1);
   A->n_part = (int32_t)std::max<int64_t>(1, (ns + 3) / 4);
   return MLAMG_OK;
 }
@@ -512,7 +524,7 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       return MLAMG_OK;
     case MLAMG_FMT_SELL:
       A->vec_width = 0;
-      return build_sell(A, s);
+      return build_sell(A, s, vec_width > 1 ? vec_width : 1);  // vec_width doubles as sigma
     case MLAMG_FMT_VECTOR: {
       drop_sell(A);
       int vw = vec_width;
@@ -527,10 +539,15 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       return MLAMG_OK;
     }
     case MLAMG_FMT_AUTO_EXACT: {
+      // SELL-64 in natural row order if its padding costs <= 15% extra entries, else
+      // SELL-64-sigma (rows sorted by length inside windows of 512) if that does, else
+      // CSR-stream
       A->vec_width = 0;
-      MLAMG_TRY(build_sell(A, s));
-      // keep SELL only if padding costs <= 15% more stored entries than CSR
-      if (A->nnz == 0 || (double)A->sell_elems > 1.15 * (double)A->nnz) drop_sell(A);
+      MLAMG_TRY(build_sell(A, s, 1));
+      if (A->nnz > 0 && (double)A->sell_elems <= 1.15 * (double)A->nnz) return MLAMG_OK;
+      MLAMG_TRY(build_sell(A, s, 512));
+      if (A->nnz > 0 && (double)A->sell_elems <= 1.15 * (double)A->nnz) return MLAMG_OK;
+      drop_sell(A);
       return MLAMG_OK;
     }
     default:
@@ -543,7 +560,7 @@ int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* 
   MLAMG_REQUIRE(A, "NULL argument");
   const int f = A->vec_width ? MLAMG_FMT_VECTOR : (A->sell_ptr ? MLAMG_FMT_SELL : MLAMG_FMT_CSR_STREAM);
   if (fmt) *fmt = f;
-  if (vec_width) *vec_width = A->vec_width;
+  if (vec_width) *vec_width = A->vec_width ? A->vec_width : A->sell_sigma;
   if (stored) *stored = A->sell_ptr ? A->sell_elems : A->nnz;
   return MLAMG_OK;
 }

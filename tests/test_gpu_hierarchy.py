@@ -73,8 +73,19 @@ def test_sell_ragged_rows(ml, torch_cuda):
     indices = np.concatenate([np.sort(rs.choice(n, l, replace=False)) for l in lens])
     A = sp.csr_matrix((rs.randn(indptr[-1]), indices, indptr), shape=(n, n))
     x = rs.randn(n)
-    Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("sell")
-    assert np.array_equal(Ad.matvec(dev(torch, x)).cpu().numpy(), A @ x)
+    for sigma in (1, 128, 512):
+        Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("sell", sigma)
+        assert Ad.get_format()[:2] == ("sell", sigma)
+        assert np.array_equal(Ad.matvec(dev(torch, x)).cpu().numpy(), A @ x)
+        from mlamg._lib import call, ptr, stream_ptr
+        b = dev(torch, rs.randn(n))
+        r = torch.empty_like(b)
+        nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
+        call("mlamg_residual", Ad.handle, ptr(b), ptr(dev(torch, x)), ptr(r), ptr(nrm),
+             stream_ptr())
+        ref = b.cpu().numpy() - A @ x
+        assert np.array_equal(r.cpu().numpy(), ref)
+        assert abs(nrm.item() - np.linalg.norm(ref)) <= 1e-13 * np.linalg.norm(ref)
 
 
 def _oracle_levels_from_device(H):
