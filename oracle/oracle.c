@@ -36,6 +36,10 @@ void ref_csr_matvec(int64_t n, const int32_t* ip, const int32_t* ij, const doubl
 void vec_matvec(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
                 const double* x, double* y, int vw) {
   double part[64], nxt[64];
+  if (vw < 1 || vw > 64 || (vw & (vw - 1))) {
+    for (int64_t i = 0; i < n; ++i) y[i] = NAN;
+    return;
+  }
   for (int64_t i = 0; i < n; ++i) {
     for (int l = 0; l < vw; ++l) {
       double s = 0.0;

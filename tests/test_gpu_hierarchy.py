@@ -92,10 +92,11 @@ def _oracle_levels_from_device(H):
     levels = []
     for L in H.levels:
         f = {k: v for k, v in zip("APR", (L.A.get_format(), L.P.get_format(), L.R.get_format()))}
+        vw = {k: (v[1] if v[0] == "vector" else 0) for k, v in f.items()}
         levels.append({
             "A": L.A.to_scipy(), "P": L.P.to_scipy(), "R": L.R.to_scipy(),
             "Dw": sp.diags(L.dinv.cpu().numpy()),
-            "A_vw": f["A"][1], "P_vw": f["P"][1], "R_vw": f["R"][1],
+            "A_vw": vw["A"], "P_vw": vw["P"], "R_vw": vw["R"],
         })
     return levels
 
