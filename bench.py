@@ -206,6 +206,7 @@ def main():
         "fine_spmv_formats": ab,
         "operator_formats": [{k: v[0] + (f"/{v[1]}" if v[1] else "") for k, v in f.items()}
                              for f in H.formats()],
+        "format_autotune_us": H.tuning,
         "setup_s": {k: round(v, 3) for k, v in H.timings.items()},
         "conv_factor_10cycles": round(conv, 5),
     }

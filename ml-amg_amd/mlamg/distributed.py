@@ -92,10 +92,14 @@ class DistributedHierarchy:
         self.part = p = partition.build(A_host, P0, L0.seeds, world, rank)
         self.lo, self.hi = p["lo"], p["hi"]
         self.n_own = self.hi - self.lo
-        # level-0 operators keep scipy's summation order (same formats as H.apply_formats)
-        self.A_loc = DeviceCSR.from_scipy(p["A_loc"], check=False).set_format(fine_format)
-        self.P_loc = DeviceCSR.from_scipy(p["P_loc"], check=False).set_format(fine_format)
-        self.R_own = DeviceCSR.from_scipy(p["R_own"], check=False).set_format(fine_format)
+        # level-0 operators: the kernel H chose for the global operator (scipy order either way)
+        def like(M_glob, M_loc):
+            fmt, arg, _ = M_glob.get_format()
+            return M_loc.set_format(fmt, arg)
+
+        self.A_loc = like(L0.A, DeviceCSR.from_scipy(p["A_loc"], check=False))
+        self.P_loc = like(L0.P, DeviceCSR.from_scipy(p["P_loc"], check=False))
+        self.R_own = like(L0.R, DeviceCSR.from_scipy(p["R_own"], check=False))
         self.dinv = L0.dinv[self.lo:self.hi].clone()
         self.hx = Halo(comm, p["halo_x"])
         self.hr = Halo(comm, p["halo_r"])

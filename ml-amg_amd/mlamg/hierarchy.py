@@ -81,24 +81,55 @@ class Hierarchy:
         H._finalize(nu_pre, nu_post)
         return H
 
-    def apply_formats(self, fine_format="auto_exact", coarse_format="vector", vec_min_row=16):
+    EXACT_CANDIDATES = (("csr_stream", 0), ("sell", 1), ("sell", 512))
+    VECTOR_CANDIDATES = (("vector", 8), ("vector", 16), ("vector", 32), ("vector", 64))
+
+    @staticmethod
+    def _time_format(M, fmt, arg, x, y, reps=5):
+        M.set_format(fmt, arg)
+        M.matvec(x, out=y)
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            M.matvec(x, out=y)
+        e1.record(s)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3  # us
+
+    def apply_formats(self, fine_format="autotune", coarse_format="vector", vec_min_row=16):
         """Choose the SpMV kernel of every operator.
 
-        Level 0 (A0, P0, R0 — operators with a scipy counterpart in the reference cycle) always
-        keeps scipy's summation order ('auto_exact': SELL-64 when its padding is small, else
-        CSR-stream). Coarser levels (the multilevel extension, no reference counterpart) use the
-        CSR-vector kernel for A_l and R_l when coarse_format='vector' and their mean row length
-        is >= vec_min_row; its fixed order is restated by the oracle (oracle.c vec_matvec)."""
+        Level-0 operators (A0, P0, R0: the ones with a scipy counterpart in the reference
+        cycle) always keep scipy's summation order: CSR-stream, SELL-64 or SELL-64-sigma, all
+        bitwise scipy. Coarser levels (the multilevel extension, no reference counterpart) may
+        also use the CSR-vector kernel for A_l and R_l when coarse_format='vector' and their
+        mean row length is >= vec_min_row; its fixed order is restated by the oracle.
+        fine_format='autotune' times every admissible kernel on each operator once and keeps
+        the fastest (results in self.tuning); any other value forces that format."""
+        self.tuning = []
+        dev = torch.device("cuda", torch.cuda.current_device())
         for i, L in enumerate(self.levels):
-            for M in (L.A, L.P, L.R):
-                M.set_format(fine_format if fine_format != "vector" else "auto_exact")
-            if i > 0 and coarse_format == "vector":
-                for M in (L.A, L.R):
-                    if M.nnz >= vec_min_row * M.shape[0]:
-                        M.set_format("vector")
-            elif i > 0:
-                for M in (L.A, L.R):
-                    M.set_format("auto_exact")
+            row = {}
+            for name, M in (("A", L.A), ("P", L.P), ("R", L.R)):
+                cands = list(self.EXACT_CANDIDATES)
+                if (i > 0 and name in ("A", "R") and coarse_format == "vector"
+                        and M.nnz >= vec_min_row * M.shape[0]):
+                    cands += list(self.VECTOR_CANDIDATES)
+                if fine_format != "autotune":
+                    M.set_format(fine_format if fine_format != "vector" else "auto_exact")
+                    row[name] = {"chosen": M.get_format()[:2]}
+                    continue
+                x = torch.randn(M.shape[1], dtype=torch.float64, device=dev)
+                y = torch.empty(M.shape[0], dtype=torch.float64, device=dev)
+                times = {}
+                for fmt, arg in cands:
+                    times[f"{fmt}/{arg}"] = self._time_format(M, fmt, arg, x, y)
+                best = min(times, key=times.get)
+                fmt, arg = best.split("/")
+                M.set_format(fmt, int(arg))
+                row[name] = {"chosen": best, "us": {k: round(v, 2) for k, v in times.items()}}
+            self.tuning.append(row)
 
     def formats(self):
         return [{"A": L.A.get_format(), "P": L.P.get_format(), "R": L.R.get_format()}
@@ -108,7 +139,7 @@ class Hierarchy:
     def build(cls, A, *, alpha=0.1, strength_mode="invabs", aggregation="bellman_ford",
               max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, seed=0, sort_seeds=True,
               lanczos_tol=1e-15, lanczos_iter=20000, lloyd_maxiter=10, nu_pre=1, nu_post=1,
-              fine_format="auto_exact", coarse_format="vector", verbose=False, finalize=True):
+              fine_format="autotune", coarse_format="vector", verbose=False, finalize=True):
         H = cls()
         H.jacobi_weight = jacobi_weight
         t_all = time.perf_counter()
