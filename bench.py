@@ -107,6 +107,9 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--dist", action="store_true",
                     help="use the distributed executor even at N=1 (tests the RCCL path)")
+    ap.add_argument("--dist-min-rows", type=int, default=50000,
+                    help="distributed run: row-partition every level with at least this many "
+                         "rows (the rest are replicated on each GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -229,13 +229,17 @@ int mlamg_halo_create(mlamg_comm* c, int64_t n_own, int32_t n_nbr, const int32_t
                       const int64_t* recv_cnt, mlamg_halo** out);
 int mlamg_halo_destroy(mlamg_halo* h);
 int mlamg_halo_exchange(mlamg_halo* h, double* x_ext, void* stream);
-/* distributed V-cycle: A_loc (n_own x n_own+ghosts_x), P_loc (n_own x n_c), R_own (owned coarse
- * rows x n_own+ghosts_r), coarse = hierarchy of the replicated levels 1..L, coarse segment
- * bounds of every rank. Iterates on x_ext (owned part first). */
-int mlamg_dhier_create(mlamg_comm* c, const mlamg_csr* A_loc, const double* dinv_w,
-                       const mlamg_csr* P_loc, const mlamg_csr* R_own, mlamg_halo* halo_x,
-                       mlamg_halo* halo_r, mlamg_hier* coarse, const int64_t* c_lo_all,
+/* partitioned V-cycle over the first K levels (mlamg/partition.py build_levels):
+ * coarse = hierarchy of the replicated levels K..L, nc = its size, c_lo_all/c_hi_all = every
+ * rank's owned segment of that space (they tile [0, nc) in rank order). Then add levels fine to
+ * coarse: A_loc (n_own x n_own+ghosts_x), R_own (owned next-level rows x n_own+ghosts_r), P_loc
+ * (n_own x next own+ghosts_p with halo_p) — or, on the last partitioned level, P_loc with the
+ * replicated coarse columns and halo_p = NULL. The cycle iterates on x_ext (owned part first). */
+int mlamg_dhier_create(mlamg_comm* c, mlamg_hier* coarse, int64_t nc, const int64_t* c_lo_all,
                        const int64_t* c_hi_all, mlamg_dhier** out);
+int mlamg_dhier_add_level(mlamg_dhier* D, const mlamg_csr* A_loc, const double* dinv_w,
+                          const mlamg_csr* P_loc, const mlamg_csr* R_own, mlamg_halo* halo_x,
+                          mlamg_halo* halo_r, mlamg_halo* halo_p);
 int mlamg_dhier_destroy(mlamg_dhier* D);
 int mlamg_dhier_set_coarse_graph(mlamg_dhier* D, int use_graph);
 int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cycles, double tol,

@@ -1,16 +1,17 @@
-// Multi-GPU fine level: RCCL communicator, halo exchange and the distributed V-cycle.
+// Multi-GPU V-cycle: RCCL communicator, halo exchange and the partitioned executor.
 //
-// One process per GPU. The fine level is row-partitioned (mlamg/partition.py builds the maps);
-// coarse levels are replicated on every rank (their setup is deterministic). Per cycle:
-//   x += Dinv r                                    local
-//   halo(x); r = b - A_loc x_ext                   RCCL send/recv with the slab neighbours
-//   halo_r(r); b_c[own] = R_own r_ext              coarse rows owned by the rank of their seed
-//   allgatherv(b_c)                                grouped send/recv of the owned segments
-//   x_c = coarse V-cycle from zero (replicated)    mlamg_hier, optionally a captured hipGraph
-//   x += P_loc x_c                                 local
-//   halo(x); t = x + Dinv(b - A x)                 post-smoothing
-//   halo(t); r = b - A t, ||r||^2 -> allreduce     end-of-cycle residual (MLAMG.py:194)
-// Local rows keep their stored column order and coarse rows their owner's full sum, so the
+// One process per GPU. The first K levels are row-partitioned (mlamg/partition.py builds the
+// maps: level 0 in near-equal blocks, level l+1 owned by the rank owning each aggregate's
+// seed); the levels below are replicated on every rank (their setup is deterministic). Per
+// partitioned level l of a cycle:
+//   x  = Dinv b  (l > 0, zero guess)  |  x += Dinv r  (l = 0, reusing the end-of-cycle r)
+//   halo_x(x); r = b - A_loc x_ext                    RCCL send/recv with the neighbours
+//   halo_r(r); b_{l+1}[own] = R_own r_ext             coarse rows summed by their owner
+//   l+1 partitioned: recurse; halo_p(x_{l+1}) ;  else: allgatherv(b_{l+1}), replicated cycle
+//   x += P_loc x_{l+1,ext}
+//   halo_x(x); t = x + Dinv(b - A x)                  post-smoothing
+//   l = 0: halo_x(t); r = b - A t, ||r||^2 -> allreduce (MLAMG.py:194); x <- t
+// Local rows keep their stored order and every coarse row is summed by one owner, so the
 // iterate is bitwise the single-GPU iterate; only the norm's summation order differs.
 #include "common.hpp"
 
@@ -78,6 +79,8 @@ int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done
 int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
 int jacobi_from_residual(double* x, const double* dinv, const double* r, int64_t n,
                          const int32_t* done, hipStream_t s);
+int jacobi_from_zero(double* x, const double* dinv, const double* b, int64_t n,
+                     const int32_t* done, hipStream_t s);
 int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
                       hipStream_t s);
 int residual_partials(const mlamg_csr* A, const double* b, const double* x, double* r,
@@ -113,23 +116,36 @@ __global__ void k_norm_finish(const double* __restrict__ sum, double* hist, int3
 
 using namespace mlamg;
 
-struct mlamg_dhier {
-  mlamg_comm* c = nullptr;
-  const mlamg_csr* A = nullptr;  // n_own x (n_own + n_ghost_x)
-  const mlamg_csr* P = nullptr;  // n_own x nc
-  const mlamg_csr* R = nullptr;  // (c_hi - c_lo) x (n_own + n_ghost_r)
+namespace {
+struct DLevel {
+  const mlamg_csr* A = nullptr;  // n_own x (n_own + ghosts_x)
+  const mlamg_csr* P = nullptr;  // n_own x (next own + ghosts_p) | n_own x n_c (last level)
+  const mlamg_csr* R = nullptr;  // next own x (n_own + ghosts_r)
   const double* dinv = nullptr;
   mlamg_halo* hx = nullptr;
   mlamg_halo* hr = nullptr;
-  mlamg_hier* coarse = nullptr;  // replicated levels 1..L
-  int64_t n_own = 0, nc = 0, c_lo = 0, c_hi = 0;
-  std::vector<int64_t> c_lo_all, c_hi_all;
-  // work
+  mlamg_halo* hp = nullptr;  // halo of x_{l+1} for P (nullptr on the last partitioned level)
+  int64_t n_own = 0;
+  // work (l > 0: x_ext, b own; every level: r_ext, t_ext; xp_ext = x_{l+1} for P)
+  double* x_ext = nullptr;
+  double* b = nullptr;
   double* r_ext = nullptr;
   double* t_ext = nullptr;
+  double* xp_ext = nullptr;
+};
+}  // namespace
+
+struct mlamg_dhier {
+  mlamg_comm* c = nullptr;
+  std::vector<DLevel> lv;
+  mlamg_hier* coarse = nullptr;  // replicated levels K..L
+  std::vector<int64_t> c_lo_all, c_hi_all;  // owned segments of the replicated space
+  int64_t nc = 0;
   double* bc = nullptr;
   double* partial = nullptr;
   int32_t* flags = nullptr;  // counter, done
+  std::vector<void*> bufs;
+  bool ready = false;
   int coarse_graph = 1;
 };
 
@@ -235,62 +251,65 @@ int mlamg_halo_exchange(mlamg_halo* h, double* x_ext, void* stream) {
   return halo_exchange_impl(h, x_ext, S(stream));
 }
 
-int mlamg_dhier_create(mlamg_comm* c, const mlamg_csr* A_loc, const double* dinv_w,
-                       const mlamg_csr* P_loc, const mlamg_csr* R_own, mlamg_halo* halo_x,
-                       mlamg_halo* halo_r, mlamg_hier* coarse, const int64_t* c_lo_all,
+int mlamg_dhier_create(mlamg_comm* c, mlamg_hier* coarse, int64_t nc, const int64_t* c_lo_all,
                        const int64_t* c_hi_all, mlamg_dhier** out) {
-  MLAMG_REQUIRE(c && A_loc && dinv_w && P_loc && R_own && halo_x && halo_r && coarse && c_lo_all &&
-                    c_hi_all && out,
-                "NULL argument");
+  MLAMG_REQUIRE(c && coarse && c_lo_all && c_hi_all && out, "NULL argument");
   auto* D = new mlamg_dhier();
   D->c = c;
-  D->A = A_loc;
-  D->P = P_loc;
-  D->R = R_own;
-  D->dinv = dinv_w;
-  D->hx = halo_x;
-  D->hr = halo_r;
   D->coarse = coarse;
-  D->n_own = A_loc->n_rows;
-  D->nc = P_loc->n_cols;
+  D->nc = nc;
   D->c_lo_all.assign(c_lo_all, c_lo_all + c->nranks);
   D->c_hi_all.assign(c_hi_all, c_hi_all + c->nranks);
-  D->c_lo = D->c_lo_all[c->rank];
-  D->c_hi = D->c_hi_all[c->rank];
-  auto bad = [&](const char* m) {
-    delete D;
-    set_error(std::string("mlamg_dhier_create: ") + m);
-    return MLAMG_EINVAL;
-  };
-  if (A_loc->n_cols != D->n_own + halo_x->n_ghost) return bad("A_loc columns != n_own + x ghosts");
-  if (halo_x->n_own != D->n_own || halo_r->n_own != D->n_own) return bad("halo n_own mismatch");
-  if (P_loc->n_rows != D->n_own) return bad("P_loc rows != n_own");
-  if (R_own->n_rows != D->c_hi - D->c_lo) return bad("R_own rows != owned coarse rows");
-  if (R_own->n_cols != D->n_own + halo_r->n_ghost) return bad("R_own columns != n_own + r ghosts");
   for (int q = 0; q < c->nranks; ++q)
-    if (D->c_lo_all[q] < 0 || D->c_hi_all[q] < D->c_lo_all[q] || D->c_hi_all[q] > D->nc)
-      return bad("coarse segment out of range");
-  const int64_t next = std::max(D->n_own + halo_r->n_ghost, D->n_own + halo_x->n_ghost);
-  const int64_t nb = part_capacity(A_loc);
-  if (hipMalloc(&D->r_ext, sizeof(double) * std::max<int64_t>(next, 1)) != hipSuccess ||
-      hipMalloc(&D->t_ext, sizeof(double) * std::max<int64_t>(next, 1)) != hipSuccess ||
-      hipMalloc(&D->bc, sizeof(double) * std::max<int64_t>(D->nc, 1)) != hipSuccess ||
-      hipMalloc(&D->partial, sizeof(double) * (nb + 1)) != hipSuccess ||
-      hipMalloc(&D->flags, sizeof(int32_t) * 2) != hipSuccess) {
-    delete D;
-    set_error("mlamg_dhier_create: device allocation failed");
-    return MLAMG_ENOMEM;
-  }
-  (void)hipMemset(D->r_ext, 0, sizeof(double) * std::max<int64_t>(next, 1));
-  (void)hipMemset(D->t_ext, 0, sizeof(double) * std::max<int64_t>(next, 1));
+    if (D->c_lo_all[q] < 0 || D->c_hi_all[q] < D->c_lo_all[q] || D->c_hi_all[q] > nc ||
+        (q > 0 && D->c_lo_all[q] != D->c_hi_all[q - 1])) {
+      delete D;
+      set_error("mlamg_dhier_create: coarse segments must tile [0, nc) in rank order");
+      return MLAMG_EINVAL;
+    }
   *out = D;
+  return MLAMG_OK;
+}
+
+int mlamg_dhier_add_level(mlamg_dhier* D, const mlamg_csr* A_loc, const double* dinv_w,
+                          const mlamg_csr* P_loc, const mlamg_csr* R_own, mlamg_halo* halo_x,
+                          mlamg_halo* halo_r, mlamg_halo* halo_p) {
+  MLAMG_REQUIRE(D && A_loc && dinv_w && P_loc && R_own && halo_x && halo_r, "NULL argument");
+  MLAMG_REQUIRE(!D->ready, "hierarchy already in use");
+  const int64_t n = A_loc->n_rows;
+  MLAMG_REQUIRE(A_loc->n_cols == n + halo_x->n_ghost, "A_loc columns != n_own + x ghosts");
+  MLAMG_REQUIRE(halo_x->n_own == n && halo_r->n_own == n, "halo n_own mismatch");
+  MLAMG_REQUIRE(P_loc->n_rows == n, "P_loc rows != n_own");
+  MLAMG_REQUIRE(R_own->n_cols == n + halo_r->n_ghost, "R_own columns != n_own + r ghosts");
+  if (!D->lv.empty()) {
+    DLevel& up = D->lv.back();
+    MLAMG_REQUIRE(up.hp != nullptr, "previous level was declared the last partitioned level");
+    MLAMG_REQUIRE(up.R->n_rows == n, "level rows != owned coarse rows of the level above");
+    MLAMG_REQUIRE(up.hp->n_own == n, "P halo of the level above has a different n_own");
+    MLAMG_REQUIRE(up.P->n_cols == n + up.hp->n_ghost, "P_loc columns != next own + p ghosts");
+  }
+  if (!halo_p) {
+    const int me = D->c->rank;
+    MLAMG_REQUIRE(P_loc->n_cols == D->nc, "last level P must have the replicated coarse columns");
+    MLAMG_REQUIRE(R_own->n_rows == D->c_hi_all[me] - D->c_lo_all[me],
+                  "R_own rows != owned coarse segment");
+  }
+  DLevel L;
+  L.A = A_loc;
+  L.P = P_loc;
+  L.R = R_own;
+  L.dinv = dinv_w;
+  L.hx = halo_x;
+  L.hr = halo_r;
+  L.hp = halo_p;
+  L.n_own = n;
+  D->lv.push_back(L);
   return MLAMG_OK;
 }
 
 int mlamg_dhier_destroy(mlamg_dhier* D) {
   if (D) {
-    for (void* p : {(void*)D->r_ext, (void*)D->t_ext, (void*)D->bc, (void*)D->partial,
-                    (void*)D->flags})
+    for (void* p : D->bufs)
       if (p) (void)hipFree(p);
     delete D;
   }
@@ -303,15 +322,49 @@ int mlamg_dhier_set_coarse_graph(mlamg_dhier* D, int use_graph) {
   return MLAMG_OK;
 }
 
+static int dalloc(mlamg_dhier* D, double** p, int64_t n) {
+  void* q = nullptr;
+  MLAMG_HIP(hipMalloc(&q, sizeof(double) * std::max<int64_t>(n, 1)));
+  MLAMG_HIP(hipMemset(q, 0, sizeof(double) * std::max<int64_t>(n, 1)));
+  D->bufs.push_back(q);
+  *p = static_cast<double*>(q);
+  return MLAMG_OK;
+}
+
+static int dprepare(mlamg_dhier* D) {
+  if (D->ready) return MLAMG_OK;
+  MLAMG_REQUIRE(!D->lv.empty(), "no partitioned level");
+  MLAMG_REQUIRE(D->lv.back().hp == nullptr, "last partitioned level must have halo_p = NULL");
+  for (size_t l = 0; l < D->lv.size(); ++l) {
+    DLevel& L = D->lv[l];
+    const int64_t ext = L.n_own + std::max(L.hx->n_ghost, L.hr->n_ghost);
+    if (l > 0) {
+      MLAMG_TRY(dalloc(D, &L.x_ext, ext));
+      MLAMG_TRY(dalloc(D, &L.b, L.n_own));
+    }
+    MLAMG_TRY(dalloc(D, &L.r_ext, ext));
+    MLAMG_TRY(dalloc(D, &L.t_ext, ext));
+    if (L.hp) MLAMG_TRY(dalloc(D, &L.xp_ext, L.hp->n_own + L.hp->n_ghost));
+  }
+  MLAMG_TRY(dalloc(D, &D->bc, D->nc));
+  MLAMG_TRY(dalloc(D, &D->partial, part_capacity(D->lv[0].A)));
+  double* f = nullptr;
+  MLAMG_TRY(dalloc(D, &f, 1));
+  D->flags = reinterpret_cast<int32_t*>(f);
+  D->ready = true;
+  return MLAMG_OK;
+}
+
 // allgatherv of the owned coarse segments into the replicated b_c
 static int allgather_segments(mlamg_dhier* D, hipStream_t s) {
   const int P = D->c->nranks, me = D->c->rank;
   if (P == 1) return MLAMG_OK;
+  const int64_t lo = D->c_lo_all[me];
+  const size_t mine = (size_t)(D->c_hi_all[me] - lo);
   MLAMG_NCCL(ncclGroupStart());
-  const size_t mine = (size_t)(D->c_hi - D->c_lo);
   for (int q = 0; q < P; ++q) {
     if (q == me) continue;
-    if (mine) MLAMG_NCCL(ncclSend(D->bc + D->c_lo, mine, ncclFloat64, q, D->c->comm, s));
+    if (mine) MLAMG_NCCL(ncclSend(D->bc + lo, mine, ncclFloat64, q, D->c->comm, s));
     const size_t theirs = (size_t)(D->c_hi_all[q] - D->c_lo_all[q]);
     if (theirs)
       MLAMG_NCCL(ncclRecv(D->bc + D->c_lo_all[q], theirs, ncclFloat64, q, D->c->comm, s));
@@ -320,27 +373,64 @@ static int allgather_segments(mlamg_dhier* D, hipStream_t s) {
   return MLAMG_OK;
 }
 
+static int dcycle_below(mlamg_dhier* D, size_t l, double** x_out, hipStream_t s);
+
+// coarse-grid correction of partitioned level l: b_{l+1} = R r, solve below, x += P x_{l+1}
+static int correct(mlamg_dhier* D, size_t l, double* x_ext, const int32_t* done, hipStream_t s) {
+  DLevel& L = D->lv[l];
+  MLAMG_TRY(halo_exchange_impl(L.hr, L.r_ext, s));
+  if (L.hp) {
+    DLevel& N = D->lv[l + 1];
+    MLAMG_TRY(spmv_set(L.R, L.r_ext, N.b, done, s));
+    double* xn = nullptr;
+    MLAMG_TRY(dcycle_below(D, l + 1, &xn, s));
+    MLAMG_HIP(hipMemcpyAsync(L.xp_ext, xn, sizeof(double) * N.n_own, hipMemcpyDeviceToDevice, s));
+    MLAMG_TRY(halo_exchange_impl(L.hp, L.xp_ext, s));
+    MLAMG_TRY(spmv_add(L.P, L.xp_ext, x_ext, done, s));
+  } else {
+    const int me = D->c->rank;
+    MLAMG_TRY(spmv_set(L.R, L.r_ext, D->bc + D->c_lo_all[me], done, s));
+    MLAMG_TRY(allgather_segments(D, s));
+    double* xc = nullptr;
+    MLAMG_TRY(hier_coarse_cycle(D->coarse, D->bc, &xc, D->coarse_graph, s));
+    MLAMG_TRY(spmv_add(L.P, xc, x_ext, done, s));
+  }
+  return MLAMG_OK;
+}
+
+// one cycle from a zero guess at partitioned level l > 0 (rhs in lv[l].b); result (own part)
+// returned through x_out
+static int dcycle_below(mlamg_dhier* D, size_t l, double** x_out, hipStream_t s) {
+  const int32_t* done = D->flags + 1;
+  DLevel& L = D->lv[l];
+  MLAMG_TRY(jacobi_from_zero(L.x_ext, L.dinv, L.b, L.n_own, done, s));
+  MLAMG_TRY(halo_exchange_impl(L.hx, L.x_ext, s));
+  MLAMG_TRY(residual_impl(L.A, L.b, L.x_ext, L.r_ext, nullptr, nullptr, nullptr,
+                          const_cast<int32_t*>(done), 0.0, nullptr, nullptr, nullptr, s));
+  MLAMG_TRY(correct(D, l, L.x_ext, done, s));
+  MLAMG_TRY(halo_exchange_impl(L.hx, L.x_ext, s));
+  MLAMG_TRY(jacobi_sweep(L.A, L.dinv, L.b, L.x_ext, L.t_ext, false, done, s));
+  *x_out = L.t_ext;
+  return MLAMG_OK;
+}
+
 static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, double tol,
                   hipStream_t s) {
   int32_t* counter = D->flags;
   int32_t* done = D->flags + 1;
-  const mlamg_csr* A = D->A;
+  DLevel& L = D->lv[0];
+  const mlamg_csr* A = L.A;
   // pre-smoothing from the end-of-cycle residual (bitwise a Jacobi sweep)
-  MLAMG_TRY(jacobi_from_residual(x_ext, D->dinv, D->r_ext, D->n_own, done, s));
-  MLAMG_TRY(halo_exchange_impl(D->hx, x_ext, s));
-  MLAMG_TRY(residual_impl(A, b, x_ext, D->r_ext, nullptr, nullptr, nullptr, done, 0.0, nullptr,
+  MLAMG_TRY(jacobi_from_residual(x_ext, L.dinv, L.r_ext, L.n_own, done, s));
+  MLAMG_TRY(halo_exchange_impl(L.hx, x_ext, s));
+  MLAMG_TRY(residual_impl(A, b, x_ext, L.r_ext, nullptr, nullptr, nullptr, done, 0.0, nullptr,
                           nullptr, nullptr, s));
-  MLAMG_TRY(halo_exchange_impl(D->hr, D->r_ext, s));
-  MLAMG_TRY(spmv_set(D->R, D->r_ext, D->bc + D->c_lo, done, s));
-  MLAMG_TRY(allgather_segments(D, s));
-  double* xc = nullptr;
-  MLAMG_TRY(hier_coarse_cycle(D->coarse, D->bc, &xc, D->coarse_graph, s));
-  MLAMG_TRY(spmv_add(D->P, xc, x_ext, done, s));
-  MLAMG_TRY(halo_exchange_impl(D->hx, x_ext, s));
-  MLAMG_TRY(jacobi_sweep(A, D->dinv, b, x_ext, D->t_ext, false, done, s));
-  MLAMG_TRY(halo_exchange_impl(D->hx, D->t_ext, s));
+  MLAMG_TRY(correct(D, 0, x_ext, done, s));
+  MLAMG_TRY(halo_exchange_impl(L.hx, x_ext, s));
+  MLAMG_TRY(jacobi_sweep(A, L.dinv, b, x_ext, L.t_ext, false, done, s));
+  MLAMG_TRY(halo_exchange_impl(L.hx, L.t_ext, s));
   // r = b - A t with per-block ||r||^2 partials, x <- t; then the global norm
-  MLAMG_TRY(residual_partials(A, b, D->t_ext, D->r_ext, x_ext, D->t_ext, D->partial, done, s));
+  MLAMG_TRY(residual_partials(A, b, L.t_ext, L.r_ext, x_ext, L.t_ext, D->partial, done, s));
   const int nb = (int)A->n_part;
   hipLaunchKernelGGL(k_local_sum, dim3(1), dim3(1024), 0, s, D->partial, nb);
   MLAMG_HIP(hipGetLastError());
@@ -357,10 +447,12 @@ int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cyc
                        double* res_hist, int32_t* cycles_done_host, void* stream) {
   MLAMG_REQUIRE(D && b && x_ext, "NULL argument");
   MLAMG_REQUIRE(n_cycles >= 0, "n_cycles < 0");
+  MLAMG_TRY(dprepare(D));
   hipStream_t s = S(stream);
+  DLevel& L = D->lv[0];
   MLAMG_HIP(hipMemsetAsync(D->flags, 0, 2 * sizeof(int32_t), s));
-  MLAMG_TRY(halo_exchange_impl(D->hx, x_ext, s));
-  MLAMG_TRY(residual_impl(D->A, b, x_ext, D->r_ext, nullptr, nullptr, nullptr, nullptr, 0.0,
+  MLAMG_TRY(halo_exchange_impl(L.hx, x_ext, s));
+  MLAMG_TRY(residual_impl(L.A, b, x_ext, L.r_ext, nullptr, nullptr, nullptr, nullptr, 0.0,
                           nullptr, nullptr, nullptr, s));
   for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(dcycle(D, b, x_ext, res_hist, tol, s));
   if (cycles_done_host) {

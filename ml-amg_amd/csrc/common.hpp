@@ -108,6 +108,11 @@ void csr_free(mlamg_csr* A);
 // scratch buffer cache (per device); grows monotonically, freed at destroy/exit.
 void* scratch(size_t bytes, int slot);
 
+// bumped by every mlamg_csr_set_format: captured hipGraphs bake kernel choice and format
+// arrays in, so graph caches compare it and re-capture after a change.
+uint64_t format_epoch();
+void bump_format_epoch();
+
 // generic kernels shared across translation units
 int launch_spmv_plain(const mlamg_csr* A, const double* x, double* y, hipStream_t s);
 int exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s);  // out[n] = total

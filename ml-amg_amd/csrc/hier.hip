@@ -71,6 +71,7 @@ struct mlamg_hier {
   hipGraph_t cgraph = nullptr;
   hipGraphExec_t cexec = nullptr;
   const double* cg_b = nullptr;
+  uint64_t g_epoch = 0, cg_epoch = 0;
   double* cg_res = nullptr;
 };
 
@@ -216,7 +217,7 @@ int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_gr
                       hipStream_t s) {
   MLAMG_TRY(hier_prepare(H));
   if (!use_graph) return cycle_coarse(H, 0, b, x_out, s);
-  if (!(H->cexec && H->cg_b == b)) {
+  if (!(H->cexec && H->cg_b == b && H->cg_epoch == format_epoch())) {
     if (H->cexec) (void)hipGraphExecDestroy(H->cexec);
     if (H->cgraph) (void)hipGraphDestroy(H->cgraph);
     H->cexec = nullptr;
@@ -235,6 +236,7 @@ int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_gr
     H->cgraph = g;
     MLAMG_HIP(hipGraphInstantiate(&H->cexec, g, nullptr, nullptr, 0));
     H->cg_b = b;
+    H->cg_epoch = format_epoch();
     H->cg_res = res;
   }
   MLAMG_HIP(hipGraphLaunch(H->cexec, s));
@@ -313,7 +315,8 @@ int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, d
                             nullptr, nullptr, s));
   }
   if (use_graph && n_cycles > 0 && !H->lv.empty()) {
-    if (!(H->exec && H->g_b == b && H->g_x == x && H->g_hist == res_hist && H->g_tol == tol)) {
+    if (!(H->exec && H->g_b == b && H->g_x == x && H->g_hist == res_hist && H->g_tol == tol &&
+          H->g_epoch == format_epoch())) {
       hier_free_graph(H);
       if (!H->cap_stream) MLAMG_HIP(hipStreamCreateWithFlags(&H->cap_stream, hipStreamNonBlocking));
       MLAMG_HIP(hipStreamBeginCapture(H->cap_stream, hipStreamCaptureModeThreadLocal));
@@ -331,6 +334,7 @@ int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, d
       H->g_x = x;
       H->g_hist = res_hist;
       H->g_tol = tol;
+      H->g_epoch = format_epoch();
     }
     for (int c = 0; c < n_cycles; ++c) MLAMG_HIP(hipGraphLaunch(H->exec, s));
   } else {

@@ -2,6 +2,8 @@
 // partitioning, scratch buffers. Host C++ compiled by hipcc; no torch dependency.
 #include "common.hpp"
 
+#include <atomic>
+
 #include <algorithm>
 #include <cstring>
 #include <mutex>
@@ -237,3 +239,9 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
 }
 
 }  // extern "C"
+
+namespace mlamg {
+static std::atomic<uint64_t> g_format_epoch{0};
+uint64_t format_epoch() { return g_format_epoch.load(); }
+void bump_format_epoch() { g_format_epoch.fetch_add(1); }
+}  // namespace mlamg

@@ -517,6 +517,7 @@ int mlamg_jacobi_explicit(const mlamg_csr* M, const double* dinv_w, const double
 int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
   MLAMG_REQUIRE(A, "NULL argument");
   hipStream_t s = S(stream);
+  bump_format_epoch();
   switch (fmt) {
     case MLAMG_FMT_CSR_STREAM:
       drop_sell(A);

@@ -102,8 +102,8 @@ SIGNATURES = {
     "mlamg_halo_create": (c_int, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vpp]),
     "mlamg_halo_destroy": (c_int, [c_vp]),
     "mlamg_halo_exchange": (c_int, [c_vp, c_vp, c_vp]),
-    "mlamg_dhier_create": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                   c_vpp]),
+    "mlamg_dhier_create": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vpp]),
+    "mlamg_dhier_add_level": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mlamg_dhier_destroy": (c_int, [c_vp]),
     "mlamg_dhier_set_coarse_graph": (c_int, [c_vp, c_int]),
     "mlamg_dhier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_vp]),

@@ -1,5 +1,5 @@
-"""Multi-GPU V-cycle: fine level row-partitioned over one process per GPU, RCCL halo exchange,
-coarse levels replicated (C side: csrc/comm.hip).
+"""Multi-GPU V-cycle: the K finest levels row-partitioned over one process per GPU with RCCL halo
+exchanges, the coarser levels replicated (C side: csrc/comm.hip).
 
 The reference's only parallel backend is a task farm over independent problems
 (ns/parallel/pool.py:139-186: pickled callables over multiprocessing pipes or mpi4py). Splitting
@@ -75,50 +75,80 @@ class Halo:
 
 
 class DistributedHierarchy:
-    """Fine level of a (replicated) Hierarchy split over `world` GPUs."""
+    """The K finest levels of a (replicated) Hierarchy split over `world` GPUs.
 
-    def __init__(self, H, A_host, comm, fine_format="auto_exact"):
-        """H: mlamg.hierarchy.Hierarchy built identically on every rank (sorted seeds);
-        A_host: the fine matrix as scipy CSR (same arrays as H.levels[0].A)."""
+    Level l+1 rows are owned by the rank that owns their aggregate's seed node on level l, so
+    restriction needs only an r-halo and prolongation a halo of the coarse correction; below
+    level K-1 the owned coarse segments are allgathered and every rank runs the replicated
+    coarse cycle. The iterate is bitwise the single-GPU Hierarchy.cycle iterate."""
+
+    def __init__(self, H, comm, min_rows=50000, max_partitioned=None, A_host=None):
+        """H: mlamg.hierarchy.Hierarchy built identically on every rank (sorted seeds, same
+        kernel formats — see sync_formats). Levels with at least `min_rows` rows (at most
+        `max_partitioned` of them) are row-partitioned; the rest are replicated."""
         if not H.levels:
             raise ValueError("distributed cycle needs at least one level above the coarse solve")
-        L0 = H.levels[0]
-        if L0.seeds is None:
+        if (H.nu_pre, H.nu_post) != (1, 1):
+            raise NotImplementedError("the distributed cycle is V(1,1)")
+        if any(L.seeds is None for L in H.levels):
             raise ValueError("hierarchy was not built by Hierarchy.build (seeds unknown)")
         self.H = H
         self.comm = comm
         world, rank = comm.world, comm.rank
-        P0 = L0.P.to_scipy()
-        self.part = p = partition.build(A_host, P0, L0.seeds, world, rank)
-        self.lo, self.hi = p["lo"], p["hi"]
+        K = 1
+        while K < len(H.levels) and H.levels[K].A.shape[0] >= min_rows:
+            K += 1
+        if max_partitioned is not None:
+            K = max(1, min(K, int(max_partitioned)))
+        self.K = K
+        As = [A_host if (l == 0 and A_host is not None) else H.levels[l].A.to_scipy()
+              for l in range(K)]
+        Ps = [H.levels[l].P.to_scipy() for l in range(K)]
+        self.parts = parts = partition.build_levels(As, Ps, [H.levels[l].seeds for l in range(K)],
+                                                    world, rank)
+        del As, Ps
+        p0 = parts[0]
+        self.lo, self.hi = p0["lo"], p0["hi"]
         self.n_own = self.hi - self.lo
-        # level-0 operators: the kernel H chose for the global operator (scipy order either way)
-        def like(M_glob, M_loc):
+
+        def like(M_glob, M_loc):  # the kernel H chose for the global operator
             fmt, arg, _ = M_glob.get_format()
             return M_loc.set_format(fmt, arg)
 
-        self.A_loc = like(L0.A, DeviceCSR.from_scipy(p["A_loc"], check=False))
-        self.P_loc = like(L0.P, DeviceCSR.from_scipy(p["P_loc"], check=False))
-        self.R_own = like(L0.R, DeviceCSR.from_scipy(p["R_own"], check=False))
-        self.dinv = L0.dinv[self.lo:self.hi].clone()
-        self.hx = Halo(comm, p["halo_x"])
-        self.hr = Halo(comm, p["halo_r"])
-        # replicated coarse hierarchy: levels 1..L + the dense coarse inverse of H
+        self._keep = []
+        last = parts[-1]
+        # replicated coarse hierarchy: levels K..L + the dense coarse inverse of H
         hh = ctypes.c_void_p()
         call("mlamg_hier_create", ctypes.byref(hh))
         self.coarse = hh
-        for L in H.levels[1:]:
+        for L in H.levels[K:]:
             call("mlamg_hier_add_level", hh, L.A.handle, ptr(L.dinv), L.P.handle, L.R.handle)
         call("mlamg_hier_set_coarse", hh, H.Ac.handle, H.dense)
         call("mlamg_hier_set_smoothing", hh, int(H.nu_pre), int(H.nu_post))
-        self.c_lo = np.array([a for a, _ in p["c_ranges"]], dtype=np.int64)
-        self.c_hi = np.array([b for _, b in p["c_ranges"]], dtype=np.int64)
+        self.c_lo = np.array([a for a, _ in last["c_ranges"]], dtype=np.int64)
+        self.c_hi = np.array([b for _, b in last["c_ranges"]], dtype=np.int64)
         d = ctypes.c_void_p()
-        call("mlamg_dhier_create", comm.handle, self.A_loc.handle, ptr(self.dinv),
-             self.P_loc.handle, self.R_own.handle, self.hx.handle, self.hr.handle, hh,
+        call("mlamg_dhier_create", comm.handle, hh, int(last["nc"]),
              self.c_lo.ctypes.data_as(ctypes.c_void_p), self.c_hi.ctypes.data_as(ctypes.c_void_p),
              ctypes.byref(d))
         self.handle = d
+        self.ghosts = []
+        for l, p in enumerate(parts):
+            Lg = H.levels[l]
+            A_loc = like(Lg.A, DeviceCSR.from_scipy(p["A_loc"], check=False))
+            P_loc = like(Lg.P, DeviceCSR.from_scipy(p["P_loc"], check=False))
+            R_own = like(Lg.R, DeviceCSR.from_scipy(p["R_own"], check=False))
+            dinv = Lg.dinv[p["lo"]:p["hi"]].clone()
+            hx = Halo(comm, p["halo_x"])
+            hr = Halo(comm, p["halo_r"])
+            hp = Halo(comm, p["halo_p"]) if p["halo_p"] is not None else None
+            self._keep.append((A_loc, P_loc, R_own, dinv, hx, hr, hp))
+            self.ghosts.append((hx.n_ghost, hr.n_ghost, hp.n_ghost if hp else 0))
+            call("mlamg_dhier_add_level", d, A_loc.handle, ptr(dinv), P_loc.handle, R_own.handle,
+                 hx.handle, hr.handle, hp.handle if hp else None)
+            if l == 0:
+                self.A_loc = A_loc
+                self.hx = hx
         self.n_ext = self.n_own + self.hx.n_ghost
 
     def new_x(self, x_own):
@@ -147,6 +177,14 @@ class DistributedHierarchy:
                 except Exception:
                     pass
                 setattr(self, attr, None)
+
+
+def sync_formats(H, world):
+    """Give every rank rank 0's SpMV kernel choice (autotune timings differ between GPUs)."""
+    if world > 1:
+        obj = [H.formats()]
+        dist.broadcast_object_list(obj, src=0)
+        H.set_formats(obj[0])
 
 
 def init_process_group(world, rank):
@@ -185,12 +223,14 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
     t0 = time.perf_counter()
     H = Hierarchy.build(A, alpha=args.alpha, strength_mode="invabs", max_coarse=args.max_coarse)
     setup_s = time.perf_counter() - t0
+    sync_formats(H, world)
     comm = Comm(world, rank)
     t1 = time.perf_counter()
-    D = DistributedHierarchy(H, A, comm)
+    D = DistributedHierarchy(H, comm, min_rows=args.dist_min_rows, A_host=A)
     part_s = time.perf_counter() - t1
-    log(f"setup {setup_s:.1f}s (replicated), partition+upload {part_s:.1f}s; rank rows "
-        f"{D.lo}..{D.hi}, x ghosts {D.hx.n_ghost}, r ghosts {D.hr.n_ghost}")
+    log(f"setup {setup_s:.1f}s (replicated), partition+upload {part_s:.1f}s; {D.K} of "
+        f"{len(H.levels)} levels partitioned; rank rows {D.lo}..{D.hi}; ghosts (x, r, p) per "
+        f"level {D.ghosts}")
     x0 = np.random.RandomState(0).randn(n)
     x0 /= np.linalg.norm(x0)
     b_own = torch.zeros(D.n_own, dtype=torch.float64, device="cuda")
@@ -252,8 +292,9 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
             "data": "synthetic",
             "config": {
                 "workload": f"C4: 3D 7-point Laplace {n1}^3 ({n} DoF), SA-AMG V(1,1) weighted "
-                            f"Jacobi, fine level row-split over {world} GPUs + RCCL halo, "
-                            f"{H.n_levels - 1} coarse levels replicated",
+                            f"Jacobi, {D.K} finest levels row-split over {world} GPUs + RCCL "
+                            f"halos, {H.n_levels - D.K} coarser levels replicated",
+                "partitioned_levels": D.K,
                 "n": n, "levels": H.n_levels, "parallelism": f"rowsplit{world}",
                 "dist_matches_single_gpu": bool(ok.item() == 1.0),
             },

@@ -135,6 +135,16 @@ class Hierarchy:
         return [{"A": L.A.get_format(), "P": L.P.get_format(), "R": L.R.get_format()}
                 for L in self.levels]
 
+    def set_formats(self, formats):
+        """Apply a formats() list (e.g. rank 0's autotune result on every rank, so that the
+        replicated hierarchies of a distributed run sum every row in the same order)."""
+        if len(formats) != len(self.levels):
+            raise ValueError("formats list does not match the number of levels")
+        for L, f in zip(self.levels, formats):
+            for name in ("A", "P", "R"):
+                fmt, arg = f[name][0], f[name][1]
+                getattr(L, name).set_format(fmt, int(arg))
+
     @classmethod
     def build(cls, A, *, alpha=0.1, strength_mode="invabs", aggregation="bellman_ford",
               max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, seed=0, sort_seeds=True,

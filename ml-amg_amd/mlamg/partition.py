@@ -73,6 +73,76 @@ def _remap(M, lo, hi, ghosts):
                          shape=(M.shape[0], n_own + len(ghosts)))
 
 
+def _halos(ghosts_all, ranges, r):
+    """Halo of rank r in an index space split by `ranges`, given every rank's ghost set."""
+    lo, hi = ranges[r]
+    his = np.array([h for _, h in ranges], dtype=np.int64)
+    sends = {}
+    for q in range(len(ranges)):
+        if q == r:
+            continue
+        g = ghosts_all[q]
+        need = g[(g >= lo) & (g < hi)]
+        if len(need):
+            sends[q] = (need - lo).astype(np.int32)
+    return Halo(hi - lo, ghosts_all[r], owner_of(ghosts_all[r], his), sends)
+
+
+def _seed_ranges(seeds, ranges, nc):
+    seeds = np.asarray(seeds, dtype=np.int64)
+    if len(seeds) != nc or (len(seeds) > 1 and np.any(np.diff(seeds) <= 0)):
+        raise ValueError("coarse unknowns must be ordered by strictly increasing seed node")
+    b = [int(np.searchsorted(seeds, lo)) for lo, _ in ranges] + [nc]
+    return [(b[r], b[r + 1]) for r in range(len(ranges))]
+
+
+def build_levels(As, Ps, seeds_list, world, rank):
+    """Partition maps of the first K = len(As) levels for `rank` (list of per-level dicts).
+
+    Level 0 rows: near-equal contiguous blocks. Level l+1 rows: the coarse unknowns whose seed
+    lies in the rank's level-l rows (contiguous because seeds are sorted). For l < K-1 the
+    prolongation P_l gets its columns renumbered into [owned level-(l+1) rows | P-ghosts] with a
+    halo of x_{l+1}; the last partitioned level's P keeps global columns (the level below is
+    replicated on every rank, gathered with an allgatherv of the owned coarse segments).
+    """
+    K = len(As)
+    ranges = row_ranges(As[0].shape[0], world)
+    out = []
+    for l in range(K):
+        A = As[l].tocsr()
+        P = Ps[l].tocsr()
+        n, nc = A.shape[0], P.shape[1]
+        c_ranges = _seed_ranges(seeds_list[l], ranges, nc)
+        R = P.T.tocsr()
+        R.sort_indices()
+        xg, rg, pg = [], [], []
+        for q, (lo, hi) in enumerate(ranges):
+            xg.append(_ghost_sets(A[lo:hi].indices, lo, hi))
+            clo, chi = c_ranges[q]
+            rg.append(_ghost_sets(R[clo:chi].indices, lo, hi))
+            pg.append(_ghost_sets(P[lo:hi].indices, clo, chi))
+        lo, hi = ranges[rank]
+        clo, chi = c_ranges[rank]
+        last = l == K - 1
+        d = {
+            "level": l, "rank": rank, "world": world, "lo": lo, "hi": hi, "n": n, "nc": nc,
+            "c_lo": clo, "c_hi": chi, "c_ranges": c_ranges, "ranges": ranges,
+            "A_loc": _remap(A[lo:hi], lo, hi, xg[rank]),
+            "R_own": _remap(R[clo:chi], lo, hi, rg[rank]),
+            "halo_x": _halos(xg, ranges, rank),
+            "halo_r": _halos(rg, ranges, rank),
+        }
+        if last:
+            d["P_loc"] = P[lo:hi].copy()
+            d["halo_p"] = None
+        else:
+            d["P_loc"] = _remap(P[lo:hi], clo, chi, pg[rank])
+            d["halo_p"] = _halos(pg, c_ranges, rank)
+        out.append(d)
+        ranges = c_ranges
+    return out
+
+
 def build(A0, P0, seeds, world, rank=None):
     """Partition maps for all ranks (or one rank). A0: n x n CSR, P0: n x nc CSR, seeds: sorted
     seed node of each coarse unknown (aggregate j's seed is seeds[j]).

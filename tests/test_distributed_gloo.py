@@ -74,7 +74,7 @@ def _problem(kind):
     return problems.jump_2d(30, np.array([[0.3, 0.4, 1e-2], [0.7, 0.6, 1e2]]))
 
 
-def _worker(rank, world, port, kind, ncyc, q):
+def _worker(rank, world, port, kind, ncyc, K, q):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -88,49 +88,80 @@ def _worker(rank, world, port, kind, ncyc, q):
         n = A.shape[0]
         levels, Ac = orc.build_hierarchy(A, alpha=0.1, seed=0, sort_seeds=True, max_coarse=40,
                                          omegas=[0.61, 0.63, 0.65, 0.67, 0.69])
+        K = min(K, len(levels))
         lu = spla.factorized(sp.csc_matrix(Ac))
         x0 = np.random.RandomState(0).randn(n)
         b = np.random.RandomState(1).randn(n)
         x_ref, h_ref = orc.vcycle_solve(levels, Ac, b, x0, ncyc, lu=lu)
-        L0 = levels[0]
-        p = partition.build(L0["A"], L0["P"], L0["seeds"], world, rank)
-        lo, hi = p["lo"], p["hi"]
+        parts = partition.build_levels([levels[l]["A"] for l in range(K)],
+                                       [levels[l]["P"] for l in range(K)],
+                                       [levels[l]["seeds"] for l in range(K)], world, rank)
+        dl = [levels[l]["Dw"].diagonal()[p["lo"]:p["hi"]] for l, p in enumerate(parts)]
+        coarse = orc.make_cycle(levels[K:], lu)
+        tag = [0]
+
+        def halo(v, h, n_own):
+            tag[0] += 1
+            _halo(v, h, n_own, tag[0])
+
+        def ext(l):
+            p = parts[l]
+            return np.zeros(p["hi"] - p["lo"] + max(p["halo_x"].n_ghost, p["halo_r"].n_ghost))
+
+        # emulation of csrc/comm.hip: correct / dcycle_below / dcycle
+        def correct(l, r):
+            p = parts[l]
+            m = p["hi"] - p["lo"]
+            halo(r, p["halo_r"], m)
+            if p["halo_p"] is not None:
+                xn = below(l + 1, orc.csr_matvec(p["R_own"], r))
+                hp = p["halo_p"]
+                xp = np.zeros(hp.n_own + hp.n_ghost)
+                xp[:hp.n_own] = xn
+                halo(xp, hp, hp.n_own)
+                return orc.csr_matvec(p["P_loc"], xp)
+            bc = np.zeros(p["nc"])
+            bc[p["c_lo"]:p["c_hi"]] = orc.csr_matvec(p["R_own"], r)
+            tag[0] += 1
+            _allgatherv(bc, p["c_ranges"], rank, world, tag[0])
+            return orc.csr_matvec(p["P_loc"], coarse(0, bc, None))
+
+        def below(l, bl):
+            p = parts[l]
+            m = p["hi"] - p["lo"]
+            d = dl[l]
+            x, r = ext(l), ext(l)
+            x[:m] = d * bl
+            halo(x, p["halo_x"], m)
+            r[:m] = bl - orc.csr_matvec(p["A_loc"], x)
+            x[:m] = x[:m] + correct(l, r)
+            halo(x, p["halo_x"], m)
+            return x[:m] + d * (bl - orc.csr_matvec(p["A_loc"], x))
+
+        p0 = parts[0]
+        lo, hi = p0["lo"], p0["hi"]
         n_own = hi - lo
-        d = L0["Dw"].diagonal()[lo:hi]
+        d = dl[0]
         bo = b[lo:hi]
-        hx, hr = p["halo_x"], p["halo_r"]
-        x = np.zeros(n_own + hx.n_ghost)
+        hx = p0["halo_x"]
+        x, r = ext(0), ext(0)
         x[:n_own] = x0[lo:hi]
-        r = np.zeros(n_own + hr.n_ghost)
-        coarse = orc.make_cycle(levels[1:], lu)
-        tag = 0
 
         def resid(v):
-            return bo - orc.csr_matvec(p["A_loc"], v)
+            return bo - orc.csr_matvec(p0["A_loc"], v)
 
-        _halo(x, hx, n_own, tag)
+        halo(x, hx, n_own)
         r[:n_own] = resid(x)
         hist = []
         for _ in range(ncyc):
             x[:n_own] = x[:n_own] + d * r[:n_own]
-            tag += 1
-            _halo(x, hx, n_own, tag)
+            halo(x, hx, n_own)
             r[:n_own] = resid(x)
-            tag += 1
-            _halo(r, hr, n_own, tag)
-            bc = np.zeros(p["nc"])
-            clo, chi = p["c_lo"], p["c_hi"]
-            bc[clo:chi] = orc.csr_matvec(p["R_own"], r)
-            tag += 1
-            _allgatherv(bc, p["c_ranges"], rank, world, tag)
-            xc = coarse(0, bc, None)
-            x[:n_own] = x[:n_own] + orc.csr_matvec(p["P_loc"], xc)
-            tag += 1
-            _halo(x, hx, n_own, tag)
+            x[:n_own] = x[:n_own] + correct(0, r)
+            halo(x, hx, n_own)
             t = np.zeros_like(x)
             t[:n_own] = x[:n_own] + d * resid(x)
-            tag += 1
-            _halo(t, hx, n_own, tag)
+            halo(t, hx, n_own)
             r[:n_own] = resid(t)
             s = torch.tensor([float(np.dot(r[:n_own], r[:n_own]))], dtype=torch.float64)
             dist.all_reduce(s)
@@ -138,20 +169,25 @@ def _worker(rank, world, port, kind, ncyc, q):
             x[:n_own] = t[:n_own]
         same_x = bool(np.array_equal(x[:n_own], x_ref[lo:hi]))
         same_h = bool(np.allclose(hist, h_ref, rtol=1e-12, atol=0))
-        q.put((rank, same_x, same_h, hx.n_ghost, hr.n_ghost, len(hx.neighbors)))
+        gp = [pp["halo_p"].n_ghost for pp in parts[:-1]]
+        q.put((rank, same_x, same_h, hx.n_ghost, p0["halo_r"].n_ghost, len(hx.neighbors), K,
+               gp))
         dist.barrier()
         dist.destroy_process_group()
-    except Exception as e:  # pragma: no cover - reported through the queue
+    except Exception:  # pragma: no cover - reported through the queue
         import traceback
         q.put((rank, "error", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,kind", [(2, "3d"), (3, "3d"), (2, "jump")])
-def test_partitioned_vcycle_bitwise(world, kind):
+@pytest.mark.parametrize("world,kind,K", [(2, "3d", 1), (3, "3d", 1), (2, "jump", 1),
+                                          (2, "3d", 2), (3, "3d", 9), (2, "jump", 9)])
+def test_partitioned_vcycle_bitwise(world, kind, K):
+    """K = number of finest levels row-partitioned (9 = all above the coarse solve)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, 4, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, 4, K, q))
+             for r in range(world)]
     for pr in procs:
         pr.start()
     res = [q.get(timeout=240) for _ in range(world)]
@@ -159,10 +195,13 @@ def test_partitioned_vcycle_bitwise(world, kind):
         pr.join(timeout=60)
     for item in res:
         assert item[1] != "error", item[2]
-        rank, same_x, same_h, gx, gr, nn = item
-        assert same_x, f"rank {rank}: iterate differs from the single-process cycle"
-        assert same_h, f"rank {rank}: residual history differs"
+        rank, same_x, same_h, gx, gr, nn, k_used, gp = item
+        assert same_x, f"rank {rank}: iterate differs from the single-process cycle (K={k_used})"
+        assert same_h, f"rank {rank}: residual history differs (K={k_used})"
         assert gx > 0 and gr > 0 and nn >= 1
+        assert len(gp) == k_used - 1
+        if K > 1:
+            assert k_used >= 2
 
 
 def test_row_ranges_and_owner():
