@@ -8,8 +8,9 @@ separately.
 
   python bench.py [--gpus N --steps K --warmup W] [--n 216] [--no-cpu-baseline]
 
-N > 1: launched by torch.distributed.run, one process per GPU; the fine level is row-partitioned
-(contiguous z-slabs) with an RCCL halo exchange, coarse levels are replicated (mlamg.distributed).
+N > 1: launched by torch.distributed.run, one process per GPU; every level with at least
+--dist-min-rows rows is row-partitioned (contiguous slabs; coarse rows follow their aggregate
+seed) with RCCL halo exchanges, the coarser levels are replicated (mlamg.distributed).
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -170,7 +171,7 @@ def main():
         t = time_kernel(lambda: Ab.matvec(xs, out=ys), reps=30)
         ab[fmt] = {"us": round(t * 1e6, 2), "GBps": round(B / t / 1e9, 1)}
     del Ab
-    pmc = load_traffic("spmv_c4_pmc.json")
+    pmc = load_traffic(f"spmv_c4_pmc_{fmt0}.json")
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     cyc_bytes = H.cycle_bytes()
     out = {

@@ -105,6 +105,7 @@ __global__ __launch_bounds__(1024) void k_local_sum(double* __restrict__ partial
 
 __global__ void k_norm_finish(const double* __restrict__ sum, double* hist, int32_t* counter,
                               int32_t* done, double tol) {
+  if (*done) return;  // converged earlier: every rank saw the same global norm
   const double nrm = sqrt(*sum);
   const int c = *counter;
   if (hist) hist[c] = nrm;

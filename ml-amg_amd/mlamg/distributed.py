@@ -299,7 +299,8 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
                 "dist_matches_single_gpu": bool(ok.item() == 1.0),
             },
             "roofline": {
-                "bound": "hbm", "kernel": "fine-level CSR-stream SpMV, local rows (slowest rank)",
+                "bound": "hbm", "kernel": f"fine-level SpMV ({D.A_loc.get_format()[0]}), local rows "
+                                    "(slowest rank)",
                 "achieved": round(achieved_min, 1), "peak": hbm_peak, "unit": "GB/s",
                 "frac": round(achieved_min / hbm_peak, 4), "traffic": None,
                 "algorithmic_bytes_per_launch": B, "avg_launch_us": round(t_spmv * 1e6, 2),

@@ -30,7 +30,9 @@ fi
 if [ "$MODE" = prof ]; then
   rm -rf $OUT/prof
   step rocprof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python bench.py --steps 30 --warmup 3 --no-cpu-baseline
-  step pmc_traffic 900 python tools/pmc_traffic.py ${ROUND:-r01}
+  step rocprof_spmv 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o spmv -- python tools/spmv_driver.py
+  step pmc_sell 600 python tools/pmc_traffic.py ${ROUND:-r01} sell
+  step pmc_csr 600 python tools/pmc_traffic.py ${ROUND:-r01} csr_stream
 fi
 if [ "$MODE" = dist ]; then
   step bench_dist1 900 python bench.py --dist --steps 30 --warmup 3

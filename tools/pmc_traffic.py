@@ -6,9 +6,10 @@ counters only, no tracing domains. Both report KiB per dispatch. gfx950 correcti
 wide coalesced streaming read, so reads are doubled; WRITE_SIZE is exact for streaming stores.
 This parent process never touches the GPU (rocprofv3 runs the driver as a child).
 
-Writes gpurun_out/pmc/spmv_c4_pmc.json and the raw counter CSVs (only gpurun_out/ comes back
-from the GPU box); they are then committed as profiles/spmv_c4_pmc.json (read by bench.py as
-roofline.traffic) and profiles/<round>/.
+Usage: pmc_traffic.py <round> [csr_stream|sell]. Writes gpurun_out/pmc/spmv_c4_pmc_<fmt>.json
+and the raw counter CSVs (only gpurun_out/ comes back from the GPU box); they are then committed
+as profiles/spmv_c4_pmc_<fmt>.json (read by bench.py as roofline.traffic for the format the
+fine-level autotune chose) and profiles/<round>/.
 """
 import csv
 import glob
@@ -20,16 +21,17 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out", "pmc")
-KERNEL = "k_csr_stream"
+KERNELS = {"csr_stream": "k_csr_stream", "sell": "k_sell"}
 
 
-def run_pass(counter):
-    d = os.path.join(OUT, counter)
+def run_pass(counter, fmt):
+    d = os.path.join(OUT, f"{counter}_{fmt}")
     shutil.rmtree(d, ignore_errors=True)
     os.makedirs(d, exist_ok=True)
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
            sys.executable, os.path.join(ROOT, "tools", "spmv_driver.py")]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    env = dict(os.environ, MLAMG_FMT=fmt)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     if r.returncode != 0:
         raise RuntimeError(f"rocprofv3 failed:\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}")
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
@@ -39,15 +41,16 @@ def run_pass(counter):
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                if KERNELS[fmt] in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     return vals, files
 
 
 def main():
     round_tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    fetch, f1 = run_pass("FETCH_SIZE")
-    write, f2 = run_pass("WRITE_SIZE")
+    fmt = sys.argv[2] if len(sys.argv) > 2 else "sell"
+    fetch, f1 = run_pass("FETCH_SIZE", fmt)
+    write, f2 = run_pass("WRITE_SIZE", fmt)
     if not fetch or not write:
         raise RuntimeError("no dispatches of the SpMV kernel found in the counter CSVs")
     # skip the first (cold) dispatch
@@ -61,7 +64,8 @@ def main():
     nnz = 70263936
     algo = 12.0 * nnz + 4.0 * (n + 1) + 8.0 * n + 8.0 * n
     res = {
-        "kernel": "k_csr_stream<EPI_AXPBY> (fine-level SpMV, C4 216^3)",
+        "kernel": f"{KERNELS[fmt]}<EPI_AXPBY> (fine-level SpMV, C4 216^3, format {fmt})",
+        "format": fmt,
         "fetch_size_kib_median": fetch_kib,
         "write_size_kib_median": write_kib,
         "correction": "reads = 2 x FETCH_SIZE (gfx950 wide-read under-count), writes = WRITE_SIZE",
@@ -72,10 +76,10 @@ def main():
         "traffic_over_algorithmic": (read_bytes + write_bytes) / algo,
         "dispatches": len(fetch),
     }
-    with open(os.path.join(OUT, "spmv_c4_pmc.json"), "w") as fh:
+    with open(os.path.join(OUT, f"spmv_c4_pmc_{fmt}.json"), "w") as fh:
         json.dump(res, fh, indent=1)
     for f, tag in ((f1[0], "FETCH_SIZE"), (f2[0], "WRITE_SIZE")):
-        shutil.copy(f, os.path.join(OUT, f"spmv_c4_pmc_{tag}_{round_tag}.csv"))
+        shutil.copy(f, os.path.join(OUT, f"spmv_c4_pmc_{fmt}_{tag}_{round_tag}.csv"))
     print(json.dumps(res, indent=1))
 
 

@@ -15,13 +15,14 @@ def main():
 
     n1 = int(os.environ.get("MLAMG_N", "216"))
     reps = int(os.environ.get("MLAMG_REPS", "20"))
-    A = DeviceCSR.from_scipy(problems.poisson_3d_7pt(n1), check=False)
+    fmt = os.environ.get("MLAMG_FMT", "auto_exact")  # bench.py's autotune picks sell for C4
+    A = DeviceCSR.from_scipy(problems.poisson_3d_7pt(n1), check=False).set_format(fmt)
     x = torch.randn(A.shape[1], dtype=torch.float64, device="cuda")
     y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
     for _ in range(reps):
         A.matvec(x, out=y)
     torch.cuda.synchronize()
-    print(f"spmv_driver: n={A.shape[0]} nnz={A.nnz} reps={reps}")
+    print(f"spmv_driver: n={A.shape[0]} nnz={A.nnz} reps={reps} format={A.get_format()}")
 
 
 if __name__ == "__main__":
