@@ -74,11 +74,17 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
  *   VECTOR      vec_width lanes per row (0 = auto from the mean row length), lane-strided
  *               partial sums + xor butterfly: a different, fixed order (oracle vec_matvec),
  *               for long-row coarse operators that have no scipy counterpart
- *   AUTO_EXACT  SELL when its padding costs <= 15% extra entries, else CSR_STREAM */
+ *   AUTO_EXACT  SELL when its padding costs <= 15% extra entries, else CSR_STREAM
+ *   SORTED      CSR_STREAM row blocks (<= 512 rows, <= 4096 nonzeros) whose entries are stored
+ *               in ascending column order with their CSR slot, so the x gathers of a
+ *               wave-instruction hit few cache lines; sums in stored order (scipy's bits).
+ *               EUNSUPPORTED if a row has > 4096 nonzeros or a block's columns do not fit
+ *               two windows of 2^20 columns */
 #define MLAMG_FMT_CSR_STREAM 0
 #define MLAMG_FMT_SELL 1
 #define MLAMG_FMT_VECTOR 2
 #define MLAMG_FMT_AUTO_EXACT 3
+#define MLAMG_FMT_SORTED 4
 int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream);
 int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored_entries);
 

@@ -53,6 +53,12 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 constexpr int kThreads = 256;
 constexpr int kBlockRows = 256;
 constexpr int kBlockNnz = 2048;   // 16 KiB of fp64 products in LDS per workgroup
+// "sorted" format blocks: 512-thread workgroups, 32 KiB of products; 12 slot bits leave 20 bits
+// of column offset, so a block's columns must span < 2^20
+constexpr int kSrtThreads = 512;
+constexpr int kSrtRows = 512;
+constexpr int kSrtNnz = 4096;
+constexpr int kSrtPosBits = 12;
 
 }  // namespace mlamg
 
@@ -83,6 +89,14 @@ struct mlamg_csr {
   // CSR-vector format (lane-strided partial sums + butterfly, NOT scipy's order): 0 = off,
   // else the number of lanes per row (4..64)
   int32_t vec_width = 0;
+  // optional gather-sorted copy ("sorted" format): row blocks of <= kSrtRows rows and
+  // <= kSrtNnz nonzeros whose entries are stored in ascending column order, each packed as
+  // (col - srt_base[block]) << kSrtPosBits | slot (its CSR position inside the block)
+  int32_t srt_nb = 0;
+  int32_t* srt_blk = nullptr;   // srt_nb+1 row boundaries
+  int32_t* srt_base = nullptr;  // per block {lo, hi, split}: column windows of the sorted entries
+  uint32_t* srt_pk = nullptr;
+  double* srt_val = nullptr;
   // number of per-block partial sums a NORM launch writes with the active format
   int32_t n_part = 0;
 };
@@ -97,7 +111,7 @@ namespace mlamg {
 // Upper bound on the per-block partial sums a NORM launch of A can write, whatever format is
 // active (CSR-stream: n_blocks; SELL-64: n/256; CSR-vector: n*VW/256 <= n/4), plus one slot.
 inline int64_t part_capacity(const mlamg_csr* A) {
-  return std::max<int64_t>(A->n_blocks, (A->n_rows + 3) / 4) + 2;
+  return std::max<int64_t>(std::max<int64_t>(A->n_blocks, A->srt_nb), (A->n_rows + 3) / 4) + 2;
 }
 // Allocate device arrays for an (n_rows x n_cols, nnz) CSR and the handle; no partition yet.
 int csr_alloc(int64_t n_rows, int64_t n_cols, int64_t nnz, mlamg_csr** out);

@@ -82,6 +82,10 @@ void csr_free(mlamg_csr* A) {
   if (A->sell_col) (void)hipFree(A->sell_col);
   if (A->sell_val) (void)hipFree(A->sell_val);
   if (A->sell_perm) (void)hipFree(A->sell_perm);
+  if (A->srt_blk) (void)hipFree(A->srt_blk);
+  if (A->srt_base) (void)hipFree(A->srt_base);
+  if (A->srt_pk) (void)hipFree(A->srt_pk);
+  if (A->srt_val) (void)hipFree(A->srt_val);
   delete A;
 }
 

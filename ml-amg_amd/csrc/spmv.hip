@@ -17,6 +17,8 @@
 // extra vector the epilogue reads/writes), SURVEY.md §8(d).
 #include "common.hpp"
 
+#include <rocprim/rocprim.hpp>
+
 namespace mlamg {
 
 enum EpiOp : int { EPI_AXPBY = 0, EPI_RESID = 1, EPI_JACOBI = 2, EPI_JACEXP = 3, EPI_ADD = 4 };
@@ -67,6 +69,14 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs (b % 8 share
+// one L2), so logical block = contiguous chunk per XCD. Neighbouring row blocks then share x
+// lines in the same L2 (7-point stencil: rows i +- 1, +- n, +- n^2). Bijective for any nb.
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+  const int64_t q = nb >> 3, r = nb & 7, g = b & 7, i = b >> 3;
+  return (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + i;
+}
+
 template <int OP, bool NORM>
 __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restrict__ indptr,
                                                          const int32_t* __restrict__ indices,
@@ -77,7 +87,7 @@ __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restri
   __shared__ int32_t rp[kBlockRows + 1];
   __shared__ double red[kThreads / 64];
   if (ep.done && *ep.done) return;
-  const int b = blockIdx.x;
+  const int b = (int)xcd_block(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x;
   const int r0 = blk[b];
   const int r1 = blk[b + 1];
@@ -89,12 +99,35 @@ __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restri
     for (int t = tid; t <= nr; t += kThreads) rp[t] = indptr[r0 + t] - e0;
     const int32_t* ci = indices + e0;
     const double* cv = vals + e0;
-    for (int e = tid; e < ne; e += kThreads) prod[e] = cv[e] * x[ci[e]];
+    // all kBlockNnz/kThreads loads of a lane issued back to back: the x gathers depend on the
+    // index loads, so without the unroll each iteration pays two full memory round trips
+    constexpr int U = kBlockNnz / kThreads;
+    int32_t cc[U];
+    double vv[U], xv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + u * kThreads;
+      cc[u] = e < ne ? __builtin_nontemporal_load(ci + e) : -1;
+      vv[u] = e < ne ? __builtin_nontemporal_load(cv + e) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (tid + u * kThreads < ne) prod[tid + u * kThreads] = vv[u] * xv[u];
     __syncthreads();
     for (int t = tid; t < nr; t += kThreads) {
       double s = 0.0;
       const int ka = rp[t], kb = rp[t + 1];
-      for (int k = ka; k < kb; ++k) s += prod[k];
+      int k = ka;
+      for (; k + 4 <= kb; k += 4) {
+        const double p0 = prod[k], p1 = prod[k + 1], p2 = prod[k + 2], p3 = prod[k + 3];
+        s += p0;
+        s += p1;
+        s += p2;
+        s += p3;
+      }
+      for (; k < kb; ++k) s += prod[k];
       sq += epilogue<OP>(r0 + t, s, ep);
     }
   } else {
@@ -163,7 +196,8 @@ __global__ __launch_bounds__(kThreads) void k_sell(const int64_t* __restrict__ s
                                                    const double* __restrict__ x, Epi ep) {
   __shared__ double red[kThreads / 64];
   if (ep.done && *ep.done) return;
-  const int64_t slice = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t slice = lb * (kThreads / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   double sq = 0.0;
   if (slice < n_slices) {
@@ -203,7 +237,7 @@ __global__ __launch_bounds__(kThreads) void k_sell(const int64_t* __restrict__ s
     if (threadIdx.x == 0) {
       double t = 0.0;
       for (int i = 0; i < kThreads / 64; ++i) t += red[i];
-      ep.partial[blockIdx.x] = t;
+      ep.partial[lb] = t;
     }
   }
 }
@@ -246,6 +280,78 @@ __global__ __launch_bounds__(kThreads) void k_csr_vec(const int32_t* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- gather-sorted CSR-stream
+// Same two phases as k_csr_stream, but each block's nonzeros are stored in ascending column
+// order, packed with their CSR slot: the 64 gathers of one wave-instruction then fall on a few
+// cache lines instead of one per row neighbourhood (the x gather, not HBM, bounds long-row
+// operators: Galerkin A_l, R = P^T). Products are written to LDS at their CSR slot and phase 2
+// sums every row in stored order, so the result is bitwise k_csr_stream's (scipy's).
+template <int OP, bool NORM>
+__global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restrict__ indptr,
+                                                        const uint32_t* __restrict__ pk,
+                                                        const double* __restrict__ av,
+                                                        const int32_t* __restrict__ blk,
+                                                        const int32_t* __restrict__ base,
+                                                        const double* __restrict__ x, Epi ep) {
+  __shared__ double prod[kSrtNnz];
+  __shared__ int32_t rp[kSrtRows + 1];
+  __shared__ double red[kSrtThreads / 64];
+  if (ep.done && *ep.done) return;
+  const int b = (int)xcd_block(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x;
+  const int r0 = blk[b], r1 = blk[b + 1], nr = r1 - r0;
+  const int e0 = indptr[r0];
+  const int ne = indptr[r1] - e0;
+  // two column windows per block: sorted entries [0, split) are offsets from lo, the rest from
+  // hi (a halo-extended local matrix has its ghost columns far from the owned ones)
+  const int lo = base[3 * b], hi = base[3 * b + 1], split = base[3 * b + 2];
+  for (int t = tid; t <= nr; t += kSrtThreads) rp[t] = indptr[r0 + t] - e0;
+  constexpr int U = kSrtNnz / kSrtThreads;
+  constexpr uint32_t kNone = 0xffffffffu, kSlot = (1u << kSrtPosBits) - 1;
+  uint32_t w[U];
+  double vv[U], xv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + u * kSrtThreads;
+    w[u] = e < ne ? __builtin_nontemporal_load(pk + e0 + e) : kNone;
+    vv[u] = e < ne ? __builtin_nontemporal_load(av + e0 + e) : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int cb = tid + u * kSrtThreads < split ? lo : hi;
+    xv[u] = w[u] != kNone ? x[cb + (int)(w[u] >> kSrtPosBits)] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (w[u] != kNone) prod[w[u] & kSlot] = vv[u] * xv[u];
+  __syncthreads();
+  double sq = 0.0;
+  for (int t = tid; t < nr; t += kSrtThreads) {
+    double s = 0.0;
+    const int ka = rp[t], kb = rp[t + 1];
+    int k = ka;
+    for (; k + 4 <= kb; k += 4) {
+      const double p0 = prod[k], p1 = prod[k + 1], p2 = prod[k + 2], p3 = prod[k + 3];
+      s += p0;
+      s += p1;
+      s += p2;
+      s += p3;
+    }
+    for (; k < kb; ++k) s += prod[k];
+    sq += epilogue<OP>(r0 + t, s, ep);
+  }
+  if constexpr (NORM) {
+    double v = wave_sum(sq);
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+      for (int i = 0; i < kSrtThreads / 64; ++i) t += red[i];
+      ep.partial[b] = t;
+    }
+  }
+}
+
 template <int OP, bool NORM, int VW>
 static int launch_vec_w(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   const int64_t threads = A->n_rows * VW;
@@ -272,6 +378,13 @@ static int launch_vec(const mlamg_csr* A, const double* x, const Epi& ep, hipStr
 template <int OP, bool NORM>
 static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   if (A->vec_width) return launch_vec<OP, NORM>(A, x, ep, s);
+  if (A->srt_pk) {
+    if (A->srt_nb == 0) return MLAMG_OK;
+    hipLaunchKernelGGL((k_sorted<OP, NORM>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s, A->indptr,
+                       A->srt_pk, A->srt_val, A->srt_blk, A->srt_base, x, ep);
+    MLAMG_HIP(hipGetLastError());
+    return MLAMG_OK;
+  }
   if (A->sell_ptr) {
     if (A->n_slices == 0) return MLAMG_OK;
     const unsigned nb = (unsigned)((A->n_slices + kThreads / 64 - 1) / (kThreads / 64));
@@ -375,6 +488,176 @@ int build_sell(mlamg_csr* A, hipStream_t s, int sigma) {
   A->sell_elems = total;
   A->sell_sigma = std::max(sigma, 1);
   A->n_part = (int32_t)std::max<int64_t>(1, (ns + 3) / 4);
+  return MLAMG_OK;
+}
+
+// ---------------------------------------------------------------- sorted-format construction
+__global__ void k_srt_keys(const int32_t* __restrict__ ip, const int32_t* __restrict__ ij,
+                           const int32_t* __restrict__ blk, int cbits, uint64_t* __restrict__ key,
+                           int32_t* __restrict__ idx) {
+  const int b = blockIdx.x;
+  const int a = ip[blk[b]], z = ip[blk[b + 1]];
+  for (int e = a + (int)threadIdx.x; e < z; e += blockDim.x) {
+    key[e] = ((uint64_t)b << cbits) | (uint32_t)ij[e];
+    idx[e] = e;
+  }
+}
+
+// One workgroup per block over its column-sorted entries: a single window [lo, lo + 2^20) if
+// the columns fit, else split at the widest gap between consecutive columns into two windows
+// (each must fit); otherwise the block is too wide and the format is refused.
+__global__ __launch_bounds__(256) void k_srt_pack(const int32_t* __restrict__ ip,
+                                                  const double* __restrict__ ax,
+                                                  const int32_t* __restrict__ blk,
+                                                  const uint64_t* __restrict__ key,
+                                                  const int32_t* __restrict__ idx, uint64_t cmask,
+                                                  int32_t* __restrict__ base,
+                                                  uint32_t* __restrict__ pk,
+                                                  double* __restrict__ av,
+                                                  int32_t* __restrict__ too_wide) {
+  __shared__ int64_t best[256];
+  const int b = blockIdx.x;
+  const int a = ip[blk[b]], z = ip[blk[b + 1]];
+  const int m = z - a;
+  if (m == 0) {
+    if (threadIdx.x == 0) base[3 * b] = base[3 * b + 1] = base[3 * b + 2] = 0;
+    return;
+  }
+  auto col = [&](int e) { return (int64_t)(key[a + e] & cmask); };
+  const int64_t span = int64_t(1) << (32 - kSrtPosBits);
+  int split = m;
+  if (col(m - 1) - col(0) >= span) {
+    // argmax gap (gap << 32 | position, max picks the widest, ties the last)
+    int64_t bv = -1;
+    for (int e = 1 + (int)threadIdx.x; e < m; e += 256) {
+      const int64_t g = ((col(e) - col(e - 1)) << 32) | e;
+      bv = g > bv ? g : bv;
+    }
+    best[threadIdx.x] = bv;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o && best[threadIdx.x + o] > best[threadIdx.x])
+        best[threadIdx.x] = best[threadIdx.x + o];
+      __syncthreads();
+    }
+    split = (int)(best[0] & 0xffffffff);
+    if (col(split - 1) - col(0) >= span || col(m - 1) - col(split) >= span) {
+      if (threadIdx.x == 0) atomicAdd(too_wide, 1);
+      return;
+    }
+  }
+  const int lo = (int)col(0), hi = split < m ? (int)col(split) : lo;
+  if (threadIdx.x == 0) {
+    base[3 * b] = lo;
+    base[3 * b + 1] = hi;
+    base[3 * b + 2] = split;
+  }
+  for (int e = (int)threadIdx.x; e < m; e += 256) {
+    const int src = idx[a + e];
+    const int c = (int)col(e) - (e < split ? lo : hi);
+    pk[a + e] = ((uint32_t)c << kSrtPosBits) | (uint32_t)(src - a);
+    av[a + e] = ax[src];
+  }
+}
+
+static void drop_sorted(mlamg_csr* A) {
+  if (A->srt_blk) (void)hipFree(A->srt_blk);
+  if (A->srt_base) (void)hipFree(A->srt_base);
+  if (A->srt_pk) (void)hipFree(A->srt_pk);
+  if (A->srt_val) (void)hipFree(A->srt_val);
+  A->srt_blk = nullptr;
+  A->srt_base = nullptr;
+  A->srt_pk = nullptr;
+  A->srt_val = nullptr;
+  A->srt_nb = 0;
+  if (!A->sell_ptr && !A->vec_width) A->n_part = A->n_blocks;
+}
+
+// Row blocks of <= kSrtRows rows / <= kSrtNnz nonzeros; inside each, entries radix-sorted by
+// (block, column) (stable, so equal columns keep CSR order; any order would give the same bits).
+// EUNSUPPORTED (A unchanged) if a row is longer than kSrtNnz or a block's columns do not fit
+// two windows of 2^20.
+static int build_sorted(mlamg_csr* A, hipStream_t s) {
+  drop_sorted(A);
+  const int64_t n = A->n_rows, nnz = A->nnz;
+  std::vector<int32_t> ip(n + 1);
+  MLAMG_HIP(hipMemcpyAsync(ip.data(), A->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  std::vector<int32_t> blk{0};
+  for (int64_t r = 0; r < n;) {
+    int64_t e = r;
+    while (e < n && e - r < kSrtRows && ip[e + 1] - ip[r] <= kSrtNnz) ++e;
+    if (e == r) {
+      set_error("sorted format: a row has more than 4096 nonzeros");
+      return MLAMG_EUNSUPPORTED;
+    }
+    blk.push_back((int32_t)e);
+    r = e;
+  }
+  const int nb = (int)blk.size() - 1;
+  int cbits = 1;
+  while ((int64_t(1) << cbits) < std::max<int64_t>(A->n_cols, 2)) ++cbits;
+  int bbits = 1;
+  while ((int64_t(1) << bbits) < std::max(nb, 2)) ++bbits;
+  MLAMG_REQUIRE(cbits + bbits <= 64, "sorted format: key does not fit 64 bits");
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  int32_t *i0 = nullptr, *i1 = nullptr, *wide = nullptr;
+  void* tmp = nullptr;
+  int rc = MLAMG_OK;
+  auto fail = [&](const char* what) {
+    if (rc == MLAMG_OK) {
+      set_error(std::string("sorted format: ") + what);
+      rc = MLAMG_ENOMEM;
+    }
+  };
+  const size_t m = (size_t)std::max<int64_t>(nnz, 1);
+  if (hipMalloc(&A->srt_blk, sizeof(int32_t) * (nb + 1)) != hipSuccess ||
+      hipMalloc(&A->srt_base, sizeof(int32_t) * 3 * std::max(nb, 1)) != hipSuccess ||
+      hipMalloc(&A->srt_pk, sizeof(uint32_t) * m) != hipSuccess ||
+      hipMalloc(&A->srt_val, sizeof(double) * m) != hipSuccess ||
+      hipMalloc(&k0, sizeof(uint64_t) * m) != hipSuccess ||
+      hipMalloc(&k1, sizeof(uint64_t) * m) != hipSuccess ||
+      hipMalloc(&i0, sizeof(int32_t) * m) != hipSuccess ||
+      hipMalloc(&i1, sizeof(int32_t) * m) != hipSuccess ||
+      hipMalloc(&wide, sizeof(int32_t)) != hipSuccess)
+    fail("out of device memory");
+  if (rc == MLAMG_OK &&
+      (hipMemcpyAsync(A->srt_blk, blk.data(), sizeof(int32_t) * (nb + 1), hipMemcpyHostToDevice,
+                      s) != hipSuccess ||
+       hipMemsetAsync(wide, 0, sizeof(int32_t), s) != hipSuccess))
+    fail("upload");
+  if (rc == MLAMG_OK && nb > 0 && nnz > 0) {
+    hipLaunchKernelGGL(k_srt_keys, dim3(nb), dim3(256), 0, s, A->indptr, A->indices, A->srt_blk,
+                       cbits, k0, i0);
+    size_t tb = 0;
+    hipError_t e = rocprim::radix_sort_pairs(nullptr, tb, k0, k1, i0, i1, (size_t)nnz, 0,
+                                             cbits + bbits, s);
+    if (e == hipSuccess) e = hipMalloc(&tmp, tb + 16);
+    if (e == hipSuccess)
+      e = rocprim::radix_sort_pairs(tmp, tb, k0, k1, i0, i1, (size_t)nnz, 0, cbits + bbits, s);
+    if (e != hipSuccess) fail("radix sort");
+    if (rc == MLAMG_OK)
+      hipLaunchKernelGGL(k_srt_pack, dim3(nb), dim3(256), 0, s, A->indptr, A->data, A->srt_blk, k1,
+                         i1, (uint64_t(1) << cbits) - 1, A->srt_base, A->srt_pk, A->srt_val, wide);
+  }
+  int32_t too_wide = 0;
+  if (rc == MLAMG_OK &&
+      (hipGetLastError() != hipSuccess ||
+       hipMemcpyAsync(&too_wide, wide, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess))
+    fail("kernel launch");
+  for (void* p : {(void*)k0, (void*)k1, (void*)i0, (void*)i1, (void*)wide, tmp})
+    if (p) (void)hipFree(p);
+  if (rc == MLAMG_OK && too_wide) {
+    set_error("sorted format: a block's columns do not fit two windows of 2^20");
+    rc = MLAMG_EUNSUPPORTED;
+  }
+  if (rc != MLAMG_OK) {
+    drop_sorted(A);
+    return rc;
+  }
+  A->srt_nb = nb;
+  A->n_part = nb;
   return MLAMG_OK;
 }
 
@@ -521,13 +804,24 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
   switch (fmt) {
     case MLAMG_FMT_CSR_STREAM:
       drop_sell(A);
+      drop_sorted(A);
       A->vec_width = 0;
       return MLAMG_OK;
     case MLAMG_FMT_SELL:
       A->vec_width = 0;
+      drop_sorted(A);
       return build_sell(A, s, vec_width > 1 ? vec_width : 1);  // vec_width doubles as sigma
+    case MLAMG_FMT_SORTED: {
+      // built first, so an unsupported matrix keeps its current format
+      MLAMG_TRY(build_sorted(A, s));
+      drop_sell(A);
+      A->vec_width = 0;
+      A->n_part = A->srt_nb;
+      return MLAMG_OK;
+    }
     case MLAMG_FMT_VECTOR: {
       drop_sell(A);
+      drop_sorted(A);
       int vw = vec_width;
       if (vw == 0) {
         vw = 4;
@@ -544,6 +838,7 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       // SELL-64-sigma (rows sorted by length inside windows of 512) if that does, else
       // CSR-stream
       A->vec_width = 0;
+      drop_sorted(A);
       MLAMG_TRY(build_sell(A, s, 1));
       if (A->nnz > 0 && (double)A->sell_elems <= 1.15 * (double)A->nnz) return MLAMG_OK;
       MLAMG_TRY(build_sell(A, s, 512));
@@ -559,9 +854,12 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
 
 int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored) {
   MLAMG_REQUIRE(A, "NULL argument");
-  const int f = A->vec_width ? MLAMG_FMT_VECTOR : (A->sell_ptr ? MLAMG_FMT_SELL : MLAMG_FMT_CSR_STREAM);
+  const int f = A->vec_width ? MLAMG_FMT_VECTOR
+                : A->srt_pk   ? MLAMG_FMT_SORTED
+                : A->sell_ptr ? MLAMG_FMT_SELL
+                              : MLAMG_FMT_CSR_STREAM;
   if (fmt) *fmt = f;
-  if (vec_width) *vec_width = A->vec_width ? A->vec_width : A->sell_sigma;
+  if (vec_width) *vec_width = A->vec_width ? A->vec_width : (A->srt_pk ? 0 : A->sell_sigma);
   if (stored) *stored = A->sell_ptr ? A->sell_elems : A->nnz;
   return MLAMG_OK;
 }

@@ -113,7 +113,12 @@ class DistributedHierarchy:
 
         def like(M_glob, M_loc):  # the kernel H chose for the global operator
             fmt, arg, _ = M_glob.get_format()
-            return M_loc.set_format(fmt, arg)
+            try:
+                return M_loc.set_format(fmt, arg)
+            except _lib.MlamgError as e:  # e.g. sorted: ghost columns too far from owned
+                if e.code != _lib.MLAMG_EUNSUPPORTED:
+                    raise
+                return M_loc.set_format("csr_stream")  # same summation order
 
         self._keep = []
         last = parts[-1]

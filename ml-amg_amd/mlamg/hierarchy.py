@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import call, ptr, stream_ptr
+from ._lib import MLAMG_EUNSUPPORTED, MlamgError, call, ptr, stream_ptr
 from .graph import aggregate_op_device, bellman_ford_device, labels_to_columns, lloyd_cluster_device
 from .multigrid import lambda_max_dinv_a
 from .sparse import DeviceCSR, _device, as_device, galerkin, to_device_vec
@@ -81,7 +81,7 @@ class Hierarchy:
         H._finalize(nu_pre, nu_post)
         return H
 
-    EXACT_CANDIDATES = (("csr_stream", 0), ("sell", 1), ("sell", 512))
+    EXACT_CANDIDATES = (("csr_stream", 0), ("sell", 1), ("sell", 512), ("sorted", 0))
     VECTOR_CANDIDATES = (("vector", 8), ("vector", 16), ("vector", 32), ("vector", 64))
 
     @staticmethod
@@ -101,8 +101,8 @@ class Hierarchy:
         """Choose the SpMV kernel of every operator.
 
         Level-0 operators (A0, P0, R0: the ones with a scipy counterpart in the reference
-        cycle) always keep scipy's summation order: CSR-stream, SELL-64 or SELL-64-sigma, all
-        bitwise scipy. Coarser levels (the multilevel extension, no reference counterpart) may
+        cycle) always keep scipy's summation order: CSR-stream, SELL-64, SELL-64-sigma or
+        gather-sorted CSR-stream, all bitwise scipy. Coarser levels (the multilevel extension, no reference counterpart) may
         also use the CSR-vector kernel for A_l and R_l when coarse_format='vector' and their
         mean row length is >= vec_min_row; its fixed order is restated by the oracle.
         fine_format='autotune' times every admissible kernel on each operator once and keeps
@@ -124,7 +124,11 @@ class Hierarchy:
                 y = torch.empty(M.shape[0], dtype=torch.float64, device=dev)
                 times = {}
                 for fmt, arg in cands:
-                    times[f"{fmt}/{arg}"] = self._time_format(M, fmt, arg, x, y)
+                    try:
+                        times[f"{fmt}/{arg}"] = self._time_format(M, fmt, arg, x, y)
+                    except MlamgError as e:  # format limits (e.g. sorted: row > 4096 nnz)
+                        if e.code != MLAMG_EUNSUPPORTED:
+                            raise
                 best = min(times, key=times.get)
                 fmt, arg = best.split("/")
                 M.set_format(fmt, int(arg))

@@ -134,10 +134,10 @@ class DeviceCSR:
             return self.matvec(other)
         return NotImplemented
 
-    FORMATS = {"csr_stream": 0, "sell": 1, "vector": 2, "auto_exact": 3}
+    FORMATS = {"csr_stream": 0, "sell": 1, "vector": 2, "auto_exact": 3, "sorted": 4}
 
     def set_format(self, fmt, vec_width=0):
-        """SpMV kernel/storage: 'csr_stream' | 'sell' | 'auto_exact' (scipy summation order)
+        """SpMV kernel/storage: 'csr_stream' | 'sell' | 'sorted' | 'auto_exact' (scipy order)
         or 'vector' (lane-strided order, see include/mlamg.h)."""
         call("mlamg_csr_set_format", self.handle, self.FORMATS[fmt], int(vec_width), stream_ptr())
         return self

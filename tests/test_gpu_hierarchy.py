@@ -32,7 +32,7 @@ def dev(torch, x):
 
 
 @pytest.mark.parametrize("k", MATS)
-@pytest.mark.parametrize("fmt", ("sell", "csr_stream", "auto_exact"))
+@pytest.mark.parametrize("fmt", ("sell", "csr_stream", "auto_exact", "sorted"))
 def test_exact_formats_bitwise(golden, ml, torch_cuda, k, fmt):
     torch = torch_cuda
     A = golden_csr(golden, k)
@@ -86,6 +86,56 @@ def test_sell_ragged_rows(ml, torch_cuda):
         ref = b.cpu().numpy() - A @ x
         assert np.array_equal(r.cpu().numpy(), ref)
         assert abs(nrm.item() - np.linalg.norm(ref)) <= 1e-13 * np.linalg.norm(ref)
+
+
+def test_sorted_format_ragged_and_limits(ml, torch_cuda):
+    """sorted format: bitwise CSR order on ragged rows (empty rows, rows spanning several
+    blocks' worth of columns), and EUNSUPPORTED (format unchanged) past its limits."""
+    torch = torch_cuda
+    from mlamg._lib import MlamgError, call, ptr, stream_ptr
+    rs = np.random.RandomState(5)
+    n, m = 3000, 200000
+    lens = rs.randint(0, 300, n)
+    lens[::37] = 0
+    lens[5] = 4096  # exactly one full block
+    indptr = np.concatenate([[0], np.cumsum(lens)])
+    indices = np.concatenate([np.sort(rs.choice(m, l, replace=False)) for l in lens])
+    A = sp.csr_matrix((rs.randn(indptr[-1]), indices, indptr), shape=(n, m))
+    x = rs.randn(m)
+    Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("sorted")
+    assert Ad.get_format()[0] == "sorted"
+    assert np.array_equal(Ad.matvec(dev(torch, x)).cpu().numpy(), A @ x)
+    Sq = (sp.random(n, n, density=0.01, random_state=rs, format="csr")
+          + sp.eye(n, format="csr")).tocsr()
+    Sq.sort_indices()
+    Sd = ml.sparse.DeviceCSR.from_scipy(Sq).set_format("sorted")
+    xs, b = rs.randn(n), rs.randn(n)
+    r = torch.empty(n, dtype=torch.float64, device="cuda")
+    nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
+    call("mlamg_residual", Sd.handle, ptr(dev(torch, b)), ptr(dev(torch, xs)), ptr(r), ptr(nrm),
+         stream_ptr())
+    ref = b - Sq @ xs
+    assert np.array_equal(r.cpu().numpy(), ref)
+    assert abs(nrm.item() - np.linalg.norm(ref)) <= 1e-13 * np.linalg.norm(ref)
+    # a row longer than one block
+    L = sp.csr_matrix((np.ones(5000), np.arange(5000), [0, 5000]), shape=(1, 5000))
+    Ld = ml.sparse.DeviceCSR.from_scipy(L).set_format("sell")
+    with pytest.raises(MlamgError):
+        Ld.set_format("sorted")
+    assert Ld.get_format()[0] == "sell"
+    # a block whose columns need two windows (owned | far ghosts) is supported ...
+    mw = (1 << 21) + 11
+    xw = rs.randn(mw)
+    W = sp.csr_matrix((rs.randn(4), [0, 7, 1 << 20, (1 << 20) + 3], [0, 2, 4]), shape=(2, mw))
+    Wd = ml.sparse.DeviceCSR.from_scipy(W).set_format("sorted")
+    assert np.array_equal(Wd.matvec(dev(torch, xw)).cpu().numpy(), W @ xw)
+    # ... three far-apart clusters are not
+    W3 = sp.csr_matrix((np.ones(3), [0, (1 << 20) + 5, (1 << 21) + 10], [0, 3]), shape=(1, mw))
+    W3d = ml.sparse.DeviceCSR.from_scipy(W3)
+    with pytest.raises(MlamgError):
+        W3d.set_format("sorted")
+    assert W3d.get_format()[0] == "csr_stream"
+    assert np.array_equal(W3d.matvec(dev(torch, xw)).cpu().numpy(), W3 @ xw)
 
 
 def _oracle_levels_from_device(H):
