@@ -69,29 +69,11 @@ int halo_exchange_impl(mlamg_halo* h, double* x_ext, hipStream_t s) {
   return MLAMG_OK;
 }
 
-// declared in other TUs
-int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
-                  double* hist, int32_t* counter, int32_t* done, double tol, double* copy_to,
-                  const double* copy_from, double* partial, hipStream_t s);
-int jacobi_sweep(const mlamg_csr* A, const double* dinv, const double* b, const double* xin,
-                 double* xout, bool explicit_form, const int32_t* done, hipStream_t s);
-int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
-int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
-int jacobi_from_residual(double* x, const double* dinv, const double* r, int64_t n,
-                         const int32_t* done, hipStream_t s);
-int jacobi_from_zero(double* x, const double* dinv, const double* b, int64_t n,
-                     const int32_t* done, hipStream_t s);
-int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
-                      hipStream_t s);
-int residual_partials(const mlamg_csr* A, const double* b, const double* x, double* r,
-                      double* copy_to, const double* copy_from, double* partial,
-                      const int32_t* done, hipStream_t s);
-
 // sum the residual partials of this rank into partial[n] (fixed order)
 __global__ __launch_bounds__(1024) void k_local_sum(double* __restrict__ partial, int n) {
   __shared__ double red[16];
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 1024) s += partial[i];
+  s = strided_sum(partial, n, threadIdx.x, 1024);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;

@@ -108,6 +108,26 @@ struct mlamg_dense {
 };
 
 namespace mlamg {
+// s = p[start] + p[start+step] + ... in that order (bitwise a plain strided loop), with the loads
+// issued 8 at a time: a one-workgroup reduction over tens of thousands of partials is otherwise
+// a chain of dependent memory round trips.
+__device__ __forceinline__ double strided_sum(const double* __restrict__ p, int n, int start,
+                                              int step) {
+  double s = 0.0;
+  int i = start;
+  for (; i + 7 * step < n; i += 8 * step) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[i + u * step];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; i < n; i += step) s += p[i];
+  return s;
+}
+}  // namespace mlamg
+
+namespace mlamg {
 // Upper bound on the per-block partial sums a NORM launch of A can write, whatever format is
 // active (CSR-stream: n_blocks; SELL-64: n/256; CSR-vector: n*VW/256 <= n/4), plus one slot.
 inline int64_t part_capacity(const mlamg_csr* A) {
@@ -132,6 +152,26 @@ int launch_spmv_plain(const mlamg_csr* A, const double* x, double* y, hipStream_
 int exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s);  // out[n] = total
 int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, hipStream_t s);
 // entries of a[0..n) outside [lo, hi) (device check before any kernel indexes with them); syncs
+// V-cycle building blocks (spmv.hip, vec.hip, dense.hip, hier.hip), shared by the executors
+int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
+                  double* hist, int32_t* counter, int32_t* done, double tol, double* copy_to,
+                  const double* copy_from, double* partial, hipStream_t s,
+                  const double* smooth_dinv = nullptr);
+int residual_partials(const mlamg_csr* A, const double* b, const double* x, double* r,
+                      double* copy_to, const double* copy_from, double* partial,
+                      const int32_t* done, hipStream_t s, const double* smooth_dinv = nullptr);
+int jacobi_sweep(const mlamg_csr* A, const double* dinv, const double* b, const double* xin,
+                 double* xout, bool explicit_form, const int32_t* done, hipStream_t s);
+int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
+int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
+int jacobi_from_residual(double* x, const double* dinv, const double* r, int64_t n,
+                         const int32_t* done, hipStream_t s);
+int jacobi_from_zero(double* x, const double* dinv, const double* b, int64_t n,
+                     const int32_t* done, hipStream_t s);
+int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int32_t* done,
+                     hipStream_t s);
+int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
+                      hipStream_t s);
 int count_out_of_range(const int32_t* a, int64_t n, int64_t lo, int64_t hi, hipStream_t s,
                        int64_t* bad_out);
 }  // namespace mlamg

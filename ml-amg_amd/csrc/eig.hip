@@ -77,7 +77,7 @@ __global__ __launch_bounds__(1024) void k_reduce_to(const double* __restrict__ p
                                                     double* __restrict__ out, int take_sqrt) {
   __shared__ double red[16];
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 1024) s += partial[i];
+  s = strided_sum(partial, n, threadIdx.x, 1024);
   s = wsum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();

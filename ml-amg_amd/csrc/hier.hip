@@ -17,22 +17,6 @@
 
 #include <hip/hip_runtime.h>
 
-namespace mlamg {
-int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
-                  double* hist, int32_t* counter, int32_t* done, double tol, double* copy_to,
-                  const double* copy_from, double* partial, hipStream_t s);
-int jacobi_sweep(const mlamg_csr* A, const double* dinv, const double* b, const double* xin,
-                 double* xout, bool explicit_form, const int32_t* done, hipStream_t s);
-int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
-int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
-int jacobi_from_residual(double* x, const double* dinv, const double* r, int64_t n,
-                         const int32_t* done, hipStream_t s);
-int jacobi_from_zero(double* x, const double* dinv, const double* b, int64_t n,
-                     const int32_t* done, hipStream_t s);
-int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int32_t* done,
-                     hipStream_t s);
-}  // namespace mlamg
-
 namespace {
 struct Level {
   const mlamg_csr* A = nullptr;
@@ -179,7 +163,17 @@ static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, 
   return MLAMG_OK;
 }
 
-// one finest-level cycle; requires L0.r == b - A x on entry, leaves it so on exit
+// Fused mode (nu_pre >= 1, odd nu_post, so the cycle's result t lands in L0.tmp): the
+// end-of-cycle residual kernel r = b - A t also writes x = t + Dinv_w r, i.e. the NEXT cycle's
+// first pre-smoothing sweep (same roundings), and the cycle starts from that. The caller applies
+// the very first sweep before the first cycle and copies t back into x after the last one (t is
+// still in tmp even when the tolerance flag stopped later cycles). Saves one pass over x, d, r.
+static bool fused_presmooth(const mlamg_hier* H) {
+  return !H->lv.empty() && H->nu_pre >= 1 && (H->nu_post & 1);
+}
+
+// one finest-level cycle; requires L0.r == b - A x on entry, leaves it so on exit (fused mode:
+// x on entry is already pre-smoothed once, and on exit t is in L0.tmp, x = t + Dinv_w r)
 static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, double tol,
                      hipStream_t s) {
   int32_t* counter = H->flags;
@@ -189,10 +183,11 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
     return MLAMG_OK;
   }
   Level& L = H->lv[0];
+  const bool fused = fused_presmooth(H);
   double* cur = x;
   double* other = L.tmp;
   if (H->nu_pre > 0) {
-    MLAMG_TRY(jacobi_from_residual(cur, L.dinv, L.r, L.n, done, s));
+    if (!fused) MLAMG_TRY(jacobi_from_residual(cur, L.dinv, L.r, L.n, done, s));
     MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre - 1, done, s));
     MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, done, 0.0, nullptr,
                             nullptr, nullptr, s));
@@ -206,7 +201,8 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
   MLAMG_TRY(smooth(L, b, cur, other, H->nu_post, done, s));
   // end-of-cycle residual + norm (+ copy the iterate back into x when it sits in tmp)
   MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, hist, counter, done, tol,
-                          cur != x ? x : nullptr, cur != x ? cur : nullptr, H->partial, s));
+                          cur != x ? x : nullptr, cur != x ? cur : nullptr, H->partial, s,
+                          fused ? L.dinv : nullptr));
   return MLAMG_OK;
 }
 
@@ -308,11 +304,13 @@ int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, d
   MLAMG_TRY(hier_prepare(H));
   hipStream_t s = S(stream);
   MLAMG_HIP(hipMemsetAsync(H->flags, 0, 2 * sizeof(int32_t), s));
+  const bool fused = fused_presmooth(H) && n_cycles > 0;
   if (!H->lv.empty()) {
     Level& L = H->lv[0];
     // r = b - A x for the first cycle's pre-smoothing sweep
     MLAMG_TRY(residual_impl(L.A, b, x, L.r, nullptr, nullptr, nullptr, nullptr, 0.0, nullptr,
                             nullptr, nullptr, s));
+    if (fused) MLAMG_TRY(jacobi_from_residual(x, L.dinv, L.r, L.n, nullptr, s));
   }
   if (use_graph && n_cycles > 0 && !H->lv.empty()) {
     if (!(H->exec && H->g_b == b && H->g_x == x && H->g_hist == res_hist && H->g_tol == tol &&
@@ -340,6 +338,9 @@ int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, d
   } else {
     for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(cycle_top(H, b, x, res_hist, tol, s));
   }
+  if (fused)  // the iterate is t (in tmp); x holds t + Dinv_w r for a cycle that never ran
+    MLAMG_HIP(hipMemcpyAsync(x, H->lv[0].tmp, sizeof(double) * H->lv[0].n,
+                             hipMemcpyDeviceToDevice, s));
   MLAMG_HIP(hipGetLastError());
   if (cycles_done_host) {
     int32_t cnt = 0;
@@ -362,14 +363,16 @@ int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes) {
     const double n = (double)L.n;
     const double jac = spmv_bytes(L.A) + 16.0 * n;  // + b, dinv
     const double res = spmv_bytes(L.A) + 8.0 * n;   // + b
+    const bool fused = l == 0 && fused_presmooth(H);
     if (H->nu_pre > 0) {
-      t += (l == 0) ? 32.0 * n : 24.0 * n;  // first sweep: elementwise
+      if (!fused) t += (l == 0) ? 32.0 * n : 24.0 * n;  // first sweep: elementwise
       t += (H->nu_pre - 1) * jac + res;
     }
     t += spmv_bytes(L.R);
     t += spmv_bytes(L.P) + 8.0 * n;  // + read x before the add
     t += H->nu_post * jac;
-    if (l == 0) t += res;  // end-of-cycle residual norm
+    // end-of-cycle residual norm, + x = t (read t, write x) or, fused, x = t + Dinv_w r
+    if (l == 0) t += res + (fused ? 24.0 * n : ((H->nu_post & 1) ? 16.0 * n : 0.0));
   }
   if (H->D) t += 8.0 * H->D->n * H->D->n + 16.0 * H->D->n;
   *bytes = t;

@@ -35,32 +35,66 @@ struct Epi {
   const int32_t* done; // nullable: device flag; nonzero -> kernel is a no-op
 };
 
+// The per-row operands an epilogue reads, fetched apart from the store so kernels can issue
+// these loads at the start (before the nonzero stream) and keep their latency off the tail.
+struct EpiIn {
+  double a = 0.0, b = 0.0, c = 0.0;
+};
+
 template <int OP>
-__device__ __forceinline__ double epilogue(int row, double s, const Epi& e) {
+__device__ __forceinline__ EpiIn epi_load(int row, const Epi& e) {
+  EpiIn v;
+  if constexpr (OP == EPI_AXPBY) {
+    if (e.beta != 0.0) v.a = e.y[row];
+  } else if constexpr (OP == EPI_RESID) {
+    v.a = e.b[row];
+    if (e.copy_to) {
+      v.b = e.copy_from[row];
+      if (e.dinv) v.c = e.dinv[row];
+    }
+  } else if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) {
+    v.a = e.b[row];
+    v.b = e.xin[row];
+    v.c = e.dinv[row];
+  } else {  // EPI_ADD
+    v.a = e.y[row];
+  }
+  return v;
+}
+
+template <int OP>
+__device__ __forceinline__ double epi_store(int row, double s, const EpiIn& v, const Epi& e) {
   if constexpr (OP == EPI_AXPBY) {
     if (e.beta == 0.0) {
       e.y[row] = (e.alpha == 1.0) ? s : e.alpha * s;
     } else {
-      e.y[row] = e.alpha * s + e.beta * e.y[row];
+      e.y[row] = e.alpha * s + e.beta * v.a;
     }
     return 0.0;
   } else if constexpr (OP == EPI_RESID) {
-    const double r = e.b[row] - s;
+    const double r = v.a - s;
     e.y[row] = r;
-    if (e.copy_to) e.copy_to[row] = e.copy_from[row];
+    // optional copy-back of the iterate; with dinv also the next cycle's first Jacobi sweep
+    // x + dinv*r, fused here (same two roundings as the stand-alone sweep)
+    if (e.copy_to) e.copy_to[row] = e.dinv ? v.b + v.c * r : v.b;
     return r * r;
   } else if constexpr (OP == EPI_JACOBI) {
-    const double r = e.b[row] - s;
-    e.y[row] = e.xin[row] + e.dinv[row] * r;
+    const double r = v.a - s;
+    e.y[row] = v.b + v.c * r;
     return 0.0;
   } else if constexpr (OP == EPI_JACEXP) {
-    const double t1 = e.dinv[row] * e.b[row];
-    e.y[row] = e.xin[row] + (t1 - s);
+    const double t1 = v.c * v.a;
+    e.y[row] = v.b + (t1 - s);
     return 0.0;
   } else {  // EPI_ADD
-    e.y[row] = e.y[row] + s;
+    e.y[row] = v.a + s;
     return 0.0;
   }
+}
+
+template <int OP>
+__device__ __forceinline__ double epilogue(int row, double s, const Epi& e) {
+  return epi_store<OP>(row, s, epi_load<OP>(row, e), e);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -96,6 +130,9 @@ __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restri
   const int ne = indptr[r1] - e0;
   double sq = 0.0;
   if (ne <= kBlockNnz) {
+    static_assert(kBlockRows <= kThreads, "one row per thread in phase 2");
+    EpiIn pre;
+    if (tid < nr) pre = epi_load<OP>(r0 + tid, ep);
     for (int t = tid; t <= nr; t += kThreads) rp[t] = indptr[r0 + t] - e0;
     const int32_t* ci = indices + e0;
     const double* cv = vals + e0;
@@ -116,7 +153,8 @@ __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restri
     for (int u = 0; u < U; ++u)
       if (tid + u * kThreads < ne) prod[tid + u * kThreads] = vv[u] * xv[u];
     __syncthreads();
-    for (int t = tid; t < nr; t += kThreads) {
+    if (tid < nr) {
+      const int t = tid;
       double s = 0.0;
       const int ka = rp[t], kb = rp[t + 1];
       int k = ka;
@@ -128,7 +166,7 @@ __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restri
         s += p3;
       }
       for (; k < kb; ++k) s += prod[k];
-      sq += epilogue<OP>(r0 + t, s, ep);
+      sq += epi_store<OP>(r0 + t, s, pre, ep);
     }
   } else {
     // one over-long row: stream it through LDS in chunks, lane 0 keeps the ordered sum
@@ -166,7 +204,7 @@ __global__ __launch_bounds__(1024) void k_finalize_norm(const double* __restrict
   if (done && *done) return;
   const int tid = threadIdx.x;
   double s = 0.0;
-  for (int i = tid; i < n; i += 1024) s += partial[i];
+  s = strided_sum(partial, n, tid, 1024);
   s = wave_sum(s);
   if ((tid & 63) == 0) red[tid >> 6] = s;
   __syncthreads();
@@ -201,6 +239,10 @@ __global__ __launch_bounds__(kThreads) void k_sell(const int64_t* __restrict__ s
   const int lane = threadIdx.x & 63;
   double sq = 0.0;
   if (slice < n_slices) {
+    const int64_t srow = slice * 64 + lane;
+    const int prow = srow < n_rows ? (perm ? perm[srow] : (int)srow) : 0;
+    EpiIn pre;
+    if (srow < n_rows) pre = epi_load<OP>(prow, ep);
     const int64_t base = sp[slice];
     const int w = (int)((sp[slice + 1] - base) >> 6);
     const int32_t* c = cols + base + lane;
@@ -227,8 +269,7 @@ __global__ __launch_bounds__(kThreads) void k_sell(const int64_t* __restrict__ s
       const double vv = __builtin_nontemporal_load(v + (int64_t)k * 64);
       if (cc >= 0) s += vv * x[cc];
     }
-    const int64_t srow = slice * 64 + lane;
-    if (srow < n_rows) sq = epilogue<OP>(perm ? perm[srow] : (int)srow, s, ep);
+    if (srow < n_rows) sq = epi_store<OP>(prow, s, pre, ep);
   }
   if constexpr (NORM) {
     double w = wave_sum(sq);
@@ -306,6 +347,9 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   // hi (a halo-extended local matrix has its ghost columns far from the owned ones)
   const int lo = base[3 * b], hi = base[3 * b + 1], split = base[3 * b + 2];
   for (int t = tid; t <= nr; t += kSrtThreads) rp[t] = indptr[r0 + t] - e0;
+  static_assert(kSrtRows <= kSrtThreads, "one row per thread in phase 2");
+  EpiIn pre;
+  if (tid < nr) pre = epi_load<OP>(r0 + tid, ep);
   constexpr int U = kSrtNnz / kSrtThreads;
   constexpr uint32_t kNone = 0xffffffffu, kSlot = (1u << kSrtPosBits) - 1;
   uint32_t w[U];
@@ -326,7 +370,8 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
     if (w[u] != kNone) prod[w[u] & kSlot] = vv[u] * xv[u];
   __syncthreads();
   double sq = 0.0;
-  for (int t = tid; t < nr; t += kSrtThreads) {
+  if (tid < nr) {
+    const int t = tid;
     double s = 0.0;
     const int ka = rp[t], kb = rp[t + 1];
     int k = ka;
@@ -338,7 +383,7 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
       s += p3;
     }
     for (; k < kb; ++k) s += prod[k];
-    sq += epilogue<OP>(r0 + t, s, ep);
+    sq += epi_store<OP>(r0 + t, s, pre, ep);
   }
   if constexpr (NORM) {
     double v = wave_sum(sq);
@@ -677,13 +722,15 @@ static double* partial_buf(const mlamg_csr* A) {
 
 int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
                   double* hist, int32_t* counter, int32_t* done, double tol, double* copy_to,
-                  const double* copy_from, double* partial, hipStream_t s) {
+                  const double* copy_from, double* partial, hipStream_t s,
+                  const double* smooth_dinv) {
   Epi ep{};
   ep.b = b;
   ep.y = r;
   ep.done = done;
   ep.copy_to = copy_to;
   ep.copy_from = copy_from;
+  ep.dinv = copy_to ? smooth_dinv : nullptr;
   const bool want = norm2 || hist || counter;
   if (!want) return launch<EPI_RESID, false>(A, x, ep, s);
   ep.partial = partial ? partial : partial_buf(A);
@@ -698,13 +745,14 @@ int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* 
 // r = b - A x with per-block sums of r^2 in partial[0..n_blocks) (no finalize), optional copy
 int residual_partials(const mlamg_csr* A, const double* b, const double* x, double* r,
                       double* copy_to, const double* copy_from, double* partial,
-                      const int32_t* done, hipStream_t s) {
+                      const int32_t* done, hipStream_t s, const double* smooth_dinv) {
   Epi ep{};
   ep.b = b;
   ep.y = r;
   ep.done = done;
   ep.copy_to = copy_to;
   ep.copy_from = copy_from;
+  ep.dinv = copy_to ? smooth_dinv : nullptr;
   ep.partial = partial;
   return launch<EPI_RESID, true>(A, x, ep, s);
 }

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(1024) void k_sum_sqrt(const double* __restrict__ pa
   __shared__ double red[16];
   if (done && *done) return;
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 1024) s += partial[i];
+  s = strided_sum(partial, n, threadIdx.x, 1024);
   s = wave_sum_v(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();

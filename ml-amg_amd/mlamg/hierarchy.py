@@ -85,14 +85,25 @@ class Hierarchy:
     VECTOR_CANDIDATES = (("vector", 8), ("vector", 16), ("vector", 32), ("vector", 64))
 
     @staticmethod
-    def _time_format(M, fmt, arg, x, y, reps=5):
+    def _time_format(M, fmt, arg, x, y, reps=5, kind="A"):
+        """Average time of M's cycle operation in format fmt: the residual epilogue for A
+        (r = b - A x, as in the cycle; here b = y), y += M x for P, y = M x for R."""
         M.set_format(fmt, arg)
-        M.matvec(x, out=y)
+        if kind == "A":
+            def op():
+                call("mlamg_residual", M.handle, ptr(y), ptr(x), ptr(y), None, stream_ptr())
+        elif kind == "P":
+            def op():
+                call("mlamg_prolong_add", M.handle, ptr(x), ptr(y), stream_ptr())
+        else:
+            def op():
+                M.matvec(x, out=y)
+        op()
         s = torch.cuda.current_stream()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         for _ in range(reps):
-            M.matvec(x, out=y)
+            op()
         e1.record(s)
         e1.synchronize()
         return e0.elapsed_time(e1) / reps * 1e3  # us
@@ -121,11 +132,12 @@ class Hierarchy:
                     row[name] = {"chosen": M.get_format()[:2]}
                     continue
                 x = torch.randn(M.shape[1], dtype=torch.float64, device=dev)
-                y = torch.empty(M.shape[0], dtype=torch.float64, device=dev)
+                y = torch.zeros(M.shape[0], dtype=torch.float64, device=dev)
                 times = {}
                 for fmt, arg in cands:
                     try:
-                        times[f"{fmt}/{arg}"] = self._time_format(M, fmt, arg, x, y)
+                        times[f"{fmt}/{arg}"] = self._time_format(M, fmt, arg, x, y,
+                                                                  kind=name)
                     except MlamgError as e:  # format limits (e.g. sorted: row > 4096 nnz)
                         if e.code != MLAMG_EUNSUPPORTED:
                             raise

@@ -81,8 +81,8 @@ def test_sell_ragged_rows(ml, torch_cuda):
         b = dev(torch, rs.randn(n))
         r = torch.empty_like(b)
         nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
-        call("mlamg_residual", Ad.handle, ptr(b), ptr(dev(torch, x)), ptr(r), ptr(nrm),
-             stream_ptr())
+        xd = dev(torch, x)
+        call("mlamg_residual", Ad.handle, ptr(b), ptr(xd), ptr(r), ptr(nrm), stream_ptr())
         ref = b.cpu().numpy() - A @ x
         assert np.array_equal(r.cpu().numpy(), ref)
         assert abs(nrm.item() - np.linalg.norm(ref)) <= 1e-13 * np.linalg.norm(ref)
@@ -112,8 +112,8 @@ def test_sorted_format_ragged_and_limits(ml, torch_cuda):
     xs, b = rs.randn(n), rs.randn(n)
     r = torch.empty(n, dtype=torch.float64, device="cuda")
     nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
-    call("mlamg_residual", Sd.handle, ptr(dev(torch, b)), ptr(dev(torch, xs)), ptr(r), ptr(nrm),
-         stream_ptr())
+    bd, xd = dev(torch, b), dev(torch, xs)  # keep the device copies alive across the call
+    call("mlamg_residual", Sd.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), stream_ptr())
     ref = b - Sq @ xs
     assert np.array_equal(r.cpu().numpy(), ref)
     assert abs(nrm.item() - np.linalg.norm(ref)) <= 1e-13 * np.linalg.norm(ref)

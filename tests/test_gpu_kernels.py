@@ -77,7 +77,8 @@ def test_mlamg_jacobi_bitwise(golden, ml, oracle, torch_cuda, k):
     x = dev(torch, golden[f"{k}_x"])
     tmp = torch.empty_like(x)
     from mlamg._lib import call, ptr, stream_ptr
-    call("mlamg_jacobi", Ad.handle, ptr(dw), ptr(dev(torch, golden[f"{k}_b"])), ptr(x), ptr(tmp),
+    bd = dev(torch, golden[f"{k}_b"])
+    call("mlamg_jacobi", Ad.handle, ptr(dw), ptr(bd), ptr(x), ptr(tmp),
          3, stream_ptr())
     assert np.array_equal(host(x), ref)
 
@@ -96,12 +97,14 @@ def test_restrict_prolong_transpose_bitwise(golden, ml, torch_cuda):
     r = np.random.RandomState(5).randn(1024)
     rc = torch.empty(342, dtype=torch.float64, device="cuda")
     from mlamg._lib import call, ptr, stream_ptr
-    call("mlamg_restrict", Rd.handle, ptr(dev(torch, r)), ptr(rc), stream_ptr())
+    rd = dev(torch, r)
+    call("mlamg_restrict", Rd.handle, ptr(rd), ptr(rc), stream_ptr())
     assert np.array_equal(host(rc), P.T @ r)  # scipy csc_matvec
     e = np.random.RandomState(6).randn(342)
     x = np.random.RandomState(7).randn(1024)
     xd = dev(torch, x)
-    call("mlamg_prolong_add", Pd.handle, ptr(dev(torch, e)), ptr(xd), stream_ptr())
+    ed = dev(torch, e)
+    call("mlamg_prolong_add", Pd.handle, ptr(ed), ptr(xd), stream_ptr())
     xr = x.copy()
     xr += P @ e
     assert np.array_equal(host(xd), xr)
@@ -242,7 +245,8 @@ def test_dense_coarse_solve(golden, ml, torch_cuda):
     h = ctypes.c_void_p()
     call("mlamg_dense_create", Ad.handle, ctypes.byref(h), stream_ptr())
     x = torch.empty(AH.shape[0], dtype=torch.float64, device="cuda")
-    call("mlamg_dense_solve", h, ptr(dev(torch, b)), ptr(x), stream_ptr())
+    bd = dev(torch, b)
+    call("mlamg_dense_solve", h, ptr(bd), ptr(x), stream_ptr())
     ref = np.linalg.solve(AH.toarray(), b)
     call("mlamg_dense_destroy", h)
     assert np.allclose(host(x), ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
