@@ -236,9 +236,138 @@ struct DevBuf {
     }                                                                           \
   } while (0)
 
+// ---------------------------------------------------------------- SpGEMM, sorted output
+// Global formulation of the same expand-sort-compress for order 0 (ascending columns): one
+// thread per nonzero of A expands its products (row i, A's stored order, then B's row order
+// = csr_matmat's accumulation order); a STABLE radix sort by (row, col) keeps equal keys in that
+// order; each run head sums its run left to right and the nonzero sums are compacted in key
+// order, which is already CSR order. Every phase is a flat data-parallel pass (no thread walks
+// a whole long row), so it scales with the product count instead of the longest row.
+__global__ void k_prod_len(const int32_t* __restrict__ aj, const int32_t* __restrict__ bp,
+                           int64_t nnz, int64_t* __restrict__ len) {
+  int64_t k = blockIdx.x * 256ll + threadIdx.x;
+  if (k >= nnz) return;
+  const int j = aj[k];
+  len[k] = bp[j + 1] - bp[j];
+}
+
+__global__ void k_expand_entries(const int32_t* __restrict__ rows, const int32_t* __restrict__ aj,
+                                 const double* __restrict__ ax, const int32_t* __restrict__ bp,
+                                 const int32_t* __restrict__ bj, const double* __restrict__ bx,
+                                 int64_t nnz, const int64_t* __restrict__ poff, int cbits,
+                                 uint64_t* __restrict__ keys, double* __restrict__ vals) {
+  int64_t k = blockIdx.x * 256ll + threadIdx.x;
+  if (k >= nnz) return;
+  const uint64_t hi = (uint64_t)(uint32_t)rows[k] << cbits;
+  const int j = aj[k];
+  const double v = ax[k];
+  int64_t o = poff[k];
+  for (int kk = bp[j]; kk < bp[j + 1]; ++kk, ++o) {
+    keys[o] = hi | (uint32_t)bj[kk];
+    vals[o] = v * bx[kk];
+  }
+}
+
+__global__ void k_run_sums(const uint64_t* __restrict__ keys, const double* __restrict__ vals,
+                           int64_t total, double* __restrict__ sums, int32_t* __restrict__ keep) {
+  int64_t e = blockIdx.x * 256ll + threadIdx.x;
+  if (e >= total) return;
+  const uint64_t key = keys[e];
+  if (e > 0 && keys[e - 1] == key) {
+    keep[e] = 0;
+    return;
+  }
+  double acc = 0.0;
+  for (int64_t f = e; f < total && keys[f] == key; ++f) acc += vals[f];
+  sums[e] = acc;
+  keep[e] = acc != 0.0 ? 1 : 0;
+}
+
+__global__ void k_emit(const uint64_t* __restrict__ keys, const double* __restrict__ sums,
+                       const int32_t* __restrict__ keep, const int32_t* __restrict__ pos,
+                       int64_t total, int cbits, int32_t* __restrict__ cj,
+                       double* __restrict__ cx, int32_t* __restrict__ rowcnt) {
+  int64_t e = blockIdx.x * 256ll + threadIdx.x;
+  if (e >= total || !keep[e]) return;
+  const uint64_t key = keys[e];
+  const int32_t p = pos[e];
+  cj[p] = (int32_t)(key & ((uint64_t(1) << cbits) - 1));
+  cx[p] = sums[e];
+  atomicAdd(&rowcnt[key >> cbits], 1);
+}
+
+static int spgemm_sorted_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out,
+                              int rbits, int cbits, hipStream_t s) {
+  const int64_t n = A->n_rows, nz = A->nnz;
+  DevBuf db;
+  int32_t* rows = nullptr;
+  int64_t *len = nullptr, *poff = nullptr;
+  DB_CHECK(db.get(&rows, nz));
+  DB_CHECK(db.get(&len, nz + 1));
+  DB_CHECK(db.get(&poff, nz + 1));
+  if (n) hipLaunchKernelGGL(k_entry_rows, dim3((n + 255) / 256), dim3(256), 0, s, A->indptr, n, rows);
+  if (nz)
+    hipLaunchKernelGGL(k_prod_len, dim3((nz + 255) / 256), dim3(256), 0, s, A->indices, B->indptr,
+                       nz, len);
+  MLAMG_TRY(exclusive_scan_i64(len, poff, nz, s));
+  int64_t total = 0;
+  DB_CHECK(hipMemcpyAsync(&total, poff + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  DB_CHECK(hipStreamSynchronize(s));
+  MLAMG_REQUIRE(total < (int64_t(1) << 31) - 1, "too many intermediate products (>2G)");
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  double *v0 = nullptr, *v1 = nullptr, *sums = nullptr;
+  int32_t *keep = nullptr, *pos = nullptr, *rowcnt = nullptr;
+  DB_CHECK(db.get(&k0, total));
+  DB_CHECK(db.get(&k1, total));
+  DB_CHECK(db.get(&v0, total));
+  DB_CHECK(db.get(&v1, total));
+  DB_CHECK(db.get(&sums, total));
+  DB_CHECK(db.get(&keep, total + 1));
+  DB_CHECK(db.get(&pos, total + 1));
+  DB_CHECK(db.get(&rowcnt, n + 1));
+  DB_CHECK(hipMemsetAsync(rowcnt, 0, sizeof(int32_t) * (n + 1), s));
+  if (nz)
+    hipLaunchKernelGGL(k_expand_entries, dim3((nz + 255) / 256), dim3(256), 0, s, rows,
+                       A->indices, A->data, B->indptr, B->indices, B->data, nz, poff, cbits, k0, v0);
+  if (total > 0) {
+    size_t tb = 0;
+    DB_CHECK(rocprim::radix_sort_pairs(nullptr, tb, k0, k1, v0, v1, (size_t)total, 0,
+                                       rbits + cbits, s));
+    void* tmp = nullptr;
+    DB_CHECK(db.get((char**)&tmp, tb + 16));
+    DB_CHECK(rocprim::radix_sort_pairs(tmp, tb, k0, k1, v0, v1, (size_t)total, 0, rbits + cbits,
+                                       s));
+    hipLaunchKernelGGL(k_run_sums, dim3((total + 255) / 256), dim3(256), 0, s, k1, v1, total,
+                       sums, keep);
+  }
+  MLAMG_TRY(exclusive_scan_i32(keep, pos, total, s));
+  int32_t nnzc = 0;
+  DB_CHECK(hipMemcpyAsync(&nnzc, pos + total, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  DB_CHECK(hipStreamSynchronize(s));
+  mlamg_csr* C = nullptr;
+  MLAMG_TRY(csr_alloc(n, B->n_cols, nnzc, &C));
+  if (total > 0)
+    hipLaunchKernelGGL(k_emit, dim3((total + 255) / 256), dim3(256), 0, s, k1, sums, keep, pos,
+                       total, cbits, C->indices, C->data, rowcnt);
+  int rc = exclusive_scan_i32(rowcnt, C->indptr, n, s);
+  if (rc == MLAMG_OK) rc = csr_finalize(C, s);  // syncs before DevBuf frees
+  else (void)hipStreamSynchronize(s);
+  if (rc != MLAMG_OK) {
+    csr_free(C);
+    return rc;
+  }
+  *out = C;
+  return MLAMG_OK;
+}
+
 int spgemm_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out, int order,
                 hipStream_t s) {
   MLAMG_REQUIRE(A->n_cols == B->n_rows, "inner dimensions differ");
+  if (order == 0) {
+    const int rbits = bits_for(std::max<int64_t>(A->n_rows, 2));
+    const int cb = bits_for(std::max<int64_t>(B->n_cols, 2));
+    if (rbits + cb <= 64) return spgemm_sorted_impl(A, B, out, rbits, cb, s);
+  }
   const int64_t n = A->n_rows;
   DevBuf db;
   int64_t* cnt = nullptr;

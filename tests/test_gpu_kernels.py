@@ -128,6 +128,32 @@ def test_sa_prolongator_galerkin_bitwise(golden, ml):
     assert np.array_equal(AH.data, golden["c1_AH_data"])
 
 
+@pytest.mark.parametrize("seed", (0, 1))
+def test_galerkin_random_bitwise(ml, seed):
+    """(P^T A) P on the device vs scipy's P.T @ A @ P (CSC path), values bit for bit, including
+    cancellations (exact zeros dropped) and rows with no products."""
+    rs = np.random.RandomState(seed)
+    n, nc = 4000, 500
+    A = sp.random(n, n, density=0.003, random_state=rs, format="csr") + sp.eye(n, format="csr")
+    A = A.tocsr()
+    A.sort_indices()
+    A.data[::5] *= -1
+    agg = rs.randint(0, nc, n)
+    agg[:7] = nc - 1  # some coarse columns empty, others heavy
+    T = sp.csr_matrix((np.ones(n), agg, np.arange(n + 1)), shape=(n, nc))
+    P = (T + sp.random(n, nc, density=0.002, random_state=rs, format="csr")).tocsr()
+    P.sort_indices()
+    P.data[::3] = np.round(P.data[::3] * 4) / 4  # small dyadic values make exact cancellations
+    ref = (P.T @ A @ P).tocsr()
+    ref.sort_indices()
+    ref.eliminate_zeros()
+    Ad, Pd = ml.sparse.DeviceCSR.from_scipy(A), ml.sparse.DeviceCSR.from_scipy(P)
+    AH = ml.sparse.galerkin(Pd.transpose(), Ad, Pd).to_scipy()
+    assert np.array_equal(AH.indptr, ref.indptr)
+    assert np.array_equal(AH.indices, ref.indices)
+    assert np.array_equal(AH.data, ref.data)
+
+
 @pytest.mark.parametrize("k", ("c1", "p2d", "lap3d", "rnd"))
 def test_lambda_max_vs_arpack(golden, ml, oracle, k):
     A = golden_csr(golden, k)
