@@ -99,7 +99,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=216, help="grid points per dimension (C4: 216)")
+    ap.add_argument("--n", "--grid", dest="n", type=int, default=216,
+                    help="grid points per dimension (C4: 216); use --grid under torchrun")
     ap.add_argument("--alpha", type=float, default=0.1)
     ap.add_argument("--max-coarse", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -116,6 +117,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("MLAMG_ONE_DEVICE") == "1":
+        local_rank = 0  # rehearsal only: every rank on GPU 0 (checks the RCCL code path on 1 GPU)
     if world != args.gpus:
         log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
     torch.cuda.set_device(local_rank)

@@ -130,7 +130,25 @@ struct mlamg_dhier {
   std::vector<void*> bufs;
   bool ready = false;
   int coarse_graph = 1;
+  // whole-cycle hipGraph (kernels + RCCL calls captured together), keyed like mlamg_hier's
+  int cycle_graph = 0;
+  bool capturing = false;
+  hipStream_t cap_stream = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  const double* g_b = nullptr;
+  double* g_x = nullptr;
+  double* g_hist = nullptr;
+  double g_tol = -1.0;
+  uint64_t g_epoch = 0;
 };
+
+static void dhier_free_graph(mlamg_dhier* D) {
+  if (D->exec) (void)hipGraphExecDestroy(D->exec);
+  if (D->graph) (void)hipGraphDestroy(D->graph);
+  D->exec = nullptr;
+  D->graph = nullptr;
+}
 
 extern "C" {
 
@@ -292,6 +310,8 @@ int mlamg_dhier_add_level(mlamg_dhier* D, const mlamg_csr* A_loc, const double* 
 
 int mlamg_dhier_destroy(mlamg_dhier* D) {
   if (D) {
+    dhier_free_graph(D);
+    if (D->cap_stream) (void)hipStreamDestroy(D->cap_stream);
     for (void* p : D->bufs)
       if (p) (void)hipFree(p);
     delete D;
@@ -302,6 +322,13 @@ int mlamg_dhier_destroy(mlamg_dhier* D) {
 int mlamg_dhier_set_coarse_graph(mlamg_dhier* D, int use_graph) {
   MLAMG_REQUIRE(D, "NULL argument");
   D->coarse_graph = use_graph;
+  return MLAMG_OK;
+}
+
+int mlamg_dhier_set_cycle_graph(mlamg_dhier* D, int use_graph) {
+  MLAMG_REQUIRE(D, "NULL argument");
+  D->cycle_graph = use_graph;
+  dhier_free_graph(D);
   return MLAMG_OK;
 }
 
@@ -375,7 +402,8 @@ static int correct(mlamg_dhier* D, size_t l, double* x_ext, const int32_t* done,
     MLAMG_TRY(spmv_set(L.R, L.r_ext, D->bc + D->c_lo_all[me], done, s));
     MLAMG_TRY(allgather_segments(D, s));
     double* xc = nullptr;
-    MLAMG_TRY(hier_coarse_cycle(D->coarse, D->bc, &xc, D->coarse_graph, s));
+    // inside a whole-cycle capture the coarse kernels are captured directly (no nested graph)
+    MLAMG_TRY(hier_coarse_cycle(D->coarse, D->bc, &xc, D->coarse_graph && !D->capturing, s));
     MLAMG_TRY(spmv_add(L.P, xc, x_ext, done, s));
   }
   return MLAMG_OK;
@@ -397,14 +425,15 @@ static int dcycle_below(mlamg_dhier* D, size_t l, double** x_out, hipStream_t s)
   return MLAMG_OK;
 }
 
+// Fused as in hier.hip: the end-of-cycle residual kernel also writes x = t + Dinv_w r (the next
+// cycle's first pre-smoothing sweep); the caller applies the first sweep before the first cycle
+// and copies t (still in t_ext) back into x after the last.
 static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, double tol,
                   hipStream_t s) {
   int32_t* counter = D->flags;
   int32_t* done = D->flags + 1;
   DLevel& L = D->lv[0];
   const mlamg_csr* A = L.A;
-  // pre-smoothing from the end-of-cycle residual (bitwise a Jacobi sweep)
-  MLAMG_TRY(jacobi_from_residual(x_ext, L.dinv, L.r_ext, L.n_own, done, s));
   MLAMG_TRY(halo_exchange_impl(L.hx, x_ext, s));
   MLAMG_TRY(residual_impl(A, b, x_ext, L.r_ext, nullptr, nullptr, nullptr, done, 0.0, nullptr,
                           nullptr, nullptr, s));
@@ -413,7 +442,8 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
   MLAMG_TRY(jacobi_sweep(A, L.dinv, b, x_ext, L.t_ext, false, done, s));
   MLAMG_TRY(halo_exchange_impl(L.hx, L.t_ext, s));
   // r = b - A t with per-block ||r||^2 partials, x <- t; then the global norm
-  MLAMG_TRY(residual_partials(A, b, L.t_ext, L.r_ext, x_ext, L.t_ext, D->partial, done, s));
+  MLAMG_TRY(residual_partials(A, b, L.t_ext, L.r_ext, x_ext, L.t_ext, D->partial, done, s,
+                              L.dinv));
   const int nb = (int)A->n_part;
   hipLaunchKernelGGL(k_local_sum, dim3(1), dim3(1024), 0, s, D->partial, nb);
   MLAMG_HIP(hipGetLastError());
@@ -437,7 +467,49 @@ int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cyc
   MLAMG_TRY(halo_exchange_impl(L.hx, x_ext, s));
   MLAMG_TRY(residual_impl(L.A, b, x_ext, L.r_ext, nullptr, nullptr, nullptr, nullptr, 0.0,
                           nullptr, nullptr, nullptr, s));
-  for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(dcycle(D, b, x_ext, res_hist, tol, s));
+  if (n_cycles > 0) {
+    // the first cycle's first pre-smoothing sweep (later ones are fused into the cycle end)
+    MLAMG_TRY(jacobi_from_residual(x_ext, L.dinv, L.r_ext, L.n_own, nullptr, s));
+    if (D->cycle_graph) {
+      if (!(D->exec && D->g_b == b && D->g_x == x_ext && D->g_hist == res_hist &&
+            D->g_tol == tol && D->g_epoch == format_epoch())) {
+        dhier_free_graph(D);
+        MLAMG_TRY(hier_prepare_ext(D->coarse));
+        if (!D->cap_stream)
+          MLAMG_HIP(hipStreamCreateWithFlags(&D->cap_stream, hipStreamNonBlocking));
+        // order the capture stream after the work already queued on s
+        hipEvent_t ev;
+        MLAMG_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        MLAMG_HIP(hipEventRecord(ev, s));
+        MLAMG_HIP(hipStreamWaitEvent(D->cap_stream, ev, 0));
+        MLAMG_HIP(hipStreamSynchronize(D->cap_stream));
+        (void)hipEventDestroy(ev);
+        MLAMG_HIP(hipStreamBeginCapture(D->cap_stream, hipStreamCaptureModeThreadLocal));
+        D->capturing = true;
+        int rc = dcycle(D, b, x_ext, res_hist, tol, D->cap_stream);
+        D->capturing = false;
+        hipGraph_t g = nullptr;
+        hipError_t e = hipStreamEndCapture(D->cap_stream, &g);
+        if (rc != MLAMG_OK) {
+          if (g) (void)hipGraphDestroy(g);
+          return rc;
+        }
+        MLAMG_HIP(e);
+        D->graph = g;
+        MLAMG_HIP(hipGraphInstantiate(&D->exec, g, nullptr, nullptr, 0));
+        D->g_b = b;
+        D->g_x = x_ext;
+        D->g_hist = res_hist;
+        D->g_tol = tol;
+        D->g_epoch = format_epoch();
+      }
+      for (int c = 0; c < n_cycles; ++c) MLAMG_HIP(hipGraphLaunch(D->exec, s));
+    } else {
+      for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(dcycle(D, b, x_ext, res_hist, tol, s));
+    }
+    // the iterate is t; x holds t + Dinv_w r for a cycle that never ran
+    MLAMG_HIP(hipMemcpyAsync(x_ext, L.t_ext, sizeof(double) * L.n_own, hipMemcpyDeviceToDevice, s));
+  }
   if (cycles_done_host) {
     int32_t cnt = 0;
     MLAMG_HIP(hipMemcpyAsync(&cnt, D->flags, sizeof(int32_t), hipMemcpyDeviceToHost, s));

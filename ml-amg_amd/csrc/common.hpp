@@ -172,6 +172,7 @@ int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int
                      hipStream_t s);
 int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
                       hipStream_t s);
+int hier_prepare_ext(mlamg_hier* H);
 int count_out_of_range(const int32_t* a, int64_t n, int64_t lo, int64_t hi, hipStream_t s,
                        int64_t* bad_out);
 }  // namespace mlamg

@@ -207,6 +207,9 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
 }
 
 namespace mlamg {
+// allocate the work buffers now (not capture-safe), so a later capture only records launches
+int hier_prepare_ext(mlamg_hier* H) { return hier_prepare(H); }
+
 // One cycle from a zero guess on (b -> *x_out) treating level 0 of H as a coarse level
 // (used by the distributed executor, whose H holds the replicated levels 1..L).
 int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,

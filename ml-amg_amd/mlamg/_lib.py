@@ -106,6 +106,7 @@ SIGNATURES = {
     "mlamg_dhier_add_level": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mlamg_dhier_destroy": (c_int, [c_vp]),
     "mlamg_dhier_set_coarse_graph": (c_int, [c_vp, c_int]),
+    "mlamg_dhier_set_cycle_graph": (c_int, [c_vp, c_int]),
     "mlamg_dhier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_vp]),
 }
 

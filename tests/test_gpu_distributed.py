@@ -33,12 +33,14 @@ def test_distributed_single_rank_bitwise(setup, min_rows):
     b = torch.as_tensor(np.random.RandomState(1).randn(n)).cuda()
     x = torch.as_tensor(x0).cuda()
     h_ref = H.cycle(b, x, 6, use_graph=False)
-    for coarse_graph in (False, True):
+    for coarse_graph, cycle_graph in ((False, False), (True, False), (True, True), (False, True)):
         D.set_coarse_graph(coarse_graph)
-        xe = D.new_x(torch.as_tensor(x0))
-        h = D.cycle(b.clone(), xe, 6)
-        assert torch.equal(xe[:n], x), f"K={D.K} graph={coarse_graph}"
-        np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
+        D.set_cycle_graph(cycle_graph)
+        for rep in range(2):  # the second call replays the captured cycle
+            xe = D.new_x(torch.as_tensor(x0))
+            h = D.cycle(b, xe, 6)
+            assert torch.equal(xe[:n], x), f"K={D.K} graphs={coarse_graph},{cycle_graph}"
+            np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
 
 
 def test_distributed_tolerance_stop(setup):
@@ -49,7 +51,9 @@ def test_distributed_tolerance_stop(setup):
     b = torch.as_tensor(np.random.RandomState(2).randn(n)).cuda()
     x = torch.zeros(n, dtype=torch.float64, device="cuda")
     h_ref = H.cycle(b, x, 50, tol=1e-6 * float(torch.linalg.norm(b)), use_graph=False)
-    xe = D.new_x(torch.zeros(n, dtype=torch.float64))
-    h = D.cycle(b, xe, 50, tol=1e-6 * float(torch.linalg.norm(b)))
-    assert len(h) == len(h_ref) < 50
-    assert torch.equal(xe[:n], x)
+    for cycle_graph in (False, True):
+        D.set_cycle_graph(cycle_graph)
+        xe = D.new_x(torch.zeros(n, dtype=torch.float64))
+        h = D.cycle(b, xe, 50, tol=1e-6 * float(torch.linalg.norm(b)))
+        assert len(h) == len(h_ref) < 50
+        assert torch.equal(xe[:n], x)
