@@ -85,6 +85,13 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
 #define MLAMG_FMT_VECTOR 2
 #define MLAMG_FMT_AUTO_EXACT 3
 #define MLAMG_FMT_SORTED 4
+/* SELL_DICT   SELL-64[-sigma] whose elements are 2-byte codes into per-matrix dictionaries of
+ *             <= 255 distinct column offsets (col - row) and <= 256 distinct values (bit
+ *             patterns): lossless, same products in the same order as SELL (scipy's bits).
+ *             For constant-coefficient stencils (C4: 7 offsets, 2 values) the matrix stream is
+ *             2 B/nonzero instead of 12. vec_width = sigma as for SELL. EUNSUPPORTED (format
+ *             reset to CSR_STREAM) when the dictionaries overflow. */
+#define MLAMG_FMT_SELL_DICT 5
 int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream);
 int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored_entries);
 

@@ -86,6 +86,14 @@ struct mlamg_csr {
   int32_t* sell_perm = nullptr;  // SELL-C-sigma row order (nullptr: natural order)
   int32_t sell_sigma = 0;
   int64_t sell_elems = 0;
+  // optional dictionary-coded SELL ("sell_dict"): same slices, each element a uint16 code
+  // (offset index | value index << 8) into <= 255 distinct column offsets (col - row) and <= 256
+  // distinct values (bit patterns); code & 0xFF == 0xFF marks padding. Lossless: products and
+  // their order are those of SELL. sell_col/sell_val are dropped while it is active.
+  uint16_t* dict_code = nullptr;
+  int32_t* dict_off = nullptr;   // 256 offsets
+  double* dict_val = nullptr;    // 256 values
+  int32_t dict_n_off = 0, dict_n_val = 0;
   // CSR-vector format (lane-strided partial sums + butterfly, NOT scipy's order): 0 = off,
   // else the number of lanes per row (4..64)
   int32_t vec_width = 0;

@@ -248,32 +248,94 @@ __global__ __launch_bounds__(kThreads) void k_sell(const int64_t* __restrict__ s
     const int32_t* c = cols + base + lane;
     const double* v = vals + base + lane;
     double s = 0.0;
-    int k = 0;
-    for (; k + 4 <= w; k += 4) {
-      int32_t cc[4];
-      double vv[4];
+    // batches of 8 with predicated tails, so a 7-point row issues all its loads at once
+    for (int k = 0; k < w; k += 8) {
+      int32_t cc[8];
+      double vv[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        cc[u] = __builtin_nontemporal_load(c + (int64_t)(k + u) * 64);
-        vv[u] = __builtin_nontemporal_load(v + (int64_t)(k + u) * 64);
+      for (int u = 0; u < 8; ++u) {
+        cc[u] = k + u < w ? __builtin_nontemporal_load(c + (int64_t)(k + u) * 64) : -1;
+        vv[u] = k + u < w ? __builtin_nontemporal_load(v + (int64_t)(k + u) * 64) : 0.0;
       }
-      double xv[4];
+      double xv[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
+      for (int u = 0; u < 8; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
         if (cc[u] >= 0) s += vv[u] * xv[u];
-    }
-    for (; k < w; ++k) {
-      const int32_t cc = __builtin_nontemporal_load(c + (int64_t)k * 64);
-      const double vv = __builtin_nontemporal_load(v + (int64_t)k * 64);
-      if (cc >= 0) s += vv * x[cc];
     }
     if (srow < n_rows) sq = epi_store<OP>(prow, s, pre, ep);
   }
   if constexpr (NORM) {
     double w = wave_sum(sq);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+      ep.partial[lb] = t;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- dictionary-coded SELL-64
+// k_sell with 2-byte elements: code = offset index | value index << 8 into per-matrix tables
+// (staged in LDS), col = row + offset. For a constant-coefficient stencil (C4: 7 offsets, 2
+// values) the matrix stream drops from 12 to 2 bytes per nonzero; the products, and the order
+// they are summed in, are exactly SELL's, hence scipy's.
+template <int OP, bool NORM>
+__global__ __launch_bounds__(kThreads) void k_sell_dict(const int64_t* __restrict__ sp,
+                                                        const uint16_t* __restrict__ codes,
+                                                        const int32_t* __restrict__ dict_off,
+                                                        const double* __restrict__ dict_val,
+                                                        const int32_t* __restrict__ perm,
+                                                        int64_t n_rows, int64_t n_slices,
+                                                        const double* __restrict__ x, Epi ep) {
+  __shared__ int32_t offt[256];
+  __shared__ double valt[256];
+  __shared__ double red[kThreads / 64];
+  if (ep.done && *ep.done) return;
+  static_assert(kThreads == 256, "one table entry per thread");
+  offt[threadIdx.x] = dict_off[threadIdx.x];
+  valt[threadIdx.x] = dict_val[threadIdx.x];
+  const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t slice = lb * (kThreads / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  double sq = 0.0;
+  int64_t srow = 0;
+  int row = 0;
+  EpiIn pre;
+  int w = 0;
+  int64_t base = 0;
+  if (slice < n_slices) {
+    srow = slice * 64 + lane;
+    row = srow < n_rows ? (perm ? perm[srow] : (int)srow) : 0;
+    if (srow < n_rows) pre = epi_load<OP>(row, ep);
+    base = sp[slice];
+    w = (int)((sp[slice + 1] - base) >> 6);
+  }
+  __syncthreads();
+  if (slice < n_slices) {
+    const uint16_t* c = codes + base + lane;
+    double s = 0.0;
+    // batches of 8 with predicated tails, so a 7-point row issues all its loads at once
+    for (int k = 0; k < w; k += 8) {
+      uint16_t cc[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        cc[u] = k + u < w ? __builtin_nontemporal_load(c + (int64_t)(k + u) * 64) : (uint16_t)0xFF;
+      double xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xv[u] = (cc[u] & 0xFF) != 0xFF ? x[row + offt[cc[u] & 0xFF]] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if ((cc[u] & 0xFF) != 0xFF) s += valt[cc[u] >> 8] * xv[u];
+    }
+    if (srow < n_rows) sq = epi_store<OP>(row, s, pre, ep);
+  }
+  if constexpr (NORM) {
+    double v = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     if (threadIdx.x == 0) {
       double t = 0.0;
@@ -430,6 +492,15 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_
     MLAMG_HIP(hipGetLastError());
     return MLAMG_OK;
   }
+  if (A->dict_code) {
+    if (A->n_slices == 0) return MLAMG_OK;
+    const unsigned nb = (unsigned)((A->n_slices + kThreads / 64 - 1) / (kThreads / 64));
+    hipLaunchKernelGGL((k_sell_dict<OP, NORM>), dim3(nb), dim3(kThreads), 0, s, A->sell_ptr,
+                       A->dict_code, A->dict_off, A->dict_val, A->sell_perm, A->n_rows,
+                       A->n_slices, x, ep);
+    MLAMG_HIP(hipGetLastError());
+    return MLAMG_OK;
+  }
   if (A->sell_ptr) {
     if (A->n_slices == 0) return MLAMG_OK;
     const unsigned nb = (unsigned)((A->n_slices + kThreads / 64 - 1) / (kThreads / 64));
@@ -467,6 +538,13 @@ __global__ void k_sell_fill(const int32_t* __restrict__ ip, const int32_t* __res
 }
 
 static void drop_sell(mlamg_csr* A) {
+  if (A->dict_code) (void)hipFree(A->dict_code);
+  if (A->dict_off) (void)hipFree(A->dict_off);
+  if (A->dict_val) (void)hipFree(A->dict_val);
+  A->dict_code = nullptr;
+  A->dict_off = nullptr;
+  A->dict_val = nullptr;
+  A->dict_n_off = A->dict_n_val = 0;
   if (A->sell_ptr) (void)hipFree(A->sell_ptr);
   if (A->sell_col) (void)hipFree(A->sell_col);
   if (A->sell_val) (void)hipFree(A->sell_val);
@@ -533,6 +611,166 @@ int build_sell(mlamg_csr* A, hipStream_t s, int sigma) {
   A->sell_elems = total;
   A->sell_sigma = std::max(sigma, 1);
   A->n_part = (int32_t)std::max<int64_t>(1, (ns + 3) / 4);
+  return MLAMG_OK;
+}
+
+// ---------------------------------------------------------------- dictionary construction
+// Open-addressing tables of kDictSlots 64-bit keys; a slot holds kDictEmpty until claimed.
+constexpr int kDictSlots = 1024;
+constexpr unsigned long long kDictEmpty = ~0ull;
+
+__device__ __forceinline__ int dict_slot(unsigned long long key, unsigned long long* tab,
+                                         int32_t* count, bool insert) {
+  unsigned h = (unsigned)((key * 0x9E3779B97F4A7C15ull) >> 54);  // 10 bits
+  for (int probe = 0; probe < kDictSlots; ++probe) {
+    const unsigned sl = (h + probe) & (kDictSlots - 1);
+    unsigned long long cur = tab[sl];
+    if (cur == key) return (int)sl;
+    if (cur == kDictEmpty) {
+      if (!insert) return -1;
+      cur = atomicCAS(&tab[sl], kDictEmpty, key);
+      if (cur == kDictEmpty) {
+        atomicAdd(count, 1);
+        return (int)sl;
+      }
+      if (cur == key) return (int)sl;
+    }
+  }
+  return -1;
+}
+
+// pass 0: insert every (offset, value) of the SELL copy; pass 1: encode with slot -> index maps
+__global__ void k_dict_pass(const int64_t* __restrict__ sp, const int32_t* __restrict__ cols,
+                            const double* __restrict__ vals, const int32_t* __restrict__ perm,
+                            int64_t n, int64_t n_slices, int pass, unsigned long long* otab,
+                            unsigned long long* vtab, int32_t* counts,
+                            const int32_t* __restrict__ oidx, const int32_t* __restrict__ vidx,
+                            uint16_t* __restrict__ codes) {
+  const int64_t sl = blockIdx.x * 4ll + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (sl >= n_slices) return;
+  const int64_t base = sp[sl];
+  const int w = (int)((sp[sl + 1] - base) >> 6);
+  const int64_t srow = sl * 64 + lane;
+  const int64_t row = (perm && srow < n) ? perm[srow] : srow;
+  for (int k = 0; k < w; ++k) {
+    const int64_t o = base + (int64_t)k * 64 + lane;
+    const int32_t c = cols[o];
+    if (pass == 0) {
+      // stop as soon as the dictionaries are known to overflow
+      if (((volatile int32_t*)counts)[0] > 255 || ((volatile int32_t*)counts)[1] > 256 ||
+          ((volatile int32_t*)counts)[2] != 0)
+        return;
+      if (c < 0) continue;
+      const unsigned long long okey = (unsigned long long)((int64_t)c - row + (int64_t(1) << 40));
+      const unsigned long long vkey = (unsigned long long)__double_as_longlong(vals[o]);
+      if (dict_slot(okey, otab, counts + 0, true) < 0 || vkey == kDictEmpty ||
+          dict_slot(vkey, vtab, counts + 1, true) < 0)
+        atomicAdd(counts + 2, 1);  // table full / unrepresentable: refuse the format
+    } else {
+      if (c < 0) {
+        codes[o] = 0x00FF;
+        continue;
+      }
+      const unsigned long long okey = (unsigned long long)((int64_t)c - row + (int64_t(1) << 40));
+      const unsigned long long vkey = (unsigned long long)__double_as_longlong(vals[o]);
+      const int so = dict_slot(okey, otab, counts, false), sv = dict_slot(vkey, vtab, counts, false);
+      codes[o] = (uint16_t)(oidx[so] | (vidx[sv] << 8));
+    }
+  }
+}
+
+// SELL (natural order or sigma-sorted) re-coded with dictionaries; EUNSUPPORTED (A back in plain
+// CSR-stream form) when the operator has more than 255 distinct offsets or 256 distinct values.
+static int build_sell_dict(mlamg_csr* A, hipStream_t s, int sigma) {
+  MLAMG_TRY(build_sell(A, s, sigma));
+  const int64_t ns = A->n_slices;
+  unsigned long long *otab = nullptr, *vtab = nullptr;
+  int32_t *counts = nullptr, *oidx = nullptr, *vidx = nullptr;
+  int rc = MLAMG_OK;
+  auto fail = [&](int code, const char* what) {
+    if (rc == MLAMG_OK) {
+      set_error(std::string("sell_dict: ") + what);
+      rc = code;
+    }
+  };
+  if (hipMalloc(&otab, sizeof(unsigned long long) * kDictSlots) != hipSuccess ||
+      hipMalloc(&vtab, sizeof(unsigned long long) * kDictSlots) != hipSuccess ||
+      hipMalloc(&counts, sizeof(int32_t) * 4) != hipSuccess ||
+      hipMalloc(&oidx, sizeof(int32_t) * kDictSlots) != hipSuccess ||
+      hipMalloc(&vidx, sizeof(int32_t) * kDictSlots) != hipSuccess ||
+      hipMalloc(&A->dict_code, sizeof(uint16_t) * std::max<int64_t>(A->sell_elems, 1)) != hipSuccess ||
+      hipMalloc(&A->dict_off, sizeof(int32_t) * 256) != hipSuccess ||
+      hipMalloc(&A->dict_val, sizeof(double) * 256) != hipSuccess)
+    fail(MLAMG_ENOMEM, "out of device memory");
+  if (rc == MLAMG_OK &&
+      (hipMemsetAsync(otab, 0xFF, sizeof(unsigned long long) * kDictSlots, s) != hipSuccess ||
+       hipMemsetAsync(vtab, 0xFF, sizeof(unsigned long long) * kDictSlots, s) != hipSuccess ||
+       hipMemsetAsync(counts, 0, sizeof(int32_t) * 4, s) != hipSuccess ||
+       hipMemsetAsync(A->dict_off, 0, sizeof(int32_t) * 256, s) != hipSuccess ||
+       hipMemsetAsync(A->dict_val, 0, sizeof(double) * 256, s) != hipSuccess))
+    fail(MLAMG_EHIP, "memset");
+  if (rc == MLAMG_OK && ns)
+    hipLaunchKernelGGL(k_dict_pass, dim3((ns + 3) / 4), dim3(256), 0, s, A->sell_ptr, A->sell_col,
+                       A->sell_val, A->sell_perm, A->n_rows, ns, 0, otab, vtab, counts, oidx,
+                       vidx, A->dict_code);
+  std::vector<unsigned long long> ho(kDictSlots), hv(kDictSlots);
+  int32_t hc[4] = {0, 0, 0, 0};
+  if (rc == MLAMG_OK &&
+      (hipGetLastError() != hipSuccess ||
+       hipMemcpyAsync(ho.data(), otab, sizeof(unsigned long long) * kDictSlots,
+                      hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipMemcpyAsync(hv.data(), vtab, sizeof(unsigned long long) * kDictSlots,
+                      hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipMemcpyAsync(hc, counts, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess))
+    fail(MLAMG_EHIP, "dictionary scan");
+  if (rc == MLAMG_OK && (hc[2] != 0 || hc[0] > 255 || hc[1] > 256))
+    fail(MLAMG_EUNSUPPORTED, "more than 255 distinct column offsets or 256 distinct values");
+  if (rc == MLAMG_OK) {
+    // deterministic indices: offsets ascending, values by ascending bit pattern
+    std::vector<std::pair<unsigned long long, int>> os, vs;
+    for (int i = 0; i < kDictSlots; ++i) {
+      if (ho[i] != kDictEmpty) os.push_back({ho[i], i});
+      if (hv[i] != kDictEmpty) vs.push_back({hv[i], i});
+    }
+    std::sort(os.begin(), os.end());
+    std::sort(vs.begin(), vs.end());
+    std::vector<int32_t> hoi(kDictSlots, 0), hvi(kDictSlots, 0), offt(256, 0);
+    std::vector<double> valt(256, 0.0);
+    for (size_t k = 0; k < os.size(); ++k) {
+      hoi[os[k].second] = (int32_t)k;
+      offt[k] = (int32_t)((int64_t)os[k].first - (int64_t(1) << 40));
+    }
+    for (size_t k = 0; k < vs.size(); ++k) {
+      hvi[vs[k].second] = (int32_t)k;
+      std::memcpy(&valt[k], &vs[k].first, sizeof(double));
+    }
+    A->dict_n_off = (int32_t)os.size();
+    A->dict_n_val = (int32_t)vs.size();
+    if (hipMemcpyAsync(oidx, hoi.data(), sizeof(int32_t) * kDictSlots, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(vidx, hvi.data(), sizeof(int32_t) * kDictSlots, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(A->dict_off, offt.data(), sizeof(int32_t) * 256, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(A->dict_val, valt.data(), sizeof(double) * 256, hipMemcpyHostToDevice, s) != hipSuccess)
+      fail(MLAMG_EHIP, "upload");
+    if (rc == MLAMG_OK && ns)
+      hipLaunchKernelGGL(k_dict_pass, dim3((ns + 3) / 4), dim3(256), 0, s, A->sell_ptr,
+                         A->sell_col, A->sell_val, A->sell_perm, A->n_rows, ns, 1, otab, vtab,
+                         counts, oidx, vidx, A->dict_code);
+    if (rc == MLAMG_OK && (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess))
+      fail(MLAMG_EHIP, "encode");
+  }
+  for (void* p : {(void*)otab, (void*)vtab, (void*)counts, (void*)oidx, (void*)vidx})
+    if (p) (void)hipFree(p);
+  if (rc != MLAMG_OK) {
+    drop_sell(A);
+    return rc;
+  }
+  // the coded copy replaces the SELL arrays
+  (void)hipFree(A->sell_col);
+  (void)hipFree(A->sell_val);
+  A->sell_col = nullptr;
+  A->sell_val = nullptr;
   return MLAMG_OK;
 }
 
@@ -859,6 +1097,10 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       A->vec_width = 0;
       drop_sorted(A);
       return build_sell(A, s, vec_width > 1 ? vec_width : 1);  // vec_width doubles as sigma
+    case MLAMG_FMT_SELL_DICT:
+      A->vec_width = 0;
+      drop_sorted(A);
+      return build_sell_dict(A, s, vec_width > 1 ? vec_width : 1);
     case MLAMG_FMT_SORTED: {
       // built first, so an unsupported matrix keeps its current format
       MLAMG_TRY(build_sorted(A, s));
@@ -902,10 +1144,11 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
 
 int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored) {
   MLAMG_REQUIRE(A, "NULL argument");
-  const int f = A->vec_width ? MLAMG_FMT_VECTOR
-                : A->srt_pk   ? MLAMG_FMT_SORTED
-                : A->sell_ptr ? MLAMG_FMT_SELL
-                              : MLAMG_FMT_CSR_STREAM;
+  const int f = A->vec_width  ? MLAMG_FMT_VECTOR
+                : A->srt_pk    ? MLAMG_FMT_SORTED
+                : A->dict_code ? MLAMG_FMT_SELL_DICT
+                : A->sell_ptr  ? MLAMG_FMT_SELL
+                               : MLAMG_FMT_CSR_STREAM;
   if (fmt) *fmt = f;
   if (vec_width) *vec_width = A->vec_width ? A->vec_width : (A->srt_pk ? 0 : A->sell_sigma);
   if (stored) *stored = A->sell_ptr ? A->sell_elems : A->nnz;

@@ -81,7 +81,8 @@ class Hierarchy:
         H._finalize(nu_pre, nu_post)
         return H
 
-    EXACT_CANDIDATES = (("csr_stream", 0), ("sell", 1), ("sell", 512), ("sorted", 0))
+    EXACT_CANDIDATES = (("csr_stream", 0), ("sell", 1), ("sell", 512), ("sorted", 0),
+                        ("sell_dict", 1), ("sell_dict", 512))
     VECTOR_CANDIDATES = (("vector", 8), ("vector", 16), ("vector", 32), ("vector", 64))
 
     @staticmethod

@@ -32,11 +32,17 @@ def dev(torch, x):
 
 
 @pytest.mark.parametrize("k", MATS)
-@pytest.mark.parametrize("fmt", ("sell", "csr_stream", "auto_exact", "sorted"))
+@pytest.mark.parametrize("fmt", ("sell", "csr_stream", "auto_exact", "sorted", "sell_dict"))
 def test_exact_formats_bitwise(golden, ml, torch_cuda, k, fmt):
     torch = torch_cuda
     A = golden_csr(golden, k)
-    Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format(fmt)
+    from mlamg._lib import MLAMG_EUNSUPPORTED, MlamgError
+    Ad = ml.sparse.DeviceCSR.from_scipy(A)
+    try:
+        Ad.set_format(fmt)
+    except MlamgError as e:  # sell_dict on operators with many distinct values
+        assert fmt == "sell_dict" and e.code == MLAMG_EUNSUPPORTED
+        assert Ad.get_format()[0] == "csr_stream"
     x = dev(torch, golden[f"{k}_x"])
     assert np.array_equal(Ad.matvec(x).cpu().numpy(), golden[f"{k}_Ax"])
     from mlamg._lib import call, ptr, stream_ptr
@@ -136,6 +142,49 @@ def test_sorted_format_ragged_and_limits(ml, torch_cuda):
         W3d.set_format("sorted")
     assert W3d.get_format()[0] == "csr_stream"
     assert np.array_equal(W3d.matvec(dev(torch, xw)).cpu().numpy(), W3 @ xw)
+
+
+def test_sell_dict_format(ml, torch_cuda):
+    """Dictionary-coded SELL: bitwise CSR order on a stencil (ragged boundary rows, sigma
+    orders), every epilogue through the hierarchy, and refusal past 255 offsets / 256 values."""
+    torch = torch_cuda
+    from mlamg._lib import MlamgError, call, ptr, stream_ptr
+    A = ml.problems.poisson_3d_7pt(20)
+    n = A.shape[0]
+    rs = np.random.RandomState(7)
+    x, b = rs.randn(n), rs.randn(n)
+    xd, bd = dev(torch, x), dev(torch, b)
+    for sigma in (1, 512):
+        Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("sell_dict", sigma)
+        assert Ad.get_format()[:2] == ("sell_dict", sigma)
+        assert np.array_equal(Ad.matvec(xd).cpu().numpy(), A @ x)
+        r = torch.empty(n, dtype=torch.float64, device="cuda")
+        nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
+        call("mlamg_residual", Ad.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), stream_ptr())
+        assert np.array_equal(r.cpu().numpy(), b - A @ x)
+    # 2 distinct values incl. a negative zero kept apart from +0
+    B = A.copy()
+    B.data = B.data.copy()
+    B.data[5] = -0.0
+    Bd = ml.sparse.DeviceCSR.from_scipy(B).set_format("sell_dict")
+    assert np.array_equal(Bd.matvec(xd).cpu().numpy(), B @ x)
+    # too many distinct values -> refused, back to CSR-stream, still bitwise
+    R = sp.random(500, 500, density=0.05, random_state=rs, format="csr")
+    Rd = ml.sparse.DeviceCSR.from_scipy(R)
+    with pytest.raises(MlamgError):
+        Rd.set_format("sell_dict")
+    assert Rd.get_format()[0] == "csr_stream"
+    xr = rs.randn(500)
+    assert np.array_equal(Rd.matvec(dev(torch, xr)).cpu().numpy(), R @ xr)
+    # whole cycle with the fine operator dictionary-coded
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=100, fine_format="csr_stream")
+    H2 = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=100, fine_format="csr_stream")
+    H2.levels[0].A.set_format("sell_dict")
+    x1, x2 = dev(torch, x), dev(torch, x)
+    h1 = H.cycle(bd, x1, 5)
+    h2 = H2.cycle(bd, x2, 5)
+    assert torch.equal(x1, x2)
+    assert np.allclose(h1, h2, rtol=1e-14, atol=0)
 
 
 def _oracle_levels_from_device(H):
