@@ -163,16 +163,19 @@ def main():
     xs = torch.randn(n, dtype=torch.float64, device="cuda")
     ys = torch.empty_like(xs)
     t_spmv = time_kernel(lambda: A0.matvec(xs, out=ys), reps=50)
-    B = spmv_bytes(n, n, A0.nnz)
-    achieved = B / t_spmv / 1e9
+    B = spmv_bytes(n, n, A0.nnz)          # SURVEY.md §8(d) CSR bytes (format independent)
+    B_fmt = A0.format_bytes()             # bytes the chosen storage format actually streams
+    achieved = B_fmt / t_spmv / 1e9
     # A/B of the exact-order SpMV kernels on a separate copy of A0 (same bits, different layout)
     from mlamg.sparse import DeviceCSR
     Ab = DeviceCSR.from_scipy(A, check=False)
     ab = {}
-    for fmt in ("csr_stream", "sell"):
+    for fmt in ("csr_stream", "sell", "sorted", "sell_dict"):
         Ab.set_format(fmt)
         t = time_kernel(lambda: Ab.matvec(xs, out=ys), reps=30)
-        ab[fmt] = {"us": round(t * 1e6, 2), "GBps": round(B / t / 1e9, 1)}
+        fb = Ab.format_bytes()
+        ab[fmt] = {"us": round(t * 1e6, 2), "format_bytes": fb, "GBps": round(fb / t / 1e9, 1),
+                   "csr_equivalent_GBps": round(B / t / 1e9, 1)}
     del Ab
     pmc = load_traffic(f"spmv_c4_pmc_{fmt0}.json")
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
@@ -200,13 +203,15 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": f"fine-level CSR SpMV, y = A x ({fmt0} kernel, scipy summation order)",
+            "kernel": f"fine-level SpMV, y = A x ({fmt0} kernel, scipy summation order)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "algorithmic_bytes_per_launch": B,
+            "algorithmic_bytes_per_launch": B_fmt,
+            "csr_algorithmic_bytes_per_launch": B,
+            "csr_equivalent_GBps": round(B / t_spmv / 1e9, 1),
             "avg_launch_us": round(t_spmv * 1e6, 2),
         },
         "cycle_algorithmic_GBps": round(cyc_bytes / (dt / args.steps) / 1e9, 1),

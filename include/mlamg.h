@@ -94,6 +94,10 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
 #define MLAMG_FMT_SELL_DICT 5
 int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream);
 int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored_entries);
+/* algorithmic HBM bytes of one y = A@x with the active format: matrix stream as stored (CSR:
+ * 12*nnz + 4*(n+1); SELL: 12 B per padded element + slice pointers; SELL_DICT: 2 B per code +
+ * tables; SORTED: CSR + block tables) + 8*n_cols (x once) + 8*n_rows (y once) */
+int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes);
 
 /* ---------------------------------------------------------------- hot-path sparse ops
  * Each sums a row left-to-right in stored order with separate multiply and add roundings,

@@ -91,6 +91,8 @@ struct mlamg_csr {
   // distinct values (bit patterns); code & 0xFF == 0xFF marks padding. Lossless: products and
   // their order are those of SELL. sell_col/sell_val are dropped while it is active.
   uint16_t* dict_code = nullptr;
+  int64_t* dict_ptr = nullptr;   // code offset of each slice: rows padded to 8 codes, stored
+                                 // [group of 8][lane][8] so a lane reads 8 codes in one 16-B load
   int32_t* dict_off = nullptr;   // 256 offsets
   double* dict_val = nullptr;    // 256 values
   int32_t dict_n_off = 0, dict_n_val = 0;

@@ -83,6 +83,7 @@ void csr_free(mlamg_csr* A) {
   if (A->sell_val) (void)hipFree(A->sell_val);
   if (A->sell_perm) (void)hipFree(A->sell_perm);
   if (A->dict_code) (void)hipFree(A->dict_code);
+  if (A->dict_ptr) (void)hipFree(A->dict_ptr);
   if (A->dict_off) (void)hipFree(A->dict_off);
   if (A->dict_val) (void)hipFree(A->dict_val);
   if (A->srt_blk) (void)hipFree(A->srt_blk);

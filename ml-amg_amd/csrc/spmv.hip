@@ -17,6 +17,8 @@
 // extra vector the epilogue reads/writes), SURVEY.md §8(d).
 #include "common.hpp"
 
+#include <cstdlib>
+
 #include <rocprim/rocprim.hpp>
 
 namespace mlamg {
@@ -283,14 +285,17 @@ __global__ __launch_bounds__(kThreads) void k_sell(const int64_t* __restrict__ s
 // (staged in LDS), col = row + offset. For a constant-coefficient stencil (C4: 7 offsets, 2
 // values) the matrix stream drops from 12 to 2 bytes per nonzero; the products, and the order
 // they are summed in, are exactly SELL's, hence scipy's.
-template <int OP, bool NORM>
-__global__ __launch_bounds__(kThreads) void k_sell_dict(const int64_t* __restrict__ sp,
+template <int OP, bool NORM, int SPW>
+__global__ __launch_bounds__(kThreads) void k_sell_dict(const int64_t* __restrict__ dp,
                                                         const uint16_t* __restrict__ codes,
                                                         const int32_t* __restrict__ dict_off,
                                                         const double* __restrict__ dict_val,
                                                         const int32_t* __restrict__ perm,
                                                         int64_t n_rows, int64_t n_slices,
                                                         const double* __restrict__ x, Epi ep) {
+  // SPW slices per wave (lane j holds row j of each): their loads are issued together, so a
+  // wave keeps SPW x 7 gathers in flight on a 7-point stencil; each lane fetches its next 8
+  // codes with one 16-byte load
   __shared__ int32_t offt[256];
   __shared__ double valt[256];
   __shared__ double red[kThreads / 64];
@@ -299,40 +304,58 @@ __global__ __launch_bounds__(kThreads) void k_sell_dict(const int64_t* __restric
   offt[threadIdx.x] = dict_off[threadIdx.x];
   valt[threadIdx.x] = dict_val[threadIdx.x];
   const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
-  const int64_t slice = lb * (kThreads / 64) + (threadIdx.x >> 6);
+  const int64_t slice0 = (lb * (kThreads / 64) + (threadIdx.x >> 6)) * SPW;
   const int lane = threadIdx.x & 63;
-  double sq = 0.0;
-  int64_t srow = 0;
-  int row = 0;
-  EpiIn pre;
-  int w = 0;
-  int64_t base = 0;
-  if (slice < n_slices) {
-    srow = slice * 64 + lane;
-    row = srow < n_rows ? (perm ? perm[srow] : (int)srow) : 0;
-    if (srow < n_rows) pre = epi_load<OP>(row, ep);
-    base = sp[slice];
-    w = (int)((sp[slice + 1] - base) >> 6);
+  int row[SPW], ng[SPW];
+  int64_t srow[SPW], base[SPW];
+  EpiIn pre[SPW];
+  int gmax = 0;
+#pragma unroll
+  for (int q = 0; q < SPW; ++q) {
+    const int64_t sl = slice0 + q;
+    srow[q] = sl * 64 + lane;
+    row[q] = srow[q] < n_rows ? (perm ? perm[srow[q]] : (int)srow[q]) : 0;
+    if (srow[q] < n_rows) pre[q] = epi_load<OP>(row[q], ep);
+    base[q] = sl < n_slices ? dp[sl] : 0;
+    ng[q] = sl < n_slices ? (int)((dp[sl + 1] - base[q]) >> 9) : 0;  // groups of 8 x 64 codes
+    gmax = ng[q] > gmax ? ng[q] : gmax;
   }
   __syncthreads();
-  if (slice < n_slices) {
-    const uint16_t* c = codes + base + lane;
-    double s = 0.0;
-    // batches of 8 with predicated tails, so a 7-point row issues all its loads at once
-    for (int k = 0; k < w; k += 8) {
-      uint16_t cc[8];
+  double acc[SPW];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        cc[u] = k + u < w ? __builtin_nontemporal_load(c + (int64_t)(k + u) * 64) : (uint16_t)0xFF;
-      double xv[8];
+  for (int q = 0; q < SPW; ++q) acc[q] = 0.0;
+  for (int g = 0; g < gmax; ++g) {
+    uint16_t cc[SPW][8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) xv[u] = (cc[u] & 0xFF) != 0xFF ? x[row + offt[cc[u] & 0xFF]] : 0.0;
+    for (int q = 0; q < SPW; ++q) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 v = {0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu, 0x00FF00FFu};
+      if (g < ng[q])
+        v = __builtin_nontemporal_load(
+            reinterpret_cast<const u32x4*>(codes + base[q] + ((int64_t)g << 9)) + lane);
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if ((cc[u] & 0xFF) != 0xFF) s += valt[cc[u] >> 8] * xv[u];
+      for (int u = 0; u < 4; ++u) {
+        cc[q][2 * u] = (uint16_t)(wv[u] & 0xFFFFu);
+        cc[q][2 * u + 1] = (uint16_t)(wv[u] >> 16);
+      }
     }
-    if (srow < n_rows) sq = epi_store<OP>(row, s, pre, ep);
+    double xv[SPW][8];
+#pragma unroll
+    for (int q = 0; q < SPW; ++q)
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        xv[q][u] = (cc[q][u] & 0xFF) != 0xFF ? x[row[q] + offt[cc[q][u] & 0xFF]] : 0.0;
+#pragma unroll
+    for (int q = 0; q < SPW; ++q)
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if ((cc[q][u] & 0xFF) != 0xFF) acc[q] += valt[cc[q][u] >> 8] * xv[q][u];
   }
+  double sq = 0.0;
+#pragma unroll
+  for (int q = 0; q < SPW; ++q)
+    if (srow[q] < n_rows) sq += epi_store<OP>(row[q], acc[q], pre[q], ep);
   if constexpr (NORM) {
     double v = wave_sum(sq);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
@@ -481,6 +504,16 @@ static int launch_vec(const mlamg_csr* A, const double* x, const Epi& ep, hipStr
   }
 }
 
+// slices per wave of the dictionary kernel (env MLAMG_DICT_SPW = 1, 2 or 4; for A/B runs)
+static int dict_slices_per_wave() {
+  static int v = [] {
+    const char* e = std::getenv("MLAMG_DICT_SPW");
+    const int k = e ? std::atoi(e) : 2;
+    return (k == 1 || k == 2 || k == 4) ? k : 2;
+  }();
+  return v;
+}
+
 // ---------------------------------------------------------------- launch helpers
 template <int OP, bool NORM>
 static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
@@ -494,10 +527,21 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_
   }
   if (A->dict_code) {
     if (A->n_slices == 0) return MLAMG_OK;
-    const unsigned nb = (unsigned)((A->n_slices + kThreads / 64 - 1) / (kThreads / 64));
-    hipLaunchKernelGGL((k_sell_dict<OP, NORM>), dim3(nb), dim3(kThreads), 0, s, A->sell_ptr,
-                       A->dict_code, A->dict_off, A->dict_val, A->sell_perm, A->n_rows,
-                       A->n_slices, x, ep);
+    const int spw = dict_slices_per_wave();
+    const int64_t per_block = (kThreads / 64) * spw;
+    const unsigned nb = (unsigned)((A->n_slices + per_block - 1) / per_block);
+    if (spw == 1)
+      hipLaunchKernelGGL((k_sell_dict<OP, NORM, 1>), dim3(nb), dim3(kThreads), 0, s, A->dict_ptr,
+                         A->dict_code, A->dict_off, A->dict_val, A->sell_perm, A->n_rows,
+                         A->n_slices, x, ep);
+    else if (spw == 2)
+      hipLaunchKernelGGL((k_sell_dict<OP, NORM, 2>), dim3(nb), dim3(kThreads), 0, s, A->dict_ptr,
+                         A->dict_code, A->dict_off, A->dict_val, A->sell_perm, A->n_rows,
+                         A->n_slices, x, ep);
+    else
+      hipLaunchKernelGGL((k_sell_dict<OP, NORM, 4>), dim3(nb), dim3(kThreads), 0, s, A->dict_ptr,
+                         A->dict_code, A->dict_off, A->dict_val, A->sell_perm, A->n_rows,
+                         A->n_slices, x, ep);
     MLAMG_HIP(hipGetLastError());
     return MLAMG_OK;
   }
@@ -539,9 +583,11 @@ __global__ void k_sell_fill(const int32_t* __restrict__ ip, const int32_t* __res
 
 static void drop_sell(mlamg_csr* A) {
   if (A->dict_code) (void)hipFree(A->dict_code);
+  if (A->dict_ptr) (void)hipFree(A->dict_ptr);
   if (A->dict_off) (void)hipFree(A->dict_off);
   if (A->dict_val) (void)hipFree(A->dict_val);
   A->dict_code = nullptr;
+  A->dict_ptr = nullptr;
   A->dict_off = nullptr;
   A->dict_val = nullptr;
   A->dict_n_off = A->dict_n_val = 0;
@@ -645,7 +691,7 @@ __global__ void k_dict_pass(const int64_t* __restrict__ sp, const int32_t* __res
                             int64_t n, int64_t n_slices, int pass, unsigned long long* otab,
                             unsigned long long* vtab, int32_t* counts,
                             const int32_t* __restrict__ oidx, const int32_t* __restrict__ vidx,
-                            uint16_t* __restrict__ codes) {
+                            const int64_t* __restrict__ dp, uint16_t* __restrict__ codes) {
   const int64_t sl = blockIdx.x * 4ll + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (sl >= n_slices) return;
@@ -668,14 +714,12 @@ __global__ void k_dict_pass(const int64_t* __restrict__ sp, const int32_t* __res
           dict_slot(vkey, vtab, counts + 1, true) < 0)
         atomicAdd(counts + 2, 1);  // table full / unrepresentable: refuse the format
     } else {
-      if (c < 0) {
-        codes[o] = 0x00FF;
-        continue;
-      }
+      if (c < 0) continue;  // padding: the code array is pre-filled with 0x00FF
       const unsigned long long okey = (unsigned long long)((int64_t)c - row + (int64_t(1) << 40));
       const unsigned long long vkey = (unsigned long long)__double_as_longlong(vals[o]);
       const int so = dict_slot(okey, otab, counts, false), sv = dict_slot(vkey, vtab, counts, false);
-      codes[o] = (uint16_t)(oidx[so] | (vidx[sv] << 8));
+      codes[dp[sl] + ((int64_t)(k >> 3) << 9) + lane * 8 + (k & 7)] =
+          (uint16_t)(oidx[so] | (vidx[sv] << 8));
     }
   }
 }
@@ -685,6 +729,16 @@ __global__ void k_dict_pass(const int64_t* __restrict__ sp, const int32_t* __res
 static int build_sell_dict(mlamg_csr* A, hipStream_t s, int sigma) {
   MLAMG_TRY(build_sell(A, s, sigma));
   const int64_t ns = A->n_slices;
+  // packed code layout: each slice's rows padded to a multiple of 8 codes
+  std::vector<int64_t> hsp(ns + 1), hdp(ns + 1, 0);
+  MLAMG_HIP(hipMemcpyAsync(hsp.data(), A->sell_ptr, sizeof(int64_t) * (ns + 1),
+                           hipMemcpyDeviceToHost, s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  for (int64_t sl = 0; sl < ns; ++sl) {
+    const int64_t w = (hsp[sl + 1] - hsp[sl]) >> 6;
+    hdp[sl + 1] = hdp[sl] + ((w + 7) / 8) * 512;
+  }
+  const int64_t n_codes = hdp[ns];
   unsigned long long *otab = nullptr, *vtab = nullptr;
   int32_t *counts = nullptr, *oidx = nullptr, *vidx = nullptr;
   int rc = MLAMG_OK;
@@ -699,7 +753,8 @@ static int build_sell_dict(mlamg_csr* A, hipStream_t s, int sigma) {
       hipMalloc(&counts, sizeof(int32_t) * 4) != hipSuccess ||
       hipMalloc(&oidx, sizeof(int32_t) * kDictSlots) != hipSuccess ||
       hipMalloc(&vidx, sizeof(int32_t) * kDictSlots) != hipSuccess ||
-      hipMalloc(&A->dict_code, sizeof(uint16_t) * std::max<int64_t>(A->sell_elems, 1)) != hipSuccess ||
+      hipMalloc(&A->dict_code, sizeof(uint16_t) * std::max<int64_t>(n_codes, 8)) != hipSuccess ||
+      hipMalloc(&A->dict_ptr, sizeof(int64_t) * (ns + 1)) != hipSuccess ||
       hipMalloc(&A->dict_off, sizeof(int32_t) * 256) != hipSuccess ||
       hipMalloc(&A->dict_val, sizeof(double) * 256) != hipSuccess)
     fail(MLAMG_ENOMEM, "out of device memory");
@@ -708,12 +763,16 @@ static int build_sell_dict(mlamg_csr* A, hipStream_t s, int sigma) {
        hipMemsetAsync(vtab, 0xFF, sizeof(unsigned long long) * kDictSlots, s) != hipSuccess ||
        hipMemsetAsync(counts, 0, sizeof(int32_t) * 4, s) != hipSuccess ||
        hipMemsetAsync(A->dict_off, 0, sizeof(int32_t) * 256, s) != hipSuccess ||
-       hipMemsetAsync(A->dict_val, 0, sizeof(double) * 256, s) != hipSuccess))
+       hipMemsetAsync(A->dict_val, 0, sizeof(double) * 256, s) != hipSuccess ||
+       hipMemsetD16Async((hipDeviceptr_t)A->dict_code, 0x00FF, (size_t)std::max<int64_t>(n_codes, 8),
+                         s) != hipSuccess ||
+       hipMemcpyAsync(A->dict_ptr, hdp.data(), sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice,
+                      s) != hipSuccess))
     fail(MLAMG_EHIP, "memset");
   if (rc == MLAMG_OK && ns)
     hipLaunchKernelGGL(k_dict_pass, dim3((ns + 3) / 4), dim3(256), 0, s, A->sell_ptr, A->sell_col,
                        A->sell_val, A->sell_perm, A->n_rows, ns, 0, otab, vtab, counts, oidx,
-                       vidx, A->dict_code);
+                       vidx, A->dict_ptr, A->dict_code);
   std::vector<unsigned long long> ho(kDictSlots), hv(kDictSlots);
   int32_t hc[4] = {0, 0, 0, 0};
   if (rc == MLAMG_OK &&
@@ -756,7 +815,7 @@ static int build_sell_dict(mlamg_csr* A, hipStream_t s, int sigma) {
     if (rc == MLAMG_OK && ns)
       hipLaunchKernelGGL(k_dict_pass, dim3((ns + 3) / 4), dim3(256), 0, s, A->sell_ptr,
                          A->sell_col, A->sell_val, A->sell_perm, A->n_rows, ns, 1, otab, vtab,
-                         counts, oidx, vidx, A->dict_code);
+                         counts, oidx, vidx, A->dict_ptr, A->dict_code);
     if (rc == MLAMG_OK && (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess))
       fail(MLAMG_EHIP, "encode");
   }
@@ -766,6 +825,9 @@ static int build_sell_dict(mlamg_csr* A, hipStream_t s, int sigma) {
     drop_sell(A);
     return rc;
   }
+  // one partial per workgroup of dict_slices_per_wave() * 4 slices
+  A->n_part = (int32_t)std::max<int64_t>(1, (ns + 4 * dict_slices_per_wave() - 1) /
+                                                (4 * dict_slices_per_wave()));
   // the coded copy replaces the SELL arrays
   (void)hipFree(A->sell_col);
   (void)hipFree(A->sell_val);
@@ -1139,6 +1201,28 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
     default:
       MLAMG_REQUIRE(false, "unknown format");
   }
+  return MLAMG_OK;
+}
+
+int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
+  MLAMG_REQUIRE(A && bytes, "NULL argument");
+  const double n = (double)A->n_rows, m = (double)A->n_cols;
+  double b = 8.0 * m + 8.0 * n;  // x read once, y written once
+  if (A->vec_width) {
+    b += 12.0 * A->nnz + 4.0 * (n + 1);
+  } else if (A->srt_pk) {
+    b += 12.0 * A->nnz + 4.0 * (n + 1) + 4.0 * (A->srt_nb + 1) + 12.0 * A->srt_nb;
+  } else if (A->dict_code) {
+    int64_t n_codes = 0;
+    MLAMG_HIP(hipMemcpy(&n_codes, A->dict_ptr + A->n_slices, sizeof(int64_t), hipMemcpyDeviceToHost));
+    b += 2.0 * n_codes + 8.0 * (A->n_slices + 1) + (A->sell_perm ? 4.0 * n : 0.0) +
+         256.0 * 12.0;
+  } else if (A->sell_ptr) {
+    b += 12.0 * A->sell_elems + 8.0 * (A->n_slices + 1) + (A->sell_perm ? 4.0 * n : 0.0);
+  } else {
+    b += 12.0 * A->nnz + 4.0 * (n + 1);
+  }
+  *bytes = b;
   return MLAMG_OK;
 }
 

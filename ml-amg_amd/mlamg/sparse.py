@@ -150,6 +150,12 @@ class DeviceCSR:
         name = {v: k for k, v in self.FORMATS.items()}[f.value]
         return name, int(vw.value), int(st.value)
 
+    def format_bytes(self):
+        """Algorithmic HBM bytes of one y = A@x in the active storage format."""
+        b = ctypes.c_double()
+        call("mlamg_csr_format_bytes", self.handle, ctypes.byref(b))
+        return float(b.value)
+
     def diag_inv(self, omega=1.0):
         d = torch.empty(self.shape[0], dtype=torch.float64, device=_device())
         call("mlamg_diag_inv", self.handle, omega, ptr(d), stream_ptr())

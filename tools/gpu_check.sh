@@ -30,9 +30,12 @@ fi
 if [ "$MODE" = prof ]; then
   rm -rf $OUT/prof
   step rocprof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python bench.py --steps 30 --warmup 3 --no-cpu-baseline
+  export MLAMG_FMT=sell_dict
   step rocprof_spmv 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o spmv -- python tools/spmv_driver.py
+  unset MLAMG_FMT
+  step pmc_dict 600 python tools/pmc_traffic.py ${ROUND:-r01} sell_dict
   step pmc_sell 600 python tools/pmc_traffic.py ${ROUND:-r01} sell
-  step pmc_csr 600 python tools/pmc_traffic.py ${ROUND:-r01} csr_stream
+  step pmc_sorted 600 python tools/pmc_traffic.py ${ROUND:-r01} sorted
 fi
 if [ "$MODE" = dist ]; then
   step bench_dist1 900 python bench.py --dist --steps 30 --warmup 3

@@ -21,7 +21,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out", "pmc")
-KERNELS = {"csr_stream": "k_csr_stream", "sell": "k_sell"}
+KERNELS = {"csr_stream": "k_csr_stream", "sell": "k_sell<", "sorted": "k_sorted",
+           "sell_dict": "k_sell_dict"}
 
 
 def run_pass(counter, fmt):
@@ -43,14 +44,15 @@ def run_pass(counter, fmt):
             for row in csv.DictReader(fh):
                 if KERNELS[fmt] in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
-    return vals, files
+    drv = [ln for ln in r.stdout.splitlines() if ln.startswith("spmv_driver:")]
+    return vals, files, (drv[-1] if drv else "")
 
 
 def main():
     round_tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     fmt = sys.argv[2] if len(sys.argv) > 2 else "sell"
-    fetch, f1 = run_pass("FETCH_SIZE", fmt)
-    write, f2 = run_pass("WRITE_SIZE", fmt)
+    fetch, f1, drv = run_pass("FETCH_SIZE", fmt)
+    write, f2, _ = run_pass("WRITE_SIZE", fmt)
     if not fetch or not write:
         raise RuntimeError("no dispatches of the SpMV kernel found in the counter CSVs")
     # skip the first (cold) dispatch
@@ -62,7 +64,8 @@ def main():
     write_bytes = write_kib * 1024.0
     n = 216 ** 3
     nnz = 70263936
-    algo = 12.0 * nnz + 4.0 * (n + 1) + 8.0 * n + 8.0 * n
+    csr_algo = 12.0 * nnz + 4.0 * (n + 1) + 8.0 * n + 8.0 * n
+    algo = float(drv.split("format_bytes=")[1].split()[0]) if "format_bytes=" in drv else csr_algo
     res = {
         "kernel": f"{KERNELS[fmt]}<EPI_AXPBY> (fine-level SpMV, C4 216^3, format {fmt})",
         "format": fmt,
@@ -73,6 +76,8 @@ def main():
         "hbm_write_bytes_per_launch": write_bytes,
         "hbm_bytes_per_launch": read_bytes + write_bytes,
         "algorithmic_bytes_per_launch": algo,
+        "csr_algorithmic_bytes_per_launch": csr_algo,
+        "driver": drv,
         "traffic_over_algorithmic": (read_bytes + write_bytes) / algo,
         "dispatches": len(fetch),
     }

@@ -19,10 +19,17 @@ def main():
     A = DeviceCSR.from_scipy(problems.poisson_3d_7pt(n1), check=False).set_format(fmt)
     x = torch.randn(A.shape[1], dtype=torch.float64, device="cuda")
     y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
+    A.matvec(x, out=y)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     for _ in range(reps):
         A.matvec(x, out=y)
-    torch.cuda.synchronize()
-    print(f"spmv_driver: n={A.shape[0]} nnz={A.nnz} reps={reps} format={A.get_format()}")
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    print(f"spmv_driver: n={A.shape[0]} nnz={A.nnz} reps={reps} format={A.get_format()} "
+          f"avg {us:.1f} us format_bytes={A.format_bytes():.0f}")
 
 
 if __name__ == "__main__":
