@@ -107,6 +107,10 @@ struct mlamg_csr {
   int32_t* srt_base = nullptr;  // per block {lo, hi, split}: column windows of the sorted entries
   uint32_t* srt_pk = nullptr;
   double* srt_val = nullptr;
+  // value dictionary of the sorted copy (<= 256 distinct values, e.g. SA prolongators of
+  // constant-coefficient stencils): srt_vi[e] indexes srt_vtab and srt_val is dropped
+  uint8_t* srt_vi = nullptr;
+  double* srt_vtab = nullptr;
   // number of per-block partial sums a NORM launch writes with the active format
   int32_t n_part = 0;
 };

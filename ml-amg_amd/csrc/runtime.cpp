@@ -90,6 +90,8 @@ void csr_free(mlamg_csr* A) {
   if (A->srt_base) (void)hipFree(A->srt_base);
   if (A->srt_pk) (void)hipFree(A->srt_pk);
   if (A->srt_val) (void)hipFree(A->srt_val);
+  if (A->srt_vi) (void)hipFree(A->srt_vi);
+  if (A->srt_vtab) (void)hipFree(A->srt_vtab);
   delete A;
 }
 

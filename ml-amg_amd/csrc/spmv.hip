@@ -412,17 +412,24 @@ __global__ __launch_bounds__(kThreads) void k_csr_vec(const int32_t* __restrict_
 // cache lines instead of one per row neighbourhood (the x gather, not HBM, bounds long-row
 // operators: Galerkin A_l, R = P^T). Products are written to LDS at their CSR slot and phase 2
 // sums every row in stored order, so the result is bitwise k_csr_stream's (scipy's).
-template <int OP, bool NORM>
+// VD: values come from a <= 256-entry dictionary (one byte per nonzero instead of eight)
+template <int OP, bool NORM, bool VD>
 __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restrict__ indptr,
                                                         const uint32_t* __restrict__ pk,
                                                         const double* __restrict__ av,
+                                                        const uint8_t* __restrict__ vi,
+                                                        const double* __restrict__ vtab,
                                                         const int32_t* __restrict__ blk,
                                                         const int32_t* __restrict__ base,
                                                         const double* __restrict__ x, Epi ep) {
   __shared__ double prod[kSrtNnz];
   __shared__ int32_t rp[kSrtRows + 1];
   __shared__ double red[kSrtThreads / 64];
+  __shared__ double valt[VD ? 256 : 1];
   if (ep.done && *ep.done) return;
+  if constexpr (VD) {
+    if (threadIdx.x < 256) valt[threadIdx.x] = vtab[threadIdx.x];
+  }
   const int b = (int)xcd_block(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x;
   const int r0 = blk[b], r1 = blk[b + 1], nr = r1 - r0;
@@ -443,12 +450,20 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   for (int u = 0; u < U; ++u) {
     const int e = tid + u * kSrtThreads;
     w[u] = e < ne ? __builtin_nontemporal_load(pk + e0 + e) : kNone;
-    vv[u] = e < ne ? __builtin_nontemporal_load(av + e0 + e) : 0.0;
+    if constexpr (VD)
+      vv[u] = e < ne ? (double)__builtin_nontemporal_load(vi + e0 + e) : 0.0;  // index for now
+    else
+      vv[u] = e < ne ? __builtin_nontemporal_load(av + e0 + e) : 0.0;
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int cb = tid + u * kSrtThreads < split ? lo : hi;
     xv[u] = w[u] != kNone ? x[cb + (int)(w[u] >> kSrtPosBits)] : 0.0;
+  }
+  if constexpr (VD) {
+    __syncthreads();  // value table staged (the gathers above are already in flight)
+#pragma unroll
+    for (int u = 0; u < U; ++u) vv[u] = w[u] != kNone ? valt[(int)vv[u]] : 0.0;
   }
 #pragma unroll
   for (int u = 0; u < U; ++u)
@@ -520,8 +535,14 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_
   if (A->vec_width) return launch_vec<OP, NORM>(A, x, ep, s);
   if (A->srt_pk) {
     if (A->srt_nb == 0) return MLAMG_OK;
-    hipLaunchKernelGGL((k_sorted<OP, NORM>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s, A->indptr,
-                       A->srt_pk, A->srt_val, A->srt_blk, A->srt_base, x, ep);
+    if (A->srt_vi)
+      hipLaunchKernelGGL((k_sorted<OP, NORM, true>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s,
+                         A->indptr, A->srt_pk, A->srt_val, A->srt_vi, A->srt_vtab, A->srt_blk,
+                         A->srt_base, x, ep);
+    else
+      hipLaunchKernelGGL((k_sorted<OP, NORM, false>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s,
+                         A->indptr, A->srt_pk, A->srt_val, A->srt_vi, A->srt_vtab, A->srt_blk,
+                         A->srt_base, x, ep);
     MLAMG_HIP(hipGetLastError());
     return MLAMG_OK;
   }
@@ -905,17 +926,105 @@ __global__ __launch_bounds__(256) void k_srt_pack(const int32_t* __restrict__ ip
   }
 }
 
+__global__ void k_vdict_scan(const double* __restrict__ v, int64_t n, unsigned long long* vtab,
+                             int32_t* counts) {
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    if (((volatile int32_t*)counts)[1] > 256 || ((volatile int32_t*)counts)[2] != 0) return;
+    const unsigned long long key = (unsigned long long)__double_as_longlong(v[e]);
+    if (key == kDictEmpty || dict_slot(key, vtab, counts + 1, true) < 0) atomicAdd(counts + 2, 1);
+  }
+}
+
+__global__ void k_vdict_encode(const double* __restrict__ v, int64_t n, unsigned long long* vtab,
+                               const int32_t* __restrict__ vidx, uint8_t* __restrict__ out) {
+  const int64_t e = blockIdx.x * 256ll + threadIdx.x;
+  if (e >= n) return;
+  const unsigned long long key = (unsigned long long)__double_as_longlong(v[e]);
+  out[e] = (uint8_t)vidx[dict_slot(key, vtab, nullptr, false)];
+}
+
 static void drop_sorted(mlamg_csr* A) {
   if (A->srt_blk) (void)hipFree(A->srt_blk);
   if (A->srt_base) (void)hipFree(A->srt_base);
   if (A->srt_pk) (void)hipFree(A->srt_pk);
   if (A->srt_val) (void)hipFree(A->srt_val);
+  if (A->srt_vi) (void)hipFree(A->srt_vi);
+  if (A->srt_vtab) (void)hipFree(A->srt_vtab);
+  A->srt_vi = nullptr;
+  A->srt_vtab = nullptr;
   A->srt_blk = nullptr;
   A->srt_base = nullptr;
   A->srt_pk = nullptr;
   A->srt_val = nullptr;
   A->srt_nb = 0;
   if (!A->sell_ptr && !A->vec_width) A->n_part = A->n_blocks;
+}
+
+// Replace the sorted copy's fp64 values by one-byte indices into a table when the operator has
+// at most 256 distinct values (bit patterns). Returns EUNSUPPORTED (nothing changed) otherwise.
+static int sorted_value_dict(mlamg_csr* A, hipStream_t s) {
+  const int64_t nnz = A->nnz;
+  if (!A->srt_val || nnz == 0) return MLAMG_EUNSUPPORTED;
+  unsigned long long* vtab = nullptr;
+  int32_t *counts = nullptr, *vidx = nullptr;
+  uint8_t* vi = nullptr;
+  double* table = nullptr;
+  int rc = MLAMG_OK;
+  if (hipMalloc(&vtab, sizeof(unsigned long long) * kDictSlots) != hipSuccess ||
+      hipMalloc(&counts, sizeof(int32_t) * 4) != hipSuccess ||
+      hipMalloc(&vidx, sizeof(int32_t) * kDictSlots) != hipSuccess ||
+      hipMemsetAsync(vtab, 0xFF, sizeof(unsigned long long) * kDictSlots, s) != hipSuccess ||
+      hipMemsetAsync(counts, 0, sizeof(int32_t) * 4, s) != hipSuccess)
+    rc = MLAMG_ENOMEM;
+  std::vector<unsigned long long> hv(kDictSlots);
+  int32_t hc[4] = {0, 0, 0, 0};
+  if (rc == MLAMG_OK) {
+    const int64_t nb = std::min<int64_t>((nnz + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_vdict_scan, dim3((unsigned)nb), dim3(256), 0, s, A->srt_val, nnz, vtab,
+                       counts);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(hv.data(), vtab, sizeof(unsigned long long) * kDictSlots,
+                       hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(hc, counts, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = MLAMG_EHIP;
+  }
+  if (rc == MLAMG_OK && (hc[2] != 0 || hc[1] > 256)) rc = MLAMG_EUNSUPPORTED;
+  if (rc == MLAMG_OK) {
+    std::vector<std::pair<unsigned long long, int>> vs;
+    for (int i = 0; i < kDictSlots; ++i)
+      if (hv[i] != kDictEmpty) vs.push_back({hv[i], i});
+    std::sort(vs.begin(), vs.end());
+    std::vector<int32_t> hvi(kDictSlots, 0);
+    std::vector<double> valt(256, 0.0);
+    for (size_t k = 0; k < vs.size(); ++k) {
+      hvi[vs[k].second] = (int32_t)k;
+      std::memcpy(&valt[k], &vs[k].first, sizeof(double));
+    }
+    if (hipMalloc(&vi, (size_t)nnz) != hipSuccess || hipMalloc(&table, sizeof(double) * 256) != hipSuccess)
+      rc = MLAMG_ENOMEM;
+    if (rc == MLAMG_OK &&
+        (hipMemcpyAsync(vidx, hvi.data(), sizeof(int32_t) * kDictSlots, hipMemcpyHostToDevice, s) != hipSuccess ||
+         hipMemcpyAsync(table, valt.data(), sizeof(double) * 256, hipMemcpyHostToDevice, s) != hipSuccess))
+      rc = MLAMG_EHIP;
+    if (rc == MLAMG_OK) {
+      hipLaunchKernelGGL(k_vdict_encode, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s,
+                         A->srt_val, nnz, vtab, vidx, vi);
+      if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) rc = MLAMG_EHIP;
+    }
+  }
+  for (void* p : {(void*)vtab, (void*)counts, (void*)vidx})
+    if (p) (void)hipFree(p);
+  if (rc != MLAMG_OK) {
+    if (vi) (void)hipFree(vi);
+    if (table) (void)hipFree(table);
+    return rc;
+  }
+  (void)hipFree(A->srt_val);
+  A->srt_val = nullptr;
+  A->srt_vi = vi;
+  A->srt_vtab = table;
+  return MLAMG_OK;
 }
 
 // Row blocks of <= kSrtRows rows / <= kSrtNnz nonzeros; inside each, entries radix-sorted by
@@ -1003,6 +1112,7 @@ static int build_sorted(mlamg_csr* A, hipStream_t s) {
   }
   A->srt_nb = nb;
   A->n_part = nb;
+  (void)sorted_value_dict(A, s);  // optional: keeps the fp64 values when it does not apply
   return MLAMG_OK;
 }
 
@@ -1211,7 +1321,8 @@ int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
   if (A->vec_width) {
     b += 12.0 * A->nnz + 4.0 * (n + 1);
   } else if (A->srt_pk) {
-    b += 12.0 * A->nnz + 4.0 * (n + 1) + 4.0 * (A->srt_nb + 1) + 12.0 * A->srt_nb;
+    b += (A->srt_vi ? 5.0 : 12.0) * A->nnz + 4.0 * (n + 1) + 4.0 * (A->srt_nb + 1) +
+         12.0 * A->srt_nb;
   } else if (A->dict_code) {
     int64_t n_codes = 0;
     MLAMG_HIP(hipMemcpy(&n_codes, A->dict_ptr + A->n_slices, sizeof(int64_t), hipMemcpyDeviceToHost));
@@ -1234,7 +1345,9 @@ int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* 
                 : A->sell_ptr  ? MLAMG_FMT_SELL
                                : MLAMG_FMT_CSR_STREAM;
   if (fmt) *fmt = f;
-  if (vec_width) *vec_width = A->vec_width ? A->vec_width : (A->srt_pk ? 0 : A->sell_sigma);
+  // SORTED reports 1 in vec_width when its values are dictionary-coded
+  if (vec_width)
+    *vec_width = A->vec_width ? A->vec_width : (A->srt_pk ? (A->srt_vi ? 1 : 0) : A->sell_sigma);
   if (stored) *stored = A->sell_ptr ? A->sell_elems : A->nnz;
   return MLAMG_OK;
 }

@@ -144,6 +144,34 @@ def test_sorted_format_ragged_and_limits(ml, torch_cuda):
     assert np.array_equal(W3d.matvec(dev(torch, xw)).cpu().numpy(), W3 @ xw)
 
 
+def test_sorted_value_dictionary(ml, torch_cuda):
+    """sorted format with <= 256 distinct values codes them in one byte (SA prolongator of a
+    constant-coefficient stencil: 10 values); products and order unchanged."""
+    torch = torch_cuda
+    A = ml.problems.poisson_3d_7pt(16)
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=100, fine_format="csr_stream")
+    P = H.levels[0].P.to_scipy()
+    assert len(np.unique(P.data)) <= 256
+    Pd = ml.sparse.DeviceCSR.from_scipy(P).set_format("sorted")
+    assert Pd.get_format()[:2] == ("sorted", 1)
+    rs = np.random.RandomState(3)
+    e = rs.randn(P.shape[1])
+    ed = dev(torch, e)
+    assert np.array_equal(Pd.matvec(ed).cpu().numpy(), P @ e)
+    R = P.T.tocsr()
+    R.sort_indices()
+    Rd = ml.sparse.DeviceCSR.from_scipy(R).set_format("sorted")
+    assert Rd.get_format()[:2] == ("sorted", 1)
+    r = rs.randn(R.shape[1])
+    assert np.array_equal(Rd.matvec(dev(torch, r)).cpu().numpy(), R @ r)
+    # many distinct values: plain fp64 values
+    Q = sp.random(400, 300, density=0.05, random_state=rs, format="csr")
+    Qd = ml.sparse.DeviceCSR.from_scipy(Q).set_format("sorted")
+    assert Qd.get_format()[:2] == ("sorted", 0)
+    q = rs.randn(300)
+    assert np.array_equal(Qd.matvec(dev(torch, q)).cpu().numpy(), Q @ q)
+
+
 def test_sell_dict_format(ml, torch_cuda):
     """Dictionary-coded SELL: bitwise CSR order on a stencil (ragged boundary rows, sigma
     orders), every epilogue through the hierarchy, and refusal past 255 offsets / 256 values."""
