@@ -299,7 +299,8 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
     e1.record(s)
     e1.synchronize()
     t_spmv = e0.elapsed_time(e1) / 1000.0 / 50
-    B = 12.0 * D.A_loc.nnz + 4.0 * (D.n_own + 1) + 8.0 * D.n_ext + 8.0 * D.n_own
+    B = D.A_loc.format_bytes()  # bytes the chosen storage format streams for y = A_loc x_ext
+    B_csr = 12.0 * D.A_loc.nnz + 4.0 * (D.n_own + 1) + 8.0 * D.n_ext + 8.0 * D.n_own
     achieved = B / t_spmv / 1e9
     achieved_min = _max(-achieved, world) * -1.0  # slowest rank
     if rank == 0:
@@ -330,7 +331,8 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
                                     "(slowest rank)",
                 "achieved": round(achieved_min, 1), "peak": hbm_peak, "unit": "GB/s",
                 "frac": round(achieved_min / hbm_peak, 4), "traffic": None,
-                "algorithmic_bytes_per_launch": B, "avg_launch_us": round(t_spmv * 1e6, 2),
+                "algorithmic_bytes_per_launch": B, "csr_algorithmic_bytes_per_launch": B_csr,
+                "avg_launch_us": round(t_spmv * 1e6, 2),
             },
         }
         print(json.dumps(out), flush=True)
