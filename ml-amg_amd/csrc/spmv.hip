@@ -388,7 +388,22 @@ __global__ __launch_bounds__(kThreads) void k_csr_vec(const int32_t* __restrict_
   double s = 0.0;
   if (row < n_rows) {
     const int a = indptr[row], b = indptr[row + 1];
-    for (int k = a + l; k < b; k += VW) s += vals[k] * x[indices[k]];
+    // 4 strided entries per lane per step, loads issued together, summed in the same order
+    for (int k = a + l; k < b; k += 4 * VW) {
+      int32_t cc[4];
+      double vv[4], xv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = k + u * VW;
+        cc[u] = e < b ? __builtin_nontemporal_load(indices + e) : -1;
+        vv[u] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (cc[u] >= 0) s += vv[u] * xv[u];
+    }
   }
 #pragma unroll
   for (int off = VW / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, VW);
