@@ -391,7 +391,8 @@ static int correct(mlamg_dhier* D, size_t l, double* x_ext, const int32_t* done,
   MLAMG_TRY(halo_exchange_impl(L.hr, L.r_ext, s));
   if (L.hp) {
     DLevel& N = D->lv[l + 1];
-    MLAMG_TRY(spmv_set(L.R, L.r_ext, N.b, done, s));
+    // restriction fused with the next level's zero-guess sweep (x = Dinv_w b on owned rows)
+    MLAMG_TRY(spmv_set(L.R, L.r_ext, N.b, done, s, N.x_ext, N.dinv));
     double* xn = nullptr;
     MLAMG_TRY(dcycle_below(D, l + 1, &xn, s));
     MLAMG_HIP(hipMemcpyAsync(L.xp_ext, xn, sizeof(double) * N.n_own, hipMemcpyDeviceToDevice, s));
@@ -414,7 +415,7 @@ static int correct(mlamg_dhier* D, size_t l, double* x_ext, const int32_t* done,
 static int dcycle_below(mlamg_dhier* D, size_t l, double** x_out, hipStream_t s) {
   const int32_t* done = D->flags + 1;
   DLevel& L = D->lv[l];
-  MLAMG_TRY(jacobi_from_zero(L.x_ext, L.dinv, L.b, L.n_own, done, s));
+  // x = Dinv_w b was written by the restriction kernel of the level above (correct())
   MLAMG_TRY(halo_exchange_impl(L.hx, L.x_ext, s));
   MLAMG_TRY(residual_impl(L.A, L.b, L.x_ext, L.r_ext, nullptr, nullptr, nullptr,
                           const_cast<int32_t*>(done), 0.0, nullptr, nullptr, nullptr, s));

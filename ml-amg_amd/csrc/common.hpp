@@ -177,7 +177,8 @@ int residual_partials(const mlamg_csr* A, const double* b, const double* x, doub
 int jacobi_sweep(const mlamg_csr* A, const double* dinv, const double* b, const double* xin,
                  double* xout, bool explicit_form, const int32_t* done, hipStream_t s);
 int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
-int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
+int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s,
+             double* smooth_x = nullptr, const double* smooth_dinv = nullptr);
 int jacobi_from_residual(double* x, const double* dinv, const double* r, int64_t n,
                          const int32_t* done, hipStream_t s);
 int jacobi_from_zero(double* x, const double* dinv, const double* b, int64_t n,

@@ -132,8 +132,10 @@ static int smooth(const Level& L, const double* b, double*& cur, double* other, 
   return MLAMG_OK;
 }
 
-// one V-cycle below the finest level; result pointer returned through `res`
-static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, hipStream_t s) {
+// one V-cycle below the finest level; result pointer returned through `res`. presmoothed: the
+// caller's restriction kernel already wrote the first zero-guess sweep x = Dinv_w b into L.x.
+static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, hipStream_t s,
+                        bool presmoothed = false) {
   const int32_t* done = H->flags + 1;
   if (l == H->lv.size()) {
     MLAMG_TRY(dense_solve_impl(H->D, b, H->xc, done, s));
@@ -144,7 +146,7 @@ static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, 
   double* cur = L.x;
   double* other = L.tmp;
   if (H->nu_pre > 0) {
-    MLAMG_TRY(jacobi_from_zero(cur, L.dinv, b, L.n, done, s));
+    if (!presmoothed) MLAMG_TRY(jacobi_from_zero(cur, L.dinv, b, L.n, done, s));
     MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre - 1, done, s));
     MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, const_cast<int32_t*>(done),
                             0.0, nullptr, nullptr, nullptr, s));
@@ -152,10 +154,15 @@ static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, 
     MLAMG_HIP(hipMemsetAsync(cur, 0, sizeof(double) * L.n, s));
     MLAMG_HIP(hipMemcpyAsync(L.r, b, sizeof(double) * L.n, hipMemcpyDeviceToDevice, s));
   }
-  double* bn = (l + 1 == H->lv.size()) ? H->bc : H->lv[l + 1].b;
-  MLAMG_TRY(spmv_set(L.R, L.r, bn, done, s));
+  const bool fuse_next = l + 1 < H->lv.size() && H->nu_pre > 0;
+  double* bn = fuse_next ? H->lv[l + 1].b : H->bc;
+  if (fuse_next) {
+    MLAMG_TRY(spmv_set(L.R, L.r, bn, done, s, H->lv[l + 1].x, H->lv[l + 1].dinv));
+  } else {
+    MLAMG_TRY(spmv_set(L.R, L.r, bn, done, s));
+  }
   double* xn = nullptr;
-  MLAMG_TRY(cycle_coarse(H, l + 1, bn, &xn, s));
+  MLAMG_TRY(cycle_coarse(H, l + 1, bn, &xn, s, fuse_next));
   MLAMG_TRY(spmv_add(L.P, xn, cur, done, s));
   other = (cur == L.x) ? L.tmp : L.x;
   MLAMG_TRY(smooth(L, b, cur, other, H->nu_post, done, s));
@@ -192,10 +199,15 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
     MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, done, 0.0, nullptr,
                             nullptr, nullptr, s));
   }
-  double* bn = (H->lv.size() == 1) ? H->bc : H->lv[1].b;
-  MLAMG_TRY(spmv_set(L.R, L.r, bn, done, s));
+  const bool fuse_next = H->lv.size() > 1 && H->nu_pre > 0;
+  double* bn = fuse_next ? H->lv[1].b : H->bc;
+  if (fuse_next) {
+    MLAMG_TRY(spmv_set(L.R, L.r, bn, done, s, H->lv[1].x, H->lv[1].dinv));
+  } else {
+    MLAMG_TRY(spmv_set(L.R, L.r, bn, done, s));
+  }
   double* xn = nullptr;
-  MLAMG_TRY(cycle_coarse(H, 1, bn, &xn, s));
+  MLAMG_TRY(cycle_coarse(H, 1, bn, &xn, s, fuse_next));
   MLAMG_TRY(spmv_add(L.P, xn, cur, done, s));
   other = (cur == x) ? L.tmp : x;
   MLAMG_TRY(smooth(L, b, cur, other, H->nu_post, done, s));
@@ -368,7 +380,9 @@ int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes) {
     const double res = spmv_bytes(L.A) + 8.0 * n;   // + b
     const bool fused = l == 0 && fused_presmooth(H);
     if (H->nu_pre > 0) {
-      if (!fused) t += (l == 0) ? 32.0 * n : 24.0 * n;  // first sweep: elementwise
+      // first sweep: elementwise at the top (unless fused into the cycle end); below, fused
+      // into the restriction kernel above (+ read dinv, write x)
+      if (!fused) t += (l == 0) ? 32.0 * n : 16.0 * n;
       t += (H->nu_pre - 1) * jac + res;
     }
     t += spmv_bytes(L.R);

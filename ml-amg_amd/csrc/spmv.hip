@@ -48,6 +48,7 @@ __device__ __forceinline__ EpiIn epi_load(int row, const Epi& e) {
   EpiIn v;
   if constexpr (OP == EPI_AXPBY) {
     if (e.beta != 0.0) v.a = e.y[row];
+    if (e.copy_to) v.c = e.dinv[row];
   } else if constexpr (OP == EPI_RESID) {
     v.a = e.b[row];
     if (e.copy_to) {
@@ -67,11 +68,15 @@ __device__ __forceinline__ EpiIn epi_load(int row, const Epi& e) {
 template <int OP>
 __device__ __forceinline__ double epi_store(int row, double s, const EpiIn& v, const Epi& e) {
   if constexpr (OP == EPI_AXPBY) {
+    double y;
     if (e.beta == 0.0) {
-      e.y[row] = (e.alpha == 1.0) ? s : e.alpha * s;
+      y = (e.alpha == 1.0) ? s : e.alpha * s;
     } else {
-      e.y[row] = e.alpha * s + e.beta * v.a;
+      y = e.alpha * s + e.beta * v.a;
     }
+    e.y[row] = y;
+    // restriction fused with the next level's zero-guess sweep: x = Dinv_w * b (0 + d*(b - 0))
+    if (e.copy_to) e.copy_to[row] = v.c * y;
     return 0.0;
   } else if constexpr (OP == EPI_RESID) {
     const double r = v.a - s;
@@ -1201,12 +1206,17 @@ int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done
   return launch<EPI_ADD, false>(A, x, ep, s);
 }
 
-int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s) {
+int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s,
+             double* smooth_x, const double* smooth_dinv) {
   Epi ep{};
   ep.alpha = 1.0;
   ep.beta = 0.0;
   ep.y = y;
   ep.done = done;
+  if (smooth_x) {
+    ep.copy_to = smooth_x;  // smooth_x = smooth_dinv * y as well
+    ep.dinv = smooth_dinv;
+  }
   return launch<EPI_AXPBY, false>(A, x, ep, s);
 }
 
