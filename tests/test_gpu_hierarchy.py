@@ -172,6 +172,34 @@ def test_sorted_value_dictionary(ml, torch_cuda):
     assert np.array_equal(Qd.matvec(dev(torch, q)).cpu().numpy(), Q @ q)
 
 
+def test_graph_recaptured_after_format_change(ml, torch_cuda):
+    """A captured cycle graph bakes in kernels and format arrays: changing an operator's format
+    must force a re-capture (format epoch), and the iterate stays bitwise the same."""
+    torch = torch_cuda
+    A = ml.problems.poisson_3d_7pt(20)
+    n = A.shape[0]
+    rs = np.random.RandomState(4)
+    x0, b = rs.randn(n), rs.randn(n)
+    bd = dev(torch, b)
+    # exact-order formats only, so every storage gives the same bits
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=100, coarse_format="exact")
+    ref = dev(torch, x0)
+    h_ref = H.cycle(bd, ref, 4, use_graph=False)
+    for fmt in ("csr_stream", "sell_dict", "sorted", "sell"):
+        x = dev(torch, x0)
+        H.cycle(bd, x, 1, use_graph=True)   # capture with the current formats
+        for L in H.levels:                  # then swap every operator's storage
+            for M in (L.A, L.P, L.R):
+                try:
+                    M.set_format(fmt)
+                except Exception:
+                    M.set_format("csr_stream")
+        x = dev(torch, x0)
+        h = H.cycle(bd, x, 4, use_graph=True)
+        assert torch.equal(x, ref), fmt
+        assert np.allclose(h, h_ref, rtol=1e-14, atol=0)
+
+
 def test_sell_dict_format(ml, torch_cuda):
     """Dictionary-coded SELL: bitwise CSR order on a stencil (ragged boundary rows, sigma
     orders), every epilogue through the hierarchy, and refusal past 255 offsets / 256 values."""
