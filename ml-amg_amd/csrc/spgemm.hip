@@ -18,6 +18,10 @@
 //    downstream (they are the summation orders of the next product) and are reproduced here.
 #include "common.hpp"
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 #include <rocprim/rocprim.hpp>
 
 namespace mlamg {
@@ -214,10 +218,12 @@ __global__ void k_scatter_rows(const int64_t* __restrict__ off, const int32_t* _
 
 struct DevBuf {
   std::vector<void*> ptrs;
-  ~DevBuf() {
+  void release() {
     for (void* p : ptrs)
       if (p) (void)hipFree(p);
+    ptrs.clear();
   }
+  ~DevBuf() { release(); }
   template <class T>
   hipError_t get(T** p, size_t count) {
     *p = nullptr;
@@ -251,54 +257,121 @@ __global__ void k_prod_len(const int32_t* __restrict__ aj, const int32_t* __rest
   len[k] = bp[j + 1] - bp[j];
 }
 
-__global__ void k_expand_entries(const int32_t* __restrict__ rows, const int32_t* __restrict__ aj,
-                                 const double* __restrict__ ax, const int32_t* __restrict__ bp,
-                                 const int32_t* __restrict__ bj, const double* __restrict__ bx,
-                                 int64_t nnz, const int64_t* __restrict__ poff, int cbits,
-                                 uint64_t* __restrict__ keys, double* __restrict__ vals) {
-  int64_t k = blockIdx.x * 256ll + threadIdx.x;
-  if (k >= nnz) return;
-  const uint64_t hi = (uint64_t)(uint32_t)rows[k] << cbits;
-  const int j = aj[k];
-  const double v = ax[k];
-  int64_t o = poff[k];
-  for (int kk = bp[j]; kk < bp[j + 1]; ++kk, ++o) {
-    keys[o] = hi | (uint32_t)bj[kk];
-    vals[o] = v * bx[kk];
+// Block-cooperative expansion: a workgroup owns 256 consecutive nonzeros of A, whose products
+// form one contiguous output range [poff[k0], poff[k0+256]); every thread walks that range with
+// stride 256 (coalesced key/value stores), finding its nonzero by binary search in LDS.
+__global__ __launch_bounds__(256) void k_expand_entries(const int32_t* __restrict__ rows,
+                                                        const int32_t* __restrict__ aj,
+                                                        const double* __restrict__ ax,
+                                                        const int32_t* __restrict__ bp,
+                                                        const int32_t* __restrict__ bj,
+                                                        const double* __restrict__ bx, int64_t nnz,
+                                                        const int64_t* __restrict__ poff, int cbits,
+                                                        uint64_t* __restrict__ keys,
+                                                        double* __restrict__ vals) {
+  __shared__ int64_t off[257];
+  __shared__ int32_t bstart[256];
+  __shared__ uint64_t hi[256];
+  __shared__ double av[256];
+  const int64_t k0 = (int64_t)blockIdx.x * 256;
+  const int cnt = (int)std::min<int64_t>(256, nnz - k0);
+  const int t = threadIdx.x;
+  if (t < cnt) {
+    const int64_t k = k0 + t;
+    off[t] = poff[k];
+    const int j = aj[k];
+    bstart[t] = bp[j];
+    hi[t] = (uint64_t)(uint32_t)rows[k] << cbits;
+    av[t] = ax[k];
+  }
+  if (t == 0) off[cnt] = poff[k0 + cnt];
+  __syncthreads();
+  const int64_t o0 = off[0], o1 = off[cnt];
+  for (int64_t o = o0 + t; o < o1; o += 256) {
+    int lo = 0, up = cnt;  // largest i with off[i] <= o
+    while (up - lo > 1) {
+      const int mid = (lo + up) >> 1;
+      if (off[mid] <= o) lo = mid;
+      else up = mid;
+    }
+    const int kk = bstart[lo] + (int)(o - off[lo]);
+    keys[o] = hi[lo] | (uint32_t)bj[kk];
+    vals[o] = av[lo] * bx[kk];
   }
 }
 
-__global__ void k_run_sums(const uint64_t* __restrict__ keys, const double* __restrict__ vals,
-                           int64_t total, double* __restrict__ sums, int32_t* __restrict__ keep) {
-  int64_t e = blockIdx.x * 256ll + threadIdx.x;
-  if (e >= total) return;
-  const uint64_t key = keys[e];
-  if (e > 0 && keys[e - 1] == key) {
-    keep[e] = 0;
-    return;
+// Run sums over LDS chunks of 2048 sorted products: run heads sum their run left to right
+// (continuing in global memory when a run crosses the chunk end); keep = sum != 0.
+__global__ __launch_bounds__(256) void k_run_sums(const uint64_t* __restrict__ keys,
+                                                  const double* __restrict__ vals, int64_t total,
+                                                  double* __restrict__ sums,
+                                                  int32_t* __restrict__ keep) {
+  constexpr int C = 2048;
+  __shared__ uint64_t kk[C];
+  __shared__ double vv[C];
+  const int64_t c0 = (int64_t)blockIdx.x * C;
+  const int m = (int)std::min<int64_t>(C, total - c0);
+  for (int i = threadIdx.x; i < m; i += 256) {
+    kk[i] = keys[c0 + i];
+    vv[i] = vals[c0 + i];
   }
-  double acc = 0.0;
-  for (int64_t f = e; f < total && keys[f] == key; ++f) acc += vals[f];
-  sums[e] = acc;
-  keep[e] = acc != 0.0 ? 1 : 0;
+  const uint64_t before = c0 > 0 ? keys[c0 - 1] : ~0ull;
+  __syncthreads();
+  for (int i = threadIdx.x; i < m; i += 256) {
+    const uint64_t key = kk[i];
+    const bool head = i > 0 ? kk[i - 1] != key : (c0 == 0 || before != key);
+    if (!head) {
+      keep[c0 + i] = 0;
+      continue;
+    }
+    double acc = 0.0;
+    int f = i;
+    for (; f < m && kk[f] == key; ++f) acc += vv[f];
+    if (f == m)  // the run may continue into the next chunk
+      for (int64_t g = c0 + m; g < total && keys[g] == key; ++g) acc += vals[g];
+    sums[c0 + i] = acc;
+    keep[c0 + i] = acc != 0.0 ? 1 : 0;
+  }
 }
 
 __global__ void k_emit(const uint64_t* __restrict__ keys, const double* __restrict__ sums,
                        const int32_t* __restrict__ keep, const int32_t* __restrict__ pos,
                        int64_t total, int cbits, int32_t* __restrict__ cj,
-                       double* __restrict__ cx, int32_t* __restrict__ rowcnt) {
+                       double* __restrict__ cx, int32_t* __restrict__ crow) {
   int64_t e = blockIdx.x * 256ll + threadIdx.x;
   if (e >= total || !keep[e]) return;
   const uint64_t key = keys[e];
   const int32_t p = pos[e];
   cj[p] = (int32_t)(key & ((uint64_t(1) << cbits) - 1));
   cx[p] = sums[e];
-  atomicAdd(&rowcnt[key >> cbits], 1);
+  crow[p] = (int32_t)(key >> cbits);
+}
+
+// indptr from the (row-sorted) output rows: entry p opens rows crow[p-1]+1 .. crow[p]
+__global__ void k_rowptr(const int32_t* __restrict__ crow, int64_t nnz, int64_t n,
+                         int32_t* __restrict__ indptr) {
+  const int64_t p = blockIdx.x * 256ll + threadIdx.x;
+  if (p > nnz) return;
+  const int64_t r0 = p > 0 ? crow[p - 1] + 1 : 0;
+  const int64_t r1 = p < nnz ? crow[p] : n;
+  for (int64_t r = r0; r <= r1; ++r) indptr[r] = (int32_t)p;
 }
 
 static int spgemm_sorted_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out,
                               int rbits, int cbits, hipStream_t s) {
   const int64_t n = A->n_rows, nz = A->nnz;
+  // MLAMG_TIMING=1: per-phase wall times on stderr (syncs the stream at each phase)
+  static const bool timing = std::getenv("MLAMG_TIMING") != nullptr;
+  auto t_prev = std::chrono::steady_clock::now();
+  auto tick = [&](const char* what) {
+    if (!timing) return;
+    (void)hipDeviceSynchronize();
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[spgemm %lldx%lld nnzA=%lld] %-8s %8.2f ms\n", (long long)n,
+                 (long long)B->n_cols, (long long)nz, what,
+                 std::chrono::duration<double, std::milli>(t - t_prev).count());
+    t_prev = t;
+  };
   DevBuf db;
   int32_t* rows = nullptr;
   int64_t *len = nullptr, *poff = nullptr;
@@ -314,9 +387,11 @@ static int spgemm_sorted_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr*
   DB_CHECK(hipMemcpyAsync(&total, poff + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   DB_CHECK(hipStreamSynchronize(s));
   MLAMG_REQUIRE(total < (int64_t(1) << 31) - 1, "too many intermediate products (>2G)");
+  tick("count");
+  if (timing) std::fprintf(stderr, "[spgemm] products %lld\n", (long long)total);
   uint64_t *k0 = nullptr, *k1 = nullptr;
   double *v0 = nullptr, *v1 = nullptr, *sums = nullptr;
-  int32_t *keep = nullptr, *pos = nullptr, *rowcnt = nullptr;
+  int32_t *keep = nullptr, *pos = nullptr, *crow = nullptr;
   DB_CHECK(db.get(&k0, total));
   DB_CHECK(db.get(&k1, total));
   DB_CHECK(db.get(&v0, total));
@@ -324,11 +399,11 @@ static int spgemm_sorted_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr*
   DB_CHECK(db.get(&sums, total));
   DB_CHECK(db.get(&keep, total + 1));
   DB_CHECK(db.get(&pos, total + 1));
-  DB_CHECK(db.get(&rowcnt, n + 1));
-  DB_CHECK(hipMemsetAsync(rowcnt, 0, sizeof(int32_t) * (n + 1), s));
+  tick("alloc");
   if (nz)
-    hipLaunchKernelGGL(k_expand_entries, dim3((nz + 255) / 256), dim3(256), 0, s, rows,
+    hipLaunchKernelGGL(k_expand_entries, dim3((unsigned)((nz + 255) / 256)), dim3(256), 0, s, rows,
                        A->indices, A->data, B->indptr, B->indices, B->data, nz, poff, cbits, k0, v0);
+  tick("expand");
   if (total > 0) {
     size_t tb = 0;
     DB_CHECK(rocprim::radix_sort_pairs(nullptr, tb, k0, k1, v0, v1, (size_t)total, 0,
@@ -337,19 +412,153 @@ static int spgemm_sorted_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr*
     DB_CHECK(db.get((char**)&tmp, tb + 16));
     DB_CHECK(rocprim::radix_sort_pairs(tmp, tb, k0, k1, v0, v1, (size_t)total, 0, rbits + cbits,
                                        s));
-    hipLaunchKernelGGL(k_run_sums, dim3((total + 255) / 256), dim3(256), 0, s, k1, v1, total,
-                       sums, keep);
+    tick("sort");
+    hipLaunchKernelGGL(k_run_sums, dim3((unsigned)((total + 2047) / 2048)), dim3(256), 0, s, k1,
+                       v1, total, sums, keep);
+    tick("runsum");
   }
   MLAMG_TRY(exclusive_scan_i32(keep, pos, total, s));
   int32_t nnzc = 0;
   DB_CHECK(hipMemcpyAsync(&nnzc, pos + total, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   DB_CHECK(hipStreamSynchronize(s));
   mlamg_csr* C = nullptr;
+  DB_CHECK(db.get(&crow, (size_t)nnzc + 1));
   MLAMG_TRY(csr_alloc(n, B->n_cols, nnzc, &C));
   if (total > 0)
     hipLaunchKernelGGL(k_emit, dim3((total + 255) / 256), dim3(256), 0, s, k1, sums, keep, pos,
-                       total, cbits, C->indices, C->data, rowcnt);
-  int rc = exclusive_scan_i32(rowcnt, C->indptr, n, s);
+                       total, cbits, C->indices, C->data, crow);
+  hipLaunchKernelGGL(k_rowptr, dim3((unsigned)((nnzc + 1 + 255) / 256)), dim3(256), 0, s, crow,
+                     (int64_t)nnzc, n, C->indptr);
+  int rc = MLAMG_OK;
+  if (hipGetLastError() != hipSuccess) {
+    set_error("spgemm: kernel launch failed");
+    rc = MLAMG_EHIP;
+  }
+  tick("emit");
+  if (rc == MLAMG_OK) rc = csr_finalize(C, s);  // syncs before DevBuf frees
+  else (void)hipStreamSynchronize(s);
+  tick("finalize");
+  if (rc != MLAMG_OK) {
+    csr_free(C);
+    return rc;
+  }
+  *out = C;
+  db.release();
+  tick("free");
+  return MLAMG_OK;
+}
+
+// ---------------------------------------------------------------- SpGEMM, dense row accumulator
+// For a narrow product (B->n_cols doubles fit in LDS) with long rows — the coarsest Galerkin
+// products, where expand-sort would materialise ~0.7 G products: one workgroup per row of C
+// keeps the whole row in LDS. It walks A's row in stored order; at each step the entries of B's
+// row are distinct columns, so its threads add in parallel without conflicts, and a barrier
+// orders consecutive steps: every C_ij is 0 + A_ik1 B_k1j + A_ik2 B_k2j + ... in csr_matmat's
+// order, bit for bit. Zeros (never touched or cancelled) are dropped like scipy drops them.
+constexpr int kDenseMaxCols = 15360;  // 120 KiB of LDS
+
+__global__ __launch_bounds__(512) void k_dense_rows(const int32_t* __restrict__ ap,
+                                                    const int32_t* __restrict__ aj,
+                                                    const double* __restrict__ ax,
+                                                    const int32_t* __restrict__ bp,
+                                                    const int32_t* __restrict__ bj,
+                                                    const double* __restrict__ bx, int ncols,
+                                                    double* __restrict__ dense,
+                                                    int32_t* __restrict__ rowcnt) {
+  extern __shared__ double acc[];
+  __shared__ int32_t cnt[512 / 64];
+  const int64_t i = blockIdx.x;
+  const int t = threadIdx.x;
+  for (int j = t; j < ncols; j += 512) acc[j] = 0.0;
+  __syncthreads();
+  for (int k = ap[i]; k < ap[i + 1]; ++k) {
+    const int r = aj[k];
+    const double a = ax[k];
+    for (int e = bp[r] + t; e < bp[r + 1]; e += 512) acc[bj[e]] += a * bx[e];
+    __syncthreads();
+  }
+  int c = 0;
+  double* row = dense + i * (int64_t)ncols;
+  for (int j = t; j < ncols; j += 512) {
+    const double v = acc[j];
+    row[j] = v;
+    c += v != 0.0;
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if ((t & 63) == 0) cnt[t >> 6] = c;
+  __syncthreads();
+  if (t == 0) {
+    int tot = 0;
+    for (int w = 0; w < 512 / 64; ++w) tot += cnt[w];
+    rowcnt[i] = tot;
+  }
+}
+
+// compact the dense rows (ascending columns) into CSR; one workgroup per row
+__global__ __launch_bounds__(256) void k_dense_compact(const double* __restrict__ dense, int ncols,
+                                                       const int32_t* __restrict__ ip,
+                                                       int32_t* __restrict__ cj,
+                                                       double* __restrict__ cx) {
+  __shared__ int32_t wsum[4];
+  __shared__ int32_t base;
+  const int64_t i = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const double* row = dense + i * (int64_t)ncols;
+  if (t == 0) base = ip[i];
+  __syncthreads();
+  for (int j0 = 0; j0 < ncols; j0 += 256) {
+    const int j = j0 + t;
+    const double v = j < ncols ? row[j] : 0.0;
+    const bool nz = v != 0.0;
+    const unsigned long long m = __ballot(nz);
+    const int before = __popcll(m & ((1ull << lane) - 1));
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int q = 0; q < w; ++q) off += wsum[q];
+    if (nz) {
+      cj[off + before] = j;
+      cx[off + before] = v;
+    }
+    __syncthreads();
+    if (t == 0) base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+}
+
+static int spgemm_dense_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out,
+                             hipStream_t s) {
+  const int64_t n = A->n_rows, nc = B->n_cols;
+  DevBuf db;
+  double* dense = nullptr;
+  int32_t* rowcnt = nullptr;
+  DB_CHECK(db.get(&dense, (size_t)(n * nc)));
+  DB_CHECK(db.get(&rowcnt, n + 1));
+  if (n)
+    hipLaunchKernelGGL(k_dense_rows, dim3((unsigned)n), dim3(512), sizeof(double) * nc, s,
+                       A->indptr, A->indices, A->data, B->indptr, B->indices, B->data, (int)nc,
+                       dense, rowcnt);
+  int32_t* cip = nullptr;
+  DB_CHECK(db.get(&cip, n + 1));
+  MLAMG_TRY(exclusive_scan_i32(rowcnt, cip, n, s));
+  int32_t nnzc = 0;
+  DB_CHECK(hipMemcpyAsync(&nnzc, cip + n, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  DB_CHECK(hipStreamSynchronize(s));
+  mlamg_csr* C = nullptr;
+  MLAMG_TRY(csr_alloc(n, nc, nnzc, &C));
+  int rc = MLAMG_OK;
+  if (hipMemcpyAsync(C->indptr, cip, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToDevice, s) !=
+      hipSuccess) {
+    set_error("spgemm(dense): indptr copy failed");
+    rc = MLAMG_EHIP;
+  }
+  if (rc == MLAMG_OK && n)
+    hipLaunchKernelGGL(k_dense_compact, dim3((unsigned)n), dim3(256), 0, s, dense, (int)nc, cip,
+                       C->indices, C->data);
+  if (rc == MLAMG_OK && hipGetLastError() != hipSuccess) {
+    set_error("spgemm(dense): kernel launch failed");
+    rc = MLAMG_EHIP;
+  }
   if (rc == MLAMG_OK) rc = csr_finalize(C, s);  // syncs before DevBuf frees
   else (void)hipStreamSynchronize(s);
   if (rc != MLAMG_OK) {
@@ -364,6 +573,14 @@ int spgemm_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out, int ord
                 hipStream_t s) {
   MLAMG_REQUIRE(A->n_cols == B->n_rows, "inner dimensions differ");
   if (order == 0) {
+    // narrow output with many products per entry: dense LDS rows (no sort, no product buffers).
+    // MLAMG_SPGEMM=dense|esc forces a path where it applies (tests cover both).
+    const char* force = std::getenv("MLAMG_SPGEMM");
+    const bool fits = B->n_cols <= kDenseMaxCols && A->n_rows * B->n_cols <= (int64_t(1) << 28);
+    const bool heavy = (double)A->nnz * ((double)B->nnz / std::max<int64_t>(B->n_rows, 1)) >
+                       8.0 * (double)A->n_rows * (double)std::min<int64_t>(B->n_cols, 2048);
+    const bool want_dense = force ? std::strcmp(force, "dense") == 0 : heavy;
+    if (fits && want_dense) return spgemm_dense_impl(A, B, out, s);
     const int rbits = bits_for(std::max<int64_t>(A->n_rows, 2));
     const int cb = bits_for(std::max<int64_t>(B->n_cols, 2));
     if (rbits + cb <= 64) return spgemm_sorted_impl(A, B, out, rbits, cb, s);

@@ -172,7 +172,7 @@ class Hierarchy:
         t_all = time.perf_counter()
         A_dev = as_device(A)
         tm = {"aggregation": 0.0, "lambda_max": 0.0, "prolongator": 0.0, "galerkin": 0.0,
-              "dense": 0.0}
+              "formats": 0.0, "dense": 0.0}
         while True:
             n = A_dev.shape[0]
             if n <= max_coarse or len(H.levels) + 1 >= max_levels:
@@ -231,9 +231,12 @@ class Hierarchy:
             return H
         t5 = time.perf_counter()
         H.apply_formats(fine_format, coarse_format)
+        torch.cuda.synchronize()
+        t6 = time.perf_counter()
         H._finalize(nu_pre, nu_post)
         torch.cuda.synchronize()
-        tm["dense"] = time.perf_counter() - t5
+        tm["formats"] = t6 - t5
+        tm["dense"] = time.perf_counter() - t6
         tm["total"] = time.perf_counter() - t_all
         H.timings = tm
         return H

@@ -128,8 +128,15 @@ def test_sa_prolongator_galerkin_bitwise(golden, ml):
     assert np.array_equal(AH.data, golden["c1_AH_data"])
 
 
+@pytest.fixture(params=("esc", "dense"))
+def spgemm_path(request, monkeypatch):
+    """Run with each SpGEMM algorithm (expand-sort-compress / dense LDS rows)."""
+    monkeypatch.setenv("MLAMG_SPGEMM", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("seed", (0, 1))
-def test_galerkin_random_bitwise(ml, seed):
+def test_galerkin_random_bitwise(ml, seed, spgemm_path):
     """(P^T A) P on the device vs scipy's P.T @ A @ P (CSC path), values bit for bit, including
     cancellations (exact zeros dropped) and rows with no products."""
     rs = np.random.RandomState(seed)
