@@ -71,9 +71,10 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
  *   SELL        SELL-64 slices, lane-per-row sums in stored order (scipy's bits); vec_width > 1
  *               is read as sigma: rows sorted by length inside windows of sigma rows
  *               (SELL-C-sigma; get_format reports sigma in vec_width)
- *   VECTOR      vec_width lanes per row (0 = auto from the mean row length), lane-strided
- *               partial sums + xor butterfly: a different, fixed order (oracle vec_matvec),
- *               for long-row coarse operators that have no scipy counterpart
+ *   VECTOR      vec_width lanes per row (0 = auto from the mean row length; 4..512), lane-
+ *               strided partial sums + xor butterfly per 64-lane wave (+ wave sums left to right
+ *               for 128..512, one 512-lane workgroup; <= 2^20 rows): a different, fixed order
+ *               (oracle vec_matvec), for long-row coarse operators with no scipy counterpart
  *   AUTO_EXACT  SELL when its padding costs <= 15% extra entries, else CSR_STREAM
  *   SORTED      CSR_STREAM row blocks (<= 512 rows, <= 4096 nonzeros) whose entries are stored
  *               in ascending column order with their CSR slot, so the x gathers of a

@@ -144,8 +144,13 @@ __device__ __forceinline__ double strided_sum(const double* __restrict__ p, int 
 namespace mlamg {
 // Upper bound on the per-block partial sums a NORM launch of A can write, whatever format is
 // active (CSR-stream: n_blocks; SELL-64: n/256; CSR-vector: n*VW/256 <= n/4), plus one slot.
+// Wide CSR-vector widths (128..512 lanes per row, one workgroup of 512 lanes) write one partial
+// per 512/VW rows; they are only accepted on operators with at most kWideMaxRows rows.
+constexpr int64_t kWideMaxRows = int64_t(1) << 20;
 inline int64_t part_capacity(const mlamg_csr* A) {
-  return std::max<int64_t>(std::max<int64_t>(A->n_blocks, A->srt_nb), (A->n_rows + 3) / 4) + 2;
+  int64_t c = std::max<int64_t>(std::max<int64_t>(A->n_blocks, A->srt_nb), (A->n_rows + 3) / 4);
+  if (A->n_rows <= kWideMaxRows) c = std::max<int64_t>(c, A->n_rows);
+  return c + 2;
 }
 // Allocate device arrays for an (n_rows x n_cols, nnz) CSR and the handle; no partition yet.
 int csr_alloc(int64_t n_rows, int64_t n_cols, int64_t nnz, mlamg_csr** out);

@@ -517,6 +517,75 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   }
 }
 
+// Wide variant: VW = 128, 256 or 512 lanes per row inside a 512-lane workgroup (512/VW rows).
+// Lane l sums entries l, l+VW, ... in order; each 64-lane wave folds its lanes with the same xor
+// butterfly as VW = 64; the row's wave sums are then added left to right (w0 + w1 + ...). A fixed
+// order, restated by the oracle (vec_matvec); for the long rows of the coarsest operators, where
+// 64 lanes per row leave the chip mostly idle.
+template <int VW, int OP, bool NORM>
+__global__ __launch_bounds__(512) void k_csr_vecw(const int32_t* __restrict__ indptr,
+                                                  const int32_t* __restrict__ indices,
+                                                  const double* __restrict__ vals, int64_t n_rows,
+                                                  const double* __restrict__ x, Epi ep) {
+  constexpr int RPB = 512 / VW, WPR = VW / 64;
+  __shared__ double wsum[512 / 64];
+  __shared__ double red[RPB];
+  if (ep.done && *ep.done) return;
+  const int t = threadIdx.x;
+  const int64_t row = (int64_t)blockIdx.x * RPB + t / VW;
+  const int l = t & (VW - 1);
+  double s = 0.0;
+  if (row < n_rows) {
+    const int a = indptr[row], b = indptr[row + 1];
+    for (int k = a + l; k < b; k += 4 * VW) {
+      int32_t cc[4];
+      double vv[4], xv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = k + u * VW;
+        cc[u] = e < b ? __builtin_nontemporal_load(indices + e) : -1;
+        vv[u] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (cc[u] >= 0) s += vv[u] * xv[u];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((t & 63) == 0) wsum[t >> 6] = s;
+  __syncthreads();
+  double sq = 0.0;
+  if (l == 0 && row < n_rows) {
+    const int w0 = (t >> 6);
+    double r = wsum[w0];
+#pragma unroll
+    for (int q = 1; q < WPR; ++q) r += wsum[w0 + q];
+    sq = epilogue<OP>((int)row, r, ep);
+  }
+  if constexpr (NORM) {
+    if (l == 0) red[t / VW] = sq;
+    __syncthreads();
+    if (t == 0) {
+      double tot = 0.0;
+      for (int i = 0; i < RPB; ++i) tot += red[i];
+      ep.partial[blockIdx.x] = tot;
+    }
+  }
+}
+
+template <int OP, bool NORM, int VW>
+static int launch_vec_wide(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  constexpr int RPB = 512 / VW;
+  const unsigned nb = (unsigned)std::max<int64_t>(1, (A->n_rows + RPB - 1) / RPB);
+  hipLaunchKernelGGL((k_csr_vecw<VW, OP, NORM>), dim3(nb), dim3(512), 0, s, A->indptr,
+                     A->indices, A->data, A->n_rows, x, ep);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
 template <int OP, bool NORM, int VW>
 static int launch_vec_w(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   const int64_t threads = A->n_rows * VW;
@@ -535,6 +604,9 @@ static int launch_vec(const mlamg_csr* A, const double* x, const Epi& ep, hipStr
     case 8: return launch_vec_w<OP, NORM, 8>(A, x, ep, s);
     case 16: return launch_vec_w<OP, NORM, 16>(A, x, ep, s);
     case 32: return launch_vec_w<OP, NORM, 32>(A, x, ep, s);
+    case 128: return launch_vec_wide<OP, NORM, 128>(A, x, ep, s);
+    case 256: return launch_vec_wide<OP, NORM, 256>(A, x, ep, s);
+    case 512: return launch_vec_wide<OP, NORM, 512>(A, x, ep, s);
     default: return launch_vec_w<OP, NORM, 64>(A, x, ep, s);
   }
 }
@@ -1314,10 +1386,16 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
         vw = 4;
         while (vw < 64 && 2.0 * vw <= A->avg_row_len) vw *= 2;
       }
-      MLAMG_REQUIRE(vw == 4 || vw == 8 || vw == 16 || vw == 32 || vw == 64,
-                    "vec_width must be 0 (auto), 4, 8, 16, 32 or 64");
+      MLAMG_REQUIRE(vw == 4 || vw == 8 || vw == 16 || vw == 32 || vw == 64 || vw == 128 ||
+                        vw == 256 || vw == 512,
+                    "vec_width must be 0 (auto), 4, 8, 16, 32, 64, 128, 256 or 512");
+      if (vw >= 128 && A->n_rows > kWideMaxRows) {
+        set_error("vec_width >= 128 needs <= 2^20 rows");
+        return MLAMG_EUNSUPPORTED;
+      }
       A->vec_width = vw;
-      A->n_part = (int32_t)std::max<int64_t>(1, (A->n_rows * vw + kThreads - 1) / kThreads);
+      A->n_part = vw >= 128 ? (int32_t)std::max<int64_t>(1, (A->n_rows * vw + 511) / 512)
+                            : (int32_t)std::max<int64_t>(1, (A->n_rows * vw + kThreads - 1) / kThreads);
       return MLAMG_OK;
     }
     case MLAMG_FMT_AUTO_EXACT: {

@@ -83,7 +83,8 @@ class Hierarchy:
 
     EXACT_CANDIDATES = (("csr_stream", 0), ("sell", 1), ("sell", 512), ("sorted", 0),
                         ("sell_dict", 1), ("sell_dict", 512))
-    VECTOR_CANDIDATES = (("vector", 8), ("vector", 16), ("vector", 32), ("vector", 64))
+    VECTOR_CANDIDATES = (("vector", 8), ("vector", 16), ("vector", 32), ("vector", 64),
+                         ("vector", 128), ("vector", 256), ("vector", 512))
 
     @staticmethod
     def _time_format(M, fmt, arg, x, y, reps=5, kind="A"):

@@ -33,24 +33,30 @@ void ref_csr_matvec(int64_t n, const int32_t* ip, const int32_t* ij, const doubl
 
 /* The device CSR-vector order (mlamg_csr_set_format VECTOR): lane l of vw sums entries
  * l, l+vw, ... of the row in order, then partials combine by an xor butterfly off=vw/2..1. */
+/* device CSR-vector order (spmv.hip k_csr_vec / k_csr_vecw): lane l of vw sums entries l, l+vw,
+ * ... in order; each group of min(vw, 64) lanes folds with an xor butterfly; for vw > 64 the
+ * group (wave) sums are then added left to right. */
 void vec_matvec(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
                 const double* x, double* y, int vw) {
-  double part[64], nxt[64];
-  if (vw < 1 || vw > 64 || (vw & (vw - 1))) {
+  double part[512], nxt[512];
+  if (vw < 1 || vw > 512 || (vw & (vw - 1))) {
     for (int64_t i = 0; i < n; ++i) y[i] = NAN;
     return;
   }
+  const int g = vw < 64 ? vw : 64;
   for (int64_t i = 0; i < n; ++i) {
     for (int l = 0; l < vw; ++l) {
       double s = 0.0;
       for (int32_t k = ip[i] + l; k < ip[i + 1]; k += vw) s += ax[k] * x[ij[k]];
       part[l] = s;
     }
-    for (int off = vw / 2; off > 0; off >>= 1) {
-      for (int l = 0; l < vw; ++l) nxt[l] = part[l] + part[l ^ off];
+    for (int off = g / 2; off > 0; off >>= 1) {
+      for (int l = 0; l < vw; ++l) nxt[l] = part[l] + part[(l & ~(g - 1)) | ((l & (g - 1)) ^ off)];
       for (int l = 0; l < vw; ++l) part[l] = nxt[l];
     }
-    y[i] = part[0];
+    double r = part[0];
+    for (int w = 1; w < vw / g; ++w) r += part[w * g];
+    y[i] = r;
   }
 }
 

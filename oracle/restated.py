@@ -65,8 +65,8 @@ def csr_matvec(A, x):
 
 def vec_matvec(A, x, vw):
     """The device CSR-vector summation order (oracle.c vec_matvec)."""
-    if vw not in (4, 8, 16, 32, 64):
-        raise ValueError(f"vector width must be 4..64 (power of two), got {vw}")
+    if vw not in (4, 8, 16, 32, 64, 128, 256, 512):
+        raise ValueError(f"vector width must be 4..512 (power of two), got {vw}")
     ip, ij, ax = _csr_arrays(A)
     x = np.ascontiguousarray(x, dtype=np.float64)
     y = np.empty(A.shape[0])

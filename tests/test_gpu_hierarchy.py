@@ -55,7 +55,7 @@ def test_exact_formats_bitwise(golden, ml, torch_cuda, k, fmt):
     assert abs(nrm.item() - ref) <= 1e-13 * ref
 
 
-@pytest.mark.parametrize("vw", (4, 8, 16, 32, 64))
+@pytest.mark.parametrize("vw", (4, 8, 16, 32, 64, 128, 256, 512))
 def test_vector_format_matches_oracle_order(ml, oracle, torch_cuda, vw):
     torch = torch_cuda
     rs = np.random.RandomState(vw)
