@@ -280,7 +280,7 @@ int mlamg_dhier_add_level(mlamg_dhier* D, const mlamg_csr* A_loc, const double* 
   const int64_t n = A_loc->n_rows;
   MLAMG_REQUIRE(A_loc->n_cols == n + halo_x->n_ghost, "A_loc columns != n_own + x ghosts");
   MLAMG_REQUIRE(halo_x->n_own == n && halo_r->n_own == n, "halo n_own mismatch");
-  MLAMG_REQUIRE(P_loc->n_rows == n, "P_loc rows != n_own");
+  MLAMG_REQUIRE(P_loc->n_rows == n + halo_x->n_ghost, "P_loc rows != n_own + x ghosts");
   MLAMG_REQUIRE(R_own->n_cols == n + halo_r->n_ghost, "R_own columns != n_own + r ghosts");
   if (!D->lv.empty()) {
     DLevel& up = D->lv.back();
@@ -353,8 +353,10 @@ static int dprepare(mlamg_dhier* D) {
       MLAMG_TRY(dalloc(D, &L.b, L.n_own));
     }
     MLAMG_TRY(dalloc(D, &L.r_ext, ext));
-    MLAMG_TRY(dalloc(D, &L.t_ext, ext));
-    if (L.hp) MLAMG_TRY(dalloc(D, &L.xp_ext, L.hp->n_own + L.hp->n_ghost));
+    // t_ext of level l > 0 doubles as the P-halo buffer (xp_ext) of level l - 1
+    const int64_t pg = l > 0 ? D->lv[l - 1].hp->n_ghost : 0;
+    MLAMG_TRY(dalloc(D, &L.t_ext, std::max(ext, L.n_own + pg)));
+    if (l > 0) D->lv[l - 1].xp_ext = L.t_ext;
   }
   MLAMG_TRY(dalloc(D, &D->bc, D->nc));
   MLAMG_TRY(dalloc(D, &D->partial, part_capacity(D->lv[0].A)));
@@ -395,8 +397,11 @@ static int correct(mlamg_dhier* D, size_t l, double* x_ext, const int32_t* done,
     MLAMG_TRY(spmv_set(L.R, L.r_ext, N.b, done, s, N.x_ext, N.dinv));
     double* xn = nullptr;
     MLAMG_TRY(dcycle_below(D, l + 1, &xn, s));
-    MLAMG_HIP(hipMemcpyAsync(L.xp_ext, xn, sizeof(double) * N.n_own, hipMemcpyDeviceToDevice, s));
+    // xp_ext is the level below's t_ext: its owned part is the correction, the P-halo lands in
+    // its (no longer needed) ghost region
     MLAMG_TRY(halo_exchange_impl(L.hp, L.xp_ext, s));
+    // P rows cover the owned AND the x-ghost rows: x_ext's ghosts get the same update their
+    // owners compute (same row, same order, same inputs), so no x halo is needed afterwards
     MLAMG_TRY(spmv_add(L.P, L.xp_ext, x_ext, done, s));
   } else {
     const int me = D->c->rank;
@@ -420,7 +425,6 @@ static int dcycle_below(mlamg_dhier* D, size_t l, double** x_out, hipStream_t s)
   MLAMG_TRY(residual_impl(L.A, L.b, L.x_ext, L.r_ext, nullptr, nullptr, nullptr,
                           const_cast<int32_t*>(done), 0.0, nullptr, nullptr, nullptr, s));
   MLAMG_TRY(correct(D, l, L.x_ext, done, s));
-  MLAMG_TRY(halo_exchange_impl(L.hx, L.x_ext, s));
   MLAMG_TRY(jacobi_sweep(L.A, L.dinv, L.b, L.x_ext, L.t_ext, false, done, s));
   *x_out = L.t_ext;
   return MLAMG_OK;
@@ -439,7 +443,6 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
   MLAMG_TRY(residual_impl(A, b, x_ext, L.r_ext, nullptr, nullptr, nullptr, done, 0.0, nullptr,
                           nullptr, nullptr, s));
   MLAMG_TRY(correct(D, 0, x_ext, done, s));
-  MLAMG_TRY(halo_exchange_impl(L.hx, x_ext, s));
   MLAMG_TRY(jacobi_sweep(A, L.dinv, b, x_ext, L.t_ext, false, done, s));
   MLAMG_TRY(halo_exchange_impl(L.hx, L.t_ext, s));
   // r = b - A t with per-block ||r||^2 partials, x <- t; then the global norm

@@ -100,10 +100,12 @@ def build_levels(As, Ps, seeds_list, world, rank):
     """Partition maps of the first K = len(As) levels for `rank` (list of per-level dicts).
 
     Level 0 rows: near-equal contiguous blocks. Level l+1 rows: the coarse unknowns whose seed
-    lies in the rank's level-l rows (contiguous because seeds are sorted). For l < K-1 the
-    prolongation P_l gets its columns renumbered into [owned level-(l+1) rows | P-ghosts] with a
-    halo of x_{l+1}; the last partitioned level's P keeps global columns (the level below is
-    replicated on every rank, gathered with an allgatherv of the owned coarse segments).
+    lies in the rank's level-l rows (contiguous because seeds are sorted). P_loc holds the rows
+    of P_l for the owned rows AND the x-ghost rows (in x_ext order): prolonging into the ghosts
+    locally reproduces their owners' update bit for bit, so no x halo is needed after the coarse
+    correction. For l < K-1 its columns are renumbered into [owned level-(l+1) rows | P-ghosts]
+    with a halo of x_{l+1}; the last partitioned level's P keeps global columns (the level below
+    is replicated on every rank, gathered with an allgatherv of the owned coarse segments).
     """
     K = len(As)
     ranges = row_ranges(As[0].shape[0], world)
@@ -115,12 +117,14 @@ def build_levels(As, Ps, seeds_list, world, rank):
         c_ranges = _seed_ranges(seeds_list[l], ranges, nc)
         R = P.T.tocsr()
         R.sort_indices()
-        xg, rg, pg = [], [], []
+        xg, rg, pg, prow = [], [], [], []
         for q, (lo, hi) in enumerate(ranges):
             xg.append(_ghost_sets(A[lo:hi].indices, lo, hi))
             clo, chi = c_ranges[q]
             rg.append(_ghost_sets(R[clo:chi].indices, lo, hi))
-            pg.append(_ghost_sets(P[lo:hi].indices, clo, chi))
+            rows = np.concatenate([np.arange(lo, hi), xg[q]]).astype(np.int64)
+            prow.append(rows)
+            pg.append(_ghost_sets(P[rows].indices, clo, chi))
         lo, hi = ranges[rank]
         clo, chi = c_ranges[rank]
         last = l == K - 1
@@ -132,11 +136,12 @@ def build_levels(As, Ps, seeds_list, world, rank):
             "halo_x": _halos(xg, ranges, rank),
             "halo_r": _halos(rg, ranges, rank),
         }
+        P_ext = P[prow[rank]]  # owned rows, then the x-ghost rows (x_ext order)
         if last:
-            d["P_loc"] = P[lo:hi].copy()
+            d["P_loc"] = P_ext.tocsr()
             d["halo_p"] = None
         else:
-            d["P_loc"] = _remap(P[lo:hi], clo, chi, pg[rank])
+            d["P_loc"] = _remap(P_ext, clo, chi, pg[rank])
             d["halo_p"] = _halos(pg, c_ranges, rank)
         out.append(d)
         ranges = c_ranges

@@ -126,6 +126,11 @@ def _worker(rank, world, port, kind, ncyc, K, q):
             _allgatherv(bc, p["c_ranges"], rank, world, tag[0])
             return orc.csr_matvec(p["P_loc"], coarse(0, bc, None))
 
+        def prolong(l, x, r):
+            # P_loc rows = owned + x-ghost rows: the ghosts are updated locally (no x halo)
+            k = parts[l]["P_loc"].shape[0]
+            x[:k] = x[:k] + correct(l, r)
+
         def below(l, bl):
             p = parts[l]
             m = p["hi"] - p["lo"]
@@ -134,8 +139,7 @@ def _worker(rank, world, port, kind, ncyc, K, q):
             x[:m] = d * bl
             halo(x, p["halo_x"], m)
             r[:m] = bl - orc.csr_matvec(p["A_loc"], x)
-            x[:m] = x[:m] + correct(l, r)
-            halo(x, p["halo_x"], m)
+            prolong(l, x, r)
             return x[:m] + d * (bl - orc.csr_matvec(p["A_loc"], x))
 
         p0 = parts[0]
@@ -157,8 +161,7 @@ def _worker(rank, world, port, kind, ncyc, K, q):
             x[:n_own] = x[:n_own] + d * r[:n_own]
             halo(x, hx, n_own)
             r[:n_own] = resid(x)
-            x[:n_own] = x[:n_own] + correct(0, r)
-            halo(x, hx, n_own)
+            prolong(0, x, r)
             t = np.zeros_like(x)
             t[:n_own] = x[:n_own] + d * resid(x)
             halo(t, hx, n_own)
