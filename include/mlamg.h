@@ -219,6 +219,13 @@ int mlamg_hier_add_level(mlamg_hier* H, const mlamg_csr* A, const double* dinv_w
                          const mlamg_csr* P, const mlamg_csr* R);
 int mlamg_hier_set_coarse(mlamg_hier* H, const mlamg_csr* A_coarse, const mlamg_dense* D);
 int mlamg_hier_set_smoothing(mlamg_hier* H, int nu_pre, int nu_post);
+/* smoother of one level: a Gauss-Seidel handle built on that level's operator (pyamg forward
+ * sweep, in place; ns/lib/multigrid.py:175,184 — the reference amg_2_v), or NULL for weighted
+ * Jacobi (default) */
+int mlamg_hier_set_level_smoother(mlamg_hier* H, int level, const mlamg_gs* gs);
+/* what res_hist records each cycle: 0 = ||b - A x||_2 (default, MLAMG.py:194 / res_tol),
+ * 1 = ||x||_2 (amg_2_v error_tol, multigrid.py:193); the tolerance test applies to it */
+int mlamg_hier_set_norm(mlamg_hier* H, int mode);
 /* run n_cycles V-cycles on (b, x) (x updated in place). After each cycle ||b - A x||_2 is
  * written to res_hist[c] (DEVICE, may be NULL). If tol > 0 the cycle loop stops after the first
  * cycle with ||r|| <= tol (MLAMG.py:194); *cycles_done_host (nullable) receives the count and

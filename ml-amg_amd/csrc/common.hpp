@@ -193,6 +193,12 @@ int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int
 int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
                       hipStream_t s);
 int hier_prepare_ext(mlamg_hier* H);
+int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
+                  const int32_t* done, hipStream_t s);
+int64_t gs_rows(const mlamg_gs* G);
+// ||x||_2 of one cycle into hist[*counter] (+ tolerance flag), like the residual-norm path
+int norm_hist_impl(const double* x, int64_t n, double* partial, double* hist, int32_t* counter,
+                   int32_t* done, double tol, hipStream_t s);
 int count_out_of_range(const int32_t* a, int64_t n, int64_t lo, int64_t hi, hipStream_t s,
                        int64_t* bad_out);
 }  // namespace mlamg

@@ -12,20 +12,18 @@
 struct mlamg_gs {
   const mlamg_csr* A = nullptr;
   int32_t n_levels = 0;
+  int32_t max_level_rows = 0;
   std::vector<int32_t> level_ptr;  // host
+  int32_t* d_level_ptr = nullptr;  // device copy
   int32_t* rows = nullptr;         // device, rows grouped by level (ascending within a level)
 };
 
 namespace mlamg {
 
-__global__ __launch_bounds__(256) void k_gs_level(const int32_t* __restrict__ ip,
-                                                  const int32_t* __restrict__ ij,
-                                                  const double* __restrict__ ax,
-                                                  const int32_t* __restrict__ rows, int32_t cnt,
-                                                  double* x, const double* __restrict__ b) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= cnt) return;
-  const int32_t i = rows[t];
+__device__ __forceinline__ void gs_row(const int32_t* __restrict__ ip,
+                                       const int32_t* __restrict__ ij,
+                                       const double* __restrict__ ax, int32_t i, double* x,
+                                       const double* __restrict__ b) {
   double rsum = 0.0, diag = 0.0;
   for (int k = ip[i]; k < ip[i + 1]; ++k) {
     const int32_t j = ij[k];
@@ -33,6 +31,64 @@ __global__ __launch_bounds__(256) void k_gs_level(const int32_t* __restrict__ ip
     else rsum += ax[k] * x[j];
   }
   if (diag != 0.0) x[i] = (b[i] - rsum) / diag;
+}
+
+__global__ __launch_bounds__(256) void k_gs_level(const int32_t* __restrict__ ip,
+                                                  const int32_t* __restrict__ ij,
+                                                  const double* __restrict__ ax,
+                                                  const int32_t* __restrict__ rows, int32_t cnt,
+                                                  double* x, const double* __restrict__ b,
+                                                  const int32_t* done) {
+  if (done && *done) return;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= cnt) return;
+  gs_row(ip, ij, ax, rows[t], x, b);
+}
+
+// The whole sweep in one workgroup: levels in order, a barrier between consecutive levels
+// (workgroup-scope visibility of the x updates). For operators whose levels are narrow, where
+// one launch per level would make the sweep launch-bound.
+constexpr int kGsBlock = 1024;
+constexpr int kGsBlockMaxLevelRows = 8 * kGsBlock;
+
+__global__ __launch_bounds__(kGsBlock) void k_gs_block(const int32_t* __restrict__ ip,
+                                                       const int32_t* __restrict__ ij,
+                                                       const double* __restrict__ ax,
+                                                       const int32_t* __restrict__ rows,
+                                                       const int32_t* __restrict__ lptr,
+                                                       int32_t n_levels, int iterations, double* x,
+                                                       const double* __restrict__ b,
+                                                       const int32_t* done) {
+  if (done && *done) return;
+  for (int it = 0; it < iterations; ++it) {
+    for (int32_t l = 0; l < n_levels; ++l) {
+      const int32_t a = lptr[l], z = lptr[l + 1];
+      for (int32_t t = a + (int32_t)threadIdx.x; t < z; t += kGsBlock) gs_row(ip, ij, ax, rows[t], x, b);
+      __syncthreads();
+    }
+  }
+}
+
+int64_t gs_rows(const mlamg_gs* G) { return G->A->n_rows; }
+
+int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
+                  const int32_t* done, hipStream_t s) {
+  const mlamg_csr* A = G->A;
+  if (A->n_rows == 0 || iterations <= 0) return MLAMG_OK;
+  if (G->max_level_rows <= kGsBlockMaxLevelRows && G->n_levels > 4) {
+    hipLaunchKernelGGL(k_gs_block, dim3(1), dim3(kGsBlock), 0, s, A->indptr, A->indices, A->data,
+                       G->rows, G->d_level_ptr, G->n_levels, iterations, x, b, done);
+  } else {
+    for (int it = 0; it < iterations; ++it) {
+      for (int32_t l = 0; l < G->n_levels; ++l) {
+        const int32_t a = G->level_ptr[l], cnt = G->level_ptr[l + 1] - a;
+        hipLaunchKernelGGL(k_gs_level, dim3((cnt + 255) / 256), dim3(256), 0, s, A->indptr,
+                           A->indices, A->data, G->rows + a, cnt, x, b, done);
+      }
+    }
+  }
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
 }
 
 }  // namespace mlamg
@@ -80,6 +136,16 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
     return MLAMG_ENOMEM;
   }
   if (n) (void)hipMemcpy(G->rows, rows.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice);
+  for (int32_t l = 0; l < nlev; ++l)
+    G->max_level_rows = std::max(G->max_level_rows, G->level_ptr[l + 1] - G->level_ptr[l]);
+  if (hipMalloc(&G->d_level_ptr, sizeof(int32_t) * (nlev + 1)) != hipSuccess) {
+    (void)hipFree(G->rows);
+    delete G;
+    set_error("gs_create: hipMalloc failed");
+    return MLAMG_ENOMEM;
+  }
+  (void)hipMemcpy(G->d_level_ptr, G->level_ptr.data(), sizeof(int32_t) * (nlev + 1),
+                  hipMemcpyHostToDevice);
   *out = G;
   return MLAMG_OK;
 }
@@ -87,6 +153,7 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
 int mlamg_gs_destroy(mlamg_gs* G) {
   if (G) {
     if (G->rows) (void)hipFree(G->rows);
+    if (G->d_level_ptr) (void)hipFree(G->d_level_ptr);
     delete G;
   }
   return MLAMG_OK;
@@ -100,17 +167,7 @@ int mlamg_gs_levels(const mlamg_gs* G, int32_t* n_levels) {
 
 int mlamg_gs_sweep(const mlamg_gs* G, double* x, const double* b, int iterations, void* stream) {
   MLAMG_REQUIRE(G && (G->A->n_rows == 0 || (x && b)), "NULL argument");
-  hipStream_t s = S(stream);
-  const mlamg_csr* A = G->A;
-  for (int it = 0; it < iterations; ++it) {
-    for (int32_t l = 0; l < G->n_levels; ++l) {
-      const int32_t a = G->level_ptr[l], cnt = G->level_ptr[l + 1] - a;
-      hipLaunchKernelGGL(k_gs_level, dim3((cnt + 255) / 256), dim3(256), 0, s, A->indptr,
-                         A->indices, A->data, G->rows + a, cnt, x, b);
-    }
-  }
-  MLAMG_HIP(hipGetLastError());
-  return MLAMG_OK;
+  return gs_sweep_impl(G, x, b, iterations, nullptr, S(stream));
 }
 
 }  // extern "C"

@@ -28,6 +28,7 @@ struct Level {
   double* b = nullptr;    // l > 0: right-hand side
   double* r = nullptr;    // residual
   double* tmp = nullptr;  // ping-pong partner of x
+  const mlamg_gs* gs = nullptr;  // Gauss-Seidel smoother (in place) instead of weighted Jacobi
 };
 }  // namespace
 
@@ -38,6 +39,7 @@ struct mlamg_hier {
   double* xc = nullptr;
   double* bc = nullptr;
   int nu_pre = 1, nu_post = 1;
+  int norm_mode = 0;  // per-cycle history: 0 = ||b - A x||_2, 1 = ||x||_2 (amg_2_v error_tol)
   void* mem = nullptr;
   size_t mem_bytes = 0;
   double* partial = nullptr;
@@ -125,6 +127,7 @@ static int hier_prepare(mlamg_hier* H) {
 // smoothing sweeps starting from `cur` (x or tmp); returns buffer holding the result
 static int smooth(const Level& L, const double* b, double*& cur, double* other, int nu,
                   const int32_t* done, hipStream_t s) {
+  if (L.gs) return gs_sweep_impl(L.gs, cur, b, nu, done, s);  // in place, cur unchanged
   for (int i = 0; i < nu; ++i) {
     MLAMG_TRY(jacobi_sweep(L.A, L.dinv, b, cur, other, false, done, s));
     std::swap(cur, other);
@@ -145,7 +148,12 @@ static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, 
   Level& L = H->lv[l];
   double* cur = L.x;
   double* other = L.tmp;
-  if (H->nu_pre > 0) {
+  if (H->nu_pre > 0 && L.gs) {
+    MLAMG_HIP(hipMemsetAsync(cur, 0, sizeof(double) * L.n, s));
+    MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre, done, s));
+    MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, const_cast<int32_t*>(done),
+                            0.0, nullptr, nullptr, nullptr, s));
+  } else if (H->nu_pre > 0) {
     if (!presmoothed) MLAMG_TRY(jacobi_from_zero(cur, L.dinv, b, L.n, done, s));
     MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre - 1, done, s));
     MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, const_cast<int32_t*>(done),
@@ -154,8 +162,8 @@ static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, 
     MLAMG_HIP(hipMemsetAsync(cur, 0, sizeof(double) * L.n, s));
     MLAMG_HIP(hipMemcpyAsync(L.r, b, sizeof(double) * L.n, hipMemcpyDeviceToDevice, s));
   }
-  const bool fuse_next = l + 1 < H->lv.size() && H->nu_pre > 0;
-  double* bn = fuse_next ? H->lv[l + 1].b : H->bc;
+  const bool fuse_next = l + 1 < H->lv.size() && H->nu_pre > 0 && !H->lv[l + 1].gs;
+  double* bn = (l + 1 < H->lv.size()) ? H->lv[l + 1].b : H->bc;
   if (fuse_next) {
     MLAMG_TRY(spmv_set(L.R, L.r, bn, done, s, H->lv[l + 1].x, H->lv[l + 1].dinv));
   } else {
@@ -176,7 +184,8 @@ static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, 
 // the very first sweep before the first cycle and copies t back into x after the last one (t is
 // still in tmp even when the tolerance flag stopped later cycles). Saves one pass over x, d, r.
 static bool fused_presmooth(const mlamg_hier* H) {
-  return !H->lv.empty() && H->nu_pre >= 1 && (H->nu_post & 1);
+  return !H->lv.empty() && H->nu_pre >= 1 && (H->nu_post & 1) && !H->lv[0].gs &&
+         H->norm_mode == 0;
 }
 
 // one finest-level cycle; requires L0.r == b - A x on entry, leaves it so on exit (fused mode:
@@ -193,14 +202,18 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
   const bool fused = fused_presmooth(H);
   double* cur = x;
   double* other = L.tmp;
-  if (H->nu_pre > 0) {
+  if (H->nu_pre > 0 && L.gs) {
+    MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre, done, s));
+    MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, done, 0.0, nullptr,
+                            nullptr, nullptr, s));
+  } else if (H->nu_pre > 0) {
     if (!fused) MLAMG_TRY(jacobi_from_residual(cur, L.dinv, L.r, L.n, done, s));
     MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre - 1, done, s));
     MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, done, 0.0, nullptr,
                             nullptr, nullptr, s));
   }
-  const bool fuse_next = H->lv.size() > 1 && H->nu_pre > 0;
-  double* bn = fuse_next ? H->lv[1].b : H->bc;
+  const bool fuse_next = H->lv.size() > 1 && H->nu_pre > 0 && !H->lv[1].gs;
+  double* bn = H->lv.size() > 1 ? H->lv[1].b : H->bc;
   if (fuse_next) {
     MLAMG_TRY(spmv_set(L.R, L.r, bn, done, s, H->lv[1].x, H->lv[1].dinv));
   } else {
@@ -212,6 +225,12 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
   other = (cur == x) ? L.tmp : x;
   MLAMG_TRY(smooth(L, b, cur, other, H->nu_post, done, s));
   // end-of-cycle residual + norm (+ copy the iterate back into x when it sits in tmp)
+  if (H->norm_mode == 1) {  // history of ||x||_2 (amg_2_v error_tol): residual kept for reuse
+    MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, done, 0.0,
+                            cur != x ? x : nullptr, cur != x ? cur : nullptr, nullptr, s));
+    MLAMG_TRY(norm_hist_impl(x, L.n, H->partial, hist, counter, done, tol, s));
+    return MLAMG_OK;
+  }
   MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, hist, counter, done, tol,
                           cur != x ? x : nullptr, cur != x ? cur : nullptr, H->partial, s,
                           fused ? L.dinv : nullptr));
@@ -300,6 +319,21 @@ int mlamg_hier_set_coarse(mlamg_hier* H, const mlamg_csr* A_coarse, const mlamg_
     MLAMG_REQUIRE(H->lv.back().P->n_cols == D->n, "coarse size does not match last P");
   H->Ac = A_coarse;
   H->D = D;
+  return MLAMG_OK;
+}
+
+int mlamg_hier_set_level_smoother(mlamg_hier* H, int level, const mlamg_gs* gs) {
+  MLAMG_REQUIRE(H && level >= 0 && (size_t)level < H->lv.size(), "invalid level");
+  MLAMG_REQUIRE(!gs || gs_rows(gs) == H->lv[level].n, "Gauss-Seidel handle of another size");
+  H->lv[level].gs = gs;
+  hier_free_graph(H);
+  return MLAMG_OK;
+}
+
+int mlamg_hier_set_norm(mlamg_hier* H, int mode) {
+  MLAMG_REQUIRE(H && (mode == 0 || mode == 1), "mode must be 0 (residual) or 1 (x)");
+  H->norm_mode = mode;
+  hier_free_graph(H);
   return MLAMG_OK;
 }
 

@@ -60,6 +60,35 @@ int norm2_impl(const double* x, int64_t n, double* out, double* partial, const i
   return MLAMG_OK;
 }
 
+__global__ __launch_bounds__(1024) void k_sum_hist(const double* __restrict__ partial, int n,
+                                                   double* hist, int32_t* counter, int32_t* done,
+                                                   double tol) {
+  __shared__ double red[16];
+  if (done && *done) return;
+  double s = strided_sum(partial, n, threadIdx.x, 1024);
+  s = wave_sum_v(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < 16; ++i) t += red[i];
+    const double nrm = sqrt(t);
+    const int c = *counter;
+    if (hist) hist[c] = nrm;
+    *counter = c + 1;
+    if (tol > 0.0 && nrm <= tol) *done = 1;
+  }
+}
+
+int norm_hist_impl(const double* x, int64_t n, double* partial, double* hist, int32_t* counter,
+                   int32_t* done, double tol, hipStream_t s) {
+  const int nb = (int)std::min<int64_t>(kNormBlocks, std::max<int64_t>(1, (n + 255) / 256));
+  hipLaunchKernelGGL(k_sumsq_partial, dim3(nb), dim3(256), 0, s, x, n, partial, done);
+  hipLaunchKernelGGL(k_sum_hist, dim3(1), dim3(1024), 0, s, partial, nb, hist, counter, done, tol);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
 __global__ __launch_bounds__(256) void k_diag_inv(const int32_t* __restrict__ indptr,
                                                   const int32_t* __restrict__ indices,
                                                   const double* __restrict__ vals, int64_t n,

@@ -94,6 +94,8 @@ SIGNATURES = {
     "mlamg_hier_add_level": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mlamg_hier_set_coarse": (c_int, [c_vp, c_vp, c_vp]),
     "mlamg_hier_set_smoothing": (c_int, [c_vp, c_int, c_int]),
+    "mlamg_hier_set_level_smoother": (c_int, [c_vp, c_int, c_vp]),
+    "mlamg_hier_set_norm": (c_int, [c_vp, c_int]),
     "mlamg_hier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_int, c_vp]),
     "mlamg_hier_cycle_bytes": (c_int, [c_vp, P_dbl]),
     "mlamg_comm_unique_id": (c_int, [c_vp]),

@@ -40,7 +40,7 @@ def strength(A_dev, mode="invabs"):
 
 class Level:
     __slots__ = ("A", "dinv", "P", "R", "Agg", "omega", "lam", "lanczos_iters", "n_seeds",
-                 "bf_sweeps", "seeds")
+                 "bf_sweeps", "seeds", "gs")
 
     def __init__(self, A):
         self.A = A
@@ -51,6 +51,7 @@ class Level:
         self.n_seeds = 0
         self.bf_sweeps = 0
         self.seeds = None
+        self.gs = None
 
 
 class Hierarchy:
@@ -68,8 +69,12 @@ class Hierarchy:
 
     # ------------------------------------------------------------------ construction
     @classmethod
-    def two_level(cls, A, P, omega=2.0 / 3.0, nu_pre=1, nu_post=1, dinv_w=None):
-        """Two-level cycle of MLAMG.amg_2_v with a given P (ns/preconditioner/MLAMG.py:120-122)."""
+    def two_level(cls, A, P, omega=2.0 / 3.0, nu_pre=1, nu_post=1, dinv_w=None,
+                  smoother="jacobi", norm="residual"):
+        """Two-level cycle with a given P: MLAMG.amg_2_v (ns/preconditioner/MLAMG.py:120-122,
+        smoother='jacobi') or multigrid.amg_2_v (multigrid.py:111-210, smoother='gauss_seidel';
+        norm='x' records ||x||_2 per cycle, the error_tol mode)."""
+        from .multigrid import GaussSeidel
         H = cls()
         H.jacobi_weight = omega
         L = Level(as_device(A))
@@ -79,6 +84,14 @@ class Hierarchy:
         H.levels.append(L)
         H.Ac = galerkin(L.R, L.A, L.P)
         H._finalize(nu_pre, nu_post)
+        if smoother == "gauss_seidel":
+            L.gs = GaussSeidel(L.A)
+            call("mlamg_hier_set_level_smoother", H.handle, 0, L.gs.handle)
+        elif smoother != "jacobi":
+            raise ValueError(f"unknown smoother {smoother!r}")
+        if norm not in ("residual", "x"):
+            raise ValueError(f"unknown norm {norm!r}")
+        call("mlamg_hier_set_norm", H.handle, 0 if norm == "residual" else 1)
         return H
 
     EXACT_CANDIDATES = (("csr_stream", 0), ("sell", 1), ("sell", 512), ("sorted", 0),

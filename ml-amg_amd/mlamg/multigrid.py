@@ -210,48 +210,20 @@ def amg_2_v(A, P, b, x,
     if smoother not in ("gauss_seidel", "jacobi"):
         raise ValueError(f"unknown smoother {smoother!r}")
     err = np.zeros(max_iter)
+    from .hierarchy import Hierarchy
     try:
-        two = TwoLevel(A, P)
+        # the whole solve is one device call: cycles replayed from a captured graph, the
+        # norm and tolerance test on the device (no host round trip per iteration)
+        H = Hierarchy.two_level(A, P, omega=jacobi_weight, nu_pre=pre_smoothing_steps,
+                                nu_post=post_smoothing_steps, smoother=smoother,
+                                norm="residual" if res_tol is not None else "x")
     except _lib.MlamgError as e:
         if e.code == _lib.MLAMG_EINVAL and "singular" in str(e):
             return x, np.float64(1.), err, 0  # multigrid.py:167-170
         raise
-    n = two.n
     dev_x = to_device_vec(x).clone()  # x = x.copy()  (:171)
     dev_b = to_device_vec(b)
-    r = torch.empty(n, dtype=torch.float64, device=dev_x.device)
-    tmp = torch.empty_like(r)
-    rc = torch.empty(two.nc, dtype=torch.float64, device=dev_x.device)
-    ec = torch.empty_like(rc)
-    nrm = torch.empty(1, dtype=torch.float64, device=dev_x.device)
-    s = stream_ptr()
-    if smoother == "gauss_seidel":
-        gs = GaussSeidel(two.A)
-
-        def smooth(nu):
-            if nu:
-                gs.sweep(dev_x, dev_b, nu)
-    else:
-        dinv_w = two.A.diag_inv(jacobi_weight)
-
-        def smooth(nu):
-            if nu:
-                call("mlamg_jacobi", two.A.handle, ptr(dinv_w), ptr(dev_b), ptr(dev_x), ptr(tmp),
-                     int(nu), s)
-
-    for i in range(max_iter):
-        smooth(pre_smoothing_steps)
-        two.coarse_correct(dev_x, dev_b, r, rc, ec)
-        smooth(post_smoothing_steps)
-        if res_tol is not None:
-            call("mlamg_residual", two.A.handle, ptr(dev_b), ptr(dev_x), ptr(r), ptr(nrm), s)
-        else:
-            call("mlamg_norm2", ptr(dev_x), n, ptr(nrm), s)
-        e = float(nrm.item())
-        err[i] = e
-        if e <= tol:
-            err = err[:i + 1]
-            break
+    err = H.cycle(dev_b, dev_x, max_iter, tol=tol)  # err[i]; stops after the first e <= tol
     return dev_x.cpu().numpy(), conv_factor(err), err, len(err)
 
 

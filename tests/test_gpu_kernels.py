@@ -300,6 +300,26 @@ def _P1(golden):
                          shape=(1024, 342))
 
 
+@pytest.mark.parametrize("case", ("wide_levels", "grid_200"))
+def test_gauss_seidel_both_schedules(ml, oracle, case):
+    """Level-scheduled GS through the one-workgroup kernel (narrow levels) and the per-level
+    launches (a level wider than 8192 rows), bitwise the sequential pyamg sweep."""
+    rs = np.random.RandomState(11)
+    if case == "wide_levels":
+        n = 30000  # diagonal + a sparse upper band: a few levels of ~10^4 independent rows
+        U = sp.random(n, n, density=2e-5, random_state=rs, format="csr")
+        A = (sp.eye(n) * 4.0 + sp.triu(U, k=1) - sp.triu(U, k=1).T).tocsr()
+    else:
+        A = ml.problems.poisson_2d_5pt(200)
+    A.sort_indices()
+    b = rs.randn(A.shape[0])
+    x0 = rs.randn(A.shape[0])
+    gs = ml.multigrid.GaussSeidel(ml.sparse.as_device(A))
+    ref = oracle.gauss_seidel(A, x0.copy(), b, iterations=3)
+    got = ml.multigrid.gauss_seidel(A, b, x0.copy(), nu=3)
+    assert np.array_equal(got, ref), (case, gs.n_levels)
+
+
 def test_amg_2_v_gauss_seidel(golden, ml):
     A, P = golden_csr(golden, "c1"), _P1(golden)
     x0 = np.random.RandomState(0).normal(0, 1, 1024)
