@@ -170,7 +170,7 @@ def main():
     from mlamg.sparse import DeviceCSR
     Ab = DeviceCSR.from_scipy(A, check=False)
     ab = {}
-    for fmt in ("csr_stream", "sell", "sorted", "sell_dict"):
+    for fmt in ("csr_stream", "sell", "sorted", "sell_dict", "rowpat"):
         Ab.set_format(fmt)
         t = time_kernel(lambda: Ab.matvec(xs, out=ys), reps=30)
         fb = Ab.format_bytes()
@@ -178,7 +178,9 @@ def main():
                    "csr_equivalent_GBps": round(B / t / 1e9, 1)}
     del Ab
     pmc = load_traffic(f"spmv_c4_pmc_{fmt0}.json")
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    # only a PMC measurement of this very kernel (same format, same operator size) applies
+    traffic = (pmc.get("hbm_bytes_per_launch")
+               if pmc and pmc.get("algorithmic_bytes_per_launch") == B_fmt else None)
     cyc_bytes = H.cycle_bytes()
     out = {
         "metric": METRIC,

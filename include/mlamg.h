@@ -93,11 +93,17 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
  *             2 B/nonzero instead of 12. vec_width = sigma as for SELL. EUNSUPPORTED (format
  *             reset to CSR_STREAM) when the dictionaries overflow. */
 #define MLAMG_FMT_SELL_DICT 5
+/* ROWPAT      every row is one of <= 255 distinct patterns (its (col - row, value) sequence in
+ *             stored order; C4's 7-point Laplacian: 27 interior/face/edge/corner patterns) held
+ *             in LDS tables (<= 4096 entries), one byte per row in HBM: lossless, each row summed
+ *             in stored order (scipy's bits). get_format reports the pattern count in
+ *             vec_width. EUNSUPPORTED (format unchanged) when the patterns do not fit. */
+#define MLAMG_FMT_ROWPAT 6
 int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream);
 int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored_entries);
 /* algorithmic HBM bytes of one y = A@x with the active format: matrix stream as stored (CSR:
  * 12*nnz + 4*(n+1); SELL: 12 B per padded element + slice pointers; SELL_DICT: 2 B per code +
- * tables; SORTED: CSR + block tables) + 8*n_cols (x once) + 8*n_rows (y once) */
+ * tables; SORTED: CSR + block tables; ROWPAT: 1 B per row + tables) + 8*n_cols (x once) + 8*n_rows (y once) */
 int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes);
 
 /* ---------------------------------------------------------------- hot-path sparse ops

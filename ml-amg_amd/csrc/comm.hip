@@ -475,8 +475,13 @@ int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cyc
     // the first cycle's first pre-smoothing sweep (later ones are fused into the cycle end)
     MLAMG_TRY(jacobi_from_residual(x_ext, L.dinv, L.r_ext, L.n_own, nullptr, s));
     if (D->cycle_graph) {
+      int c0 = 0;
       if (!(D->exec && D->g_b == b && D->g_x == x_ext && D->g_hist == res_hist &&
             D->g_tol == tol && D->g_epoch == format_epoch())) {
+        // the first cycle runs eagerly: every RCCL peer connection (halo neighbours, the
+        // allgather of coarse segments, the norm all-reduce) is set up outside the capture
+        MLAMG_TRY(dcycle(D, b, x_ext, res_hist, tol, s));
+        c0 = 1;
         dhier_free_graph(D);
         MLAMG_TRY(hier_prepare_ext(D->coarse));
         if (!D->cap_stream)
@@ -507,7 +512,7 @@ int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cyc
         D->g_tol = tol;
         D->g_epoch = format_epoch();
       }
-      for (int c = 0; c < n_cycles; ++c) MLAMG_HIP(hipGraphLaunch(D->exec, s));
+      for (int c = c0; c < n_cycles; ++c) MLAMG_HIP(hipGraphLaunch(D->exec, s));
     } else {
       for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(dcycle(D, b, x_ext, res_hist, tol, s));
     }

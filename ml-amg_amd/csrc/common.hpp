@@ -111,6 +111,17 @@ struct mlamg_csr {
   // constant-coefficient stencils): srt_vi[e] indexes srt_vtab and srt_val is dropped
   uint8_t* srt_vi = nullptr;
   double* srt_vtab = nullptr;
+  // optional row-pair pattern copy ("rowpat" format): every pair of rows (2i, 2i+1) is one of
+  // <= 255 distinct pair patterns (the merge by column offset of the two rows' (col - row,
+  // value) sequences), kept in LDS tables; the matrix stream is one byte per pair.
+  // Constant-coefficient stencils only (C4: 27 pair patterns).
+  uint8_t* rp_pid = nullptr;     // pattern id of each pair
+  int32_t* rp_ptr = nullptr;     // 257 pattern starts into the entry arrays
+  int32_t* rp_off = nullptr;     // per entry (column offset col - row, row 2i mask, row 2i+1
+                                 // mask, flags: bit 0/1 = entry of row 2i/2i+1, bit 2 = "wide");
+                                 // patterns padded to multiples of 8 entries
+  double* rp_val = nullptr;      // per entry (row 2i's value, row 2i+1's value)
+  int32_t rp_n_pat = 0, rp_n_ent = 0;
   // number of per-block partial sums a NORM launch writes with the active format
   int32_t n_part = 0;
 };

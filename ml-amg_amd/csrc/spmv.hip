@@ -373,6 +373,217 @@ __global__ __launch_bounds__(kThreads) void k_sell_dict(const int64_t* __restric
   }
 }
 
+// ---------------------------------------------------------------- row-pair pattern format
+// A constant-coefficient stencil has few distinct rows: as sequences of (col - row, value)
+// pairs in stored order, C4's Laplacian has 27 (interior / face / edge / corner rows). This
+// format keys rows two at a time: pair (2i, 2i+1) carries a one-byte id into <= 255 pair
+// patterns held in LDS, each the merge of its two rows' entries by column offset, with flags
+// saying which row an entry belongs to. Lane per pair: an offset both rows have is ONE 16-byte
+// load x[2i+off .. 2i+off+1], and the epilogue vectors move as 16-byte pairs, so the matrix
+// stream is half a byte per row and a wave instruction moves 1 KB (a lane per row leaves the
+// kernel latency-bound at ~3.3 TB/s). Each row still sums its own entries in stored (ascending
+// column) order: the products and their order are CSR's, hence scipy's bits.
+constexpr int kRpMaxEnt = 2048;
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef double dbl2u __attribute__((ext_vector_type(2), aligned(8)));  // 8-byte aligned pair
+
+__device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// v0 = p[i], v1 = p[i+1] (i even; p[i+1] only when both): one 16-byte load when p is aligned
+__device__ __forceinline__ void ld2(const double* p, int i, bool both, double& v0, double& v1) {
+  if (both && al16(p)) {
+    const dbl2 t = *reinterpret_cast<const dbl2*>(p + i);
+    v0 = t.x;
+    v1 = t.y;
+  } else {
+    v0 = p[i];
+    v1 = both ? p[i + 1] : 0.0;
+  }
+}
+
+__device__ __forceinline__ void st2(double* p, int i, bool both, double v0, double v1) {
+  if (both && al16(p)) {
+    dbl2 t;
+    t.x = v0;
+    t.y = v1;
+    *reinterpret_cast<dbl2*>(p + i) = t;
+  } else {
+    p[i] = v0;
+    if (both) p[i + 1] = v1;
+  }
+}
+
+// epi_load for rows r, r+1
+template <int OP>
+__device__ __forceinline__ void epi_load2(int r, bool both, const Epi& e, EpiIn& u, EpiIn& w) {
+  if constexpr (OP == EPI_AXPBY) {
+    if (e.beta != 0.0) ld2(e.y, r, both, u.a, w.a);
+    if (e.copy_to) ld2(e.dinv, r, both, u.c, w.c);
+  } else if constexpr (OP == EPI_RESID) {
+    ld2(e.b, r, both, u.a, w.a);
+    if (e.copy_to) {
+      ld2(e.copy_from, r, both, u.b, w.b);
+      if (e.dinv) ld2(e.dinv, r, both, u.c, w.c);
+    }
+  } else if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) {
+    ld2(e.b, r, both, u.a, w.a);
+    ld2(e.xin, r, both, u.b, w.b);
+    ld2(e.dinv, r, both, u.c, w.c);
+  } else {  // EPI_ADD
+    ld2(e.y, r, both, u.a, w.a);
+  }
+}
+
+// epi_store's arithmetic for one row, returned instead of stored: the output, the copy_to value
+// (AXPBY/RESID) and the row's r^2 (RESID)
+template <int OP>
+__device__ __forceinline__ double epi_value(double s, const EpiIn& v, const Epi& e, double& c,
+                                            double& sq) {
+  if constexpr (OP == EPI_AXPBY) {
+    const double y = (e.beta == 0.0) ? ((e.alpha == 1.0) ? s : e.alpha * s)
+                                     : e.alpha * s + e.beta * v.a;
+    c = v.c * y;
+    return y;
+  } else if constexpr (OP == EPI_RESID) {
+    const double r = v.a - s;
+    c = e.dinv ? v.b + v.c * r : v.b;
+    sq = r * r;
+    return r;
+  } else if constexpr (OP == EPI_JACOBI) {
+    const double r = v.a - s;
+    return v.b + v.c * r;
+  } else if constexpr (OP == EPI_JACEXP) {
+    const double t1 = v.c * v.a;
+    return v.b + (t1 - s);
+  } else {  // EPI_ADD
+    return v.a + s;
+  }
+}
+
+template <int OP>
+__device__ __forceinline__ double epi_store2(int r, bool both, double s0, double s1,
+                                             const EpiIn& u, const EpiIn& w, const Epi& e) {
+  double c0 = 0.0, c1 = 0.0, q0 = 0.0, q1 = 0.0;
+  const double y0 = epi_value<OP>(s0, u, e, c0, q0);
+  const double y1 = epi_value<OP>(s1, w, e, c1, q1);
+  st2(e.y, r, both, y0, y1);
+  if constexpr (OP == EPI_AXPBY || OP == EPI_RESID)
+    if (e.copy_to) st2(e.copy_to, r, both, c0, c1);
+  return both ? q0 + q1 : q0;
+}
+
+// One pair's row sums (rows r, r+1; patterns padded to multiples of 8 entries from a) from the
+// LDS tables: vv[e] = (row 2i's value, row 2i+1's value), of[e] = (column offset, row 2i mask,
+// row 2i+1 mask, flags).
+__device__ __forceinline__ void rowpair_sums(const double* __restrict__ x, int64_t n_cols, int r,
+                                             int a, int len, const dbl2* vv, const int4* of,
+                                             double& s0, double& s1) {
+  s0 = 0.0;
+  s1 = 0.0;
+  if (len > 0 && (of[a].w & 4)) {
+    // "wide" pattern: x[2i+off .. 2i+off+1] is in range for every entry, so each entry is one
+    // 16-byte buffer load; an entry a row does not have is masked to +0.0 (its table value is
+    // 0.0 too), and adding +0.0 leaves the sum's bits alone (a sum that starts at +0.0 is never
+    // -0.0), so the products and the order each row sums them in are CSR's
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(n_cols * 8), 0x00020000);
+    const int r8 = r * 8;
+    for (int k = 0; k < len; k += 8) {
+      u32x4 t[8];
+      int4 f[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        f[q] = of[a + k + q];
+        t[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, r8 + f[q].x * 8, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const dbl2 v = vv[a + k + q];
+        const uint64_t b0 = ((uint64_t)(t[q].y & (uint32_t)f[q].y) << 32) | (t[q].x & (uint32_t)f[q].y);
+        const uint64_t b1 = ((uint64_t)(t[q].w & (uint32_t)f[q].z) << 32) | (t[q].z & (uint32_t)f[q].z);
+        s0 += v.x * __longlong_as_double((long long)b0);
+        s1 += v.y * __longlong_as_double((long long)b1);
+      }
+    }
+    return;
+  }
+  // edge pairs (first / last rows of the matrix, odd tail): per-row loads as needed
+  const double* xr = x + r;
+  for (int k = 0; k < len; k += 8) {
+    double x0[8], x1[8];
+    int fl[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int4 f = of[a + k + q];
+      fl[q] = f.w;
+      x0[q] = (fl[q] & 1) ? xr[f.x] : 0.0;
+      x1[q] = (fl[q] & 2) ? xr[f.x + 1] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (fl[q] & 1) s0 += vv[a + k + q].x * x0[q];
+      if (fl[q] & 2) s1 += vv[a + k + q].y * x1[q];
+    }
+  }
+}
+
+// CH chunks of 256 pairs per workgroup (tables staged once; the next chunk's pattern ids are
+// fetched while the current chunk gathers)
+template <int OP, bool NORM, int CH>
+__global__ __launch_bounds__(kThreads) void k_rowpair(const uint8_t* __restrict__ pid,
+                                                      const int32_t* __restrict__ pat_ptr,
+                                                      const int4* __restrict__ pat_of,
+                                                      const dbl2* __restrict__ pat_vv,
+                                                      int n_ent, int64_t n_rows, int64_t n_cols,
+                                                      const double* __restrict__ x, Epi ep) {
+  // LDS: vv[n_ent] (16 B) | of[n_ent] (16 B) | starts[257]
+  extern __shared__ dbl2 rp_lds[];
+  __shared__ double red[kThreads / 64];
+  if (ep.done && *ep.done) return;
+  dbl2* vv = rp_lds;
+  int4* of = reinterpret_cast<int4*>(rp_lds + n_ent);
+  int32_t* pst = reinterpret_cast<int32_t*>(of + n_ent);
+  const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t pr0 = lb * CH * kThreads + threadIdx.x;  // this lane's pair in chunk 0
+  int p = 2 * pr0 < n_rows ? (int)pid[pr0] : 0;
+  for (int i = threadIdx.x; i < n_ent; i += kThreads) {
+    vv[i] = pat_vv[i];
+    of[i] = pat_of[i];
+  }
+  for (int i = threadIdx.x; i < 257; i += kThreads) pst[i] = pat_ptr[i];
+  double sq = 0.0;
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < CH; ++c) {
+    const int64_t pr = pr0 + (int64_t)c * kThreads;
+    const bool ok0 = 2 * pr < n_rows;
+    const bool both = 2 * pr + 1 < n_rows;
+    const int r = ok0 ? (int)(2 * pr) : 0;
+    const int p_next =
+        (c + 1 < CH && 2 * (pr + kThreads) < n_rows) ? (int)pid[pr + kThreads] : 0;
+    EpiIn u, w;
+    if (ok0) epi_load2<OP>(r, both, ep, u, w);
+    const int a = pst[p];
+    const int len = ok0 ? pst[p + 1] - a : 0;
+    double s0, s1;
+    rowpair_sums(x, n_cols, r, a, len, vv, of, s0, s1);
+    if (ok0) sq += epi_store2<OP>(r, both, s0, s1, u, w, ep);
+    p = p_next;
+  }
+  if constexpr (NORM) {
+    double v = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+      ep.partial[lb] = t;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- CSR-vector variant
 // VW lanes per row (long rows of coarse Galerkin operators). Lane l sums entries l, l+VW, ...
 // in order, then the VW partials are combined by an xor butterfly (off = VW/2 .. 1). This is a
@@ -621,10 +832,47 @@ static int dict_slices_per_wave() {
   return v;
 }
 
+// 256-pair chunks per workgroup of the row-pair kernel (env MLAMG_RP_CHUNKS = 1, 2, 4 or 8)
+static int rowpair_chunks() {
+  static int v = [] {
+    const char* e = std::getenv("MLAMG_RP_CHUNKS");
+    const int k = e ? std::atoi(e) : 4;
+    return (k == 1 || k == 2 || k == 4 || k == 8) ? k : 4;
+  }();
+  return v;
+}
+
+template <int OP, bool NORM, int CH>
+static int launch_rowpair_ch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  const int64_t n_pairs = (A->n_rows + 1) / 2;
+  const unsigned nb = (unsigned)((n_pairs + CH * kThreads - 1) / (CH * kThreads));
+  const size_t lds = (size_t)A->rp_n_ent * 32 + 257 * 4;
+  hipLaunchKernelGGL((k_rowpair<OP, NORM, CH>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid,
+                     A->rp_ptr, reinterpret_cast<const int4*>(A->rp_off),
+                     reinterpret_cast<const dbl2*>(A->rp_val), A->rp_n_ent, A->n_rows,
+                     A->n_cols, x, ep);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+template <int OP, bool NORM>
+static int launch_rowpair(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  switch (rowpair_chunks()) {
+    case 1: return launch_rowpair_ch<OP, NORM, 1>(A, x, ep, s);
+    case 2: return launch_rowpair_ch<OP, NORM, 2>(A, x, ep, s);
+    case 8: return launch_rowpair_ch<OP, NORM, 8>(A, x, ep, s);
+    default: return launch_rowpair_ch<OP, NORM, 4>(A, x, ep, s);
+  }
+}
+
 // ---------------------------------------------------------------- launch helpers
 template <int OP, bool NORM>
 static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   if (A->vec_width) return launch_vec<OP, NORM>(A, x, ep, s);
+  if (A->rp_pid) {
+    if (A->n_rows == 0) return MLAMG_OK;
+    return launch_rowpair<OP, NORM>(A, x, ep, s);
+  }
   if (A->srt_pk) {
     if (A->srt_nb == 0) return MLAMG_OK;
     if (A->srt_vi)
@@ -1208,6 +1456,308 @@ static int build_sorted(mlamg_csr* A, hipStream_t s) {
   return MLAMG_OK;
 }
 
+// ---------------------------------------------------------------- row-pair pattern construction
+// A pair's key: a 64-bit hash of both rows' lengths and (col - row, value bits) sequences. Pairs
+// are inserted into an open-addressing table (<= 255 keys, else refused) with the smallest pair
+// of each key as its representative; the host orders patterns by representative, reads their
+// rows and merges them by offset (rows must be strictly column-sorted), and k_rp_assign then
+// checks every pair against its pattern entry by entry (a hash collision makes the format
+// refuse, it never changes a result).
+__device__ __forceinline__ unsigned long long rp_mix(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ unsigned long long rp_row_key(const int32_t* __restrict__ ip,
+                                                         const int32_t* __restrict__ ij,
+                                                         const double* __restrict__ ax,
+                                                         int64_t row, unsigned long long h) {
+  const int a = ip[row], b = ip[row + 1];
+  h = rp_mix(h ^ (0x9E3779B97F4A7C15ull + (unsigned long long)(b - a)));
+  for (int e = a; e < b; ++e) {
+    h = rp_mix(h ^ (unsigned long long)(uint32_t)(ij[e] - (int32_t)row));
+    h = rp_mix(h ^ (unsigned long long)__double_as_longlong(ax[e]));
+  }
+  return h;
+}
+
+// "wide" pair: every 16-byte load x[col0 .. col0+1] of the kernel's wide path is in range, i.e.
+// row 2i's columns are <= n_cols - 2 and row 2i+1's >= 1 (false only at the matrix edges)
+__device__ __forceinline__ bool rp_pair_wide(const int32_t* __restrict__ ip,
+                                             const int32_t* __restrict__ ij, int64_t n,
+                                             int64_t n_cols, int64_t pr) {
+  if (2 * pr + 1 >= n) return false;
+  for (int e = ip[2 * pr]; e < ip[2 * pr + 1]; ++e)
+    if (ij[e] > n_cols - 2) return false;
+  for (int e = ip[2 * pr + 1]; e < ip[2 * pr + 2]; ++e)
+    if (ij[e] < 1) return false;
+  return true;
+}
+
+__device__ __forceinline__ unsigned long long rp_pair_key(const int32_t* __restrict__ ip,
+                                                          const int32_t* __restrict__ ij,
+                                                          const double* __restrict__ ax,
+                                                          int64_t n, int64_t n_cols, int64_t pr) {
+  unsigned long long h = rp_row_key(ip, ij, ax, 2 * pr, 0x243F6A8885A308D3ull);
+  h = 2 * pr + 1 < n ? rp_row_key(ip, ij, ax, 2 * pr + 1, h) : rp_mix(h ^ 0xA5A5A5A5ull);
+  h = rp_mix(h ^ (rp_pair_wide(ip, ij, n, n_cols, pr) ? 0x1234567ull : 0x7654321ull));
+  return h == kDictEmpty ? 0x5DEECE66Dull : h;
+}
+
+__global__ void k_rp_insert(const int32_t* __restrict__ ip, const int32_t* __restrict__ ij,
+                            const double* __restrict__ ax, int64_t n, int64_t n_cols,
+                            int64_t n_pairs, unsigned long long* tab, int32_t* rep,
+                            int32_t* counts) {
+  const int64_t pr = blockIdx.x * 256ll + threadIdx.x;
+  if (pr >= n_pairs) return;
+  if (((volatile int32_t*)counts)[0] > 255 || ((volatile int32_t*)counts)[2] != 0) return;
+  const int sl = dict_slot(rp_pair_key(ip, ij, ax, n, n_cols, pr), tab, counts, true);
+  if (sl < 0) {
+    atomicAdd(counts + 2, 1);
+    return;
+  }
+  if ((int32_t)pr < ((volatile int32_t*)rep)[sl]) atomicMin(rep + sl, (int32_t)pr);
+}
+
+// does row `row` consist exactly of the pattern entries flagged `bit`, in order? (pat_of[4k] =
+// offset, pat_of[4k+3] = flags; pat_vv[2k + (bit == 2)] = the row's value)
+__device__ __forceinline__ bool rp_row_matches(const int32_t* __restrict__ ip,
+                                               const int32_t* __restrict__ ij,
+                                               const double* __restrict__ ax, int64_t row,
+                                               int pa, int pb, int bit,
+                                               const int32_t* __restrict__ pat_of,
+                                               const double* __restrict__ pat_vv) {
+  int e = ip[row];
+  const int eb = ip[row + 1];
+  for (int k = pa; k < pb; ++k) {
+    if (!(pat_of[4 * k + 3] & bit)) continue;  // bit 2 (wide) is not a row flag
+    if (e >= eb || ij[e] - (int32_t)row != pat_of[4 * k] ||
+        __double_as_longlong(ax[e]) != __double_as_longlong(pat_vv[2 * k + (bit == 2)]))
+      return false;
+    ++e;
+  }
+  return e == eb;
+}
+
+__global__ void k_rp_assign(const int32_t* __restrict__ ip, const int32_t* __restrict__ ij,
+                            const double* __restrict__ ax, int64_t n, int64_t n_cols,
+                            int64_t n_pairs, unsigned long long* tab,
+                            const int32_t* __restrict__ slot_pid,
+                            const int32_t* __restrict__ pat_ptr, const int32_t* __restrict__ pat_of,
+                            const double* __restrict__ pat_vv, uint8_t* __restrict__ pid,
+                            int32_t* bad) {
+  const int64_t pr = blockIdx.x * 256ll + threadIdx.x;
+  if (pr >= n_pairs) return;
+  const int sl = dict_slot(rp_pair_key(ip, ij, ax, n, n_cols, pr), tab, nullptr, false);
+  bool ok = sl >= 0;
+  const int p = ok ? slot_pid[sl] : 0;
+  if (ok) {
+    const int pa = pat_ptr[p], pb = pat_ptr[p + 1];
+    // the kernel takes the wide path on the first entry's bit 2: it must be this pair's own
+    const bool wide_ok =
+        pb == pa || ((pat_of[4 * pa + 3] & 4) != 0) == rp_pair_wide(ip, ij, n, n_cols, pr);
+    ok = wide_ok && rp_row_matches(ip, ij, ax, 2 * pr, pa, pb, 1, pat_of, pat_vv);
+    if (ok && 2 * pr + 1 < n)
+      ok = rp_row_matches(ip, ij, ax, 2 * pr + 1, pa, pb, 2, pat_of, pat_vv);
+    if (ok && 2 * pr + 1 >= n)  // the last pair of an odd n has no row 2i+1 entries
+      for (int k = pa; k < pb; ++k) ok = ok && !(pat_of[4 * k + 3] & 2);
+  }
+  if (!ok) atomicAdd(bad, 1);
+  pid[pr] = (uint8_t)p;
+}
+
+static void drop_rowpat(mlamg_csr* A) {
+  for (void* p : {(void*)A->rp_pid, (void*)A->rp_ptr, (void*)A->rp_off, (void*)A->rp_val})
+    if (p) (void)hipFree(p);
+  A->rp_pid = nullptr;
+  A->rp_ptr = nullptr;
+  A->rp_off = nullptr;
+  A->rp_val = nullptr;
+  A->rp_n_pat = A->rp_n_ent = 0;
+  if (!A->sell_ptr && !A->vec_width && !A->srt_pk) A->n_part = A->n_blocks;
+}
+
+// EUNSUPPORTED (A unchanged) past 255 distinct pair patterns, kRpMaxEnt pattern entries, or
+// when a representative row is not strictly column-sorted.
+static int build_rowpat(mlamg_csr* A, hipStream_t s) {
+  const int64_t n = A->n_rows;
+  const int64_t n_pairs = (n + 1) / 2;
+  MLAMG_REQUIRE(n < (int64_t(1) << 31) - 1, "rowpat: more than 2^31 - 2 rows");
+  if (A->n_cols >= (int64_t(1) << 29)) {  // x is addressed by 32-bit buffer byte offsets
+    set_error("rowpat: more than 2^29 columns");
+    return MLAMG_EUNSUPPORTED;
+  }
+  unsigned long long* tab = nullptr;
+  int32_t *rep = nullptr, *counts = nullptr, *slot_pid = nullptr;
+  uint8_t* pid = nullptr;
+  int32_t *pptr = nullptr, *poff = nullptr;
+  double* pval = nullptr;
+  int rc = MLAMG_OK;
+  auto fail = [&](int code, const std::string& what) {
+    if (rc == MLAMG_OK) {
+      set_error("rowpat: " + what);
+      rc = code;
+    }
+  };
+  if (hipMalloc(&tab, sizeof(unsigned long long) * kDictSlots) != hipSuccess ||
+      hipMalloc(&rep, sizeof(int32_t) * kDictSlots) != hipSuccess ||
+      hipMalloc(&counts, sizeof(int32_t) * 4) != hipSuccess ||
+      hipMalloc(&slot_pid, sizeof(int32_t) * kDictSlots) != hipSuccess ||
+      hipMalloc(&pid, std::max<int64_t>(n_pairs, 1)) != hipSuccess ||
+      hipMalloc(&pptr, sizeof(int32_t) * 257) != hipSuccess)
+    fail(MLAMG_ENOMEM, "out of device memory");
+  if (rc == MLAMG_OK &&
+      (hipMemsetAsync(tab, 0xFF, sizeof(unsigned long long) * kDictSlots, s) != hipSuccess ||
+       hipMemsetAsync(rep, 0x7F, sizeof(int32_t) * kDictSlots, s) != hipSuccess ||
+       hipMemsetAsync(counts, 0, sizeof(int32_t) * 4, s) != hipSuccess))
+    fail(MLAMG_EHIP, "memset");
+  const unsigned nb = (unsigned)((n_pairs + 255) / 256);
+  if (rc == MLAMG_OK && n_pairs)
+    hipLaunchKernelGGL(k_rp_insert, dim3(nb), dim3(256), 0, s, A->indptr, A->indices, A->data, n,
+                       A->n_cols, n_pairs, tab, rep, counts);
+  std::vector<unsigned long long> ht(kDictSlots);
+  std::vector<int32_t> hrep(kDictSlots);
+  int32_t hc[4] = {0, 0, 0, 0};
+  if (rc == MLAMG_OK &&
+      (hipGetLastError() != hipSuccess ||
+       hipMemcpyAsync(ht.data(), tab, sizeof(unsigned long long) * kDictSlots,
+                      hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipMemcpyAsync(hrep.data(), rep, sizeof(int32_t) * kDictSlots, hipMemcpyDeviceToHost,
+                      s) != hipSuccess ||
+       hipMemcpyAsync(hc, counts, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
+       hipStreamSynchronize(s) != hipSuccess))
+    fail(MLAMG_EHIP, "pattern scan");
+  if (rc == MLAMG_OK && (hc[2] != 0 || hc[0] > 255))
+    fail(MLAMG_EUNSUPPORTED, "more than 255 distinct row-pair patterns");
+  std::vector<int32_t> hptr(257, 0), hoff;
+  std::vector<double> hv0, hv1;
+  std::vector<uint8_t> hfl;
+  int n_pat = 0;
+  if (rc == MLAMG_OK) {
+    // patterns in order of first occurrence: deterministic ids
+    std::vector<std::pair<int32_t, int>> pats;
+    for (int i = 0; i < kDictSlots; ++i)
+      if (ht[i] != kDictEmpty) pats.push_back({hrep[i], i});
+    std::sort(pats.begin(), pats.end());
+    n_pat = (int)pats.size();
+    std::vector<int32_t> hslot(kDictSlots, 0);
+    auto fetch_row = [&](int64_t row, std::vector<int32_t>& off, std::vector<double>& val) {
+      off.clear();
+      val.clear();
+      if (row >= n) return true;
+      int32_t ab[2];
+      if (hipMemcpy(ab, A->indptr + row, sizeof(ab), hipMemcpyDeviceToHost) != hipSuccess)
+        return false;
+      const int len = ab[1] - ab[0];
+      off.resize(len);
+      val.resize(len);
+      if (len && (hipMemcpy(off.data(), A->indices + ab[0], sizeof(int32_t) * len,
+                            hipMemcpyDeviceToHost) != hipSuccess ||
+                  hipMemcpy(val.data(), A->data + ab[0], sizeof(double) * len,
+                            hipMemcpyDeviceToHost) != hipSuccess))
+        return false;
+      for (auto& c : off) c -= (int32_t)row;
+      return true;
+    };
+    std::vector<int32_t> o0, o1;
+    std::vector<double> w0, w1;
+    for (size_t k = 0; k < pats.size() && rc == MLAMG_OK; ++k) {
+      hslot[pats[k].second] = (int32_t)k;
+      const int64_t r0 = 2 * (int64_t)pats[k].first;
+      if (!fetch_row(r0, o0, w0) || !fetch_row(r0 + 1, o1, w1)) {
+        fail(MLAMG_EHIP, "pattern fetch");
+        break;
+      }
+      for (auto* o : {&o0, &o1})
+        for (size_t e = 1; e < o->size(); ++e)
+          if ((*o)[e] <= (*o)[e - 1]) fail(MLAMG_EUNSUPPORTED, "rows are not column-sorted");
+      if (rc != MLAMG_OK) break;
+      // wide (see rp_pair_wide): the same rule on the representative pair
+      bool wide = r0 + 1 < n;
+      for (int32_t o : o0) wide = wide && r0 + o <= A->n_cols - 2;
+      for (int32_t o : o1) wide = wide && r0 + 1 + o >= 1;
+      // merge the two rows by offset (each row keeps its stored = ascending order)
+      size_t i = 0, j = 0;
+      while (i < o0.size() || j < o1.size()) {
+        const bool t0 = i < o0.size() && (j >= o1.size() || o0[i] <= o1[j]);
+        const bool t1 = j < o1.size() && (i >= o0.size() || o1[j] <= o0[i]);
+        hoff.push_back(t0 ? o0[i] : o1[j]);
+        hv0.push_back(t0 ? w0[i] : 0.0);
+        hv1.push_back(t1 ? w1[j] : 0.0);
+        hfl.push_back((uint8_t)((t0 ? 1 : 0) | (t1 ? 2 : 0) | (wide ? 4 : 0)));
+        i += t0;
+        j += t1;
+      }
+      while (hoff.size() % 8) {  // pad to whole 8-entry steps of the kernel: null entries
+        hoff.push_back(0);
+        hv0.push_back(0.0);
+        hv1.push_back(0.0);
+        hfl.push_back((uint8_t)(wide ? 4 : 0));
+      }
+      if ((int)hoff.size() > kRpMaxEnt) {
+        fail(MLAMG_EUNSUPPORTED, "row-pair patterns hold more than 2048 (padded) entries");
+        break;
+      }
+      hptr[k + 1] = (int32_t)hoff.size();
+    }
+    for (size_t k = pats.size() + 1; k < 257; ++k) hptr[k] = (int32_t)hoff.size();
+    const size_t ne = hoff.size(), na = std::max<size_t>(ne, 1);
+    // interleaved records: (offset, flags) and (row 2i value, row 2i+1 value)
+    std::vector<int32_t> hof(4 * ne);
+    std::vector<double> hvv(2 * ne);
+    for (size_t e = 0; e < ne; ++e) {
+      hof[4 * e] = hoff[e];
+      hof[4 * e + 1] = (hfl[e] & 1) ? -1 : 0;
+      hof[4 * e + 2] = (hfl[e] & 2) ? -1 : 0;
+      hof[4 * e + 3] = hfl[e];
+      hvv[2 * e] = hv0[e];
+      hvv[2 * e + 1] = hv1[e];
+    }
+    if (rc == MLAMG_OK &&
+        (hipMalloc(&poff, sizeof(int32_t) * 4 * na) != hipSuccess ||
+         hipMalloc(&pval, sizeof(double) * 2 * na) != hipSuccess))
+      fail(MLAMG_ENOMEM, "out of device memory");
+    if (rc == MLAMG_OK &&
+        (hipMemcpyAsync(pptr, hptr.data(), sizeof(int32_t) * 257, hipMemcpyHostToDevice, s) != hipSuccess ||
+         (ne && (hipMemcpyAsync(poff, hof.data(), sizeof(int32_t) * 4 * ne, hipMemcpyHostToDevice, s) != hipSuccess ||
+                 hipMemcpyAsync(pval, hvv.data(), sizeof(double) * 2 * ne, hipMemcpyHostToDevice, s) != hipSuccess)) ||
+         hipMemcpyAsync(slot_pid, hslot.data(), sizeof(int32_t) * kDictSlots, hipMemcpyHostToDevice, s) != hipSuccess ||
+         hipMemsetAsync(counts, 0, sizeof(int32_t) * 4, s) != hipSuccess))
+      fail(MLAMG_EHIP, "upload");
+    if (rc == MLAMG_OK && n_pairs)
+      hipLaunchKernelGGL(k_rp_assign, dim3(nb), dim3(256), 0, s, A->indptr, A->indices, A->data,
+                         n, A->n_cols, n_pairs, tab, slot_pid, pptr, poff, pval, pid, counts);
+    if (rc == MLAMG_OK &&
+        (hipGetLastError() != hipSuccess ||
+         hipMemcpyAsync(hc, counts, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
+         hipStreamSynchronize(s) != hipSuccess))
+      fail(MLAMG_EHIP, "assign");
+    if (rc == MLAMG_OK && hc[0] != 0)
+      fail(MLAMG_EUNSUPPORTED, "row-pair pattern hash collision");
+  }
+  for (void* p : {(void*)tab, (void*)rep, (void*)counts, (void*)slot_pid})
+    if (p) (void)hipFree(p);
+  if (rc != MLAMG_OK) {
+    for (void* p : {(void*)pid, (void*)pptr, (void*)poff, (void*)pval})
+      if (p) (void)hipFree(p);
+    return rc;
+  }
+  drop_rowpat(A);
+  A->rp_pid = pid;
+  A->rp_ptr = pptr;
+  A->rp_off = poff;
+  A->rp_val = pval;
+  A->rp_n_pat = n_pat;
+  A->rp_n_ent = (int32_t)hoff.size();
+  return MLAMG_OK;
+}
+
+static int32_t rowpat_parts(const mlamg_csr* A) {
+  const int64_t n_pairs = (A->n_rows + 1) / 2, per = (int64_t)rowpair_chunks() * kThreads;
+  return (int32_t)std::max<int64_t>(1, (n_pairs + per - 1) / per);
+}
+
 int launch_spmv_plain(const mlamg_csr* A, const double* x, double* y, hipStream_t s) {
   Epi ep{};
   ep.alpha = 1.0;
@@ -1358,27 +1908,32 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
   bump_format_epoch();
   switch (fmt) {
     case MLAMG_FMT_CSR_STREAM:
+      drop_rowpat(A);
       drop_sell(A);
       drop_sorted(A);
       A->vec_width = 0;
       return MLAMG_OK;
     case MLAMG_FMT_SELL:
       A->vec_width = 0;
+      drop_rowpat(A);
       drop_sorted(A);
       return build_sell(A, s, vec_width > 1 ? vec_width : 1);  // vec_width doubles as sigma
     case MLAMG_FMT_SELL_DICT:
       A->vec_width = 0;
+      drop_rowpat(A);
       drop_sorted(A);
       return build_sell_dict(A, s, vec_width > 1 ? vec_width : 1);
     case MLAMG_FMT_SORTED: {
       // built first, so an unsupported matrix keeps its current format
       MLAMG_TRY(build_sorted(A, s));
+      drop_rowpat(A);
       drop_sell(A);
       A->vec_width = 0;
       A->n_part = A->srt_nb;
       return MLAMG_OK;
     }
     case MLAMG_FMT_VECTOR: {
+      drop_rowpat(A);
       drop_sell(A);
       drop_sorted(A);
       int vw = vec_width;
@@ -1403,12 +1958,21 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       // SELL-64-sigma (rows sorted by length inside windows of 512) if that does, else
       // CSR-stream
       A->vec_width = 0;
+      drop_rowpat(A);
       drop_sorted(A);
       MLAMG_TRY(build_sell(A, s, 1));
       if (A->nnz > 0 && (double)A->sell_elems <= 1.15 * (double)A->nnz) return MLAMG_OK;
       MLAMG_TRY(build_sell(A, s, 512));
       if (A->nnz > 0 && (double)A->sell_elems <= 1.15 * (double)A->nnz) return MLAMG_OK;
       drop_sell(A);
+      return MLAMG_OK;
+    }
+    case MLAMG_FMT_ROWPAT: {
+      MLAMG_TRY(build_rowpat(A, s));  // built first: an unsupported matrix keeps its format
+      drop_sell(A);
+      drop_sorted(A);
+      A->vec_width = 0;
+      A->n_part = rowpat_parts(A);
       return MLAMG_OK;
     }
     default:
@@ -1423,6 +1987,8 @@ int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
   double b = 8.0 * m + 8.0 * n;  // x read once, y written once
   if (A->vec_width) {
     b += 12.0 * A->nnz + 4.0 * (n + 1);
+  } else if (A->rp_pid) {
+    b += 1.0 * ((A->n_rows + 1) / 2) + 4.0 * 257 + 32.0 * A->rp_n_ent;  // pair ids + tables
   } else if (A->srt_pk) {
     b += (A->srt_vi ? 5.0 : 12.0) * A->nnz + 4.0 * (n + 1) + 4.0 * (A->srt_nb + 1) +
          12.0 * A->srt_nb;
@@ -1443,6 +2009,7 @@ int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
 int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored) {
   MLAMG_REQUIRE(A, "NULL argument");
   const int f = A->vec_width  ? MLAMG_FMT_VECTOR
+                : A->rp_pid    ? MLAMG_FMT_ROWPAT
                 : A->srt_pk    ? MLAMG_FMT_SORTED
                 : A->dict_code ? MLAMG_FMT_SELL_DICT
                 : A->sell_ptr  ? MLAMG_FMT_SELL
@@ -1450,7 +2017,10 @@ int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* 
   if (fmt) *fmt = f;
   // SORTED reports 1 in vec_width when its values are dictionary-coded
   if (vec_width)
-    *vec_width = A->vec_width ? A->vec_width : (A->srt_pk ? (A->srt_vi ? 1 : 0) : A->sell_sigma);
+    *vec_width = A->vec_width ? A->vec_width
+                 : A->rp_pid  ? A->rp_n_pat
+                 : A->srt_pk  ? (A->srt_vi ? 1 : 0)
+                              : A->sell_sigma;
   if (stored) *stored = A->sell_ptr ? A->sell_elems : A->nnz;
   return MLAMG_OK;
 }

@@ -95,7 +95,7 @@ class Hierarchy:
         return H
 
     EXACT_CANDIDATES = (("csr_stream", 0), ("sell", 1), ("sell", 512), ("sorted", 0),
-                        ("sell_dict", 1), ("sell_dict", 512))
+                        ("sell_dict", 1), ("sell_dict", 512), ("rowpat", 0))
     VECTOR_CANDIDATES = (("vector", 8), ("vector", 16), ("vector", 32), ("vector", 64),
                          ("vector", 128), ("vector", 256), ("vector", 512))
 

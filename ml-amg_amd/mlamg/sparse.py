@@ -135,7 +135,7 @@ class DeviceCSR:
         return NotImplemented
 
     FORMATS = {"csr_stream": 0, "sell": 1, "vector": 2, "auto_exact": 3, "sorted": 4,
-               "sell_dict": 5}
+               "sell_dict": 5, "rowpat": 6}
 
     def set_format(self, fmt, vec_width=0):
         """SpMV kernel/storage: 'csr_stream' | 'sell' | 'sorted' | 'auto_exact' (scipy order)

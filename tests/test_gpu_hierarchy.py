@@ -32,7 +32,8 @@ def dev(torch, x):
 
 
 @pytest.mark.parametrize("k", MATS)
-@pytest.mark.parametrize("fmt", ("sell", "csr_stream", "auto_exact", "sorted", "sell_dict"))
+@pytest.mark.parametrize("fmt", ("sell", "csr_stream", "auto_exact", "sorted", "sell_dict",
+                                 "rowpat"))
 def test_exact_formats_bitwise(golden, ml, torch_cuda, k, fmt):
     torch = torch_cuda
     A = golden_csr(golden, k)
@@ -40,8 +41,8 @@ def test_exact_formats_bitwise(golden, ml, torch_cuda, k, fmt):
     Ad = ml.sparse.DeviceCSR.from_scipy(A)
     try:
         Ad.set_format(fmt)
-    except MlamgError as e:  # sell_dict on operators with many distinct values
-        assert fmt == "sell_dict" and e.code == MLAMG_EUNSUPPORTED
+    except MlamgError as e:  # sell_dict / rowpat on operators with many distinct values
+        assert fmt in ("sell_dict", "rowpat") and e.code == MLAMG_EUNSUPPORTED
         assert Ad.get_format()[0] == "csr_stream"
     x = dev(torch, golden[f"{k}_x"])
     assert np.array_equal(Ad.matvec(x).cpu().numpy(), golden[f"{k}_Ax"])
@@ -185,7 +186,7 @@ def test_graph_recaptured_after_format_change(ml, torch_cuda):
     H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=100, coarse_format="exact")
     ref = dev(torch, x0)
     h_ref = H.cycle(bd, ref, 4, use_graph=False)
-    for fmt in ("csr_stream", "sell_dict", "sorted", "sell"):
+    for fmt in ("csr_stream", "sell_dict", "sorted", "sell", "rowpat"):
         x = dev(torch, x0)
         H.cycle(bd, x, 1, use_graph=True)   # capture with the current formats
         for L in H.levels:                  # then swap every operator's storage
@@ -329,3 +330,84 @@ def test_c4_full_size_properties(ml, oracle, torch_cuda):
     assert np.all(np.diff(hist) < 0)
     conv = (hist[-1] / hist[-4]) ** (1 / 3)
     assert 0.3 < conv < 0.8
+
+
+def _pair_patterns(A):
+    """Distinct row-pair patterns of the rowpat format and their merged entry counts."""
+    n = A.shape[0]
+
+    def row(i):
+        if i >= n:
+            return (), b""
+        a, b = A.indptr[i], A.indptr[i + 1]
+        return tuple(A.indices[a:b] - i), A.data[a:b].tobytes()
+
+    pats = {}
+    for i in range(0, n, 2):
+        (o0, v0), (o1, v1) = row(i), row(i + 1)
+        pats[(o0, v0, o1, v1)] = -(-len(set(o0) | set(o1)) // 8) * 8  # padded to 8
+    return len(pats), sum(pats.values())
+
+
+def test_rowpat_format(ml, torch_cuda):
+    """Row-pair pattern format: bitwise CSR order on stencils (3D, 2D with odd n so pairs
+    straddle grid lines and the last pair is single), boundary rows and empty rows included,
+    every epilogue through the hierarchy, a -0.0 entry kept apart, refusal (format unchanged)
+    past 255 patterns, format bytes."""
+    torch = torch_cuda
+    from mlamg._lib import MLAMG_EUNSUPPORTED, MlamgError, call, ptr, stream_ptr
+    rs = np.random.RandomState(11)
+    for A in (ml.problems.poisson_3d_7pt(20), ml.problems.poisson_2d_5pt(37)):
+        n = A.shape[0]
+        npat, n_ent = _pair_patterns(A)
+        x, b = rs.randn(n), rs.randn(n)
+        xd, bd = dev(torch, x), dev(torch, b)
+        Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("rowpat")
+        assert Ad.get_format()[:2] == ("rowpat", npat)
+        assert Ad.format_bytes() == 16.0 * n + (n + 1) // 2 + 4 * 257 + 32 * n_ent
+        assert np.array_equal(Ad.matvec(xd).cpu().numpy(), A @ x)
+        r = torch.empty(n, dtype=torch.float64, device="cuda")
+        nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
+        call("mlamg_residual", Ad.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), stream_ptr())
+        assert np.array_equal(r.cpu().numpy(), b - A @ x)
+        assert abs(nrm.item() - np.linalg.norm(b - A @ x)) <= 1e-13 * np.linalg.norm(b - A @ x)
+        # misaligned vectors (8-byte aligned views): the scalar epilogue path, same bits
+        xo = torch.zeros(n + 1, dtype=torch.float64, device="cuda")
+        xo[1:] = xd
+        yo = torch.zeros(n + 1, dtype=torch.float64, device="cuda")
+        call("mlamg_spmv", Ad.handle, ptr(xo[1:]), ptr(yo[1:]), 1.0, 0.0, stream_ptr())
+        assert np.array_equal(yo[1:].cpu().numpy(), A @ x)
+    A = ml.problems.poisson_3d_7pt(20)
+    n = A.shape[0]
+    x = rs.randn(n)
+    xd = dev(torch, x)
+    # a -0.0 value and an emptied row make pair patterns of their own
+    B = A.tolil()
+    B[7, :] = 0
+    B = B.tocsr()
+    B.eliminate_zeros()
+    B.data = B.data.copy()
+    B.data[100] = -0.0
+    Bd = ml.sparse.DeviceCSR.from_scipy(B).set_format("rowpat")
+    assert Bd.get_format()[1] == _pair_patterns(B)[0]
+    assert np.array_equal(Bd.matvec(xd).cpu().numpy(), B @ x)
+    # > 255 patterns -> refused, format unchanged, still bitwise
+    R = sp.random(2000, 2000, density=0.01, random_state=rs, format="csr")
+    Rd = ml.sparse.DeviceCSR.from_scipy(R).set_format("sell")
+    with pytest.raises(MlamgError) as ei:
+        Rd.set_format("rowpat")
+    assert ei.value.code == MLAMG_EUNSUPPORTED
+    assert Rd.get_format()[0] == "sell"
+    xr = rs.randn(2000)
+    assert np.array_equal(Rd.matvec(dev(torch, xr)).cpu().numpy(), R @ xr)
+    # whole cycle with the fine operator as row-pair patterns == all-CSR-stream cycle
+    b = rs.randn(n)
+    bd = dev(torch, b)
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=100, fine_format="csr_stream")
+    H2 = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=100, fine_format="csr_stream")
+    H2.levels[0].A.set_format("rowpat")
+    x1, x2 = dev(torch, x), dev(torch, x)
+    h1 = H.cycle(bd, x1, 5)
+    h2 = H2.cycle(bd, x2, 5)
+    assert torch.equal(x1, x2)
+    assert np.allclose(h1, h2, rtol=1e-14, atol=0)

@@ -18,7 +18,7 @@ step() {  # name timeout cmd...
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step pytest_gpu 900 python -m pytest tests -q -m gpu --timeout 300 -rf
+  step pytest_gpu 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -rf
 fi
 if [ "$MODE" = all ] || [ "$MODE" = smoke ]; then
   step smoke 300 python __graft_entry__.py smoke

@@ -1,0 +1,160 @@
+// Gather-pattern lab for the C4 fine-level SpMV (216^3 7-point Laplacian): how fast can the
+// x gather of a 7-point stencil run on MI355X, compared with a plain stream of the same bytes?
+// Diagnostics only (no bitwise claims): every variant reads x (80 MB) and writes y (80 MB).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/stencil_lab.hip -o /tmp/stencil_lab
+//   /tmp/stencil_lab [n=216] [reps=50]
+// Variants (MASK of neighbour offsets gathered besides the centre: bit0 +-1, bit1 +-n,
+// bit2 +-n^2); ORDER 0 = XCD-chunked block order, 1 = plain blockIdx order;
+// PAIR 1 = lane per row pair with 16-byte loads, 0 = lane per row with 8-byte loads.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e = (x);                                                              \
+    if (e != hipSuccess) {                                                           \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));       \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef double dbl2u __attribute__((ext_vector_type(2), aligned(8)));
+
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+  const int64_t q = nb >> 3, r = nb & 7, g = b & 7, i = b >> 3;
+  return (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + i;
+}
+
+__global__ __launch_bounds__(256) void k_copy(const double* __restrict__ x, double* __restrict__ y,
+                                              int64_t N) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (2 * p + 1 < N) {
+    *reinterpret_cast<dbl2*>(y + 2 * p) = *reinterpret_cast<const dbl2*>(x + 2 * p);
+  }
+}
+
+// lane per row pair, every neighbour load 16 B (interior pairs; boundary pairs read clamped)
+template <int MASK, int ORDER>
+__global__ __launch_bounds__(256) void k_pair(const double* __restrict__ x, double* __restrict__ y,
+                                              int n, int64_t N) {
+  const int64_t lb = ORDER == 0 ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int64_t p = lb * 256 + threadIdx.x;
+  const int64_t r = 2 * p;
+  if (r + 1 >= N) return;
+  const int64_t n2 = (int64_t)n * n;
+  const double* xr = x + r;
+  dbl2 c = *reinterpret_cast<const dbl2u*>(xr);
+  double s0 = 6.0 * c.x, s1 = 6.0 * c.y;
+  auto nb = [&](int64_t off) {
+    if (r + off >= 0 && r + off + 1 < N) {
+      const dbl2 t = *reinterpret_cast<const dbl2u*>(xr + off);
+      s0 -= t.x;
+      s1 -= t.y;
+    }
+  };
+  if (MASK & 1) {
+    nb(-1);
+    nb(1);
+  }
+  if (MASK & 2) {
+    nb(-n);
+    nb(n);
+  }
+  if (MASK & 4) {
+    nb(-n2);
+    nb(n2);
+  }
+  dbl2 o;
+  o.x = s0;
+  o.y = s1;
+  *reinterpret_cast<dbl2*>(y + r) = o;
+}
+
+// lane per row, 8-byte loads
+template <int MASK, int ORDER>
+__global__ __launch_bounds__(256) void k_row(const double* __restrict__ x, double* __restrict__ y,
+                                             int n, int64_t N) {
+  const int64_t lb = ORDER == 0 ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int64_t r = lb * 256 + threadIdx.x;
+  if (r >= N) return;
+  const int64_t n2 = (int64_t)n * n;
+  double s = 6.0 * x[r];
+  auto nb = [&](int64_t off) {
+    if (r + off >= 0 && r + off < N) s -= x[r + off];
+  };
+  if (MASK & 1) {
+    nb(-1);
+    nb(1);
+  }
+  if (MASK & 2) {
+    nb(-n);
+    nb(n);
+  }
+  if (MASK & 4) {
+    nb(-n2);
+    nb(n2);
+  }
+  y[r] = s;
+}
+
+template <class F>
+static float timeit(F f, int reps) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  f();
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) f();
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  return ms * 1000.f / reps;
+}
+
+template <int MASK, int ORDER>
+static void run_pair(const double* x, double* y, int n, int64_t N, int reps) {
+  const unsigned nb = (unsigned)((N / 2 + 255) / 256);
+  float us = timeit([&] { hipLaunchKernelGGL((k_pair<MASK, ORDER>), dim3(nb), dim3(256), 0, 0, x, y, n, N); }, reps);
+  printf("pair mask=%d order=%d: %7.1f us  %6.0f GB/s (x+y)\n", MASK, ORDER, us, 16.0 * N / us / 1e3);
+}
+
+template <int MASK, int ORDER>
+static void run_row(const double* x, double* y, int n, int64_t N, int reps) {
+  const unsigned nb = (unsigned)((N + 255) / 256);
+  float us = timeit([&] { hipLaunchKernelGGL((k_row<MASK, ORDER>), dim3(nb), dim3(256), 0, 0, x, y, n, N); }, reps);
+  printf("row  mask=%d order=%d: %7.1f us  %6.0f GB/s (x+y)\n", MASK, ORDER, us, 16.0 * N / us / 1e3);
+}
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 216;
+  const int reps = argc > 2 ? atoi(argv[2]) : 50;
+  const int64_t N = (int64_t)n * n * n;
+  double *x, *y;
+  CK(hipMalloc(&x, sizeof(double) * N));
+  CK(hipMalloc(&y, sizeof(double) * N));
+  std::vector<double> h(N);
+  for (int64_t i = 0; i < N; ++i) h[i] = (double)((i * 2654435761u) % 1000) / 1000.0;
+  CK(hipMemcpy(x, h.data(), sizeof(double) * N, hipMemcpyHostToDevice));
+  {
+    const unsigned nb = (unsigned)((N / 2 + 255) / 256);
+    float us = timeit([&] { hipLaunchKernelGGL(k_copy, dim3(nb), dim3(256), 0, 0, x, y, N); }, reps);
+    printf("copy 16B/lane     : %7.1f us  %6.0f GB/s\n", us, 16.0 * N / us / 1e3);
+  }
+  run_pair<0, 0>(x, y, n, N, reps);
+  run_pair<1, 0>(x, y, n, N, reps);
+  run_pair<2, 0>(x, y, n, N, reps);
+  run_pair<4, 0>(x, y, n, N, reps);
+  run_pair<7, 0>(x, y, n, N, reps);
+  run_pair<7, 1>(x, y, n, N, reps);
+  run_row<0, 0>(x, y, n, N, reps);
+  run_row<7, 0>(x, y, n, N, reps);
+  run_row<7, 1>(x, y, n, N, reps);
+  return 0;
+}
