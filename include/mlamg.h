@@ -101,6 +101,14 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
 #define MLAMG_FMT_ROWPAT 6
 int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream);
 int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored_entries);
+/* Attach the level's Jacobi weights dinv_w (device, n_rows) to a ROWPAT operator: checked on the
+ * device to be constant over each row-pair pattern (true for the diagonal of a constant-
+ * coefficient stencil), after which every epilogue of A whose dinv pointer IS dinv_w takes the
+ * values from the pattern table instead of reading the vector (same bits). The caller keeps
+ * dinv_w alive and unchanged while attached; NULL detaches; any set_format detaches.
+ * EUNSUPPORTED (nothing attached) if A is not ROWPAT or dinv_w is not pattern-constant.
+ * Replaces no reference call: an optimisation of the weighted-Jacobi sweep (MLAMG.py:143-146). */
+int mlamg_csr_attach_dinv(mlamg_csr* A, const double* dinv_w, void* stream);
 /* algorithmic HBM bytes of one y = A@x with the active format: matrix stream as stored (CSR:
  * 12*nnz + 4*(n+1); SELL: 12 B per padded element + slice pointers; SELL_DICT: 2 B per code +
  * tables; SORTED: CSR + block tables; ROWPAT: 1 B per row + tables) + 8*n_cols (x once) + 8*n_rows (y once) */

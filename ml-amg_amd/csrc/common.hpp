@@ -122,6 +122,11 @@ struct mlamg_csr {
                                  // patterns padded to multiples of 8 entries
   double* rp_val = nullptr;      // per entry (row 2i's value, row 2i+1's value)
   int32_t rp_n_pat = 0, rp_n_ent = 0;
+  std::vector<int32_t> rp_rep;         // representative pair of each pattern (host)
+  // attached Jacobi weights (mlamg_csr_attach_dinv): an epilogue whose dinv pointer equals
+  // rp_dinv_att reads the per-pattern values rp_dinv[2p], rp_dinv[2p+1] instead of memory
+  const double* rp_dinv_att = nullptr;
+  double* rp_dinv = nullptr;
   // number of per-block partial sums a NORM launch writes with the active format
   int32_t n_part = 0;
 };

@@ -96,6 +96,7 @@ void csr_free(mlamg_csr* A) {
   if (A->rp_ptr) (void)hipFree(A->rp_ptr);
   if (A->rp_off) (void)hipFree(A->rp_off);
   if (A->rp_val) (void)hipFree(A->rp_val);
+  if (A->rp_dinv) (void)hipFree(A->rp_dinv);
   delete A;
 }
 

@@ -415,21 +415,23 @@ __device__ __forceinline__ void st2(double* p, int i, bool both, double v0, doub
 }
 
 // epi_load for rows r, r+1
+// (no_dinv: the dinv operand comes from the caller's pattern table instead of memory)
 template <int OP>
-__device__ __forceinline__ void epi_load2(int r, bool both, const Epi& e, EpiIn& u, EpiIn& w) {
+__device__ __forceinline__ void epi_load2(int r, bool both, const Epi& e, EpiIn& u, EpiIn& w,
+                                          bool no_dinv) {
   if constexpr (OP == EPI_AXPBY) {
     if (e.beta != 0.0) ld2(e.y, r, both, u.a, w.a);
-    if (e.copy_to) ld2(e.dinv, r, both, u.c, w.c);
+    if (e.copy_to && !no_dinv) ld2(e.dinv, r, both, u.c, w.c);
   } else if constexpr (OP == EPI_RESID) {
     ld2(e.b, r, both, u.a, w.a);
     if (e.copy_to) {
       ld2(e.copy_from, r, both, u.b, w.b);
-      if (e.dinv) ld2(e.dinv, r, both, u.c, w.c);
+      if (e.dinv && !no_dinv) ld2(e.dinv, r, both, u.c, w.c);
     }
   } else if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) {
     ld2(e.b, r, both, u.a, w.a);
     ld2(e.xin, r, both, u.b, w.b);
-    ld2(e.dinv, r, both, u.c, w.c);
+    if (!no_dinv) ld2(e.dinv, r, both, u.c, w.c);
   } else {  // EPI_ADD
     ld2(e.y, r, both, u.a, w.a);
   }
@@ -537,14 +539,21 @@ __global__ __launch_bounds__(kThreads) void k_rowpair(const uint8_t* __restrict_
                                                       const int4* __restrict__ pat_of,
                                                       const dbl2* __restrict__ pat_vv,
                                                       int n_ent, int64_t n_rows, int64_t n_cols,
-                                                      const double* __restrict__ x, Epi ep) {
-  // LDS: vv[n_ent] (16 B) | of[n_ent] (16 B) | starts[257]
+                                                      const double* __restrict__ dinv_att,
+                                                      const dbl2* __restrict__ pat_dinv,
+                                                      int n_pat, const double* __restrict__ x,
+                                                      Epi ep) {
+  // LDS: vv[n_ent] (16 B) | of[n_ent] (16 B) | dinv[n_pat] (16 B) | starts[257]
   extern __shared__ dbl2 rp_lds[];
   __shared__ double red[kThreads / 64];
   if (ep.done && *ep.done) return;
   dbl2* vv = rp_lds;
   int4* of = reinterpret_cast<int4*>(rp_lds + n_ent);
-  int32_t* pst = reinterpret_cast<int32_t*>(of + n_ent);
+  dbl2* dt = reinterpret_cast<dbl2*>(of + n_ent);
+  int32_t* pst = reinterpret_cast<int32_t*>(dt + n_pat);
+  // the epilogue's dinv is the vector attached to this operator (mlamg_csr_attach_dinv): its
+  // entries are per-pattern constants, verified at attach time, read from LDS
+  const bool tab_dinv = ep.dinv != nullptr && ep.dinv == dinv_att;
   const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
   const int64_t pr0 = lb * CH * kThreads + threadIdx.x;  // this lane's pair in chunk 0
   int p = 2 * pr0 < n_rows ? (int)pid[pr0] : 0;
@@ -553,6 +562,8 @@ __global__ __launch_bounds__(kThreads) void k_rowpair(const uint8_t* __restrict_
     of[i] = pat_of[i];
   }
   for (int i = threadIdx.x; i < 257; i += kThreads) pst[i] = pat_ptr[i];
+  if (tab_dinv)
+    for (int i = threadIdx.x; i < n_pat; i += kThreads) dt[i] = pat_dinv[i];
   double sq = 0.0;
   __syncthreads();
 #pragma unroll 1
@@ -564,7 +575,12 @@ __global__ __launch_bounds__(kThreads) void k_rowpair(const uint8_t* __restrict_
     const int p_next =
         (c + 1 < CH && 2 * (pr + kThreads) < n_rows) ? (int)pid[pr + kThreads] : 0;
     EpiIn u, w;
-    if (ok0) epi_load2<OP>(r, both, ep, u, w);
+    if (ok0) epi_load2<OP>(r, both, ep, u, w, tab_dinv);
+    if (tab_dinv) {
+      const dbl2 d = dt[p];
+      u.c = d.x;
+      w.c = d.y;
+    }
     const int a = pst[p];
     const int len = ok0 ? pst[p + 1] - a : 0;
     double s0, s1;
@@ -846,11 +862,12 @@ template <int OP, bool NORM, int CH>
 static int launch_rowpair_ch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   const int64_t n_pairs = (A->n_rows + 1) / 2;
   const unsigned nb = (unsigned)((n_pairs + CH * kThreads - 1) / (CH * kThreads));
-  const size_t lds = (size_t)A->rp_n_ent * 32 + 257 * 4;
+  const size_t lds = (size_t)A->rp_n_ent * 32 + (size_t)A->rp_n_pat * 16 + 257 * 4;
   hipLaunchKernelGGL((k_rowpair<OP, NORM, CH>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid,
                      A->rp_ptr, reinterpret_cast<const int4*>(A->rp_off),
                      reinterpret_cast<const dbl2*>(A->rp_val), A->rp_n_ent, A->n_rows,
-                     A->n_cols, x, ep);
+                     A->n_cols, A->rp_dinv_att, reinterpret_cast<const dbl2*>(A->rp_dinv),
+                     A->rp_n_pat, x, ep);
   MLAMG_HIP(hipGetLastError());
   return MLAMG_OK;
 }
@@ -1568,8 +1585,12 @@ __global__ void k_rp_assign(const int32_t* __restrict__ ip, const int32_t* __res
 }
 
 static void drop_rowpat(mlamg_csr* A) {
-  for (void* p : {(void*)A->rp_pid, (void*)A->rp_ptr, (void*)A->rp_off, (void*)A->rp_val})
+  for (void* p : {(void*)A->rp_pid, (void*)A->rp_ptr, (void*)A->rp_off, (void*)A->rp_val,
+                  (void*)A->rp_dinv})
     if (p) (void)hipFree(p);
+  A->rp_dinv = nullptr;
+  A->rp_dinv_att = nullptr;
+  A->rp_rep.clear();
   A->rp_pid = nullptr;
   A->rp_ptr = nullptr;
   A->rp_off = nullptr;
@@ -1630,7 +1651,7 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
     fail(MLAMG_EHIP, "pattern scan");
   if (rc == MLAMG_OK && (hc[2] != 0 || hc[0] > 255))
     fail(MLAMG_EUNSUPPORTED, "more than 255 distinct row-pair patterns");
-  std::vector<int32_t> hptr(257, 0), hoff;
+  std::vector<int32_t> hptr(257, 0), hoff, reps;
   std::vector<double> hv0, hv1;
   std::vector<uint8_t> hfl;
   int n_pat = 0;
@@ -1642,6 +1663,7 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
     std::sort(pats.begin(), pats.end());
     n_pat = (int)pats.size();
     std::vector<int32_t> hslot(kDictSlots, 0);
+    for (auto& pk : pats) reps.push_back(pk.first);
     auto fetch_row = [&](int64_t row, std::vector<int32_t>& off, std::vector<double>& val) {
       off.clear();
       val.clear();
@@ -1750,7 +1772,20 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
   A->rp_val = pval;
   A->rp_n_pat = n_pat;
   A->rp_n_ent = (int32_t)hoff.size();
+  A->rp_rep = std::move(reps);
   return MLAMG_OK;
+}
+
+// per-pattern (dinv[2i], dinv[2i+1]) must equal the representative pair's, for every pair
+__global__ void k_rp_dinv_check(const uint8_t* __restrict__ pid, const double* __restrict__ dinv,
+                                const double* __restrict__ tab, int64_t n, int32_t* bad) {
+  const int64_t pr = blockIdx.x * 256ll + threadIdx.x;
+  if (2 * pr >= n) return;
+  const int p = pid[pr];
+  bool ok = __double_as_longlong(dinv[2 * pr]) == __double_as_longlong(tab[2 * p]);
+  if (2 * pr + 1 < n)
+    ok = ok && __double_as_longlong(dinv[2 * pr + 1]) == __double_as_longlong(tab[2 * p + 1]);
+  if (!ok) atomicAdd(bad, 1);
 }
 
 static int32_t rowpat_parts(const mlamg_csr* A) {
@@ -2003,6 +2038,60 @@ int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
     b += 12.0 * A->nnz + 4.0 * (n + 1);
   }
   *bytes = b;
+  return MLAMG_OK;
+}
+
+int mlamg_csr_attach_dinv(mlamg_csr* A, const double* dinv_w, void* stream) {
+  MLAMG_REQUIRE(A, "NULL argument");
+  hipStream_t s = S(stream);
+  bump_format_epoch();
+  if (A->rp_dinv) (void)hipFree(A->rp_dinv);
+  A->rp_dinv = nullptr;
+  A->rp_dinv_att = nullptr;
+  if (!dinv_w) return MLAMG_OK;  // detach
+  if (!A->rp_pid) {
+    set_error("attach_dinv: the operator is not in rowpat format");
+    return MLAMG_EUNSUPPORTED;
+  }
+  const int np = A->rp_n_pat;
+  const int64_t n = A->n_rows;
+  std::vector<double> tab(2 * std::max(np, 1), 0.0);
+  for (int p = 0; p < np; ++p) {
+    const int64_t r0 = 2 * (int64_t)A->rp_rep[p];
+    MLAMG_HIP(hipMemcpy(&tab[2 * p], dinv_w + r0, sizeof(double) * (r0 + 1 < n ? 2 : 1),
+                        hipMemcpyDeviceToHost));
+  }
+  double* d = nullptr;
+  int32_t* bad = nullptr;
+  MLAMG_HIP(hipMalloc(&d, sizeof(double) * tab.size()));
+  if (hipMalloc(&bad, sizeof(int32_t)) != hipSuccess) {
+    (void)hipFree(d);
+    set_error("attach_dinv: out of device memory");
+    return MLAMG_ENOMEM;
+  }
+  int32_t hb = 0;
+  hipError_t e = hipMemcpyAsync(d, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, sizeof(int32_t), s);
+  const int64_t n_pairs = (n + 1) / 2;
+  if (e == hipSuccess && n_pairs) {
+    hipLaunchKernelGGL(k_rp_dinv_check, dim3((unsigned)((n_pairs + 255) / 256)), dim3(256), 0, s,
+                       A->rp_pid, dinv_w, d, n, bad);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(&hb, bad, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(bad);
+  if (e != hipSuccess || hb != 0) {
+    (void)hipFree(d);
+    if (e != hipSuccess) {
+      set_error(std::string("attach_dinv: ") + hipGetErrorString(e));
+      return MLAMG_EHIP;
+    }
+    set_error("attach_dinv: dinv is not constant over the operator's row-pair patterns");
+    return MLAMG_EUNSUPPORTED;
+  }
+  A->rp_dinv = d;
+  A->rp_dinv_att = dinv_w;
   return MLAMG_OK;
 }
 

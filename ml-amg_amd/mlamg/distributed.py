@@ -144,6 +144,8 @@ class DistributedHierarchy:
             P_loc = like(Lg.P, DeviceCSR.from_scipy(p["P_loc"], check=False))
             R_own = like(Lg.R, DeviceCSR.from_scipy(p["R_own"], check=False))
             dinv = Lg.dinv[p["lo"]:p["hi"]].clone()
+            if A_loc.get_format()[0] == "rowpat":
+                A_loc.attach_dinv(dinv)
             hx = Halo(comm, p["halo_x"])
             hr = Halo(comm, p["halo_r"])
             hp = Halo(comm, p["halo_p"]) if p["halo_p"] is not None else None

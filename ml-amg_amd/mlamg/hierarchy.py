@@ -161,6 +161,13 @@ class Hierarchy:
                 M.set_format(fmt, int(arg))
                 row[name] = {"chosen": best, "us": {k: round(v, 2) for k, v in times.items()}}
             self.tuning.append(row)
+        self.attach_dinvs()
+
+    def attach_dinvs(self):
+        """Let every rowpat level operator take its Jacobi weights from its pattern table."""
+        for L in self.levels:
+            if L.A.get_format()[0] == "rowpat":
+                L.A.attach_dinv(L.dinv)
 
     def formats(self):
         return [{"A": L.A.get_format(), "P": L.P.get_format(), "R": L.R.get_format()}
@@ -175,6 +182,7 @@ class Hierarchy:
             for name in ("A", "P", "R"):
                 fmt, arg = f[name][0], f[name][1]
                 getattr(L, name).set_format(fmt, int(arg))
+        self.attach_dinvs()
 
     @classmethod
     def build(cls, A, *, alpha=0.1, strength_mode="invabs", aggregation="bellman_ford",

@@ -49,7 +49,7 @@ def canonical_rows(A):
 class DeviceCSR:
     """An int32/fp64 CSR matrix resident on the GPU (owns a `mlamg_csr*`)."""
 
-    __slots__ = ("handle", "shape", "nnz", "_keep", "__weakref__")
+    __slots__ = ("handle", "shape", "nnz", "_keep", "_dinv_ref", "__weakref__")
 
     def __init__(self, handle, keep=()):
         self.handle = handle
@@ -58,6 +58,7 @@ class DeviceCSR:
         self.shape = (int(nr.value), int(nc.value))
         self.nnz = int(nz.value)
         self._keep = keep
+        self._dinv_ref = None
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -155,6 +156,21 @@ class DeviceCSR:
         b = ctypes.c_double()
         call("mlamg_csr_format_bytes", self.handle, ctypes.byref(b))
         return float(b.value)
+
+    def attach_dinv(self, dinv):
+        """Attach Jacobi weights to a 'rowpat' operator (include/mlamg.h mlamg_csr_attach_dinv):
+        epilogues given this very tensor read its per-pattern values from the pattern table.
+        Returns False (nothing attached) when A is not rowpat or dinv is not pattern-constant."""
+        try:
+            call("mlamg_csr_attach_dinv", self.handle, ptr(dinv) if dinv is not None else None,
+                 stream_ptr())
+        except _lib.MlamgError as e:
+            if e.code != _lib.MLAMG_EUNSUPPORTED:
+                raise
+            self._dinv_ref = None
+            return False
+        self._dinv_ref = dinv  # keeps the attached vector alive
+        return dinv is not None
 
     def diag_inv(self, omega=1.0):
         d = torch.empty(self.shape[0], dtype=torch.float64, device=_device())

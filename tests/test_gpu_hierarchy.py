@@ -411,3 +411,26 @@ def test_rowpat_format(ml, torch_cuda):
     h2 = H2.cycle(bd, x2, 5)
     assert torch.equal(x1, x2)
     assert np.allclose(h1, h2, rtol=1e-14, atol=0)
+    # attached Jacobi weights (per-pattern constants from the table): the same bits, eager and
+    # through the re-captured graph
+    A2 = H2.levels[0].A
+    assert A2.attach_dinv(H2.levels[0].dinv)
+    for use_graph in (False, True):
+        x1, x2 = dev(torch, x), dev(torch, x)
+        h1 = H.cycle(bd, x1, 5, use_graph=use_graph)
+        h2 = H2.cycle(bd, x2, 5, use_graph=use_graph)
+        assert torch.equal(x1, x2)
+        assert np.allclose(h1, h2, rtol=1e-14, atol=0)
+    # weights that are not constant over the patterns are refused (nothing attached)
+    d2 = H2.levels[0].dinv.clone()
+    d2[5] *= 2.0
+    assert not A2.attach_dinv(d2)
+    y1 = torch.empty(n, dtype=torch.float64, device="cuda")
+    y2 = torch.empty(n, dtype=torch.float64, device="cuda")
+    t1 = torch.empty_like(y1)
+    xs = dev(torch, x)
+    call("mlamg_jacobi", A2.handle, ptr(d2), ptr(bd), ptr(xs), ptr(t1), 1, stream_ptr())
+    Ad = ml.sparse.DeviceCSR.from_scipy(A)
+    xs2 = dev(torch, x)
+    call("mlamg_jacobi", Ad.handle, ptr(d2), ptr(bd), ptr(xs2), ptr(t1), 1, stream_ptr())
+    assert torch.equal(xs, xs2)
