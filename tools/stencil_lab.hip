@@ -102,6 +102,45 @@ __global__ __launch_bounds__(256) void k_row(const double* __restrict__ x, doubl
   y[r] = s;
 }
 
+// k_pair<7,0> plus the row-pair kernel's indirections: V=1 a pattern-id byte load feeding the
+// offsets (pid is all zero here), V=2 also the offsets from an LDS table indexed by the id
+template <int V>
+__global__ __launch_bounds__(256) void k_pair_ind(const double* __restrict__ x,
+                                                  double* __restrict__ y,
+                                                  const uint8_t* __restrict__ pid, int n,
+                                                  int64_t N) {
+  __shared__ int offt[8];
+  const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t p = lb * 256 + threadIdx.x;
+  const int64_t r = 2 * p;
+  const int64_t n2 = (int64_t)n * n;
+  if (V == 2) {
+    if (threadIdx.x < 8) {
+      const int o[8] = {(int)-n2, -n, -1, 0, 1, n, (int)n2, 0};
+      offt[threadIdx.x] = o[threadIdx.x];
+    }
+    __syncthreads();
+  }
+  if (r + 1 >= N) return;
+  const int id = pid[p];
+  const double* xr = x + r + id;
+  double s0 = 0.0, s1 = 0.0;
+  const int o[7] = {(int)-n2, -n, -1, 0, 1, n, (int)n2};
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    const int off = V == 2 ? offt[id * 8 + q] : o[q];
+    if (r + off >= 0 && r + off + 1 < N) {
+      const dbl2 t = *reinterpret_cast<const dbl2u*>(xr + off);
+      s0 += (q == 3 ? 6.0 : -1.0) * t.x;
+      s1 += (q == 3 ? 6.0 : -1.0) * t.y;
+    }
+  }
+  dbl2 out;
+  out.x = s0;
+  out.y = s1;
+  *reinterpret_cast<dbl2*>(y + r) = out;
+}
+
 template <class F>
 static float timeit(F f, int reps) {
   hipEvent_t a, b;
@@ -153,6 +192,15 @@ int main(int argc, char** argv) {
   run_pair<4, 0>(x, y, n, N, reps);
   run_pair<7, 0>(x, y, n, N, reps);
   run_pair<7, 1>(x, y, n, N, reps);
+  {
+    uint8_t* pid;
+    CK(hipMalloc(&pid, N / 2 + 1));
+    CK(hipMemset(pid, 0, N / 2 + 1));
+    const unsigned nb = (unsigned)((N / 2 + 255) / 256);
+    float us1 = timeit([&] { hipLaunchKernelGGL((k_pair_ind<1>), dim3(nb), dim3(256), 0, 0, x, y, pid, n, N); }, reps);
+    float us2 = timeit([&] { hipLaunchKernelGGL((k_pair_ind<2>), dim3(nb), dim3(256), 0, 0, x, y, pid, n, N); }, reps);
+    printf("pair + pid load      : %7.1f us\npair + pid + LDS offs: %7.1f us\n", us1, us2);
+  }
   run_row<0, 0>(x, y, n, N, reps);
   run_row<7, 0>(x, y, n, N, reps);
   run_row<7, 1>(x, y, n, N, reps);
