@@ -532,9 +532,15 @@ __device__ __forceinline__ void rowpair_sums(const double* __restrict__ x, int64
 }
 
 // CH chunks of 256 pairs per workgroup (tables staged once; the next chunk's pattern ids are
-// fetched while the current chunk gathers)
+// fetched while the current chunk gathers). MLAMG_RP_WAVES: minimum waves per SIMD the register
+// allocation must leave room for (0 = compiler's choice; build-time knob for A/B runs)
+#ifndef MLAMG_RP_WAVES
+#define MLAMG_RP_WAVES 0
+#endif
 template <int OP, bool NORM, int CH>
-__global__ __launch_bounds__(kThreads) void k_rowpair(const uint8_t* __restrict__ pid,
+__global__ __launch_bounds__(kThreads)
+__attribute__((amdgpu_waves_per_eu(MLAMG_RP_WAVES > 0 ? MLAMG_RP_WAVES : 1, 8)))
+void k_rowpair(const uint8_t* __restrict__ pid,
                                                       const int32_t* __restrict__ pat_ptr,
                                                       const int4* __restrict__ pat_of,
                                                       const dbl2* __restrict__ pat_vv,
