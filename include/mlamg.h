@@ -221,6 +221,21 @@ int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream);
 int mlamg_dense_destroy(mlamg_dense* D);
 int mlamg_dense_solve(const mlamg_dense* D, const double* b, double* x, void* stream);
 
+/* Least squares by LSQR: x = argmin ||A x - b||_2 from x0 = 0, scipy.sparse.linalg.lsqr
+ * semantics with damp = 0 (its defaults: atol = btol = 1e-6, conlim = 1e8, iter_lim <= 0 means
+ * 2 * n_cols). Replaces spla.lsqr(P.T@A@P, P.T@(b - A@x))[0], the singular (Neumann) coarse solve
+ * of ns/lib/multigrid.py:178-179. AT is A's explicit transpose (mlamg_transpose), the operator of
+ * scipy's rmatvec. b (n_rows) and x (n_cols) are device vectors; the iteration runs on the device
+ * (scalar recurrences in one thread, stop test on the device); synchronizes `stream`. istop_out /
+ * itn_out (nullable): scipy's istop code (0..7) and iteration count. */
+int mlamg_lsqr(const mlamg_csr* A, const mlamg_csr* AT, const double* b, double* x, double atol,
+               double btol, double conlim, int iter_lim, int* istop_out, int* itn_out,
+               void* stream);
+
+/* x -= mean(x) (device vector; fixed-order sum / n): the nullspace normalisation of the singular
+ * cycle, ns/lib/multigrid.py:186-187. */
+int mlamg_remove_mean(double* x, int64_t n, void* stream);
+
 /* ---------------------------------------------------------------- V-cycle executor
  * Multilevel weighted-Jacobi V(nu1,nu2) cycle: the two-level cycle of MLAMG.py:189-195 applied
  * recursively (the multilevel solver the PyAMG PC runs, PyAMG.py:94,119), coarsest level solved

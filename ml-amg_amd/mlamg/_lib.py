@@ -64,6 +64,9 @@ SIGNATURES = {
     "mlamg_csr_get_format": (c_int, [c_vp, P_int, P_int, P_i64]),
     "mlamg_csr_format_bytes": (c_int, [c_vp, P_dbl]),
     "mlamg_csr_attach_dinv": (c_int, [c_vp, c_vp, c_vp]),
+    "mlamg_lsqr": (c_int, [c_vp, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_dbl, c_int, P_int, P_int,
+                           c_vp]),
+    "mlamg_remove_mean": (c_int, [c_vp, c_i64, c_vp]),
     "mlamg_spmv": (c_int, [c_vp, c_vp, c_vp, c_dbl, c_dbl, c_vp]),
     "mlamg_residual": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mlamg_jacobi": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),

@@ -186,6 +186,76 @@ class TwoLevel:
             self.dense = None
 
 
+def lsqr(A, b, atol=1e-6, btol=1e-6, conlim=1e8, iter_lim=None, AT=None):
+    """scipy.sparse.linalg.lsqr(A, b)[:3] (damp = 0, x0 = 0) on the device: (x, istop, itn).
+
+    A and b may be scipy/numpy or device objects; AT (optional DeviceCSR) is A's transpose, the
+    operator of scipy's rmatvec. x comes back as a device tensor when b is one, else numpy."""
+    A_dev = as_device(A)
+    AT = A_dev.transpose() if AT is None else AT
+    bd = to_device_vec(b)
+    xd = torch.empty(A_dev.shape[1], dtype=torch.float64, device=bd.device)
+    istop, itn = ctypes.c_int(), ctypes.c_int()
+    call("mlamg_lsqr", A_dev.handle, AT.handle, ptr(bd), ptr(xd), float(atol), float(btol),
+         float(conlim), int(iter_lim or 0), ctypes.byref(istop), ctypes.byref(itn), stream_ptr())
+    x = xd if isinstance(b, torch.Tensor) else xd.cpu().numpy()
+    return x, int(istop.value), int(itn.value)
+
+
+def _amg_2_v_singular(A, P, b, x, nu_pre, nu_post, jacobi_weight, res_tol, tol, max_iter,
+                      smoother):
+    """The singular branch of ns/lib/multigrid.py:111-210 (Neumann problems, constant
+    nullspace): coarse correction x += P @ lsqr(P.T@A@P, P.T@(b - A@x))[0] (:178-179), mean
+    removal after post-smoothing (:186-187), no factorization. Device-resident; one host read of
+    the norm per cycle for the tolerance test."""
+    A_dev, P_dev = as_device(A), as_device(P)
+    R = P_dev.transpose()
+    A_H = galerkin(R, A_dev, P_dev)
+    A_HT = A_H.transpose()
+    s = stream_ptr()
+    xd = to_device_vec(x).clone()  # x = x.copy()  (:171)
+    bd = to_device_vec(b)
+    n, nc = A_dev.shape[0], P_dev.shape[1]
+    r = torch.empty(n, dtype=torch.float64, device=xd.device)
+    t = torch.empty_like(r)
+    rc = torch.empty(nc, dtype=torch.float64, device=xd.device)
+    ec = torch.empty_like(rc)
+    nrm = torch.zeros(1, dtype=torch.float64, device=xd.device)
+    istop, itn = ctypes.c_int(), ctypes.c_int()
+    if smoother == "gauss_seidel":
+        gs = GaussSeidel(A_dev)
+
+        def smooth(nu):
+            if nu > 0:
+                gs.sweep(xd, bd, nu)
+    else:
+        dw = A_dev.diag_inv(jacobi_weight)
+
+        def smooth(nu):
+            if nu > 0:
+                call("mlamg_jacobi", A_dev.handle, ptr(dw), ptr(bd), ptr(xd), ptr(t), int(nu), s)
+    err = np.zeros(max_iter)
+    for i in range(max_iter):
+        smooth(nu_pre)
+        call("mlamg_residual", A_dev.handle, ptr(bd), ptr(xd), ptr(r), None, s)
+        call("mlamg_restrict", R.handle, ptr(r), ptr(rc), s)
+        call("mlamg_lsqr", A_H.handle, A_HT.handle, ptr(rc), ptr(ec), 1e-6, 1e-6, 1e8, 0,
+             ctypes.byref(istop), ctypes.byref(itn), s)
+        call("mlamg_prolong_add", P_dev.handle, ptr(ec), ptr(xd), s)
+        smooth(nu_post)
+        call("mlamg_remove_mean", ptr(xd), int(n), s)
+        if res_tol is not None:
+            call("mlamg_residual", A_dev.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), s)
+        else:
+            call("mlamg_norm2", ptr(xd), int(n), ptr(nrm), s)
+        e = float(nrm.item())
+        err[i] = e
+        if e <= tol:
+            err = err[:i + 1]
+            break
+    return xd.cpu().numpy(), conv_factor(err), err, len(err)
+
+
 def amg_2_v(A, P, b, x,
             pre_smoothing_steps=1,
             post_smoothing_steps=1,
@@ -204,11 +274,11 @@ def amg_2_v(A, P, b, x,
     if res_tol is None and error_tol is None:
         raise RuntimeError('One of res_tol or error_tol must be set!')
     tol = res_tol if res_tol is not None else error_tol
-    if singular:
-        raise NotImplementedError("singular=True (lsqr coarse solve + mean removal, "
-                                  "multigrid.py:178-187) is not implemented on the GPU path")
     if smoother not in ("gauss_seidel", "jacobi"):
         raise ValueError(f"unknown smoother {smoother!r}")
+    if singular:
+        return _amg_2_v_singular(A, P, b, x, pre_smoothing_steps, post_smoothing_steps,
+                                 jacobi_weight, res_tol, tol, max_iter, smoother)
     err = np.zeros(max_iter)
     from .hierarchy import Hierarchy
     try:

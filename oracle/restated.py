@@ -155,18 +155,23 @@ def conv_factor(err):
 
 
 def amg_2_v(A, P, b, x, pre_smoothing_steps=1, post_smoothing_steps=1, jacobi_weight=0.666,
-            res_tol=None, error_tol=None, max_iter=500, smoother="gauss_seidel"):
-    """ns/lib/multigrid.py:111-210 (non-singular branch); smoother='jacobi' swaps in the
-    MLAMG.py:143-146 Jacobi form with weight jacobi_weight."""
+            res_tol=None, error_tol=None, max_iter=500, singular=False, smoother="gauss_seidel"):
+    """ns/lib/multigrid.py:111-210; smoother='jacobi' swaps in the MLAMG.py:143-146 Jacobi form
+    with weight jacobi_weight. singular=True: lsqr coarse solve (scipy defaults, :178-179) and
+    mean removal after post-smoothing (:186-187), no factorization."""
     if res_tol is None and error_tol is None:
         raise RuntimeError('One of res_tol or error_tol must be set!')
     tol = res_tol if res_tol is not None else error_tol
     err = np.zeros(max_iter)
     A_H = P.T @ A @ P
-    try:
-        A_H_LU = spla.factorized(A_H)
-    except Exception:
-        return x, np.float64(1.), err, 0
+    if singular:
+        def coarse(r_H):
+            return spla.lsqr(P.T @ A @ P, r_H)[0]
+    else:
+        try:
+            coarse = spla.factorized(A_H)
+        except Exception:
+            return x, np.float64(1.), err, 0
     x = x.copy()
     if smoother == "jacobi":
         Dw = mlamg_dinv(A, jacobi_weight)
@@ -178,8 +183,10 @@ def amg_2_v(A, P, b, x, pre_smoothing_steps=1, post_smoothing_steps=1, jacobi_we
             gauss_seidel(A, x, b, iterations=nu)
     for i in range(max_iter):
         smooth(pre_smoothing_steps)
-        x += P @ A_H_LU(P.T @ (b - A @ x))
+        x += P @ coarse(P.T @ (b - A @ x))
         smooth(post_smoothing_steps)
+        if singular:
+            x -= np.mean(x)
         if res_tol is not None:
             e = la.norm(b - A @ x, 2)
         else:

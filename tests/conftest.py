@@ -10,6 +10,7 @@ for p in (ROOT, os.path.join(ROOT, "ml-amg_amd")):
         sys.path.insert(0, p)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "reference_vectors.npz")
+GOLDEN_SINGULAR = os.path.join(ROOT, "tests", "golden", "reference_singular.npz")
 
 
 def pytest_configure(config):
@@ -20,6 +21,11 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden():
     return dict(np.load(GOLDEN, allow_pickle=False))
+
+
+@pytest.fixture(scope="session")
+def golden_singular():
+    return dict(np.load(GOLDEN_SINGULAR, allow_pickle=False))
 
 
 def golden_csr(g, key):

@@ -135,3 +135,17 @@ def test_gridio_matches_golden(golden):
     assert np.array_equal(A.data, golden["lap3d_data"])
     assert np.array_equal(A.indices, golden["lap3d_indices"])
     assert A.shape == (1331, 1331) and A.nnz == 17191
+
+
+@pytest.mark.parametrize("key", ("n1d", "n2d"))
+def test_amg_2_v_singular_driver(golden_singular, oracle, key):
+    """multigrid.py:111-210 with singular=True (lsqr coarse solve + mean removal) on Neumann
+    problems: the oracle reproduces the reference's history, conv factor and iterate bitwise."""
+    g = golden_singular
+    A, P = golden_csr(g, f"{key}_A"), golden_csr(g, f"{key}_P")
+    kw = {"res_tol": 1e-8} if key == "n1d" else {"error_tol": 1e-9}
+    x, conv, err, it = oracle.amg_2_v(A, P, g[f"{key}_b"], g[f"{key}_x0"], singular=True,
+                                      max_iter=60, **kw)
+    assert np.array_equal(err, g[f"{key}_err"])
+    assert conv == g[f"{key}_conv"]
+    assert np.array_equal(x, g[f"{key}_x"])
