@@ -607,6 +607,12 @@ void k_rowpair(const uint8_t* __restrict__ pid,
 }
 
 // ---------------------------------------------------------------- CSR-vector variant
+// strided entries per lane loaded together (summation order unchanged: entry l, l+VW, ...);
+// build-time knob (tools/build_variant.sh -DMLAMG_VEC_UNROLL=N)
+#ifndef MLAMG_VEC_UNROLL
+#define MLAMG_VEC_UNROLL 4
+#endif
+constexpr int kVecUnroll = MLAMG_VEC_UNROLL;
 // VW lanes per row (long rows of coarse Galerkin operators). Lane l sums entries l, l+VW, ...
 // in order, then the VW partials are combined by an xor butterfly (off = VW/2 .. 1). This is a
 // DIFFERENT summation order from scipy's, restated exactly by the oracle (oracle.c
@@ -624,29 +630,31 @@ __global__ __launch_bounds__(kThreads) void k_csr_vec(const int32_t* __restrict_
   const int64_t row = gid / VW;
   const int l = threadIdx.x & (VW - 1);
   double s = 0.0;
+  EpiIn pre;
+  if (l == 0 && row < n_rows) pre = epi_load<OP>((int)row, ep);
   if (row < n_rows) {
     const int a = indptr[row], b = indptr[row + 1];
-    // 4 strided entries per lane per step, loads issued together, summed in the same order
-    for (int k = a + l; k < b; k += 4 * VW) {
-      int32_t cc[4];
-      double vv[4], xv[4];
+    // kVecUnroll strided entries per lane per step, loads issued together, summed in order
+    for (int k = a + l; k < b; k += kVecUnroll * VW) {
+      int32_t cc[kVecUnroll];
+      double vv[kVecUnroll], xv[kVecUnroll];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kVecUnroll; ++u) {
         const int e = k + u * VW;
         cc[u] = e < b ? __builtin_nontemporal_load(indices + e) : -1;
         vv[u] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
+      for (int u = 0; u < kVecUnroll; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < kVecUnroll; ++u)
         if (cc[u] >= 0) s += vv[u] * xv[u];
     }
   }
 #pragma unroll
   for (int off = VW / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, VW);
   double sq = 0.0;
-  if (l == 0 && row < n_rows) sq = epilogue<OP>((int)row, s, ep);
+  if (l == 0 && row < n_rows) sq = epi_store<OP>((int)row, s, pre, ep);
   if constexpr (NORM) {
     double w = wave_sum(sq);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
@@ -768,21 +776,23 @@ __global__ __launch_bounds__(512) void k_csr_vecw(const int32_t* __restrict__ in
   const int64_t row = (int64_t)blockIdx.x * RPB + t / VW;
   const int l = t & (VW - 1);
   double s = 0.0;
+  EpiIn pre;
+  if (l == 0 && row < n_rows) pre = epi_load<OP>((int)row, ep);
   if (row < n_rows) {
     const int a = indptr[row], b = indptr[row + 1];
-    for (int k = a + l; k < b; k += 4 * VW) {
-      int32_t cc[4];
-      double vv[4], xv[4];
+    for (int k = a + l; k < b; k += kVecUnroll * VW) {
+      int32_t cc[kVecUnroll];
+      double vv[kVecUnroll], xv[kVecUnroll];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kVecUnroll; ++u) {
         const int e = k + u * VW;
         cc[u] = e < b ? __builtin_nontemporal_load(indices + e) : -1;
         vv[u] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
+      for (int u = 0; u < kVecUnroll; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < kVecUnroll; ++u)
         if (cc[u] >= 0) s += vv[u] * xv[u];
     }
   }
@@ -796,7 +806,7 @@ __global__ __launch_bounds__(512) void k_csr_vecw(const int32_t* __restrict__ in
     double r = wsum[w0];
 #pragma unroll
     for (int q = 1; q < WPR; ++q) r += wsum[w0 + q];
-    sq = epilogue<OP>((int)row, r, ep);
+    sq = epi_store<OP>((int)row, r, pre, ep);
   }
   if constexpr (NORM) {
     if (l == 0) red[t / VW] = sq;
