@@ -122,6 +122,7 @@ struct mlamg_csr {
                                  // patterns padded to multiples of 8 entries
   double* rp_val = nullptr;      // per entry (row 2i's value, row 2i+1's value)
   int32_t rp_n_pat = 0, rp_n_ent = 0;
+  int32_t rp_k = 8;                    // entries per kernel step (patterns padded to multiples)
   std::vector<int32_t> rp_rep;         // representative pair of each pattern (host)
   // attached Jacobi weights (mlamg_csr_attach_dinv): an epilogue whose dinv pointer equals
   // rp_dinv_att reads the per-pattern values rp_dinv[2p], rp_dinv[2p+1] instead of memory

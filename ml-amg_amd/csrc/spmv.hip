@@ -478,6 +478,7 @@ __device__ __forceinline__ double epi_store2(int r, bool both, double s0, double
 // One pair's row sums (rows r, r+1; patterns padded to multiples of 8 entries from a) from the
 // LDS tables: vv[e] = (row 2i's value, row 2i+1's value), of[e] = (column offset, row 2i mask,
 // row 2i+1 mask, flags).
+template <int K>
 __device__ __forceinline__ void rowpair_sums(const double* __restrict__ x, int64_t n_cols, int r,
                                              int a, int len, const dbl2* vv, const int4* of,
                                              double& s0, double& s1) {
@@ -492,16 +493,16 @@ __device__ __forceinline__ void rowpair_sums(const double* __restrict__ x, int64
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(n_cols * 8), 0x00020000);
     const int r8 = r * 8;
-    for (int k = 0; k < len; k += 8) {
-      u32x4 t[8];
-      int4 f[8];
+    for (int k = 0; k < len; k += K) {
+      u32x4 t[K];
+      int4 f[K];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < K; ++q) {
         f[q] = of[a + k + q];
         t[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, r8 + f[q].x * 8, 0, 0);
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < K; ++q) {
         const dbl2 v = vv[a + k + q];
         const uint64_t b0 = ((uint64_t)(t[q].y & (uint32_t)f[q].y) << 32) | (t[q].x & (uint32_t)f[q].y);
         const uint64_t b1 = ((uint64_t)(t[q].w & (uint32_t)f[q].z) << 32) | (t[q].z & (uint32_t)f[q].z);
@@ -513,18 +514,18 @@ __device__ __forceinline__ void rowpair_sums(const double* __restrict__ x, int64
   }
   // edge pairs (first / last rows of the matrix, odd tail): per-row loads as needed
   const double* xr = x + r;
-  for (int k = 0; k < len; k += 8) {
-    double x0[8], x1[8];
-    int fl[8];
+  for (int k = 0; k < len; k += K) {
+    double x0[K], x1[K];
+    int fl[K];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < K; ++q) {
       const int4 f = of[a + k + q];
       fl[q] = f.w;
       x0[q] = (fl[q] & 1) ? xr[f.x] : 0.0;
       x1[q] = (fl[q] & 2) ? xr[f.x + 1] : 0.0;
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < K; ++q) {
       if (fl[q] & 1) s0 += vv[a + k + q].x * x0[q];
       if (fl[q] & 2) s1 += vv[a + k + q].y * x1[q];
     }
@@ -537,7 +538,7 @@ __device__ __forceinline__ void rowpair_sums(const double* __restrict__ x, int64
 #ifndef MLAMG_RP_WAVES
 #define MLAMG_RP_WAVES 0
 #endif
-template <int OP, bool NORM, int CH>
+template <int OP, bool NORM, int CH, int K>
 __global__ __launch_bounds__(kThreads)
 __attribute__((amdgpu_waves_per_eu(MLAMG_RP_WAVES > 0 ? MLAMG_RP_WAVES : 1, 8)))
 void k_rowpair(const uint8_t* __restrict__ pid,
@@ -590,7 +591,7 @@ void k_rowpair(const uint8_t* __restrict__ pid,
     const int a = pst[p];
     const int len = ok0 ? pst[p + 1] - a : 0;
     double s0, s1;
-    rowpair_sums(x, n_cols, r, a, len, vv, of, s0, s1);
+    rowpair_sums<K>(x, n_cols, r, a, len, vv, of, s0, s1);
     if (ok0) sq += epi_store2<OP>(r, both, s0, s1, u, w, ep);
     p = p_next;
   }
@@ -864,22 +865,15 @@ static int dict_slices_per_wave() {
   return v;
 }
 
-// 256-pair chunks per workgroup of the row-pair kernel (env MLAMG_RP_CHUNKS = 1, 2, 4 or 8)
-static int rowpair_chunks() {
-  static int v = [] {
-    const char* e = std::getenv("MLAMG_RP_CHUNKS");
-    const int k = e ? std::atoi(e) : 4;
-    return (k == 1 || k == 2 || k == 4 || k == 8) ? k : 4;
-  }();
-  return v;
-}
+// 256-pair chunks per workgroup of the row-pair kernel (measured: 2-4 best, 1 and 8 slower)
+constexpr int kRpChunks = 4;
 
-template <int OP, bool NORM, int CH>
-static int launch_rowpair_ch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+template <int OP, bool NORM, int CH, int K>
+static int launch_rowpair_ck(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   const int64_t n_pairs = (A->n_rows + 1) / 2;
   const unsigned nb = (unsigned)((n_pairs + CH * kThreads - 1) / (CH * kThreads));
   const size_t lds = (size_t)A->rp_n_ent * 32 + (size_t)A->rp_n_pat * 16 + 257 * 4;
-  hipLaunchKernelGGL((k_rowpair<OP, NORM, CH>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid,
+  hipLaunchKernelGGL((k_rowpair<OP, NORM, CH, K>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid,
                      A->rp_ptr, reinterpret_cast<const int4*>(A->rp_off),
                      reinterpret_cast<const dbl2*>(A->rp_val), A->rp_n_ent, A->n_rows,
                      A->n_cols, A->rp_dinv_att, reinterpret_cast<const dbl2*>(A->rp_dinv),
@@ -888,14 +882,19 @@ static int launch_rowpair_ch(const mlamg_csr* A, const double* x, const Epi& ep,
   return MLAMG_OK;
 }
 
+template <int OP, bool NORM, int CH>
+static int launch_rowpair_ch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  switch (A->rp_k) {  // the pattern step chosen at build time (longest pattern, 5..8)
+    case 5: return launch_rowpair_ck<OP, NORM, CH, 5>(A, x, ep, s);
+    case 6: return launch_rowpair_ck<OP, NORM, CH, 6>(A, x, ep, s);
+    case 7: return launch_rowpair_ck<OP, NORM, CH, 7>(A, x, ep, s);
+    default: return launch_rowpair_ck<OP, NORM, CH, 8>(A, x, ep, s);
+  }
+}
+
 template <int OP, bool NORM>
 static int launch_rowpair(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
-  switch (rowpair_chunks()) {
-    case 1: return launch_rowpair_ch<OP, NORM, 1>(A, x, ep, s);
-    case 2: return launch_rowpair_ch<OP, NORM, 2>(A, x, ep, s);
-    case 8: return launch_rowpair_ch<OP, NORM, 8>(A, x, ep, s);
-    default: return launch_rowpair_ch<OP, NORM, 4>(A, x, ep, s);
-  }
+  return launch_rowpair_ch<OP, NORM, kRpChunks>(A, x, ep, s);
 }
 
 // ---------------------------------------------------------------- launch helpers
@@ -1668,6 +1667,7 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
   if (rc == MLAMG_OK && (hc[2] != 0 || hc[0] > 255))
     fail(MLAMG_EUNSUPPORTED, "more than 255 distinct row-pair patterns");
   std::vector<int32_t> hptr(257, 0), hoff, reps;
+  int kstep = 8;
   std::vector<double> hv0, hv1;
   std::vector<uint8_t> hfl;
   int n_pat = 0;
@@ -1700,6 +1700,14 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
     };
     std::vector<int32_t> o0, o1;
     std::vector<double> w0, w1;
+    struct Ent {
+      int32_t off;
+      double v0, v1;
+      uint8_t fl;
+    };
+    std::vector<std::vector<Ent>> pent(pats.size());
+    std::vector<bool> pwide(pats.size(), false);
+    size_t maxlen = 0;
     for (size_t k = 0; k < pats.size() && rc == MLAMG_OK; ++k) {
       hslot[pats[k].second] = (int32_t)k;
       const int64_t r0 = 2 * (int64_t)pats[k].first;
@@ -1717,21 +1725,33 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
       for (int32_t o : o1) wide = wide && r0 + 1 + o >= 1;
       // merge the two rows by offset (each row keeps its stored = ascending order)
       size_t i = 0, j = 0;
+      auto& pe = pent[k];
       while (i < o0.size() || j < o1.size()) {
         const bool t0 = i < o0.size() && (j >= o1.size() || o0[i] <= o1[j]);
         const bool t1 = j < o1.size() && (i >= o0.size() || o1[j] <= o0[i]);
-        hoff.push_back(t0 ? o0[i] : o1[j]);
-        hv0.push_back(t0 ? w0[i] : 0.0);
-        hv1.push_back(t1 ? w1[j] : 0.0);
-        hfl.push_back((uint8_t)((t0 ? 1 : 0) | (t1 ? 2 : 0) | (wide ? 4 : 0)));
+        pe.push_back({t0 ? o0[i] : o1[j], t0 ? w0[i] : 0.0, t1 ? w1[j] : 0.0,
+                      (uint8_t)((t0 ? 1 : 0) | (t1 ? 2 : 0) | (wide ? 4 : 0))});
         i += t0;
         j += t1;
       }
-      while (hoff.size() % 8) {  // pad to whole 8-entry steps of the kernel: null entries
+      pwide[k] = wide;
+      maxlen = std::max(maxlen, pe.size());
+    }
+    // the kernel's step: the longest pattern when it fits one step of 5..8 entries, else 8;
+    // every pattern is padded with null entries to whole steps
+    kstep = maxlen <= 5 ? 5 : (maxlen <= 8 ? (int)maxlen : 8);
+    for (size_t k = 0; k < pats.size() && rc == MLAMG_OK; ++k) {
+      for (auto& en : pent[k]) {
+        hoff.push_back(en.off);
+        hv0.push_back(en.v0);
+        hv1.push_back(en.v1);
+        hfl.push_back(en.fl);
+      }
+      while ((hoff.size() - hptr[k]) % kstep) {
         hoff.push_back(0);
         hv0.push_back(0.0);
         hv1.push_back(0.0);
-        hfl.push_back((uint8_t)(wide ? 4 : 0));
+        hfl.push_back((uint8_t)(pwide[k] ? 4 : 0));
       }
       if ((int)hoff.size() > kRpMaxEnt) {
         fail(MLAMG_EUNSUPPORTED, "row-pair patterns hold more than 2048 (padded) entries");
@@ -1788,6 +1808,7 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
   A->rp_val = pval;
   A->rp_n_pat = n_pat;
   A->rp_n_ent = (int32_t)hoff.size();
+  A->rp_k = kstep;
   A->rp_rep = std::move(reps);
   return MLAMG_OK;
 }
@@ -1805,7 +1826,7 @@ __global__ void k_rp_dinv_check(const uint8_t* __restrict__ pid, const double* _
 }
 
 static int32_t rowpat_parts(const mlamg_csr* A) {
-  const int64_t n_pairs = (A->n_rows + 1) / 2, per = (int64_t)rowpair_chunks() * kThreads;
+  const int64_t n_pairs = (A->n_rows + 1) / 2, per = (int64_t)kRpChunks * kThreads;
   return (int32_t)std::max<int64_t>(1, (n_pairs + per - 1) / per);
 }
 

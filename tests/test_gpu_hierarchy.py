@@ -345,8 +345,11 @@ def _pair_patterns(A):
     pats = {}
     for i in range(0, n, 2):
         (o0, v0), (o1, v1) = row(i), row(i + 1)
-        pats[(o0, v0, o1, v1)] = -(-len(set(o0) | set(o1)) // 8) * 8  # padded to 8
-    return len(pats), sum(pats.values())
+        pats[(o0, v0, o1, v1)] = len(set(o0) | set(o1))
+    # padded to whole kernel steps: the longest pattern when 5..8 entries, else 8
+    mx = max(pats.values())
+    k = 5 if mx <= 5 else (mx if mx <= 8 else 8)
+    return len(pats), sum(-(-m // k) * k for m in pats.values())
 
 
 def test_rowpat_format(ml, torch_cuda):

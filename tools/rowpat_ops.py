@@ -1,6 +1,6 @@
 """Time the C4 fine-level operator's kernels in one storage format (default rowpat): y = A x,
 r = b - A x with the norm, two weighted-Jacobi sweeps (attached weights when rowpat), for A/B runs
-of kernel variants (MLAMG_LIB=<variant .so>, MLAMG_FMT, MLAMG_RP_CHUNKS ...). GPU box only.
+of kernel variants (MLAMG_LIB=<variant .so>, MLAMG_FMT). GPU box only.
 
   python tools/rowpat_ops.py [n=216] [reps=30]
 """
