@@ -55,9 +55,12 @@ constexpr int kBlockRows = 256;
 constexpr int kBlockNnz = 2048;   // 16 KiB of fp64 products in LDS per workgroup
 // "sorted" format blocks: 512-thread workgroups, 32 KiB of products; 12 slot bits leave 20 bits
 // of column offset, so a block's columns must span < 2^20
-constexpr int kSrtThreads = 512;
-constexpr int kSrtRows = 512;
-constexpr int kSrtNnz = 4096;
+#ifndef MLAMG_SRT_THREADS  // build-time A/B knob (measured: 256 is 2-10 % slower than 512)
+#define MLAMG_SRT_THREADS 512
+#endif
+constexpr int kSrtThreads = MLAMG_SRT_THREADS;
+constexpr int kSrtRows = MLAMG_SRT_THREADS;
+constexpr int kSrtNnz = 8 * MLAMG_SRT_THREADS;
 constexpr int kSrtPosBits = 12;
 
 }  // namespace mlamg

@@ -3,5 +3,6 @@ set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python tools/kernel_roofline.py > gpurun_out/kernel_roofline.md 2> gpurun_out/kernel_roofline.err || { tail -20 gpurun_out/kernel_roofline.err; exit 1; }
-cat gpurun_out/kernel_roofline.md
+timeout -k 10 300 python tools/kernel_roofline.py > gpurun_out/kr_a.md 2>/dev/null || exit 1
+MLAMG_LIB=$PWD/tools/variants/libmlamg_srt256.so timeout -k 10 300 python tools/kernel_roofline.py > gpurun_out/kr_b.md 2>/dev/null || exit 1
+paste -d'|' <(cut -d'|' -f2,3,4,8 gpurun_out/kr_a.md) <(cut -d'|' -f4,8 gpurun_out/kr_b.md)
