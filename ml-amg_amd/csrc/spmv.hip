@@ -1492,7 +1492,8 @@ static int build_sorted(mlamg_csr* A, hipStream_t s) {
 // A pair's key: a 64-bit hash of both rows' lengths and (col - row, value bits) sequences. Pairs
 // are inserted into an open-addressing table (<= 255 keys, else refused) with the smallest pair
 // of each key as its representative; the host orders patterns by representative, reads their
-// rows and merges them by offset (rows must be strictly column-sorted), and k_rp_assign then
+// rows and merges them by offset (or, for rows not in ascending column order, by the shortest
+// merge that keeps each row's stored order), and k_rp_assign then
 // checks every pair against its pattern entry by entry (a hash collision makes the format
 // refuse, it never changes a result).
 __device__ __forceinline__ unsigned long long rp_mix(unsigned long long z) {
@@ -1614,8 +1615,7 @@ static void drop_rowpat(mlamg_csr* A) {
   if (!A->sell_ptr && !A->vec_width && !A->srt_pk) A->n_part = A->n_blocks;
 }
 
-// EUNSUPPORTED (A unchanged) past 255 distinct pair patterns, kRpMaxEnt pattern entries, or
-// when a representative row is not strictly column-sorted.
+// EUNSUPPORTED (A unchanged) past 255 distinct pair patterns or kRpMaxEnt pattern entries.
 static int build_rowpat(mlamg_csr* A, hipStream_t s) {
   const int64_t n = A->n_rows;
   const int64_t n_pairs = (n + 1) / 2;
@@ -1715,24 +1715,51 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
         fail(MLAMG_EHIP, "pattern fetch");
         break;
       }
+      bool sorted_rows = true;
       for (auto* o : {&o0, &o1})
-        for (size_t e = 1; e < o->size(); ++e)
-          if ((*o)[e] <= (*o)[e - 1]) fail(MLAMG_EUNSUPPORTED, "rows are not column-sorted");
-      if (rc != MLAMG_OK) break;
+        for (size_t e = 1; e < o->size(); ++e) sorted_rows = sorted_rows && (*o)[e] > (*o)[e - 1];
       // wide (see rp_pair_wide): the same rule on the representative pair
       bool wide = r0 + 1 < n;
       for (int32_t o : o0) wide = wide && r0 + o <= A->n_cols - 2;
       for (int32_t o : o1) wide = wide && r0 + 1 + o >= 1;
-      // merge the two rows by offset (each row keeps its stored = ascending order)
-      size_t i = 0, j = 0;
       auto& pe = pent[k];
-      while (i < o0.size() || j < o1.size()) {
-        const bool t0 = i < o0.size() && (j >= o1.size() || o0[i] <= o1[j]);
-        const bool t1 = j < o1.size() && (i >= o0.size() || o1[j] <= o0[i]);
+      auto emit = [&](bool t0, bool t1, size_t i, size_t j) {
         pe.push_back({t0 ? o0[i] : o1[j], t0 ? w0[i] : 0.0, t1 ? w1[j] : 0.0,
                       (uint8_t)((t0 ? 1 : 0) | (t1 ? 2 : 0) | (wide ? 4 : 0))});
-        i += t0;
-        j += t1;
+      };
+      if (sorted_rows) {
+        // merge the two rows by offset (each row keeps its stored = ascending order)
+        size_t i = 0, j = 0;
+        while (i < o0.size() || j < o1.size()) {
+          const bool t0 = i < o0.size() && (j >= o1.size() || o0[i] <= o1[j]);
+          const bool t1 = j < o1.size() && (i >= o0.size() || o1[j] <= o0[i]);
+          emit(t0, t1, i, j);
+          i += t0;
+          j += t1;
+        }
+      } else {
+        // rows in stored but not ascending column order (a partitioned operator whose ghost
+        // columns follow the owned ones, csrc/comm.hip): the shortest merge that keeps each
+        // row's stored order, sharing one 16-byte load where both rows have the same offset
+        // (longest common subsequence of the two offset sequences)
+        const size_t a = o0.size(), b = o1.size();
+        std::vector<int32_t> L((a + 1) * (b + 1), 0);  // L[i][j] = LCS of o0[i:], o1[j:]
+        for (size_t i = a; i-- > 0;)
+          for (size_t j = b; j-- > 0;)
+            L[i * (b + 1) + j] = o0[i] == o1[j] ? 1 + L[(i + 1) * (b + 1) + j + 1]
+                                                : std::max(L[(i + 1) * (b + 1) + j],
+                                                           L[i * (b + 1) + j + 1]);
+        size_t i = 0, j = 0;
+        while (i < a || j < b) {
+          if (i < a && j < b && o0[i] == o1[j] &&
+              L[i * (b + 1) + j] == 1 + L[(i + 1) * (b + 1) + j + 1]) {
+            emit(true, true, i++, j++);
+          } else if (j >= b || (i < a && L[(i + 1) * (b + 1) + j] >= L[i * (b + 1) + j + 1])) {
+            emit(true, false, i++, j);
+          } else {
+            emit(false, true, i, j++);
+          }
+        }
       }
       pwide[k] = wide;
       maxlen = std::max(maxlen, pe.size());
