@@ -82,10 +82,13 @@ class DistributedHierarchy:
     level K-1 the owned coarse segments are allgathered and every rank runs the replicated
     coarse cycle. The iterate is bitwise the single-GPU Hierarchy.cycle iterate."""
 
-    def __init__(self, H, comm, min_rows=50000, max_partitioned=None, A_host=None):
+    def __init__(self, H, comm, min_rows=50000, max_partitioned=None, A_host=None,
+                 local_autotune=True):
         """H: mlamg.hierarchy.Hierarchy built identically on every rank (sorted seeds, same
         kernel formats — see sync_formats). Levels with at least `min_rows` rows (at most
-        `max_partitioned` of them) are row-partitioned; the rest are replicated."""
+        `max_partitioned` of them) are row-partitioned; the rest are replicated.
+        local_autotune: time every exact-order kernel on each rank's local operators (see
+        tune_local) instead of reusing the global operator's choice."""
         if not H.levels:
             raise ValueError("distributed cycle needs at least one level above the coarse solve")
         if (H.nu_pre, H.nu_post) != (1, 1):
@@ -111,14 +114,12 @@ class DistributedHierarchy:
         self.lo, self.hi = p0["lo"], p0["hi"]
         self.n_own = self.hi - self.lo
 
-        def like(M_glob, M_loc):  # the kernel H chose for the global operator
-            fmt, arg, _ = M_glob.get_format()
-            try:
-                return M_loc.set_format(fmt, arg)
-            except _lib.MlamgError as e:  # e.g. sorted: ghost columns too far from owned
-                if e.code != _lib.MLAMG_EUNSUPPORTED:
-                    raise
-                return M_loc.set_format("csr_stream")  # same summation order
+        self.tuning = []
+
+        def like(M_glob, M_loc, kind):
+            M, t = tune_local(M_glob, M_loc, kind, autotune=local_autotune)
+            self.tuning.append(t)
+            return M
 
         self._keep = []
         last = parts[-1]
@@ -140,9 +141,9 @@ class DistributedHierarchy:
         self.ghosts = []
         for l, p in enumerate(parts):
             Lg = H.levels[l]
-            A_loc = like(Lg.A, DeviceCSR.from_scipy(p["A_loc"], check=False))
-            P_loc = like(Lg.P, DeviceCSR.from_scipy(p["P_loc"], check=False))
-            R_own = like(Lg.R, DeviceCSR.from_scipy(p["R_own"], check=False))
+            A_loc = like(Lg.A, DeviceCSR.from_scipy(p["A_loc"], check=False), "A")
+            P_loc = like(Lg.P, DeviceCSR.from_scipy(p["P_loc"], check=False), "P")
+            R_own = like(Lg.R, DeviceCSR.from_scipy(p["R_own"], check=False), "R")
             dinv = Lg.dinv[p["lo"]:p["hi"]].clone()
             if A_loc.get_format()[0] == "rowpat":
                 A_loc.attach_dinv(dinv)
@@ -188,6 +189,40 @@ class DistributedHierarchy:
                 except Exception:
                     pass
                 setattr(self, attr, None)
+
+
+def tune_local(M_glob, M_loc, kind, autotune=True):
+    """Kernel for one rank's local operator. Every exact-order format (CSR-stream, SELL, sorted,
+    dictionary SELL, row-pair patterns) sums each row in its stored order, so when the global
+    operator uses one of them any of them reproduces its rows bit for bit: with autotune the
+    fastest on the local operator (ghost columns change what the encoders accept and how well
+    they pack) is kept. A CSR-vector global operator keeps its lane width (that order is part of
+    the result). Returns (M_loc, {"chosen": ..., "us": {...}})."""
+    from .hierarchy import Hierarchy
+    fmt, arg, _ = M_glob.get_format()
+    if fmt == "vector" or not autotune:
+        try:
+            M_loc.set_format(fmt, arg)
+        except _lib.MlamgError as e:  # e.g. sorted: ghost columns too far from owned
+            if e.code != _lib.MLAMG_EUNSUPPORTED or fmt == "vector":
+                raise
+            M_loc.set_format("csr_stream")  # same summation order
+        return M_loc, {"chosen": "/".join(map(str, M_loc.get_format()[:2]))}
+    x = torch.randn(M_loc.shape[1], dtype=torch.float64, device="cuda")
+    y = torch.zeros(M_loc.shape[0], dtype=torch.float64, device="cuda")
+    if kind == "A" and M_loc.shape[0] != M_loc.shape[1]:
+        kind = "R"  # ghost columns: mlamg_residual is square-only, time y = A x instead
+    times = {}
+    for f, a in Hierarchy.EXACT_CANDIDATES:
+        try:
+            times[f"{f}/{a}"] = Hierarchy._time_format(M_loc, f, a, x, y, kind=kind)
+        except _lib.MlamgError as e:
+            if e.code != _lib.MLAMG_EUNSUPPORTED:
+                raise
+    best = min(times, key=times.get)
+    f, a = best.split("/")
+    M_loc.set_format(f, int(a))
+    return M_loc, {"chosen": best, "us": {k: round(v, 2) for k, v in times.items()}}
 
 
 def sync_formats(H, world):
@@ -327,6 +362,9 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
                 "n": n, "levels": H.n_levels, "parallelism": f"rowsplit{world}",
                 "dist_matches_single_gpu": bool(ok.item() == 1.0),
                 "cycle_graph": graph_on,
+                "rank0_local_formats": [
+                    {k: t["chosen"] for k, t in zip("APR", D.tuning[3 * l:3 * l + 3])}
+                    for l in range(D.K)],
             },
             "roofline": {
                 "bound": "hbm", "kernel": f"fine-level SpMV ({D.A_loc.get_format()[0]}), local rows "
