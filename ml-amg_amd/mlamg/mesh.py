@@ -207,6 +207,103 @@ def poisson_dirichlet(mesh, epsilon=1.0, theta=0.0):
     return _dirichlet(p1_stiffness(mesh.points, mesh.cells["triangle"], kappa), mesh)
 
 
+def unit_cube_tets(Nx, Ny, Nz, flip=(0, 0, 0)):
+    """Tetrahedral mesh of [0,1]^3 with Nx x Ny x Nz cells, each split into the 6 tetrahedra
+    that share one main diagonal of the cell (firedrake UnitCubeMesh, the mesh of
+    utils/create_3d_laplace.py:36). Nodes are numbered lexicographically, x fastest:
+    p = i + (Nx+1) (j + (Ny+1) k). flip[a] = 1 reflects the shared diagonal along axis a; the
+    default (0,0,0)-(1,1,1) diagonal is the one the reference's laplace_3d.grid was built on
+    (tests/test_mesh.py pins it)."""
+    nxp, nyp = Nx + 1, Ny + 1
+    i, j, k = np.meshgrid(np.arange(Nx + 1), np.arange(Ny + 1), np.arange(Nz + 1), indexing="ij")
+    pts = np.stack([i.ravel(order="F") / Nx, j.ravel(order="F") / Ny, k.ravel(order="F") / Nz],
+                   axis=1)
+    ci, cj, ck = np.meshgrid(np.arange(Nx), np.arange(Ny), np.arange(Nz), indexing="ij")
+    ci, cj, ck = ci.ravel(order="F"), cj.ravel(order="F"), ck.ravel(order="F")
+    f = np.asarray(flip, dtype=np.int64)
+    tets = []
+    for perm in ((0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1), (2, 1, 0)):
+        o = np.zeros(3, dtype=np.int64)
+        verts = []
+        for step in range(4):
+            if step:
+                o = o.copy()
+                o[perm[step - 1]] = 1
+            oo = o ^ f
+            verts.append((ci + oo[0]) + nxp * ((cj + oo[1]) + nyp * (ck + oo[2])))
+        tets.append(np.stack(verts, axis=1))
+    return pts, np.concatenate(tets).astype(np.int64)
+
+
+def p1_stiffness_3d(points, tets, D=None):
+    """Global P1 grad-grad matrix inner(D grad u, grad v) dx on tetrahedra (n x n CSR, duplicates
+    summed, sorted columns); D a constant (3, 3) tensor or None (identity). Exact for P1."""
+    P = points[tets]                                    # (t, 4, 3)
+    J = P[:, 1:] - P[:, :1]                             # rows p_k - p_0
+    det = np.linalg.det(J)
+    Jinv = np.linalg.inv(J)                             # grad lambda_k = column k of J^-1
+    G = np.empty((len(tets), 4, 3))
+    G[:, 1:] = np.transpose(Jinv, (0, 2, 1))
+    G[:, 0] = -G[:, 1:].sum(axis=1)
+    KG = G if D is None else np.einsum("ij,tkj->tki", np.asarray(D, dtype=np.float64), G)
+    Ke = (np.abs(det) / 6.0)[:, None, None] * np.einsum("tki,tli->tkl", G, KG)
+    rows = np.repeat(tets, 4, axis=1).ravel()
+    cols = np.tile(tets, (1, 4)).ravel()
+    n = points.shape[0]
+    A = sp.coo_matrix((Ke.ravel(), (rows, cols)), shape=(n, n)).tocsr()
+    A.sort_indices()
+    return A
+
+
+def aniso_tensor_3d(theta_y, theta_z, eps_x, eps_y):
+    """D = R^T diag(eps_x, eps_y, 1) R with R = R_y(theta_y) R_z(theta_z)
+    (utils/create_3d_laplace.py:45-57)."""
+    cz, sz, cy, sy = np.cos(theta_z), np.sin(theta_z), np.cos(theta_y), np.sin(theta_y)
+    R_z = np.array([[cz, -sz, 0.0], [sz, cz, 0.0], [0.0, 0.0, 1.0]])
+    R_y = np.array([[cy, 0.0, sy], [0.0, 1.0, 0.0], [-sy, 0.0, cy]])
+    R = R_y @ R_z
+    return R.T @ np.diag([eps_x, eps_y, 1.0]) @ R
+
+
+def aniso_laplace_3d(Nx, Ny, Nz, theta_y=0.0, theta_z=0.0, eps_x=1.0, eps_y=1.0):
+    """gen_aniso_laplace (utils/create_3d_laplace.py:35-76) restated without firedrake: P1 on
+    unit_cube_tets, D = aniso_tensor_3d, the 6 cube faces' nodes removed (R A R^T, :68-76).
+    Returns (A, xyz) with A (interior nodes in lexicographic order, int32 CSR, sorted columns,
+    exact zeros dropped as scipy's SpGEMM does) and the interior node coordinates. The reference
+    numbers DoFs in firedrake's order; tests/test_mesh.py matches its laplace_3d.grid by
+    coordinates."""
+    pts, tets = unit_cube_tets(Nx, Ny, Nz)
+    A = p1_stiffness_3d(pts, tets, aniso_tensor_3d(theta_y, theta_z, eps_x, eps_y))
+    eps = 1e-12
+    interior = np.all((pts > eps) & (pts < 1.0 - eps), axis=1)
+    R = sp.eye(pts.shape[0], format="csr")[interior]
+    A_d = (R @ A @ R.T).tocsr()
+    A_d.eliminate_zeros()
+    A_d.sort_indices()
+    A_d.indices = A_d.indices.astype(np.int32)
+    A_d.indptr = A_d.indptr.astype(np.int32)
+    return A_d, pts[interior]
+
+
+def random_aniso_laplace_3d(rand, anisotropic=True):
+    """One grid of create_3d_laplace.py's loop (:79-95): N in [8, 15) per axis; theta_y, theta_z
+    ~ U[0, 2 pi), eps_x, eps_y ~ 10^U[-4, 4] when anisotropic. Draw order follows the
+    reference (Nx, Ny, Nz, theta_z, theta_y, eps_x, eps_y). Returns (A, xyz, extra)."""
+    Nx, Ny, Nz = rand.randint(8, 15), rand.randint(8, 15), rand.randint(8, 15)
+    if anisotropic:
+        theta_z = rand.uniform(0, 2 * np.pi)
+        theta_y = rand.uniform(0, 2 * np.pi)
+        eps_x = 10.0 ** rand.uniform(-4.0, 4.0)
+        eps_y = 10.0 ** rand.uniform(-4.0, 4.0)
+    else:
+        theta_z = theta_y = 0.0
+        eps_x = eps_y = 1.0
+    A, xyz = aniso_laplace_3d(Nx, Ny, Nz, theta_y, theta_z, eps_x, eps_y)
+    extra = {"theta_z": theta_z, "theta_y": theta_y, "eps_x": eps_x, "eps_y": eps_y,
+             "eps_z": 1.0, "dim": 3, "Nx": Nx, "Ny": Ny, "Nz": Nz}
+    return A, xyz, extra
+
+
 def poisson_dirichlet_jumps(mesh, jumps):
     """meshio_2d_poisson_dirichlet_jump_coeffs (ns/model/data.py:346-394): scalar coefficient of
     the nearest jump seed (rows [x, y, d]), evaluated at the element centroid."""

@@ -52,10 +52,17 @@ def _matrix(name):
         jumps = np.column_stack([rs.uniform(0, 4, 3), rs.uniform(0, 1, 3),
                                  10.0 ** rs.uniform(-4, 4, 3)])
         return mesh.poisson_dirichlet_jumps(mesh.load_npz(MESH), jumps)[0]
+    if name == "lap3d_grid":  # the reference's own demos/laplace_3d.grid (1331 DoF, aniso P1)
+        g = np.load(os.path.join(HERE, "golden", "laplace_3d_grid.npz"))
+        return sp.csr_matrix((g["data"], g["indices"], g["indptr"]))
+    if name == "aniso3d_48":  # utils/create_3d_laplace.py family at 47^3 interior DoF
+        return mesh.aniso_laplace_3d(48, 48, 48, theta_y=1.0, theta_z=0.5, eps_x=1e-2,
+                                     eps_y=10.0)[0]
     raise KeyError(name)
 
 
-@pytest.mark.parametrize("name", ("c2_1024", "c3", "c3_r2", "c5_grid", "c5_mesh"))
+@pytest.mark.parametrize("name", ("c2_1024", "c3", "c3_r2", "c5_grid", "c5_mesh", "lap3d_grid",
+                                  "aniso3d_48"))
 def test_config_hierarchy_and_cycle_parity(ml, oracle, torch_cuda, name):
     torch = torch_cuda
     A = _matrix(name)

@@ -133,3 +133,53 @@ def test_jump_and_anisotropic_coefficients():
     Aa, _ = mesh.poisson_dirichlet(m, epsilon=0.01, theta=np.pi / 6)
     assert abs(Aa - Aa.T).max() <= 1e-12
     assert np.all(np.linalg.eigvalsh(Aa.toarray()[:300, :300]) > 0)
+
+
+GRID3D = os.path.join(HERE, "golden", "laplace_3d_grid.npz")
+
+
+def test_aniso_laplace_3d_matches_reference_grid():
+    """mesh.aniso_laplace_3d (utils/create_3d_laplace.py:35-76 without firedrake) against the
+    reference's own output demos/laplace_3d.grid (fixture: tests/golden/make_grid_fixture.py):
+    after matching DoFs by coordinates, the same sparsity and the same values to assembly
+    rounding (different element summation order: 1e-14 of max|a_ij|)."""
+    g = np.load(GRID3D)
+    Aref = sp.csr_matrix((g["data"], g["indices"], g["indptr"]))
+    N = 12  # 11^3 = 1331 interior nodes
+    from mlamg import mesh
+    A, xyz = mesh.aniso_laplace_3d(N, N, N, float(g["theta_y"]), float(g["theta_z"]),
+                                   float(g["eps_x"]), float(g["eps_y"]))
+    assert A.shape == Aref.shape and A.nnz == Aref.nnz
+    assert A.indices.dtype == np.int32 and A.has_sorted_indices
+
+    def key(c):
+        return np.rint(c * N).astype(np.int64) @ np.array([1, 100, 10000])
+    mine = {k: i for i, k in enumerate(key(xyz))}
+    p = np.array([mine[k] for k in key(g["x"])])
+    assert len(set(p.tolist())) == A.shape[0]
+    B = A[p][:, p].tocsr()
+    B.sort_indices()
+    Ar = Aref.copy()
+    Ar.sort_indices()
+    assert np.array_equal(B.indptr, Ar.indptr) and np.array_equal(B.indices, Ar.indices)
+    assert np.abs(B.data - Ar.data).max() <= 1e-14 * np.abs(Ar.data).max()
+    # the other diagonal orientations give a different operator: the split is pinned
+    pts, tets = mesh.unit_cube_tets(N, N, N, flip=(1, 0, 0))
+    K = mesh.p1_stiffness_3d(pts, tets, mesh.aniso_tensor_3d(
+        float(g["theta_y"]), float(g["theta_z"]), float(g["eps_x"]), float(g["eps_y"])))
+    assert abs(K.sum() - 0.0) < 1e-10  # Neumann operator annihilates constants
+    interior = np.all((pts > 1e-12) & (pts < 1 - 1e-12), axis=1)
+    Kf = K[interior][:, interior].tocsr()
+    assert np.abs((Kf[p][:, p] - Ar)).max() > 1e-3
+
+
+def test_random_aniso_laplace_3d_family():
+    from mlamg import mesh
+    A, xyz, extra = mesh.random_aniso_laplace_3d(np.random.RandomState(0))
+    Nx, Ny, Nz = extra["Nx"], extra["Ny"], extra["Nz"]
+    assert all(8 <= v < 15 for v in (Nx, Ny, Nz))
+    assert A.shape[0] == (Nx - 1) * (Ny - 1) * (Nz - 1) == xyz.shape[0]
+    assert abs(A - A.T).max() <= 1e-12 * abs(A).max()
+    # SPD after the Dirichlet reduction: Cholesky-free check via the smallest eigenvalue
+    w = np.linalg.eigvalsh(A.toarray())
+    assert w.min() > 0
