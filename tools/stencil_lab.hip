@@ -75,6 +75,45 @@ __global__ __launch_bounds__(256) void k_pair(const double* __restrict__ x, doub
   *reinterpret_cast<dbl2*>(y + r) = o;
 }
 
+// as k_pair<7> but the +-1 neighbours come from the adjacent lanes' centre loads (DPP/bpermute
+// shuffles); only the wave's edge lanes load them (8 B). 5 x loads of 16 B per pair instead of 7.
+template <int ORDER>
+__global__ __launch_bounds__(256) void k_pair_shfl(const double* __restrict__ x,
+                                                   double* __restrict__ y, int n, int64_t N) {
+  const int64_t lb = ORDER == 0 ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int64_t p = lb * 256 + threadIdx.x;
+  const int64_t r = 2 * p;
+  const bool live = r + 1 < N;
+  const int64_t n2 = (int64_t)n * n;
+  const int lane = threadIdx.x & 63;
+  dbl2 c = live ? *reinterpret_cast<const dbl2*>(x + r) : dbl2{0.0, 0.0};
+  double prev = __shfl_up(c.y, 1, 64);
+  double next = __shfl_down(c.x, 1, 64);
+  if (lane == 0) prev = (live && r > 0) ? x[r - 1] : 0.0;
+  if (lane == 63) next = (live && r + 2 < N) ? x[r + 2] : 0.0;
+  if (!live) return;
+  double s0 = 6.0 * c.x, s1 = 6.0 * c.y;
+  s0 -= prev;
+  s1 -= c.x;
+  s0 -= c.y;
+  s1 -= next;
+  auto nb = [&](int64_t off) {
+    if (r + off >= 0 && r + off + 1 < N) {
+      const dbl2 t = *reinterpret_cast<const dbl2u*>(x + r + off);
+      s0 -= t.x;
+      s1 -= t.y;
+    }
+  };
+  nb(-n);
+  nb(n);
+  nb(-n2);
+  nb(n2);
+  dbl2 o;
+  o.x = s0;
+  o.y = s1;
+  *reinterpret_cast<dbl2*>(y + r) = o;
+}
+
 // lane per row, 8-byte loads
 template <int MASK, int ORDER>
 __global__ __launch_bounds__(256) void k_row(const double* __restrict__ x, double* __restrict__ y,
@@ -192,6 +231,11 @@ int main(int argc, char** argv) {
   run_pair<4, 0>(x, y, n, N, reps);
   run_pair<7, 0>(x, y, n, N, reps);
   run_pair<7, 1>(x, y, n, N, reps);
+  {
+    const unsigned nb = (unsigned)((N / 2 + 255) / 256);
+    float us = timeit([&] { hipLaunchKernelGGL((k_pair_shfl<0>), dim3(nb), dim3(256), 0, 0, x, y, n, N); }, reps);
+    printf("pair shfl +-1       : %7.1f us  %6.0f GB/s (x+y)\n", us, 16.0 * N / us / 1e3);
+  }
   {
     uint8_t* pid;
     CK(hipMalloc(&pid, N / 2 + 1));
