@@ -302,6 +302,32 @@ int mlamg_dhier_set_cycle_graph(mlamg_dhier* D, int use_graph);
 int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cycles, double tol,
                        double* res_hist, int32_t* cycles_done_host, void* stream);
 
+/* ---------------------------------------------------------------- boundary-contract spellings
+ * The entry points as the drop-in contract names them, thin forms of the API
+ * above (csrc/contract.hip). */
+/* lloyd_cluster of ns/lib/graph.py:232 (pyamg 4.x): = mlamg_lloyd_cluster without the distance
+ * output. seeds_inout, cluster_out on the DEVICE. Syncs. */
+int mlamg_lloyd(const mlamg_csr* G, int32_t* seeds_inout, int32_t k, int maxiter,
+                int32_t* cluster_out, void* stream);
+/* n_cycles V-cycles (MLAMG.py:189-195 per level), ||b - A x||_2 per cycle into res_hist (DEVICE,
+ * nullable), no tolerance stop, replayed from a captured hipGraph: = mlamg_hier_vcycle. */
+int mlamg_vcycle(const mlamg_hier* H, const double* b, double* x, int n_cycles, double* res_hist,
+                 void* stream);
+/* process-default RCCL communicator (one per process; the id from mlamg_comm_unique_id on rank
+ * 0, broadcast by the caller); mlamg_comm_default returns it, mlamg_comm_finalize frees it. */
+int mlamg_comm_init(const void* nccl_unique_id, int nranks, int rank);
+int mlamg_comm_default(mlamg_comm** out);
+int mlamg_comm_finalize(void);
+/* one rank's operator: n_own owned rows, columns renumbered into x_ext = [owned | n_ghost
+ * ghosts] (mlamg/partition.py), plus its x halo on the default communicator (layout as in
+ * mlamg_halo_create; recv counts must add up to n_ghost). */
+int mlamg_csr_create_partitioned(int64_t n_own, int64_t n_ghost, int64_t nnz,
+                                 const int32_t* indptr, const int32_t* indices,
+                                 const double* data, int on_device, int32_t n_nbr,
+                                 const int32_t* nbr, const int64_t* send_cnt,
+                                 const int32_t* send_idx_host, const int64_t* recv_cnt,
+                                 mlamg_csr** A_out, mlamg_halo** halo_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,91 @@
+// Entry points under the names of the drop-in boundary contract ("C-ABI the
+// shim must export"): thin forms of the general API declared in include/mlamg.h, for a binding
+// written against that contract.
+//   mlamg_lloyd                  -> mlamg_lloyd_cluster (dist kept internal)
+//   mlamg_vcycle                 -> mlamg_hier_vcycle (no tolerance, graph replay)
+//   mlamg_comm_init              -> mlamg_comm_create into a process-default communicator
+//   mlamg_csr_create_partitioned -> mlamg_csr_create (local columns [owned | ghosts]) +
+//                                   mlamg_halo_create on the default communicator
+#include <mutex>
+
+#include "common.hpp"
+#include "mlamg.h"
+
+namespace {
+std::mutex g_comm_mu;
+mlamg_comm* g_comm = nullptr;  // set by mlamg_comm_init, freed by mlamg_comm_finalize
+}  // namespace
+
+extern "C" {
+
+int mlamg_lloyd(const mlamg_csr* G, int32_t* seeds_inout, int32_t k, int maxiter,
+                int32_t* cluster_out, void* stream) {
+  MLAMG_REQUIRE(G && seeds_inout && cluster_out, "NULL argument");
+  double* dist = nullptr;
+  MLAMG_HIP(hipMalloc(&dist, sizeof(double) * std::max<int64_t>(G->n_rows, 1)));
+  int32_t iters = 0;
+  const int rc =
+      mlamg_lloyd_cluster(G, seeds_inout, k, maxiter, dist, cluster_out, &iters, stream);
+  (void)hipFree(dist);  // mlamg_lloyd_cluster synchronised the stream
+  return rc;
+}
+
+int mlamg_vcycle(const mlamg_hier* H, const double* b, double* x, int n_cycles, double* res_hist,
+                 void* stream) {
+  return mlamg_hier_vcycle(const_cast<mlamg_hier*>(H), b, x, n_cycles, 0.0, res_hist, nullptr, 1,
+                           stream);
+}
+
+int mlamg_comm_init(const void* nccl_unique_id, int nranks, int rank) {
+  MLAMG_REQUIRE(nccl_unique_id, "NULL argument");
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  MLAMG_REQUIRE(g_comm == nullptr, "default communicator already initialised");
+  mlamg_comm* c = nullptr;
+  MLAMG_TRY(mlamg_comm_create(nccl_unique_id, nranks, rank, &c));
+  g_comm = c;
+  return MLAMG_OK;
+}
+
+int mlamg_comm_default(mlamg_comm** out) {
+  MLAMG_REQUIRE(out, "NULL argument");
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  MLAMG_REQUIRE(g_comm != nullptr, "mlamg_comm_init was not called");
+  *out = g_comm;
+  return MLAMG_OK;
+}
+
+int mlamg_comm_finalize(void) {
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  if (g_comm) {
+    (void)mlamg_comm_destroy(g_comm);
+    g_comm = nullptr;
+  }
+  return MLAMG_OK;
+}
+
+int mlamg_csr_create_partitioned(int64_t n_own, int64_t n_ghost, int64_t nnz,
+                                 const int32_t* indptr, const int32_t* indices,
+                                 const double* data, int on_device, int32_t n_nbr,
+                                 const int32_t* nbr, const int64_t* send_cnt,
+                                 const int32_t* send_idx_host, const int64_t* recv_cnt,
+                                 mlamg_csr** A_out, mlamg_halo** halo_out) {
+  MLAMG_REQUIRE(A_out && halo_out && n_own >= 0 && n_ghost >= 0, "invalid argument");
+  int64_t ghosts = 0;
+  for (int32_t q = 0; q < n_nbr; ++q) ghosts += recv_cnt ? recv_cnt[q] : 0;
+  MLAMG_REQUIRE(ghosts == n_ghost, "recv counts do not add up to n_ghost");
+  mlamg_comm* c = nullptr;
+  MLAMG_TRY(mlamg_comm_default(&c));
+  mlamg_halo* h = nullptr;
+  MLAMG_TRY(mlamg_halo_create(c, n_own, n_nbr, nbr, send_cnt, send_idx_host, recv_cnt, &h));
+  mlamg_csr* A = nullptr;
+  const int rc = mlamg_csr_create(n_own, n_own + n_ghost, nnz, indptr, indices, data, on_device, &A);
+  if (rc != MLAMG_OK) {
+    (void)mlamg_halo_destroy(h);
+    return rc;
+  }
+  *A_out = A;
+  *halo_out = h;
+  return MLAMG_OK;
+}
+
+}  // extern "C"

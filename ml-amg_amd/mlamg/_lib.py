@@ -115,6 +115,14 @@ SIGNATURES = {
     "mlamg_dhier_set_coarse_graph": (c_int, [c_vp, c_int]),
     "mlamg_dhier_set_cycle_graph": (c_int, [c_vp, c_int]),
     "mlamg_dhier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_vp]),
+    # boundary-contract spellings (csrc/contract.hip)
+    "mlamg_lloyd": (c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp]),
+    "mlamg_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "mlamg_comm_init": (c_int, [c_vp, c_int, c_int]),
+    "mlamg_comm_default": (c_int, [c_vpp]),
+    "mlamg_comm_finalize": (c_int, []),
+    "mlamg_csr_create_partitioned": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_i32,
+                                             c_vp, c_vp, c_vp, c_vp, c_vpp, c_vpp]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
