@@ -274,6 +274,15 @@ typedef struct mlamg_dhier mlamg_dhier;
 int mlamg_comm_unique_id(void* id_out);
 int mlamg_comm_create(const void* id, int nranks, int rank, mlamg_comm** out);
 int mlamg_comm_destroy(mlamg_comm* c);
+/* In-process test transport (RCCL refuses two ranks on one GPU): the ranks of a loop group are
+ * host threads of ONE process, each with its own stream on the same device; send/recv become
+ * device-to-device copies ordered by events, the all-reduce sums in rank order. Same message
+ * order as the RCCL calls it stands in for; not capturable into a graph. For testing the
+ * distributed executor at world sizes > 1 on a single GPU. */
+typedef struct mlamg_loop_group mlamg_loop_group;
+int mlamg_loop_group_create(int nranks, mlamg_loop_group** out);
+int mlamg_loop_group_destroy(mlamg_loop_group* g);
+int mlamg_comm_create_loopback(mlamg_loop_group* g, int rank, mlamg_comm** out);
 int mlamg_comm_allreduce_sum(mlamg_comm* c, double* buf, int64_t n, void* stream);
 /* ghost layout of one rank: x_ext = [owned n_own | ghosts]; for neighbour q (ascending),
  * send_cnt[q] owned entries (send_idx_host, concatenated) and recv_cnt[q] ghosts, stored

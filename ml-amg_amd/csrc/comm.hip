@@ -17,9 +17,62 @@
 
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <functional>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+
+// In-process transport for testing the executor with several ranks on ONE device (RCCL refuses
+// two ranks on one GPU): every rank is a host thread with its own stream; a send posts (buffer,
+// ready event) into a shared mailbox, the receiver orders its stream after the ready event and
+// copies device-to-device, and the sender's stream is then ordered after that copy (so it cannot
+// overwrite its send buffer early). Same message order and grouping semantics as the RCCL calls
+// it stands in for; never used by a communicator made with mlamg_comm_create.
+struct LoopPost {
+  const double* p = nullptr;
+  size_t n = 0;
+  hipEvent_t ready = nullptr;
+  hipEvent_t done = nullptr;
+  bool consumed = false;
+  ~LoopPost() {
+    if (ready) (void)hipEventDestroy(ready);
+    if (done) (void)hipEventDestroy(done);
+  }
+};
+
+struct LoopRound {  // one all-reduce: every rank's (buffer, ready), then (copied) events
+  std::vector<const double*> buf;
+  std::vector<hipEvent_t> ready, copied;
+  int posted = 0, finished = 0, left = 0;
+};
+
+struct mlamg_loop_group {
+  int W = 1;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<std::tuple<int, int, uint64_t>, std::shared_ptr<LoopPost>> box;
+  std::vector<uint64_t> send_seq, recv_seq;  // [src * W + dst]
+  std::map<uint64_t, LoopRound> rounds;
+  int members = 0;
+};
+
 struct mlamg_comm {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  mlamg_loop_group* loop = nullptr;  // in-process test transport instead of RCCL
+  struct Recv {
+    double* buf;
+    size_t n;
+    int peer;
+  };
+  std::vector<std::shared_ptr<LoopPost>> sends;  // posted in the open group
+  std::vector<Recv> recvs;                       // completed at group end
+  uint64_t ar_seq = 0;
+  double* ar_stage = nullptr;
+  size_t ar_cap = 0;
 };
 
 struct mlamg_halo {
@@ -43,6 +96,175 @@ struct mlamg_halo {
 
 namespace mlamg {
 
+constexpr auto kLoopTimeout = std::chrono::seconds(120);
+
+static int loop_wait(mlamg_loop_group* g, std::unique_lock<std::mutex>& lk,
+                     const std::function<bool()>& ready, const char* what) {
+  if (!g->cv.wait_for(lk, kLoopTimeout, ready)) {
+    set_error(std::string("loopback transport: timed out waiting for ") + what);
+    return MLAMG_ENCCL;
+  }
+  return MLAMG_OK;
+}
+
+static int xgroup_begin(mlamg_comm* c) {
+  if (!c->loop) MLAMG_NCCL(ncclGroupStart());
+  return MLAMG_OK;
+}
+
+static int xsend(mlamg_comm* c, const double* buf, size_t n, int peer, hipStream_t s) {
+  if (!c->loop) {
+    MLAMG_NCCL(ncclSend(buf, n, ncclFloat64, peer, c->comm, s));
+    return MLAMG_OK;
+  }
+  auto post = std::make_shared<LoopPost>();
+  post->p = buf;
+  post->n = n;
+  MLAMG_HIP(hipEventCreateWithFlags(&post->ready, hipEventDisableTiming));
+  MLAMG_HIP(hipEventRecord(post->ready, s));
+  mlamg_loop_group* g = c->loop;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    const uint64_t seq = g->send_seq[c->rank * g->W + peer]++;
+    g->box[std::make_tuple(c->rank, peer, seq)] = post;
+  }
+  g->cv.notify_all();
+  c->sends.push_back(post);
+  return MLAMG_OK;
+}
+
+static int xrecv(mlamg_comm* c, double* buf, size_t n, int peer, hipStream_t s) {
+  if (!c->loop) {
+    MLAMG_NCCL(ncclRecv(buf, n, ncclFloat64, peer, c->comm, s));
+    return MLAMG_OK;
+  }
+  c->recvs.push_back({buf, n, peer});
+  return MLAMG_OK;
+}
+
+static int xgroup_end(mlamg_comm* c, hipStream_t s) {
+  if (!c->loop) {
+    MLAMG_NCCL(ncclGroupEnd());
+    return MLAMG_OK;
+  }
+  mlamg_loop_group* g = c->loop;
+  std::vector<mlamg_comm::Recv> recvs;
+  recvs.swap(c->recvs);
+  std::vector<std::shared_ptr<LoopPost>> sends;
+  sends.swap(c->sends);
+  for (const auto& r : recvs) {
+    std::shared_ptr<LoopPost> post;
+    {
+      std::unique_lock<std::mutex> lk(g->mu);
+      const auto key = std::make_tuple(r.peer, c->rank, g->recv_seq[r.peer * g->W + c->rank]);
+      MLAMG_TRY(loop_wait(g, lk, [&] { return g->box.count(key) != 0; }, "a matching send"));
+      post = g->box[key];
+      g->box.erase(key);
+      ++g->recv_seq[r.peer * g->W + c->rank];
+    }
+    MLAMG_REQUIRE(post->n == r.n, "loopback transport: send/recv sizes differ");
+    MLAMG_HIP(hipStreamWaitEvent(s, post->ready, 0));
+    if (r.n) MLAMG_HIP(hipMemcpyAsync(r.buf, post->p, sizeof(double) * r.n, hipMemcpyDeviceToDevice, s));
+    MLAMG_HIP(hipEventCreateWithFlags(&post->done, hipEventDisableTiming));
+    MLAMG_HIP(hipEventRecord(post->done, s));
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      post->consumed = true;
+    }
+    g->cv.notify_all();
+  }
+  for (const auto& p : sends) {
+    {
+      std::unique_lock<std::mutex> lk(g->mu);
+      MLAMG_TRY(loop_wait(g, lk, [&] { return p->consumed; }, "the receiver of a send"));
+    }
+    MLAMG_HIP(hipStreamWaitEvent(s, p->done, 0));
+  }
+  return MLAMG_OK;
+}
+
+__global__ void k_loop_sum(const double* __restrict__ stage, int W, int64_t n,
+                           double* __restrict__ out) {
+  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  double t = stage[i];
+  for (int r = 1; r < W; ++r) t += stage[(int64_t)r * n + i];
+  out[i] = t;
+}
+
+static int xallreduce_sum(mlamg_comm* c, double* buf, size_t n, hipStream_t s) {
+  if (!c->loop) {
+    MLAMG_NCCL(ncclAllReduce(buf, buf, n, ncclFloat64, ncclSum, c->comm, s));
+    return MLAMG_OK;
+  }
+  mlamg_loop_group* g = c->loop;
+  const int W = g->W;
+  if (c->ar_cap < (size_t)W * n) {
+    MLAMG_HIP(hipStreamSynchronize(s));
+    if (c->ar_stage) (void)hipFree(c->ar_stage);
+    c->ar_stage = nullptr;
+    MLAMG_HIP(hipMalloc(&c->ar_stage, sizeof(double) * std::max<size_t>((size_t)W * n, 1)));
+    c->ar_cap = (size_t)W * n;
+  }
+  const uint64_t round = c->ar_seq++;
+  hipEvent_t ready = nullptr, copied = nullptr;
+  MLAMG_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  MLAMG_HIP(hipEventRecord(ready, s));
+  std::vector<const double*> bufs;
+  std::vector<hipEvent_t> readies;
+  {
+    std::unique_lock<std::mutex> lk(g->mu);
+    LoopRound& R = g->rounds[round];
+    if (R.buf.empty()) {
+      R.buf.assign(W, nullptr);
+      R.ready.assign(W, nullptr);
+      R.copied.assign(W, nullptr);
+    }
+    R.buf[c->rank] = buf;
+    R.ready[c->rank] = ready;
+    ++R.posted;
+    g->cv.notify_all();
+    MLAMG_TRY(loop_wait(g, lk, [&] { return g->rounds[round].posted == W; }, "all-reduce peers"));
+    bufs = g->rounds[round].buf;
+    readies = g->rounds[round].ready;
+  }
+  // every rank's buffer, in rank order, into this rank's staging area
+  for (int r = 0; r < W; ++r) {
+    MLAMG_HIP(hipStreamWaitEvent(s, readies[r], 0));
+    if (n) MLAMG_HIP(hipMemcpyAsync(c->ar_stage + (size_t)r * n, bufs[r], sizeof(double) * n,
+                                    hipMemcpyDeviceToDevice, s));
+  }
+  MLAMG_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
+  MLAMG_HIP(hipEventRecord(copied, s));
+  std::vector<hipEvent_t> copies;
+  {
+    std::unique_lock<std::mutex> lk(g->mu);
+    LoopRound& R = g->rounds[round];
+    R.copied[c->rank] = copied;
+    ++R.finished;
+    g->cv.notify_all();
+    MLAMG_TRY(loop_wait(g, lk, [&] { return g->rounds[round].finished == W; }, "all-reduce copies"));
+    copies = g->rounds[round].copied;
+  }
+  // nobody reads this rank's buffer any more once every copy is done: overwrite it
+  for (int r = 0; r < W; ++r) MLAMG_HIP(hipStreamWaitEvent(s, copies[r], 0));
+  if (n) {
+    hipLaunchKernelGGL(k_loop_sum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       c->ar_stage, W, (int64_t)n, buf);
+    MLAMG_HIP(hipGetLastError());
+  }
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    LoopRound& R = g->rounds[round];
+    if (++R.left == W) {  // last one out: the events have all been waited on by every stream
+      for (auto e : R.ready) (void)hipEventDestroy(e);
+      for (auto e : R.copied) (void)hipEventDestroy(e);
+      g->rounds.erase(round);
+    }
+  }
+  return MLAMG_OK;
+}
+
 __global__ void k_pack(const double* __restrict__ x, const int32_t* __restrict__ idx, int64_t n,
                        double* __restrict__ out) {
   int64_t i = blockIdx.x * 256ll + threadIdx.x;
@@ -56,17 +278,15 @@ int halo_exchange_impl(mlamg_halo* h, double* x_ext, hipStream_t s) {
     MLAMG_HIP(hipGetLastError());
   }
   if (h->nbr.empty()) return MLAMG_OK;
-  MLAMG_NCCL(ncclGroupStart());
+  MLAMG_TRY(xgroup_begin(h->c));
   for (size_t q = 0; q < h->nbr.size(); ++q) {
     if (h->send_cnt[q])
-      MLAMG_NCCL(ncclSend(h->send_buf + h->send_off[q], (size_t)h->send_cnt[q], ncclFloat64,
-                          h->nbr[q], h->c->comm, s));
+      MLAMG_TRY(xsend(h->c, h->send_buf + h->send_off[q], (size_t)h->send_cnt[q], h->nbr[q], s));
     if (h->recv_cnt[q])
-      MLAMG_NCCL(ncclRecv(x_ext + h->n_own + h->recv_off[q], (size_t)h->recv_cnt[q], ncclFloat64,
-                          h->nbr[q], h->c->comm, s));
+      MLAMG_TRY(xrecv(h->c, x_ext + h->n_own + h->recv_off[q], (size_t)h->recv_cnt[q],
+                      h->nbr[q], s));
   }
-  MLAMG_NCCL(ncclGroupEnd());
-  return MLAMG_OK;
+  return xgroup_end(h->c, s);
 }
 
 // sum the residual partials of this rank into partial[n] (fixed order)
@@ -180,15 +400,54 @@ int mlamg_comm_create(const void* id, int nranks, int rank, mlamg_comm** out) {
 int mlamg_comm_destroy(mlamg_comm* c) {
   if (c) {
     if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->ar_stage) (void)hipFree(c->ar_stage);
+    if (c->loop) {
+      std::lock_guard<std::mutex> lk(c->loop->mu);
+      --c->loop->members;
+    }
     delete c;
   }
   return MLAMG_OK;
 }
 
+int mlamg_loop_group_create(int nranks, mlamg_loop_group** out) {
+  MLAMG_REQUIRE(out && nranks >= 1, "invalid argument");
+  auto* g = new mlamg_loop_group();
+  g->W = nranks;
+  g->send_seq.assign((size_t)nranks * nranks, 0);
+  g->recv_seq.assign((size_t)nranks * nranks, 0);
+  *out = g;
+  return MLAMG_OK;
+}
+
+int mlamg_loop_group_destroy(mlamg_loop_group* g) {
+  if (g) {
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      MLAMG_REQUIRE(g->members == 0, "loop group still has communicators");
+    }
+    delete g;
+  }
+  return MLAMG_OK;
+}
+
+int mlamg_comm_create_loopback(mlamg_loop_group* g, int rank, mlamg_comm** out) {
+  MLAMG_REQUIRE(g && out && rank >= 0 && rank < g->W, "invalid argument");
+  auto* c = new mlamg_comm();
+  c->nranks = g->W;
+  c->rank = rank;
+  c->loop = g;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    ++g->members;
+  }
+  *out = c;
+  return MLAMG_OK;
+}
+
 int mlamg_comm_allreduce_sum(mlamg_comm* c, double* buf, int64_t n, void* stream) {
   MLAMG_REQUIRE(c && (n == 0 || buf), "NULL argument");
-  MLAMG_NCCL(ncclAllReduce(buf, buf, (size_t)n, ncclFloat64, ncclSum, c->comm, S(stream)));
-  return MLAMG_OK;
+  return xallreduce_sum(c, buf, (size_t)n, S(stream));
 }
 
 int mlamg_halo_create(mlamg_comm* c, int64_t n_own, int32_t n_nbr, const int32_t* nbr,
@@ -363,6 +622,9 @@ static int dprepare(mlamg_dhier* D) {
   double* f = nullptr;
   MLAMG_TRY(dalloc(D, &f, 1));
   D->flags = reinterpret_cast<int32_t*>(f);
+  // the zero fills run on the null stream and may still be in flight: finish them before work
+  // on the caller's (possibly non-blocking) stream touches these buffers
+  MLAMG_HIP(hipDeviceSynchronize());
   D->ready = true;
   return MLAMG_OK;
 }
@@ -373,16 +635,14 @@ static int allgather_segments(mlamg_dhier* D, hipStream_t s) {
   if (P == 1) return MLAMG_OK;
   const int64_t lo = D->c_lo_all[me];
   const size_t mine = (size_t)(D->c_hi_all[me] - lo);
-  MLAMG_NCCL(ncclGroupStart());
+  MLAMG_TRY(xgroup_begin(D->c));
   for (int q = 0; q < P; ++q) {
     if (q == me) continue;
-    if (mine) MLAMG_NCCL(ncclSend(D->bc + lo, mine, ncclFloat64, q, D->c->comm, s));
+    if (mine) MLAMG_TRY(xsend(D->c, D->bc + lo, mine, q, s));
     const size_t theirs = (size_t)(D->c_hi_all[q] - D->c_lo_all[q]);
-    if (theirs)
-      MLAMG_NCCL(ncclRecv(D->bc + D->c_lo_all[q], theirs, ncclFloat64, q, D->c->comm, s));
+    if (theirs) MLAMG_TRY(xrecv(D->c, D->bc + D->c_lo_all[q], theirs, q, s));
   }
-  MLAMG_NCCL(ncclGroupEnd());
-  return MLAMG_OK;
+  return xgroup_end(D->c, s);
 }
 
 static int dcycle_below(mlamg_dhier* D, size_t l, double** x_out, hipStream_t s);
@@ -451,9 +711,7 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
   const int nb = (int)A->n_part;
   hipLaunchKernelGGL(k_local_sum, dim3(1), dim3(1024), 0, s, D->partial, nb);
   MLAMG_HIP(hipGetLastError());
-  if (D->c->nranks > 1)
-    MLAMG_NCCL(ncclAllReduce(D->partial + nb, D->partial + nb, 1, ncclFloat64, ncclSum,
-                             D->c->comm, s));
+  if (D->c->nranks > 1) MLAMG_TRY(xallreduce_sum(D->c, D->partial + nb, 1, s));
   hipLaunchKernelGGL(k_norm_finish, dim3(1), dim3(1), 0, s, D->partial + nb, hist, counter, done,
                      tol);
   MLAMG_HIP(hipGetLastError());
@@ -474,6 +732,8 @@ int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cyc
   if (n_cycles > 0) {
     // the first cycle's first pre-smoothing sweep (later ones are fused into the cycle end)
     MLAMG_TRY(jacobi_from_residual(x_ext, L.dinv, L.r_ext, L.n_own, nullptr, s));
+    MLAMG_REQUIRE(!(D->cycle_graph && D->c->loop),
+                  "the loopback transport cannot be captured into a graph");
     if (D->cycle_graph) {
       int c0 = 0;
       if (!(D->exec && D->g_b == b && D->g_x == x_ext && D->g_hist == res_hist &&

@@ -120,6 +120,9 @@ static int hier_prepare(mlamg_hier* H) {
   H->partial = take(maxblk);
   H->flags = reinterpret_cast<int32_t*>(p);
   MLAMG_HIP(hipMemset(H->mem, 0, total));
+  // hipMemset runs on the null stream and may return before it completes: a caller on a
+  // non-blocking stream (one thread per rank, csrc/comm.hip's loopback) must not race it
+  MLAMG_HIP(hipDeviceSynchronize());
   H->ready = true;
   return MLAMG_OK;
 }

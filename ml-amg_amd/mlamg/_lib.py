@@ -105,6 +105,9 @@ SIGNATURES = {
     "mlamg_comm_unique_id": (c_int, [c_vp]),
     "mlamg_comm_create": (c_int, [c_vp, c_int, c_int, c_vpp]),
     "mlamg_comm_destroy": (c_int, [c_vp]),
+    "mlamg_loop_group_create": (c_int, [c_int, c_vpp]),
+    "mlamg_loop_group_destroy": (c_int, [c_vp]),
+    "mlamg_comm_create_loopback": (c_int, [c_vp, c_int, c_vpp]),
     "mlamg_comm_allreduce_sum": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "mlamg_halo_create": (c_int, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vpp]),
     "mlamg_halo_destroy": (c_int, [c_vp]),

@@ -49,6 +49,40 @@ class Comm:
             self.handle = None
 
 
+class LoopbackGroup:
+    """In-process test transport (include/mlamg.h mlamg_loop_group): `world` communicators whose
+    ranks are host threads of this process sharing one GPU, each on its own stream. RCCL refuses
+    two ranks on one device; this runs the distributed executor itself (csrc/comm.hip, eager
+    mode) at world sizes > 1 on a single GPU."""
+
+    def __init__(self, world):
+        h = ctypes.c_void_p()
+        call("mlamg_loop_group_create", int(world), ctypes.byref(h))
+        self.handle = h
+        self.world = world
+        self.comms = [LoopbackComm(self, r) for r in range(world)]
+
+    def close(self):
+        for c in self.comms:
+            c.close()
+        if self.handle:
+            call("mlamg_loop_group_destroy", self.handle)
+            self.handle = None
+
+
+class LoopbackComm:
+    def __init__(self, group, rank):
+        self.world, self.rank = group.world, rank
+        h = ctypes.c_void_p()
+        call("mlamg_comm_create_loopback", group.handle, int(rank), ctypes.byref(h))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            _lib.lib.mlamg_comm_destroy(self.handle)
+            self.handle = None
+
+
 class Halo:
     def __init__(self, comm, halo: partition.Halo):
         nn = len(halo.neighbors)

@@ -1,0 +1,119 @@
+"""GPU, one process, world sizes 2, 3 and 8: the distributed executor of csrc/comm.hip — halo
+packs and exchanges, restriction into owned coarse rows, P-halos aliased to the level below's
+buffers, the allgather of coarse segments, the replicated coarse cycle, the norm all-reduce —
+run with every rank a host thread on its own stream of the same GPU, over the in-process loopback
+transport (mlamg_loop_group; RCCL refuses two ranks on one device). Every rank's owned iterate
+must equal the single-GPU iterate bit for bit, and the residual history must agree (only the
+norm's summation order differs). The RCCL calls themselves are the loopback's counterparts, one
+for one (xsend/xrecv/xgroup_*/xallreduce_sum in comm.hip)."""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def setup():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from mlamg import problems
+    from mlamg.hierarchy import Hierarchy
+    A = problems.poisson_3d_7pt(36)
+    H = Hierarchy.build(A, alpha=0.1, max_coarse=200)
+    assert H.n_levels >= 3
+    return A, H
+
+
+def _run(A, H, world, min_rows, ncyc=6, tol=0.0, b=None, x0=None, K=None):
+    import torch
+    from mlamg.distributed import DistributedHierarchy, LoopbackGroup
+    n = A.shape[0]
+    group = LoopbackGroup(world)
+    try:
+        Ds = [DistributedHierarchy(H, group.comms[r], min_rows=min_rows, A_host=A,
+                                   max_partitioned=K)
+              for r in range(world)]
+        for D in Ds:
+            D.set_cycle_graph(False)
+            D.set_coarse_graph(False)
+        bs = [torch.as_tensor(b[D.lo:D.hi]).cuda() for D in Ds]
+        xs = [D.new_x(torch.as_tensor(x0[D.lo:D.hi])) for D in Ds]
+        torch.cuda.synchronize()
+        out = [None] * world
+        errs = []
+
+        def work(r):
+            try:
+                torch.cuda.set_device(0)
+                s = torch.cuda.Stream()
+                with torch.cuda.stream(s):
+                    h = Ds[r].cycle(bs[r], xs[r], ncyc, tol=tol)
+                    s.synchronize()
+                    out[r] = (xs[r][: Ds[r].n_own].cpu().numpy(), h)
+            except Exception as e:  # surfaces in the main thread
+                errs.append((r, e))
+
+        th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=300)
+        assert not any(t.is_alive() for t in th), "a rank did not finish"
+        assert not errs, errs
+        return Ds, out
+    finally:
+        torch.cuda.synchronize()
+        Ds = None
+        group.close()
+
+
+@pytest.mark.parametrize("world,K", [(2, 1), (2, None), (3, 2), (5, 1), (8, 1), (8, 2), (8, None)])
+def test_loopback_distributed_cycle_bitwise(setup, world, K):
+    import torch
+    A, H = setup
+    n = A.shape[0]
+    x0 = np.random.RandomState(0).randn(n)
+    b = np.random.RandomState(1).randn(n)
+    xd = torch.as_tensor(x0).cuda()
+    h_ref = H.cycle(torch.as_tensor(b).cuda(), xd, 6, use_graph=False)
+    x_ref = xd.cpu().numpy()
+    Ds, out = _run(A, H, world, 0, b=b, x0=x0, K=K)
+    assert Ds[0].K == (K or len(H.levels))
+    for D, (x_own, h) in zip(Ds, out):
+        assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank} of {world}, K={D.K}"
+        np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
+
+
+def test_loopback_tolerance_stop(setup):
+    import torch
+    A, H = setup
+    n = A.shape[0]
+    b = np.random.RandomState(2).randn(n)
+    x0 = np.zeros(n)
+    tol = 1e-6 * float(np.linalg.norm(b))
+    xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    h_ref = H.cycle(torch.as_tensor(b).cuda(), xd, 50, tol=tol, use_graph=False)
+    Ds, out = _run(A, H, 4, 0, ncyc=50, tol=tol, b=b, x0=x0)
+    for D, (x_own, h) in zip(Ds, out):
+        assert len(h) == len(h_ref) < 50  # every rank stops after the same cycle
+        assert np.array_equal(x_own, xd.cpu().numpy()[D.lo:D.hi])
+
+
+def test_loopback_refuses_graph_capture(setup):
+    import torch
+    from mlamg import _lib
+    from mlamg.distributed import DistributedHierarchy, LoopbackGroup
+    A, H = setup
+    group = LoopbackGroup(1)
+    try:
+        D = DistributedHierarchy(H, group.comms[0], min_rows=0, A_host=A)
+        D.set_cycle_graph(True)
+        xe = D.new_x(torch.zeros(A.shape[0], dtype=torch.float64))
+        with pytest.raises(_lib.MlamgError):
+            D.cycle(torch.zeros(A.shape[0], dtype=torch.float64, device="cuda"), xe, 2)
+        del D
+    finally:
+        group.close()
