@@ -117,3 +117,29 @@ def test_loopback_refuses_graph_capture(setup):
         del D
     finally:
         group.close()
+
+
+@pytest.mark.slow
+def test_loopback_c4_world8_bench_partition():
+    """The bench's own configuration at world 8 (C4 216^3, levels with >= 50,000 rows
+    partitioned, per-rank autotuned local kernels), eager loopback cycles: every rank's
+    iterate bitwise the single-GPU iterate after 3 cycles."""
+    import torch
+    from mlamg import problems
+    from mlamg.hierarchy import Hierarchy
+    A = problems.poisson_3d_7pt(216)
+    H = Hierarchy.build(A, alpha=0.1, strength_mode="invabs", max_coarse=2000)
+    n = A.shape[0]
+    x0 = np.random.RandomState(0).randn(n)
+    x0 /= np.linalg.norm(x0)
+    b = np.zeros(n)
+    xd = torch.as_tensor(x0).cuda()
+    h_ref = H.cycle(torch.zeros(n, dtype=torch.float64, device="cuda"), xd, 3, use_graph=True)
+    x_ref = xd.cpu().numpy()
+    del xd
+    Ds, out = _run(A, H, 8, 50000, ncyc=3, b=b, x0=x0)
+    assert Ds[0].K == 3
+    assert Ds[0].tuning[0]["chosen"].startswith("rowpat")  # fine local operator stays rowpat
+    for D, (x_own, h) in zip(Ds, out):
+        assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank}"
+        np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
