@@ -143,3 +143,28 @@ def test_loopback_c4_world8_bench_partition():
     for D, (x_own, h) in zip(Ds, out):
         assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank}"
         np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("world", (6, 8))
+def test_loopback_ranks_with_empty_coarse_parts(world):
+    """A problem so small that coarse levels have fewer rows than ranks: some ranks own no rows
+    (or no coarse segment) on a partitioned level; empty halos, packs and operators must still
+    line up, and every rank's iterate stays bitwise."""
+    import torch
+    from mlamg import problems
+    from mlamg.hierarchy import Hierarchy
+    A = problems.poisson_3d_7pt(12)
+    H = Hierarchy.build(A, alpha=0.1, max_coarse=10)
+    n = A.shape[0]
+    x0 = np.random.RandomState(5).randn(n)
+    b = np.random.RandomState(6).randn(n)
+    xd = torch.as_tensor(x0).cuda()
+    h_ref = H.cycle(torch.as_tensor(b).cuda(), xd, 4, use_graph=False)
+    x_ref = xd.cpu().numpy()
+    Ds, out = _run(A, H, world, 0, ncyc=4, b=b, x0=x0)
+    sizes = [[p["hi"] - p["lo"] for p in D.parts] for D in Ds]
+    segs = [int(D.c_hi[D.comm.rank] - D.c_lo[D.comm.rank]) for D in Ds]
+    assert min(min(s) for s in sizes) == 0 or min(segs) == 0, (sizes, segs)
+    for D, (x_own, h) in zip(Ds, out):
+        assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank}: {sizes}, {segs}"
+        np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
