@@ -706,7 +706,8 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
   MLAMG_TRY(jacobi_sweep(A, L.dinv, b, x_ext, L.t_ext, false, done, s));
   MLAMG_TRY(halo_exchange_impl(L.hx, L.t_ext, s));
   // r = b - A t with per-block ||r||^2 partials, x <- t; then the global norm
-  MLAMG_TRY(residual_partials(A, b, L.t_ext, L.r_ext, x_ext, L.t_ext, D->partial, done, s,
+  // (r itself is not stored: the next cycle starts with its own residual)
+  MLAMG_TRY(residual_partials(A, b, L.t_ext, nullptr, x_ext, L.t_ext, D->partial, done, s,
                               L.dinv));
   const int nb = (int)A->n_part;
   hipLaunchKernelGGL(k_local_sum, dim3(1), dim3(1024), 0, s, D->partial, nb);

@@ -234,7 +234,9 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
     MLAMG_TRY(norm_hist_impl(x, L.n, H->partial, hist, counter, done, tol, s));
     return MLAMG_OK;
   }
-  MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, hist, counter, done, tol,
+  // fused: nothing reads this r (the next cycle starts with its own residual), so it is not
+  // stored — the kernel still forms it for the norm and the fused sweep x = t + Dinv_w r
+  MLAMG_TRY(residual_impl(L.A, b, cur, fused ? nullptr : L.r, nullptr, hist, counter, done, tol,
                           cur != x ? x : nullptr, cur != x ? cur : nullptr, H->partial, s,
                           fused ? L.dinv : nullptr));
   return MLAMG_OK;
@@ -426,7 +428,8 @@ int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes) {
     t += spmv_bytes(L.P) + 8.0 * n;  // + read x before the add
     t += H->nu_post * jac;
     // end-of-cycle residual norm, + x = t (read t, write x) or, fused, x = t + Dinv_w r
-    if (l == 0) t += res + (fused ? 24.0 * n : ((H->nu_post & 1) ? 16.0 * n : 0.0));
+    // (fused: + read t, dinv, write x; r itself is not stored)
+    if (l == 0) t += res + (fused ? 16.0 * n : ((H->nu_post & 1) ? 16.0 * n : 0.0));
   }
   if (H->D) t += 8.0 * H->D->n * H->D->n + 16.0 * H->D->n;
   *bytes = t;

@@ -80,7 +80,7 @@ __device__ __forceinline__ double epi_store(int row, double s, const EpiIn& v, c
     return 0.0;
   } else if constexpr (OP == EPI_RESID) {
     const double r = v.a - s;
-    e.y[row] = r;
+    if (e.y) e.y[row] = r;  // NULL: r is only needed for the norm and the fused sweep
     // optional copy-back of the iterate; with dinv also the next cycle's first Jacobi sweep
     // x + dinv*r, fused here (same two roundings as the stand-alone sweep)
     if (e.copy_to) e.copy_to[row] = e.dinv ? v.b + v.c * r : v.b;
@@ -469,7 +469,7 @@ __device__ __forceinline__ double epi_store2(int r, bool both, double s0, double
   double c0 = 0.0, c1 = 0.0, q0 = 0.0, q1 = 0.0;
   const double y0 = epi_value<OP>(s0, u, e, c0, q0);
   const double y1 = epi_value<OP>(s1, w, e, c1, q1);
-  st2(e.y, r, both, y0, y1);
+  if (OP != EPI_RESID || e.y) st2(e.y, r, both, y0, y1);
   if constexpr (OP == EPI_AXPBY || OP == EPI_RESID)
     if (e.copy_to) st2(e.copy_to, r, both, c0, c1);
   return both ? q0 + q1 : q0;
