@@ -16,6 +16,17 @@ struct mlamg_gs {
   std::vector<int32_t> level_ptr;  // host
   int32_t* d_level_ptr = nullptr;  // device copy
   int32_t* rows = nullptr;         // device, rows grouped by level (ascending within a level)
+  // level-ordered copy for the pipelined one-workgroup sweep (k_gs_pipe): position p = the p-th
+  // row of `rows`; its off-diagonal entries in stored order in slots pk_col/pk_val[p*K .. p*K+K)
+  // (column -1 pads), its diagonal (the last stored one, as the sequential sweep takes it; 0.0
+  // when absent) in pk_diag[p]; b_lvl[p] = b[rows[p]] is refreshed per sweep. Every load of a
+  // level's structure is then independent of the others. Snapshot of A at mlamg_gs_create.
+  int32_t pk_k = 0;  // slots per row (4 or 8), 0 = no packed copy
+  int32_t* pk_col = nullptr;
+  double* pk_val = nullptr;
+  double* pk_diag = nullptr;
+  double* b_lvl = nullptr;
+  int32_t max_off = 0;  // longest off-diagonal count
 };
 
 namespace mlamg {
@@ -69,13 +80,118 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_block(const int32_t* __restrict
   }
 }
 
+// Pipelined one-workgroup sweep for narrow schedules (every level <= R * 1024 rows, every row
+// <= K = 4 or 8 off-diagonals): the level-ordered structure (row id, diagonal, b, columns,
+// values) of level l+1 is loaded while level l computes, so a level's critical path is only
+// its x gathers (which depend on the level before), the ordered sum, the store and the barrier.
+// Same products, same order, same division as gs_row: bitwise the sequential sweep.
+template <int R, int K>
+struct GsRows {
+  int32_t row[R];
+  double diag[R], bi[R];
+  int32_t col[R][K];
+  double val[R][K];
+};
+
+// position p's structure: independent loads only (no pointer chasing), one round trip
+template <int R, int K>
+__device__ __forceinline__ void gs_pipe_load(GsRows<R, K>& q, int32_t a, int32_t z,
+                                             const int32_t* __restrict__ rows,
+                                             const int32_t* __restrict__ pcol,
+                                             const double* __restrict__ pval,
+                                             const double* __restrict__ pdiag,
+                                             const double* __restrict__ blvl) {
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    const int32_t p = a + (int32_t)threadIdx.x + u * kGsBlock;
+    const bool ok = p < z;
+    q.row[u] = ok ? rows[p] : -1;
+    q.diag[u] = ok ? pdiag[p] : 0.0;
+    q.bi[u] = ok ? blvl[p] : 0.0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      q.col[u][k] = ok ? pcol[(int64_t)p * K + k] : -1;
+      q.val[u][k] = ok ? pval[(int64_t)p * K + k] : 0.0;
+    }
+  }
+}
+
+template <int R, int K>
+__global__ __launch_bounds__(kGsBlock) void k_gs_pipe(const int32_t* __restrict__ rows,
+                                                      const int32_t* __restrict__ lptr,
+                                                      int32_t n_levels,
+                                                      const int32_t* __restrict__ pcol,
+                                                      const double* __restrict__ pval,
+                                                      const double* __restrict__ pdiag,
+                                                      const double* __restrict__ blvl,
+                                                      int iterations, double* x,
+                                                      const int32_t* done) {
+  if (done && *done) return;
+  for (int it = 0; it < iterations; ++it) {
+    GsRows<R, K> cur;
+    gs_pipe_load<R, K>(cur, lptr[0], lptr[1], rows, pcol, pval, pdiag, blvl);
+    for (int32_t l = 0; l < n_levels; ++l) {
+      // this level's x gathers first (they read the previous level's updates) ...
+      double xv[R][K];
+#pragma unroll
+      for (int u = 0; u < R; ++u)
+#pragma unroll
+        for (int k = 0; k < K; ++k) xv[u][k] = cur.col[u][k] >= 0 ? x[cur.col[u][k]] : 0.0;
+      // ... then the next level's structure (independent of x) in flight meanwhile
+      GsRows<R, K> nxt;
+      if (l + 1 < n_levels)
+        gs_pipe_load<R, K>(nxt, lptr[l + 1], lptr[l + 2], rows, pcol, pval, pdiag, blvl);
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        if (cur.row[u] < 0) continue;
+        double rsum = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (cur.col[u][k] >= 0) rsum += cur.val[u][k] * xv[u][k];
+        if (cur.diag[u] != 0.0) x[cur.row[u]] = (cur.bi[u] - rsum) / cur.diag[u];
+      }
+      __syncthreads();
+      if (l + 1 < n_levels) cur = nxt;
+    }
+  }
+}
+
+__global__ void k_gs_b_level(const int32_t* __restrict__ rows, int64_t n,
+                             const double* __restrict__ b, double* __restrict__ blvl,
+                             const int32_t* done) {
+  if (done && *done) return;
+  const int64_t p = blockIdx.x * 256ll + threadIdx.x;
+  if (p < n) blvl[p] = b[rows[p]];
+}
+
+template <int R, int K>
+static void launch_gs_pipe(const mlamg_gs* G, double* x, const double* b, int iterations,
+                           const int32_t* done, hipStream_t s) {
+  const int64_t n = G->A->n_rows;
+  hipLaunchKernelGGL(k_gs_b_level, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
+                     n, b, G->b_lvl, done);
+  hipLaunchKernelGGL((k_gs_pipe<R, K>), dim3(1), dim3(kGsBlock), 0, s, G->rows, G->d_level_ptr,
+                     G->n_levels, G->pk_col, G->pk_val, G->pk_diag, G->b_lvl, iterations, x,
+                     done);
+}
+
 int64_t gs_rows(const mlamg_gs* G) { return G->A->n_rows; }
 
 int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
                   const int32_t* done, hipStream_t s) {
   const mlamg_csr* A = G->A;
   if (A->n_rows == 0 || iterations <= 0) return MLAMG_OK;
-  if (G->max_level_rows <= kGsBlockMaxLevelRows && G->n_levels > 4) {
+  const bool pipe = G->pk_k > 0 && G->n_levels > 4;
+  if (pipe && G->max_level_rows <= 2 * kGsBlock) {
+    const bool one = G->max_level_rows <= kGsBlock;
+    if (G->pk_k == 4) {
+      if (one) launch_gs_pipe<1, 4>(G, x, b, iterations, done, s);
+      else launch_gs_pipe<2, 4>(G, x, b, iterations, done, s);
+    } else {
+      if (one) launch_gs_pipe<1, 8>(G, x, b, iterations, done, s);
+      else launch_gs_pipe<2, 8>(G, x, b, iterations, done, s);
+    }
+  } else if (G->max_level_rows <= kGsBlockMaxLevelRows && G->n_levels > 4) {
     hipLaunchKernelGGL(k_gs_block, dim3(1), dim3(kGsBlock), 0, s, A->indptr, A->indices, A->data,
                        G->rows, G->d_level_ptr, G->n_levels, iterations, x, b, done);
   } else {
@@ -146,14 +262,63 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
   }
   (void)hipMemcpy(G->d_level_ptr, G->level_ptr.data(), sizeof(int32_t) * (nlev + 1),
                   hipMemcpyHostToDevice);
+  // level-ordered packed copy for k_gs_pipe (rows with <= 8 off-diagonals)
+  {
+    int32_t mo = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      int32_t c = 0;
+      for (int k = ip[i]; k < ip[i + 1]; ++k) c += ij[k] != i;
+      mo = std::max(mo, c);
+    }
+    G->max_off = mo;
+    const int K = mo <= 4 ? 4 : (mo <= 8 ? 8 : 0);
+    if (K) {
+      std::vector<double> ax(A->nnz);
+      if (A->nnz)
+        MLAMG_HIP(hipMemcpy(ax.data(), A->data, sizeof(double) * A->nnz, hipMemcpyDeviceToHost));
+      std::vector<int32_t> pcol((size_t)n * K, -1);
+      std::vector<double> pval((size_t)n * K, 0.0), pdiag(n, 0.0);
+      for (int64_t p = 0; p < n; ++p) {
+        const int32_t i = rows[p];
+        int c = 0;
+        for (int k = ip[i]; k < ip[i + 1]; ++k) {
+          if (ij[k] == i) {
+            pdiag[p] = ax[k];  // the last stored diagonal entry counts, as in the sweep
+          } else {
+            pcol[(size_t)p * K + c] = ij[k];
+            pval[(size_t)p * K + c] = ax[k];
+            ++c;
+          }
+        }
+      }
+      const size_t m = std::max<size_t>((size_t)n * K, 1), nn = std::max<int64_t>(n, 1);
+      if (hipMalloc(&G->pk_col, sizeof(int32_t) * m) == hipSuccess &&
+          hipMalloc(&G->pk_val, sizeof(double) * m) == hipSuccess &&
+          hipMalloc(&G->pk_diag, sizeof(double) * nn) == hipSuccess &&
+          hipMalloc(&G->b_lvl, sizeof(double) * nn) == hipSuccess) {
+        if (n) {
+          (void)hipMemcpy(G->pk_col, pcol.data(), sizeof(int32_t) * n * K, hipMemcpyHostToDevice);
+          (void)hipMemcpy(G->pk_val, pval.data(), sizeof(double) * n * K, hipMemcpyHostToDevice);
+          (void)hipMemcpy(G->pk_diag, pdiag.data(), sizeof(double) * n, hipMemcpyHostToDevice);
+        }
+        G->pk_k = K;
+      } else {  // optional: the sweep falls back to the plain kernels
+        for (void* q : {(void*)G->pk_col, (void*)G->pk_val, (void*)G->pk_diag, (void*)G->b_lvl})
+          if (q) (void)hipFree(q);
+        G->pk_col = nullptr;
+        G->pk_val = G->pk_diag = G->b_lvl = nullptr;
+      }
+    }
+  }
   *out = G;
   return MLAMG_OK;
 }
 
 int mlamg_gs_destroy(mlamg_gs* G) {
   if (G) {
-    if (G->rows) (void)hipFree(G->rows);
-    if (G->d_level_ptr) (void)hipFree(G->d_level_ptr);
+    for (void* q : {(void*)G->rows, (void*)G->d_level_ptr, (void*)G->pk_col, (void*)G->pk_val,
+                    (void*)G->pk_diag, (void*)G->b_lvl})
+      if (q) (void)hipFree(q);
     delete G;
   }
   return MLAMG_OK;

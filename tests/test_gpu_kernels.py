@@ -300,24 +300,59 @@ def _P1(golden):
                          shape=(1024, 342))
 
 
-@pytest.mark.parametrize("case", ("wide_levels", "grid_200"))
-def test_gauss_seidel_both_schedules(ml, oracle, case):
-    """Level-scheduled GS through the one-workgroup kernel (narrow levels) and the per-level
-    launches (a level wider than 8192 rows), bitwise the sequential pyamg sweep."""
+@pytest.mark.parametrize("case", ("wide_levels", "grid_200", "grid_1100", "cube_24",
+                                  "long_rows", "unsorted_zero_diag"))
+def test_gauss_seidel_both_schedules(ml, oracle, torch_cuda, case):
+    """Level-scheduled GS through every schedule: the pipelined one-workgroup kernel (levels of
+    <= 1024 rows: grid_200; <= 2048: grid_1100 diagonals; cube_24 planes), the plain
+    one-workgroup kernel (rows with more than 8 off-diagonals), the per-level launches (a level
+    wider than 8192 rows) — bitwise the sequential pyamg sweep, including rows stored in
+    non-ascending order, a zero diagonal (row left unchanged) and a duplicated diagonal entry."""
     rs = np.random.RandomState(11)
     if case == "wide_levels":
         n = 30000  # diagonal + a sparse upper band: a few levels of ~10^4 independent rows
         U = sp.random(n, n, density=2e-5, random_state=rs, format="csr")
         A = (sp.eye(n) * 4.0 + sp.triu(U, k=1) - sp.triu(U, k=1).T).tocsr()
-    else:
+    elif case == "grid_200":
         A = ml.problems.poisson_2d_5pt(200)
-    A.sort_indices()
+    elif case == "grid_1100":  # anti-diagonal levels of up to 1100 rows
+        A = ml.problems.poisson_2d_5pt(1100)
+    elif case == "cube_24":
+        A = ml.problems.poisson_3d_7pt(24)
+    elif case == "long_rows":  # 9-point-like rows with up to 12 off-diagonals
+        m = 60
+        T = sp.diags([1.0, 1.0, 1.0, 1.0, 1.0], [-2, -1, 0, 1, 2], shape=(m, m))
+        A = (sp.kron(T, T) * -0.1 + sp.eye(m * m) * 4.0).tocsr()
+    else:
+        A = ml.problems.poisson_2d_5pt(64).tolil()
+        A[100, 100] = 0.0  # zero diagonal: that row is skipped
+        A = A.tocsr()
+        A.sort_indices()
+        ip, ij, ax = A.indptr.copy(), A.indices.copy(), A.data.copy()
+        for r in range(0, A.shape[0], 3):  # reverse the stored order of every third row
+            ij[ip[r]:ip[r + 1]] = ij[ip[r]:ip[r + 1]][::-1].copy()
+            ax[ip[r]:ip[r + 1]] = ax[ip[r]:ip[r + 1]][::-1].copy()
+        # row 7 stores its diagonal twice (the last one counts)
+        r7 = slice(ip[7], ip[8])
+        ij7, ax7 = list(ij[r7]), list(ax[r7])
+        ij = np.concatenate([ij[:ip[8]], [7], ij[ip[8]:]]).astype(np.int32)
+        ax = np.concatenate([ax[:ip[8]], [5.0], ax[ip[8]:]])
+        ip = ip.copy()
+        ip[8:] += 1
+        A = sp.csr_matrix((ax, ij, ip), shape=A.shape)
+    if case not in ("unsorted_zero_diag",):
+        A.sort_indices()
     b = rs.randn(A.shape[0])
     x0 = rs.randn(A.shape[0])
-    gs = ml.multigrid.GaussSeidel(ml.sparse.as_device(A))
+    # stored rows as they are (duplicates included: pyamg takes the last diagonal entry)
+    gs = ml.multigrid.GaussSeidel(ml.sparse.DeviceCSR.from_scipy(A, check=False))
     ref = oracle.gauss_seidel(A, x0.copy(), b, iterations=3)
-    got = ml.multigrid.gauss_seidel(A, b, x0.copy(), nu=3)
+    xd = torch_cuda.as_tensor(x0.copy()).cuda()
+    gs.sweep(xd, torch_cuda.as_tensor(b).cuda(), 3)
+    got = xd.cpu().numpy()
     assert np.array_equal(got, ref), (case, gs.n_levels)
+    if case != "unsorted_zero_diag":  # the reference-facing entry point
+        assert np.array_equal(ml.multigrid.gauss_seidel(A, b, x0.copy(), nu=3), ref)
 
 
 def test_amg_2_v_gauss_seidel(golden, ml):
