@@ -361,6 +361,7 @@ struct mlamg_dhier {
   double* g_hist = nullptr;
   double g_tol = -1.0;
   uint64_t g_epoch = 0;
+  int32_t* done_host = nullptr;  // pinned copy of the stop flag (run_cycles)
 };
 
 static void dhier_free_graph(mlamg_dhier* D) {
@@ -571,6 +572,7 @@ int mlamg_dhier_destroy(mlamg_dhier* D) {
   if (D) {
     dhier_free_graph(D);
     if (D->cap_stream) (void)hipStreamDestroy(D->cap_stream);
+    if (D->done_host) (void)hipHostFree(D->done_host);
     for (void* p : D->bufs)
       if (p) (void)hipFree(p);
     delete D;
@@ -773,9 +775,17 @@ int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cyc
         D->g_tol = tol;
         D->g_epoch = format_epoch();
       }
-      for (int c = c0; c < n_cycles; ++c) MLAMG_HIP(hipGraphLaunch(D->exec, s));
+      if (!D->done_host) (void)hipHostMalloc(&D->done_host, sizeof(int32_t), hipHostMallocDefault);
+      MLAMG_TRY(run_cycles(n_cycles - c0, tol, D->flags + 1, D->done_host, s, [&]() -> int {
+        MLAMG_HIP(hipGraphLaunch(D->exec, s));
+        return MLAMG_OK;
+      }));
     } else {
-      for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(dcycle(D, b, x_ext, res_hist, tol, s));
+      // every rank reads the same flag (set from the all-reduced norm) after the same batch,
+      // so all ranks launch the same number of cycles and their collectives stay matched
+      if (!D->done_host) (void)hipHostMalloc(&D->done_host, sizeof(int32_t), hipHostMallocDefault);
+      MLAMG_TRY(run_cycles(n_cycles, tol, D->flags + 1, D->done_host, s,
+                           [&]() { return dcycle(D, b, x_ext, res_hist, tol, s); }));
     }
     // the iterate is t; x holds t + Dinv_w r for a cycle that never ran
     MLAMG_HIP(hipMemcpyAsync(x_ext, L.t_ext, sizeof(double) * L.n_own, hipMemcpyDeviceToDevice, s));

@@ -221,4 +221,28 @@ int norm_hist_impl(const double* x, int64_t n, double* partial, double* hist, in
                    int32_t* done, double tol, hipStream_t s);
 int count_out_of_range(const int32_t* a, int64_t n, int64_t lo, int64_t hi, hipStream_t s,
                        int64_t* bad_out);
+// Cycles are launched in batches; with a tolerance, the device-side stop flag is read back
+// after each batch so the cycles after convergence are not launched at all (each would only
+// check the flag and return, ~10 launches apiece). Batches grow 4, 4, 8, 16, 32, 32, ...: at
+// most one batch of overshoot, a host sync per batch.
+template <class F>
+static int run_cycles(int n_cycles, double tol, int32_t* done_dev, int32_t* done_host,
+                      hipStream_t s, F&& one) {
+  if (!(tol > 0.0) || !done_host) {
+    for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(one());
+    return MLAMG_OK;
+  }
+  int c = 0, batch = 4, k = 0;
+  while (c < n_cycles) {
+    const int m = std::min(batch, n_cycles - c);
+    for (int i = 0; i < m; ++i) MLAMG_TRY(one());
+    c += m;
+    if (c >= n_cycles) break;
+    MLAMG_HIP(hipMemcpyAsync(done_host, done_dev, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipStreamSynchronize(s));
+    if (*done_host) break;
+    if (++k >= 2) batch = std::min(batch * 2, 32);
+  }
+  return MLAMG_OK;
+}
 }  // namespace mlamg

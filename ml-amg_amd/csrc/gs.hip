@@ -156,6 +156,49 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_pipe(const int32_t* __restrict_
   }
 }
 
+// Small systems (n <= kGsLdsMax): the same pipelined walk with x held in LDS for the whole sweep
+// (x loaded once, written back once): a level's gathers and its updates are LDS accesses, so a
+// level costs an LDS round trip and a barrier instead of a global-memory round trip.
+constexpr int kGsLdsMax = 8192;  // 64 KB of x: within the default dynamic-LDS limit
+
+template <int K>
+__global__ __launch_bounds__(kGsBlock) void k_gs_lds(const int32_t* __restrict__ rows,
+                                                     const int32_t* __restrict__ lptr,
+                                                     int32_t n_levels, int64_t n,
+                                                     const int32_t* __restrict__ pcol,
+                                                     const double* __restrict__ pval,
+                                                     const double* __restrict__ pdiag,
+                                                     const double* __restrict__ blvl,
+                                                     int iterations, double* x,
+                                                     const int32_t* done) {
+  extern __shared__ double xs[];
+  if (done && *done) return;
+  for (int64_t i = threadIdx.x; i < n; i += kGsBlock) xs[i] = x[i];
+  __syncthreads();
+  for (int it = 0; it < iterations; ++it) {
+    GsRows<1, K> cur;
+    gs_pipe_load<1, K>(cur, lptr[0], lptr[1], rows, pcol, pval, pdiag, blvl);
+    for (int32_t l = 0; l < n_levels; ++l) {
+      GsRows<1, K> nxt;
+      if (l + 1 < n_levels)
+        gs_pipe_load<1, K>(nxt, lptr[l + 1], lptr[l + 2], rows, pcol, pval, pdiag, blvl);
+      if (cur.row[0] >= 0) {
+        double xv[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) xv[k] = cur.col[0][k] >= 0 ? xs[cur.col[0][k]] : 0.0;
+        double rsum = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (cur.col[0][k] >= 0) rsum += cur.val[0][k] * xv[k];
+        if (cur.diag[0] != 0.0) xs[cur.row[0]] = (cur.bi[0] - rsum) / cur.diag[0];
+      }
+      __syncthreads();
+      if (l + 1 < n_levels) cur = nxt;
+    }
+  }
+  for (int64_t i = threadIdx.x; i < n; i += kGsBlock) x[i] = xs[i];
+}
+
 __global__ void k_gs_b_level(const int32_t* __restrict__ rows, int64_t n,
                              const double* __restrict__ b, double* __restrict__ blvl,
                              const int32_t* done) {
@@ -164,12 +207,24 @@ __global__ void k_gs_b_level(const int32_t* __restrict__ rows, int64_t n,
   if (p < n) blvl[p] = b[rows[p]];
 }
 
+// MLAMG_GS_NO_LDS=1 keeps small systems on the global-memory kernel (A/B runs, tests)
+static bool gs_lds_disabled() {
+  const char* e = std::getenv("MLAMG_GS_NO_LDS");
+  return e && e[0] == '1';
+}
+
 template <int R, int K>
 static void launch_gs_pipe(const mlamg_gs* G, double* x, const double* b, int iterations,
                            const int32_t* done, hipStream_t s) {
   const int64_t n = G->A->n_rows;
   hipLaunchKernelGGL(k_gs_b_level, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
                      n, b, G->b_lvl, done);
+  if (R == 1 && n <= kGsLdsMax && !gs_lds_disabled()) {
+    hipLaunchKernelGGL((k_gs_lds<K>), dim3(1), dim3(kGsBlock), sizeof(double) * n, s, G->rows,
+                       G->d_level_ptr, G->n_levels, n, G->pk_col, G->pk_val, G->pk_diag,
+                       G->b_lvl, iterations, x, done);
+    return;
+  }
   hipLaunchKernelGGL((k_gs_pipe<R, K>), dim3(1), dim3(kGsBlock), 0, s, G->rows, G->d_level_ptr,
                      G->n_levels, G->pk_col, G->pk_val, G->pk_diag, G->b_lvl, iterations, x,
                      done);

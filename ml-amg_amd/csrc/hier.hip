@@ -59,7 +59,9 @@ struct mlamg_hier {
   const double* cg_b = nullptr;
   uint64_t g_epoch = 0, cg_epoch = 0;
   double* cg_res = nullptr;
+  int32_t* done_host = nullptr;  // pinned copy of flags[1], polled between batches of cycles
 };
+
 
 using namespace mlamg;
 
@@ -293,6 +295,7 @@ int mlamg_hier_destroy(mlamg_hier* H) {
   hier_free_graph(H);
   if (H->cap_stream) (void)hipStreamDestroy(H->cap_stream);
   if (H->mem) (void)hipFree(H->mem);
+  if (H->done_host) (void)hipHostFree(H->done_host);
   delete H;
   return MLAMG_OK;
 }
@@ -388,9 +391,15 @@ int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, d
       H->g_tol = tol;
       H->g_epoch = format_epoch();
     }
-    for (int c = 0; c < n_cycles; ++c) MLAMG_HIP(hipGraphLaunch(H->exec, s));
+    if (!H->done_host) (void)hipHostMalloc(&H->done_host, sizeof(int32_t), hipHostMallocDefault);
+    MLAMG_TRY(run_cycles(n_cycles, tol, H->flags + 1, H->done_host, s, [&]() -> int {
+      MLAMG_HIP(hipGraphLaunch(H->exec, s));
+      return MLAMG_OK;
+    }));
   } else {
-    for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(cycle_top(H, b, x, res_hist, tol, s));
+    if (!H->done_host) (void)hipHostMalloc(&H->done_host, sizeof(int32_t), hipHostMallocDefault);
+    MLAMG_TRY(run_cycles(n_cycles, tol, H->flags + 1, H->done_host, s,
+                         [&]() { return cycle_top(H, b, x, res_hist, tol, s); }));
   }
   if (fused)  // the iterate is t (in tmp); x holds t + Dinv_w r for a cycle that never ran
     MLAMG_HIP(hipMemcpyAsync(x, H->lv[0].tmp, sizeof(double) * H->lv[0].n,

@@ -301,7 +301,7 @@ def _P1(golden):
 
 
 @pytest.mark.parametrize("case", ("wide_levels", "grid_200", "grid_1100", "cube_24",
-                                  "long_rows", "unsorted_zero_diag"))
+                                  "long_rows", "unsorted_zero_diag", "grid_60_lds", "cube_12_lds"))
 def test_gauss_seidel_both_schedules(ml, oracle, torch_cuda, case):
     """Level-scheduled GS through every schedule: the pipelined one-workgroup kernel (levels of
     <= 1024 rows: grid_200; <= 2048: grid_1100 diagonals; cube_24 planes), the plain
@@ -319,6 +319,10 @@ def test_gauss_seidel_both_schedules(ml, oracle, torch_cuda, case):
         A = ml.problems.poisson_2d_5pt(1100)
     elif case == "cube_24":
         A = ml.problems.poisson_3d_7pt(24)
+    elif case == "grid_60_lds":  # n <= 8192: x held in LDS for the whole sweep
+        A = ml.problems.poisson_2d_5pt(60)
+    elif case == "cube_12_lds":
+        A = ml.problems.poisson_3d_7pt(12)
     elif case == "long_rows":  # 9-point-like rows with up to 12 off-diagonals
         m = 60
         T = sp.diags([1.0, 1.0, 1.0, 1.0, 1.0], [-2, -1, 0, 1, 2], shape=(m, m))
