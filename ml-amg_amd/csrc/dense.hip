@@ -16,9 +16,13 @@ __global__ void k_densify(const int32_t* __restrict__ ip, const int32_t* __restr
   for (int k = ip[i]; k < ip[i + 1]; ++k) M[i * n + ij[k]] += ax[k];
 }
 
-// argmax_{i >= k} |M[i][k]| (first index on ties), single workgroup
-__global__ __launch_bounds__(1024) void k_pivot(const double* __restrict__ M, int64_t n, int64_t k,
-                                                int32_t* __restrict__ piv) {
+// One workgroup per step k: argmax_{i >= k} |M[i][k]| (first index on ties), swap rows k and
+// the pivot row, save column k, scale row k by 1/pivot (pivot slot -> 1/pivot); phases separated
+// by workgroup barriers, one launch.
+__global__ __launch_bounds__(1024) void k_gj_row(double* __restrict__ M, int64_t n, int64_t k,
+                                                 int32_t* __restrict__ piv,
+                                                 double* __restrict__ colk,
+                                                 int32_t* __restrict__ fail) {
   __shared__ double bv[1024];
   __shared__ int32_t bi[1024];
   double best = -1.0;
@@ -44,42 +48,39 @@ __global__ __launch_bounds__(1024) void k_pivot(const double* __restrict__ M, in
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    piv[k] = (bv[0] > 0.0) ? bi[0] : -1;
-  }
-}
-
-// swap rows k <-> piv[k], scale row k by 1/pivot (pivot slot -> 1/pivot), save column k
-__global__ void k_swap_scale(double* __restrict__ M, int64_t n, int64_t k,
-                             const int32_t* __restrict__ piv, double* __restrict__ colk,
-                             int32_t* __restrict__ fail) {
-  const int32_t p = piv[k];
+  const int32_t p = (bv[0] > 0.0) ? bi[0] : -1;
+  if (threadIdx.x == 0) piv[k] = p;
   if (p < 0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *fail = 1;
+    if (threadIdx.x == 0) *fail = 1;
     return;
   }
-  // phase A (grid-stride over columns): swap
-  for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < n; j += (int64_t)gridDim.x * 256) {
-    if (p != k) {
+  if (p != k)
+    for (int64_t j = threadIdx.x; j < n; j += 1024) {
       const double t = M[k * n + j];
       M[k * n + j] = M[(int64_t)p * n + j];
       M[(int64_t)p * n + j] = t;
     }
-  }
+  __syncthreads();
+  const double inv = 1.0 / M[k * n + k];
+  for (int64_t j = threadIdx.x; j < n; j += 1024) colk[j] = M[j * n + k];
+  __syncthreads();
+  for (int64_t j = threadIdx.x; j < n; j += 1024)
+    M[k * n + j] = (j == k) ? inv : M[k * n + j] * inv;
 }
 
-__global__ void k_scale_row(double* __restrict__ M, int64_t n, int64_t k,
-                            const int32_t* __restrict__ piv, double* __restrict__ colk) {
-  if (piv[k] < 0) return;
-  const double pv = M[k * n + k];
-  const double inv = 1.0 / pv;
-  for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < n; j += (int64_t)gridDim.x * 256) {
-    colk[j] = M[j * n + k];  // column k before elimination (row k entry is the pivot)
-  }
-  // row scale done in a separate loop after colk read: all threads read col k first
-  __syncthreads();
-  for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < n; j += (int64_t)gridDim.x * 256) {
-    M[k * n + j] = (j == k) ? inv : M[k * n + j] * inv;
+// undo the row interchanges as column interchanges, last to first: one thread per row applies
+// the whole sequence to its own row (one launch instead of one per interchange)
+__global__ void k_unpivot_cols(double* __restrict__ M, int64_t n, const int32_t* __restrict__ piv) {
+  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  double* r = M + i * n;
+  for (int64_t k = n - 1; k >= 0; --k) {
+    const int64_t q = piv[k];
+    if (q != k) {
+      const double t = r[k];
+      r[k] = r[q];
+      r[q] = t;
+    }
   }
 }
 
@@ -93,14 +94,6 @@ __global__ void k_eliminate(double* __restrict__ M, int64_t n, int64_t k,
   const double f = colk[i];
   if (f == 0.0) return;
   M[i * n + j] = (j == k) ? -f * M[k * n + k] : M[i * n + j] - f * M[k * n + j];
-}
-
-__global__ void k_swap_cols(double* __restrict__ M, int64_t n, int64_t a, int64_t b) {
-  int64_t i = blockIdx.x * 256ll + threadIdx.x;
-  if (i >= n) return;
-  const double t = M[i * n + a];
-  M[i * n + a] = M[i * n + b];
-  M[i * n + b] = t;
 }
 
 // x = M b, one wave per row, fixed-order reduction
@@ -178,15 +171,11 @@ int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream) {
                             A->indices, A->data, n, D->inv);
   const unsigned gcols = (unsigned)((n + 255) / 256);
   for (int64_t k = 0; k < n; ++k) {
-    hipLaunchKernelGGL(k_pivot, dim3(1), dim3(1024), 0, s, D->inv, n, k, piv);
-    hipLaunchKernelGGL(k_swap_scale, dim3(gcols), dim3(256), 0, s, D->inv, n, k, piv, colk, fail);
-    hipLaunchKernelGGL(k_scale_row, dim3(1), dim3(256), 0, s, D->inv, n, k, piv, colk);
+    hipLaunchKernelGGL(k_gj_row, dim3(1), dim3(1024), 0, s, D->inv, n, k, piv, colk, fail);
     hipLaunchKernelGGL(k_eliminate, dim3(gcols, (unsigned)n), dim3(256), 0, s, D->inv, n, k, piv,
                        colk);
   }
-  std::vector<int32_t> hpiv(n);
   int32_t hfail = 0;
-  (void)hipMemcpyAsync(hpiv.data(), piv, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s);
   (void)hipMemcpyAsync(&hfail, fail, sizeof(int32_t), hipMemcpyDeviceToHost, s);
   hipError_t e = hipStreamSynchronize(s);
   if (e != hipSuccess || hfail) {
@@ -201,9 +190,7 @@ int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream) {
     return MLAMG_EINVAL;
   }
   // undo the row interchanges as column interchanges, last to first
-  for (int64_t k = n - 1; k >= 0; --k)
-    if (hpiv[k] != k)
-      hipLaunchKernelGGL(k_swap_cols, dim3(gcols), dim3(256), 0, s, D->inv, n, k, (int64_t)hpiv[k]);
+  hipLaunchKernelGGL(k_unpivot_cols, dim3(gcols), dim3(256), 0, s, D->inv, n, piv);
   e = hipStreamSynchronize(s);
   cleanup();
   if (e != hipSuccess) {
