@@ -168,3 +168,25 @@ def test_loopback_ranks_with_empty_coarse_parts(world):
     for D, (x_own, h) in zip(Ds, out):
         assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank}: {sizes}, {segs}"
         np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
+
+
+def test_sync_formats_makes_replicas_bitwise():
+    """What sync_formats does at N > 1: each rank autotunes its own replica of the hierarchy
+    (timings, hence CSR-vector widths, may differ), then applies rank 0's format list; the
+    replicas must then cycle bit for bit alike (the replicated coarse levels rely on it)."""
+    import torch
+    from mlamg import problems
+    from mlamg.hierarchy import Hierarchy
+    A = problems.poisson_3d_7pt(40)
+    H0 = Hierarchy.build(A, alpha=0.1, max_coarse=100)
+    H1 = Hierarchy.build(A, alpha=0.1, max_coarse=100, coarse_format="exact")  # other choices
+    assert H0.formats() != H1.formats()
+    H1.set_formats(H0.formats())
+    assert H1.formats() == H0.formats()
+    n = A.shape[0]
+    x0 = np.random.RandomState(3).randn(n)
+    b = torch.as_tensor(np.random.RandomState(4).randn(n)).cuda()
+    xa, xb = torch.as_tensor(x0).cuda(), torch.as_tensor(x0).cuda()
+    ha = H0.cycle(b, xa, 4)
+    hb = H1.cycle(b, xb, 4)
+    assert torch.equal(xa, xb) and np.array_equal(ha, hb)
