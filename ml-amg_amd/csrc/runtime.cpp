@@ -15,19 +15,28 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 const char* get_error() { return g_last_error.c_str(); }
 
 // ---------------------------------------------------------------- scratch
+// Per host thread: work submitted from different threads (one stream each, e.g. concurrent
+// independent solves) never shares a scratch buffer; calls from one thread are stream-ordered.
 namespace {
 struct Scratch {
   void* p = nullptr;
   size_t bytes = 0;
 };
-std::mutex g_scratch_mu;
-std::vector<std::vector<Scratch>> g_scratch;  // [device][slot]
+struct ScratchCache {
+  std::vector<std::vector<Scratch>> v;  // [device][slot]
+  ~ScratchCache() {
+    for (auto& d : v)
+      for (auto& s : d)
+        if (s.p) (void)hipFree(s.p);
+  }
+};
+thread_local ScratchCache g_scratch_tl;
 }  // namespace
 
 void* scratch(size_t bytes, int slot) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  auto& g_scratch = g_scratch_tl.v;
   if ((int)g_scratch.size() <= dev) g_scratch.resize(dev + 1);
   auto& v = g_scratch[dev];
   if ((int)v.size() <= slot) v.resize(slot + 1);

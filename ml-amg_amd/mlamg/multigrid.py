@@ -264,12 +264,13 @@ def amg_2_v(A, P, b, x,
             error_tol=None,
             max_iter=500,
             singular=False,
-            *, smoother="gauss_seidel"):
+            *, smoother="gauss_seidel", use_graph=True):
     """Two-level AMG solver, ns/lib/multigrid.py:111-210, on the GPU.
 
     smoother='gauss_seidel' (reference default: pyamg forward GS, :175,184) or 'jacobi'
     (weighted Jacobi x += w*Dinv(b - A x) with w = jacobi_weight, the MLAMG.py:143-146 form).
-    Returns (x, conv_factor, err, num_iterations) exactly like the reference.
+    Returns (x, conv_factor, err, num_iterations) exactly like the reference. use_graph=False
+    launches the cycles eagerly instead of replaying a captured hipGraph (same kernels, same bits).
     """
     if res_tol is None and error_tol is None:
         raise RuntimeError('One of res_tol or error_tol must be set!')
@@ -293,8 +294,40 @@ def amg_2_v(A, P, b, x,
         raise
     dev_x = to_device_vec(x).clone()  # x = x.copy()  (:171)
     dev_b = to_device_vec(b)
-    err = H.cycle(dev_b, dev_x, max_iter, tol=tol)  # err[i]; stops after the first e <= tol
+    # err[i]; stops after the first e <= tol
+    err = H.cycle(dev_b, dev_x, max_iter, tol=tol, use_graph=use_graph)
     return dev_x.cpu().numpy(), conv_factor(err), err, len(err)
+
+
+def amg_2_v_batch(problems, workers=8, **kw):
+    """Many independent amg_2_v solves at once on one GPU — the reference's task farm
+    (ns/parallel/pool.py:139-186: one grid per worker process, e.g. utils/evaluate_dataset.py
+    over a dataset) as host threads sharing the device, each on its own HIP stream (the C calls
+    release the GIL; scratch buffers are per thread), so the small latency-bound solves overlap.
+
+    problems: iterable of (A, P, b, x) tuples; keyword arguments as amg_2_v. Returns the list of
+    (x, conv_factor, err, num_iterations) in input order, each equal to a sequential amg_2_v."""
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    dev = torch.cuda.current_device()
+    local = threading.local()
+
+    def run(args):
+        if not hasattr(local, "stream"):
+            torch.cuda.set_device(dev)
+            local.stream = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(local.stream):
+            # eager launches: a stream capture must not overlap the other threads' synchronous
+            # setup calls (allocations, blocking copies), and concurrency already hides launches
+            out = amg_2_v(*args, use_graph=False, **kw)
+        local.stream.synchronize()
+        return out
+
+    problems = list(problems)
+    if workers <= 1 or len(problems) <= 1:
+        return [amg_2_v(*args, **kw) for args in problems]
+    with ThreadPoolExecutor(max_workers=int(workers)) as ex:
+        return list(ex.map(run, problems))
 
 
 def amg_2_v_jacobi(A, P, b, x, dinv_w=None, omega=2. / 3., pre_smoothing_steps=1,
