@@ -95,7 +95,7 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
 #define MLAMG_FMT_SELL_DICT 5
 /* ROWPAT      every row is one of <= 255 distinct patterns (its (col - row, value) sequence in
  *             stored order; C4's 7-point Laplacian: 27 interior/face/edge/corner patterns) held
- *             in LDS tables (<= 4096 entries), one byte per row in HBM: lossless, each row summed
+ *             in LDS tables (<= 2048 padded entries), one byte per row PAIR in HBM: lossless, each row summed
  *             in stored order (scipy's bits). get_format reports the pattern count in
  *             vec_width. EUNSUPPORTED (format unchanged) when the patterns do not fit. */
 #define MLAMG_FMT_ROWPAT 6
@@ -283,6 +283,10 @@ typedef struct mlamg_loop_group mlamg_loop_group;
 int mlamg_loop_group_create(int nranks, mlamg_loop_group** out);
 int mlamg_loop_group_destroy(mlamg_loop_group* g);
 int mlamg_comm_create_loopback(mlamg_loop_group* g, int rank, mlamg_comm** out);
+/* Timing-only communicator: rank `rank` of `nranks` whose exchanges (halos, allgather,
+ * all-reduce) are skipped — ghost values and norms are NOT exchanged, results are invalid. It
+ * measures one rank's device work (kernels, packs) of the distributed cycle on one GPU. */
+int mlamg_comm_create_null(int nranks, int rank, mlamg_comm** out);
 int mlamg_comm_allreduce_sum(mlamg_comm* c, double* buf, int64_t n, void* stream);
 /* ghost layout of one rank: x_ext = [owned n_own | ghosts]; for neighbour q (ascending),
  * send_cnt[q] owned entries (send_idx_host, concatenated) and recv_cnt[q] ghosts, stored

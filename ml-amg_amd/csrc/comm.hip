@@ -63,6 +63,7 @@ struct mlamg_comm {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   mlamg_loop_group* loop = nullptr;  // in-process test transport instead of RCCL
+  bool null_transport = false;       // timing only: exchanges skipped (results are NOT valid)
   struct Recv {
     double* buf;
     size_t n;
@@ -108,11 +109,13 @@ static int loop_wait(mlamg_loop_group* g, std::unique_lock<std::mutex>& lk,
 }
 
 static int xgroup_begin(mlamg_comm* c) {
+  if (c->null_transport) return MLAMG_OK;
   if (!c->loop) MLAMG_NCCL(ncclGroupStart());
   return MLAMG_OK;
 }
 
 static int xsend(mlamg_comm* c, const double* buf, size_t n, int peer, hipStream_t s) {
+  if (c->null_transport) return MLAMG_OK;
   if (!c->loop) {
     MLAMG_NCCL(ncclSend(buf, n, ncclFloat64, peer, c->comm, s));
     return MLAMG_OK;
@@ -134,6 +137,7 @@ static int xsend(mlamg_comm* c, const double* buf, size_t n, int peer, hipStream
 }
 
 static int xrecv(mlamg_comm* c, double* buf, size_t n, int peer, hipStream_t s) {
+  if (c->null_transport) return MLAMG_OK;
   if (!c->loop) {
     MLAMG_NCCL(ncclRecv(buf, n, ncclFloat64, peer, c->comm, s));
     return MLAMG_OK;
@@ -143,6 +147,7 @@ static int xrecv(mlamg_comm* c, double* buf, size_t n, int peer, hipStream_t s) 
 }
 
 static int xgroup_end(mlamg_comm* c, hipStream_t s) {
+  if (c->null_transport) return MLAMG_OK;
   if (!c->loop) {
     MLAMG_NCCL(ncclGroupEnd());
     return MLAMG_OK;
@@ -193,6 +198,7 @@ __global__ void k_loop_sum(const double* __restrict__ stage, int W, int64_t n,
 }
 
 static int xallreduce_sum(mlamg_comm* c, double* buf, size_t n, hipStream_t s) {
+  if (c->null_transport) return MLAMG_OK;
   if (!c->loop) {
     MLAMG_NCCL(ncclAllReduce(buf, buf, n, ncclFloat64, ncclSum, c->comm, s));
     return MLAMG_OK;
@@ -429,6 +435,16 @@ int mlamg_loop_group_destroy(mlamg_loop_group* g) {
     }
     delete g;
   }
+  return MLAMG_OK;
+}
+
+int mlamg_comm_create_null(int nranks, int rank, mlamg_comm** out) {
+  MLAMG_REQUIRE(out && nranks >= 1 && rank >= 0 && rank < nranks, "invalid argument");
+  auto* c = new mlamg_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->null_transport = true;
+  *out = c;
   return MLAMG_OK;
 }
 

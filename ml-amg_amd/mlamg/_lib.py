@@ -108,6 +108,7 @@ SIGNATURES = {
     "mlamg_loop_group_create": (c_int, [c_int, c_vpp]),
     "mlamg_loop_group_destroy": (c_int, [c_vp]),
     "mlamg_comm_create_loopback": (c_int, [c_vp, c_int, c_vpp]),
+    "mlamg_comm_create_null": (c_int, [c_int, c_int, c_vpp]),
     "mlamg_comm_allreduce_sum": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "mlamg_halo_create": (c_int, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vpp]),
     "mlamg_halo_destroy": (c_int, [c_vp]),

@@ -83,6 +83,23 @@ class LoopbackComm:
             self.handle = None
 
 
+class NullComm:
+    """Timing-only communicator (include/mlamg.h mlamg_comm_create_null): rank `rank` of `world`
+    with every exchange skipped, to time one rank's device work of the distributed cycle on a
+    single GPU. Results are not valid."""
+
+    def __init__(self, world, rank):
+        self.world, self.rank = world, rank
+        h = ctypes.c_void_p()
+        call("mlamg_comm_create_null", int(world), int(rank), ctypes.byref(h))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            _lib.lib.mlamg_comm_destroy(self.handle)
+            self.handle = None
+
+
 class Halo:
     def __init__(self, comm, halo: partition.Halo):
         nn = len(halo.neighbors)
