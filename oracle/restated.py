@@ -385,3 +385,84 @@ def vcycle_solve(levels, Ac, b, x, n_cycles, tol=0.0, nu_pre=1, nu_post=1, lu=No
         if tol > 0 and r <= tol:
             break
     return x, np.array(hist)
+
+
+# ---------------------------------------------------------------- parallel CPU baseline
+_OMP = None
+
+
+def omp_lib(threads):
+    """oracle/omp_cycle.c (OpenMP row-parallel kernels), `threads` OpenMP threads."""
+    global _OMP
+    if _OMP is None:
+        path = _build.OUT_OMP if os.path.exists(_build.OUT_OMP) else _build.build_omp()
+        L = ctypes.CDLL(path)
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        L.omp_set_threads.argtypes = [ctypes.c_int]
+        for f in ("omp_resid", "omp_matvec", "omp_add_matvec"):
+            getattr(L, f).argtypes = [i64, vp, vp, vp, vp, vp] + ([vp] if f == "omp_resid" else [])
+        L.omp_jacobi.argtypes = [i64, vp, vp, vp, vp, vp, vp, vp]
+        L.omp_scale.argtypes = [i64, vp, vp, vp]
+        L.omp_gemv.argtypes = [i64, vp, vp, vp]
+        L.omp_norm2.argtypes = [i64, vp]
+        L.omp_norm2.restype = ctypes.c_double
+        _OMP = L
+    _OMP.omp_set_threads(int(threads))
+    return _OMP
+
+
+def vcycle_omp(levels, Ainv, b, x, n_cycles, threads):
+    """BASELINE ONLY: the weighted-Jacobi V(1,1) cycle of the device executor (hier.hip: zero-guess
+    first sweep on coarse levels, explicit R = P^T, dense-inverse coarse solve) with OpenMP
+    row-parallel kernels on `threads` host threads. levels: dicts with CSR "A", "P" and the
+    Jacobi weights "d" (ndarray); Ainv: the coarse inverse (dense ndarray). Returns (x, history)."""
+    L = omp_lib(threads)
+    P_ = _p
+    lv = []
+    for Lv in levels:
+        A = Lv["A"].tocsr()
+        R = Lv["P"].T.tocsr()
+        R.sort_indices()
+        P = Lv["P"].tocsr()
+        n = A.shape[0]
+        lv.append({"n": n, "A": _csr_arrays(A), "R": _csr_arrays(R), "P": _csr_arrays(P),
+                   "nc": P.shape[1], "d": np.ascontiguousarray(Lv["d"], dtype=np.float64),
+                   "x": np.zeros(n), "t": np.zeros(n), "r": np.zeros(n), "b": np.zeros(n)})
+    nc = Ainv.shape[0]
+    Ainv = np.ascontiguousarray(Ainv, dtype=np.float64)
+    xc = np.zeros(nc)
+
+    def csr(M):
+        return P_(M[0]), P_(M[1]), P_(M[2])
+
+    def cycle(l, bvec, x_in):
+        if l == len(lv):
+            L.omp_gemv(nc, P_(Ainv), P_(bvec), P_(xc))
+            return xc
+        v = lv[l]
+        n = v["n"]
+        cur = v["x"] if x_in is None else x_in
+        if x_in is None:
+            L.omp_scale(n, P_(v["d"]), P_(bvec), P_(cur))
+        else:
+            L.omp_jacobi(n, *csr(v["A"]), P_(v["d"]), P_(bvec), P_(cur), P_(v["t"]))
+            cur[:] = v["t"]
+        L.omp_resid(n, *csr(v["A"]), P_(bvec), P_(cur), P_(v["r"]))
+        bn = lv[l + 1]["b"] if l + 1 < len(lv) else np.zeros(nc)
+        L.omp_matvec(v["nc"], *csr(v["R"]), P_(v["r"]), P_(bn))
+        e = cycle(l + 1, bn, None)
+        L.omp_add_matvec(n, *csr(v["P"]), P_(e), P_(cur))
+        L.omp_jacobi(n, *csr(v["A"]), P_(v["d"]), P_(bvec), P_(cur), P_(v["t"]))
+        cur[:] = v["t"]
+        return cur
+
+    x = np.ascontiguousarray(x, dtype=np.float64).copy()
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    hist = []
+    r0 = np.zeros(x.shape[0])
+    A0 = lv[0]["A"]
+    for _ in range(n_cycles):
+        cycle(0, b, x)
+        L.omp_resid(x.shape[0], *csr(A0), P_(b), P_(x), P_(r0))
+        hist.append(L.omp_norm2(x.shape[0], P_(r0)))
+    return x, np.array(hist)

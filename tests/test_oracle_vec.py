@@ -38,3 +38,25 @@ def test_vec_matvec_order(oracle, vw):
     assert np.allclose(y, A @ x, rtol=1e-12, atol=1e-12)
     with pytest.raises(ValueError):
         oracle.vec_matvec(A, x, 1024)
+
+
+def test_omp_baseline_cycle_matches_oracle_cycle():
+    """bench.py's parallel CPU baseline (oracle/omp_cycle.c via restated.vcycle_omp) runs the same
+    cycle as the scipy restatement: histories agree to rounding (dense inverse vs SuperLU coarse
+    solve, parallel norm)."""
+    import numpy as np
+    import scipy.sparse as sp
+    from mlamg import problems
+    from oracle import restated as orc
+    A = problems.poisson_3d_7pt(20)
+    levels, Ac = orc.build_hierarchy(A, alpha=0.1, max_coarse=60)
+    for L in levels:
+        L["Dw"] = orc.mlamg_dinv(L["A"])
+        L["d"] = L["Dw"].diagonal()
+    n = A.shape[0]
+    x0 = np.random.RandomState(0).randn(n)
+    b = np.random.RandomState(1).randn(n)
+    _, h_ref = orc.vcycle_solve(levels, Ac, b, x0, 5)
+    Ainv = np.linalg.inv(Ac.toarray())
+    _, h = orc.vcycle_omp(levels, Ainv, b, x0, 5, threads=4)
+    np.testing.assert_allclose(h, h_ref, rtol=1e-10)
