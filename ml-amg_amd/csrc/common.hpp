@@ -58,8 +58,11 @@ constexpr int kBlockNnz = 2048;   // 16 KiB of fp64 products in LDS per workgrou
 #ifndef MLAMG_SRT_THREADS  // build-time A/B knob (measured: 256 is 2-10 % slower than 512)
 #define MLAMG_SRT_THREADS 512
 #endif
+#ifndef MLAMG_SRT_RPT  // rows per thread in the sorted kernel's phase 2 (2: C4 P0 102 -> 77 us; 1 for A/B)
+#define MLAMG_SRT_RPT 2
+#endif
 constexpr int kSrtThreads = MLAMG_SRT_THREADS;
-constexpr int kSrtRows = MLAMG_SRT_THREADS;
+constexpr int kSrtRows = MLAMG_SRT_THREADS * MLAMG_SRT_RPT;
 constexpr int kSrtNnz = 8 * MLAMG_SRT_THREADS;
 constexpr int kSrtPosBits = 12;
 

@@ -701,9 +701,12 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   // hi (a halo-extended local matrix has its ghost columns far from the owned ones)
   const int lo = base[3 * b], hi = base[3 * b + 1], split = base[3 * b + 2];
   for (int t = tid; t <= nr; t += kSrtThreads) rp[t] = indptr[r0 + t] - e0;
-  static_assert(kSrtRows <= kSrtThreads, "one row per thread in phase 2");
-  EpiIn pre;
-  if (tid < nr) pre = epi_load<OP>(r0 + tid, ep);
+  constexpr int RPT = kSrtRows / kSrtThreads;  // rows per thread in phase 2
+  static_assert(RPT * kSrtThreads == kSrtRows, "whole rows per thread in phase 2");
+  EpiIn pre[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q)
+    if (tid + q * kSrtThreads < nr) pre[q] = epi_load<OP>(r0 + tid + q * kSrtThreads, ep);
   constexpr int U = kSrtNnz / kSrtThreads;
   constexpr uint32_t kNone = 0xffffffffu, kSlot = (1u << kSrtPosBits) - 1;
   uint32_t w[U];
@@ -732,8 +735,10 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
     if (w[u] != kNone) prod[w[u] & kSlot] = vv[u] * xv[u];
   __syncthreads();
   double sq = 0.0;
-  if (tid < nr) {
-    const int t = tid;
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int t = tid + q * kSrtThreads;
+    if (t >= nr) break;
     double s = 0.0;
     const int ka = rp[t], kb = rp[t + 1];
     int k = ka;
@@ -745,7 +750,7 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
       s += p3;
     }
     for (; k < kb; ++k) s += prod[k];
-    sq += epi_store<OP>(r0 + t, s, pre, ep);
+    sq += epi_store<OP>(r0 + t, s, pre[q], ep);
   }
   if constexpr (NORM) {
     double v = wave_sum(sq);
