@@ -256,8 +256,9 @@ int mlamg_hier_set_level_smoother(mlamg_hier* H, int level, const mlamg_gs* gs);
  * 1 = ||x||_2 (amg_2_v error_tol, multigrid.py:193); the tolerance test applies to it */
 int mlamg_hier_set_norm(mlamg_hier* H, int mode);
 /* run n_cycles V-cycles on (b, x) (x updated in place). After each cycle ||b - A x||_2 is
- * written to res_hist[c] (DEVICE, may be NULL). If tol > 0 the cycle loop stops after the first
- * cycle with ||r|| <= tol (MLAMG.py:194); *cycles_done_host (nullable) receives the count and
+ * written to res_hist[c] (DEVICE, may be NULL). If tol >= 0 the cycle loop stops after the
+ * first cycle with ||r|| <= tol (MLAMG.py:194; tol = 0 stops on an exactly zero norm, like the
+ * reference's `e <= tol`); tol < 0 = no tolerance. *cycles_done_host (nullable) receives the count and
  * the call syncs. use_graph != 0 replays one captured hipGraph per cycle. */
 int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, double tol,
                       double* res_hist, int32_t* cycles_done_host, int use_graph, void* stream);

@@ -318,7 +318,7 @@ __global__ void k_norm_finish(const double* __restrict__ sum, double* hist, int3
   const int c = *counter;
   if (hist) hist[c] = nrm;
   *counter = c + 1;
-  if (tol > 0.0 && nrm <= tol) *done = 1;
+  if (tol >= 0.0 && nrm <= tol) *done = 1;
 }
 
 }  // namespace mlamg
@@ -701,7 +701,7 @@ static int dcycle_below(mlamg_dhier* D, size_t l, double** x_out, hipStream_t s)
   // x = Dinv_w b was written by the restriction kernel of the level above (correct())
   MLAMG_TRY(halo_exchange_impl(L.hx, L.x_ext, s));
   MLAMG_TRY(residual_impl(L.A, L.b, L.x_ext, L.r_ext, nullptr, nullptr, nullptr,
-                          const_cast<int32_t*>(done), 0.0, nullptr, nullptr, nullptr, s));
+                          const_cast<int32_t*>(done), kNoTol, nullptr, nullptr, nullptr, s));
   MLAMG_TRY(correct(D, l, L.x_ext, done, s));
   MLAMG_TRY(jacobi_sweep(L.A, L.dinv, L.b, L.x_ext, L.t_ext, false, done, s));
   *x_out = L.t_ext;
@@ -718,7 +718,7 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
   DLevel& L = D->lv[0];
   const mlamg_csr* A = L.A;
   MLAMG_TRY(halo_exchange_impl(L.hx, x_ext, s));
-  MLAMG_TRY(residual_impl(A, b, x_ext, L.r_ext, nullptr, nullptr, nullptr, done, 0.0, nullptr,
+  MLAMG_TRY(residual_impl(A, b, x_ext, L.r_ext, nullptr, nullptr, nullptr, done, kNoTol, nullptr,
                           nullptr, nullptr, s));
   MLAMG_TRY(correct(D, 0, x_ext, done, s));
   MLAMG_TRY(jacobi_sweep(A, L.dinv, b, x_ext, L.t_ext, false, done, s));
@@ -746,7 +746,7 @@ int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cyc
   DLevel& L = D->lv[0];
   MLAMG_HIP(hipMemsetAsync(D->flags, 0, 2 * sizeof(int32_t), s));
   MLAMG_TRY(halo_exchange_impl(L.hx, x_ext, s));
-  MLAMG_TRY(residual_impl(L.A, b, x_ext, L.r_ext, nullptr, nullptr, nullptr, nullptr, 0.0,
+  MLAMG_TRY(residual_impl(L.A, b, x_ext, L.r_ext, nullptr, nullptr, nullptr, nullptr, kNoTol,
                           nullptr, nullptr, nullptr, s));
   if (n_cycles > 0) {
     // the first cycle's first pre-smoothing sweep (later ones are fused into the cycle end)

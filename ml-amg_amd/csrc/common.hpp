@@ -66,6 +66,11 @@ constexpr int kSrtRows = MLAMG_SRT_THREADS * MLAMG_SRT_RPT;
 constexpr int kSrtNnz = 8 * MLAMG_SRT_THREADS;
 constexpr int kSrtPosBits = 12;
 
+// Tolerance arguments: tol >= 0 arms the device stop flag with ||.|| <= tol (the reference's
+// `e <= tol`, ns/lib/multigrid.py:197, MLAMG.py:194 — tol = 0 included: an exactly zero norm
+// stops); a negative tol means "no tolerance" (run every requested cycle).
+constexpr double kNoTol = -1.0;
+
 }  // namespace mlamg
 
 // Device CSR matrix. int32 indptr/indices, fp64 values (scipy's choice for these sizes:
@@ -231,7 +236,7 @@ int count_out_of_range(const int32_t* a, int64_t n, int64_t lo, int64_t hi, hipS
 template <class F>
 static int run_cycles(int n_cycles, double tol, int32_t* done_dev, int32_t* done_host,
                       hipStream_t s, F&& one) {
-  if (!(tol > 0.0) || !done_host) {
+  if (!(tol >= 0.0) || !done_host) {
     for (int c = 0; c < n_cycles; ++c) MLAMG_TRY(one());
     return MLAMG_OK;
   }

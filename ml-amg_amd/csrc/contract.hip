@@ -32,7 +32,7 @@ int mlamg_lloyd(const mlamg_csr* G, int32_t* seeds_inout, int32_t k, int maxiter
 
 int mlamg_vcycle(const mlamg_hier* H, const double* b, double* x, int n_cycles, double* res_hist,
                  void* stream) {
-  return mlamg_hier_vcycle(const_cast<mlamg_hier*>(H), b, x, n_cycles, 0.0, res_hist, nullptr, 1,
+  return mlamg_hier_vcycle(const_cast<mlamg_hier*>(H), b, x, n_cycles, mlamg::kNoTol, res_hist, nullptr, 1,
                            stream);
 }
 

@@ -157,12 +157,12 @@ static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, 
     MLAMG_HIP(hipMemsetAsync(cur, 0, sizeof(double) * L.n, s));
     MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre, done, s));
     MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, const_cast<int32_t*>(done),
-                            0.0, nullptr, nullptr, nullptr, s));
+                            kNoTol, nullptr, nullptr, nullptr, s));
   } else if (H->nu_pre > 0) {
     if (!presmoothed) MLAMG_TRY(jacobi_from_zero(cur, L.dinv, b, L.n, done, s));
     MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre - 1, done, s));
     MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, const_cast<int32_t*>(done),
-                            0.0, nullptr, nullptr, nullptr, s));
+                            kNoTol, nullptr, nullptr, nullptr, s));
   } else {
     MLAMG_HIP(hipMemsetAsync(cur, 0, sizeof(double) * L.n, s));
     MLAMG_HIP(hipMemcpyAsync(L.r, b, sizeof(double) * L.n, hipMemcpyDeviceToDevice, s));
@@ -183,14 +183,16 @@ static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, 
   return MLAMG_OK;
 }
 
-// Fused mode (nu_pre >= 1, odd nu_post, so the cycle's result t lands in L0.tmp): the
+// Fused mode (nu_pre >= 1 and an odd number of ping-pong sweeps after the first one, i.e.
+// (nu_pre - 1 + nu_post) odd, so the cycle's result t lands in L0.tmp — V(1,1), V(2,2), V(1,3)
+// but not V(2,1) or V(1,2), whose result ends in x itself): the
 // end-of-cycle residual kernel r = b - A t also writes x = t + Dinv_w r, i.e. the NEXT cycle's
 // first pre-smoothing sweep (same roundings), and the cycle starts from that. The caller applies
 // the very first sweep before the first cycle and copies t back into x after the last one (t is
 // still in tmp even when the tolerance flag stopped later cycles). Saves one pass over x, d, r.
 static bool fused_presmooth(const mlamg_hier* H) {
-  return !H->lv.empty() && H->nu_pre >= 1 && (H->nu_post & 1) && !H->lv[0].gs &&
-         H->norm_mode == 0;
+  return !H->lv.empty() && H->nu_pre >= 1 && ((H->nu_pre - 1 + H->nu_post) & 1) &&
+         !H->lv[0].gs && H->norm_mode == 0;
 }
 
 // one finest-level cycle; requires L0.r == b - A x on entry, leaves it so on exit (fused mode:
@@ -209,12 +211,12 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
   double* other = L.tmp;
   if (H->nu_pre > 0 && L.gs) {
     MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre, done, s));
-    MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, done, 0.0, nullptr,
+    MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, done, kNoTol, nullptr,
                             nullptr, nullptr, s));
   } else if (H->nu_pre > 0) {
     if (!fused) MLAMG_TRY(jacobi_from_residual(cur, L.dinv, L.r, L.n, done, s));
     MLAMG_TRY(smooth(L, b, cur, other, H->nu_pre - 1, done, s));
-    MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, done, 0.0, nullptr,
+    MLAMG_TRY(residual_impl(L.A, b, cur, L.r, nullptr, nullptr, nullptr, done, kNoTol, nullptr,
                             nullptr, nullptr, s));
   }
   const bool fuse_next = H->lv.size() > 1 && H->nu_pre > 0 && !H->lv[1].gs;
@@ -365,7 +367,7 @@ int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, d
   if (!H->lv.empty()) {
     Level& L = H->lv[0];
     // r = b - A x for the first cycle's pre-smoothing sweep
-    MLAMG_TRY(residual_impl(L.A, b, x, L.r, nullptr, nullptr, nullptr, nullptr, 0.0, nullptr,
+    MLAMG_TRY(residual_impl(L.A, b, x, L.r, nullptr, nullptr, nullptr, nullptr, kNoTol, nullptr,
                             nullptr, nullptr, s));
     if (fused) MLAMG_TRY(jacobi_from_residual(x, L.dinv, L.r, L.n, nullptr, s));
   }
@@ -438,7 +440,8 @@ int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes) {
     t += H->nu_post * jac;
     // end-of-cycle residual norm, + x = t (read t, write x) or, fused, x = t + Dinv_w r
     // (fused: + read t, dinv, write x; r itself is not stored)
-    if (l == 0) t += res + (fused ? 16.0 * n : ((H->nu_post & 1) ? 16.0 * n : 0.0));
+    const int swaps = L.gs ? 0 : std::max(H->nu_pre - 1, 0) + H->nu_post;
+    if (l == 0) t += res + ((fused || (swaps & 1)) ? 16.0 * n : 0.0);
   }
   if (H->D) t += 8.0 * H->D->n * H->D->n + 16.0 * H->D->n;
   *bytes = t;

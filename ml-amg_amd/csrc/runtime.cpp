@@ -191,6 +191,9 @@ int mlamg_csr_create(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t*
   MLAMG_REQUIRE(indptr != nullptr, "indptr is NULL");
   MLAMG_REQUIRE(nnz == 0 || (indices && data), "indices/data NULL with nnz > 0");
   MLAMG_REQUIRE(where >= 0 && where <= 2, "where must be 0 (host), 1 (device copy), 2 (wrap)");
+  // int32 indptr/indices (scipy's choice below 2^31 nonzeros): larger operators would wrap
+  MLAMG_REQUIRE(nnz <= INT32_MAX && n_rows < INT32_MAX && n_cols <= INT32_MAX,
+                "nnz / n_rows / n_cols exceed the int32 index range of the CSR handle");
   hipStream_t s = nullptr;
   mlamg_csr* A = nullptr;
   if (where == MLAMG_WRAP_DEVICE) {

@@ -223,7 +223,7 @@ __global__ __launch_bounds__(1024) void k_finalize_norm(const double* __restrict
     const int c = counter ? *counter : 0;
     if (hist) hist[c] = nrm;
     if (counter) *counter = c + 1;
-    if (done && tol > 0.0 && nrm <= tol) *done = 1;
+    if (done && tol >= 0.0 && nrm <= tol) *done = 1;
   }
 }
 
@@ -1966,7 +1966,7 @@ int mlamg_residual(const mlamg_csr* A, const double* b, const double* x, double*
                    void* stream) {
   MLAMG_REQUIRE(A && (A->n_rows == 0 || (b && x && r)), "NULL argument");
   MLAMG_REQUIRE(A->n_rows == A->n_cols, "residual needs a square matrix");
-  return residual_impl(A, b, x, r, norm2, nullptr, nullptr, nullptr, 0.0, nullptr, nullptr,
+  return residual_impl(A, b, x, r, norm2, nullptr, nullptr, nullptr, kNoTol, nullptr, nullptr,
                        nullptr, S(stream));
 }
 

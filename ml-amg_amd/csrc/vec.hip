@@ -76,7 +76,7 @@ __global__ __launch_bounds__(1024) void k_sum_hist(const double* __restrict__ pa
     const int c = *counter;
     if (hist) hist[c] = nrm;
     *counter = c + 1;
-    if (tol > 0.0 && nrm <= tol) *done = 1;
+    if (tol >= 0.0 && nrm <= tol) *done = 1;
   }
 }
 

@@ -161,6 +161,13 @@ def stream_ptr(stream=None):
     return ctypes.c_void_p(stream.cuda_stream)
 
 
+def _tol_arg(tol):
+    """Tolerance argument of the cycle entry points: None = no tolerance (-1.0: the C side arms
+    its stop flag only for tol >= 0, so a requested tol = 0 stops on an exactly zero norm like
+    the reference's `e <= tol`, ns/lib/multigrid.py:197)."""
+    return -1.0 if tol is None else float(tol)
+
+
 def ptr(t):
     """Device pointer of a torch tensor (None -> NULL)."""
     if t is None:

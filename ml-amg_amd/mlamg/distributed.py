@@ -19,7 +19,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib, partition
-from ._lib import call, ptr, stream_ptr
+from ._lib import _tol_arg, call, ptr, stream_ptr
 from .sparse import DeviceCSR
 
 
@@ -222,10 +222,10 @@ class DistributedHierarchy:
         """Replay each cycle from one captured hipGraph (kernels + RCCL calls)."""
         call("mlamg_dhier_set_cycle_graph", self.handle, int(bool(on)))
 
-    def cycle(self, b_own, x_ext, n_cycles, tol=0.0, history=True):
+    def cycle(self, b_own, x_ext, n_cycles, tol=None, history=True):
         hist = torch.zeros(max(n_cycles, 1), dtype=torch.float64, device="cuda") if history else None
         done = ctypes.c_int32()
-        call("mlamg_dhier_vcycle", self.handle, ptr(b_own), ptr(x_ext), int(n_cycles), float(tol),
+        call("mlamg_dhier_vcycle", self.handle, ptr(b_own), ptr(x_ext), int(n_cycles), _tol_arg(tol),
              ptr(hist), ctypes.byref(done) if history else None, stream_ptr())
         if not history:
             return None

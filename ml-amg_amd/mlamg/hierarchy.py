@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import MLAMG_EUNSUPPORTED, MlamgError, call, ptr, stream_ptr
+from ._lib import MLAMG_EUNSUPPORTED, MlamgError, _tol_arg, call, ptr, stream_ptr
 from .graph import aggregate_op_device, bellman_ford_device, labels_to_columns, lloyd_cluster_device
 from .multigrid import lambda_max_dinv_a
 from .sparse import DeviceCSR, _device, as_device, galerkin, to_device_vec
@@ -277,13 +277,14 @@ class Hierarchy:
         call("mlamg_hier_set_smoothing", hh, int(nu_pre), int(nu_post))
 
     # ------------------------------------------------------------------ cycling
-    def cycle(self, b, x, n_cycles, tol=0.0, use_graph=True, history=True):
+    def cycle(self, b, x, n_cycles, tol=None, use_graph=True, history=True):
         """Run up to n_cycles V-cycles in place on x (device tensors). Returns the residual
-        history ||b - A x||_2 after each cycle (numpy, truncated at convergence)."""
+        history ||b - A x||_2 after each cycle (numpy, truncated at convergence). tol=None runs
+        every cycle; a number (0 included) stops after the first cycle whose norm is <= tol."""
         dev = x.device
         hist = torch.zeros(max(n_cycles, 1), dtype=torch.float64, device=dev) if history else None
         done = ctypes.c_int32()
-        call("mlamg_hier_vcycle", self.handle, ptr(b), ptr(x), int(n_cycles), float(tol),
+        call("mlamg_hier_vcycle", self.handle, ptr(b), ptr(x), int(n_cycles), _tol_arg(tol),
              ptr(hist), ctypes.byref(done), int(bool(use_graph)), stream_ptr())
         if not history:
             return None
@@ -291,11 +292,12 @@ class Hierarchy:
 
     def cycle_async(self, b, x, n_cycles, use_graph=True):
         """Launch n_cycles V-cycles without reading anything back (for timing)."""
-        call("mlamg_hier_vcycle", self.handle, ptr(b), ptr(x), int(n_cycles), 0.0, None, None,
-             int(bool(use_graph)), stream_ptr())
+        call("mlamg_hier_vcycle", self.handle, ptr(b), ptr(x), int(n_cycles), _tol_arg(None),
+             None, None, int(bool(use_graph)), stream_ptr())
 
     def solve(self, b, x0=None, tol=1e-8, maxiter=500, return_history=False):
-        """Stationary V-cycle iteration until ||b - A x||_2 <= tol (absolute, MLAMG.py:194)."""
+        """Stationary V-cycle iteration until ||b - A x||_2 <= tol (absolute, MLAMG.py:194);
+        tol=None runs all maxiter cycles."""
         bd = to_device_vec(b)
         xd = torch.zeros_like(bd) if x0 is None else to_device_vec(x0).clone()
         hist = self.cycle(bd, xd, maxiter, tol=tol)

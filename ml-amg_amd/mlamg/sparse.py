@@ -46,6 +46,17 @@ def canonical_rows(A):
     return C
 
 
+_INT32_MAX = 2**31 - 1
+
+
+def _check_int32(shape, nnz):
+    """The device handle stores int32 indptr/indices (scipy's type at these sizes): refuse an
+    operator whose nonzero count or dimensions would wrap instead of uploading a corrupted one."""
+    if nnz > _INT32_MAX or shape[0] >= _INT32_MAX or shape[1] > _INT32_MAX:
+        raise ValueError(f"matrix of shape {tuple(shape)} with {nnz} nonzeros exceeds the int32 "
+                         "index range of the device CSR handle")
+
+
 class DeviceCSR:
     """An int32/fp64 CSR matrix resident on the GPU (owns a `mlamg_csr*`)."""
 
@@ -68,6 +79,7 @@ class DeviceCSR:
         if check:
             A = canonical_rows(A)
         _device()
+        _check_int32(A.shape, A.nnz)
         indptr = np.ascontiguousarray(A.indptr, dtype=np.int32)
         indices = np.ascontiguousarray(A.indices, dtype=np.int32)
         data = np.ascontiguousarray(A.data, dtype=np.float64)
@@ -83,6 +95,7 @@ class DeviceCSR:
         for t, dt in ((crow, torch.int32), (col, torch.int32), (val, torch.float64)):
             if t.dtype != dt or not t.is_cuda or not t.is_contiguous():
                 raise TypeError("from_torch needs contiguous cuda int32/int32/float64 tensors")
+        _check_int32(shape, val.numel())
         h = ctypes.c_void_p()
         where = _lib.MLAMG_WRAP_DEVICE if wrap else _lib.MLAMG_COPY_DEVICE
         call("mlamg_csr_create", shape[0], shape[1], val.numel(), ptr(crow), ptr(col), ptr(val),

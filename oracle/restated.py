@@ -368,7 +368,7 @@ def make_cycle(levels, lu, nu_pre=1, nu_post=1):
     return cycle
 
 
-def vcycle_solve(levels, Ac, b, x, n_cycles, tol=0.0, nu_pre=1, nu_post=1, lu=None):
+def vcycle_solve(levels, Ac, b, x, n_cycles, tol=None, nu_pre=1, nu_post=1, lu=None):
     """Multilevel Jacobi V(nu_pre, nu_post) iteration in the device executor's order
     (mlamg hier.hip; each level = MLAMG.py:189-195 with the coarse solve recursing).
     Returns (x, residual history). lu: a pre-factorised coarse solve (spla.factorized)."""
@@ -382,7 +382,7 @@ def vcycle_solve(levels, Ac, b, x, n_cycles, tol=0.0, nu_pre=1, nu_post=1, lu=No
         x = cycle(0, b, x) if levels else lu(b)
         r = la.norm(b - A0 @ x, 2)
         hist.append(r)
-        if tol > 0 and r <= tol:
+        if tol is not None and r <= tol:
             break
     return x, np.array(hist)
 

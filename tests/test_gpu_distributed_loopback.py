@@ -27,7 +27,7 @@ def setup():
     return A, H
 
 
-def _run(A, H, world, min_rows, ncyc=6, tol=0.0, b=None, x0=None, K=None):
+def _run(A, H, world, min_rows, ncyc=6, tol=None, b=None, x0=None, K=None):
     import torch
     from mlamg.distributed import DistributedHierarchy, LoopbackGroup
     n = A.shape[0]
