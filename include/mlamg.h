@@ -262,8 +262,13 @@ int mlamg_hier_set_norm(mlamg_hier* H, int mode);
  * the call syncs. use_graph != 0 replays one captured hipGraph per cycle. */
 int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, double tol,
                       double* res_hist, int32_t* cycles_done_host, int use_graph, void* stream);
-/* bytes one V-cycle moves by the algorithmic model of SURVEY.md §8(d) (for roofline reports) */
+/* bytes of one V-cycle with every operator priced as CSR (SURVEY.md §8(d) model): a
+ * CSR-EQUIVALENT figure — re-encoded operators (rowpat, value codes) move far fewer bytes, so
+ * this divided by the cycle time may exceed the HBM peak */
 int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes);
+/* bytes one V-cycle must move through HBM with every operator priced as the format it is stored
+ * in (mlamg_csr_format_bytes per launch + the epilogues' vectors): the cycle's roofline bytes */
+int mlamg_hier_cycle_format_bytes(const mlamg_hier* H, double* bytes);
 
 /* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI)
  * New relative to the reference, whose only parallelism is a process task farm over independent
@@ -275,6 +280,11 @@ typedef struct mlamg_dhier mlamg_dhier;
 int mlamg_comm_unique_id(void* id_out);
 int mlamg_comm_create(const void* id, int nranks, int rank, mlamg_comm** out);
 int mlamg_comm_destroy(mlamg_comm* c);
+/* the communicator's size, rank and device as the transport reports them (RCCL:
+ * ncclCommCount / ncclCommUserRank / ncclCommCuDevice); transport_out (nullable): 0 = RCCL,
+ * 1 = loopback, 2 = null (timing only). device_out nullable. */
+int mlamg_comm_info(const mlamg_comm* c, int* nranks_out, int* rank_out, int* device_out,
+                    int* transport_out);
 /* In-process test transport (RCCL refuses two ranks on one GPU): the ranks of a loop group are
  * host threads of ONE process, each with its own stream on the same device; send/recv become
  * device-to-device copies ordered by events, the all-reduce sums in rank order. Same message

@@ -404,6 +404,22 @@ int mlamg_comm_create(const void* id, int nranks, int rank, mlamg_comm** out) {
   return MLAMG_OK;
 }
 
+int mlamg_comm_info(const mlamg_comm* c, int* nranks_out, int* rank_out, int* device_out,
+                    int* transport_out) {
+  MLAMG_REQUIRE(c && nranks_out && rank_out, "NULL argument");
+  if (c->comm) {  // as RCCL itself reports them
+    MLAMG_NCCL(ncclCommCount(c->comm, nranks_out));
+    MLAMG_NCCL(ncclCommUserRank(c->comm, rank_out));
+    if (device_out) MLAMG_NCCL(ncclCommCuDevice(c->comm, device_out));
+  } else {
+    *nranks_out = c->nranks;
+    *rank_out = c->rank;
+    if (device_out) MLAMG_HIP(hipGetDevice(device_out));
+  }
+  if (transport_out) *transport_out = c->comm ? 0 : (c->loop ? 1 : 2);
+  return MLAMG_OK;
+}
+
 int mlamg_comm_destroy(mlamg_comm* c) {
   if (c) {
     if (c->comm) (void)ncclCommDestroy(c->comm);

@@ -420,14 +420,30 @@ static double spmv_bytes(const mlamg_csr* A) {
   return 12.0 * A->nnz + 4.0 * (A->n_rows + 1) + 8.0 * A->n_cols + 8.0 * A->n_rows;
 }
 
-int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes) {
-  MLAMG_REQUIRE(H && bytes, "NULL argument");
+// Bytes of one V-cycle, summed over its launches. stored = false: every operator priced as
+// CSR (SURVEY.md §8(d) model — a CSR-EQUIVALENT figure, which re-encoded operators beat);
+// stored = true: every operator priced as the format it is stored in (mlamg_csr_format_bytes:
+// matrix stream + x once + y once), Jacobi weights not read when attached to a rowpat operator,
+// end-of-cycle r not written in fused mode — the bytes the cycle must move through HBM.
+static int cycle_bytes(const mlamg_hier* H, bool stored, double* bytes) {
   double t = 0.0;
+  auto op = [&](const mlamg_csr* M, double* b) -> int {
+    if (!stored) {
+      *b = spmv_bytes(M);
+      return MLAMG_OK;
+    }
+    return mlamg_csr_format_bytes(M, b);
+  };
   for (size_t l = 0; l < H->lv.size(); ++l) {
     const Level& L = H->lv[l];
     const double n = (double)L.n;
-    const double jac = spmv_bytes(L.A) + 16.0 * n;  // + b, dinv
-    const double res = spmv_bytes(L.A) + 8.0 * n;   // + b
+    double a = 0.0, r = 0.0, p = 0.0;
+    MLAMG_TRY(op(L.A, &a));
+    MLAMG_TRY(op(L.R, &r));
+    MLAMG_TRY(op(L.P, &p));
+    const double dv = (stored && L.A->rp_dinv_att) ? 0.0 : 8.0 * n;
+    const double jac = a + 8.0 * n + dv;  // + b, dinv
+    const double res = a + 8.0 * n;       // + b
     const bool fused = l == 0 && fused_presmooth(H);
     if (H->nu_pre > 0) {
       // first sweep: elementwise at the top (unless fused into the cycle end); below, fused
@@ -435,17 +451,32 @@ int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes) {
       if (!fused) t += (l == 0) ? 32.0 * n : 16.0 * n;
       t += (H->nu_pre - 1) * jac + res;
     }
-    t += spmv_bytes(L.R);
-    t += spmv_bytes(L.P) + 8.0 * n;  // + read x before the add
+    t += r;
+    t += p + 8.0 * n;  // + read x before the add
     t += H->nu_post * jac;
     // end-of-cycle residual norm, + x = t (read t, write x) or, fused, x = t + Dinv_w r
-    // (fused: + read t, dinv, write x; r itself is not stored)
+    // (fused: + read dinv, write x; r itself is not stored)
     const int swaps = L.gs ? 0 : std::max(H->nu_pre - 1, 0) + H->nu_post;
-    if (l == 0) t += res + ((fused || (swaps & 1)) ? 16.0 * n : 0.0);
+    if (l == 0) {
+      if (stored && fused)
+        t += res + dv;  // r's store replaced by x's
+      else
+        t += res + ((fused || (swaps & 1)) ? 16.0 * n : 0.0);
+    }
   }
   if (H->D) t += 8.0 * H->D->n * H->D->n + 16.0 * H->D->n;
   *bytes = t;
   return MLAMG_OK;
+}
+
+int mlamg_hier_cycle_bytes(const mlamg_hier* H, double* bytes) {
+  MLAMG_REQUIRE(H && bytes, "NULL argument");
+  return cycle_bytes(H, false, bytes);
+}
+
+int mlamg_hier_cycle_format_bytes(const mlamg_hier* H, double* bytes) {
+  MLAMG_REQUIRE(H && bytes, "NULL argument");
+  return cycle_bytes(H, true, bytes);
 }
 
 }  // extern "C"

@@ -102,9 +102,11 @@ SIGNATURES = {
     "mlamg_hier_set_norm": (c_int, [c_vp, c_int]),
     "mlamg_hier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_int, c_vp]),
     "mlamg_hier_cycle_bytes": (c_int, [c_vp, P_dbl]),
+    "mlamg_hier_cycle_format_bytes": (c_int, [c_vp, P_dbl]),
     "mlamg_comm_unique_id": (c_int, [c_vp]),
     "mlamg_comm_create": (c_int, [c_vp, c_int, c_int, c_vpp]),
     "mlamg_comm_destroy": (c_int, [c_vp]),
+    "mlamg_comm_info": (c_int, [c_vp, P_int, P_int, P_int, P_int]),
     "mlamg_loop_group_create": (c_int, [c_int, c_vpp]),
     "mlamg_loop_group_destroy": (c_int, [c_vp]),
     "mlamg_comm_create_loopback": (c_int, [c_vp, c_int, c_vpp]),

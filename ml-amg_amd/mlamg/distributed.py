@@ -39,6 +39,9 @@ class Comm:
         call("mlamg_comm_create", uid, int(world), int(rank), ctypes.byref(h))
         self.handle = h
 
+    def info(self):
+        return comm_info(self)
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h:
@@ -47,6 +50,16 @@ class Comm:
             except Exception:
                 pass
             self.handle = None
+
+
+def comm_info(comm):
+    """{'nranks', 'rank', 'device', 'transport'} as the communicator's transport reports them
+    (RCCL: ncclCommCount / ncclCommUserRank / ncclCommCuDevice)."""
+    nr, rk, dv, tr = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    call("mlamg_comm_info", comm.handle, ctypes.byref(nr), ctypes.byref(rk), ctypes.byref(dv),
+         ctypes.byref(tr))
+    return {"nranks": nr.value, "rank": rk.value, "device": dv.value,
+            "transport": ("rccl", "loopback", "null")[tr.value]}
 
 
 class LoopbackGroup:
@@ -304,7 +317,11 @@ def _max(v, world):
 
 
 def bench_main(args, world, rank, local_rank, metric, hbm_peak):
-    """bench.py for N > 1: strong scaling of one C4 problem over N GPUs."""
+    """bench.py for N > 1: strong scaling of one C4 problem over N GPUs. Returns
+    (out, H, x0, teardown): `out` is the JSON dict on rank 0 (None elsewhere), H the replicated
+    single-GPU hierarchy (rank 0's CPU baseline runs on it), teardown() ends the run (barrier,
+    process group). Every rank reports its own fine-level SpMV roofline and its communicator's
+    rank count as RCCL itself reports it (ncclCommCount); rank 0 gathers them."""
     from . import problems
     from .hierarchy import Hierarchy
 
@@ -322,12 +339,13 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
     setup_s = time.perf_counter() - t0
     sync_formats(H, world)
     comm = Comm(world, rank)
+    cinfo = comm.info()
     t1 = time.perf_counter()
     D = DistributedHierarchy(H, comm, min_rows=args.dist_min_rows, A_host=A)
     part_s = time.perf_counter() - t1
     log(f"setup {setup_s:.1f}s (replicated), partition+upload {part_s:.1f}s; {D.K} of "
         f"{len(H.levels)} levels partitioned; rank rows {D.lo}..{D.hi}; ghosts (x, r, p) per "
-        f"level {D.ghosts}")
+        f"level {D.ghosts}; communicator {cinfo}")
     x0 = np.random.RandomState(0).randn(n)
     x0 /= np.linalg.norm(x0)
     b_own = torch.zeros(D.n_own, dtype=torch.float64, device="cuda")
@@ -361,7 +379,6 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
         graph_on = False
         D.set_cycle_graph(False)
         ok_all = check()
-    ok = torch.tensor([1.0 if ok_all else 0.0])
     del x_full, b_full
     # timing
     x_ext = D.new_x(torch.as_tensor(x0[D.lo:D.hi]))
@@ -389,9 +406,20 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
     t_spmv = e0.elapsed_time(e1) / 1000.0 / 50
     B = D.A_loc.format_bytes()  # bytes the chosen storage format streams for y = A_loc x_ext
     B_csr = 12.0 * D.A_loc.nnz + 4.0 * (D.n_own + 1) + 8.0 * D.n_ext + 8.0 * D.n_own
-    achieved = B / t_spmv / 1e9
-    achieved_min = _max(-achieved, world) * -1.0  # slowest rank
+    mine = {"rank": rank, "rccl_nranks": cinfo["nranks"], "rccl_rank": cinfo["rank"],
+            "device": cinfo["device"], "transport": cinfo["transport"],
+            "rows": [int(D.lo), int(D.hi)], "format": D.A_loc.get_format()[0],
+            "format_bytes": B, "us": round(t_spmv * 1e6, 2),
+            "GBps": round(B / t_spmv / 1e9, 1), "frac": round(B / t_spmv / 1e9 / hbm_peak, 4)}
+    per_rank = [None] * world
+    if world > 1:
+        dist.all_gather_object(per_rank, mine)
+    else:
+        per_rank = [mine]
+    out = None
     if rank == 0:
+        slow = min(per_rank, key=lambda r: r["GBps"])
+        pmc = _load_rank_pmc(world, slow["format"], slow["format_bytes"])
         out = {
             "metric": metric,
             "value": round(args.steps / dt, 3),
@@ -411,23 +439,46 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
                             f"halos, {H.n_levels - D.K} coarser levels replicated",
                 "partitioned_levels": D.K,
                 "n": n, "levels": H.n_levels, "parallelism": f"rowsplit{world}",
-                "dist_matches_single_gpu": bool(ok.item() == 1.0),
+                "dist_matches_single_gpu": bool(ok_all),
                 "cycle_graph": graph_on,
+                "rccl_nranks": sorted({r["rccl_nranks"] for r in per_rank}),
+                "devices": [r["device"] for r in per_rank],
                 "rank0_local_formats": [
                     {k: t["chosen"] for k, t in zip("APR", D.tuning[3 * l:3 * l + 3])}
                     for l in range(D.K)],
             },
             "roofline": {
-                "bound": "hbm", "kernel": f"fine-level SpMV ({D.A_loc.get_format()[0]}), local rows "
-                                    "(slowest rank)",
-                "achieved": round(achieved_min, 1), "peak": hbm_peak, "unit": "GB/s",
-                "frac": round(achieved_min / hbm_peak, 4), "traffic": None,
-                "algorithmic_bytes_per_launch": B, "csr_algorithmic_bytes_per_launch": B_csr,
-                "avg_launch_us": round(t_spmv * 1e6, 2),
+                "bound": "hbm", "kernel": f"fine-level SpMV ({slow['format']}), local rows "
+                                          f"(slowest rank {slow['rank']})",
+                "achieved": slow["GBps"], "peak": hbm_peak, "unit": "GB/s",
+                "frac": slow["frac"],
+                "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                "algorithmic_bytes_per_launch": slow["format_bytes"],
+                "csr_algorithmic_bytes_per_launch": B_csr,
+                "avg_launch_us": slow["us"],
             },
+            "per_rank_spmv": per_rank,
+            "setup_s": {"replicated_build": round(setup_s, 3), "partition": round(part_s, 3)},
         }
-        print(json.dumps(out), flush=True)
-    _barrier(world)
-    del D
-    if world > 1:
-        dist.destroy_process_group()
+
+    def teardown():
+        nonlocal D
+        _barrier(world)
+        D = None
+        if world > 1:
+            dist.destroy_process_group()
+
+    return out, H, x0, teardown
+
+
+def _load_rank_pmc(world, fmt, format_bytes):
+    """PMC-measured HBM bytes of one rank's local fine SpMV (profiles/spmv_w{world}_pmc_{fmt}.json,
+    written by tools/pmc_traffic.py on the same local operator), if its bytes match."""
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    path = os.path.join(root, "profiles", f"spmv_w{world}_pmc_{fmt}.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    return d if d.get("algorithmic_bytes_per_launch") == format_bytes else None

@@ -311,9 +311,12 @@ class Hierarchy:
         self.cycle(bd, xd, 1, history=False)
         return xd if isinstance(b, torch.Tensor) else xd.cpu().numpy()
 
-    def cycle_bytes(self):
+    def cycle_bytes(self, stored=False):
+        """Bytes of one V-cycle. stored=False: operators priced as CSR (a
+        CSR-equivalent figure); stored=True: priced as stored (the cycle's HBM roofline bytes)."""
         v = ctypes.c_double()
-        call("mlamg_hier_cycle_bytes", self.handle, ctypes.byref(v))
+        call("mlamg_hier_cycle_format_bytes" if stored else "mlamg_hier_cycle_bytes",
+             self.handle, ctypes.byref(v))
         return float(v.value)
 
     # ------------------------------------------------------------------ info

@@ -332,6 +332,54 @@ def test_c4_full_size_properties(ml, oracle, torch_cuda):
     assert 0.3 < conv < 0.8
 
 
+@pytest.mark.slow
+def test_c4_full_size_hierarchy_parity(ml, oracle, torch_cuda):
+    """C4 (216^3, the bench configuration) at full size: the device hierarchy vs the oracle's
+    build_hierarchy given the device's omegas — every level's seeds, P and A, and the coarsest
+    matrix bitwise (the SpGEMM / SA / Bellman-Ford kernels reproduce scipy's results at 70 M
+    nonzeros) — then 4 V-cycles of the device executor vs the oracle's cycle on the ORACLE's
+    operators (each operator summed in the device kernel's order: scipy order for every exact
+    format, the CSR-vector order where the autotune picked it): residual histories within
+    rtol 1e-11 (the only non-bitwise step is the coarsest solve, dense inverse vs SuperLU) and
+    the iterate within 1e-10 of its max. Reference: ns/lib/multigrid.py:102-108,165;
+    MLAMG.py:189-195 per level."""
+    import gc
+    torch = torch_cuda
+    A = ml.problems.poisson_3d_7pt(216)
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, strength_mode="invabs", max_coarse=2000)
+    assert H.n_levels == 5
+    levels, Ac = oracle.build_hierarchy(A, alpha=0.1, strength_mode="invabs", max_coarse=2000,
+                                        omegas=[L.omega for L in H.levels])
+    assert len(levels) == len(H.levels)
+    for l, (Lo, Ld) in enumerate(zip(levels, H.levels)):
+        assert np.array_equal(Ld.seeds, Lo["seeds"]), l
+        for key, M in (("P", Ld.P), ("A", Ld.A)):
+            Md = M.to_scipy()
+            for arr in ("indptr", "indices", "data"):
+                assert np.array_equal(getattr(Md, arr), getattr(Lo[key], arr)), (l, key, arr)
+            del Md
+        assert np.array_equal(Ld.dinv.cpu().numpy(), Lo["Dw"].diagonal()), l
+        f = {k: v for k, v in zip("APR", (Ld.A.get_format(), Ld.P.get_format(),
+                                          Ld.R.get_format()))}
+        for k, v in f.items():
+            Lo[f"{k}_vw"] = v[1] if v[0] == "vector" else 0
+        Lo["R"] = Lo["P"].T.tocsr()
+        gc.collect()
+    Acd = H.Ac.to_scipy()
+    assert np.array_equal(Acd.indptr, Ac.indptr) and np.array_equal(Acd.indices, Ac.indices)
+    assert np.array_equal(Acd.data, Ac.data)
+    n = A.shape[0]
+    x0 = np.random.RandomState(0).randn(n)
+    x0 /= np.linalg.norm(x0)
+    b = np.zeros(n)
+    xo, ho = oracle.vcycle_solve(levels, Ac, b, x0, 4)
+    xd = dev(torch, x0)
+    hd = H.cycle(dev(torch, b), xd, 4)
+    assert len(hd) == 4
+    assert np.allclose(hd, ho, rtol=1e-11, atol=0), (hd, ho)
+    assert np.allclose(xd.cpu().numpy(), xo, rtol=0, atol=1e-10 * np.abs(xo).max())
+
+
 def _pair_patterns(A):
     """Distinct row-pair patterns of the rowpat format and their merged entry counts."""
     n = A.shape[0]

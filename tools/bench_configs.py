@@ -65,7 +65,8 @@ def main():
                "levels": H.n_levels, "operator_complexity": round(H.operator_complexity(), 3),
                "setup_s": round(H.timings["total"], 3), "gpu_vcycles_per_s": round(1 / dt, 2),
                "ms_per_cycle": round(dt * 1e3, 4),
-               "cycle_algorithmic_GBps": round(H.cycle_bytes() / dt / 1e9, 1),
+               "cycle_hbm_frac": round(H.cycle_bytes(stored=True) / dt / 1e9 / 8000.0, 4),
+               "cycle_csr_equivalent_GBps": round(H.cycle_bytes() / dt / 1e9, 1),
                "conv_factor_10cycles": round(float((hist[-1] / hist[-4]) ** (1 / 3)), 5),
                "cpu_vcycles_per_s_1thread": round(cps, 3),
                "gpu_over_cpu": round((1 / dt) / cps, 1),
