@@ -346,6 +346,8 @@ def main():
                              for f in H.formats()],
         "format_autotune_us": H.tuning,
         "setup_s": {k: round(v, 3) for k, v in H.timings.items()},
+        "setup_galerkin_s_per_level": H.galerkin_s,
+        "setup_spgemm_phases_ms": H.spgemm_phases_ms,
         "conv_factor_10cycles": round(conv, 5),
     }
     # host-buffer boundary: solve() on numpy b/x0 pays the PCIe copies of b

@@ -43,6 +43,7 @@ typedef struct mlamg_csr mlamg_csr;
 typedef struct mlamg_dense mlamg_dense;
 typedef struct mlamg_hier mlamg_hier;
 typedef struct mlamg_gs mlamg_gs;
+typedef struct mlamg_pcg mlamg_pcg;
 typedef struct mlamg_comm mlamg_comm;
 
 /* ---------------------------------------------------------------- runtime */
@@ -161,6 +162,12 @@ int mlamg_transpose(const mlamg_csr* A, mlamg_csr** out, void* stream);
  * later C@x sums in the same order as scipy. */
 int mlamg_spgemm(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out, void* stream);
 
+/* setup scratch: SpGEMM temporaries are cached device blocks reused across calls; this frees
+ * the cached (unused) blocks. freed_bytes nullable. */
+int mlamg_scratch_trim(size_t* freed_bytes);
+/* accumulated wall times (ms) of the Galerkin/SpGEMM phases since the last reset, in the order
+ * count, alloc, expand, sort, runsum, emit, finalize, free (n <= 8 entries written) */
+int mlamg_setup_phase_times(double* ms_out, int n, int reset);
 /* A_c = (R@A)@P, left-associative like `P.T@A@P` (multigrid.py:165; MLAMG.py:121), with R = P^T
  * from mlamg_transpose. Every entry is summed over k ascending, as scipy's CSC kernels do for
  * this expression, so values are bitwise scipy's; output columns sorted ascending. */
@@ -252,6 +259,21 @@ int mlamg_hier_set_smoothing(mlamg_hier* H, int nu_pre, int nu_post);
  * sweep, in place; ns/lib/multigrid.py:175,184 — the reference amg_2_v), or NULL for weighted
  * Jacobi (default) */
 int mlamg_hier_set_level_smoother(mlamg_hier* H, int level, const mlamg_gs* gs);
+/* Coarsest solve without a size cap (replaces spla.factorized / splu, ns/lib/multigrid.py:168,
+ * MLAMG.py:122, where a dense inverse no longer fits): PCG on A (SPD) preconditioned by one
+ * V-cycle of the inner hierarchy M (built on A, finalised), to ||b - A x|| <= rtol ||b||, at most
+ * maxit iterations. A and M must outlive the solver. */
+int mlamg_pcg_create(const mlamg_csr* A, mlamg_hier* M, double rtol, int maxit, mlamg_pcg** out);
+int mlamg_pcg_destroy(mlamg_pcg* C);
+/* x = A^-1 b (DEVICE vectors), async on the stream (polls its convergence flag) */
+int mlamg_pcg_solve(mlamg_pcg* C, const double* b, double* x, void* stream);
+/* iterations of the last solve, solves that stopped at maxit, total iterations, largest final
+ * relative residual over all solves (each nullable); syncs */
+int mlamg_pcg_stats(const mlamg_pcg* C, int32_t* last_iters, int32_t* not_converged,
+                    int32_t* total_iters, double* max_rel_residual, void* stream);
+/* use the PCG solver C (size = A_coarse rows) as H's coarsest solve instead of a dense inverse;
+ * cycles of such a hierarchy run eagerly (use_graph is ignored) */
+int mlamg_hier_set_coarse_pcg(mlamg_hier* H, const mlamg_csr* A_coarse, mlamg_pcg* C);
 /* what res_hist records each cycle: 0 = ||b - A x||_2 (default, MLAMG.py:194 / res_tol),
  * 1 = ||x||_2 (amg_2_v error_tol, multigrid.py:193); the tolerance test applies to it */
 int mlamg_hier_set_norm(mlamg_hier* H, int mode);

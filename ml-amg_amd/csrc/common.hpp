@@ -220,6 +220,13 @@ int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int
                      hipStream_t s);
 int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
                       hipStream_t s);
+int32_t* hier_done_flag(mlamg_hier* H);
+int64_t hier_fine_rows(const mlamg_hier* H);
+// coarsest solve by inner-hierarchy PCG (pcg.hip)
+int pcg_solve_impl(mlamg_pcg* C, const double* b, double* x, const int32_t* outer_done,
+                   hipStream_t s);
+int64_t pcg_rows(const mlamg_pcg* C);
+mlamg_hier* pcg_inner(mlamg_pcg* C);
 int hier_prepare_ext(mlamg_hier* H);
 int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
                   const int32_t* done, hipStream_t s);

@@ -36,6 +36,7 @@ struct mlamg_hier {
   std::vector<Level> lv;
   const mlamg_csr* Ac = nullptr;
   const mlamg_dense* D = nullptr;
+  mlamg_pcg* pcg = nullptr;  // coarse solve by inner-hierarchy PCG instead of a dense inverse
   double* xc = nullptr;
   double* bc = nullptr;
   int nu_pre = 1, nu_post = 1;
@@ -76,10 +77,21 @@ static void hier_free_graph(mlamg_hier* H) {
   H->cgraph = nullptr;
 }
 
+static int64_t coarse_rows(const mlamg_hier* H) {
+  return H->D ? H->D->n : pcg_rows(H->pcg);
+}
+
+// the coarsest solve: dense inverse GEMV, or inner-hierarchy PCG (pcg.hip)
+static int coarse_solve(mlamg_hier* H, const double* b, double* x, const int32_t* done,
+                        hipStream_t s) {
+  if (H->D) return dense_solve_impl(H->D, b, x, done, s);
+  return pcg_solve_impl(H->pcg, b, x, done, s);
+}
+
 static int hier_prepare(mlamg_hier* H) {
   if (H->ready) return MLAMG_OK;
-  MLAMG_REQUIRE(!H->lv.empty() || H->D, "empty hierarchy");
-  MLAMG_REQUIRE(H->D != nullptr, "coarse solver not set (mlamg_hier_set_coarse)");
+  MLAMG_REQUIRE(H->D != nullptr || H->pcg != nullptr,
+                "coarse solver not set (mlamg_hier_set_coarse / mlamg_hier_set_coarse_pcg)");
   size_t total = 0;
   auto add = [&](int64_t n) {
     size_t b = sizeof(double) * (size_t)std::max<int64_t>(n, 1);
@@ -94,7 +106,7 @@ static int hier_prepare(mlamg_hier* H) {
     add(n);
     add(n);
   }
-  const int64_t nc = H->D->n;
+  const int64_t nc = coarse_rows(H);
   add(nc);
   add(nc);
   int64_t maxblk = 1;
@@ -146,7 +158,7 @@ static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, 
                         bool presmoothed = false) {
   const int32_t* done = H->flags + 1;
   if (l == H->lv.size()) {
-    MLAMG_TRY(dense_solve_impl(H->D, b, H->xc, done, s));
+    MLAMG_TRY(coarse_solve(H, b, H->xc, done, s));
     *res = H->xc;
     return MLAMG_OK;
   }
@@ -202,7 +214,7 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
   int32_t* counter = H->flags;
   int32_t* done = H->flags + 1;
   if (H->lv.empty()) {  // coarse-only hierarchy: x = A^-1 b
-    MLAMG_TRY(dense_solve_impl(H->D, b, x, done, s));
+    MLAMG_TRY(coarse_solve(H, b, x, done, s));
     return MLAMG_OK;
   }
   Level& L = H->lv[0];
@@ -249,13 +261,18 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
 namespace mlamg {
 // allocate the work buffers now (not capture-safe), so a later capture only records launches
 int hier_prepare_ext(mlamg_hier* H) { return hier_prepare(H); }
+// the device flag every kernel of a cycle checks (a PCG using H as preconditioner shares it)
+int32_t* hier_done_flag(mlamg_hier* H) { return H->flags + 1; }
+int64_t hier_fine_rows(const mlamg_hier* H) {
+  return H->lv.empty() ? coarse_rows(H) : H->lv[0].n;
+}
 
 // One cycle from a zero guess on (b -> *x_out) treating level 0 of H as a coarse level
 // (used by the distributed executor, whose H holds the replicated levels 1..L).
 int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
                       hipStream_t s) {
   MLAMG_TRY(hier_prepare(H));
-  if (!use_graph) return cycle_coarse(H, 0, b, x_out, s);
+  if (!use_graph || H->pcg) return cycle_coarse(H, 0, b, x_out, s);
   if (!(H->cexec && H->cg_b == b && H->cg_epoch == format_epoch())) {
     if (H->cexec) (void)hipGraphExecDestroy(H->cexec);
     if (H->cgraph) (void)hipGraphDestroy(H->cgraph);
@@ -332,6 +349,18 @@ int mlamg_hier_set_coarse(mlamg_hier* H, const mlamg_csr* A_coarse, const mlamg_
   return MLAMG_OK;
 }
 
+int mlamg_hier_set_coarse_pcg(mlamg_hier* H, const mlamg_csr* A_coarse, mlamg_pcg* C) {
+  MLAMG_REQUIRE(H && A_coarse && C, "NULL argument");
+  MLAMG_REQUIRE(!H->ready, "hierarchy already finalised");
+  MLAMG_REQUIRE(pcg_rows(C) == A_coarse->n_rows, "PCG solver of another size");
+  if (!H->lv.empty())
+    MLAMG_REQUIRE(H->lv.back().P->n_cols == A_coarse->n_rows, "coarse size does not match last P");
+  H->Ac = A_coarse;
+  H->D = nullptr;
+  H->pcg = C;
+  return MLAMG_OK;
+}
+
 int mlamg_hier_set_level_smoother(mlamg_hier* H, int level, const mlamg_gs* gs) {
   MLAMG_REQUIRE(H && level >= 0 && (size_t)level < H->lv.size(), "invalid level");
   MLAMG_REQUIRE(!gs || gs_rows(gs) == H->lv[level].n, "Gauss-Seidel handle of another size");
@@ -362,6 +391,8 @@ int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, d
   MLAMG_REQUIRE(n_cycles >= 0, "n_cycles < 0");
   MLAMG_TRY(hier_prepare(H));
   hipStream_t s = S(stream);
+  // a PCG coarse solve polls its convergence flag between iterations: cycles run eagerly
+  if (H->pcg) use_graph = 0;
   MLAMG_HIP(hipMemsetAsync(H->flags, 0, 2 * sizeof(int32_t), s));
   const bool fused = fused_presmooth(H) && n_cycles > 0;
   if (!H->lv.empty()) {
@@ -465,6 +496,15 @@ static int cycle_bytes(const mlamg_hier* H, bool stored, double* bytes) {
     }
   }
   if (H->D) t += 8.0 * H->D->n * H->D->n + 16.0 * H->D->n;
+  if (H->pcg) {  // priced per PCG iteration of the last solve: A_c x + ~10 vector passes +
+                 // one inner V-cycle
+    int32_t it = 0;
+    MLAMG_TRY(mlamg_pcg_stats(H->pcg, &it, nullptr, nullptr, nullptr, nullptr));
+    double a = 0.0, inner = 0.0;
+    MLAMG_TRY(stored ? mlamg_csr_format_bytes(H->Ac, &a) : (a = spmv_bytes(H->Ac), MLAMG_OK));
+    MLAMG_TRY(cycle_bytes(pcg_inner(H->pcg), stored, &inner));
+    t += (double)std::max(it, 1) * (a + 80.0 * (double)H->Ac->n_rows + inner);
+  }
   *bytes = t;
   return MLAMG_OK;
 }

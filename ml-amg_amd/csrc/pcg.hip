@@ -1,0 +1,333 @@
+// Coarsest-level solve without a size cap: the reference factorises
+// the Galerkin operator with SuperLU at any size (`spla.factorized(A_H)`, ns/lib/multigrid.py:168;
+// `splu(A_H, COLAMD)`, ns/preconditioner/MLAMG.py:122). A dense inverse (dense.hip) stops being
+// an option once n_c^2 doubles no longer fit or its O(n_c^3) setup dominates, so above that the
+// coarse system A_c x = b is solved by preconditioned conjugate gradients, the preconditioner
+// being one V-cycle (zero guess) of an inner multilevel hierarchy built on A_c itself — setup
+// O(nnz), a handful of V-cycles per solve. The solve runs to a relative residual
+// ||b - A_c x||_2 <= rtol * ||b||_2 (default 1e-12), i.e. it replaces an exact factorisation by
+// a solve accurate far beyond the outer cycle's own convergence (parity: tolerance, stated in
+// the tests). A_c must be symmetric positive definite (P^T A P of an SPD A, the reference's
+// use); the V(nu,nu) weighted-Jacobi cycle with R = P^T is then a symmetric preconditioner.
+//
+// Every kernel checks the solver's done flag (shared with the inner hierarchy, whose kernels
+// check it too), so once the tolerance is met the remaining launches of the solve return at
+// once. Eagerly launched solves poll the flag every few iterations and stop launching; inside a
+// stream capture every iteration up to maxit is recorded (the V-cycle executor therefore runs
+// hierarchies with a PCG coarse solver eagerly). Reductions are fixed-order (partials over a
+// fixed grid, one-workgroup finalisation), so a solve is deterministic.
+#include "common.hpp"
+
+#include <cmath>
+
+struct mlamg_pcg {
+  const mlamg_csr* A = nullptr;
+  mlamg_hier* M = nullptr;
+  int64_t n = 0;
+  double rtol = 1e-12;
+  int maxit = 200;
+  int poll = 4;
+  void* mem = nullptr;
+  double *r = nullptr, *p = nullptr, *q = nullptr, *partial = nullptr;
+  double* scal = nullptr;     // [0] rho, [1] alpha, [2] beta, [3] ||b||^2, [4] ||r||^2 (last),
+                              // [5] largest final ||r||/||b|| over solves
+  int32_t* flags = nullptr;   // [0] iterations of the last solve, [1] solves not converged,
+                              // [2] total iterations
+  int32_t* done_host = nullptr;
+  int nb = 1;
+};
+
+namespace mlamg {
+
+constexpr int kPcgThreads = 256;
+constexpr int kPcgMaxBlocks = 1024;
+
+__device__ __forceinline__ double pcg_wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ void block_partial(double s, double* partial) {
+  __shared__ double red[kPcgThreads / 64];
+  s = pcg_wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// one workgroup: fixed-order sum of nb partials
+__device__ __forceinline__ double block_total(const double* __restrict__ partial, int nb) {
+  __shared__ double red[16];
+  double s = strided_sum(partial, nb, threadIdx.x, 1024);
+  s = pcg_wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < 16; ++i) t += red[i];
+  return t;
+}
+
+// x = 0, r = b, partials of b.b; done := outer done (a finished outer iteration skips the solve)
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_init(const double* __restrict__ b,
+                                                          double* __restrict__ x,
+                                                          double* __restrict__ r, int64_t n,
+                                                          double* __restrict__ partial,
+                                                          int32_t* done, const int32_t* outer,
+                                                          int32_t* flags) {
+  const bool skip = outer && *outer;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *done = skip ? 1 : 0;
+    flags[0] = 0;
+  }
+  if (skip) return;
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kPcgThreads) {
+    const double v = b[i];
+    x[i] = 0.0;
+    r[i] = v;
+    s += v * v;
+  }
+  block_partial(s, partial);
+}
+
+// ||b||^2; a zero right-hand side is solved by x = 0
+__global__ __launch_bounds__(1024) void k_pcg_bnorm(const double* __restrict__ partial, int nb,
+                                                    double* scal, int32_t* done) {
+  if (*done) return;
+  const double t = block_total(partial, nb);
+  if (threadIdx.x == 0) {
+    scal[3] = t;
+    if (!(t > 0.0)) *done = 1;
+  }
+}
+
+// partials of u.v
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_dot(const double* __restrict__ u,
+                                                         const double* __restrict__ v, int64_t n,
+                                                         double* __restrict__ partial,
+                                                         const int32_t* done) {
+  if (*done) return;
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kPcgThreads)
+    s += u[i] * v[i];
+  block_partial(s, partial);
+}
+
+// rho = r.z (first: p = z as well, done by k_pcg_p with beta = 0)
+__global__ __launch_bounds__(1024) void k_pcg_rho(const double* __restrict__ partial, int nb,
+                                                  double* scal, const int32_t* done, int first) {
+  if (*done) return;
+  const double t = block_total(partial, nb);
+  if (threadIdx.x == 0) {
+    scal[2] = first ? 0.0 : t / scal[0];
+    scal[0] = t;
+  }
+}
+
+// p = z + beta p
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_p(const double* __restrict__ z,
+                                                       double* __restrict__ p, int64_t n,
+                                                       const double* scal, const int32_t* done) {
+  if (*done) return;
+  const double beta = scal[2];
+  for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kPcgThreads)
+    p[i] = z[i] + beta * p[i];
+}
+
+// alpha = rho / (p.q)
+__global__ __launch_bounds__(1024) void k_pcg_alpha(const double* __restrict__ partial, int nb,
+                                                    double* scal, const int32_t* done) {
+  if (*done) return;
+  const double t = block_total(partial, nb);
+  if (threadIdx.x == 0) scal[1] = scal[0] / t;
+}
+
+// x += alpha p, r -= alpha q, partials of r.r
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_update(double* __restrict__ x,
+                                                            double* __restrict__ r,
+                                                            const double* __restrict__ p,
+                                                            const double* __restrict__ q,
+                                                            int64_t n, const double* scal,
+                                                            double* __restrict__ partial,
+                                                            const int32_t* done) {
+  if (*done) return;
+  const double alpha = scal[1];
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kPcgThreads) {
+    x[i] += alpha * p[i];
+    const double v = r[i] - alpha * q[i];
+    r[i] = v;
+    s += v * v;
+  }
+  block_partial(s, partial);
+}
+
+// ||r||^2 <= rtol^2 ||b||^2 -> done; iteration count
+__global__ __launch_bounds__(1024) void k_pcg_check(const double* __restrict__ partial, int nb,
+                                                    double* scal, int32_t* done, int32_t* flags,
+                                                    double rtol) {
+  if (*done) return;
+  const double t = block_total(partial, nb);
+  if (threadIdx.x == 0) {
+    scal[4] = t;
+    flags[0] += 1;
+    flags[2] += 1;
+    if (t <= rtol * rtol * scal[3]) {
+      *done = 1;
+      const double rel = sqrt(t / scal[3]);
+      if (rel > scal[5]) scal[5] = rel;
+    }
+  }
+}
+
+// after the last launched iteration: a solve that did not reach the tolerance is counted
+__global__ void k_pcg_end(double* scal, int32_t* done, int32_t* flags, const int32_t* outer) {
+  if (threadIdx.x != 0 || *done || (outer && *outer)) return;
+  flags[1] += 1;
+  const double rel = sqrt(scal[4] / scal[3]);
+  if (rel > scal[5]) scal[5] = rel;
+  *done = 1;
+}
+
+static int pcg_grid(int64_t n) {
+  return (int)std::min<int64_t>(kPcgMaxBlocks, std::max<int64_t>(1, (n + kPcgThreads - 1) /
+                                                                        kPcgThreads));
+}
+
+static int pcg_iteration(mlamg_pcg* C, double* x, int32_t* done, hipStream_t s) {
+  const int nb = C->nb;
+  const int64_t n = C->n;
+  MLAMG_TRY(spmv_set(C->A, C->p, C->q, done, s));
+  hipLaunchKernelGGL(k_pcg_dot, dim3(nb), dim3(kPcgThreads), 0, s, C->p, C->q, n, C->partial,
+                     done);
+  hipLaunchKernelGGL(k_pcg_alpha, dim3(1), dim3(1024), 0, s, C->partial, nb, C->scal, done);
+  hipLaunchKernelGGL(k_pcg_update, dim3(nb), dim3(kPcgThreads), 0, s, x, C->r, C->p, C->q, n,
+                     C->scal, C->partial, done);
+  hipLaunchKernelGGL(k_pcg_check, dim3(1), dim3(1024), 0, s, C->partial, nb, C->scal, done,
+                     C->flags, C->rtol);
+  double* z = nullptr;
+  MLAMG_TRY(hier_coarse_cycle(C->M, C->r, &z, 0, s));
+  hipLaunchKernelGGL(k_pcg_dot, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, n, C->partial, done);
+  hipLaunchKernelGGL(k_pcg_rho, dim3(1), dim3(1024), 0, s, C->partial, nb, C->scal, done, 0);
+  hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(kPcgThreads), 0, s, z, C->p, n, C->scal, done);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+int pcg_solve_impl(mlamg_pcg* C, const double* b, double* x, const int32_t* outer_done,
+                   hipStream_t s) {
+  if (C->n == 0) return MLAMG_OK;
+  MLAMG_TRY(hier_prepare_ext(C->M));
+  int32_t* done = hier_done_flag(C->M);
+  const int nb = C->nb;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  MLAMG_HIP(hipStreamIsCapturing(s, &cap));
+  const bool poll = cap == hipStreamCaptureStatusNone && C->done_host;
+  hipLaunchKernelGGL(k_pcg_init, dim3(nb), dim3(kPcgThreads), 0, s, b, x, C->r, C->n, C->partial,
+                     done, outer_done, C->flags);
+  hipLaunchKernelGGL(k_pcg_bnorm, dim3(1), dim3(1024), 0, s, C->partial, nb, C->scal, done);
+  double* z = nullptr;
+  MLAMG_TRY(hier_coarse_cycle(C->M, C->r, &z, 0, s));
+  hipLaunchKernelGGL(k_pcg_dot, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, C->n, C->partial,
+                     done);
+  hipLaunchKernelGGL(k_pcg_rho, dim3(1), dim3(1024), 0, s, C->partial, nb, C->scal, done, 1);
+  hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(kPcgThreads), 0, s, z, C->p, C->n, C->scal, done);
+  for (int it = 0; it < C->maxit; ++it) {
+    MLAMG_TRY(pcg_iteration(C, x, done, s));
+    if (poll && (it + 1) % C->poll == 0 && it + 1 < C->maxit) {
+      MLAMG_HIP(hipMemcpyAsync(C->done_host, done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      MLAMG_HIP(hipStreamSynchronize(s));
+      if (*C->done_host) break;
+    }
+  }
+  hipLaunchKernelGGL(k_pcg_end, dim3(1), dim3(64), 0, s, C->scal, done, C->flags, outer_done);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+int64_t pcg_rows(const mlamg_pcg* C) { return C->n; }
+mlamg_hier* pcg_inner(mlamg_pcg* C) { return C->M; }
+
+}  // namespace mlamg
+
+using namespace mlamg;
+
+extern "C" {
+
+int mlamg_pcg_create(const mlamg_csr* A, mlamg_hier* M, double rtol, int maxit,
+                     mlamg_pcg** out) {
+  MLAMG_REQUIRE(A && M && out, "NULL argument");
+  MLAMG_REQUIRE(A->n_rows == A->n_cols, "square matrix required");
+  MLAMG_REQUIRE(hier_fine_rows(M) == A->n_rows, "inner hierarchy does not match A");
+  MLAMG_REQUIRE(rtol > 0.0 && maxit >= 1, "rtol > 0 and maxit >= 1 required");
+  auto* C = new mlamg_pcg();
+  C->A = A;
+  C->M = M;
+  C->n = A->n_rows;
+  C->rtol = rtol;
+  C->maxit = maxit;
+  C->nb = pcg_grid(C->n);
+  const size_t vec = ((sizeof(double) * (size_t)std::max<int64_t>(C->n, 1)) + 255) & ~size_t(255);
+  const size_t total = 3 * vec + sizeof(double) * kPcgMaxBlocks + 256 + 256;
+  if (hipMalloc(&C->mem, total) != hipSuccess) {
+    delete C;
+    set_error("pcg_create: hipMalloc failed");
+    return MLAMG_ENOMEM;
+  }
+  char* p = static_cast<char*>(C->mem);
+  C->r = reinterpret_cast<double*>(p);
+  C->p = reinterpret_cast<double*>(p + vec);
+  C->q = reinterpret_cast<double*>(p + 2 * vec);
+  C->partial = reinterpret_cast<double*>(p + 3 * vec);
+  C->scal = reinterpret_cast<double*>(p + 3 * vec + sizeof(double) * kPcgMaxBlocks);
+  C->flags = reinterpret_cast<int32_t*>(p + 3 * vec + sizeof(double) * kPcgMaxBlocks + 256);
+  if (hipMemset(C->mem, 0, total) != hipSuccess ||
+      hipHostMalloc(&C->done_host, sizeof(int32_t), hipHostMallocDefault) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    if (C->done_host) (void)hipHostFree(C->done_host);
+    (void)hipFree(C->mem);
+    delete C;
+    set_error("pcg_create: allocation failed");
+    return MLAMG_ENOMEM;
+  }
+  *out = C;
+  return MLAMG_OK;
+}
+
+int mlamg_pcg_destroy(mlamg_pcg* C) {
+  if (C) {
+    if (C->mem) (void)hipFree(C->mem);
+    if (C->done_host) (void)hipHostFree(C->done_host);
+    delete C;
+  }
+  return MLAMG_OK;
+}
+
+int mlamg_pcg_solve(mlamg_pcg* C, const double* b, double* x, void* stream) {
+  MLAMG_REQUIRE(C && (C->n == 0 || (b && x)), "NULL argument");
+  MLAMG_REQUIRE(b != x, "b and x must differ");
+  return pcg_solve_impl(C, b, x, nullptr, S(stream));
+}
+
+int mlamg_pcg_stats(const mlamg_pcg* C, int32_t* last_iters, int32_t* not_converged,
+                    int32_t* total_iters, double* max_rel_residual, void* stream) {
+  MLAMG_REQUIRE(C, "NULL argument");
+  int32_t f[3] = {0, 0, 0};
+  double sc[6] = {0, 0, 0, 0, 0, 0};
+  hipStream_t s = S(stream);
+  MLAMG_HIP(hipMemcpyAsync(f, C->flags, sizeof(f), hipMemcpyDeviceToHost, s));
+  MLAMG_HIP(hipMemcpyAsync(sc, C->scal, sizeof(sc), hipMemcpyDeviceToHost, s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  if (last_iters) *last_iters = f[0];
+  if (not_converged) *not_converged = f[1];
+  if (total_iters) *total_iters = f[2];
+  if (max_rel_residual) *max_rel_residual = sc[5];
+  return MLAMG_OK;
+}
+
+}  // extern "C"

@@ -21,6 +21,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include <rocprim/rocprim.hpp>
 
@@ -216,22 +218,83 @@ __global__ void k_scatter_rows(const int64_t* __restrict__ off, const int32_t* _
   }
 }
 
+// Setup temporaries (SpGEMM products, sort buffers, ...) come from a process-wide pool of
+// device blocks instead of a hipMalloc/hipFree pair per buffer per call: a hierarchy build runs
+// ~10 SpGEMMs whose temporaries reach several GB each, and every hipFree of such a block is an
+// implicit device synchronisation plus an unmap. Blocks are reused best-fit (up to 2x the
+// request) and returned to the pool when the DevBuf releases them (after a device sync, as
+// hipFree would); mlamg_scratch_trim() frees the cached blocks (Hierarchy.build does at its end).
+struct ScratchPool {
+  std::mutex mu;
+  std::multimap<size_t, void*> free_blocks;
+  size_t cached = 0;
+};
+static ScratchPool& scratch_pool() {
+  static ScratchPool p;
+  return p;
+}
+
+static hipError_t pool_get(void** p, size_t bytes, size_t* got) {
+  bytes = (std::max<size_t>(bytes, 1) + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+  ScratchPool& P = scratch_pool();
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto it = P.free_blocks.lower_bound(bytes);
+    if (it != P.free_blocks.end() && it->first <= 2 * bytes) {
+      *p = it->second;
+      *got = it->first;
+      P.cached -= it->first;
+      P.free_blocks.erase(it);
+      return hipSuccess;
+    }
+  }
+  *got = bytes;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipErrorOutOfMemory) {  // drop the cache and retry once
+    (void)hipGetLastError();
+    size_t freed = 0;
+    (void)mlamg_scratch_trim(&freed);
+    e = hipMalloc(p, bytes);
+  }
+  return e;
+}
+
+static void pool_put(void* p, size_t bytes) {
+  ScratchPool& P = scratch_pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  P.free_blocks.emplace(bytes, p);
+  P.cached += bytes;
+}
+
 struct DevBuf {
-  std::vector<void*> ptrs;
+  std::vector<std::pair<void*, size_t>> blocks;
   void release() {
-    for (void* p : ptrs)
-      if (p) (void)hipFree(p);
-    ptrs.clear();
+    if (blocks.empty()) return;
+    // kernels of this call may still read the blocks (error paths): wait, as hipFree would
+    (void)hipDeviceSynchronize();
+    for (auto& b : blocks) pool_put(b.first, b.second);
+    blocks.clear();
   }
   ~DevBuf() { release(); }
   template <class T>
   hipError_t get(T** p, size_t count) {
     *p = nullptr;
-    hipError_t e = hipMalloc((void**)p, sizeof(T) * std::max<size_t>(count, 1));
-    if (e == hipSuccess) ptrs.push_back(*p);
+    size_t got = 0;
+    hipError_t e = pool_get((void**)p, sizeof(T) * std::max<size_t>(count, 1), &got);
+    if (e == hipSuccess) blocks.emplace_back((void*)*p, got);
     return e;
   }
 };
+
+// Per-phase wall times of the sorted SpGEMM (Galerkin products), accumulated over calls and
+// read by mlamg_setup_phase_times: the stream is synchronised at each phase boundary (setup
+// only), so the times are the phases' own. Order: count, alloc, expand, sort, runsum, emit,
+// finalize, free.
+constexpr int kPhases = 8;
+static const char* const kPhaseNames[kPhases] = {"count", "alloc", "expand", "sort",
+                                                 "runsum", "emit", "finalize", "free"};
+static std::mutex g_phase_mu;
+static double g_phase_ms[kPhases] = {};
 
 #define DB_CHECK(expr)                                                          \
   do {                                                                          \
@@ -360,17 +423,23 @@ __global__ void k_rowptr(const int32_t* __restrict__ crow, int64_t nnz, int64_t 
 static int spgemm_sorted_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out,
                               int rbits, int cbits, hipStream_t s) {
   const int64_t n = A->n_rows, nz = A->nnz;
-  // MLAMG_TIMING=1: per-phase wall times on stderr (syncs the stream at each phase)
+  // per-phase wall times (stream synchronised at each boundary), accumulated for
+  // mlamg_setup_phase_times; MLAMG_TIMING=1 also prints them on stderr
   static const bool timing = std::getenv("MLAMG_TIMING") != nullptr;
   auto t_prev = std::chrono::steady_clock::now();
   auto tick = [&](const char* what) {
-    if (!timing) return;
-    (void)hipDeviceSynchronize();
+    (void)hipStreamSynchronize(s);
     const auto t = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[spgemm %lldx%lld nnzA=%lld] %-8s %8.2f ms\n", (long long)n,
-                 (long long)B->n_cols, (long long)nz, what,
-                 std::chrono::duration<double, std::milli>(t - t_prev).count());
+    const double ms = std::chrono::duration<double, std::milli>(t - t_prev).count();
     t_prev = t;
+    {
+      std::lock_guard<std::mutex> lk(g_phase_mu);
+      for (int i = 0; i < kPhases; ++i)
+        if (std::strcmp(kPhaseNames[i], what) == 0) g_phase_ms[i] += ms;
+    }
+    if (timing)
+      std::fprintf(stderr, "[spgemm %lldx%lld nnzA=%lld] %-8s %8.2f ms\n", (long long)n,
+                   (long long)B->n_cols, (long long)nz, what, ms);
   };
   DevBuf db;
   int32_t* rows = nullptr;
@@ -797,6 +866,29 @@ __global__ void k_strength(const double* __restrict__ x, int64_t nnz, int mode,
 using namespace mlamg;
 
 extern "C" {
+
+int mlamg_scratch_trim(size_t* freed_bytes) {
+  ScratchPool& P = scratch_pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  size_t f = 0;
+  for (auto& b : P.free_blocks) {
+    (void)hipFree(b.second);
+    f += b.first;
+  }
+  P.free_blocks.clear();
+  P.cached = 0;
+  if (freed_bytes) *freed_bytes = f;
+  return MLAMG_OK;
+}
+
+int mlamg_setup_phase_times(double* ms_out, int n, int reset) {
+  MLAMG_REQUIRE(ms_out && n >= 0, "NULL argument");
+  std::lock_guard<std::mutex> lk(g_phase_mu);
+  for (int i = 0; i < std::min(n, kPhases); ++i) ms_out[i] = g_phase_ms[i];
+  if (reset)
+    for (int i = 0; i < kPhases; ++i) g_phase_ms[i] = 0.0;
+  return MLAMG_OK;
+}
 
 int mlamg_transpose(const mlamg_csr* A, mlamg_csr** out, void* stream) {
   MLAMG_REQUIRE(A && out, "NULL argument");

@@ -78,6 +78,8 @@ SIGNATURES = {
     "mlamg_transpose": (c_int, [c_vp, c_vpp, c_vp]),
     "mlamg_spgemm": (c_int, [c_vp, c_vp, c_vpp, c_vp]),
     "mlamg_galerkin": (c_int, [c_vp, c_vp, c_vp, c_vpp, c_vp]),
+    "mlamg_scratch_trim": (c_int, [ctypes.POINTER(ctypes.c_size_t)]),
+    "mlamg_setup_phase_times": (c_int, [P_dbl, c_int, c_int]),
     "mlamg_sa_smoother": (c_int, [c_vp, c_dbl, c_vpp, c_vp]),
     "mlamg_csr_scale_rows": (c_int, [c_vp, c_vp, c_int, c_vpp, c_vp]),
     "mlamg_lambda_max_dinvA": (c_int, [c_vp, c_int, c_dbl, c_u64, P_dbl, P_int, c_vp]),
@@ -97,6 +99,11 @@ SIGNATURES = {
     "mlamg_hier_destroy": (c_int, [c_vp]),
     "mlamg_hier_add_level": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mlamg_hier_set_coarse": (c_int, [c_vp, c_vp, c_vp]),
+    "mlamg_hier_set_coarse_pcg": (c_int, [c_vp, c_vp, c_vp]),
+    "mlamg_pcg_create": (c_int, [c_vp, c_vp, c_dbl, c_int, c_vpp]),
+    "mlamg_pcg_destroy": (c_int, [c_vp]),
+    "mlamg_pcg_solve": (c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_pcg_stats": (c_int, [c_vp, P_i32, P_i32, P_i32, P_dbl, c_vp]),
     "mlamg_hier_set_smoothing": (c_int, [c_vp, c_int, c_int]),
     "mlamg_hier_set_level_smoother": (c_int, [c_vp, c_int, c_vp]),
     "mlamg_hier_set_norm": (c_int, [c_vp, c_int]),

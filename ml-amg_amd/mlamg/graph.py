@@ -3,6 +3,8 @@
   modified_bellman_ford   ns/lib/graph.py:7-53     seeded Bellman-Ford, fp32 (torch) arithmetic
   nearest_center_to_agg   ns/lib/graph.py:56-86    aggregate matrix from assignments
   lloyd_aggregation       ns/lib/graph.py:156-239  seeds + pyamg 4.x lloyd_cluster + AggOp
+  num_connected_components, check_aggregates_connected   ns/lib/graph.py:89-153 (host-side
+                          graph checks, kept so an alias of ns.lib.graph to this module is whole)
 
 Distances are bit-exact with the reference for any input (order-independent fixed point, see
 csrc/graph.hip). Seed labels are bit-exact whenever shortest paths are unique; on exact ties the
@@ -162,3 +164,43 @@ def lloyd_aggregation(C, ratio=0.03, distance='unit', maxiter=10, rand=None):
                           shape=(G.shape[0], num_seeds))
     roots = roots_dev.cpu().numpy().astype(np.intc)
     return AggOp, roots, seeds
+
+
+def num_connected_components(adj):
+    """ns/lib/graph.py:89-122: number of depth-first searches needed to visit every node, each
+    started at the first unvisited node and following, from node i, the nonzeros of column i
+    (adj[:, i]) — the connected components of a symmetric adjacency. Host-side graph utility
+    (not on the V-cycle path); iterative, O(nnz)."""
+    A = sp.csc_matrix(adj)
+    A.eliminate_zeros()
+    n = A.shape[0]
+    ip, ij = A.indptr, A.indices
+    visited = np.zeros(n, dtype=bool)
+    count = 0
+    start = 0
+    while True:
+        while start < n and visited[start]:
+            start += 1
+        if start >= n:
+            return count
+        count += 1
+        stack = [start]
+        while stack:
+            i = stack.pop()
+            visited[i] = True
+            nb = ij[ip[i]:ip[i + 1]]
+            stack.extend(nb[~visited[nb]].tolist())
+
+
+def check_aggregates_connected(A, Agg):
+    """ns/lib/graph.py:125-153: True when every aggregate (column of the tentative Agg) induces
+    a connected subgraph of A — the block diagonal of the aggregates' principal submatrices has
+    exactly k connected components."""
+    A = sp.csr_matrix(A)
+    Agg = sp.csc_matrix(Agg)
+    n, k = Agg.shape
+    blocks = []
+    for i in range(k):
+        nodes = Agg[:, i].nonzero()[0]
+        blocks.append(A[nodes][:, nodes])
+    return num_connected_components(sp.block_diag(blocks).tocsc()) == k

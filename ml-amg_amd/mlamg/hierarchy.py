@@ -21,6 +21,7 @@ import math
 import time
 
 import numpy as np
+import scipy.sparse as sp
 import torch
 
 from . import _lib
@@ -54,6 +55,43 @@ class Level:
         self.gs = None
 
 
+_PHASES = ("count", "alloc", "expand", "sort", "runsum", "emit", "finalize", "free")
+
+
+def _setup_phases(reset=False):
+    """Accumulated SpGEMM phase wall times (ms) since the last reset (mlamg_setup_phase_times)."""
+    buf = (ctypes.c_double * len(_PHASES))()
+    call("mlamg_setup_phase_times", buf, len(_PHASES), int(bool(reset)))
+    return {k: round(float(v), 2) for k, v in zip(_PHASES, buf)}
+
+
+def _level_item(spec, lvl):
+    """The level-`lvl` entry of a per-level specification (None, one item = level 0, or a
+    list / tuple of items)."""
+    if spec is None:
+        return None
+    if isinstance(spec, (list, tuple)):
+        return spec[lvl] if lvl < len(spec) else None
+    return spec if lvl == 0 else None
+
+
+def _aggregate_operator(agg, n):
+    """Agg (n x k, ones) on the device from a label vector (-1 = unaggregated) or a matrix."""
+    if isinstance(agg, DeviceCSR):
+        return agg
+    if sp.issparse(agg):
+        if agg.shape[0] != n:
+            raise ValueError(f"aggregate matrix has {agg.shape[0]} rows, the operator {n}")
+        A = sp.csr_matrix(agg, dtype=np.float64)
+        A.data[:] = 1.0
+        return DeviceCSR.from_scipy(A)
+    lab = np.asarray(agg.cpu().numpy() if isinstance(agg, torch.Tensor) else agg).astype(np.int64)
+    if lab.shape != (n,):
+        raise ValueError(f"aggregate labels must have shape ({n},), got {lab.shape}")
+    k = int(lab.max()) + 1 if lab.size else 0
+    return aggregate_op_device(torch.as_tensor(lab.astype(np.int32)).to(_device()), k)
+
+
 class Hierarchy:
     """A multilevel (or two-level) smoothed-aggregation hierarchy resident on the GPU."""
 
@@ -66,6 +104,8 @@ class Hierarchy:
         self.nu_pre = 1
         self.nu_post = 1
         self.timings = {}
+        self.pcg = None
+        self.inner = None
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -188,49 +228,84 @@ class Hierarchy:
     def build(cls, A, *, alpha=0.1, strength_mode="invabs", aggregation="bellman_ford",
               max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, seed=0, sort_seeds=True,
               lanczos_tol=1e-15, lanczos_iter=20000, lloyd_maxiter=10, nu_pre=1, nu_post=1,
-              fine_format="autotune", coarse_format="vector", verbose=False, finalize=True):
+              fine_format="autotune", coarse_format="vector", verbose=False, finalize=True,
+              aggregates=None, prolongators=None):
+        """Smoothed-aggregation hierarchy built on the GPU.
+
+        Per level: strength -> seeds RandomState(seed).permutation(n)[:ceil(alpha n)] ->
+        seeded Bellman-Ford (or Lloyd) aggregates -> SA prolongator P = (I - w D^-1 A) Agg with
+        w = (4/3)/lambda_max(D^-1 A) (ns/lib/multigrid.py:102-108) -> A_c = P^T A P (:165).
+
+        aggregates / prolongators: supplied instead of computed, for the first levels — e.g. the
+        learned aggregates of C5 or the learned P of the MLAMG PC
+        (ns/preconditioner/MLAMG.py:105-121). Each is one item (level 0) or a list (levels
+        0, 1, ...); an aggregate item is a label vector (node -> aggregate column, -1 = none)
+        or an n x k 0/1 matrix (scipy or DeviceCSR), and is smoothed into P as above; a
+        prolongator item is used as P as given (no smoothing). jacobi_weight="sa" smooths every
+        level with its SA weight w instead of a fixed one."""
         H = cls()
         H.jacobi_weight = jacobi_weight
         t_all = time.perf_counter()
         A_dev = as_device(A)
         tm = {"aggregation": 0.0, "lambda_max": 0.0, "prolongator": 0.0, "galerkin": 0.0,
               "formats": 0.0, "dense": 0.0}
+        _setup_phases(reset=True)
+        H.galerkin_s = []
         while True:
             n = A_dev.shape[0]
             if n <= max_coarse or len(H.levels) + 1 >= max_levels:
                 break
             L = Level(A_dev)
+            lvl = len(H.levels)
+            P_given = _level_item(prolongators, lvl)
+            Agg_given = _level_item(aggregates, lvl)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            C = strength(A_dev, strength_mode)
-            k = int(math.ceil(alpha * n))
-            seeds = np.random.RandomState(seed).permutation(n)[:k]
-            if sort_seeds:
-                seeds = np.sort(seeds)
-            L.seeds = seeds
-            seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
-            if aggregation == "bellman_ford":
-                _, lab, L.bf_sweeps = bellman_ford_device(C, seeds_dev)
-                col = labels_to_columns(lab, seeds_dev)
-            elif aggregation == "lloyd":
-                _, col, _, L.bf_sweeps = lloyd_cluster_device(C, seeds_dev, lloyd_maxiter)
-            else:
-                raise ValueError(f"unknown aggregation {aggregation!r}")
-            L.Agg = aggregate_op_device(col, k)
-            L.n_seeds = k
-            del C
+            if P_given is None and Agg_given is None:
+                C = strength(A_dev, strength_mode)
+                k = int(math.ceil(alpha * n))
+                seeds = np.random.RandomState(seed).permutation(n)[:k]
+                if sort_seeds:
+                    seeds = np.sort(seeds)
+                L.seeds = seeds
+                seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
+                if aggregation == "bellman_ford":
+                    _, lab, L.bf_sweeps = bellman_ford_device(C, seeds_dev)
+                    col = labels_to_columns(lab, seeds_dev)
+                elif aggregation == "lloyd":
+                    _, col, _, L.bf_sweeps = lloyd_cluster_device(C, seeds_dev, lloyd_maxiter)
+                else:
+                    raise ValueError(f"unknown aggregation {aggregation!r}")
+                L.Agg = aggregate_op_device(col, k)
+                L.n_seeds = k
+                del C
+            elif P_given is None:
+                L.Agg = _aggregate_operator(Agg_given, n)
+                L.n_seeds = L.Agg.shape[1]
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            L.lam, L.lanczos_iters = lambda_max_dinv_a(A_dev, max_iter=lanczos_iter, tol=lanczos_tol)
-            L.omega = (4.0 / 3.0) / abs(L.lam)
+            if P_given is None or jacobi_weight == "sa":
+                L.lam, L.lanczos_iters = lambda_max_dinv_a(A_dev, max_iter=lanczos_iter,
+                                                           tol=lanczos_tol)
+                L.omega = (4.0 / 3.0) / abs(L.lam)
             t2 = time.perf_counter()
-            h = ctypes.c_void_p()
-            call("mlamg_sa_smoother", A_dev.handle, float(L.omega), ctypes.byref(h), stream_ptr())
-            S = DeviceCSR(h)
-            L.P = S @ L.Agg
-            del S
+            if P_given is None:
+                h = ctypes.c_void_p()
+                call("mlamg_sa_smoother", A_dev.handle, float(L.omega), ctypes.byref(h),
+                     stream_ptr())
+                S = DeviceCSR(h)
+                L.P = S @ L.Agg
+                del S
+            else:
+                L.P = as_device(P_given)
+                if L.P.shape[0] != n:
+                    raise ValueError(f"level {lvl}: prolongator has {L.P.shape[0]} rows, "
+                                     f"the operator {n}")
+            if L.P.shape[1] >= n:
+                raise ValueError(f"level {lvl}: P has {L.P.shape[1]} columns for {n} rows "
+                                 "(no coarsening)")
             L.R = L.P.transpose()
-            L.dinv = A_dev.diag_inv(jacobi_weight)
+            L.dinv = A_dev.diag_inv(L.omega if jacobi_weight == "sa" else jacobi_weight)
             torch.cuda.synchronize()
             t3 = time.perf_counter()
             A_next = galerkin(L.R, A_dev, L.P)
@@ -240,15 +315,21 @@ class Hierarchy:
             tm["lambda_max"] += t2 - t1
             tm["prolongator"] += t3 - t2
             tm["galerkin"] += t4 - t3
+            H.galerkin_s.append(round(t4 - t3, 4))
             H.levels.append(L)
             if verbose:
-                print(f"[mlamg] level {len(H.levels) - 1}: n={n} nnz={A_dev.nnz} seeds={k} "
-                      f"bf_sweeps={L.bf_sweeps} lam={L.lam:.15g} ({L.lanczos_iters} it) "
+                print(f"[mlamg] level {len(H.levels) - 1}: n={n} nnz={A_dev.nnz} "
+                      f"seeds={L.n_seeds} bf_sweeps={L.bf_sweeps} lam={L.lam} "
+                      f"({L.lanczos_iters} it) "
                       f"P nnz={L.P.nnz} -> n_c={A_next.shape[0]} nnz_c={A_next.nnz} "
                       f"[agg {t1 - t0:.2f}s lam {t2 - t1:.2f}s P {t3 - t2:.2f}s gal {t4 - t3:.2f}s]",
                       flush=True)
             A_dev = A_next
         H.Ac = A_dev
+        # host-side view of the SpGEMM phases (Galerkin + SA products), then drop the cached
+        # scratch blocks (several GB at C4) so the cycle phase does not hold them
+        H.spgemm_phases_ms = _setup_phases(reset=True)
+        call("mlamg_scratch_trim", None)
         if not finalize:  # setup only (e.g. to take P for a two-level cycle)
             return H
         t5 = time.perf_counter()
@@ -263,18 +344,57 @@ class Hierarchy:
         H.timings = tm
         return H
 
-    def _finalize(self, nu_pre, nu_post):
+    # coarsest solve: a dense inverse up to this many rows (its setup is O(n_c^3)), above it
+    # PCG preconditioned by an inner hierarchy of the coarse operator (csrc/pcg.hip)
+    DENSE_MAX = 4096
+    COARSE_RTOL = 1e-12
+
+    def _finalize(self, nu_pre, nu_post, dense_max=None, coarse_rtol=None):
         self.nu_pre, self.nu_post = nu_pre, nu_post
-        h = ctypes.c_void_p()
-        call("mlamg_dense_create", self.Ac.handle, ctypes.byref(h), stream_ptr())
-        self.dense = h
+        dense_max = self.DENSE_MAX if dense_max is None else dense_max
+        if self.Ac.shape[0] <= dense_max:
+            h = ctypes.c_void_p()
+            call("mlamg_dense_create", self.Ac.handle, ctypes.byref(h), stream_ptr())
+            self.dense = h
+        else:
+            self._make_coarse_pcg(self.COARSE_RTOL if coarse_rtol is None else coarse_rtol)
         hh = ctypes.c_void_p()
         call("mlamg_hier_create", ctypes.byref(hh))
         self.handle = hh
         for L in self.levels:
             call("mlamg_hier_add_level", hh, L.A.handle, ptr(L.dinv), L.P.handle, L.R.handle)
-        call("mlamg_hier_set_coarse", hh, self.Ac.handle, self.dense)
+        if self.dense is not None:
+            call("mlamg_hier_set_coarse", hh, self.Ac.handle, self.dense)
+        else:
+            call("mlamg_hier_set_coarse_pcg", hh, self.Ac.handle, self.pcg)
         call("mlamg_hier_set_smoothing", hh, int(nu_pre), int(nu_post))
+
+    def _make_coarse_pcg(self, rtol, maxit=200):
+        """Coarsest solve for an operator too large for the dense inverse (the reference
+        factorises any size with SuperLU, ns/lib/multigrid.py:168): PCG on A_c with one V-cycle
+        of an inner smoothed-aggregation hierarchy of A_c as preconditioner, to
+        ||r|| <= rtol ||b||. The inner hierarchy smooths with the per-level SA weight
+        w = (4/3)/lambda_max(D^-1 A) (w * lambda_max < 2: a convergent, symmetric V-cycle, i.e.
+        an SPD preconditioner for an SPD A_c)."""
+        self.inner = Hierarchy.build(self.Ac, alpha=0.1, max_coarse=1000, jacobi_weight="sa",
+                                     fine_format="csr_stream", coarse_format="exact")
+        h = ctypes.c_void_p()
+        call("mlamg_pcg_create", self.Ac.handle, self.inner.handle, float(rtol), int(maxit),
+             ctypes.byref(h))
+        self.pcg = h
+
+    def coarse_stats(self):
+        """PCG coarse solver statistics (None with a dense coarse inverse): iterations of the
+        last solve, solves that stopped at maxit, total iterations, largest final relative
+        residual."""
+        if getattr(self, "pcg", None) is None:
+            return None
+        a, b, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        d = ctypes.c_double()
+        call("mlamg_pcg_stats", self.pcg, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
+             ctypes.byref(d), stream_ptr())
+        return {"last_iters": a.value, "not_converged": b.value, "total_iters": c.value,
+                "max_rel_residual": d.value}
 
     # ------------------------------------------------------------------ cycling
     def cycle(self, b, x, n_cycles, tol=None, use_graph=True, history=True):
@@ -335,11 +455,13 @@ class Hierarchy:
                          "P_nnz": L.P.nnz, "omega": L.omega, "lambda_max": L.lam,
                          "lanczos_iters": L.lanczos_iters, "bf_sweeps": L.bf_sweeps})
         rows.append({"level": len(self.levels), "n": self.Ac.shape[0], "nnz": self.Ac.nnz,
-                     "coarse": "dense inverse"})
+                     "coarse": "dense inverse" if self.dense is not None
+                     else "PCG, inner SA hierarchy"})
         return rows
 
     def __del__(self):
-        for attr, fn in (("handle", "mlamg_hier_destroy"), ("dense", "mlamg_dense_destroy")):
+        for attr, fn in (("handle", "mlamg_hier_destroy"), ("dense", "mlamg_dense_destroy"),
+                         ("pcg", "mlamg_pcg_destroy")):
             h = getattr(self, attr, None)
             if h:
                 try:

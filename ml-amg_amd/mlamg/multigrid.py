@@ -8,6 +8,8 @@ come out, like the reference; `DeviceCSR` operands and torch cuda tensors are al
   gauss_seidel               ns/lib/multigrid.py:58-90 (pyamg gauss_seidel order)
   smoothed_aggregation_jacobi ns/lib/multigrid.py:102-108
   amg_2_v                    ns/lib/multigrid.py:111-210
+  jacobi_torch, gauss_seidel_torch, amg_2_v_torch   ns/lib/multigrid.py:48,93,213 (torch ops as
+                             in the reference; not on the V-cycle path)
 """
 from __future__ import annotations
 
@@ -344,3 +346,57 @@ def amg_2_v_jacobi(A, P, b, x, dinv_w=None, omega=2. / 3., pre_smoothing_steps=1
     hist = H.cycle(to_device_vec(b), xd, max_iter, tol=tol)
     out = xd.cpu().numpy()
     return (out, hist) if history else out
+
+
+# ---------------------------------------------------------------- torch variants (a5'')
+# ns/lib/multigrid.py:48-55, 93-98, 213-245: the fp32 torch-sparse paths of the GNN training
+# loop (train_dataset.py:111 branch). SURVEY.md §8(a) a5'' marks them "semantics only": they are
+# kept here as the same torch operations (they run wherever the caller's tensors live, the GPU
+# included) so that aliasing ns.lib.multigrid to this module leaves those callers working.
+def jacobi_torch(A, b, x, Dinv=None, omega=0.666, nu=2):
+    """ns/lib/multigrid.py:48-55 (x updated in place and returned). Dinv defaults to the stored
+    diagonal itself, exactly as the reference does."""
+    from .sparse import get_diagonal
+    if Dinv is None:
+        Dinv = get_diagonal(A)
+    for _ in range(nu):
+        x += omega * (Dinv * b) - omega * Dinv * (A @ x)
+    return x
+
+
+def gauss_seidel_torch(A, b, x, L=None, U=None, nu=2):
+    """ns/lib/multigrid.py:93-98: x = tril(A)^-1 (b - triu(A, 1) x), nu times (dense triangular
+    solve of the lower triangle, b as a column)."""
+    from .sparse import triu
+    if U is None:
+        U = triu(A, 1)
+    Ad = A.to_dense() if A.is_sparse else A
+    for _ in range(nu):
+        rhs = (b - U @ x).unsqueeze(1)
+        x = torch.linalg.solve_triangular(torch.tril(Ad), rhs, upper=False).squeeze(1)
+    return x
+
+
+def amg_2_v_torch(A, P, b, x, pre_smoothing_steps=1, post_smoothing_steps=1,
+                  jacobi_weight=0.666, error_tol=1e-10, max_iter=20):
+    """ns/lib/multigrid.py:213-245: two-level Jacobi cycle on torch sparse tensors with a dense
+    LU of P^T A P; returns (err[i] / err[i-3]) ** (1/2) like the reference (err = ||x||_2)."""
+    from .sparse import get_diagonal
+    device = A.device
+    Dinv = 1. / get_diagonal(A)
+    Pt = P.transpose(0, 1)
+    A_H = torch.sparse.mm(torch.sparse.mm(Pt, A), P).to_dense()
+    LU, piv = torch.linalg.lu_factor(A_H)
+    err = torch.zeros(max_iter, device=device)
+    i = 0
+    for i in range(max_iter):
+        x = jacobi_torch(A, b, x, Dinv, omega=jacobi_weight, nu=pre_smoothing_steps)
+        r_H = torch.unsqueeze(Pt.matmul(b - A @ x), 1)
+        e_H = torch.linalg.lu_solve(LU, piv, r_H)
+        x += P.matmul(e_H.squeeze())
+        x = jacobi_torch(A, b, x, Dinv, omega=jacobi_weight, nu=post_smoothing_steps)
+        err[i] = torch.linalg.norm(x)
+        if err[i] < error_tol:
+            break
+    n_err = 3
+    return (err[i] / err[i - n_err]) ** (1 / (n_err - 1))

@@ -1,6 +1,9 @@
 """Device CSR handles and the scipy/torch conversions of ns/lib/sparse.py.
 
 Reference: ns/lib/sparse.py:20-32 (to_torch_sparse: scipy -> torch COO with fp32 values),
+ns/lib/sparse.py:8,35,51,78 (col_normalize_csr, get_diagonal, triu, tril: the reference's own
+scipy / torch COO helpers, kept as they are so that aliasing ns.lib.sparse to this module
+leaves its callers — ns/model/data.py:127, demos/1d_poisson.py:106 — working),
 ns/lib/sparse.py:105-106 (scipy_to_torch / torch_to_scipy aliases), ns/lib/sparse_tensor.py:54-59
 (to_scipy: torch COO -> scipy CSR). The V-cycle itself never goes through torch COO: matrices are
 uploaded once as int32/fp64 CSR into a `DeviceCSR` (C handle `mlamg_csr`, include/mlamg.h).
@@ -237,6 +240,43 @@ def to_scipy(T):
     T = T.coalesce() if not T.is_coalesced() else T
     idx = T.indices().cpu().numpy()
     return sp.coo_matrix((T.values().cpu().numpy(), (idx[0], idx[1])), shape=tuple(T.shape)).tocsr()
+
+
+def col_normalize_csr(A_sp, ord=1):
+    """ns/lib/sparse.py:8-17: divide every nonzero by its column's `ord`-norm (scipy CSR)."""
+    import scipy.sparse.linalg as spla
+    if not sp.isspmatrix_csr(A_sp):
+        A_sp = A_sp.tocsr()
+    norms = spla.norm(A_sp, axis=0, ord=ord)
+    return sp.csr_matrix((A_sp.data / norms[A_sp.indices], A_sp.indices, A_sp.indptr), A_sp.shape)
+
+
+def get_diagonal(A_T, as_vector=True):
+    """ns/lib/sparse.py:35-48: diagonal entries of a torch sparse COO tensor (the stored ones, in
+    storage order), as a vector or as a sparse COO tensor. Runs where A_T lives."""
+    values = A_T.values()
+    indices = A_T.indices()
+    diag_entries = indices[0] == indices[1]
+    if as_vector:
+        return values[diag_entries]
+    return torch.sparse_coo_tensor(indices[:, diag_entries], values[diag_entries],
+                                   size=A_T.shape)
+
+
+def triu(A_T, diag=0):
+    """ns/lib/sparse.py:51-75: entries with col - row >= diag of a torch sparse COO tensor."""
+    values = A_T.values()
+    indices = A_T.indices()
+    keep = (indices[1] - indices[0]) >= diag
+    return torch.sparse_coo_tensor(indices[:, keep], values[keep], size=A_T.shape)
+
+
+def tril(A_T, diag=0):
+    """ns/lib/sparse.py:78-102: entries with row - col >= diag of a torch sparse COO tensor."""
+    values = A_T.values()
+    indices = A_T.indices()
+    keep = (indices[0] - indices[1]) >= diag
+    return torch.sparse_coo_tensor(indices[:, keep], values[keep], size=A_T.shape)
 
 
 scipy_to_torch = to_torch_sparse

@@ -485,3 +485,36 @@ def test_rowpat_format(ml, torch_cuda):
     xs2 = dev(torch, x)
     call("mlamg_jacobi", Ad.handle, ptr(d2), ptr(bd), ptr(xs2), ptr(t1), 1, stream_ptr())
     assert torch.equal(xs, xs2)
+
+
+def test_supplied_aggregates_and_prolongator(ml, oracle, torch_cuda):
+    """Hierarchy.build with supplied level-0 aggregates (C5: learned/supplied aggregates on the
+    jump-coefficient problem) and with a supplied P (the MLAMG PC's learned P,
+    ns/preconditioner/MLAMG.py:105-121): level-0 P = the oracle's SA prolongator of those
+    aggregates with the device omega (bitwise) / the given P itself; the cycle matches the
+    oracle's on the device's operators."""
+    torch = torch_cuda
+    m = 48
+    A = ml.problems.jump_2d(m, ml.problems.voronoi_jumps(np.random.RandomState(0)))
+    Agg = ml.problems.box_aggregates_2d(m, m, 3)
+    labels = np.asarray(Agg.argmax(axis=1)).ravel()
+    for spec in (labels, Agg):
+        H = ml.hierarchy.Hierarchy.build(A, aggregates=spec, max_coarse=60)
+        assert H.levels[0].n_seeds == Agg.shape[1]
+        P_ref, _ = oracle.smoothed_aggregation_jacobi(A, Agg, omega=H.levels[0].omega)
+        Pd = H.levels[0].P.to_scipy()
+        assert np.array_equal(Pd.indptr, P_ref.indptr) and np.array_equal(Pd.data, P_ref.data)
+    lv = _oracle_levels_from_device(H)
+    n = A.shape[0]
+    x0 = np.random.RandomState(0).randn(n)
+    b = np.random.RandomState(1).randn(n)
+    xo, ho = oracle.vcycle_solve(lv, H.Ac.to_scipy(), b, x0, 5)
+    xd = dev(torch, x0)
+    hd = H.cycle(dev(torch, b), xd, 5)
+    assert np.allclose(hd, ho, rtol=1e-11, atol=0)
+    # a supplied P is used as given (no smoothing)
+    H2 = ml.hierarchy.Hierarchy.build(A, prolongators=[P_ref], max_levels=2)
+    P2 = H2.levels[0].P.to_scipy()
+    assert np.array_equal(P2.data, P_ref.data) and np.array_equal(P2.indices, P_ref.indices)
+    with pytest.raises(ValueError):
+        ml.hierarchy.Hierarchy.build(A, aggregates=labels[:-1])
