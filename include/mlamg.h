@@ -274,6 +274,34 @@ int mlamg_pcg_stats(const mlamg_pcg* C, int32_t* last_iters, int32_t* not_conver
 /* use the PCG solver C (size = A_coarse rows) as H's coarsest solve instead of a dense inverse;
  * cycles of such a hierarchy run eagerly (use_graph is ignored) */
 int mlamg_hier_set_coarse_pcg(mlamg_hier* H, const mlamg_csr* A_coarse, mlamg_pcg* C);
+/* ---------------------------------------------------------------- batched reference solves
+ * The reference's own call pattern — two-level amg_2_v(A, P, b, x, ...) on small grids
+ * (ns/lib/multigrid.py:111-210, called per grid by utils/common.py:77,106,
+ * utils/evaluate_dataset.py:96, utils/train_dataset.py:114) — for a whole batch of problems in
+ * ONE kernel launch, one workgroup per problem: Galerkin P^T A P, dense coarse inverse, every
+ * cycle and the tolerance test on the device (csrc/batch.hip). All arrays are HOST memory (the
+ * caller's scipy/numpy buffers); the call packs them, copies them in once, runs, copies the
+ * results out and returns (synchronous on `stream`). Limits: mlamg_amg2v_batch_limits. */
+typedef struct mlamg_amg2v_problem {
+  int64_t n, n_c;                                          /* A is n x n, P is n x n_c */
+  const int32_t* A_indptr; const int32_t* A_indices; const double* A_data; int64_t A_nnz;
+  const int32_t* P_indptr; const int32_t* P_indices; const double* P_data; int64_t P_nnz;
+  const double* b; const double* x0;                       /* length n */
+  double* x_out;                                           /* length n */
+  double* err_out;                                         /* length max_iter; err[:iters] written */
+  int32_t iters_out;                                       /* len(err) */
+  int32_t status_out;                                      /* 0 ok, 1 A_H exactly singular (x = x0,
+                                                              iters 0: multigrid.py:167-170) */
+} mlamg_amg2v_problem;
+/* smoother 0 = pyamg forward Gauss-Seidel (the reference's), 1 = weighted Jacobi
+ * x += w D^-1 (b - A x) (MLAMG.py:143-146 form, w = jacobi_weight); norm_mode 0 = res_tol
+ * (||b - A x||_2), 1 = error_tol (||x||_2); stop after the first cycle with norm <= tol
+ * (tol < 0: never). */
+int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int nu_pre,
+                      int nu_post, double jacobi_weight, int norm_mode, double tol, int max_iter,
+                      void* stream);
+/* largest n, n_c and off-diagonal entries per row of A the batched solver accepts */
+int mlamg_amg2v_batch_limits(int64_t* max_rows, int64_t* max_coarse, int* max_row_entries);
 /* what res_hist records each cycle: 0 = ||b - A x||_2 (default, MLAMG.py:194 / res_tol),
  * 1 = ||x||_2 (amg_2_v error_tol, multigrid.py:193); the tolerance test applies to it */
 int mlamg_hier_set_norm(mlamg_hier* H, int mode);

@@ -48,6 +48,18 @@ P_i64 = ctypes.POINTER(ctypes.c_int64)
 P_dbl = ctypes.POINTER(ctypes.c_double)
 P_int = ctypes.POINTER(ctypes.c_int)
 
+class Amg2vProblem(ctypes.Structure):
+    """mlamg_amg2v_problem (include/mlamg.h)."""
+    _fields_ = [("n", ctypes.c_int64), ("n_c", ctypes.c_int64),
+                ("A_indptr", ctypes.c_void_p), ("A_indices", ctypes.c_void_p),
+                ("A_data", ctypes.c_void_p), ("A_nnz", ctypes.c_int64),
+                ("P_indptr", ctypes.c_void_p), ("P_indices", ctypes.c_void_p),
+                ("P_data", ctypes.c_void_p), ("P_nnz", ctypes.c_int64),
+                ("b", ctypes.c_void_p), ("x0", ctypes.c_void_p),
+                ("x_out", ctypes.c_void_p), ("err_out", ctypes.c_void_p),
+                ("iters_out", ctypes.c_int32), ("status_out", ctypes.c_int32)]
+
+
 # name -> (restype, argtypes); every symbol of include/mlamg.h
 SIGNATURES = {
     "mlamg_version": (c_int, []),
@@ -99,6 +111,9 @@ SIGNATURES = {
     "mlamg_hier_destroy": (c_int, [c_vp]),
     "mlamg_hier_add_level": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mlamg_hier_set_coarse": (c_int, [c_vp, c_vp, c_vp]),
+    "mlamg_amg2v_batch": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_dbl, c_int, c_dbl, c_int,
+                                  c_vp]),
+    "mlamg_amg2v_batch_limits": (c_int, [P_i64, P_i64, P_int]),
     "mlamg_hier_set_coarse_pcg": (c_int, [c_vp, c_vp, c_vp]),
     "mlamg_pcg_create": (c_int, [c_vp, c_vp, c_dbl, c_int, c_vpp]),
     "mlamg_pcg_destroy": (c_int, [c_vp]),

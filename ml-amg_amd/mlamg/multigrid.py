@@ -258,6 +258,91 @@ def _amg_2_v_singular(A, P, b, x, nu_pre, nu_post, jacobi_weight, res_tol, tol, 
     return xd.cpu().numpy(), conv_factor(err), err, len(err)
 
 
+_BATCH_LIMITS = None
+
+
+def _batch_limits():
+    global _BATCH_LIMITS
+    if _BATCH_LIMITS is None:
+        n, nc, k = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
+        call("mlamg_amg2v_batch_limits", ctypes.byref(n), ctypes.byref(nc), ctypes.byref(k))
+        _BATCH_LIMITS = (int(n.value), int(nc.value), int(k.value))
+    return _BATCH_LIMITS
+
+
+def _host_problem(A, P, b, x):
+    """Host CSR / vector arrays of one amg_2_v problem in the layout the batched kernel takes
+    (int32 indices, fp64 values, duplicate-free rows in their stored order)."""
+    from .sparse import canonical_rows
+    if sp.issparse(A) and sp.issparse(P):
+        A = canonical_rows(A)
+        P = sp.csr_matrix(P) if not sp.isspmatrix_csr(P) else P
+        arrs = []
+        for M in (A, P):
+            arrs.append((np.ascontiguousarray(M.indptr, dtype=np.int32),
+                         np.ascontiguousarray(M.indices, dtype=np.int32),
+                         np.ascontiguousarray(M.data, dtype=np.float64)))
+        bv = np.ascontiguousarray(np.asarray(b, dtype=np.float64).ravel())
+        xv = np.ascontiguousarray(np.asarray(x, dtype=np.float64).ravel())
+        return A.shape, P.shape, arrs, bv, xv
+    return None
+
+
+def _fused_eligible(A, P, singular):
+    if singular or not (sp.issparse(A) and sp.issparse(P)):
+        return False
+    max_n, max_nc, _ = _batch_limits()
+    n, nc = A.shape[0], P.shape[1]
+    return (A.shape[0] == A.shape[1] == P.shape[0] and 1 <= n <= max_n and 1 <= nc <= max_nc
+            and nc <= n and A.nnz < 2**31 and P.nnz < 2**31)
+
+
+def _amg_2_v_fused(items, pre, post, jacobi_weight, res_tol, error_tol, max_iter, smoother):
+    """Run amg_2_v on every (A, P, b, x) of `items` in ONE device launch (csrc/batch.hip): one
+    workgroup per problem does its Galerkin product, coarse inverse, cycles and tolerance test.
+    Returns a list of (x, conv_factor, err, iters), or None when a problem is outside the
+    kernel's limits (the caller then takes the hierarchy path)."""
+    from ._lib import Amg2vProblem
+    tol = res_tol if res_tol is not None else error_tol
+    probs = (Amg2vProblem * len(items))()
+    keep = []
+    outs = []
+    for q, (A, P, b, x) in enumerate(items):
+        hp = _host_problem(A, P, b, x)
+        if hp is None:
+            return None
+        (n, _), (_, nc), ((aip, aij, av), (pip, pij, pv)), bv, xv = hp
+        xo = np.empty(n)
+        eo = np.empty(max(max_iter, 1))
+        keep.append((aip, aij, av, pip, pij, pv, bv, xv))
+        outs.append((xo, eo))
+        pr = probs[q]
+        pr.n, pr.n_c = n, nc
+        pr.A_indptr, pr.A_indices, pr.A_data = aip.ctypes.data, aij.ctypes.data, av.ctypes.data
+        pr.A_nnz = int(aij.size)
+        pr.P_indptr, pr.P_indices, pr.P_data = pip.ctypes.data, pij.ctypes.data, pv.ctypes.data
+        pr.P_nnz = int(pij.size)
+        pr.b, pr.x0 = bv.ctypes.data, xv.ctypes.data
+        pr.x_out, pr.err_out = xo.ctypes.data, eo.ctypes.data
+    rc = _lib.lib.mlamg_amg2v_batch(probs, len(items), 0 if smoother == "gauss_seidel" else 1,
+                                    int(pre), int(post), float(jacobi_weight),
+                                    0 if res_tol is not None else 1, float(tol), int(max_iter),
+                                    stream_ptr())
+    if rc == _lib.MLAMG_EUNSUPPORTED:
+        return None
+    _lib.check(rc, "mlamg_amg2v_batch")
+    res = []
+    for q, (A, P, b, x) in enumerate(items):
+        xo, eo = outs[q]
+        if probs[q].status_out == 1:  # factorisation failure: multigrid.py:167-170
+            res.append((x, np.float64(1.), np.zeros(max_iter), 0))
+            continue
+        it = int(probs[q].iters_out)
+        err = eo[:it].copy() if it < max_iter else eo[:max_iter].copy()
+        res.append((xo, conv_factor(err), err, len(err)))
+    return res
+
+
 def amg_2_v(A, P, b, x,
             pre_smoothing_steps=1,
             post_smoothing_steps=1,
@@ -266,19 +351,33 @@ def amg_2_v(A, P, b, x,
             error_tol=None,
             max_iter=500,
             singular=False,
-            *, smoother="gauss_seidel", use_graph=True):
+            *, smoother="gauss_seidel", use_graph=True, engine="auto"):
     """Two-level AMG solver, ns/lib/multigrid.py:111-210, on the GPU.
 
     smoother='gauss_seidel' (reference default: pyamg forward GS, :175,184) or 'jacobi'
     (weighted Jacobi x += w*Dinv(b - A x) with w = jacobi_weight, the MLAMG.py:143-146 form).
-    Returns (x, conv_factor, err, num_iterations) exactly like the reference. use_graph=False
-    launches the cycles eagerly instead of replaying a captured hipGraph (same kernels, same bits).
+    Returns (x, conv_factor, err, num_iterations) exactly like the reference.
+
+    engine='auto' runs problems within mlamg_amg2v_batch_limits (the reference's small-grid
+    calls) as ONE fused device launch (csrc/batch.hip) and larger ones through a device
+    Hierarchy (one kernel per operation; the coarse solve switches to PCG past
+    Hierarchy.DENSE_MAX rows); 'fused' / 'hierarchy' force one of them. use_graph=False
+    (hierarchy engine) launches the cycles eagerly instead of replaying a captured hipGraph.
     """
     if res_tol is None and error_tol is None:
         raise RuntimeError('One of res_tol or error_tol must be set!')
     tol = res_tol if res_tol is not None else error_tol
     if smoother not in ("gauss_seidel", "jacobi"):
         raise ValueError(f"unknown smoother {smoother!r}")
+    if engine not in ("auto", "fused", "hierarchy"):
+        raise ValueError(f"unknown engine {engine!r}")
+    if engine != "hierarchy" and _fused_eligible(A, P, singular):
+        out = _amg_2_v_fused([(A, P, b, x)], pre_smoothing_steps, post_smoothing_steps,
+                             jacobi_weight, res_tol, error_tol, max_iter, smoother)
+        if out is not None:
+            return out[0]
+    if engine == "fused":
+        raise ValueError("problem outside the fused solver's limits (mlamg_amg2v_batch_limits)")
     if singular:
         return _amg_2_v_singular(A, P, b, x, pre_smoothing_steps, post_smoothing_steps,
                                  jacobi_weight, res_tol, tol, max_iter, smoother)
@@ -308,9 +407,44 @@ def amg_2_v_batch(problems, workers=8, **kw):
     release the GIL; scratch buffers are per thread), so the small latency-bound solves overlap.
 
     problems: iterable of (A, P, b, x) tuples; keyword arguments as amg_2_v. Returns the list of
-    (x, conv_factor, err, num_iterations) in input order, each equal to a sequential amg_2_v."""
+    (x, conv_factor, err, num_iterations) in input order, each equal to a sequential amg_2_v.
+
+    Problems within the fused solver's limits (all of the reference's small-grid datasets) run
+    together in ONE launch, one workgroup each (csrc/batch.hip); the rest go through the
+    threaded per-problem path below."""
     import threading
     from concurrent.futures import ThreadPoolExecutor
+    problems = list(problems)
+    engine = kw.pop("engine", "auto")
+    if engine != "hierarchy" and problems:
+        opts = dict(pre_smoothing_steps=1, post_smoothing_steps=1, jacobi_weight=0.666,
+                    res_tol=None, error_tol=None, max_iter=500, singular=False,
+                    smoother="gauss_seidel")
+        unknown = set(kw) - set(opts) - {"use_graph"}
+        if unknown:
+            raise TypeError(f"unexpected keyword arguments {sorted(unknown)}")
+        opts.update({k: v for k, v in kw.items() if k in opts})
+        if opts["res_tol"] is None and opts["error_tol"] is None:
+            raise RuntimeError('One of res_tol or error_tol must be set!')
+        idx = [i for i, (A, P, b, x) in enumerate(problems)
+               if _fused_eligible(A, P, opts["singular"])]
+        results = [None] * len(problems)
+        if idx:
+            out = _amg_2_v_fused([problems[i] for i in idx], opts["pre_smoothing_steps"],
+                                 opts["post_smoothing_steps"], opts["jacobi_weight"],
+                                 opts["res_tol"], opts["error_tol"], opts["max_iter"],
+                                 opts["smoother"])
+            if out is not None:
+                for i, o in zip(idx, out):
+                    results[i] = o
+        rest = [i for i in range(len(problems)) if results[i] is None]
+        if not rest:
+            return results
+        sub = amg_2_v_batch([problems[i] for i in rest], workers=workers, engine="hierarchy",
+                            **kw)
+        for i, o in zip(rest, sub):
+            results[i] = o
+        return results
     dev = torch.cuda.current_device()
     local = threading.local()
 
@@ -321,13 +455,12 @@ def amg_2_v_batch(problems, workers=8, **kw):
         with torch.cuda.stream(local.stream):
             # eager launches: a stream capture must not overlap the other threads' synchronous
             # setup calls (allocations, blocking copies), and concurrency already hides launches
-            out = amg_2_v(*args, use_graph=False, **kw)
+            out = amg_2_v(*args, use_graph=False, engine="hierarchy", **kw)
         local.stream.synchronize()
         return out
 
-    problems = list(problems)
     if workers <= 1 or len(problems) <= 1:
-        return [amg_2_v(*args, **kw) for args in problems]
+        return [amg_2_v(*args, engine="hierarchy", **kw) for args in problems]
     with ThreadPoolExecutor(max_workers=int(workers)) as ex:
         return list(ex.map(run, problems))
 

@@ -39,3 +39,148 @@ def test_batch_equals_sequential(oracle, smoother):
         assert its == itb and np.array_equal(es, eb), i
         assert np.array_equal(xs, xb), i
         assert cs == cb or (np.isnan(cs) and np.isnan(cb)), i
+
+
+@pytest.mark.parametrize("smoother", ("gauss_seidel", "jacobi"))
+def test_threaded_engine_equals_sequential(oracle, smoother):
+    """The per-problem (hierarchy) engine of amg_2_v_batch: host threads, one stream each."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mlamg.multigrid
+    import mlamg.problems
+    import mlamg as ml
+    probs = _problems(ml, oracle, 8)
+    seq = [ml.multigrid.amg_2_v(A, P, b, x.copy(), res_tol=1e-10, smoother=smoother,
+                                engine="hierarchy") for A, P, b, x in probs]
+    bat = ml.multigrid.amg_2_v_batch([(A, P, b, x.copy()) for A, P, b, x in probs], workers=4,
+                                     res_tol=1e-10, smoother=smoother, engine="hierarchy")
+    for i, ((xs, cs, es, its), (xb, cb, eb, itb)) in enumerate(zip(seq, bat)):
+        assert its == itb and np.array_equal(es, eb) and np.array_equal(xs, xb), i
+
+
+@pytest.mark.parametrize("smoother", ("gauss_seidel", "jacobi"))
+@pytest.mark.parametrize("mode", ("res", "err"))
+def test_fused_matches_oracle_and_hierarchy(oracle, smoother, mode):
+    """The fused one-launch solver (csrc/batch.hip) vs the oracle's amg_2_v (SuperLU coarse
+    solve) and vs the per-operation hierarchy engine: same iteration counts, histories within
+    rtol 1e-10 (Galerkin + dense inverse vs scipy + SuperLU: rounding only), conv factors within
+    1e-8, iterates within 1e-9 of their max. Smoothing/restriction/prolongation are bitwise
+    scipy's, so any larger deviation is a bug, not rounding."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mlamg.multigrid
+    import mlamg.problems
+    import mlamg as ml
+    kw = {"res_tol": 1e-10} if mode == "res" else {"error_tol": 1e-8}
+    for m, agg in ((17, 3), (40, 3), (64, 2), (90, 3)):
+        A = ml.problems.poisson_2d_5pt(m)
+        P, _ = oracle.smoothed_aggregation_jacobi(A, ml.problems.box_aggregates_2d(m, m, agg),
+                                                  omega=2.0 / 3.0)
+        x0 = np.random.RandomState(m).randn(A.shape[0])
+        x0 /= np.linalg.norm(x0)
+        # b = 0 (the reference's evaluation loops, utils/common.py:48): x -> 0, so the history
+        # keeps its relative accuracy down to the tolerance; with b != 0 the residual's rounding
+        # floor eps*|A||x| is reached near res_tol and the tail is not comparable to 1e-10
+        b = np.zeros(A.shape[0])
+        xr, cr, er, ir = oracle.amg_2_v(A, P, b, x0, smoother=smoother, jacobi_weight=0.666,
+                                        max_iter=200, **kw)
+        xf, cf, ef, itf = ml.multigrid.amg_2_v(A, P, b, x0, smoother=smoother, max_iter=200,
+                                               engine="fused", **kw)
+        xh, ch, eh, ith = ml.multigrid.amg_2_v(A, P, b, x0, smoother=smoother, max_iter=200,
+                                               engine="hierarchy", **kw)
+        assert itf == ir == ith, (m, itf, ir, ith)
+        for e in (ef, eh):
+            assert np.allclose(e, er, rtol=1e-10, atol=1e-14 * er[0]), (m, e, er)
+        assert abs(cf - cr) <= 1e-8 and abs(ch - cr) <= 1e-8
+        scale = max(np.abs(xr).max(), 1e-300)
+        assert np.abs(xf - xr).max() <= 1e-9 * scale + 1e-14
+        assert np.abs(xf - xh).max() <= 1e-9 * scale + 1e-14
+    # a nonzero right-hand side: the solution itself (x -> A^-1 b = xs) agrees
+    m = 48
+    A = ml.problems.poisson_2d_5pt(m)
+    P, _ = oracle.smoothed_aggregation_jacobi(A, ml.problems.box_aggregates_2d(m, m, 3),
+                                              omega=2.0 / 3.0)
+    xs = np.random.RandomState(1).randn(A.shape[0])
+    x0 = np.zeros(A.shape[0])
+    xr, cr, er, ir = oracle.amg_2_v(A, P, A @ xs, x0, smoother=smoother, max_iter=60, **kw)
+    xf, cf, ef, itf = ml.multigrid.amg_2_v(A, P, A @ xs, x0, smoother=smoother, max_iter=60,
+                                           engine="fused", **kw)
+    assert np.abs(xf - xr).max() <= 1e-9 * np.abs(xs).max()
+    assert np.allclose(ef[:10], er[:10], rtol=1e-10, atol=0)
+
+
+def test_fused_batch_mixed_sizes_bitwise_single(oracle):
+    """One launch over problems of different sizes equals one launch per problem, bit for bit
+    (each workgroup owns its problem)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mlamg.multigrid
+    import mlamg.problems
+    import mlamg as ml
+    probs = _problems(ml, oracle, 21)
+    one = [ml.multigrid.amg_2_v(A, P, b, x, res_tol=1e-10, engine="fused") for A, P, b, x in probs]
+    bat = ml.multigrid.amg_2_v_batch(probs, res_tol=1e-10)
+    for i, (a, c) in enumerate(zip(one, bat)):
+        assert a[3] == c[3] and np.array_equal(a[2], c[2]) and np.array_equal(a[0], c[0]), i
+
+
+def test_fused_edge_cases(oracle):
+    """Singular Galerkin operator -> (x, 1.0, zeros, 0) like the reference's failed
+    factorisation (multigrid.py:167-170); max_iter 0 and 1 (conv-factor quirks); a row with more
+    than 32 off-diagonals falls back to the hierarchy engine with the same results."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import scipy.sparse as sp
+    import mlamg.multigrid
+    import mlamg.problems
+    import mlamg as ml
+    m = 20
+    A = ml.problems.poisson_2d_5pt(m)
+    Agg = ml.problems.box_aggregates_2d(m, m, 4)
+    P = sp.hstack([sp.csr_matrix(Agg, dtype=np.float64),
+                   sp.csr_matrix((A.shape[0], 1))]).tocsr()     # an empty coarse column
+    x0 = np.random.RandomState(0).randn(A.shape[0])
+    x, c, e, it = ml.multigrid.amg_2_v(A, P, np.zeros(A.shape[0]), x0, res_tol=1e-10)
+    xr, cr, er, ir = oracle.amg_2_v(A, P, np.zeros(A.shape[0]), x0, res_tol=1e-10)
+    assert (it, c) == (ir, cr) == (0, 1.0) and np.array_equal(x, x0) and not np.any(e)
+    P2, _ = oracle.smoothed_aggregation_jacobi(A, Agg, omega=2.0 / 3.0)
+    for mi in (0, 1, 2):
+        got = ml.multigrid.amg_2_v(A, P2, np.zeros(A.shape[0]), x0, res_tol=1e-300, max_iter=mi)
+        ref = oracle.amg_2_v(A, P2, np.zeros(A.shape[0]), x0, res_tol=1e-300, max_iter=mi)
+        assert got[3] == ref[3] == mi and len(got[2]) == mi
+        assert np.allclose(got[1], ref[1], rtol=1e-10, atol=0)
+    # a dense-ish operator: 40 off-diagonals per row -> hierarchy engine (same answers)
+    rs = np.random.RandomState(5)
+    n = 300
+    B = sp.random(n, n, density=40 / n, random_state=rs, format="csr")
+    Ad = (B + B.T + sp.diags(np.full(n, 100.0))).tocsr()
+    Pd, _ = oracle.smoothed_aggregation_jacobi(
+        Ad, sp.csr_matrix((np.ones(n), (np.arange(n), np.arange(n) // 5))), omega=2.0 / 3.0)
+    xa = ml.multigrid.amg_2_v(Ad, Pd, np.zeros(n), x0[:n], res_tol=1e-10)
+    xb = ml.multigrid.amg_2_v(Ad, Pd, np.zeros(n), x0[:n], res_tol=1e-10, engine="hierarchy")
+    assert xa[3] == xb[3] and np.array_equal(xa[2], xb[2])
+
+
+def test_fused_wide_coarse(oracle):
+    """n_c = 2025 (> 1024 + panel: the column-per-thread update branch of the blocked
+    Gauss-Jordan) and n = 8100 with 2x2 aggregates, vs the oracle."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mlamg.multigrid
+    import mlamg.problems
+    import mlamg as ml
+    m = 90
+    A = ml.problems.poisson_2d_5pt(m)
+    P, _ = oracle.smoothed_aggregation_jacobi(A, ml.problems.box_aggregates_2d(m, m, 2),
+                                              omega=2.0 / 3.0)
+    assert P.shape[1] == 2025
+    x0 = np.random.RandomState(3).randn(A.shape[0])
+    xr, cr, er, ir = oracle.amg_2_v(A, P, np.zeros(A.shape[0]), x0, res_tol=1e-10)
+    xf, cf, ef, itf = ml.multigrid.amg_2_v(A, P, np.zeros(A.shape[0]), x0, res_tol=1e-10,
+                                           engine="fused")
+    assert itf == ir and np.allclose(ef, er, rtol=1e-10, atol=0) and abs(cf - cr) <= 1e-8
