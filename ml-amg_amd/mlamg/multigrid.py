@@ -288,10 +288,21 @@ def _host_problem(A, P, b, x):
     return None
 
 
-def _fused_eligible(A, P, singular):
+# Engine choice for engine='auto' (measured on MI355X, profiles/r02/amg2v_timing.json): one
+# workgroup runs a whole fused solve, so a single call pays its coarse inverse (O(n_c^3) on one
+# CU) and its serial sweep levels alone — it beats the per-operation hierarchy engine up to
+# n_c ~ 256 (32^2: 3.0 vs 6.3 ms; 64^2, n_c = 484: 15 vs 11 ms). In a batch the problems run
+# side by side on the CUs, so up to n_c = 1024 the fused launch wins by a wide margin (48 grids
+# 32^2-64^2: 28 ms vs 190 ms for 16 threads of the hierarchy engine).
+FUSED_SINGLE_MAX_NC = 256
+FUSED_BATCH_MAX_NC = 1024
+
+
+def _fused_eligible(A, P, singular, max_nc=None):
     if singular or not (sp.issparse(A) and sp.issparse(P)):
         return False
-    max_n, max_nc, _ = _batch_limits()
+    max_n, lim_nc, _ = _batch_limits()
+    max_nc = lim_nc if max_nc is None else min(max_nc, lim_nc)
     n, nc = A.shape[0], P.shape[1]
     return (A.shape[0] == A.shape[1] == P.shape[0] and 1 <= n <= max_n and 1 <= nc <= max_nc
             and nc <= n and A.nnz < 2**31 and P.nnz < 2**31)
@@ -371,7 +382,8 @@ def amg_2_v(A, P, b, x,
         raise ValueError(f"unknown smoother {smoother!r}")
     if engine not in ("auto", "fused", "hierarchy"):
         raise ValueError(f"unknown engine {engine!r}")
-    if engine != "hierarchy" and _fused_eligible(A, P, singular):
+    if engine != "hierarchy" and _fused_eligible(
+            A, P, singular, None if engine == "fused" else FUSED_SINGLE_MAX_NC):
         out = _amg_2_v_fused([(A, P, b, x)], pre_smoothing_steps, post_smoothing_steps,
                              jacobi_weight, res_tol, error_tol, max_iter, smoother)
         if out is not None:
@@ -427,7 +439,8 @@ def amg_2_v_batch(problems, workers=8, **kw):
         if opts["res_tol"] is None and opts["error_tol"] is None:
             raise RuntimeError('One of res_tol or error_tol must be set!')
         idx = [i for i, (A, P, b, x) in enumerate(problems)
-               if _fused_eligible(A, P, opts["singular"])]
+               if _fused_eligible(A, P, opts["singular"],
+                                  None if engine == "fused" else FUSED_BATCH_MAX_NC)]
         results = [None] * len(problems)
         if idx:
             out = _amg_2_v_fused([problems[i] for i in idx], opts["pre_smoothing_steps"],
