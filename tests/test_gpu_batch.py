@@ -1,7 +1,8 @@
 """GPU: many independent reference-style amg_2_v solves at once (mlamg.multigrid.amg_2_v_batch —
-the reference's per-grid task farm, ns/parallel/pool.py, as host threads with one HIP stream each
-on one GPU). Every result must equal the sequential call bit for bit: concurrent solves share no
-buffer (per-thread scratch, per-handle work buffers)."""
+the reference's per-grid task farm, ns/parallel/pool.py): one fused launch for the whole batch
+(csrc/batch.hip, a workgroup per problem), or host threads with one HIP stream each over the
+hierarchy engine. Every result must equal the sequential call of the same engine bit for bit,
+and both engines match the oracle within the stated fp64 tolerances."""
 import numpy as np
 import pytest
 
@@ -30,8 +31,10 @@ def test_batch_equals_sequential(oracle, smoother):
     import mlamg.problems
     import mlamg as ml
     probs = _problems(ml, oracle, 14)
-    seq = [ml.multigrid.amg_2_v(A, P, b, x.copy(), res_tol=1e-10, smoother=smoother)
-           for A, P, b, x in probs]
+    # the batch runs every problem through the fused kernel (n_c <= FUSED_BATCH_MAX_NC); single
+    # calls pick their engine by size, so they are asked for the fused one explicitly
+    seq = [ml.multigrid.amg_2_v(A, P, b, x.copy(), res_tol=1e-10, smoother=smoother,
+                                engine="fused") for A, P, b, x in probs]
     bat = ml.multigrid.amg_2_v_batch([(A, P, b, x.copy()) for A, P, b, x in probs], workers=6,
                                      res_tol=1e-10, smoother=smoother)
     assert len(bat) == len(seq)
