@@ -31,9 +31,17 @@
 // the kernel.
 #include "common.hpp"
 
+#include <sched.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
 namespace mlamg {
@@ -52,6 +60,10 @@ constexpr size_t kBLdsBytes = 156 * 1024;
 struct BDesc {
   int32_t n, nc, smoother, nu_pre, nu_post, norm_mode, max_iter;
   int32_t K, KA, KP, KT, nlev, panel, n_chunks, cap, timing;
+  int32_t spd;    // A symmetric: try the inverse Cholesky factor before Gauss-Jordan
+  int32_t chol_nb;  // its panel width (4..32, from n_c)
+  int32_t gs_rw;  // one-wave sweep (rows of K = 4 or 8 slots, levels <= 64 * gs_rw rows), 1 or 2
+                  // rows per lane; 0: the workgroup sweeps each level
   double tol, omega;
   // byte offsets into the arena; packed arrays are slot-major: a[s * rows + row]
   int64_t ak_col, ak_val;                  // A rows, stored order incl. diagonal (KA slots)
@@ -147,6 +159,85 @@ __device__ __forceinline__ double packed_dot(const int32_t* __restrict__ col,
   return y;
 }
 
+// packed_dot for R rows at once (rows[u] < 0: no row): every row's loads of a slot group are
+// issued before any gather, so R rows cost the round trips of one; each row sums in slot order
+template <int R>
+__device__ __forceinline__ void packed_dot_rows(const int32_t* __restrict__ col,
+                                                const double* __restrict__ val, int stride,
+                                                const int* rows, int width, const double* src,
+                                                double* y) {
+  constexpr int G = R >= 4 ? 2 : 4;  // R * G slots in flight: registers stay below 128
+#pragma unroll
+  for (int u = 0; u < R; ++u) y[u] = 0.0;
+  for (int k0 = 0; k0 < width; k0 += G) {
+    int c[R][G];
+    double v[R][G], g[R][G];
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+#pragma unroll
+      for (int q = 0; q < G; ++q) {
+        const bool in = rows[u] >= 0 && k0 + q < width;
+        const int at = (k0 + q) * stride + (rows[u] >= 0 ? rows[u] : 0);
+        c[u][q] = in ? col[at] : -1;
+        v[u][q] = in ? val[at] : 0.0;
+      }
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+#pragma unroll
+      for (int q = 0; q < G; ++q) g[u][q] = src[c[u][q] >= 0 ? c[u][q] : 0];
+    bool more = false;
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+#pragma unroll
+      for (int q = 0; q < G; ++q)
+        if (c[u][q] >= 0) y[u] += v[u][q] * g[u][q];
+      more |= c[u][G - 1] >= 0;
+    }
+    if (!more) break;
+  }
+}
+
+// out[j] = sum over the row's span of M[j][k] v[k], a wave per row, lane-strided partial sums in
+// k then a butterfly (fixed order); two rows per wave in flight. SPAN 0: [0, nc) (the
+// Gauss-Jordan inverse), 1: [0, j] (L^-1, lower), 2: [j, nc) (L^-T, upper).
+template <int SPAN>
+__device__ __forceinline__ void rows_dot(const double* __restrict__ M, int nc,
+                                         const double* v, double* out, int tid) {
+  const int w = tid >> 6, lane = tid & 63;
+  for (int j = w; j < nc; j += 2 * kBWaves) {
+    const int jb = j + kBWaves;
+    const bool two = jb < nc;
+    const int lo1 = SPAN == 2 ? j : 0, hi1 = SPAN == 1 ? j + 1 : nc;
+    const int lo2 = SPAN == 2 ? jb : 0, hi2 = two ? (SPAN == 1 ? jb + 1 : nc) : 0;
+    const double* r1 = M + (int64_t)j * nc;
+    const double* r2 = M + (int64_t)(two ? jb : j) * nc;
+    double s1 = 0.0, s2 = 0.0;
+    for (int o = 0; lo1 + o < hi1 || lo2 + o < hi2; o += 4 * 64) {
+      double m1[4], x1[4], m2[4], x2[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k1 = lo1 + o + lane + u * 64, k2 = lo2 + o + lane + u * 64;
+        const bool in1 = k1 < hi1, in2 = k2 < hi2;
+        m1[u] = in1 ? r1[k1] : 0.0;
+        x1[u] = in1 ? v[k1] : 0.0;
+        m2[u] = in2 ? r2[k2] : 0.0;
+        x2[u] = in2 ? v[k2] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s1 = fma(m1[u], x1[u], s1);
+        s2 = fma(m2[u], x2[u], s2);
+      }
+    }
+    s1 = bw_sum(s1);
+    s2 = bw_sum(s2);
+    if (lane == 0) {
+      out[j] = s1;
+      if (two) out[jb] = s2;
+    }
+  }
+}
+
 // rows [i0, i1) of column j: M[i][j] = (i in the panel rows ? 0 : M[i][j]) + sum_t pan[i][t] B[t]
 // (t ascending, fused multiply-adds: the inverse is a dense-coarse substitute for SuperLU, held
 // to a tolerance, not to scipy's roundings), logical row i stored at physical row phys[i].
@@ -195,43 +286,167 @@ __device__ __forceinline__ void panel_update(double* AH, const double* pan, int 
   }
 }
 
-// one workgroup per problem: Galerkin product and coarse inverse
-__global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ descs,
-                                                     char* __restrict__ arena) {
-  extern __shared__ double lds[];
-  __shared__ double redv[kBWaves];
-  __shared__ int redi[kBWaves];
-  const BDesc D = descs[blockIdx.x];
-  const int tid = threadIdx.x;
-  const int n = D.n, nc = D.nc;
-  const double* __restrict__ b = at<double>(arena, D.b);
-  double* AH = at<double>(arena, D.AH);
-  double* AI = at<double>(arena, D.AI);
-  double* x_out = at<double>(arena, D.x_out);
-  double* err = at<double>(arena, D.err_out);
-  int32_t* stat = at<int32_t>(arena, D.stat_out);
-  const int KA = D.KA, KP = D.KP, KT = D.KT;
+// In-place inverse Cholesky factor of an SPD matrix: M (nc x nc, row-major, lower triangle read)
+// becomes L^-1 (lower triangle; the upper triangle is left as scratch), A = L L^T. Right-looking
+// blocked elimination of [A | I] by NB-column panels: per panel the diagonal block is factorised
+// (L11) and inverted (Li = L11^-1) in LDS, L21 = A21 Li^T and the panel's final rows
+// Z = Li [X_top | I] are formed, then every trailing row i takes
+//   M[i, 0:k1]  <- [X_i, 0] - L21_i Z          (the rows of L^-1 being accumulated)
+//   M[i, k1:i]  <- M[i, k1:i] - L21_i L21^T     (the Schur complement, lower triangle)
+// in 4x4 register tiles over LDS operands: nc^3/3 fused multiply-adds, no pivoting. Returns
+// false (uniformly) on a non-positive pivot: the caller falls back to Gauss-Jordan.
+template <int NB, class Stamp>
+__device__ bool chol_inverse(double* __restrict__ M, int nc, double* lds, int tid, Stamp stamp) {
+  constexpr int ds = NB + 1;
+  double* Dg = lds;                           // NB x ds: diagonal block -> L11
+  double* Li = Dg + NB * ds;                  // NB x ds: L11^-1
+  double* P21 = Li + NB * ds;                 // (nc - k1) x ds: A21 -> L21
+  double* Z = P21 + (int64_t)nc * ds;         // NB x nc: the panel's rows of L^-1
+  const int r = tid / NB, c = tid % NB;
+  const bool act = tid < NB * NB;
+  for (int k0 = 0; k0 < nc; k0 += NB) {
+    const int bw = min(NB, nc - k0), k1 = k0 + bw;
+    if (act) Dg[r * ds + c] = (r < bw && c <= r) ? M[(int64_t)(k0 + r) * nc + k0 + c] : 0.0;
+    __syncthreads();
+    for (int t = 0; t < bw; ++t) {
+      const double dtt = Dg[t * ds + t];
+      if (!(dtt > 0.0)) return false;  // same value in every thread
+      const double s = sqrt(dtt);
+      const double lrt = (act && r < bw && r > t) ? Dg[r * ds + t] / s : 0.0;
+      const double lct = (act && c < bw && c > t) ? Dg[c * ds + t] / s : 0.0;
+      __syncthreads();
+      if (act && r < bw) {
+        if (c == t && r >= t)
+          Dg[r * ds + t] = (r == t) ? s : lrt;
+        else if (c > t && c <= r)
+          Dg[r * ds + c] -= lrt * lct;
+      }
+      __syncthreads();
+    }
+    // Li = L11^-1, a column per thread (each column depends only on itself)
+    if (tid < bw) {
+      const int cc = tid;
+      Li[cc * ds + cc] = 1.0 / Dg[cc * ds + cc];
+      for (int rr = cc + 1; rr < bw; ++rr) {
+        double s2 = 0.0;
+        for (int k = cc; k < rr; ++k) s2 = fma(Dg[rr * ds + k], Li[k * ds + cc], s2);
+        Li[rr * ds + cc] = -s2 / Dg[rr * ds + rr];
+      }
+    }
+    __syncthreads();
+    stamp(4);
+    // A21 (rows below the panel; bw == NB whenever such rows exist) and X_top into LDS
+    for (int64_t q = tid; q < (int64_t)(nc - k1) * NB; q += kBT) {
+      const int i = (int)(q / NB), s = (int)(q % NB);
+      P21[(int64_t)i * ds + s] = M[(int64_t)(k1 + i) * nc + k0 + s];
+    }
+    for (int64_t q = tid; q < (int64_t)bw * k0; q += kBT) {
+      const int t = (int)(q / k0), j = (int)(q % k0);
+      Z[(int64_t)t * nc + j] = M[(int64_t)(k0 + t) * nc + j];
+    }
+    __syncthreads();
+    // L21 = A21 Li^T in place, a row per thread: column t needs columns s <= t only, so going
+    // from the last column down leaves every operand unread-over
+    for (int i = tid; i < nc - k1; i += kBT) {
+      double* row = P21 + (int64_t)i * ds;
+      for (int t = NB - 1; t >= 0; --t) {
+        double l = 0.0;
+        for (int s = 0; s <= t; ++s) l = fma(row[s], Li[t * ds + s], l);
+        row[t] = l;
+      }
+    }
+    // Z = Li [X_top | I]: final rows k0..k1-1 of L^-1, kept in LDS for the trailing update (in
+    // place per column, last row first, as above)
+    for (int j = tid; j < k1; j += kBT) {
+      if (j < k0) {
+        for (int t = bw - 1; t >= 0; --t) {
+          double z = 0.0;
+          for (int s = 0; s <= t; ++s) z = fma(Li[t * ds + s], Z[(int64_t)s * nc + j], z);
+          Z[(int64_t)t * nc + j] = z;
+          M[(int64_t)(k0 + t) * nc + j] = z;
+        }
+      } else {
+        const int s0 = j - k0;
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+          if (t < bw) {
+            const double z = s0 <= t ? Li[t * ds + s0] : 0.0;
+            Z[(int64_t)t * nc + j] = z;
+            if (s0 <= t) M[(int64_t)(k0 + t) * nc + j] = z;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (k1 < nc) {
+      // 4x4 tiles over rows [k1, nc) x columns [0, i]: row block rb has a4 + rb + 1 column
+      // blocks (k1 is a multiple of 4), C(rb) tiles precede it
+      const int64_t a4 = k1 / 4, nrb = (nc - k1 + 3) / 4;
+      auto C = [&](int64_t rb) { return rb * (a4 + 1) + rb * (rb - 1) / 2; };
+      const int64_t T = C(nrb);
+      const int last = nc - k1 - 1;
+      for (int64_t q = tid; q < T; q += kBT) {
+        const double bq = (double)a4 + 0.5;
+        int64_t rb = (int64_t)(-bq + sqrt(bq * bq + 2.0 * (double)q));
+        while (rb > 0 && C(rb) > q) --rb;
+        while (C(rb + 1) <= q) ++rb;
+        const int i0 = k1 + 4 * (int)rb, j0 = 4 * (int)(q - C(rb));
+        const bool xpart = j0 < k1, zero = j0 >= k0 && j0 < k1;
+        double acc[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int i = i0 + u, j = j0 + v;
+            acc[u][v] = (!zero && i < nc && j < nc) ? M[(int64_t)i * nc + j] : 0.0;
+          }
+        const double* ar[4];
+        const double* wr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ar[u] = P21 + (int64_t)min(i0 + u - k1, last) * ds;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) wr[v] = P21 + (int64_t)min(max(j0 + v - k1, 0), last) * ds;
+#pragma unroll 4
+        for (int t = 0; t < NB; ++t) {
+          double a[4], w[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) a[u] = ar[u][t];
+          if (xpart) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) w[v] = Z[(int64_t)t * nc + j0 + v];
+          } else {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) w[v] = wr[v][t];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[u][v] = fma(-a[u], w[v], acc[u][v]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int i = i0 + u, j = j0 + v;
+            if (i < nc && j < nc) M[(int64_t)i * nc + j] = acc[u][v];
+          }
+      }
+      __syncthreads();
+    }
+    stamp(5);
+  }
+  return true;
+}
+
+// A_H = P^T A P (dense, row j = coarse row j; accumulation order of the packed rows)
+__device__ void dense_galerkin(const BDesc& D, char* arena, double* AH, int tid) {
+  const int n = D.n, nc = D.nc, KA = D.KA, KP = D.KP, KT = D.KT;
   const int32_t* __restrict__ akc = at<int32_t>(arena, D.ak_col);
   const double* __restrict__ akv = at<double>(arena, D.ak_val);
   const int32_t* __restrict__ ppc = at<int32_t>(arena, D.pp_col);
   const double* __restrict__ ppv = at<double>(arena, D.pp_val);
   const int32_t* __restrict__ ptc = at<int32_t>(arena, D.pt_row);
   const double* __restrict__ ptv = at<double>(arena, D.pt_val);
-
-  // phase wall times (100 MHz clock) when requested: [galerkin, inverse, smoothing, rest]
-  int64_t* tstat = at<int64_t>(arena, D.stat_out + 8);
-  int64_t t_mark = D.timing ? wall_clock64() : 0;
-  auto stamp = [&](int slot) {
-    if (D.timing && tid == 0) {
-      const int64_t t = wall_clock64();
-      tstat[slot] += t - t_mark;
-      t_mark = t;
-    }
-  };
-  if (D.timing && tid == 0)
-    for (int q = 0; q < 6; ++q) tstat[q] = 0;
-
-  // ---------------------------------------------------------------- A_H = P^T A P (dense)
   for (int64_t q = tid; q < (int64_t)nc * nc; q += kBT) AH[q] = 0.0;
   __syncthreads();
   for (int j = tid; j < nc; j += kBT) {
@@ -253,7 +468,65 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
     }
   }
   __syncthreads();
+}
+
+// one workgroup per problem: Galerkin product and coarse inverse (operator mode in stat[2]:
+// 1 = inverse Cholesky factor L^-1 in AH's lower triangle and its transpose in AI's upper
+// triangle, 0 = the Gauss-Jordan inverse in AI)
+__global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ descs,
+                                                     char* __restrict__ arena) {
+  extern __shared__ double lds[];
+  __shared__ double redv[kBWaves];
+  __shared__ int redi[kBWaves];
+  const BDesc D = descs[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int nc = D.nc;
+  double* AH = at<double>(arena, D.AH);
+  double* AI = at<double>(arena, D.AI);
+  int32_t* stat = at<int32_t>(arena, D.stat_out);
+
+  // phase wall times (100 MHz clock) when requested: [galerkin, inverse, smoothing, rest,
+  // panels, updates]
+  int64_t* tstat = at<int64_t>(arena, D.stat_out + 16);
+  int64_t t_mark = D.timing ? wall_clock64() : 0;
+  auto stamp = [&](int slot) {
+    if (D.timing && tid == 0) {
+      const int64_t t = wall_clock64();
+      tstat[slot] += t - t_mark;
+      t_mark = t;
+    }
+  };
+  if (D.timing && tid == 0)
+    for (int q = 0; q < 6; ++q) tstat[q] = 0;
+
+  dense_galerkin(D, arena, AH, tid);
   stamp(0);
+
+  if (D.spd) {
+    // the panel width is the problem's own (a function of n_c alone): a problem's roundings do
+    // not depend on the batch it is launched with
+    const bool ok = D.chol_nb == 32   ? chol_inverse<32>(AH, nc, lds, tid, stamp)
+                    : D.chol_nb == 16 ? chol_inverse<16>(AH, nc, lds, tid, stamp)
+                    : D.chol_nb == 8  ? chol_inverse<8>(AH, nc, lds, tid, stamp)
+                                      : chol_inverse<4>(AH, nc, lds, tid, stamp);
+    if (ok) {
+      // AI[j][i] = L^-1[i][j] (i >= j): the rows of L^-T for the second solve phase
+      for (int64_t q = tid; q < (int64_t)nc * nc; q += kBT) {
+        const int64_t i = q / nc;
+        const int j = (int)(q - i * nc);
+        if (j <= i) AI[(int64_t)j * nc + i] = AH[q];
+      }
+      __syncthreads();
+      stamp(1);
+      if (tid == 0) {
+        stat[1] = 0;
+        stat[2] = 1;
+      }
+      return;
+    }
+    __syncthreads();
+    dense_galerkin(D, arena, AH, tid);  // not SPD in floating point: Gauss-Jordan on a fresh A_H
+  }
 
   // ---------------------------------------------------------------- A_H^-1, blocked Gauss-Jordan
   const int pb = D.panel;           // power of two, 4..16
@@ -406,7 +679,10 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
   }
   __syncthreads();
   stamp(1);
-  if (tid == 0) stat[1] = status;
+  if (tid == 0) {
+    stat[1] = status;
+    stat[2] = 0;
+  }
 }
 
 // one workgroup per problem: the cycles (reads the setup kernel's inverse and status)
@@ -420,6 +696,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
   const int n = D.n, nc = D.nc;
   const double* __restrict__ b = at<double>(arena, D.b);
   const double* __restrict__ AI = at<double>(arena, D.AI);
+  const double* __restrict__ AH = at<double>(arena, D.AH);
   double* x_out = at<double>(arena, D.x_out);
   double* err = at<double>(arena, D.err_out);
   int32_t* stat = at<int32_t>(arena, D.stat_out);
@@ -430,7 +707,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
   const double* __restrict__ ppv = at<double>(arena, D.pp_val);
   const int32_t* __restrict__ ptc = at<int32_t>(arena, D.pt_row);
   const double* __restrict__ ptv = at<double>(arena, D.pt_val);
-  int64_t* tstat = at<int64_t>(arena, D.stat_out + 8);
+  int64_t* tstat = at<int64_t>(arena, D.stat_out + 16);
   int64_t t_mark = D.timing ? wall_clock64() : 0;
   auto stamp = [&](int slot) {
     if (D.timing && tid == 0) {
@@ -439,17 +716,23 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
       t_mark = t;
     }
   };
-  const int status = stat[1];
+  const int status = stat[1], mode = stat[2];
 
   // ---------------------------------------------------------------- cycles
-  double* xs = lds;                                     // n
-  double* rcs = xs + n;                                 // nc: restricted residual
+  double* xs = lds;                                     // n + 2: x, a zero slot, a sink slot
+  double* rcs = xs + n + 2;                             // nc: restricted residual
   double* es = rcs + nc;                                // nc: coarse correction
-  double* rs = R_LDS ? es + nc : at<double>(arena, D.rg);  // n: residual
-  double* stage = R_LDS ? rs + n : es + nc;             // GS staging area
+  double* ys = es + nc;                                 // nc: L^-1 r_H
+  double* rs = R_LDS ? ys + nc : at<double>(arena, D.rg);  // n: residual
+  // GS staging area, 16-byte aligned (the one-wave sweep reads its rows with 16-byte loads)
+  // (an even double offset from the LDS base: index arithmetic keeps the LDS address space,
+  // which an integer round trip would lose to flat accesses)
+  const int64_t stage_off = ((R_LDS ? (ys - lds) + nc + n : (ys - lds) + nc) + 1) & ~int64_t(1);
+  double* stage = lds + stage_off;
   const double* __restrict__ x0 = at<double>(arena, D.x0);
   #pragma unroll 1
   for (int i = tid; i < n; i += kBT) xs[i] = x0[i];
+  if (tid == 0) xs[n] = 0.0;  // pad columns of the one-wave sweep read it; nothing writes it
   __syncthreads();
   if (status != 0) {  // multigrid.py:167-170: x returned untouched, no iteration
     #pragma unroll 1
@@ -473,8 +756,28 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
     }
   }
 
-  // (b - A x)_i in csr_matvec's order (0 + a_1 x_1 + ... in stored order, then b_i - y)
-  auto resid_row = [&](int i) -> double { return b[i] - packed_dot(akc, akv, n, i, KA, xs); };
+  // (b - A x)_i in csr_matvec's order (0 + a_1 x_1 + ... in stored order, then b_i - y) for
+  // the rows i = tid + kBT * q, four at a time; out (nullable) takes r, part += r_i^2 in row order
+  auto resid_rows = [&](double* out, double* part) {
+    #pragma unroll 1
+    for (int i0 = tid; i0 < n; i0 += 4 * kBT) {
+      int rows[4];
+      double y[4], bb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        rows[u] = i0 + u * kBT < n ? i0 + u * kBT : -1;
+        bb[u] = rows[u] >= 0 ? b[rows[u]] : 0.0;
+      }
+      packed_dot_rows<4>(akc, akv, n, rows, KA, xs, y);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (rows[u] >= 0) {
+          const double ri = bb[u] - y[u];
+          if (out) out[rows[u]] = ri;
+          if (part) *part += ri * ri;
+        }
+    }
+  };
 
   const int32_t* __restrict__ lptr = at<int32_t>(arena, D.lev_ptr);
   const int32_t* __restrict__ clev = at<int32_t>(arena, D.chunk_lev);
@@ -492,9 +795,133 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
   int32_t* sr = sc + (int64_t)cap * K;                      // cap rows
   int32_t* slp = sr + cap;                                  // level starts of the chunk
 
+  // One wave sweeps the staged levels of a chunk (one-wave layout: position-major rows of KM
+  // slots, pads = column n, the zero slot, value 0.0; a zero diagonal or a lane past the level's
+  // end writes the sink slot n + 1; position cnt is such a dummy). A level's rows are
+  // independent and a wave's LDS accesses complete in order, so consecutive levels need no
+  // workgroup barrier — only a wavefront fence that keeps the compiler from moving the next
+  // level's x gathers above this level's stores. Level l+1's rows are loaded while level l
+  // gathers and divides. The padded sum adds +0.0 products to a sum that started at +0.0 (never
+  // -0.0), so it is bitwise pyamg's.
+  auto wave_sweep = [&](auto km_tag, auto rw_tag, int nl, int cnt) {
+    constexpr int KM = decltype(km_tag)::value, RW = decltype(rw_tag)::value;
+    const int lane = tid & 63;
+    const double* sv = stage;
+    const double* sd = sv + (int64_t)(cap + 1) * KM;
+    const double* sb = sd + (cap + 1);
+    const int32_t* sc = reinterpret_cast<const int32_t*>(sb + (cap + 1));
+    const int32_t* sr = sc + (int64_t)(cap + 1) * KM;
+    const int32_t* slp = sr + (cap + 1);
+    int c[RW][KM], row[RW];
+    double v[RW][KM], d[RW], bv[RW];
+    auto load_level = [&](int l, int (&cc)[RW][KM], double (&vv)[RW][KM], double* dd,
+                          double* bb, int* rr) {
+      const int a = slp[l], z = slp[l + 1];
+#pragma unroll
+      for (int u = 0; u < RW; ++u) {
+        const int p = a + lane + 64 * u < z ? a + lane + 64 * u : cnt;
+#pragma unroll
+        for (int k = 0; k < KM; k += 4) {
+          const int4 c4 = *reinterpret_cast<const int4*>(sc + (int64_t)p * KM + k);
+          cc[u][k] = c4.x;
+          cc[u][k + 1] = c4.y;
+          cc[u][k + 2] = c4.z;
+          cc[u][k + 3] = c4.w;
+        }
+#pragma unroll
+        for (int k = 0; k < KM; k += 2) {
+          const double2 v2 = *reinterpret_cast<const double2*>(sv + (int64_t)p * KM + k);
+          vv[u][k] = v2.x;
+          vv[u][k + 1] = v2.y;
+        }
+        dd[u] = sd[p];
+        bb[u] = sb[p];
+        rr[u] = sr[p];
+      }
+    };
+    load_level(0, c, v, d, bv, row);
+    #pragma unroll 1
+    for (int l = 0; l < nl; ++l) {
+      double g[RW][KM];
+#pragma unroll
+      for (int u = 0; u < RW; ++u)
+#pragma unroll
+        for (int k = 0; k < KM; ++k) g[u][k] = xs[c[u][k]];
+      int c2[RW][KM], row2[RW];
+      double v2[RW][KM], d2[RW], bv2[RW];
+      load_level(l + 1 < nl ? l + 1 : l, c2, v2, d2, bv2, row2);
+#pragma unroll
+      for (int u = 0; u < RW; ++u) {
+        double y = 0.0;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) y += v[u][k] * g[u][k];
+        xs[row[u]] = (bv[u] - y) / d[u];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int u = 0; u < RW; ++u) {
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+          c[u][k] = c2[u][k];
+          v[u][k] = v2[u][k];
+        }
+        d[u] = d2[u];
+        bv[u] = bv2[u];
+        row[u] = row2[u];
+      }
+    }
+  };
+
   auto gs_sweep = [&]() {
     // pyamg gauss_seidel: rsum over the off-diagonals in stored order, diag = the last stored
     // diagonal entry, x_i = (b_i - rsum) / diag unless diag == 0
+    if (D.gs_rw > 0) {  // one-wave sweep, position-major rows of K (= 4 or 8) slots
+      double* wv = stage;
+      double* wd = wv + (int64_t)(cap + 1) * K;
+      double* wb = wd + (cap + 1);
+      int32_t* wc = reinterpret_cast<int32_t*>(wb + (cap + 1));
+      int32_t* wr = wc + (int64_t)(cap + 1) * K;
+      int32_t* wl = wr + (cap + 1);
+      for (int ch = 0; ch < D.n_chunks; ++ch) {
+        const int l0 = clev[ch], l1 = clev[ch + 1];
+        const int P0 = lptr[l0], cnt = lptr[l1] - P0;
+        for (int q = tid; q < cnt * K; q += kBT) {
+          wc[q] = pkc[(int64_t)P0 * K + q];
+          wv[q] = pkv[(int64_t)P0 * K + q];
+        }
+        for (int q = tid; q < cnt; q += kBT) {
+          wd[q] = pkd[P0 + q];
+          wb[q] = bl[P0 + q];
+          wr[q] = pkr[P0 + q];
+        }
+        if (tid < K) {  // the dummy position
+          wc[cnt * K + tid] = n;
+          wv[cnt * K + tid] = 0.0;
+        }
+        if (tid == 0) {
+          wd[cnt] = 1.0;
+          wb[cnt] = 0.0;
+          wr[cnt] = n + 1;
+        }
+        for (int q = tid; q <= l1 - l0; q += kBT) wl[q] = lptr[l0 + q] - P0;
+        __syncthreads();
+        if (tid < 64) {
+          if (K == 4 && D.gs_rw == 1)
+            wave_sweep(std::integral_constant<int, 4>(), std::integral_constant<int, 1>(),
+                       l1 - l0, cnt);
+          else if (K == 4)
+            wave_sweep(std::integral_constant<int, 4>(), std::integral_constant<int, 2>(),
+                       l1 - l0, cnt);
+          else
+            wave_sweep(std::integral_constant<int, 8>(), std::integral_constant<int, 1>(),
+                       l1 - l0, cnt);
+        }
+        __syncthreads();
+      }
+      return;
+    }
     for (int ch = 0; ch < D.n_chunks; ++ch) {
       const int l0 = clev[ch], l1 = clev[ch + 1];
       const int P0 = lptr[l0], cnt = lptr[l1] - P0;
@@ -542,8 +969,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
       if (D.smoother == 0) {
         gs_sweep();
       } else {  // MLAMG.py:143-146: x += Dinv_w (b - A x)
-        #pragma unroll 1
-        for (int i = tid; i < n; i += kBT) rs[i] = resid_row(i);
+        resid_rows(rs, nullptr);
         __syncthreads();
         #pragma unroll 1
         for (int i = tid; i < n; i += kBT) xs[i] = xs[i] + dwg[i] * rs[i];
@@ -556,48 +982,41 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
   int iters = 0;
   for (int itn = 0; itn < D.max_iter; ++itn) {
     smooth(D.nu_pre);
-    #pragma unroll 1
-    for (int i = tid; i < n; i += kBT) rs[i] = resid_row(i);
+    resid_rows(rs, nullptr);
     __syncthreads();
     #pragma unroll 1
-    for (int j = tid; j < nc; j += kBT)  // P^T r: csc_matvec's order
-      rcs[j] = packed_dot(ptc, ptv, nc, j, KT, rs);
+    for (int j0 = tid; j0 < nc; j0 += 2 * kBT) {  // P^T r: csc_matvec's order
+      int rows[2] = {j0, j0 + kBT < nc ? j0 + kBT : -1};
+      double y[2];
+      packed_dot_rows<2>(ptc, ptv, nc, rows, KT, rs, y);
+      rcs[j0] = y[0];
+      if (rows[1] >= 0) rcs[rows[1]] = y[1];
+    }
     __syncthreads();
-    {  // e = A_H^-1 r_H: wave per row, k_gemv's order
-      const int w = tid >> 6, lane = tid & 63;
-      #pragma unroll 1
-      for (int j = w; j < nc; j += kBWaves) {
-        const double* rw = AI + (int64_t)j * nc;
-        double s = 0.0;
-        int l = lane;
-        for (; l + 7 * 64 < nc; l += 8 * 64) {
-          double m[8], v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            m[u] = rw[l + u * 64];
-            v[u] = rcs[l + u * 64];
-          }
-#pragma unroll
-          for (int u = 0; u < 8; ++u) s += m[u] * v[u];
-        }
-        for (; l < nc; l += 64) s += rw[l] * rcs[l];
-        s = bw_sum(s);
-        if (lane == 0) es[j] = s;
-      }
+    if (mode == 1) {  // e = L^-T (L^-1 r_H)
+      rows_dot<1>(AH, nc, rcs, ys, tid);
+      __syncthreads();
+      rows_dot<2>(AI, nc, ys, es, tid);
+    } else {  // e = A_H^-1 r_H (Gauss-Jordan inverse)
+      rows_dot<0>(AI, nc, rcs, es, tid);
     }
     __syncthreads();
     #pragma unroll 1
-    for (int i = tid; i < n; i += kBT)  // x += P e
-      xs[i] = xs[i] + packed_dot(ppc, ppv, n, i, KP, es);
+    for (int i0 = tid; i0 < n; i0 += 4 * kBT) {  // x += P e
+      int rows[4];
+      double y[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) rows[u] = i0 + u * kBT < n ? i0 + u * kBT : -1;
+      packed_dot_rows<4>(ppc, ppv, n, rows, KP, es, y);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (rows[u] >= 0) xs[rows[u]] = xs[rows[u]] + y[u];
+    }
     __syncthreads();
     smooth(D.nu_post);
     double part = 0.0;
     if (D.norm_mode == 0) {
-      #pragma unroll 1
-      for (int i = tid; i < n; i += kBT) {
-        const double ri = resid_row(i);
-        part += ri * ri;
-      }
+      resid_rows(nullptr, &part);
     } else {
       #pragma unroll 1
       for (int i = tid; i < n; i += kBT) part += xs[i] * xs[i];
@@ -640,6 +1059,36 @@ bool valid_csr(int64_t rows, int64_t cols, int64_t nnz, const int32_t* ip, const
   return true;
 }
 
+// A == A^T exactly (values included): then A_H = P^T A P is symmetric and, A being SPD, the
+// coarse solve can take the inverse Cholesky factor
+bool csr_symmetric(int64_t n, const int32_t* ip, const int32_t* ij, const double* v) {
+  const int64_t nnz = ip[n];
+  std::vector<int32_t> tp(n + 1, 0), ti(nnz);
+  std::vector<double> tv(nnz);
+  for (int64_t k = 0; k < nnz; ++k) tp[ij[k] + 1]++;
+  for (int64_t j = 0; j < n; ++j) tp[j + 1] += tp[j];
+  std::vector<int32_t> fill(tp.begin(), tp.end() - 1);
+  for (int64_t i = 0; i < n; ++i)
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
+      ti[fill[ij[k]]] = (int32_t)i;
+      tv[fill[ij[k]]++] = v[k];
+    }
+  // row i of A^T lists its columns ascending; compare with row i of A sorted by column
+  std::vector<std::pair<int32_t, double>> row;
+  for (int64_t i = 0; i < n; ++i) {
+    if (ip[i + 1] - ip[i] != tp[i + 1] - tp[i]) return false;
+    row.clear();
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) row.emplace_back(ij[k], v[k]);
+    std::sort(row.begin(), row.end(),
+              [](const std::pair<int32_t, double>& a, const std::pair<int32_t, double>& b) {
+                return a.first < b.first;
+              });
+    for (size_t q = 0; q < row.size(); ++q)
+      if (row[q].first != ti[tp[i] + q] || !(row[q].second == tv[tp[i] + q])) return false;
+  }
+  return true;
+}
+
 // rows of a CSR into a slot-major fixed-width layout (col -1 / value 0 pads); width = the
 // longest row (>= 1)
 int pack_rows(int64_t rows, const int32_t* ip, const int32_t* ij, const double* v,
@@ -654,6 +1103,33 @@ int pack_rows(int64_t rows, const int32_t* ip, const int32_t* ij, const double* 
       val[(size_t)(k - ip[i]) * rows + i] = v[k];
     }
   return w;
+}
+
+// f(0 .. count-1) on up to MLAMG_HOST_THREADS (default: the CPUs this process may run on, at
+// most 16) host threads; the calling thread takes a share. Small counts run inline.
+template <class F>
+void parallel_for(int count, F&& f) {
+  static const int max_threads = [] {
+    int t = 16;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) t = std::min(t, CPU_COUNT(&set));
+    if (const char* e = std::getenv("MLAMG_HOST_THREADS")) t = std::max(1, std::atoi(e));
+    return std::max(1, t);
+  }();
+  const int nt = std::min(max_threads, count / 2);
+  if (nt <= 1) {
+    for (int q = 0; q < count; ++q) f(q);
+    return;
+  }
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    for (int q = next.fetch_add(1); q < count; q = next.fetch_add(1)) f(q);
+  };
+  std::vector<std::thread> pool;
+  pool.reserve(nt - 1);
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
 }
 
 }  // namespace
@@ -682,32 +1158,50 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   // ---- host: validation, structure analysis, layout
   struct Plan {
     std::vector<int32_t> lev, pkr, pkc, clev, akc, ppc, ptc;
-    std::vector<double> pkv, pkd, akv, ppv, ptv;
+    std::vector<double> pkv, pkd, akv, ppv, ptv, blv;  // blv: b in sweep (level) order
     int K = 1, KA = 1, KP = 1, KT = 1, nlev = 0, panel = 8, cap = 0;
+    bool spd = false;
+    int chol_nb = 4, gs_rw = 0;
+    size_t lds_setup = 0, lds_cycles = 0;
+    int code = MLAMG_OK;  // analysis failure: code + message (reported for the first problem)
+    std::string err;
   };
   static const bool timing = std::getenv("MLAMG_BATCH_TIMING") != nullptr;
+  const auto t_begin = std::chrono::steady_clock::now();
   std::vector<Plan> plans(count);
   std::vector<BDesc> desc(count);
   // residual in LDS when every problem leaves room for it
   bool r_lds = true;
   for (int q = 0; q < count; ++q) {
-    const size_t need = (size_t)probs[q].n * 16 + (size_t)probs[q].n_c * 16 + 16 * 1024;
+    const size_t need = (size_t)probs[q].n * 16 + 16 + (size_t)probs[q].n_c * 24 + 16 * 1024;
     if (need > kBLdsBytes) r_lds = false;
   }
   Layout lay;
   const int64_t desc_off = lay.take(sizeof(BDesc) * count);
   size_t lds_setup = 0, lds_cycles = 0;
-  for (int q = 0; q < count; ++q) {
+  // inverse-Cholesky LDS: two NB x (NB+1) blocks, the L21 panel and the Z rows
+  auto chol_lds = [](int nb, int64_t nc) {
+    return (size_t)8 * (2 * nb * (nb + 1) + (size_t)nc * (nb + 1) + (size_t)nb * nc);
+  };
+  auto analyse = [&](int q) {
     mlamg_amg2v_problem& P = probs[q];
-    const int64_t n = P.n, nc = P.n_c;
-    MLAMG_REQUIRE(n >= 1 && n <= kBMaxN, "problem rows out of range for the batched solver");
-    MLAMG_REQUIRE(nc >= 1 && nc <= kBMaxNc && nc <= n, "coarse size out of range");
-    MLAMG_REQUIRE(valid_csr(n, n, P.A_nnz, P.A_indptr, P.A_indices) && P.A_data,
-                  "A is not a valid n x n CSR");
-    MLAMG_REQUIRE(valid_csr(n, nc, P.P_nnz, P.P_indptr, P.P_indices) && P.P_data,
-                  "P is not a valid n x n_c CSR");
-    MLAMG_REQUIRE(P.b && P.x0 && P.x_out && (max_iter == 0 || P.err_out), "NULL vector");
     Plan& L = plans[q];
+#define REQ(cond, msg)       \
+  do {                       \
+    if (!(cond)) {           \
+      L.code = MLAMG_EINVAL; \
+      L.err = (msg);         \
+      return;                \
+    }                        \
+  } while (0)
+    const int64_t n = P.n, nc = P.n_c;
+    REQ(n >= 1 && n <= kBMaxN, "problem rows out of range for the batched solver");
+    REQ(nc >= 1 && nc <= kBMaxNc && nc <= n, "coarse size out of range");
+    REQ(valid_csr(n, n, P.A_nnz, P.A_indptr, P.A_indices) && P.A_data,
+        "A is not a valid n x n CSR");
+    REQ(valid_csr(n, nc, P.P_nnz, P.P_indptr, P.P_indices) && P.P_data,
+        "P is not a valid n x n_c CSR");
+    REQ(P.b && P.x0 && P.x_out && (max_iter == 0 || P.err_out), "NULL vector");
     L.KA = pack_rows(n, P.A_indptr, P.A_indices, P.A_data, L.akc, L.akv);
     L.KP = pack_rows(n, P.P_indptr, P.P_indices, P.P_data, L.ppc, L.ppv);
     {  // P^T: entries of coarse column j in ascending fine row
@@ -726,9 +1220,20 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       L.KT = pack_rows(nc, tp.data(), ti.data(), tv.data(), L.ptc, L.ptv);
     }
     if (L.KA > kBMaxK + 1 || L.KP > kBMaxKP || L.KT > kBMaxKT) {
-      set_error("amg2v_batch: rows of A, P or P^T longer than the batched solver's slots");
-      return MLAMG_EUNSUPPORTED;
+      L.code = MLAMG_EUNSUPPORTED;
+      L.err = "amg2v_batch: rows of A, P or P^T longer than the batched solver's slots";
+      return;
     }
+    int chol_nb = 32;  // the widest panel that fits
+    while (chol_nb > 4 && chol_lds(chol_nb, nc) > kBLdsBytes) chol_nb >>= 1;
+    const bool spd = csr_symmetric(n, P.A_indptr, P.A_indices, P.A_data) &&
+                     chol_lds(chol_nb, nc) <= kBLdsBytes;
+    if (spd) L.lds_setup = chol_lds(chol_nb, nc);
+    // cycle vectors in LDS: x (+ zero and sink slots), r when it fits, r_H, e_H, L^-1 r_H; the
+    // sweep's staging area gets the rest
+    const size_t vec_lds = (size_t)n * 8 * (r_lds ? 2 : 1) + 16 + (size_t)nc * 24;
+    const size_t room = kBLdsBytes > vec_lds + 64 ? kBLdsBytes - vec_lds - 64 : 0;
+    int gs_rw = 0;
     if (smoother == 0) {
       // level schedule of the forward sweep (gs.hip): level(i) = 1 + max level(j) over j < i
       // coupled in either direction; rows ascending within a level
@@ -751,30 +1256,48 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
         L.nlev = std::max(L.nlev, lv + 1);
       }
       if (maxoff > kBMaxK) {
-        set_error("amg2v_batch: a row of A has more than 32 off-diagonal entries");
-        return MLAMG_EUNSUPPORTED;
+        L.code = MLAMG_EUNSUPPORTED;
+        L.err = "amg2v_batch: a row of A has more than 32 off-diagonal entries";
+        return;
       }
-      L.K = std::max(maxoff, 1);
       L.lev.assign(L.nlev + 1, 0);
       for (int64_t i = 0; i < n; ++i) L.lev[level[i] + 1]++;
       for (int l = 0; l < L.nlev; ++l) L.lev[l + 1] += L.lev[l];
+      int wmax = 0;
+      for (int l = 0; l < L.nlev; ++l) wmax = std::max(wmax, L.lev[l + 1] - L.lev[l]);
+      // one-wave sweep: rows of 4 slots and levels of <= 128 rows, or 8 slots and <= 64 rows,
+      // and a staging area that holds the widest level (+ the dummy position)
+      const int km = maxoff <= 4 ? 4 : maxoff <= 8 ? 8 : 0;
+      if (km == 4 && wmax <= 128) gs_rw = wmax <= 64 ? 1 : 2;
+      if (km == 8 && wmax <= 64) gs_rw = 1;
+      if (gs_rw && (int)std::min<size_t>(4096, room / (12 * km + 24)) - 1 < wmax) gs_rw = 0;
+      L.K = gs_rw ? km : std::max(maxoff, 1);
+      const int64_t K = L.K;
       L.pkr.resize(n);
-      L.pkc.assign((size_t)n * L.K, -1);
-      L.pkv.assign((size_t)n * L.K, 0.0);
+      L.pkc.assign((size_t)n * K, gs_rw ? (int32_t)n : -1);
+      L.pkv.assign((size_t)n * K, 0.0);
       L.pkd.assign(n, 0.0);
       std::vector<int32_t> fill(L.lev.begin(), L.lev.end() - 1);
+      L.blv.resize(n);
       for (int64_t i = 0; i < n; ++i) {
         const int32_t p = fill[level[i]]++;
         L.pkr[p] = (int32_t)i;
+        L.blv[p] = P.b[i];
         int s2 = 0;
         for (int32_t k = P.A_indptr[i]; k < P.A_indptr[i + 1]; ++k) {
           if (P.A_indices[k] == i) {
             L.pkd[p] = P.A_data[k];  // the last stored diagonal entry, as the sweep takes it
           } else {
-            L.pkc[(size_t)s2 * n + p] = P.A_indices[k];
-            L.pkv[(size_t)s2 * n + p] = P.A_data[k];
+            // slot-major for the workgroup sweep, position-major for the one-wave sweep
+            const size_t at = gs_rw ? (size_t)p * K + s2 : (size_t)s2 * n + p;
+            L.pkc[at] = P.A_indices[k];
+            L.pkv[at] = P.A_data[k];
             ++s2;
           }
+        }
+        if (gs_rw && L.pkd[p] == 0.0) {  // pyamg leaves x_i alone: write the sink slot
+          L.pkd[p] = 1.0;
+          L.pkr[p] = (int32_t)n + 1;
         }
       }
     }
@@ -783,15 +1306,14 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     int pb = kBMaxPanel;
     auto setup_lds = [&](int b) { return (size_t)nc * (b + 1) * 8 + 16 * b + (size_t)nc * 12; };
     while (pb > 4 && setup_lds(pb) > kBLdsBytes) pb >>= 1;
-    MLAMG_REQUIRE(setup_lds(pb) <= kBLdsBytes, "coarse too large");
+    REQ(setup_lds(pb) <= kBLdsBytes, "coarse too large");
     L.panel = pb;
     // GS staging chunks: runs of consecutive levels with <= cap rows, cap from the LDS left
-    // after the cycle vectors (a wider level is swept straight from the arena)
-    const size_t vec_lds = (size_t)n * 8 * (r_lds ? 2 : 1) + (size_t)nc * 16;
+    // after the cycle vectors, one position kept for the one-wave sweep's dummy (a level wider
+    // than cap is swept by the workgroup straight from the arena)
     if (smoother == 0) {
       const size_t per_pos = 12 * (size_t)L.K + 24;
-      const size_t room = kBLdsBytes > vec_lds + 64 ? kBLdsBytes - vec_lds - 64 : 0;
-      L.cap = (int)std::min<size_t>(4096, room / per_pos);
+      L.cap = (int)std::min<size_t>(4096, room / per_pos) - 1;
       L.clev.push_back(0);
       int l = 0;
       while (l < L.nlev) {
@@ -804,8 +1326,26 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
         L.clev.push_back(l);
       }
     }
-    lds_setup = std::max(lds_setup, setup_lds(pb));
-    lds_cycles = std::max(lds_cycles, vec_lds + (size_t)L.cap * (12 * L.K + 24) + 8);
+    L.lds_setup = std::max(L.lds_setup, setup_lds(pb));
+    L.lds_cycles = vec_lds + 16 + (size_t)(L.cap + 1) * (12 * L.K + 24) + 8;
+    L.spd = spd;
+    L.chol_nb = chol_nb;
+    L.gs_rw = gs_rw;
+    L.panel = pb;
+  };
+  // per-problem analysis on the host's cores (one problem per task)
+  parallel_for(count, analyse);
+  const auto t_analysed = std::chrono::steady_clock::now();
+  for (int q = 0; q < count; ++q) {
+    const Plan& L = plans[q];
+    if (L.code != MLAMG_OK) {
+      set_error(L.err + " (problem " + std::to_string(q) + ")");
+      return L.code;
+    }
+    lds_setup = std::max(lds_setup, L.lds_setup);
+    lds_cycles = std::max(lds_cycles, L.lds_cycles);
+    const mlamg_amg2v_problem& P = probs[q];
+    const int64_t n = P.n, nc = P.n_c;
     BDesc& D = desc[q];
     std::memset(&D, 0, sizeof(D));
     D.n = (int32_t)n;
@@ -820,10 +1360,13 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     D.KP = L.KP;
     D.KT = L.KT;
     D.nlev = L.nlev;
-    D.panel = pb;
+    D.panel = L.panel;
     D.n_chunks = L.clev.empty() ? 0 : (int32_t)L.clev.size() - 1;
     D.cap = L.cap;
     D.timing = timing ? 1 : 0;
+    D.spd = L.spd ? 1 : 0;
+    D.chol_nb = L.chol_nb;
+    D.gs_rw = L.gs_rw;
     D.tol = tol;
     D.omega = jacobi_weight;
     D.ak_col = lay.take(4 * L.akc.size());
@@ -842,6 +1385,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     D.b = lay.take(8 * n);
     D.x0 = lay.take(8 * n);
   }
+#undef REQ
   MLAMG_REQUIRE(lds_setup <= kBLdsBytes + 1024 && lds_cycles <= kBLdsBytes + 1024,
                 "LDS budget exceeded");
   const size_t in_bytes = lay.off;
@@ -857,7 +1401,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     BDesc& D = desc[q];
     D.x_out = lay.take(8 * (size_t)D.n);
     D.err_out = lay.take(8 * (size_t)std::max(max_iter, 1));
-    D.stat_out = lay.take(8 + 8 * 6);
+    D.stat_out = lay.take(16 + 8 * 6);
   }
   const size_t total = lay.off;
   // ---- pack the inputs into pinned host memory, one copy in
@@ -867,15 +1411,17 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     if (H.p) (void)hipHostFree(H.p);
     H.p = nullptr;
     H.cap = 0;
-    MLAMG_HIP(hipHostMalloc(&H.p, host_need, hipHostMallocDefault));
-    H.cap = host_need;
+    const size_t grow = host_need + host_need / 2;  // geometric: batches of similar size reuse it
+    MLAMG_HIP(hipHostMalloc(&H.p, grow, hipHostMallocDefault));
+    H.cap = grow;
   }
   char* hb = static_cast<char*>(H.p);
+  const auto t_pinned = std::chrono::steady_clock::now();
   std::memcpy(hb + desc_off, desc.data(), sizeof(BDesc) * count);
   auto put = [&](int64_t off, const void* src, size_t bytes) {
     if (bytes) std::memcpy(hb + off, src, bytes);
   };
-  for (int q = 0; q < count; ++q) {
+  parallel_for(count, [&](int q) {
     const mlamg_amg2v_problem& P = probs[q];
     const BDesc& D = desc[q];
     const Plan& L = plans[q];
@@ -892,15 +1438,14 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     put(D.pk_col, L.pkc.data(), 4 * L.pkc.size());
     put(D.pk_val, L.pkv.data(), 8 * L.pkv.size());
     put(D.pk_diag, L.pkd.data(), 8 * L.pkd.size());
-    if (!L.pkr.empty()) {
-      double* blv = reinterpret_cast<double*>(hb + D.b_lvl);
-      for (size_t p = 0; p < L.pkr.size(); ++p) blv[p] = P.b[L.pkr[p]];
-    }
+    put(D.b_lvl, L.blv.data(), 8 * L.blv.size());
     put(D.b, P.b, 8 * n);
     put(D.x0, P.x0, 8 * n);
-  }
+  });
+  const auto t_filled = std::chrono::steady_clock::now();
   char* arena = static_cast<char*>(scratch(total, 11));
   MLAMG_REQUIRE(arena, "device arena allocation failed");
+  const auto t_packed = std::chrono::steady_clock::now();
   MLAMG_HIP(hipMemcpyAsync(arena, hb, in_bytes, hipMemcpyHostToDevice, s));
   const BDesc* dd = reinterpret_cast<const BDesc*>(arena + desc_off);
   hipLaunchKernelGGL(k_amg2v_setup, dim3((unsigned)count), dim3(kBT), lds_setup, s, dd, arena);
@@ -915,6 +1460,17 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   // kernel (same stream), and the copy-out below is ordered after it
   MLAMG_HIP(hipMemcpyAsync(hb, arena + out_begin, total - out_begin, hipMemcpyDeviceToHost, s));
   MLAMG_HIP(hipStreamSynchronize(s));
+  if (timing) {
+    const auto t_done = std::chrono::steady_clock::now();
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    std::fprintf(stderr,
+                 "[amg2v_batch] %d problems: host %.3f ms (analysis %.3f, layout + pinned buffer "
+                 "%.3f, fill %.3f, device arena %.3f), copy in + kernels + copy out %.3f ms "
+                 "(%.2f MB in)\n",
+                 count, ms(t_begin, t_packed), ms(t_begin, t_analysed), ms(t_analysed, t_pinned),
+                 ms(t_pinned, t_filled), ms(t_filled, t_packed), ms(t_packed, t_done),
+                 in_bytes * 1e-6);
+  }
   for (int q = 0; q < count; ++q) {
     mlamg_amg2v_problem& P = probs[q];
     const BDesc& D = desc[q];
@@ -922,14 +1478,15 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     P.iters_out = st[0];
     P.status_out = st[1];
     if (timing) {
-      const int64_t* ts = reinterpret_cast<const int64_t*>(st + 2);
+      const int64_t* ts = reinterpret_cast<const int64_t*>(st + 4);
       std::fprintf(stderr,
                    "[amg2v_batch] problem %d n=%lld n_c=%lld iters=%d: galerkin %.3f ms, inverse "
-                   "%.3f ms (panels %.3f, updates %.3f), smoothing %.3f ms, rest of cycles "
-                   "%.3f ms\n",
+                   "(%s) %.3f ms (panels %.3f, updates %.3f), smoothing (%s) %.3f ms, rest of "
+                   "cycles %.3f ms\n",
                    q, (long long)P.n, (long long)P.n_c, st[0], ts[0] * 1e-5,
-                   (ts[1] + ts[4] + ts[5]) * 1e-5, ts[4] * 1e-5, ts[5] * 1e-5, ts[2] * 1e-5,
-                   ts[3] * 1e-5);
+                   st[2] == 1 ? "cholesky" : "gauss-jordan", 
+                   (ts[1] + ts[4] + ts[5]) * 1e-5, ts[4] * 1e-5, ts[5] * 1e-5,
+                   D.gs_rw ? "one wave" : "workgroup", ts[2] * 1e-5, ts[3] * 1e-5);
     }
     std::memcpy(P.x_out, hb + (D.x_out - out_begin), 8 * (size_t)P.n);
     if (max_iter > 0) std::memcpy(P.err_out, hb + (D.err_out - out_begin), 8 * (size_t)st[0]);

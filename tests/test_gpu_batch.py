@@ -168,6 +168,34 @@ def test_fused_edge_cases(oracle):
     assert xa[3] == xb[3] and np.array_equal(xa[2], xb[2])
 
 
+def test_fused_zero_diagonal_rows(oracle):
+    """Rows whose stored diagonal is 0.0: pyamg's sweep leaves x_i alone (the one-wave sweep
+    sends them to its sink slot), and the operator is no longer SPD, so the coarse solve takes
+    the Gauss-Jordan fallback. Histories vs the oracle (SuperLU coarse solve)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mlamg.multigrid
+    import mlamg.problems
+    import mlamg as ml
+    m = 24
+    A0 = ml.problems.poisson_2d_5pt(m)
+    P, _ = oracle.smoothed_aggregation_jacobi(A0, ml.problems.box_aggregates_2d(m, m, 3),
+                                              omega=2.0 / 3.0)
+    A = A0.copy()
+    for i in (0, 37, 300, m * m - 1):
+        lo, hi = A.indptr[i], A.indptr[i + 1]
+        A.data[lo + np.flatnonzero(A.indices[lo:hi] == i)] = 0.0
+    x0 = np.random.RandomState(11).randn(A.shape[0])
+    b = np.random.RandomState(12).randn(A.shape[0])
+    xr, cr, er, ir = oracle.amg_2_v(A, P, b, x0, res_tol=1e-300, max_iter=8)
+    xf, cf, ef, itf = ml.multigrid.amg_2_v(A, P, b, x0, res_tol=1e-300, max_iter=8,
+                                           engine="fused")
+    assert itf == ir == 8
+    assert np.allclose(ef, er, rtol=1e-10, atol=0), (ef, er)
+    assert np.abs(xf - xr).max() <= 1e-9 * np.abs(xr).max()
+
+
 def test_fused_wide_coarse(oracle):
     """n_c = 2025 (> 1024 + panel: the column-per-thread update branch of the blocked
     Gauss-Jordan) and n = 8100 with 2x2 aggregates, vs the oracle."""

@@ -101,9 +101,16 @@ def main():
     probs = _PROBS
     multigrid.amg_2_v_batch(probs[:6], res_tol=1e-10)
     torch.cuda.synchronize()
+    # first call at this batch size (host and device buffers grow inside it), then the steady
+    # state of a loop over a dataset (buffers reused): best of 5
     t0 = time.perf_counter()
     out = multigrid.amg_2_v_batch(probs, res_tol=1e-10)
-    t_f = time.perf_counter() - t0
+    rec["farm"]["device_fused_batch_first_call_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
+    t_f = 1e9
+    for _ in range(5):
+        t0 = time.perf_counter()
+        out = multigrid.amg_2_v_batch(probs, res_tol=1e-10)
+        t_f = min(t_f, time.perf_counter() - t0)
     its = [o[3] for o in out]
     ref_its = [orc.amg_2_v(*p, res_tol=1e-10)[3] for p in probs]
     rec["farm"]["device_fused_batch_ms"] = round(t_f * 1e3, 2)
