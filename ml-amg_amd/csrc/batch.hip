@@ -61,7 +61,7 @@ struct BDesc {
   int32_t n, nc, smoother, nu_pre, nu_post, norm_mode, max_iter;
   int32_t K, KA, KP, KT, nlev, panel, n_chunks, cap, timing;
   int32_t spd;    // A symmetric: try the inverse Cholesky factor before Gauss-Jordan
-  int32_t chol_nb;  // its panel width (4..32, from n_c)
+  int32_t chol_nb;  // its panel width (4..16, from n_c)
   int32_t gs_rw;  // one-wave sweep (rows of K = 4 or 8 slots, levels <= 64 * gs_rw rows), 1 or 2
                   // rows per lane; 0: the workgroup sweeps each level
   double tol, omega;
@@ -197,43 +197,55 @@ __device__ __forceinline__ void packed_dot_rows(const int32_t* __restrict__ col,
   }
 }
 
-// out[j] = sum over the row's span of M[j][k] v[k], a wave per row, lane-strided partial sums in
-// k then a butterfly (fixed order); two rows per wave in flight. SPAN 0: [0, nc) (the
-// Gauss-Jordan inverse), 1: [0, j] (L^-1, lower), 2: [j, nc) (L^-T, upper).
+// out[j] = sum over the row's span of M[j][k] v[k]: a wave takes four rows at a time (rows
+// w, w + 16, w + 32, w + 48 of its group) and streams them in 64-column chunks at absolute
+// positions k = o + lane, four chunks per pass (16 matrix loads per lane in flight, the vector
+// loads shared by the four rows); lane partial sums in chunk order, then a butterfly (fixed
+// order). SPAN 0: [0, nc) (the Gauss-Jordan inverse), 1: [0, j] (L^-1, lower), 2: [j, nc)
+// (L^-T, upper).
 template <int SPAN>
 __device__ __forceinline__ void rows_dot(const double* __restrict__ M, int nc,
                                          const double* v, double* out, int tid) {
+  constexpr int R = 4, U = 4;
   const int w = tid >> 6, lane = tid & 63;
-  for (int j = w; j < nc; j += 2 * kBWaves) {
-    const int jb = j + kBWaves;
-    const bool two = jb < nc;
-    const int lo1 = SPAN == 2 ? j : 0, hi1 = SPAN == 1 ? j + 1 : nc;
-    const int lo2 = SPAN == 2 ? jb : 0, hi2 = two ? (SPAN == 1 ? jb + 1 : nc) : 0;
-    const double* r1 = M + (int64_t)j * nc;
-    const double* r2 = M + (int64_t)(two ? jb : j) * nc;
-    double s1 = 0.0, s2 = 0.0;
-    for (int o = 0; lo1 + o < hi1 || lo2 + o < hi2; o += 4 * 64) {
-      double m1[4], x1[4], m2[4], x2[4];
+  for (int j0 = w; j0 < nc; j0 += R * kBWaves) {
+    int lo[R], hi[R];
+    const double* rp[R];
+    int omin = nc, omax = 0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k1 = lo1 + o + lane + u * 64, k2 = lo2 + o + lane + u * 64;
-        const bool in1 = k1 < hi1, in2 = k2 < hi2;
-        m1[u] = in1 ? r1[k1] : 0.0;
-        x1[u] = in1 ? v[k1] : 0.0;
-        m2[u] = in2 ? r2[k2] : 0.0;
-        x2[u] = in2 ? v[k2] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        s1 = fma(m1[u], x1[u], s1);
-        s2 = fma(m2[u], x2[u], s2);
+    for (int r = 0; r < R; ++r) {
+      const int j = j0 + r * kBWaves;
+      const bool ok = j < nc;
+      lo[r] = ok ? (SPAN == 2 ? j : 0) : 0;
+      hi[r] = ok ? (SPAN == 1 ? j + 1 : nc) : 0;
+      rp[r] = M + (int64_t)(ok ? j : j0) * nc;
+      if (ok) {
+        omin = min(omin, lo[r]);
+        omax = max(omax, hi[r]);
       }
     }
-    s1 = bw_sum(s1);
-    s2 = bw_sum(s2);
-    if (lane == 0) {
-      out[j] = s1;
-      if (two) out[jb] = s2;
+    double sum[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) sum[r] = 0.0;
+    for (int o = omin & ~63; o < omax; o += U * 64) {
+      double m[R][U], x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = o + u * 64 + lane;
+        x[u] = k < nc ? v[k] : 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) m[r][u] = (k >= lo[r] && k < hi[r]) ? rp[r][k] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r) sum[r] = fma(m[r][u], x[u], sum[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double t = bw_sum(sum[r]);
+      const int j = j0 + r * kBWaves;
+      if (lane == 0 && j < nc) out[j] = t;
     }
   }
 }
@@ -289,147 +301,175 @@ __device__ __forceinline__ void panel_update(double* AH, const double* pan, int 
 // In-place inverse Cholesky factor of an SPD matrix: M (nc x nc, row-major, lower triangle read)
 // becomes L^-1 (lower triangle; the upper triangle is left as scratch), A = L L^T. Right-looking
 // blocked elimination of [A | I] by NB-column panels: per panel the diagonal block is factorised
-// (L11) and inverted (Li = L11^-1) in LDS, L21 = A21 Li^T and the panel's final rows
-// Z = Li [X_top | I] are formed, then every trailing row i takes
+// (L11) in LDS, L21 = A21 L11^-T and the panel's final rows Z = L11^-1 [X_top | I] are formed by
+// triangular solves, then every trailing row i takes
 //   M[i, 0:k1]  <- [X_i, 0] - L21_i Z          (the rows of L^-1 being accumulated)
 //   M[i, k1:i]  <- M[i, k1:i] - L21_i L21^T     (the Schur complement, lower triangle)
-// in 4x4 register tiles over LDS operands: nc^3/3 fused multiply-adds, no pivoting. Returns
+// in 16x16 fp64 MFMA tiles over LDS operands: nc^3/3 multiply-adds, no pivoting. Returns
 // false (uniformly) on a non-positive pivot: the caller falls back to Gauss-Jordan.
+typedef double mfma_d4 __attribute__((ext_vector_type(4)));
+
 template <int NB, class Stamp>
 __device__ bool chol_inverse(double* __restrict__ M, int nc, double* lds, int tid, Stamp stamp) {
   constexpr int ds = NB + 1;
   double* Dg = lds;                           // NB x ds: diagonal block -> L11
-  double* Li = Dg + NB * ds;                  // NB x ds: L11^-1
+  double* Li = Dg + NB * ds;                  // NB: 1 / diag(L11)
   double* P21 = Li + NB * ds;                 // (nc - k1) x ds: A21 -> L21
   double* Z = P21 + (int64_t)nc * ds;         // NB x nc: the panel's rows of L^-1
-  const int r = tid / NB, c = tid % NB;
-  const bool act = tid < NB * NB;
+  __shared__ int fail;
+  const int lane = tid & 63;
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
   for (int k0 = 0; k0 < nc; k0 += NB) {
     const int bw = min(NB, nc - k0), k1 = k0 + bw;
-    if (act) Dg[r * ds + c] = (r < bw && c <= r) ? M[(int64_t)(k0 + r) * nc + k0 + c] : 0.0;
-    __syncthreads();
-    for (int t = 0; t < bw; ++t) {
-      const double dtt = Dg[t * ds + t];
-      if (!(dtt > 0.0)) return false;  // same value in every thread
-      const double s = sqrt(dtt);
-      const double lrt = (act && r < bw && r > t) ? Dg[r * ds + t] / s : 0.0;
-      const double lct = (act && c < bw && c > t) ? Dg[c * ds + t] / s : 0.0;
-      __syncthreads();
-      if (act && r < bw) {
-        if (c == t && r >= t)
-          Dg[r * ds + t] = (r == t) ? s : lrt;
-        else if (c > t && c <= r)
-          Dg[r * ds + c] -= lrt * lct;
+    if (tid < 64) {
+      // wave 0: the diagonal block, factorised (right-looking, wave-synchronous steps) with its
+      // reciprocal diagonal, while the other waves stage the panel below it and [X_top | I]
+      for (int q = lane; q < NB * NB; q += 64) {
+        const int rr = q / NB, cc = q % NB;
+        Dg[rr * ds + cc] = (rr < bw && cc <= rr) ? M[(int64_t)(k0 + rr) * nc + k0 + cc] : 0.0;
       }
-      __syncthreads();
-    }
-    // Li = L11^-1, a column per thread (each column depends only on itself)
-    if (tid < bw) {
-      const int cc = tid;
-      Li[cc * ds + cc] = 1.0 / Dg[cc * ds + cc];
-      for (int rr = cc + 1; rr < bw; ++rr) {
-        double s2 = 0.0;
-        for (int k = cc; k < rr; ++k) s2 = fma(Dg[rr * ds + k], Li[k * ds + cc], s2);
-        Li[rr * ds + cc] = -s2 / Dg[rr * ds + rr];
-      }
-    }
-    __syncthreads();
-    stamp(4);
-    // A21 (rows below the panel; bw == NB whenever such rows exist) and X_top into LDS
-    for (int64_t q = tid; q < (int64_t)(nc - k1) * NB; q += kBT) {
-      const int i = (int)(q / NB), s = (int)(q % NB);
-      P21[(int64_t)i * ds + s] = M[(int64_t)(k1 + i) * nc + k0 + s];
-    }
-    for (int64_t q = tid; q < (int64_t)bw * k0; q += kBT) {
-      const int t = (int)(q / k0), j = (int)(q % k0);
-      Z[(int64_t)t * nc + j] = M[(int64_t)(k0 + t) * nc + j];
-    }
-    __syncthreads();
-    // L21 = A21 Li^T in place, a row per thread: column t needs columns s <= t only, so going
-    // from the last column down leaves every operand unread-over
-    for (int i = tid; i < nc - k1; i += kBT) {
-      double* row = P21 + (int64_t)i * ds;
-      for (int t = NB - 1; t >= 0; --t) {
-        double l = 0.0;
-        for (int s = 0; s <= t; ++s) l = fma(row[s], Li[t * ds + s], l);
-        row[t] = l;
-      }
-    }
-    // Z = Li [X_top | I]: final rows k0..k1-1 of L^-1, kept in LDS for the trailing update (in
-    // place per column, last row first, as above)
-    for (int j = tid; j < k1; j += kBT) {
-      if (j < k0) {
-        for (int t = bw - 1; t >= 0; --t) {
-          double z = 0.0;
-          for (int s = 0; s <= t; ++s) z = fma(Li[t * ds + s], Z[(int64_t)s * nc + j], z);
-          Z[(int64_t)t * nc + j] = z;
-          M[(int64_t)(k0 + t) * nc + j] = z;
+      wave_sync();
+      // each lane owns entries q = lane + 64 e of the block; a step reads its column-t
+      // factors, then (after every lane has read) writes the step's new values
+      constexpr int E = (NB * NB + 63) / 64;
+      bool ok = true;
+      for (int t = 0; t < bw; ++t) {
+        const double dtt = Dg[t * ds + t];
+        if (!(dtt > 0.0)) {  // same value in every lane
+          ok = false;
+          break;
         }
-      } else {
-        const int s0 = j - k0;
+        const double sq = sqrt(dtt);
+        double nv[E];
+        bool wr[E];
 #pragma unroll
-        for (int t = 0; t < NB; ++t) {
-          if (t < bw) {
-            const double z = s0 <= t ? Li[t * ds + s0] : 0.0;
-            Z[(int64_t)t * nc + j] = z;
-            if (s0 <= t) M[(int64_t)(k0 + t) * nc + j] = z;
+        for (int e = 0; e < E; ++e) {
+          const int q = lane + 64 * e, rr = q / NB, cc = q % NB;
+          wr[e] = q < NB * NB && rr < bw && cc <= rr && cc >= t;
+          nv[e] = 0.0;
+          if (wr[e]) {
+            if (cc == t)
+              nv[e] = rr == t ? sq : Dg[rr * ds + t] / sq;
+            else
+              nv[e] = Dg[rr * ds + cc] - (Dg[rr * ds + t] / sq) * (Dg[cc * ds + t] / sq);
           }
         }
+        wave_sync();
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int q = lane + 64 * e;
+          if (wr[e]) Dg[(q / NB) * ds + q % NB] = nv[e];
+        }
+        wave_sync();
+      }
+      if (ok && lane < bw) Li[lane] = 1.0 / Dg[lane * ds + lane];  // reciprocal diagonal
+      if (lane == 0) fail = ok ? 0 : 1;
+    } else {
+      // A21 (rows below the panel; bw == NB whenever such rows exist) and X_top into LDS
+      const int t2 = tid - 64, nt2 = kBT - 64;
+      for (int64_t q = t2; q < (int64_t)(nc - k1) * NB; q += nt2) {
+        const int i = (int)(q / NB), s = (int)(q % NB);
+        P21[(int64_t)i * ds + s] = M[(int64_t)(k1 + i) * nc + k0 + s];
+      }
+      for (int64_t q = t2; q < (int64_t)bw * k0; q += nt2) {
+        const int t = (int)(q / k0), j = (int)(q % k0);
+        Z[(int64_t)t * nc + j] = M[(int64_t)(k0 + t) * nc + j];
+      }
+      for (int q = t2; q < bw * bw; q += nt2) {  // [X_top | I]: the identity columns
+        const int t = q / bw, jj = q % bw;
+        Z[(int64_t)t * nc + k0 + jj] = t == jj ? 1.0 : 0.0;
+      }
+    }
+    __syncthreads();
+    if (fail) return false;  // uniform
+    stamp(4);
+    // L21 = A21 L11^-T and Z = L11^-1 [X_top | I] by triangular solves with L11, a row of L21
+    // or a column of Z per thread, in place (entry t needs only entries s < t): the identity
+    // columns make Z's last bw columns L11^-1
+    for (int i = tid; i < nc - k1; i += kBT) {
+      double* row = P21 + (int64_t)i * ds;
+      for (int t = 0; t < NB; ++t) {
+        double l = row[t];
+        for (int s = 0; s < t; ++s) l = fma(-row[s], Dg[t * ds + s], l);
+        row[t] = l * Li[t];
+      }
+    }
+    for (int j = tid; j < k1; j += kBT) {
+      for (int t = 0; t < bw; ++t) {
+        double z = Z[(int64_t)t * nc + j];
+        for (int s = 0; s < t; ++s) z = fma(-Dg[t * ds + s], Z[(int64_t)s * nc + j], z);
+        z *= Li[t];
+        Z[(int64_t)t * nc + j] = z;
+        M[(int64_t)(k0 + t) * nc + j] = z;
       }
     }
     __syncthreads();
     if (k1 < nc) {
-      // 4x4 tiles over rows [k1, nc) x columns [0, i]: row block rb has a4 + rb + 1 column
-      // blocks (k1 is a multiple of 4), C(rb) tiles precede it
-      const int64_t a4 = k1 / 4, nrb = (nc - k1 + 3) / 4;
-      auto C = [&](int64_t rb) { return rb * (a4 + 1) + rb * (rb - 1) / 2; };
+      // 16 x 16 tiles over rows [k1, nc) x columns [0, i], a wave per tile, on the fp64 matrix
+      // cores: D = C + (-L21 rows) x W, W = Z (columns < k1) or L21^T (columns >= k1), NB/4
+      // v_mfma_f64_16x16x4 steps. Lane l supplies A[row l&15][k l>>4] and B[k l>>4][col l&15]
+      // and holds D[row (l>>4) + 4 r][col l&15]. Row block rb has a16 + rb + 1 column blocks,
+      // C(rb) tiles precede it; a tile may straddle k0 or k1 (sources are picked per element).
+      const int w = tid >> 6, lr = lane & 15, lk = lane >> 4;
+      const int64_t a16 = (k1 + 15) / 16, nrb = (nc - k1 + 15) / 16;
+      auto C = [&](int64_t rb) { return rb * (a16 + 1) + rb * (rb - 1) / 2; };
       const int64_t T = C(nrb);
       const int last = nc - k1 - 1;
-      for (int64_t q = tid; q < T; q += kBT) {
-        const double bq = (double)a4 + 0.5;
+      auto coords = [&](int64_t q, int& i0, int& j0) {
+        const double bq = (double)a16 + 0.5;
         int64_t rb = (int64_t)(-bq + sqrt(bq * bq + 2.0 * (double)q));
         while (rb > 0 && C(rb) > q) --rb;
         while (C(rb + 1) <= q) ++rb;
-        const int i0 = k1 + 4 * (int)rb, j0 = 4 * (int)(q - C(rb));
-        const bool xpart = j0 < k1, zero = j0 >= k0 && j0 < k1;
-        double acc[4][4];
+        i0 = k1 + 16 * (int)rb;
+        j0 = 16 * (int)(q - C(rb));
+      };
+      auto load_c = [&](int i0, int j0, mfma_d4& acc) {
+        const int jc = j0 + lr;
+        const bool zero = jc >= k0 && jc < k1;
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + lk + 4 * r;
+          acc[r] = (!zero && i < nc && jc < nc) ? M[(int64_t)i * nc + jc] : 0.0;
+        }
+      };
+      // the next tile's C is loaded before this tile's MFMAs (its global round trip overlaps)
+      int i0 = 0, j0 = 0;
+      mfma_d4 acc;
+      if (w < T) {
+        coords(w, i0, j0);
+        load_c(i0, j0, acc);
+      }
+      for (int64_t q = w; q < T; q += kBWaves) {
+        int i0n = i0, j0n = j0;
+        mfma_d4 accn = acc;
+        if (q + kBWaves < T) {
+          coords(q + kBWaves, i0n, j0n);
+          load_c(i0n, j0n, accn);
+        }
+        const int jc = j0 + lr;  // this lane's output column
+        const double* arow = P21 + (int64_t)min(i0 + lr - k1, last) * ds;
+        const bool from_z = jc < k1;
+        const double* brow = P21 + (int64_t)min(max(jc - k1, 0), last) * ds;
+        const int jz = min(jc, k1 - 1);
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const int i = i0 + u, j = j0 + v;
-            acc[u][v] = (!zero && i < nc && j < nc) ? M[(int64_t)i * nc + j] : 0.0;
-          }
-        const double* ar[4];
-        const double* wr[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) ar[u] = P21 + (int64_t)min(i0 + u - k1, last) * ds;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) wr[v] = P21 + (int64_t)min(max(j0 + v - k1, 0), last) * ds;
-#pragma unroll 4
-        for (int t = 0; t < NB; ++t) {
-          double a[4], w[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) a[u] = ar[u][t];
-          if (xpart) {
-#pragma unroll
-            for (int v = 0; v < 4; ++v) w[v] = Z[(int64_t)t * nc + j0 + v];
-          } else {
-#pragma unroll
-            for (int v = 0; v < 4; ++v) w[v] = wr[v][t];
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) acc[u][v] = fma(-a[u], w[v], acc[u][v]);
+        for (int kk = 0; kk < NB; kk += 4) {
+          const int k = kk + lk;
+          const double av = -arow[k];
+          const double bv = from_z ? Z[(int64_t)k * nc + jz] : brow[k];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const int i = i0 + u, j = j0 + v;
-            if (i < nc && j < nc) M[(int64_t)i * nc + j] = acc[u][v];
-          }
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + lk + 4 * r;
+          if (i < nc && jc < nc) M[(int64_t)i * nc + jc] = acc[r];
+        }
+        i0 = i0n;
+        j0 = j0n;
+        acc = accn;
       }
       __syncthreads();
     }
@@ -497,7 +537,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
     }
   };
   if (D.timing && tid == 0)
-    for (int q = 0; q < 6; ++q) tstat[q] = 0;
+    for (int q = 0; q < 8; ++q) tstat[q] = 0;
 
   dense_galerkin(D, arena, AH, tid);
   stamp(0);
@@ -505,8 +545,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
   if (D.spd) {
     // the panel width is the problem's own (a function of n_c alone): a problem's roundings do
     // not depend on the batch it is launched with
-    const bool ok = D.chol_nb == 32   ? chol_inverse<32>(AH, nc, lds, tid, stamp)
-                    : D.chol_nb == 16 ? chol_inverse<16>(AH, nc, lds, tid, stamp)
+    const bool ok = D.chol_nb == 16   ? chol_inverse<16>(AH, nc, lds, tid, stamp)
                     : D.chol_nb == 8  ? chol_inverse<8>(AH, nc, lds, tid, stamp)
                                       : chol_inverse<4>(AH, nc, lds, tid, stamp);
     if (ok) {
@@ -722,12 +761,13 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
   double* xs = lds;                                     // n + 2: x, a zero slot, a sink slot
   double* rcs = xs + n + 2;                             // nc: restricted residual
   double* es = rcs + nc;                                // nc: coarse correction
-  double* ys = es + nc;                                 // nc: L^-1 r_H
-  double* rs = R_LDS ? ys + nc : at<double>(arena, D.rg);  // n: residual
+  double* rs = R_LDS ? es + nc : at<double>(arena, D.rg);  // n: residual
+  double* ys = rs;  // nc <= n: L^-1 r_H, in r's storage (r is dead from the restriction to the
+                    // next residual)
   // GS staging area, 16-byte aligned (the one-wave sweep reads its rows with 16-byte loads)
   // (an even double offset from the LDS base: index arithmetic keeps the LDS address space,
   // which an integer round trip would lose to flat accesses)
-  const int64_t stage_off = ((R_LDS ? (ys - lds) + nc + n : (ys - lds) + nc) + 1) & ~int64_t(1);
+  const int64_t stage_off = ((R_LDS ? (es - lds) + nc + n : (es - lds) + nc) + 1) & ~int64_t(1);
   double* stage = lds + stage_off;
   const double* __restrict__ x0 = at<double>(arena, D.x0);
   #pragma unroll 1
@@ -993,6 +1033,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
       if (rows[1] >= 0) rcs[rows[1]] = y[1];
     }
     __syncthreads();
+    stamp(3);
     if (mode == 1) {  // e = L^-T (L^-1 r_H)
       rows_dot<1>(AH, nc, rcs, ys, tid);
       __syncthreads();
@@ -1001,6 +1042,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
       rows_dot<0>(AI, nc, rcs, es, tid);
     }
     __syncthreads();
+    stamp(6);
     #pragma unroll 1
     for (int i0 = tid; i0 < n; i0 += 4 * kBT) {  // x += P e
       int rows[4];
@@ -1173,7 +1215,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   // residual in LDS when every problem leaves room for it
   bool r_lds = true;
   for (int q = 0; q < count; ++q) {
-    const size_t need = (size_t)probs[q].n * 16 + 16 + (size_t)probs[q].n_c * 24 + 16 * 1024;
+    const size_t need = (size_t)probs[q].n * 16 + 16 + (size_t)probs[q].n_c * 16 + 16 * 1024;
     if (need > kBLdsBytes) r_lds = false;
   }
   Layout lay;
@@ -1224,14 +1266,15 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       L.err = "amg2v_batch: rows of A, P or P^T longer than the batched solver's slots";
       return;
     }
-    int chol_nb = 32;  // the widest panel that fits
+    int chol_nb = 16;  // the widest panel that fits (wider panels lengthen the per-thread
+                       // triangular solves more than they save in trailing passes)
     while (chol_nb > 4 && chol_lds(chol_nb, nc) > kBLdsBytes) chol_nb >>= 1;
     const bool spd = csr_symmetric(n, P.A_indptr, P.A_indices, P.A_data) &&
                      chol_lds(chol_nb, nc) <= kBLdsBytes;
     if (spd) L.lds_setup = chol_lds(chol_nb, nc);
-    // cycle vectors in LDS: x (+ zero and sink slots), r when it fits, r_H, e_H, L^-1 r_H; the
-    // sweep's staging area gets the rest
-    const size_t vec_lds = (size_t)n * 8 * (r_lds ? 2 : 1) + 16 + (size_t)nc * 24;
+    // cycle vectors in LDS: x (+ zero and sink slots), r when it fits (L^-1 r_H shares it), r_H,
+    // e_H; the sweep's staging area gets the rest
+    const size_t vec_lds = (size_t)n * 8 * (r_lds ? 2 : 1) + 16 + (size_t)nc * 16;
     const size_t room = kBLdsBytes > vec_lds + 64 ? kBLdsBytes - vec_lds - 64 : 0;
     int gs_rw = 0;
     if (smoother == 0) {
@@ -1401,7 +1444,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     BDesc& D = desc[q];
     D.x_out = lay.take(8 * (size_t)D.n);
     D.err_out = lay.take(8 * (size_t)std::max(max_iter, 1));
-    D.stat_out = lay.take(16 + 8 * 6);
+    D.stat_out = lay.take(16 + 8 * 8);
   }
   const size_t total = lay.off;
   // ---- pack the inputs into pinned host memory, one copy in
@@ -1482,11 +1525,12 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       std::fprintf(stderr,
                    "[amg2v_batch] problem %d n=%lld n_c=%lld iters=%d: galerkin %.3f ms, inverse "
                    "(%s) %.3f ms (panels %.3f, updates %.3f), smoothing (%s) %.3f ms, rest of "
-                   "cycles %.3f ms\n",
+                   "cycles %.3f ms (coarse solve %.3f ms)\n",
                    q, (long long)P.n, (long long)P.n_c, st[0], ts[0] * 1e-5,
                    st[2] == 1 ? "cholesky" : "gauss-jordan", 
                    (ts[1] + ts[4] + ts[5]) * 1e-5, ts[4] * 1e-5, ts[5] * 1e-5,
-                   D.gs_rw ? "one wave" : "workgroup", ts[2] * 1e-5, ts[3] * 1e-5);
+                   D.gs_rw ? "one wave" : "workgroup", ts[2] * 1e-5, (ts[3] + ts[6]) * 1e-5,
+                   ts[6] * 1e-5);
     }
     std::memcpy(P.x_out, hb + (D.x_out - out_begin), 8 * (size_t)P.n);
     if (max_iter > 0) std::memcpy(P.err_out, hb + (D.err_out - out_begin), 8 * (size_t)st[0]);

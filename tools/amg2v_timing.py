@@ -68,6 +68,14 @@ def main():
         t_pool = time.perf_counter() - t0
     rec["farm"]["cpu_sequential_ms"] = round(t_seq * 1e3, 2)
     rec["farm"]["cpu_pool_ms"] = round(t_pool * 1e3, 2)
+    # the same pool over a 256-grid farm
+    _PROBS = make_farm(256)
+    with mp.get_context("fork").Pool(threads) as pool:
+        pool.map(_cpu_solve, range(threads))
+        t0 = time.perf_counter()
+        pool.map(_cpu_solve, range(len(_PROBS)), chunksize=1)
+        rec["farm"]["cpu_pool256_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
+    _PROBS = make_farm()
     print(f"48 grids: CPU restatement sequential {t_seq*1e3:.1f} ms ({t_seq/48*1e3:.2f} ms/grid); "
           f"pool of {threads} processes {t_pool*1e3:.1f} ms", flush=True)
     # ---- GPU
@@ -82,7 +90,7 @@ def main():
         x0 = np.random.RandomState(0).randn(n)
         b = np.zeros(n)
         row = {"grid": f"{m}^2", "n": n, "n_c": P.shape[1]}
-        for eng in ("auto", "hierarchy"):
+        for eng in ("auto", "fused", "hierarchy"):
             multigrid.amg_2_v(A, P, b, x0, res_tol=1e-10, engine=eng)  # warm
             reps = 5
             t0 = time.perf_counter()
@@ -121,6 +129,22 @@ def main():
     rec["farm"]["device_threaded_hierarchy_ms"] = round(t_h * 1e3, 2)
     rec["farm"]["speedup_vs_cpu_pool"] = round(t_pool / t_f, 2)
     print(json.dumps(rec["farm"]), flush=True)
+    # a dataset-sized farm: 256 grids (one launch fills more of the 256 CUs)
+    big = make_farm(256)
+    t0 = time.perf_counter()
+    out = multigrid.amg_2_v_batch(big, res_tol=1e-10)
+    t_first = time.perf_counter() - t0
+    t_b = 1e9
+    for _ in range(3):
+        t0 = time.perf_counter()
+        out = multigrid.amg_2_v_batch(big, res_tol=1e-10)
+        t_b = min(t_b, time.perf_counter() - t0)
+    rec["farm256"] = {"device_fused_batch_first_call_ms": round(t_first * 1e3, 2),
+                      "device_fused_batch_ms": round(t_b * 1e3, 2),
+                      "cpu_pool_ms": rec["farm"].get("cpu_pool256_ms")}
+    if rec["farm256"]["cpu_pool_ms"]:
+        rec["farm256"]["speedup_vs_cpu_pool"] = round(rec["farm256"]["cpu_pool_ms"] / (t_b * 1e3), 2)
+    print(json.dumps(rec["farm256"]), flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as fh:
         json.dump(rec, fh, indent=1)
