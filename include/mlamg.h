@@ -190,6 +190,16 @@ int mlamg_lambda_max_dinvA(const mlamg_csr* A, int max_iter, double tol, uint64_
 /* strength-of-connection graph (utils/common.py:26,28,29): mode 0 abs, 1 invabs, 2 unit. */
 int mlamg_strength(const mlamg_csr* A, int mode, mlamg_csr** out, void* stream);
 
+/* Evolution strength of connection: pyamg.strength.evolution_strength_of_connection(A) at the
+ * reference's arguments (B = ones, k = 2, proj_type 'l2', symmetrized; epsilon = the drop
+ * tolerance, pyamg default 4.0), as used by utils/common.py:27,30 (csrc/strength.hip). A: CSR with
+ * ascending column indices and no explicit zeros; rho = spectral radius of D^-1 A (pyamg
+ * estimates it by Arnoldi; the caller supplies it). mode 0: the evolution measure itself,
+ * 1: + 0.1 * unit(A) (the reference's 'evolution'), 2: + 1/|A| (the reference's 'olson').
+ * *out: new CSR, ascending columns. Syncs. */
+int mlamg_evolution_strength(const mlamg_csr* A, double rho, double epsilon, int mode,
+                             mlamg_csr** out, void* stream);
+
 /* Seeded Bellman-Ford (ns/lib/graph.py:7-53) on edge weights G (row i -> col j, weight g_ij,
  * evaluated in fp32 like the torch reference). dist_f32[n], cluster[n] (node id of the nearest
  * seed, -1 if unreachable). Ties broken deterministically by the smallest seed node id.

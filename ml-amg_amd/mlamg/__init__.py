@@ -7,6 +7,8 @@ Mirrors the reference modules on the hot path:
   mlamg.graph           <- ns/lib/graph.py       (modified_bellman_ford, nearest_center_to_agg,
                                                   lloyd_aggregation)
   mlamg.sparse          <- ns/lib/sparse.py      (scipy <-> torch, device CSR handles)
+  mlamg.strength        <- utils/common.py:25-31 (strength_measure_funcs; pyamg's evolution
+                                                  strength of connection on the device)
   mlamg.preconditioner  <- ns/preconditioner     (MLAMG PC: initialize/update/apply)
   mlamg.hierarchy       multilevel device hierarchy + V-cycle executor (precondition/solve)
   mlamg.distributed     fine level row-partitioned over GPUs (RCCL halo exchange)
@@ -19,8 +21,8 @@ import importlib
 
 __version__ = "0.1.0"
 
-_SUBMODULES = ("multigrid", "graph", "sparse", "hierarchy", "preconditioner", "problems",
-               "gridio", "distributed", "_lib")
+_SUBMODULES = ("multigrid", "graph", "sparse", "strength", "hierarchy", "preconditioner",
+               "problems", "gridio", "distributed", "_lib")
 
 
 def __getattr__(name):

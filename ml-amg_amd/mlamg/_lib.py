@@ -96,6 +96,7 @@ SIGNATURES = {
     "mlamg_csr_scale_rows": (c_int, [c_vp, c_vp, c_int, c_vpp, c_vp]),
     "mlamg_lambda_max_dinvA": (c_int, [c_vp, c_int, c_dbl, c_u64, P_dbl, P_int, c_vp]),
     "mlamg_strength": (c_int, [c_vp, c_int, c_vpp, c_vp]),
+    "mlamg_evolution_strength": (c_int, [c_vp, c_dbl, c_dbl, c_int, c_vpp, c_vp]),
     "mlamg_bellman_ford": (c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, P_i32, c_vp]),
     "mlamg_aggregate_op": (c_int, [c_vp, c_i64, c_i64, c_vpp, c_vp]),
     "mlamg_labels_to_columns": (c_int, [c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),

@@ -1,7 +1,8 @@
 """Device AMG hierarchy: setup on the GPU and the V-cycle executor (mlamg_hier_*).
 
 Setup per level follows the reference's aggregation-based SA recipe, all on the device:
-  C = strength(A)                                    utils/common.py:25-31 ('invabs', 'abs', 'unit')
+  C = strength(A)                                    utils/common.py:25-31 ('invabs', 'abs', 'unit',
+                                                     'evolution', 'olson')
   seeds = RandomState(seed).permutation(n)[:ceil(alpha*n)]       graph.py:230-231; evaluate_dataset.py:80-85
   (dist, label) = Bellman-Ford(C, seeds)            graph.py:7-53   (or Lloyd: graph.py:156-239)
   Agg = aggregate operator(label)                   graph.py:56-86
@@ -33,7 +34,13 @@ from .sparse import DeviceCSR, _device, as_device, galerkin, to_device_vec
 STRENGTH_MODES = {"abs": 0, "invabs": 1, "unit": 2, "same": 3}
 
 
-def strength(A_dev, mode="invabs"):
+def strength(A_dev, mode="invabs", rho=None):
+    """Strength graph of a device operator: the elementwise measures of utils/common.py:26,28,29
+    or the evolution measures of :27,30 ('evolution', 'olson'; rho(D^-1 A) = rho, default the
+    device Lanczos value)."""
+    if mode in ("evolution", "olson"):
+        from .strength import evolution_device
+        return evolution_device(A_dev, mode, rho=rho)
     h = ctypes.c_void_p()
     call("mlamg_strength", A_dev.handle, STRENGTH_MODES[mode], ctypes.byref(h), stream_ptr())
     return DeviceCSR(h)

@@ -306,17 +306,22 @@ STRENGTH = {
 
 
 def build_hierarchy(A, alpha=0.1, strength_mode="invabs", seed=0, sort_seeds=True,
-                    max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, omegas=None):
+                    max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, omegas=None,
+                    rhos=None):
     """CPU restatement of mlamg.hierarchy.Hierarchy.build (aggregation='bellman_ford').
 
     omegas: per-level SA weights to use (e.g. the device's); None -> ARPACK (multigrid.py:105).
+    rhos: per-level rho(D^-1 A) for the evolution measures ('evolution', 'olson').
     Returns a list of level dicts and the coarsest matrix.
     """
     levels = []
     A = canonical(A)
     while A.shape[0] > max_coarse and len(levels) + 1 < max_levels:
         n = A.shape[0]
-        C = STRENGTH[strength_mode](A)
+        if strength_mode in ("evolution", "olson"):
+            C = strength_measure(A, strength_mode, rho=None if rhos is None else rhos[len(levels)])
+        else:
+            C = STRENGTH[strength_mode](A)
         k = int(math.ceil(alpha * n))
         seeds = np.random.RandomState(seed).permutation(n)[:k]
         if sort_seeds:
@@ -466,3 +471,148 @@ def vcycle_omp(levels, Ainv, b, x, n_cycles, threads):
         L.omp_resid(x.shape[0], *csr(A0), P_(b), P_(x), P_(r0))
         hist.append(L.omp_norm2(x.shape[0], P_(r0)))
     return x, np.array(hist)
+
+
+# --------------------------------------------------------------------------------------------
+# Evolution strength of connection: pyamg.strength.evolution_strength_of_connection (pyamg 4.x/5.x,
+# absent here: restated from its published algorithm; parity unpinned — no reference fixture
+# pins it) at the reference's arguments (B=None -> ones, epsilon=4, k=2, proj_type 'l2',
+# symmetrize_measure=True), as called by utils/common.py:27,30. The scipy steps are pyamg's own
+# scipy calls; its three amg_core kernels are restated below.
+
+def approximate_spectral_radius(A, tol=0.01, maxiter=15, restart=5):
+    """pyamg.util.linalg.approximate_spectral_radius (nonsymmetric Arnoldi with modified
+    Gram-Schmidt, restarted from the Ritz vector; initial vector np.random.rand)."""
+    n = A.shape[0]
+    maxiter = min(n, maxiter)
+    v0 = np.random.rand(n, 1)
+    ev_max = 0.0
+    for _ in range(restart + 1):
+        v = v0 / la.norm(v0)
+        H = np.zeros((maxiter + 1, maxiter))
+        V = [v]
+        breakdown = np.finfo(float).eps * 1e6
+        flag = False
+        j = 0
+        for j in range(maxiter):
+            w = A @ V[-1]
+            for i, vi in enumerate(V):
+                H[i, j] = np.dot(vi.ravel(), w.ravel())
+                w = w - H[i, j] * vi
+            H[j + 1, j] = la.norm(w)
+            if H[j + 1, j] < breakdown:
+                flag = True
+                if H[j + 1, j] != 0.0:
+                    w = w / H[j + 1, j]
+                V.append(w)
+                break
+            w = w / H[j + 1, j]
+            V.append(w)
+        import scipy.linalg
+        ev, evect = scipy.linalg.eig(H[:j + 1, :j + 1])
+        k = int(np.abs(ev).argmax())
+        ev_max = abs(ev[k])
+        err = H[j + 1, j] * evect[-1, k]
+        v0 = np.hstack(V[:j + 1]) @ evect[:, k].reshape(-1, 1)
+        v0 = np.real(v0)
+        if abs(err) / abs(ev[k]) < tol or flag:
+            break
+    return float(ev_max)
+
+
+def _incomplete_mat_mult(T, mask):
+    """amg_core incomplete_mat_mult_csr(T, T.tocsc(), mask): S_ij = sum_k T_ik T_kj on mask's
+    pattern, ascending k — the order in which csr_matmat accumulates the same products, so the
+    product restricted to the mask (x * 1.0, zeros dropped = eliminate_zeros) is bitwise it."""
+    ones = mask.copy()
+    ones.data[:] = 1.0
+    S = (T @ T).multiply(ones).tocsr()
+    S.sort_indices()
+    return S
+
+
+def _row_reduce(M, fn, init):
+    out = np.full(M.shape[0], init)
+    nz = np.diff(M.indptr) > 0
+    if M.nnz:
+        red = fn.reduceat(M.data, M.indptr[:-1][nz])
+        out[nz] = red
+    return out
+
+
+def evolution_strength(A, rho=None, epsilon=4.0):
+    """pyamg evolution_strength_of_connection(A) (reference defaults). rho: rho(D^-1 A)
+    (None: approximate_spectral_radius, pyamg's estimate)."""
+    A = sp.csr_matrix(A, dtype=np.float64, copy=True)
+    D = A.diagonal()
+    Dinv = np.zeros_like(D)
+    mask = D != 0.0
+    Dinv[mask] = 1.0 / D[mask]
+    Dinv[D == 0] = 1.0
+    Dinv_A = A.copy()
+    Dinv_A.data = Dinv_A.data * np.repeat(Dinv, np.diff(Dinv_A.indptr))  # csr_scale_rows
+    A.eliminate_zeros()
+    A.sort_indices()
+    n = A.shape[0]
+    if rho is None:
+        rho = approximate_spectral_radius(Dinv_A)
+    Id = sp.eye(n, n, format="csr", dtype=A.dtype)
+    Atilde = (Id - (1.0 / rho) * Dinv_A)
+    Atilde = Atilde.T.tocsr()
+    Atilde.sort_indices()
+    S = _incomplete_mat_mult(Atilde, A)           # k = 2: one incomplete product
+    S.eliminate_zeros()
+    # B = ones shortcut
+    DA = S.diagonal()
+    rows = np.repeat(np.arange(n), np.diff(S.indptr))
+    data = S.data.copy()
+    zt = DA[rows] * 1.0                           # scale_rows(ones, DA / 1) then columns by 1
+    angle = (zt * data + 0.0 * 0.0) < 0.0
+    ratio = zt / data
+    weak = np.abs(ratio) < 1e-4
+    v = np.abs(1.0 - ratio)
+    v[weak] = 0.0
+    v[angle] = 0.0
+    S.data = v
+    S.eliminate_zeros()
+    S.data[S.data < np.sqrt(np.finfo(float).eps)] = 1e-4
+    # amg_core apply_distance_filter
+    rows = np.repeat(np.arange(n), np.diff(S.indptr))
+    off = S.indices != rows
+    offv = np.where(off, S.data, np.finfo(float).max)
+    Sm = S.copy()
+    Sm.data = offv
+    mn = _row_reduce(Sm, np.minimum, np.finfo(float).max)
+    thr = epsilon * mn
+    newv = S.data.copy()
+    newv[~off] = 1.0
+    newv[off & (S.data >= thr[rows])] = 0.0
+    S.data = newv
+    S.eliminate_zeros()
+    # symmetrize, unit diagonal, invert, scale rows by the largest entry
+    S = 0.5 * (S + S.T)
+    Id = sp.eye(n, n, format="csr")
+    Id.data -= S.diagonal()
+    S = S + Id
+    S.data = 1.0 / S.data
+    mx = _row_reduce(abs(S).tocsr(), np.maximum, 0.0)   # amg_core maximum_row_value
+    mx[mx != 0] = 1.0 / mx[mx != 0]
+    S = sp.csr_matrix(S)
+    S.data = S.data * np.repeat(mx, np.diff(S.indptr))  # scale_rows
+    return S
+
+
+def strength_measure(A, name, rho=None):
+    """utils/common.py:25-31 strength_measure_funcs[name](A)."""
+    if name == "abs":
+        return abs(A)
+    if name == "invabs":
+        return sp.csr_matrix((1.0 / np.abs(A.data), A.indices, A.indptr), A.shape)
+    if name == "unit":
+        return sp.csr_matrix((np.ones_like(A.data), A.indices, A.indptr), A.shape)
+    ev = evolution_strength(A, rho=rho)
+    if name == "evolution":
+        return ev + sp.csr_matrix((np.ones_like(A.data), A.indices, A.indptr), A.shape) * 0.1
+    if name == "olson":
+        return ev + sp.csr_matrix((1. / np.abs(A.data), A.indices, A.indptr), A.shape)
+    raise KeyError(name)

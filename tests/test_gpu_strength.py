@@ -1,0 +1,102 @@
+"""GPU: the evolution strength of connection on the device (csrc/strength.hip,
+mlamg.strength) against the oracle's restatement of pyamg at the same rho: bitwise (indices and
+values) for the plain measure and the reference's 'evolution' and 'olson' (utils/common.py:27,30).
+The device's own rho (Lanczos lambda_max of D^-1 A) agrees with the exact spectral radius to
+1e-10; pyamg's Arnoldi estimate is within its 1e-2 tolerance of both (parity unpinned)."""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch
+
+
+def _matrix(name):
+    from mlamg import mesh, problems
+    if name == "poisson2d":
+        return problems.poisson_2d_5pt(40)
+    if name == "lap3d_grid":  # the reference's own demos/laplace_3d.grid
+        g = np.load(os.path.join(HERE, "golden", "laplace_3d_grid.npz"))
+        A = sp.csr_matrix((g["data"], g["indices"], g["indptr"]))
+        A.sort_indices()
+        return A
+    if name == "c3_mesh":
+        return mesh.poisson_dirichlet(mesh.load_npz(os.path.join(HERE, "golden",
+                                                                 "cylflow_highres_mesh.npz")))[0]
+    if name == "jump2d":
+        jumps = problems.voronoi_jumps(np.random.RandomState(0))
+        return problems.jump_2d(48, jumps)
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("name", ("poisson2d", "lap3d_grid", "c3_mesh", "jump2d"))
+@pytest.mark.parametrize("mode", ("plain", "evolution", "olson"))
+def test_evolution_bitwise_vs_oracle(oracle, torch_cuda, name, mode):
+    from mlamg import strength
+    A = _matrix(name).tocsr()
+    A.sort_indices()
+    rho = 1.9 if name == "poisson2d" else 1.95  # any rho: both sides take the same one
+    if mode == "plain":
+        got = strength.evolution_strength_of_connection(A, rho=rho)
+        ref = oracle.evolution_strength(A, rho=rho)
+    else:
+        got = (strength.evolution if mode == "evolution" else strength.olson)(A, rho=rho)
+        ref = oracle.strength_measure(A, mode, rho=rho)
+    ref = sp.csr_matrix(ref)
+    ref.sort_indices()
+    assert got.shape == ref.shape and got.nnz == ref.nnz, (got.nnz, ref.nnz)
+    assert np.array_equal(got.indptr, ref.indptr) and np.array_equal(got.indices, ref.indices)
+    assert np.array_equal(got.data, ref.data), np.abs(got.data - ref.data).max()
+
+
+def test_device_rho_and_default_path(oracle, torch_cuda):
+    """The mirror's default rho (device Lanczos) vs the exact spectral radius, pyamg's Arnoldi
+    estimate within its tolerance, and the default-path measure feeding lloyd_aggregation like
+    utils/common.py:53-56."""
+    from mlamg import graph, strength
+    from mlamg.sparse import DeviceCSR
+    A = _matrix("jump2d")
+    Dinv_A = sp.diags(1.0 / A.diagonal()) @ A
+    lam = np.abs(np.linalg.eigvals(Dinv_A.toarray())).max()
+    rho = strength.spectral_radius_dinv_a(DeviceCSR.from_scipy(A))
+    assert abs(rho - lam) <= 1e-10 * lam
+    np.random.seed(0)
+    rho_pyamg = oracle.approximate_spectral_radius(Dinv_A.tocsr())
+    assert abs(rho_pyamg - lam) <= 1e-2 * lam
+    C = strength.strength_measure_funcs["olson"](A)
+    ref = oracle.strength_measure(A, "olson", rho=rho)
+    assert np.array_equal(C.indices, ref.indices) and np.array_equal(C.data, ref.data)
+    AggOp, roots, seeds = graph.lloyd_aggregation(C, ratio=0.1, distance="same", rand=0)
+    assert AggOp.shape == (A.shape[0], int(np.ceil(0.1 * A.shape[0])))
+
+
+@pytest.mark.parametrize("mode", ("olson", "evolution"))
+def test_hierarchy_with_evolution_measure(oracle, torch_cuda, mode):
+    """Hierarchy.build(strength_mode='olson' | 'evolution') — the reference's default measure —
+    level by level bitwise against the oracle's build with the same per-level rho (the device
+    Lanczos value, also the level's SA lambda_max)."""
+    from mlamg import hierarchy
+    A = _matrix("c3_mesh")
+    H = hierarchy.Hierarchy.build(A, alpha=0.1, strength_mode=mode, max_coarse=500)
+    assert H.n_levels >= 2
+    levels, Ac = oracle.build_hierarchy(A, alpha=0.1, strength_mode=mode, max_coarse=500,
+                                        omegas=[L.omega for L in H.levels],
+                                        rhos=[abs(L.lam) for L in H.levels])
+    assert len(levels) == len(H.levels)
+    for Lo, Ld in zip(levels, H.levels):
+        assert np.array_equal(Ld.seeds, Lo["seeds"])
+        for key, M in (("P", Ld.P), ("A", Ld.A)):
+            Md = M.to_scipy()
+            assert np.array_equal(Md.indptr, Lo[key].indptr), key
+            assert np.array_equal(Md.indices, Lo[key].indices), key
+            assert np.array_equal(Md.data, Lo[key].data), key
