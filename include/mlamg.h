@@ -200,6 +200,41 @@ int mlamg_strength(const mlamg_csr* A, int mode, mlamg_csr** out, void* stream);
 int mlamg_evolution_strength(const mlamg_csr* A, double rho, double epsilon, int mode,
                              mlamg_csr** out, void* stream);
 
+/* GNN inference layers of ns/model/agg_interp.py FullAggNet.forward (:432-486), fp32, device
+ * pointers (csrc/gnn.hip). Graph = the CSR pattern of A (ns/model/data.py:22-46): edge e = stored
+ * entry (src i, tgt j); tptr[n+1]/teid[E] list each target's incoming edges, ascending source.
+ * Dense weights in torch Linear layout [out, in]; act 0 none, 1 relu; R (nullable) is added
+ * after the activation, rc = its columns (1: broadcast). */
+int mlamg_gnn_linear(const float* X, int64_t M, int K, const float* W, const float* b, int N,
+                     int act, float beta, const float* R, int rc, float* Y, void* stream);
+/* gcn_norm without self loops (TAGConv normalize=True): wn_e = deg^-1/2[src] w_e deg^-1/2[tgt] */
+int mlamg_gnn_gcn_norm(const int32_t* tptr, const int32_t* teid, const int32_t* src,
+                       const int32_t* tgt, const float* w, int64_t n, int64_t E, float* dis_tmp,
+                       float* wn, void* stream);
+/* Y[i] = sum over incoming edges of w_e X[src_e] (TAGConv propagate, aggr 'add'), F <= 64 */
+int mlamg_gnn_propagate(const int32_t* tptr, const int32_t* teid, const int32_t* src,
+                        const float* w, const float* X, int64_t n, int F, float* Y, void* stream);
+/* torch_geometric InstanceNorm (affine False, no running stats): per channel over the nodes */
+int mlamg_gnn_instance_norm(const float* X, int64_t n, int F, float eps, float* Y, void* stream);
+/* NNConv(Fin, Fout, nn = Linear(fe,4)-ReLU-Linear(4,16)-ReLU-Linear(16,Fin*Fout)-ReLU), aggr
+ * 'add', root weight `root` = X W_root^T (precomputed), bias; msg_tmp[E*Fout] scratch */
+int mlamg_gnn_nnconv(const int32_t* tptr, const int32_t* teid, const int32_t* src,
+                     const float* ea, int64_t E, int fe, const float* L1, const float* c1,
+                     const float* L2, const float* c2, const float* L3, const float* c3,
+                     const float* X, int64_t n, int Fin, int Fout, const float* root,
+                     const float* bias, int act, const float* R, int rc, float* msg_tmp,
+                     float* Y, void* stream);
+/* smallEdgeModel: Linear(2F+fe, H)-ReLU-LayerNorm(H)-Linear(H, C) on [x_src | x_tgt | ea] */
+int mlamg_gnn_edge_mlp(const int32_t* src, const int32_t* tgt, const float* X, int F,
+                       const float* ea, int fe, int64_t E, const float* W1, const float* b1,
+                       int H, const float* g, const float* beta, const float* W2,
+                       const float* b2, int C, int act, const float* R, int rc, float* out,
+                       void* stream);
+/* topk_vec (agg_interp.py:14-22): vec[n] = 1 at the k largest scores (ties: smaller index
+ * first), idx[k] (nullable) = those nodes in that order. Syncs. */
+int mlamg_gnn_topk(const float* scores, int64_t n, int64_t k, float* vec, int32_t* idx,
+                   void* stream);
+
 /* Seeded Bellman-Ford (ns/lib/graph.py:7-53) on edge weights G (row i -> col j, weight g_ij,
  * evaluated in fp32 like the torch reference). dist_f32[n], cluster[n] (node id of the nearest
  * seed, -1 if unreachable). Ties broken deterministically by the smallest seed node id.

@@ -10,6 +10,7 @@ Mirrors the reference modules on the hot path:
   mlamg.strength        <- utils/common.py:25-31 (strength_measure_funcs; pyamg's evolution
                                                   strength of connection on the device)
   mlamg.preconditioner  <- ns/preconditioner     (MLAMG PC: initialize/update/apply)
+  mlamg.gnn             <- ns/model/agg_interp.py (FullAggNet inference: AggNet, MPNN)
   mlamg.hierarchy       multilevel device hierarchy + V-cycle executor (precondition/solve)
   mlamg.distributed     fine level row-partitioned over GPUs (RCCL halo exchange)
 
@@ -21,8 +22,8 @@ import importlib
 
 __version__ = "0.1.0"
 
-_SUBMODULES = ("multigrid", "graph", "sparse", "strength", "hierarchy", "preconditioner",
-               "problems", "gridio", "distributed", "_lib")
+_SUBMODULES = ("multigrid", "graph", "sparse", "strength", "gnn", "hierarchy",
+               "preconditioner", "problems", "gridio", "distributed", "_lib")
 
 
 def __getattr__(name):

@@ -97,6 +97,19 @@ SIGNATURES = {
     "mlamg_lambda_max_dinvA": (c_int, [c_vp, c_int, c_dbl, c_u64, P_dbl, P_int, c_vp]),
     "mlamg_strength": (c_int, [c_vp, c_int, c_vpp, c_vp]),
     "mlamg_evolution_strength": (c_int, [c_vp, c_dbl, c_dbl, c_int, c_vpp, c_vp]),
+    "mlamg_gnn_linear": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_int, c_int, ctypes.c_float,
+                                 c_vp, c_int, c_vp, c_vp]),
+    "mlamg_gnn_gcn_norm": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
+                                   c_vp]),
+    "mlamg_gnn_propagate": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp]),
+    "mlamg_gnn_instance_norm": (c_int, [c_vp, c_i64, c_int, ctypes.c_float, c_vp, c_vp]),
+    "mlamg_gnn_nnconv": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp,
+                                 c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_int,
+                                 c_vp, c_int, c_vp, c_vp, c_vp]),
+    "mlamg_gnn_edge_mlp": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_i64, c_vp, c_vp,
+                                   c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_int,
+                                   c_vp, c_vp]),
+    "mlamg_gnn_topk": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "mlamg_bellman_ford": (c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, P_i32, c_vp]),
     "mlamg_aggregate_op": (c_int, [c_vp, c_i64, c_i64, c_vpp, c_vp]),
     "mlamg_labels_to_columns": (c_int, [c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
