@@ -64,6 +64,9 @@ int mlamg_csr_shape(const mlamg_csr* A, int64_t* n_rows, int64_t* n_cols, int64_
 int mlamg_csr_device_arrays(const mlamg_csr* A, int32_t** indptr, int32_t** indices,
                             double** data);
 /* copy the arrays back to host buffers (indptr n_rows+1, indices/data nnz); syncs */
+/* copies of the CSR arrays into caller DEVICE buffers (any may be NULL), async on `stream` */
+int mlamg_csr_copy_device(const mlamg_csr* A, int32_t* indptr, int32_t* indices, double* data,
+                          void* stream);
 int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indices_host,
                        double* data_host);
 

@@ -265,6 +265,22 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
   return MLAMG_OK;
 }
 
+int mlamg_csr_copy_device(const mlamg_csr* A, int32_t* indptr, int32_t* indices, double* data,
+                          void* stream) {
+  MLAMG_REQUIRE(A, "A is NULL");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (indptr)
+    MLAMG_HIP(hipMemcpyAsync(indptr, A->indptr, sizeof(int32_t) * (A->n_rows + 1),
+                             hipMemcpyDeviceToDevice, s));
+  if (indices && A->nnz)
+    MLAMG_HIP(hipMemcpyAsync(indices, A->indices, sizeof(int32_t) * A->nnz,
+                             hipMemcpyDeviceToDevice, s));
+  if (data && A->nnz)
+    MLAMG_HIP(hipMemcpyAsync(data, A->data, sizeof(double) * A->nnz, hipMemcpyDeviceToDevice,
+                             s));
+  return MLAMG_OK;
+}
+
 }  // extern "C"
 
 namespace mlamg {

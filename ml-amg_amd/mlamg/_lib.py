@@ -72,6 +72,7 @@ SIGNATURES = {
     "mlamg_csr_shape": (c_int, [c_vp, P_i64, P_i64, P_i64]),
     "mlamg_csr_device_arrays": (c_int, [c_vp, c_vpp, c_vpp, c_vpp]),
     "mlamg_csr_download": (c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_csr_copy_device": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mlamg_csr_set_format": (c_int, [c_vp, c_int, c_int, c_vp]),
     "mlamg_csr_get_format": (c_int, [c_vp, P_int, P_int, P_i64]),
     "mlamg_csr_format_bytes": (c_int, [c_vp, P_dbl]),

@@ -49,6 +49,7 @@ class Graph:
         tptr = np.zeros(n + 1, dtype=np.int32)
         np.cumsum(np.bincount(tgt, minlength=n), out=tptr[1:])
         self.n, self.E, self.fe = n, int(len(src)), ea.shape[1]
+        self.crow = torch.as_tensor(A.indptr.astype(np.int32), device=dev)
         self.src = torch.as_tensor(src, device=dev)
         self.tgt = torch.as_tensor(tgt, device=dev)
         self.tptr = torch.as_tensor(tptr, device=dev)
@@ -57,6 +58,25 @@ class Graph:
         self.x = torch.full((n, 1), 1.0 / n, dtype=torch.float32, device=dev)
         self.edge_index = torch.stack([self.src.long(), self.tgt.long()])
         self._gcn = None
+
+    def with_clusters(self, col):
+        """graph_from_matrix(A, Agg) from this graph and the device aggregate column of every
+        node (-1: none; agg_op.argmax(axis=1) of an empty row is 0): edge feature 2 =
+        cluster_adj = 0 if both ends are in the same aggregate, else 1. Shares the structure."""
+        g = object.__new__(Graph)
+        g.__dict__.update(self.__dict__)
+        c = torch.where(col < 0, torch.zeros_like(col), col)
+        adj = (c[self.src.long()] != c[self.tgt.long()]).to(torch.float32)
+        g.edge_attr = torch.stack([self.edge_attr[:, 0], adj], dim=1).contiguous()
+        g.fe = 2
+        g._gcn = None
+        return g
+
+    def csr(self, values):
+        """A DeviceCSR on this graph's pattern with the given per-edge values (fp64 copy)."""
+        from .sparse import DeviceCSR
+        return DeviceCSR.from_torch(self.crow, self.tgt, values.reshape(-1).double().contiguous(),
+                                    (self.n, self.n))
 
     def gcn_weights(self):
         """gcn_norm(edge_index, edge_attr[:, 0]) without self loops (TAGConv normalize=True)."""
@@ -303,37 +323,30 @@ class FullAggNet(nn.Module):
         """Returns (agg, P, bf_weights, cluster_centers, node_weights) like :442-486: agg and P
         as torch sparse COO (n x k, fp32), bf_weights as torch sparse COO (the CNet edge
         values), cluster_centers the seed nodes (ascending), node_weights the 0/1 scores."""
-        from .graph import bellman_ford_device, labels_to_columns
-        from .sparse import DeviceCSR
+        from .graph import aggregate_op_device, bellman_ford_device, labels_to_columns
         A = sp.csr_matrix(A)
         m = A.shape[0]
         k = int(np.ceil(alpha * m))
         g = Graph(A, device=self.device)
         node_scores = self.AggNet.run(g, k).reshape(-1)
         top_k = torch.nonzero(node_scores == 1).reshape(-1)
+        # Bellman-Ford over the CNet edge weights from the seeds (pyamg.graph.bellman_ford,
+        # :466-473), all on the device
         _, bf_edges = self.CNet.run(g)
-        w = bf_edges.reshape(-1)
-        # Bellman-Ford over the CNet weights from the seeds (pyamg.graph.bellman_ford, :470-473)
-        C = sp.csr_matrix((w.double().cpu().numpy(), A.indices, A.indptr), shape=A.shape)
+        C = g.csr(bf_edges)
         seeds = top_k.to(torch.int32)
-        _, lab, _ = bellman_ford_device(DeviceCSR.from_scipy(C), seeds)
+        _, lab, _ = bellman_ford_device(C, seeds)
         col = labels_to_columns(lab, seeds)
-        colh = col.cpu().numpy()
-        rows = np.nonzero(colh >= 0)[0]
-        Agg = sp.csr_matrix((np.ones(len(rows), dtype=np.float32), (rows, colh[rows])),
-                            shape=(m, k))
-        # P_hat from PNet on graph_from_matrix(A, Agg), P = P_hat Agg (:478-484)
-        gp = Graph(A, agg=Agg, device=self.device)
-        _, p_edges = self.PNet.run(gp)
-        P_hat = sp.csr_matrix((p_edges.reshape(-1).double().cpu().numpy(), A.indices, A.indptr),
-                              shape=A.shape)
-        Pd = DeviceCSR.from_scipy(P_hat) @ DeviceCSR.from_scipy(Agg.astype(np.float64))
-        P = Pd.to_scipy().astype(np.float32)
-        dev = self.device
+        Agg = aggregate_op_device(col, k)
+        # P_hat from PNet on graph_from_matrix(A, Agg), P = P_hat Agg (:476-484)
+        _, p_edges = self.PNet.run(g.with_clusters(col))
+        P = g.csr(p_edges) @ Agg
 
-        def to_t(M):
-            M = M.tocoo()
-            idx = np.vstack([M.row, M.col]).astype(np.int64)
-            return torch.sparse_coo_tensor(idx, M.data, M.shape, device=dev).coalesce()
+        def to_t(M, dtype=torch.float32):
+            crow, cj, v = M.to_torch()
+            rows = torch.repeat_interleave(torch.arange(M.shape[0], device=crow.device),
+                                           (crow[1:] - crow[:-1]).long())
+            return torch.sparse_coo_tensor(torch.stack([rows, cj.long()]), v.to(dtype),
+                                           M.shape).coalesce()
 
-        return to_t(Agg), to_t(P), to_t(C.astype(np.float32)), top_k, node_scores
+        return to_t(Agg), to_t(P), to_t(C), top_k, node_scores

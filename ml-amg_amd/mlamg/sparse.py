@@ -110,6 +110,16 @@ class DeviceCSR:
         return cls(handle)
 
     # ------------------------------------------------------------------ export
+    def to_torch(self):
+        """Device copies (crow int32, col int32, val float64) as torch tensors."""
+        n = self.shape[0]
+        dev = _device()
+        crow = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        col = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=dev)
+        val = torch.empty(max(self.nnz, 1), dtype=torch.float64, device=dev)
+        call("mlamg_csr_copy_device", self.handle, ptr(crow), ptr(col), ptr(val), stream_ptr())
+        return crow, col[:self.nnz], val[:self.nnz]
+
     def to_scipy(self):
         n, m = self.shape
         indptr = np.empty(n + 1, dtype=np.int32)
