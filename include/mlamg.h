@@ -274,6 +274,9 @@ int mlamg_gs_sweep(const mlamg_gs* G, double* x, const double* b, int iterations
  * dense GEMV. Returns MLAMG_EINVAL if the matrix is numerically singular. */
 int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream);
 int mlamg_dense_destroy(mlamg_dense* D);
+/* which inverse was built: 1 = inverse Cholesky factor (symmetric positive definite), 0 =
+ * Gauss-Jordan with partial pivoting (any other nonsingular operator) */
+int mlamg_dense_info(const mlamg_dense* D, int* method, int64_t* n);
 int mlamg_dense_solve(const mlamg_dense* D, const double* b, double* x, void* stream);
 
 /* Least squares by LSQR: x = argmin ||A x - b||_2 from x0 = 0, scipy.sparse.linalg.lsqr

@@ -147,6 +147,7 @@ struct mlamg_csr {
 struct mlamg_dense {
   int64_t n = 0;
   double* inv = nullptr;  // row-major n x n
+  int method = 0;         // 0 Gauss-Jordan, 1 inverse Cholesky factor (dense.hip)
 };
 
 namespace mlamg {

@@ -1,11 +1,22 @@
 // Coarsest-level direct solve. Replaces spla.factorized / splu (ns/lib/multigrid.py:168,
 // ns/preconditioner/MLAMG.py:122): the coarse operator (n_c up to a few thousand) is expanded
-// to a dense row-major matrix and inverted in place by Gauss-Jordan elimination with partial
-// pivoting (fp64) once at setup; each V-cycle's coarse solve is then one dense GEMV
-// (n_c^2 * 8 bytes, HBM/L2-bound) instead of two sequential triangular solves.
+// to a dense row-major matrix and inverted once at setup; each V-cycle's coarse solve is then one
+// dense GEMV (n_c^2 * 8 bytes, HBM/L2-bound) instead of two sequential triangular solves.
+//
+// Inverse: a symmetric operator (every Galerkin P^T A P of the reference's SPD A) is inverted
+// through its inverse Cholesky factor X = L^-1, built in place by right-looking blocked
+// elimination of [A | I] (lower triangle) over the whole GPU — per 32-column panel one panel launch (every
+// workgroup factorises the 32 x 32 diagonal block in LDS and solves its share of the rows below
+// (L21 = A21 L11^-T) and of the panel's rows of X (Z = L11^-1 [X_top | I])) and one trailing
+// launch (16 x 16 tiles on the fp64 matrix cores, v_mfma_f64_16x16x4_f64) — then A^-1 = X^T X
+// (an MFMA tile per 16 x 16 block): n^3/3 + n^3/3 multiply-adds in 2 n/32 + 1 launches. A
+// non-positive pivot (not SPD in floating point) or an unsymmetric operator takes Gauss-Jordan
+// elimination with partial pivoting (one pivot launch + one elimination launch per column),
+// which also reports an exactly singular operator like spla.factorized fails.
 #include "common.hpp"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace mlamg {
 
@@ -125,6 +136,257 @@ __global__ __launch_bounds__(256) void k_gemv(const double* __restrict__ M, int6
   if (lane == 0) x[row] = s;
 }
 
+// ------------------------------------------------------------ inverse Cholesky factor
+constexpr int kNB = 32;
+typedef double d4v __attribute__((ext_vector_type(4)));
+
+// wave 0 of a workgroup: the diagonal block of panel k0 (lower part of M) into Dg (ld kNB + 1),
+// factorised L11 (right-looking, wave-synchronous), and 1/diag(L11) into rd. Returns false on a
+// non-positive pivot (same in every lane).
+__device__ bool panel_factor(const double* __restrict__ M, int64_t n, int64_t k0, int bw,
+                             double* Dg, double* rd) {
+  constexpr int ds = kNB + 1, E = kNB * kNB / 64;
+  const int lane = threadIdx.x & 63;
+  for (int q = lane; q < kNB * kNB; q += 64) {
+    const int rr = q / kNB, cc = q % kNB;
+    Dg[rr * ds + cc] = (rr < bw && cc <= rr) ? M[(k0 + rr) * n + k0 + cc] : 0.0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  for (int t = 0; t < bw; ++t) {
+    const double dtt = Dg[t * ds + t];
+    if (!(dtt > 0.0)) return false;
+    const double sq = sqrt(dtt);
+    double nv[E];
+    bool wr[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int q = lane + 64 * e, rr = q / kNB, cc = q % kNB;
+      wr[e] = rr < bw && cc <= rr && cc >= t;
+      nv[e] = 0.0;
+      if (wr[e]) {
+        if (cc == t)
+          nv[e] = rr == t ? sq : Dg[rr * ds + t] / sq;
+        else
+          nv[e] = Dg[rr * ds + cc] - (Dg[rr * ds + t] / sq) * (Dg[cc * ds + t] / sq);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int q = lane + 64 * e;
+      if (wr[e]) Dg[(q / kNB) * ds + q % kNB] = nv[e];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  if (lane < bw) rd[lane] = 1.0 / Dg[lane * ds + lane];
+  return true;
+}
+
+// Panel k0: block b of the grid takes rows below the panel (L21 = A21 L11^-T into Lp, row-major
+// (n - k1) x kNB) and columns < k1 of the panel's rows (Z = L11^-1 [X_top | I], written into M's
+// rows k0..k1-1: the final rows of X), a row / column per thread with its values in registers.
+__global__ __launch_bounds__(256) void k_chol_panel(double* __restrict__ M, int64_t n, int64_t k0,
+                                                    double* __restrict__ Lp,
+                                                    double* __restrict__ Zd,
+                                                    int32_t* __restrict__ fail) {
+  __shared__ double Dg[kNB * (kNB + 1)];
+  __shared__ double rd[kNB];
+  __shared__ int ok_s;
+  if (*fail) return;
+  const int bw = (int)min<int64_t>(kNB, n - k0);
+  const int64_t k1 = k0 + bw;
+  if (threadIdx.x < 64) {
+    const bool ok = panel_factor(M, n, k0, bw, Dg, rd);
+    if (threadIdx.x == 0) ok_s = ok ? 1 : 0;
+  }
+  __syncthreads();
+  if (!ok_s) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *fail = 1;
+    return;
+  }
+  constexpr int ds = kNB + 1;
+  const int64_t nrows = n - k1;  // rows below: bw == kNB whenever there are any
+  const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (item < nrows) {
+    const int64_t i = k1 + item;
+    double a[kNB];
+#pragma unroll
+    for (int t = 0; t < kNB; ++t) a[t] = M[i * n + k0 + t];
+#pragma unroll
+    for (int t = 0; t < kNB; ++t) {
+      double l = a[t];
+#pragma unroll
+      for (int q = 0; q < t; ++q) l = fma(-a[q], Dg[t * ds + q], l);
+      a[t] = l * rd[t];
+      Lp[item * kNB + t] = a[t];
+    }
+  } else if (item < nrows + k1) {
+    const int64_t j = item - nrows;  // a column of [X_top | I]
+    double z[kNB];
+#pragma unroll
+    for (int t = 0; t < kNB; ++t)
+      z[t] = t >= bw ? 0.0 : (j < k0 ? M[(k0 + t) * n + j] : (j - k0 == t ? 1.0 : 0.0));
+#pragma unroll
+    for (int t = 0; t < kNB; ++t) {
+      if (t < bw) {
+        double v = z[t];
+#pragma unroll
+        for (int q = 0; q < t; ++q) v = fma(-Dg[t * ds + q], z[q], v);
+        z[t] = v * rd[t];
+        // the diagonal block's columns (L11^-1) go to Zd: other workgroups of this launch are
+        // still reading the block from M; the update launch copies them in
+        if (j < k0)
+          M[(k0 + t) * n + j] = z[t];
+        else
+          Zd[t * kNB + (j - k0)] = z[t];
+      }
+    }
+  }
+}
+
+// Trailing update of panel k0, a wave per 16 x 16 tile of rows [k1, n) x columns [0, i]:
+//   M[i, j] <- (j in [k0, k1) ? 0 : M[i, j]) - sum_t L21[i][t] W[t][j],
+//   W = the panel's rows of X (j < k1) or L21^T (j >= k1).
+__global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ M, int64_t n,
+                                                     int64_t k0, const double* __restrict__ Lp,
+                                                     const double* __restrict__ Zd,
+                                                     const int32_t* __restrict__ fail) {
+  if (*fail) return;
+  const int64_t k1 = min<int64_t>(k0 + kNB, n);
+  if (blockIdx.x == 0)  // L11^-1 into M's diagonal block (no tile of this launch reads it there)
+    for (int q = threadIdx.x; q < kNB * kNB; q += 256) {
+      const int t = q / kNB, c = q % kNB;
+      if (k0 + t < n && c <= t) M[(k0 + t) * n + k0 + c] = Zd[q];
+    }
+  if (k1 >= n) return;
+  const int64_t a16 = (k1 + 15) / 16, nrb = (n - k1 + 15) / 16;
+  auto C = [&](int64_t rb) { return rb * (a16 + 1) + rb * (rb - 1) / 2; };
+  const int64_t T = C(nrb);
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= T) return;
+  const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
+  const double bq = (double)a16 + 0.5;
+  int64_t rb = (int64_t)(-bq + sqrt(bq * bq + 2.0 * (double)q));
+  while (rb > 0 && C(rb) > q) --rb;
+  while (C(rb + 1) <= q) ++rb;
+  const int64_t i0 = k1 + 16 * rb, j0 = 16 * (q - C(rb));
+  const int64_t last = n - k1 - 1;
+  const int64_t jc = j0 + lr;
+  const bool zero = jc >= k0 && jc < k1;
+  d4v acc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t i = i0 + lk + 4 * r;
+    acc[r] = (!zero && i < n && jc < n) ? M[i * n + jc] : 0.0;
+  }
+  const double* arow = Lp + min(i0 + lr - k1, last) * kNB;
+  const bool from_x = jc < k1;
+  const double* brow = Lp + min(max(jc - k1, (int64_t)0), last) * kNB;
+  const int64_t jz = min(jc, k1 - 1);
+#pragma unroll
+  for (int kk = 0; kk < kNB; kk += 4) {
+    const int k = kk + lk;
+    const double av = -arow[k];
+    const double bv = from_x ? (jz >= k0 ? Zd[k * kNB + (jz - k0)] : M[(k0 + k) * n + jz])
+                             : brow[k];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t i = i0 + lk + 4 * r;
+    if (i < n && jc < n) M[i * n + jc] = acc[r];
+  }
+}
+
+// A^-1 = X^T X from X = L^-1 (lower triangle of X; its upper triangle is not read): a wave per
+// 16 x 16 tile, C_ij = sum over k >= max(i, j) of X_ki X_kj.
+__global__ __launch_bounds__(256) void k_xtx(const double* __restrict__ X, int64_t n,
+                                             double* __restrict__ Cm) {
+  const int64_t nb = (n + 15) / 16;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nb * nb) return;
+  const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
+  const int64_t i0 = 16 * (q / nb), j0 = 16 * (q % nb);
+  const int64_t ia = i0 + lr, jb = j0 + lr;  // this lane's A row (i) and B column (j)
+  d4v acc = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t kb = (max(i0, j0) / 4) * 4; kb < n; kb += 4) {
+    const int64_t k = kb + lk;
+    const double av = (k < n && ia < n && k >= ia) ? X[k * n + ia] : 0.0;
+    const double bv = (k < n && jb < n && k >= jb) ? X[k * n + jb] : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t i = i0 + lk + 4 * r;
+    if (i < n && jb < n) Cm[i * n + jb] = acc[r];
+  }
+}
+
+// A symmetric up to rounding, checked on the device: |a_ij - a_ji| <= 1e-12 max(|a_ii|, |a_jj|)
+// (a Galerkin P^T A P of a symmetric A is symmetric up to its SpGEMM's summation order; a
+// genuinely unsymmetric operator differs by far more). bad[0] counts violations.
+__global__ void k_asym(const double* __restrict__ M, int64_t n, int32_t* __restrict__ bad) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= n * n) return;
+  const int64_t i = q / n, j = q - i * n;
+  if (j >= i) return;
+  const double d = fmax(fabs(M[i * n + i]), fabs(M[j * n + j]));
+  if (!(fabs(M[i * n + j] - M[j * n + i]) <= 1e-12 * d)) atomicAdd(bad, 1);
+}
+
+// the inverse Cholesky path; false when A is not SPD in floating point (inv untouched garbage)
+static int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t s) {
+  *spd = false;
+  double* Lp = nullptr;
+  int32_t* flag = nullptr;
+  if (hipMalloc(&Lp, sizeof(double) * (std::max<int64_t>(n, 1) + kNB) * kNB) != hipSuccess ||
+      hipMalloc(&flag, sizeof(int32_t) * 2) != hipSuccess) {
+    if (Lp) (void)hipFree(Lp);
+    set_error("dense_create: hipMalloc failed");
+    return MLAMG_ENOMEM;
+  }
+  (void)hipMemsetAsync(flag, 0, sizeof(int32_t) * 2, s);
+  hipLaunchKernelGGL(k_asym, dim3((unsigned)((n * n + 255) / 256)), dim3(256), 0, s, M, n,
+                     flag + 1);
+  int32_t h[2] = {0, 0};
+  hipError_t e = hipMemcpyAsync(h, flag, sizeof(h), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess && h[1] == 0) {
+    double* Zd = Lp + std::max<int64_t>(n, 1) * kNB;  // kNB x kNB
+    for (int64_t k0 = 0; k0 < n; k0 += kNB) {
+      const int64_t k1 = std::min<int64_t>(k0 + kNB, n);
+      const int64_t items = (n - k1) + k1;
+      hipLaunchKernelGGL(k_chol_panel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, M,
+                         n, k0, Lp, Zd, flag);
+      int64_t T = 0;
+      if (k1 < n) {
+        const int64_t a16 = (k1 + 15) / 16, nrb = (n - k1 + 15) / 16;
+        T = nrb * (a16 + 1) + nrb * (nrb - 1) / 2;
+      }
+      hipLaunchKernelGGL(k_chol_update, dim3((unsigned)std::max<int64_t>(1, (T + 3) / 4)),
+                         dim3(256), 0, s, M, n, k0, Lp, Zd, flag);
+    }
+    e = hipMemcpyAsync(h, flag, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess && h[0] == 0) {
+      const int64_t nb = (n + 15) / 16;
+      hipLaunchKernelGGL(k_xtx, dim3((unsigned)((nb * nb + 3) / 4)), dim3(256), 0, s, M, n, inv);
+      e = hipStreamSynchronize(s);
+      *spd = e == hipSuccess;
+    }
+  }
+  (void)hipFree(Lp);
+  (void)hipFree(flag);
+  if (e != hipSuccess) {
+    set_error(std::string("dense_create: ") + hipGetErrorString(e));
+    return MLAMG_EHIP;
+  }
+  return MLAMG_OK;
+}
+
 int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int32_t* done,
                      hipStream_t s) {
   if (D->n == 0) return MLAMG_OK;
@@ -165,6 +427,30 @@ int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream) {
     set_error("dense_create: hipMalloc failed");
     return MLAMG_ENOMEM;
   }
+  if (n >= 2 * kNB && !std::getenv("MLAMG_DENSE_GJ")) {
+    // inverse Cholesky factor in a scratch copy, the inverse into D->inv
+    double* M = nullptr;
+    if (hipMalloc(&M, sizeof(double) * n * n) == hipSuccess) {
+      (void)hipMemsetAsync(M, 0, sizeof(double) * n * n, s);
+      hipLaunchKernelGGL(k_densify, dim3((n + 255) / 256), dim3(256), 0, s, A->indptr,
+                         A->indices, A->data, n, M);
+      bool spd = false;
+      const int rc = dense_chol_inverse(M, n, D->inv, &spd, s);
+      (void)hipFree(M);
+      if (rc != MLAMG_OK) {
+        cleanup();
+        (void)hipFree(D->inv);
+        delete D;
+        return rc;
+      }
+      if (spd) {
+        cleanup();
+        D->method = 1;
+        *out = D;
+        return MLAMG_OK;
+      }
+    }
+  }
   (void)hipMemsetAsync(D->inv, 0, sizeof(double) * n * n, s);
   (void)hipMemsetAsync(fail, 0, sizeof(int32_t), s);
   if (n) hipLaunchKernelGGL(k_densify, dim3((n + 255) / 256), dim3(256), 0, s, A->indptr,
@@ -200,6 +486,13 @@ int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream) {
     return MLAMG_EHIP;
   }
   *out = D;
+  return MLAMG_OK;
+}
+
+int mlamg_dense_info(const mlamg_dense* D, int* method, int64_t* n) {
+  MLAMG_REQUIRE(D, "NULL argument");
+  if (method) *method = D->method;
+  if (n) *n = D->n;
   return MLAMG_OK;
 }
 

@@ -120,6 +120,7 @@ SIGNATURES = {
     "mlamg_gs_levels": (c_int, [c_vp, P_i32]),
     "mlamg_gs_sweep": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp]),
     "mlamg_dense_create": (c_int, [c_vp, c_vpp, c_vp]),
+    "mlamg_dense_info": (c_int, [c_vp, P_int, P_i64]),
     "mlamg_dense_destroy": (c_int, [c_vp]),
     "mlamg_dense_solve": (c_int, [c_vp, c_vp, c_vp, c_vp]),
     "mlamg_hier_create": (c_int, [c_vpp]),

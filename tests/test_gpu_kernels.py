@@ -285,6 +285,48 @@ def test_dense_coarse_solve(golden, ml, torch_cuda):
     assert np.allclose(host(x), ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("n", (64, 97, 300, 1025))
+def test_dense_inverse_cholesky(ml, torch_cuda, n):
+    """Symmetric positive definite coarse operators take the device-wide inverse Cholesky
+    factor (dense.hip: 32-column panels, MFMA trailing updates, A^-1 = X^T X); an unsymmetric
+    one takes Gauss-Jordan. Both against numpy's inverse at fp64 tolerance (sizes straddle the
+    panel and tile edges)."""
+    torch = torch_cuda
+    import ctypes
+    from mlamg._lib import call, ptr, stream_ptr
+    rs = np.random.RandomState(n)
+    B = sp.random(n, n, density=min(1.0, 12.0 / n), random_state=rs, format="csr")
+    S = (B + B.T).tocsr()
+    A = (S + sp.diags(np.asarray(abs(S).sum(axis=1)).ravel() + 1.0)).tocsr()  # SPD (diag. dom.)
+    for M, method in ((A, 1), ((A + sp.triu(B, 1) * 0.5).tocsr(), 0)):
+        Md = ml.sparse.DeviceCSR.from_scipy(M)
+        h = ctypes.c_void_p()
+        call("mlamg_dense_create", Md.handle, ctypes.byref(h), stream_ptr())
+        meth = ctypes.c_int()
+        call("mlamg_dense_info", h, ctypes.byref(meth), None)
+        assert meth.value == method
+        b = rs.randn(n)
+        x = torch.empty(n, dtype=torch.float64, device="cuda")
+        call("mlamg_dense_solve", h, ptr(dev(torch, b)), ptr(x), stream_ptr())
+        call("mlamg_dense_destroy", h)
+        ref = np.linalg.solve(M.toarray(), b)
+        assert np.allclose(host(x), ref, rtol=1e-11, atol=1e-12 * np.abs(ref).max())
+
+
+def test_two_level_large_coarse_histories(oracle, ml):
+    """Two-level amg_2_v at 96^2 (n_c = 1024, the hierarchy engine's dense coarse solve via
+    the inverse Cholesky factor) against the oracle's SuperLU-based histories."""
+    m = 96
+    A = ml.problems.poisson_2d_5pt(m)
+    P, _ = oracle.smoothed_aggregation_jacobi(A, ml.problems.box_aggregates_2d(m, m, 3),
+                                              omega=2.0 / 3.0)
+    x0 = np.random.RandomState(4).randn(A.shape[0])
+    b = np.zeros(A.shape[0])
+    xr, cr, er, ir = oracle.amg_2_v(A, P, b, x0, res_tol=1e-10)
+    x, c, e, it = ml.multigrid.amg_2_v(A, P, b, x0, res_tol=1e-10, engine="hierarchy")
+    assert it == ir and np.allclose(e, er, rtol=1e-10, atol=0) and abs(c - cr) <= 1e-8
+
+
 def test_dense_singular_reported(ml):
     import ctypes
     from mlamg._lib import MlamgError, call, stream_ptr

@@ -8,7 +8,7 @@ from mlamg.sparse import as_device, galerkin, to_device_vec
 from oracle import restated as orc
 torch.cuda.set_device(0)
 def T(): torch.cuda.synchronize(); return time.perf_counter()
-for m in (32, 96):
+for m in (96, 128):
     A = problems.poisson_2d_5pt(m); Agg = problems.box_aggregates_2d(m, m, 3)
     P, _ = orc.smoothed_aggregation_jacobi(A, Agg, omega=2.0/3.0)
     n = A.shape[0]; x0 = np.random.RandomState(0).randn(n); b = np.zeros(n)
