@@ -55,6 +55,7 @@ constexpr int kBMaxK = 32;          // off-diagonal entries per row of A
 constexpr int kBMaxKP = 32;         // entries per row of P
 constexpr int kBMaxKT = 256;        // entries per row of P^T
 constexpr int kBMaxPanel = 16;
+constexpr int kExtCoarseMin = 512;  // single calls above this n_c: device-wide coarse factor
 constexpr size_t kBLdsBytes = 156 * 1024;
 
 struct BDesc {
@@ -62,6 +63,8 @@ struct BDesc {
   int32_t K, KA, KP, KT, nlev, panel, n_chunks, cap, timing;
   int32_t spd;    // A symmetric: try the inverse Cholesky factor before Gauss-Jordan
   int32_t chol_nb;  // its panel width (4..16, from n_c)
+  int32_t setup_mode;  // 0: Galerkin + coarse inverse here; 1: Galerkin only (the inverse is
+                       // built by the device-wide factorisation, dense.hip)
   int32_t gs_rw;  // one-wave sweep (rows of K = 4 or 8 slots, levels <= 64 * gs_rw rows), 1 or 2
                   // rows per lane; 0: the workgroup sweeps each level
   double tol, omega;
@@ -541,6 +544,13 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
 
   dense_galerkin(D, arena, AH, tid);
   stamp(0);
+  if (D.setup_mode == 1) {
+    if (tid == 0) {
+      stat[1] = 0;
+      stat[2] = 0;
+    }
+    return;
+  }
 
   if (D.spd) {
     // the panel width is the problem's own (a function of n_c alone): a problem's roundings do
@@ -1447,6 +1457,10 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     D.stat_out = lay.take(16 + 8 * 8);
   }
   const size_t total = lay.off;
+  // a single problem with a large coarse operator takes the device-wide coarse factorisation
+  const bool ext_coarse = count == 1 && desc[0].nc > kExtCoarseMin && plans[0].spd &&
+                          !std::getenv("MLAMG_BATCH_NO_EXT");
+  if (ext_coarse) desc[0].setup_mode = 1;
   // ---- pack the inputs into pinned host memory, one copy in
   HostPinned& H = g_batch_host;
   const size_t host_need = std::max(in_bytes, total - out_begin);
@@ -1492,6 +1506,23 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   MLAMG_HIP(hipMemcpyAsync(arena, hb, in_bytes, hipMemcpyHostToDevice, s));
   const BDesc* dd = reinterpret_cast<const BDesc*>(arena + desc_off);
   hipLaunchKernelGGL(k_amg2v_setup, dim3((unsigned)count), dim3(kBT), lds_setup, s, dd, arena);
+  if (ext_coarse) {
+    // a single call with a large SPD coarse operator: the device-wide inverse Cholesky factor
+    // (all CUs) instead of one workgroup's; Gauss-Jordan in the setup kernel when not SPD
+    const BDesc& D = desc[0];
+    bool spd = false;
+    MLAMG_TRY(dense_chol_inverse(reinterpret_cast<double*>(arena + D.AH), D.nc,
+                                 reinterpret_cast<double*>(arena + D.AI), &spd, s));
+    if (!spd) {
+      BDesc& Dh = *reinterpret_cast<BDesc*>(hb + desc_off);
+      Dh.setup_mode = 0;
+      Dh.spd = 0;
+      MLAMG_HIP(hipMemcpyAsync(arena + desc_off, hb + desc_off, sizeof(BDesc),
+                               hipMemcpyHostToDevice, s));
+      MLAMG_HIP(hipStreamSynchronize(s));
+      hipLaunchKernelGGL(k_amg2v_setup, dim3(1), dim3(kBT), lds_setup, s, dd, arena);
+    }
+  }
   if (r_lds)
     hipLaunchKernelGGL(k_amg2v_cycles<true>, dim3((unsigned)count), dim3(kBT), lds_cycles, s,
                        dd, arena);

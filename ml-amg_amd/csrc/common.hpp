@@ -219,6 +219,9 @@ int jacobi_from_zero(double* x, const double* dinv, const double* b, int64_t n,
                      const int32_t* done, hipStream_t s);
 int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int32_t* done,
                      hipStream_t s);
+// A^-1 of a dense row-major n x n operator (destroyed) through its inverse Cholesky factor on the
+// whole GPU (dense.hip); *spd = false: not symmetric to rounding / not SPD, inv not written
+int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t s);
 int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
                       hipStream_t s);
 int32_t* hier_done_flag(mlamg_hier* H);

@@ -337,8 +337,9 @@ __global__ void k_asym(const double* __restrict__ M, int64_t n, int32_t* __restr
   if (!(fabs(M[i * n + j] - M[j * n + i]) <= 1e-12 * d)) atomicAdd(bad, 1);
 }
 
-// the inverse Cholesky path; false when A is not SPD in floating point (inv untouched garbage)
-static int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t s) {
+// the inverse Cholesky path; *spd false when A is not symmetric to rounding or not SPD in
+// floating point (M destroyed, inv untouched garbage)
+int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t s) {
   *spd = false;
   double* Lp = nullptr;
   int32_t* flag = nullptr;

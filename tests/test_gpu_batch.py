@@ -23,7 +23,10 @@ def _problems(ml, oracle, count):
 
 
 @pytest.mark.parametrize("smoother", ("gauss_seidel", "jacobi"))
-def test_batch_equals_sequential(oracle, smoother):
+def test_batch_equals_sequential(oracle, smoother, monkeypatch):
+    # single calls with n_c > 512 factor the coarse operator device-wide (own roundings, see
+    # test_fused_single_device_wide_coarse); here both sides take the one-workgroup factor
+    monkeypatch.setenv("MLAMG_BATCH_NO_EXT", "1")
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -114,9 +117,10 @@ def test_fused_matches_oracle_and_hierarchy(oracle, smoother, mode):
     assert np.allclose(ef[:10], er[:10], rtol=1e-10, atol=0)
 
 
-def test_fused_batch_mixed_sizes_bitwise_single(oracle):
+def test_fused_batch_mixed_sizes_bitwise_single(oracle, monkeypatch):
     """One launch over problems of different sizes equals one launch per problem, bit for bit
-    (each workgroup owns its problem)."""
+    (each workgroup owns its problem; single calls held to the one-workgroup coarse factor)."""
+    monkeypatch.setenv("MLAMG_BATCH_NO_EXT", "1")
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -196,9 +200,11 @@ def test_fused_zero_diagonal_rows(oracle):
     assert np.abs(xf - xr).max() <= 1e-9 * np.abs(xr).max()
 
 
-def test_fused_wide_coarse(oracle):
+def test_fused_wide_coarse(oracle, monkeypatch):
     """n_c = 2025 (> 1024 + panel: the column-per-thread update branch of the blocked
-    Gauss-Jordan) and n = 8100 with 2x2 aggregates, vs the oracle."""
+    Gauss-Jordan) and n = 8100 with 2x2 aggregates, vs the oracle. The one-workgroup coarse
+    setup is forced (a single call this size otherwise factors device-wide)."""
+    monkeypatch.setenv("MLAMG_BATCH_NO_EXT", "1")
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -215,3 +221,32 @@ def test_fused_wide_coarse(oracle):
     xf, cf, ef, itf = ml.multigrid.amg_2_v(A, P, np.zeros(A.shape[0]), x0, res_tol=1e-10,
                                            engine="fused")
     assert itf == ir and np.allclose(ef, er, rtol=1e-10, atol=0) and abs(cf - cr) <= 1e-8
+
+
+@pytest.mark.parametrize("m,agg", ((48, 2), (96, 3)))
+def test_fused_single_device_wide_coarse(oracle, monkeypatch, m, agg):
+    """A single fused call with n_c > 512 (576, 1024) builds its coarse inverse with the
+    device-wide inverse Cholesky factor (csrc/dense.hip) instead of one workgroup's: same
+    iteration count and histories as the one-workgroup factor and the oracle (SuperLU) to
+    rounding (rtol 1e-10), iterates within 1e-9 of their max."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mlamg.multigrid
+    import mlamg.problems
+    import mlamg as ml
+    A = ml.problems.poisson_2d_5pt(m)
+    P, _ = oracle.smoothed_aggregation_jacobi(A, ml.problems.box_aggregates_2d(m, m, agg),
+                                              omega=2.0 / 3.0)
+    assert P.shape[1] > 512
+    x0 = np.random.RandomState(m).randn(A.shape[0])
+    b = np.zeros(A.shape[0])
+    xe, ce, ee, ie = ml.multigrid.amg_2_v(A, P, b, x0, res_tol=1e-10, engine="fused")
+    monkeypatch.setenv("MLAMG_BATCH_NO_EXT", "1")
+    xw, cw, ew, iw = ml.multigrid.amg_2_v(A, P, b, x0, res_tol=1e-10, engine="fused")
+    xr, cr, er, ir = oracle.amg_2_v(A, P, b, x0, res_tol=1e-10)
+    assert ie == iw == ir
+    for e in (ee, ew):
+        assert np.allclose(e, er, rtol=1e-10, atol=0)
+    scale = np.abs(xr).max()
+    assert np.abs(xe - xr).max() <= 1e-9 * scale and np.abs(xe - xw).max() <= 1e-9 * scale
