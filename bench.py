@@ -209,6 +209,9 @@ def main():
     ap.add_argument("--dist-min-rows", type=int, default=50000,
                     help="distributed run: row-partition every level with at least this many "
                          "rows (the rest are replicated on each GPU)")
+    ap.add_argument("--overlap-min-rows", type=int, default=2_000_000,
+                    help="distributed run: split local operators of at least this many rows so "
+                         "their halo exchange overlaps the interior rows (-1: never)")
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the unstructured (C3) fine-SpMV roofline line")
     ap.add_argument("--launch-selftest", action="store_true",

@@ -420,6 +420,17 @@ int mlamg_dhier_add_level(mlamg_dhier* D, const mlamg_csr* A_loc, const double* 
                           const mlamg_csr* P_loc, const mlamg_csr* R_own, mlamg_halo* halo_x,
                           mlamg_halo* halo_r, mlamg_halo* halo_p);
 int mlamg_dhier_destroy(mlamg_dhier* D);
+/* halo / interior overlap (SURVEY.md §8e "overlapped with the interior SpMV"): operator `which`
+ * (0 = A_loc behind halo_x, 1 = R_own behind halo_r, 2 = P_loc behind halo_p) of `level` given
+ * as three consecutive row blocks lo | mid | hi (lo, hi may be NULL; each starts on an even row;
+ * same columns as the operator) where mid reads no ghost entry. The cycle then posts the
+ * exchange on a stream of its own and runs mid meanwhile, lo and hi after it; every row is
+ * summed as in the unsplit operator (exact-order formats), so the iterate is unchanged. Call
+ * before the first cycle. */
+int mlamg_dhier_set_split(mlamg_dhier* D, int level, int which, const mlamg_csr* lo,
+                          const mlamg_csr* mid, const mlamg_csr* hi);
+/* use the splits (default 1) or run every exchange before its whole operator (0) */
+int mlamg_dhier_set_overlap(mlamg_dhier* D, int on);
 int mlamg_dhier_set_coarse_graph(mlamg_dhier* D, int use_graph);
 /* capture one whole distributed cycle (kernels and RCCL send/recv/all-reduce) into a hipGraph
  * and replay it (default off); re-captured when b, x, res_hist, tol or a kernel format change */

@@ -277,12 +277,17 @@ __global__ void k_pack(const double* __restrict__ x, const int32_t* __restrict__
   if (i < n) out[i] = x[idx[i]];
 }
 
-int halo_exchange_impl(mlamg_halo* h, double* x_ext, hipStream_t s) {
+static int halo_pack(mlamg_halo* h, const double* x_ext, hipStream_t s) {
   if (h->n_send) {
     hipLaunchKernelGGL(k_pack, dim3((h->n_send + 255) / 256), dim3(256), 0, s, x_ext, h->send_idx,
                        h->n_send, h->send_buf);
     MLAMG_HIP(hipGetLastError());
   }
+  return MLAMG_OK;
+}
+
+// the grouped send/recv of a packed halo, on stream s
+static int halo_post(mlamg_halo* h, double* x_ext, hipStream_t s) {
   if (h->nbr.empty()) return MLAMG_OK;
   MLAMG_TRY(xgroup_begin(h->c));
   for (size_t q = 0; q < h->nbr.size(); ++q) {
@@ -293,6 +298,11 @@ int halo_exchange_impl(mlamg_halo* h, double* x_ext, hipStream_t s) {
                       h->nbr[q], s));
   }
   return xgroup_end(h->c, s);
+}
+
+int halo_exchange_impl(mlamg_halo* h, double* x_ext, hipStream_t s) {
+  MLAMG_TRY(halo_pack(h, x_ext, s));
+  return halo_post(h, x_ext, s);
 }
 
 // sum the residual partials of this rank into partial[n] (fixed order)
@@ -326,6 +336,16 @@ __global__ void k_norm_finish(const double* __restrict__ sum, double* hist, int3
 using namespace mlamg;
 
 namespace {
+// An operator split by rows for overlapping its halo exchange: part 1 is a run
+// of rows that read no ghost entry, parts 0 and 2 the rows before and after it (either may be
+// empty). Part k holds rows [r0[k], r0[k] + rows) of the operator, stored in the same order and
+// in an exact-order kernel format, so every row's sum is the unsplit operator's bit for bit.
+struct OpSplit {
+  const mlamg_csr* m[3] = {nullptr, nullptr, nullptr};
+  int64_t r0[3] = {0, 0, 0};
+  bool on() const { return m[1] != nullptr; }
+};
+
 struct DLevel {
   const mlamg_csr* A = nullptr;  // n_own x (n_own + ghosts_x)
   const mlamg_csr* P = nullptr;  // n_own x (next own + ghosts_p) | n_own x n_c (last level)
@@ -334,6 +354,7 @@ struct DLevel {
   mlamg_halo* hx = nullptr;
   mlamg_halo* hr = nullptr;
   mlamg_halo* hp = nullptr;  // halo of x_{l+1} for P (nullptr on the last partitioned level)
+  OpSplit sA, sR, sP;        // row splits behind hx, hr, hp (optional)
   int64_t n_own = 0;
   // work (l > 0: x_ext, b own; every level: r_ext, t_ext; xp_ext = x_{l+1} for P)
   double* x_ext = nullptr;
@@ -368,7 +389,45 @@ struct mlamg_dhier {
   double g_tol = -1.0;
   uint64_t g_epoch = 0;
   int32_t* done_host = nullptr;  // pinned copy of the stop flag (run_cycles)
+  // halo / interior overlap: the RCCL group of a split operator's exchange runs on comm_s while
+  // the interior rows run on the cycle's stream (events fork and join the two)
+  int overlap = 1;
+  hipStream_t comm_s = nullptr;
+  std::vector<hipEvent_t> evs;
+  size_t ev_next = 0;
+  int64_t part_cap = 0;
 };
+
+// the exchange of halo h into buf followed by the operator `whole`, through op(M, row0, part):
+// unsplit, the exchange then op(whole, 0, -1); split, the pack on s, the RCCL group on comm_s
+// (forked from s after the pack, so every earlier reader of the ghost region is done), the
+// interior rows on s meanwhile, then s joins comm_s and runs the boundary rows
+template <class Op>
+static int exchange_then(mlamg_dhier* D, mlamg_halo* h, double* buf, const mlamg_csr* whole,
+                         const OpSplit& sp, hipStream_t s, Op&& op) {
+  if (!(D->overlap && sp.on() && !h->nbr.empty())) {
+    MLAMG_TRY(halo_exchange_impl(h, buf, s));
+    return op(whole, (int64_t)0, -1);
+  }
+  if (D->ev_next + 2 > D->evs.size()) {
+    for (int q = 0; q < 16; ++q) {
+      hipEvent_t e;
+      MLAMG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      D->evs.push_back(e);
+    }
+  }
+  hipEvent_t fork = D->evs[D->ev_next++], join = D->evs[D->ev_next++];
+  MLAMG_TRY(halo_pack(h, buf, s));
+  MLAMG_HIP(hipEventRecord(fork, s));
+  MLAMG_HIP(hipStreamWaitEvent(D->comm_s, fork, 0));
+  MLAMG_TRY(halo_post(h, buf, D->comm_s));
+  MLAMG_HIP(hipEventRecord(join, D->comm_s));
+  MLAMG_TRY(op(sp.m[1], sp.r0[1], 1));
+  MLAMG_HIP(hipStreamWaitEvent(s, join, 0));
+  if (sp.m[0]) MLAMG_TRY(op(sp.m[0], sp.r0[0], 0));
+  if (sp.m[2]) MLAMG_TRY(op(sp.m[2], sp.r0[2], 2));
+  return MLAMG_OK;
+}
 
 static void dhier_free_graph(mlamg_dhier* D) {
   if (D->exec) (void)hipGraphExecDestroy(D->exec);
@@ -600,10 +659,46 @@ int mlamg_dhier_add_level(mlamg_dhier* D, const mlamg_csr* A_loc, const double* 
   return MLAMG_OK;
 }
 
+int mlamg_dhier_set_split(mlamg_dhier* D, int level, int which, const mlamg_csr* lo,
+                          const mlamg_csr* mid, const mlamg_csr* hi) {
+  MLAMG_REQUIRE(D && mid, "NULL argument");
+  MLAMG_REQUIRE(!D->ready, "hierarchy already in use");
+  MLAMG_REQUIRE(level >= 0 && (size_t)level < D->lv.size(), "level out of range");
+  MLAMG_REQUIRE(which >= 0 && which <= 2, "which: 0 = A, 1 = R, 2 = P");
+  DLevel& L = D->lv[level];
+  MLAMG_REQUIRE(which != 2 || L.hp, "P is split only where a P halo precedes it");
+  const mlamg_csr* whole = which == 0 ? L.A : which == 1 ? L.R : L.P;
+  OpSplit sp;
+  sp.m[0] = lo;
+  sp.m[1] = mid;
+  sp.m[2] = hi;
+  int64_t r = 0;
+  for (int k = 0; k < 3; ++k) {
+    sp.r0[k] = r;
+    if (!sp.m[k]) continue;
+    MLAMG_REQUIRE(sp.m[k]->n_cols == whole->n_cols, "split part has other columns");
+    // the row-pair kernels load epilogue vectors as 16-byte pairs: parts start on even rows
+    MLAMG_REQUIRE(r % 2 == 0, "split parts must start on even rows");
+    r += sp.m[k]->n_rows;
+  }
+  MLAMG_REQUIRE(r == whole->n_rows, "split parts do not cover the operator's rows");
+  (which == 0 ? L.sA : which == 1 ? L.sR : L.sP) = sp;
+  return MLAMG_OK;
+}
+
+int mlamg_dhier_set_overlap(mlamg_dhier* D, int on) {
+  MLAMG_REQUIRE(D, "NULL argument");
+  D->overlap = on ? 1 : 0;
+  dhier_free_graph(D);
+  return MLAMG_OK;
+}
+
 int mlamg_dhier_destroy(mlamg_dhier* D) {
   if (D) {
     dhier_free_graph(D);
     if (D->cap_stream) (void)hipStreamDestroy(D->cap_stream);
+    if (D->comm_s) (void)hipStreamDestroy(D->comm_s);
+    for (hipEvent_t e : D->evs) (void)hipEventDestroy(e);
     if (D->done_host) (void)hipHostFree(D->done_host);
     for (void* p : D->bufs)
       if (p) (void)hipFree(p);
@@ -652,7 +747,11 @@ static int dprepare(mlamg_dhier* D) {
     if (l > 0) D->lv[l - 1].xp_ext = L.t_ext;
   }
   MLAMG_TRY(dalloc(D, &D->bc, D->nc));
-  MLAMG_TRY(dalloc(D, &D->partial, part_capacity(D->lv[0].A)));
+  int64_t pc = part_capacity(D->lv[0].A), ps = 0;
+  for (int k = 0; k < 3; ++k)
+    if (D->lv[0].sA.m[k]) ps += part_capacity(D->lv[0].sA.m[k]);
+  MLAMG_TRY(dalloc(D, &D->partial, std::max(pc, ps)));
+  if (!D->comm_s) MLAMG_HIP(hipStreamCreateWithFlags(&D->comm_s, hipStreamNonBlocking));
   double* f = nullptr;
   MLAMG_TRY(dalloc(D, &f, 1));
   D->flags = reinterpret_cast<int32_t*>(f);
@@ -684,22 +783,31 @@ static int dcycle_below(mlamg_dhier* D, size_t l, double** x_out, hipStream_t s)
 // coarse-grid correction of partitioned level l: b_{l+1} = R r, solve below, x += P x_{l+1}
 static int correct(mlamg_dhier* D, size_t l, double* x_ext, const int32_t* done, hipStream_t s) {
   DLevel& L = D->lv[l];
-  MLAMG_TRY(halo_exchange_impl(L.hr, L.r_ext, s));
   if (L.hp) {
     DLevel& N = D->lv[l + 1];
     // restriction fused with the next level's zero-guess sweep (x = Dinv_w b on owned rows)
-    MLAMG_TRY(spmv_set(L.R, L.r_ext, N.b, done, s, N.x_ext, N.dinv));
+    MLAMG_TRY(exchange_then(D, L.hr, L.r_ext, L.R, L.sR, s,
+                            [&](const mlamg_csr* M, int64_t r0, int) {
+                              return spmv_set(M, L.r_ext, N.b + r0, done, s, N.x_ext + r0,
+                                              N.dinv + r0);
+                            }));
     double* xn = nullptr;
     MLAMG_TRY(dcycle_below(D, l + 1, &xn, s));
     // xp_ext is the level below's t_ext: its owned part is the correction, the P-halo lands in
-    // its (no longer needed) ghost region
-    MLAMG_TRY(halo_exchange_impl(L.hp, L.xp_ext, s));
-    // P rows cover the owned AND the x-ghost rows: x_ext's ghosts get the same update their
-    // owners compute (same row, same order, same inputs), so no x halo is needed afterwards
-    MLAMG_TRY(spmv_add(L.P, L.xp_ext, x_ext, done, s));
+    // its (no longer needed) ghost region. P rows cover the owned AND the x-ghost rows: x_ext's
+    // ghosts get the same update their owners compute (same row, same order, same inputs), so
+    // no x halo is needed afterwards
+    MLAMG_TRY(exchange_then(D, L.hp, L.xp_ext, L.P, L.sP, s,
+                            [&](const mlamg_csr* M, int64_t r0, int) {
+                              return spmv_add(M, L.xp_ext, x_ext + r0, done, s);
+                            }));
   } else {
     const int me = D->c->rank;
-    MLAMG_TRY(spmv_set(L.R, L.r_ext, D->bc + D->c_lo_all[me], done, s));
+    double* bo = D->bc + D->c_lo_all[me];
+    MLAMG_TRY(exchange_then(D, L.hr, L.r_ext, L.R, L.sR, s,
+                            [&](const mlamg_csr* M, int64_t r0, int) {
+                              return spmv_set(M, L.r_ext, bo + r0, done, s);
+                            }));
     MLAMG_TRY(allgather_segments(D, s));
     double* xc = nullptr;
     // inside a whole-cycle capture the coarse kernels are captured directly (no nested graph)
@@ -715,9 +823,12 @@ static int dcycle_below(mlamg_dhier* D, size_t l, double** x_out, hipStream_t s)
   const int32_t* done = D->flags + 1;
   DLevel& L = D->lv[l];
   // x = Dinv_w b was written by the restriction kernel of the level above (correct())
-  MLAMG_TRY(halo_exchange_impl(L.hx, L.x_ext, s));
-  MLAMG_TRY(residual_impl(L.A, L.b, L.x_ext, L.r_ext, nullptr, nullptr, nullptr,
-                          const_cast<int32_t*>(done), kNoTol, nullptr, nullptr, nullptr, s));
+  MLAMG_TRY(exchange_then(D, L.hx, L.x_ext, L.A, L.sA, s,
+                          [&](const mlamg_csr* M, int64_t r0, int) {
+                            return residual_impl(M, L.b + r0, L.x_ext, L.r_ext + r0, nullptr,
+                                                 nullptr, nullptr, const_cast<int32_t*>(done),
+                                                 kNoTol, nullptr, nullptr, nullptr, s);
+                          }));
   MLAMG_TRY(correct(D, l, L.x_ext, done, s));
   MLAMG_TRY(jacobi_sweep(L.A, L.dinv, L.b, L.x_ext, L.t_ext, false, done, s));
   *x_out = L.t_ext;
@@ -733,17 +844,32 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
   int32_t* done = D->flags + 1;
   DLevel& L = D->lv[0];
   const mlamg_csr* A = L.A;
-  MLAMG_TRY(halo_exchange_impl(L.hx, x_ext, s));
-  MLAMG_TRY(residual_impl(A, b, x_ext, L.r_ext, nullptr, nullptr, nullptr, done, kNoTol, nullptr,
-                          nullptr, nullptr, s));
+  D->ev_next = 0;
+  MLAMG_TRY(exchange_then(D, L.hx, x_ext, A, L.sA, s, [&](const mlamg_csr* M, int64_t r0, int) {
+    return residual_impl(M, b + r0, x_ext, L.r_ext + r0, nullptr, nullptr, nullptr, done, kNoTol,
+                         nullptr, nullptr, nullptr, s);
+  }));
   MLAMG_TRY(correct(D, 0, x_ext, done, s));
   MLAMG_TRY(jacobi_sweep(A, L.dinv, b, x_ext, L.t_ext, false, done, s));
-  MLAMG_TRY(halo_exchange_impl(L.hx, L.t_ext, s));
   // r = b - A t with per-block ||r||^2 partials, x <- t; then the global norm
-  // (r itself is not stored: the next cycle starts with its own residual)
-  MLAMG_TRY(residual_partials(A, b, L.t_ext, nullptr, x_ext, L.t_ext, D->partial, done, s,
-                              L.dinv));
-  const int nb = (int)A->n_part;
+  // (r itself is not stored: the next cycle starts with its own residual). Split: the parts'
+  // partials lie in part order (0, 1, 2), whatever order the parts ran in
+  int64_t poff[3] = {0, 0, 0};
+  int nb = (int)A->n_part;
+  if (D->overlap && L.sA.on() && !L.hx->nbr.empty()) {
+    nb = 0;
+    for (int k = 0; k < 3; ++k) {
+      poff[k] = nb;
+      if (L.sA.m[k]) nb += (int)L.sA.m[k]->n_part;
+    }
+  }
+  MLAMG_TRY(exchange_then(D, L.hx, L.t_ext, A, L.sA, s,
+                          [&](const mlamg_csr* M, int64_t r0, int part) {
+                            return residual_partials(M, b + r0, L.t_ext, nullptr, x_ext + r0,
+                                                     L.t_ext + r0,
+                                                     D->partial + (part < 0 ? 0 : poff[part]),
+                                                     done, s, L.dinv + r0);
+                          }));
   hipLaunchKernelGGL(k_local_sum, dim3(1), dim3(1024), 0, s, D->partial, nb);
   MLAMG_HIP(hipGetLastError());
   if (D->c->nranks > 1) MLAMG_TRY(xallreduce_sum(D->c, D->partial + nb, 1, s));

@@ -158,6 +158,8 @@ SIGNATURES = {
     "mlamg_dhier_destroy": (c_int, [c_vp]),
     "mlamg_dhier_set_coarse_graph": (c_int, [c_vp, c_int]),
     "mlamg_dhier_set_cycle_graph": (c_int, [c_vp, c_int]),
+    "mlamg_dhier_set_split": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp]),
+    "mlamg_dhier_set_overlap": (c_int, [c_vp, c_int]),
     "mlamg_dhier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_vp]),
     # boundary-contract spellings (csrc/contract.hip)
     "mlamg_lloyd": (c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp]),

@@ -147,12 +147,19 @@ class DistributedHierarchy:
     coarse cycle. The iterate is bitwise the single-GPU Hierarchy.cycle iterate."""
 
     def __init__(self, H, comm, min_rows=50000, max_partitioned=None, A_host=None,
-                 local_autotune=True):
+                 local_autotune=True, overlap_min_rows=2_000_000):
         """H: mlamg.hierarchy.Hierarchy built identically on every rank (sorted seeds, same
         kernel formats — see sync_formats). Levels with at least `min_rows` rows (at most
         `max_partitioned` of them) are row-partitioned; the rest are replicated.
         local_autotune: time every exact-order kernel on each rank's local operators (see
-        tune_local) instead of reusing the global operator's choice."""
+        tune_local) instead of reusing the global operator's choice.
+        overlap_min_rows: local operators with at least this many rows are split into
+        boundary | interior | boundary row blocks (partition.interior_split) so their halo
+        exchange overlaps the interior rows (mlamg_dhier_set_split); None: no splits. A split
+        costs two more launches and a stream fork/join per exchange (measured with the null
+        communicator at world 8, C4: +7 us per split operator), so it pays only where the
+        interior rows take longer than that: the default splits local operators of >= 2 M rows
+        (C4 level 0 at world <= 4)."""
         if not H.levels:
             raise ValueError("distributed cycle needs at least one level above the coarse solve")
         if (H.nu_pre, H.nu_post) != (1, 1):
@@ -203,6 +210,7 @@ class DistributedHierarchy:
              ctypes.byref(d))
         self.handle = d
         self.ghosts = []
+        self.splits = []
         for l, p in enumerate(parts):
             Lg = H.levels[l]
             A_loc = like(Lg.A, DeviceCSR.from_scipy(p["A_loc"], check=False), "A")
@@ -218,10 +226,46 @@ class DistributedHierarchy:
             self.ghosts.append((hx.n_ghost, hr.n_ghost, hp.n_ghost if hp else 0))
             call("mlamg_dhier_add_level", d, A_loc.handle, ptr(dinv), P_loc.handle, R_own.handle,
                  hx.handle, hr.handle, hp.handle if hp else None)
+            if overlap_min_rows is not None:
+                n_l = p["hi"] - p["lo"]
+                ops = [(0, Lg.A, p["A_loc"], n_l, dinv), (1, Lg.R, p["R_own"], n_l, None)]
+                if hp is not None:
+                    ops.append((2, Lg.P, p["P_loc"], p["c_hi"] - p["c_lo"], None))
+                for which, M_glob, M_host, n_owned, dv in ops:
+                    if M_host.shape[0] >= overlap_min_rows:
+                        self._split(l, which, M_glob, M_host, n_owned, dv, like)
             if l == 0:
                 self.A_loc = A_loc
                 self.hx = hx
         self.n_ext = self.n_own + self.hx.n_ghost
+
+    def _split(self, l, which, M_glob, M_host, n_owned, dinv, like):
+        cut = partition.interior_split(M_host, n_owned)
+        if cut is None:
+            return
+        lo, hi = cut
+        parts = []
+        for a, b in ((0, lo), (lo, hi), (hi, M_host.shape[0])):
+            if b == a:
+                parts.append(None)
+                continue
+            M = like(M_glob, DeviceCSR.from_scipy(M_host[a:b], check=False), "APR"[which])
+            self.tuning.pop()  # keep D.tuning = the whole operators' choices, 3 per level
+            if dinv is not None and M.get_format()[0] == "rowpat":
+                # a view: the epilogues are handed dinv + a, the very pointer attached
+                M.attach_dinv(dinv[a:b])
+            self._keep.append(M)
+            parts.append(M)
+        call("mlamg_dhier_set_split", self.handle, int(l), int(which),
+             parts[0].handle if parts[0] else None, parts[1].handle,
+             parts[2].handle if parts[2] else None)
+        self.splits.append({"level": l, "op": "APR"[which], "rows": [0, lo, hi, M_host.shape[0]],
+                            "formats": ["/".join(map(str, M.get_format()[:2])) if M else None
+                                        for M in parts]})
+
+    def set_overlap(self, on):
+        """Overlap each split operator's halo exchange with its interior rows (default on)."""
+        call("mlamg_dhier_set_overlap", self.handle, int(bool(on)))
 
     def new_x(self, x_own):
         x = torch.zeros(self.n_ext, dtype=torch.float64, device="cuda")
@@ -341,7 +385,9 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
     comm = Comm(world, rank)
     cinfo = comm.info()
     t1 = time.perf_counter()
-    D = DistributedHierarchy(H, comm, min_rows=args.dist_min_rows, A_host=A)
+    omr = getattr(args, "overlap_min_rows", 2_000_000)
+    D = DistributedHierarchy(H, comm, min_rows=args.dist_min_rows, A_host=A,
+                             overlap_min_rows=None if omr < 0 else omr)
     part_s = time.perf_counter() - t1
     log(f"setup {setup_s:.1f}s (replicated), partition+upload {part_s:.1f}s; {D.K} of "
         f"{len(H.levels)} levels partitioned; rank rows {D.lo}..{D.hi}; ghosts (x, r, p) per "
@@ -438,6 +484,7 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
                             f"Jacobi, {D.K} finest levels row-split over {world} GPUs + RCCL "
                             f"halos, {H.n_levels - D.K} coarser levels replicated",
                 "partitioned_levels": D.K,
+                "overlap_splits": [(s["level"], s["op"]) for s in D.splits],
                 "n": n, "levels": H.n_levels, "parallelism": f"rowsplit{world}",
                 "dist_matches_single_gpu": bool(ok_all),
                 "cycle_graph": graph_on,

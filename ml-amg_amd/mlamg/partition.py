@@ -203,3 +203,34 @@ def build(A0, P0, seeds, world, rank=None):
             "A_loc": A_loc, "P_loc": P_loc, "R_own": R_own, "halo_x": hx, "halo_r": hr,
         })
     return out[rank] if rank is not None else out
+
+
+def interior_split(M, n_owned_cols, min_frac=0.5):
+    """Row split of a local operator for overlapping its halo exchange: the
+    longest run of rows whose columns are all owned (< n_owned_cols), as (lo, hi) with both ends
+    even (the row-pair kernels load epilogue vectors as 16-byte pairs; rounding only moves
+    interior rows into the boundary parts). None when that run is shorter than min_frac of the
+    rows or no row reads a ghost."""
+    M = M.tocsr()
+    n = M.shape[0]
+    if n == 0:
+        return None
+    ghost = np.zeros(n, dtype=bool)
+    lens = np.diff(M.indptr)
+    rows = np.repeat(np.arange(n), lens)
+    ghost[rows[M.indices >= n_owned_cols]] = True
+    if not ghost.any():
+        return None
+    # runs of interior rows: boundaries where ghost flips
+    interior = ~ghost
+    edges = np.flatnonzero(np.diff(np.concatenate(([0], interior.astype(np.int8), [0]))))
+    starts, ends = edges[0::2], edges[1::2]
+    if len(starts) == 0:
+        return None
+    k = int(np.argmax(ends - starts))
+    lo, hi = int(starts[k]), int(ends[k])
+    lo += lo & 1
+    hi -= hi & 1
+    if hi - lo < max(2, min_frac * n):
+        return None
+    return lo, hi

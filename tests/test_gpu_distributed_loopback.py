@@ -27,18 +27,20 @@ def setup():
     return A, H
 
 
-def _run(A, H, world, min_rows, ncyc=6, tol=None, b=None, x0=None, K=None):
+def _run(A, H, world, min_rows, ncyc=6, tol=None, b=None, x0=None, K=None,
+         overlap_min_rows=100000, overlap=True):
     import torch
     from mlamg.distributed import DistributedHierarchy, LoopbackGroup
     n = A.shape[0]
     group = LoopbackGroup(world)
     try:
         Ds = [DistributedHierarchy(H, group.comms[r], min_rows=min_rows, A_host=A,
-                                   max_partitioned=K)
+                                   max_partitioned=K, overlap_min_rows=overlap_min_rows)
               for r in range(world)]
         for D in Ds:
             D.set_cycle_graph(False)
             D.set_coarse_graph(False)
+            D.set_overlap(overlap)
         bs = [torch.as_tensor(b[D.lo:D.hi]).cuda() for D in Ds]
         xs = [D.new_x(torch.as_tensor(x0[D.lo:D.hi])) for D in Ds]
         torch.cuda.synchronize()
@@ -82,6 +84,32 @@ def test_loopback_distributed_cycle_bitwise(setup, world, K):
     x_ref = xd.cpu().numpy()
     Ds, out = _run(A, H, world, 0, b=b, x0=x0, K=K)
     assert Ds[0].K == (K or len(H.levels))
+    for D, (x_own, h) in zip(Ds, out):
+        assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank} of {world}, K={D.K}"
+        np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("world,K,overlap", [(2, None, True), (3, 2, True), (8, None, True),
+                                             (3, None, False)])
+def test_loopback_overlap_split_bitwise(setup, world, K, overlap):
+    """Every local operator split into boundary | interior | boundary rows (overlap_min_rows=0):
+    the exchange runs on the executor's communication stream while the interior rows run, the
+    boundary rows after it. The iterate stays bitwise the single-GPU iterate (and with the
+    splits present but overlap off)."""
+    import torch
+    A, H = setup
+    n = A.shape[0]
+    x0 = np.random.RandomState(7).randn(n)
+    b = np.random.RandomState(8).randn(n)
+    xd = torch.as_tensor(x0).cuda()
+    h_ref = H.cycle(torch.as_tensor(b).cuda(), xd, 6, use_graph=False)
+    x_ref = xd.cpu().numpy()
+    Ds, out = _run(A, H, world, 0, b=b, x0=x0, K=K, overlap_min_rows=0, overlap=overlap)
+    # interior rows exist on every rank's fine operator, so every rank split it
+    for D in Ds:
+        assert any(s["level"] == 0 and s["op"] == "A" for s in D.splits), D.splits
+    if world <= 3:  # thick slabs: the restriction / prolongation are split as well
+        assert sum(len(D.splits) for D in Ds) >= 2 * world
     for D, (x_own, h) in zip(Ds, out):
         assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank} of {world}, K={D.K}"
         np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
@@ -139,6 +167,10 @@ def test_loopback_c4_world8_bench_partition():
     del xd
     Ds, out = _run(A, H, 8, 50000, ncyc=3, b=b, x0=x0)
     assert Ds[0].K == 3
+    # the fine operator of every rank is split (two z-planes of boundary rows, one on the ends)
+    for D in Ds:
+        s0 = [s for s in D.splits if s["level"] == 0 and s["op"] == "A"]
+        assert s0 and s0[0]["formats"][1].startswith("rowpat"), D.splits
     assert Ds[0].tuning[0]["chosen"].startswith("rowpat")  # fine local operator stays rowpat
     for D, (x_own, h) in zip(Ds, out):
         assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank}"

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--min-rows", default="50000", help="comma list of dist_min_rows values")
+    ap.add_argument("--overlap", default="1", help="comma list: halo/interior overlap off (0) / on (1)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     A = problems.poisson_3d_7pt(a.n)
@@ -47,21 +48,24 @@ def main():
         for r in sorted({0, w // 2, w - 1}):
             c = NullComm(w, r)
             D = DistributedHierarchy(H, c, min_rows=mr, A_host=A)
-            D.set_cycle_graph(True)
-            x = D.new_x(torch.zeros(D.n_own, dtype=torch.float64))
-            b = torch.zeros(D.n_own, dtype=torch.float64, device="cuda")
-            D.cycle(b, x, 3, history=False)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            D.cycle(b, x, a.steps, history=False)
-            torch.cuda.synchronize()
-            t = (time.perf_counter() - t0) / a.steps
-            row = {"world": w, "rank": r, "min_rows": mr, "K": D.K, "rows": D.n_own,
-                   "compute_ms_per_cycle": round(t * 1e3, 4),
-                   "compute_bound_cycles_per_s": round(1.0 / t, 1),
-                   "local_formats": [x["chosen"] for x in D.tuning]}
-            out["ranks"].append(row)
-            print(json.dumps(row), flush=True)
+            for ov in map(int, a.overlap.split(",")):
+                D.set_overlap(ov)
+                D.set_cycle_graph(True)
+                x = D.new_x(torch.zeros(D.n_own, dtype=torch.float64))
+                b = torch.zeros(D.n_own, dtype=torch.float64, device="cuda")
+                D.cycle(b, x, 3, history=False)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                D.cycle(b, x, a.steps, history=False)
+                torch.cuda.synchronize()
+                t = (time.perf_counter() - t0) / a.steps
+                row = {"world": w, "rank": r, "min_rows": mr, "K": D.K, "rows": D.n_own,
+                       "overlap": ov, "splits": [(s["level"], s["op"]) for s in D.splits],
+                       "compute_ms_per_cycle": round(t * 1e3, 4),
+                       "compute_bound_cycles_per_s": round(1.0 / t, 1),
+                       "local_formats": [x["chosen"] for x in D.tuning]}
+                out["ranks"].append(row)
+                print(json.dumps(row), flush=True)
             del D
             c.close()
     print(json.dumps(out))
