@@ -419,9 +419,14 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
         return bool(ok.item() == 1.0)
 
     graph_on = not args.no_graph
+    overlap_on = bool(D.splits)
     D.set_cycle_graph(graph_on)
     ok_all = check()
-    if not ok_all and graph_on:  # never time a path that does not reproduce the iterate
+    if not ok_all and overlap_on:  # never time a path that does not reproduce the iterate
+        overlap_on = False
+        D.set_overlap(False)
+        ok_all = check()
+    if not ok_all and graph_on:
         graph_on = False
         D.set_cycle_graph(False)
         ok_all = check()
@@ -484,7 +489,7 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
                             f"Jacobi, {D.K} finest levels row-split over {world} GPUs + RCCL "
                             f"halos, {H.n_levels - D.K} coarser levels replicated",
                 "partitioned_levels": D.K,
-                "overlap_splits": [(s["level"], s["op"]) for s in D.splits],
+                "overlap_splits": [(s["level"], s["op"]) for s in D.splits] if overlap_on else [],
                 "n": n, "levels": H.n_levels, "parallelism": f"rowsplit{world}",
                 "dist_matches_single_gpu": bool(ok_all),
                 "cycle_graph": graph_on,
