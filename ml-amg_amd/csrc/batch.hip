@@ -55,7 +55,7 @@ constexpr int kBMaxK = 32;          // off-diagonal entries per row of A
 constexpr int kBMaxKP = 32;         // entries per row of P
 constexpr int kBMaxKT = 256;        // entries per row of P^T
 constexpr int kBMaxPanel = 16;
-constexpr int kExtCoarseMin = 512;  // single calls above this n_c: device-wide coarse factor
+constexpr int kExtCoarseMin = 300;  // single calls above this n_c: device-wide coarse factor
 constexpr size_t kBLdsBytes = 156 * 1024;
 
 struct BDesc {
@@ -67,6 +67,9 @@ struct BDesc {
                        // built by the device-wide factorisation, dense.hip)
   int32_t gs_rw;  // one-wave sweep (rows of K = 4 or 8 slots, levels <= 64 * gs_rw rows), 1 or 2
                   // rows per lane; 0: the workgroup sweeps each level
+  int32_t gs_db;   // one-wave sweep: double-buffered chunk staging (chunks of >= 3 levels)
+  int32_t phased;  // single large problem: each cycle is two launches, the workgroup's half
+                   // cycles and the coarse solve on every CU (k_amg2v_coarse); r_H, e_H global
   double tol, omega;
   // byte offsets into the arena; packed arrays are slot-major: a[s * rows + row]
   int64_t ak_col, ak_val;                  // A rows, stored order incl. diagonal (KA slots)
@@ -77,6 +80,7 @@ struct BDesc {
   int64_t AH, AI, rg, dinv;                // Galerkin / un-pivoted inverse / r when not in
                                            // LDS / weighted-Jacobi weights
   int64_t x_out, err_out, stat_out;
+  int64_t rcg, eg;  // phased: r_H and e_H in the arena
 };
 
 template <class T>
@@ -513,6 +517,49 @@ __device__ void dense_galerkin(const BDesc& D, char* arena, double* AH, int tid)
   __syncthreads();
 }
 
+// The Galerkin product of a single problem on the whole GPU (setup_mode 1): a workgroup per
+// block of R coarse rows, each row accumulated by one thread in LDS in dense_galerkin's order
+// (so A_H is bitwise the workgroup kernel's) instead of by read-modify-writes to global memory
+// (a chain of ~800 dependent round trips per row), then written out coalesced.
+__global__ __launch_bounds__(256) void k_galerkin_rows(const BDesc* __restrict__ descs,
+                                                       char* __restrict__ arena, int R) {
+  extern __shared__ double rows_lds[];
+  const BDesc D = descs[0];
+  const int n = D.n, nc = D.nc, KA = D.KA, KP = D.KP, KT = D.KT;
+  const int j0 = blockIdx.x * R, nr = min(R, nc - j0);
+  if (nr <= 0) return;
+  for (int q = threadIdx.x; q < nr * nc; q += 256) rows_lds[q] = 0.0;
+  __syncthreads();
+  if ((int)threadIdx.x < nr) {
+    const int32_t* __restrict__ akc = at<int32_t>(arena, D.ak_col);
+    const double* __restrict__ akv = at<double>(arena, D.ak_val);
+    const int32_t* __restrict__ ppc = at<int32_t>(arena, D.pp_col);
+    const double* __restrict__ ppv = at<double>(arena, D.pp_val);
+    const int32_t* __restrict__ ptc = at<int32_t>(arena, D.pt_row);
+    const double* __restrict__ ptv = at<double>(arena, D.pt_val);
+    const int j = j0 + threadIdx.x;
+    double* row = rows_lds + (int64_t)threadIdx.x * nc;
+    for (int t = 0; t < KT; ++t) {
+      const int i = ptc[(int64_t)t * nc + j];
+      if (i < 0) break;
+      const double p = ptv[(int64_t)t * nc + j];
+      for (int k = 0; k < KA; ++k) {
+        const int c = akc[(int64_t)k * n + i];
+        if (c < 0) break;
+        const double pa = p * akv[(int64_t)k * n + i];
+        for (int m = 0; m < KP; ++m) {
+          const int cc = ppc[(int64_t)m * n + c];
+          if (cc < 0) break;
+          row[cc] += pa * ppv[(int64_t)m * n + c];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  double* AH = at<double>(arena, D.AH) + (int64_t)j0 * nc;
+  for (int q = threadIdx.x; q < nr * nc; q += 256) AH[q] = rows_lds[q];
+}
+
 // one workgroup per problem: Galerkin product and coarse inverse (operator mode in stat[2]:
 // 1 = inverse Cholesky factor L^-1 in AH's lower triangle and its transpose in AI's upper
 // triangle, 0 = the Gauss-Jordan inverse in AI)
@@ -541,16 +588,20 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
   };
   if (D.timing && tid == 0)
     for (int q = 0; q < 8; ++q) tstat[q] = 0;
+  if (tid == 0) {  // phased cycles: done flag, half cycles run
+    stat[3] = 0;
+    tstat[7] = 0;
+  }
 
-  dense_galerkin(D, arena, AH, tid);
-  stamp(0);
-  if (D.setup_mode == 1) {
+  if (D.setup_mode == 1) {  // A_H from k_galerkin_rows, the inverse from dense.hip
     if (tid == 0) {
       stat[1] = 0;
       stat[2] = 0;
     }
     return;
   }
+  dense_galerkin(D, arena, AH, tid);
+  stamp(0);
 
   if (D.spd) {
     // the panel width is the problem's own (a function of n_c alone): a problem's roundings do
@@ -734,8 +785,42 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
   }
 }
 
-// one workgroup per problem: the cycles (reads the setup kernel's inverse and status)
-template <bool R_LDS>
+// e_H = A_H^-1 r_H of a phased problem on every CU: a wave per row, the order and operations of
+// rows_dot<0> (lane l sums columns l, l + 64, ... with fma, then the butterfly), so the result
+// is the one-workgroup cycle's bit for bit
+__global__ __launch_bounds__(256) void k_amg2v_coarse(const BDesc* __restrict__ descs,
+                                                      char* __restrict__ arena) {
+  const BDesc D = descs[0];
+  const int32_t* stat = at<int32_t>(arena, D.stat_out);
+  if (stat[3]) return;
+  const int nc = D.nc;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= nc) return;
+  const double* __restrict__ M = at<double>(arena, D.AI) + (int64_t)row * nc;
+  const double* __restrict__ v = at<double>(arena, D.rcg);
+  // rows_dot's steps of 4 x 64 columns, zero-padded past nc exactly as there (fma(0, 0, s))
+  double s = 0.0;
+  for (int o = 0; o < nc; o += 4 * 64) {
+    double m[4], x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = o + u * 64 + lane;
+      m[u] = k < nc ? M[k] : 0.0;
+      x[u] = k < nc ? v[k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s = fma(m[u], x[u], s);
+  }
+  s = bw_sum(s);
+  if (lane == 0) at<double>(arena, D.eg)[row] = s;
+}
+
+// one workgroup per problem: the cycles (reads the setup kernel's inverse and status).
+// PHASED (a single problem): one launch runs the second half of cycle k - 1 (x += P e_H from
+// k_amg2v_coarse, post-smoothing, norm, tolerance test) and the first half of cycle k
+// (pre-smoothing, residual, r_H = P^T r), x kept in x_out between launches; stat[3] = done,
+// tstat[7] = launches so far
+template <bool R_LDS, bool PHASED>
 __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ descs,
                                                       char* __restrict__ arena) {
   extern __shared__ double lds[];
@@ -766,20 +851,36 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
     }
   };
   const int status = stat[1], mode = stat[2];
+  int64_t phase = 0;
+  if constexpr (PHASED) {
+    if (stat[3]) return;  // finished in an earlier launch
+    phase = tstat[7];
+  }
 
   // ---------------------------------------------------------------- cycles
   double* xs = lds;                                     // n + 2: x, a zero slot, a sink slot
-  double* rcs = xs + n + 2;                             // nc: restricted residual
-  double* es = rcs + nc;                                // nc: coarse correction
-  double* rs = R_LDS ? es + nc : at<double>(arena, D.rg);  // n: residual
+  double* rcs;                                          // nc: restricted residual
+  double* es;                                           // nc: coarse correction
+  double* rs;                                           // n: residual
+  int64_t stage_off;
+  if constexpr (PHASED) {
+    rcs = at<double>(arena, D.rcg);
+    es = at<double>(arena, D.eg);
+    rs = R_LDS ? xs + n + 2 : at<double>(arena, D.rg);
+    stage_off = ((R_LDS ? n + 2 + n : n + 2) + 1) & ~int64_t(1);
+  } else {
+    rcs = xs + n + 2;
+    es = rcs + nc;
+    rs = R_LDS ? es + nc : at<double>(arena, D.rg);
+    stage_off = ((R_LDS ? (es - lds) + nc + n : (es - lds) + nc) + 1) & ~int64_t(1);
+  }
   double* ys = rs;  // nc <= n: L^-1 r_H, in r's storage (r is dead from the restriction to the
                     // next residual)
   // GS staging area, 16-byte aligned (the one-wave sweep reads its rows with 16-byte loads)
   // (an even double offset from the LDS base: index arithmetic keeps the LDS address space,
   // which an integer round trip would lose to flat accesses)
-  const int64_t stage_off = ((R_LDS ? (es - lds) + nc + n : (es - lds) + nc) + 1) & ~int64_t(1);
   double* stage = lds + stage_off;
-  const double* __restrict__ x0 = at<double>(arena, D.x0);
+  const double* __restrict__ x0 = PHASED && phase > 0 ? x_out : at<double>(arena, D.x0);
   #pragma unroll 1
   for (int i = tid; i < n; i += kBT) xs[i] = x0[i];
   if (tid == 0) xs[n] = 0.0;  // pad columns of the one-wave sweep read it; nothing writes it
@@ -787,13 +888,16 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
   if (status != 0) {  // multigrid.py:167-170: x returned untouched, no iteration
     #pragma unroll 1
     for (int i = tid; i < n; i += kBT) x_out[i] = xs[i];
-    if (tid == 0) stat[0] = 0;
+    if (tid == 0) {
+      stat[0] = 0;
+      stat[3] = 1;
+    }
     return;
   }
   // weighted-Jacobi weights (1/a_ii) * w, a_ii = the sum of the stored diagonal entries
-  // (csr_diagonal)
+  // (csr_diagonal); a phased problem keeps them from its first launch
   double* dwg = at<double>(arena, D.dinv);
-  if (D.smoother == 1) {
+  if (D.smoother == 1 && phase == 0) {
     #pragma unroll 1
     for (int i = tid; i < n; i += kBT) {
       double d = 0.0;
@@ -853,10 +957,10 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
   // level's x gathers above this level's stores. Level l+1's rows are loaded while level l
   // gathers and divides. The padded sum adds +0.0 products to a sum that started at +0.0 (never
   // -0.0), so it is bitwise pyamg's.
-  auto wave_sweep = [&](auto km_tag, auto rw_tag, int nl, int cnt) {
+  auto wave_sweep = [&](auto km_tag, auto rw_tag, const double* stg, int nl, int cnt) {
     constexpr int KM = decltype(km_tag)::value, RW = decltype(rw_tag)::value;
     const int lane = tid & 63;
-    const double* sv = stage;
+    const double* sv = stg;
     const double* sd = sv + (int64_t)(cap + 1) * KM;
     const double* sb = sd + (cap + 1);
     const int32_t* sc = reinterpret_cast<const int32_t*>(sb + (cap + 1));
@@ -928,45 +1032,64 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
     // pyamg gauss_seidel: rsum over the off-diagonals in stored order, diag = the last stored
     // diagonal entry, x_i = (b_i - rsum) / diag unless diag == 0
     if (D.gs_rw > 0) {  // one-wave sweep, position-major rows of K (= 4 or 8) slots
-      double* wv = stage;
-      double* wd = wv + (int64_t)(cap + 1) * K;
-      double* wb = wd + (cap + 1);
-      int32_t* wc = reinterpret_cast<int32_t*>(wb + (cap + 1));
-      int32_t* wr = wc + (int64_t)(cap + 1) * K;
-      int32_t* wl = wr + (cap + 1);
-      for (int ch = 0; ch < D.n_chunks; ++ch) {
+      // gs_db: two staging buffers, wave 0 sweeps chunk ch from one while waves 1-15 stage
+      // chunk ch + 1 into the other, so a chunk's global round trip hides behind the previous
+      // sweep (when the LDS left holds two buffers of >= 3 levels; else one buffer, restaged
+      // by the whole workgroup between chunks)
+      const int64_t buf_doubles = (((int64_t)(cap + 1) * (3 * K + 6) + 1) / 2 + 1) & ~int64_t(1);
+      auto stage_chunk = [&](int ch, double* wv, int t0, int nt) {
+        double* wd = wv + (int64_t)(cap + 1) * K;
+        double* wb = wd + (cap + 1);
+        int32_t* wc = reinterpret_cast<int32_t*>(wb + (cap + 1));
+        int32_t* wr = wc + (int64_t)(cap + 1) * K;
+        int32_t* wl = wr + (cap + 1);
         const int l0 = clev[ch], l1 = clev[ch + 1];
         const int P0 = lptr[l0], cnt = lptr[l1] - P0;
-        for (int q = tid; q < cnt * K; q += kBT) {
+        for (int q = t0; q < cnt * K; q += nt) {
           wc[q] = pkc[(int64_t)P0 * K + q];
           wv[q] = pkv[(int64_t)P0 * K + q];
         }
-        for (int q = tid; q < cnt; q += kBT) {
+        for (int q = t0; q < cnt; q += nt) {
           wd[q] = pkd[P0 + q];
           wb[q] = bl[P0 + q];
           wr[q] = pkr[P0 + q];
         }
-        if (tid < K) {  // the dummy position
-          wc[cnt * K + tid] = n;
-          wv[cnt * K + tid] = 0.0;
+        if (t0 < K) {  // the dummy position
+          wc[cnt * K + t0] = n;
+          wv[cnt * K + t0] = 0.0;
         }
-        if (tid == 0) {
+        if (t0 == 0) {
           wd[cnt] = 1.0;
           wb[cnt] = 0.0;
           wr[cnt] = n + 1;
         }
-        for (int q = tid; q <= l1 - l0; q += kBT) wl[q] = lptr[l0 + q] - P0;
-        __syncthreads();
-        if (tid < 64) {
+        for (int q = t0; q <= l1 - l0; q += nt) wl[q] = lptr[l0 + q] - P0;
+      };
+      const bool db = D.gs_db != 0;
+      // half-steps h = 2 ch - 1 (staging of chunk 0), 2 ch (wave 0 sweeps ch; with db, waves
+      // 1-15 stage ch + 1 meanwhile), 2 ch + 1 (without db: waves 1-15 stage ch + 1)
+      for (int h = -1; h < 2 * D.n_chunks; ++h) {
+        const int ch = h < 0 ? -1 : h >> 1;
+        const bool sweep_half = h >= 0 && (h & 1) == 0;
+        const int nx = ch + 1;
+        if (!sweep_half && db && h >= 0) continue;  // uniform: nothing to stage after a sweep
+        double* cur = stage + (db ? (ch & 1) * buf_doubles : 0);
+        if (sweep_half && tid < 64) {
+          const int l0 = clev[ch], l1 = clev[ch + 1];
+          const int cnt = lptr[l1] - lptr[l0];
           if (K == 4 && D.gs_rw == 1)
-            wave_sweep(std::integral_constant<int, 4>(), std::integral_constant<int, 1>(),
+            wave_sweep(std::integral_constant<int, 4>(), std::integral_constant<int, 1>(), cur,
                        l1 - l0, cnt);
           else if (K == 4)
-            wave_sweep(std::integral_constant<int, 4>(), std::integral_constant<int, 2>(),
+            wave_sweep(std::integral_constant<int, 4>(), std::integral_constant<int, 2>(), cur,
                        l1 - l0, cnt);
           else
-            wave_sweep(std::integral_constant<int, 8>(), std::integral_constant<int, 1>(),
+            wave_sweep(std::integral_constant<int, 8>(), std::integral_constant<int, 1>(), cur,
                        l1 - l0, cnt);
+        } else if (nx < D.n_chunks && (sweep_half == db || h < 0) && (tid >= 64 || !db)) {
+          // without db wave 0 is idle here and stages too
+          stage_chunk(nx, stage + (db ? (nx & 1) * buf_doubles : 0), db ? tid - 64 : tid,
+                      db ? kBT - 64 : kBT);
         }
         __syncthreads();
       }
@@ -1029,30 +1152,8 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
     stamp(2);
   };
 
-  int iters = 0;
-  for (int itn = 0; itn < D.max_iter; ++itn) {
-    smooth(D.nu_pre);
-    resid_rows(rs, nullptr);
-    __syncthreads();
-    #pragma unroll 1
-    for (int j0 = tid; j0 < nc; j0 += 2 * kBT) {  // P^T r: csc_matvec's order
-      int rows[2] = {j0, j0 + kBT < nc ? j0 + kBT : -1};
-      double y[2];
-      packed_dot_rows<2>(ptc, ptv, nc, rows, KT, rs, y);
-      rcs[j0] = y[0];
-      if (rows[1] >= 0) rcs[rows[1]] = y[1];
-    }
-    __syncthreads();
-    stamp(3);
-    if (mode == 1) {  // e = L^-T (L^-1 r_H)
-      rows_dot<1>(AH, nc, rcs, ys, tid);
-      __syncthreads();
-      rows_dot<2>(AI, nc, ys, es, tid);
-    } else {  // e = A_H^-1 r_H (Gauss-Jordan inverse)
-      rows_dot<0>(AI, nc, rcs, es, tid);
-    }
-    __syncthreads();
-    stamp(6);
+  // x += P e_H, post-smoothing, err[itn]; true when the tolerance is met
+  auto second_half = [&](int itn) -> bool {
     #pragma unroll 1
     for (int i0 = tid; i0 < n; i0 += 4 * kBT) {  // x += P e
       int rows[4];
@@ -1075,13 +1176,72 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
     }
     const double nrm = sqrt(block_sum(part, redv));
     if (tid == 0) err[itn] = nrm;
-    iters = itn + 1;
-    if (D.tol >= 0.0 && nrm <= D.tol) break;
+    return D.tol >= 0.0 && nrm <= D.tol;
+  };
+
+  if constexpr (PHASED) {
+    const int k = (int)phase;
+    bool fin = D.max_iter == 0;
+    if (k > 0) fin = second_half(k - 1) || k == D.max_iter;
+    if (!fin) {
+      smooth(D.nu_pre);
+      resid_rows(rs, nullptr);
+      __syncthreads();
+      #pragma unroll 1
+      for (int j0 = tid; j0 < nc; j0 += 2 * kBT) {  // P^T r: csc_matvec's order
+        int rows[2] = {j0, j0 + kBT < nc ? j0 + kBT : -1};
+        double y[2];
+        packed_dot_rows<2>(ptc, ptv, nc, rows, KT, rs, y);
+        rcs[j0] = y[0];
+        if (rows[1] >= 0) rcs[rows[1]] = y[1];
+      }
+      __syncthreads();
+      stamp(3);
+    }
+    #pragma unroll 1
+    for (int i = tid; i < n; i += kBT) x_out[i] = xs[i];
+    stamp(3);
+    if (tid == 0) {
+      tstat[7] = phase + 1;
+      if (fin) {
+        stat[0] = k;
+        stat[3] = 1;
+      }
+    }
+    return;
+  } else {
+    int iters = 0;
+    for (int itn = 0; itn < D.max_iter; ++itn) {
+      smooth(D.nu_pre);
+      resid_rows(rs, nullptr);
+      __syncthreads();
+      #pragma unroll 1
+      for (int j0 = tid; j0 < nc; j0 += 2 * kBT) {  // P^T r: csc_matvec's order
+        int rows[2] = {j0, j0 + kBT < nc ? j0 + kBT : -1};
+        double y[2];
+        packed_dot_rows<2>(ptc, ptv, nc, rows, KT, rs, y);
+        rcs[j0] = y[0];
+        if (rows[1] >= 0) rcs[rows[1]] = y[1];
+      }
+      __syncthreads();
+      stamp(3);
+      if (mode == 1) {  // e = L^-T (L^-1 r_H)
+        rows_dot<1>(AH, nc, rcs, ys, tid);
+        __syncthreads();
+        rows_dot<2>(AI, nc, ys, es, tid);
+      } else {  // e = A_H^-1 r_H (Gauss-Jordan inverse)
+        rows_dot<0>(AI, nc, rcs, es, tid);
+      }
+      __syncthreads();
+      stamp(6);
+      iters = itn + 1;
+      if (second_half(itn)) break;
+    }
+    #pragma unroll 1
+    for (int i = tid; i < n; i += kBT) x_out[i] = xs[i];
+    stamp(3);
+    if (tid == 0) stat[0] = iters;
   }
-  #pragma unroll 1
-  for (int i = tid; i < n; i += kBT) x_out[i] = xs[i];
-  stamp(3);
-  if (tid == 0) stat[0] = iters;
 }
 
 struct Layout {
@@ -1213,7 +1373,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     std::vector<double> pkv, pkd, akv, ppv, ptv, blv;  // blv: b in sweep (level) order
     int K = 1, KA = 1, KP = 1, KT = 1, nlev = 0, panel = 8, cap = 0;
     bool spd = false;
-    int chol_nb = 4, gs_rw = 0;
+    int chol_nb = 4, gs_rw = 0, gs_db = 0;
     size_t lds_setup = 0, lds_cycles = 0;
     int code = MLAMG_OK;  // analysis failure: code + message (reported for the first problem)
     std::string err;
@@ -1222,10 +1382,19 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   const auto t_begin = std::chrono::steady_clock::now();
   std::vector<Plan> plans(count);
   std::vector<BDesc> desc(count);
-  // residual in LDS when every problem leaves room for it
+  // a single problem with a large coarse operator: the coarse inverse from the device-wide
+  // factorisation (dense.hip) and phased cycles, the coarse solve on every CU
+  static const int ext_min = [] {
+    const char* e = std::getenv("MLAMG_BATCH_EXT_MIN");
+    return e ? std::atoi(e) : kExtCoarseMin;
+  }();
+  const bool ext_ok = count == 1 && probs[0].n_c > ext_min && !std::getenv("MLAMG_BATCH_NO_EXT");
+  const bool phased = ext_ok && !std::getenv("MLAMG_BATCH_NO_PHASED");
+  // residual in LDS when every problem leaves room for it (phased: r_H, e_H live in the arena)
   bool r_lds = true;
   for (int q = 0; q < count; ++q) {
-    const size_t need = (size_t)probs[q].n * 16 + 16 + (size_t)probs[q].n_c * 16 + 16 * 1024;
+    const size_t need = (size_t)probs[q].n * 16 + 16 + (phased ? 0 : (size_t)probs[q].n_c * 16) +
+                        16 * 1024;
     if (need > kBLdsBytes) r_lds = false;
   }
   Layout lay;
@@ -1284,7 +1453,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     if (spd) L.lds_setup = chol_lds(chol_nb, nc);
     // cycle vectors in LDS: x (+ zero and sink slots), r when it fits (L^-1 r_H shares it), r_H,
     // e_H; the sweep's staging area gets the rest
-    const size_t vec_lds = (size_t)n * 8 * (r_lds ? 2 : 1) + 16 + (size_t)nc * 16;
+    const size_t vec_lds = (size_t)n * 8 * (r_lds ? 2 : 1) + 16 + (phased ? 0 : (size_t)nc * 16);
     const size_t room = kBLdsBytes > vec_lds + 64 ? kBLdsBytes - vec_lds - 64 : 0;
     int gs_rw = 0;
     if (smoother == 0) {
@@ -1324,6 +1493,11 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       if (km == 4 && wmax <= 128) gs_rw = wmax <= 64 ? 1 : 2;
       if (km == 8 && wmax <= 64) gs_rw = 1;
       if (gs_rw && (int)std::min<size_t>(4096, room / (12 * km + 24)) - 1 < wmax) gs_rw = 0;
+      // two staging buffers when each still holds >= 3 of the widest levels
+      static const bool no_db = std::getenv("MLAMG_BATCH_NO_DB") != nullptr;  // A/B knob
+      if (gs_rw && !no_db &&
+          (int)std::min<size_t>(4096, room / (2 * (12 * km + 24) + 16)) - 1 >= 3 * wmax)
+        L.gs_db = 1;
       L.K = gs_rw ? km : std::max(maxoff, 1);
       const int64_t K = L.K;
       L.pkr.resize(n);
@@ -1365,8 +1539,9 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     // after the cycle vectors, one position kept for the one-wave sweep's dummy (a level wider
     // than cap is swept by the workgroup straight from the arena)
     if (smoother == 0) {
-      const size_t per_pos = 12 * (size_t)L.K + 24;
-      L.cap = (int)std::min<size_t>(4096, room / per_pos) - 1;
+      const size_t per_pos = (12 * (size_t)L.K + 24) * (L.gs_db ? 2 : 1);
+      const size_t slack = L.gs_db ? 32 : 0;
+      L.cap = (int)std::min<size_t>(4096, (room > slack ? room - slack : 0) / per_pos) - 1;
       L.clev.push_back(0);
       int l = 0;
       while (l < L.nlev) {
@@ -1380,7 +1555,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       }
     }
     L.lds_setup = std::max(L.lds_setup, setup_lds(pb));
-    L.lds_cycles = vec_lds + 16 + (size_t)(L.cap + 1) * (12 * L.K + 24) + 8;
+    L.lds_cycles = vec_lds + 16 + (size_t)(L.cap + 1) * (12 * L.K + 24) * (L.gs_db ? 2 : 1) + 40;
     L.spd = spd;
     L.chol_nb = chol_nb;
     L.gs_rw = gs_rw;
@@ -1420,6 +1595,8 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     D.spd = L.spd ? 1 : 0;
     D.chol_nb = L.chol_nb;
     D.gs_rw = L.gs_rw;
+    D.gs_db = L.gs_db;
+    D.phased = phased ? 1 : 0;
     D.tol = tol;
     D.omega = jacobi_weight;
     D.ak_col = lay.take(4 * L.akc.size());
@@ -1448,6 +1625,10 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     D.AI = lay.take((size_t)8 * D.nc * D.nc);
     D.rg = lay.take(8 * (size_t)D.n);
     D.dinv = lay.take(8 * (size_t)D.n);
+    if (phased) {
+      D.rcg = lay.take(8 * (size_t)D.nc);
+      D.eg = lay.take(8 * (size_t)D.nc);
+    }
   }
   const size_t out_begin = lay.off;
   for (int q = 0; q < count; ++q) {
@@ -1457,9 +1638,8 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     D.stat_out = lay.take(16 + 8 * 8);
   }
   const size_t total = lay.off;
-  // a single problem with a large coarse operator takes the device-wide coarse factorisation
-  const bool ext_coarse = count == 1 && desc[0].nc > kExtCoarseMin && plans[0].spd &&
-                          !std::getenv("MLAMG_BATCH_NO_EXT");
+  // a single problem with a large SPD coarse operator takes the device-wide coarse factorisation
+  const bool ext_coarse = ext_ok && plans[0].spd;
   if (ext_coarse) desc[0].setup_mode = 1;
   // ---- pack the inputs into pinned host memory, one copy in
   HostPinned& H = g_batch_host;
@@ -1507,6 +1687,10 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   const BDesc* dd = reinterpret_cast<const BDesc*>(arena + desc_off);
   hipLaunchKernelGGL(k_amg2v_setup, dim3((unsigned)count), dim3(kBT), lds_setup, s, dd, arena);
   if (ext_coarse) {
+    const int nc = desc[0].nc;
+    const int R = std::max(1, std::min(64, (int)((size_t)128 * 1024 / (8 * (size_t)nc))));
+    hipLaunchKernelGGL(k_galerkin_rows, dim3((unsigned)((nc + R - 1) / R)), dim3(256),
+                       (size_t)R * nc * 8, s, dd, arena, R);
     // a single call with a large SPD coarse operator: the device-wide inverse Cholesky factor
     // (all CUs) instead of one workgroup's; Gauss-Jordan in the setup kernel when not SPD
     const BDesc& D = desc[0];
@@ -1523,12 +1707,54 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       hipLaunchKernelGGL(k_amg2v_setup, dim3(1), dim3(kBT), lds_setup, s, dd, arena);
     }
   }
-  if (r_lds)
-    hipLaunchKernelGGL(k_amg2v_cycles<true>, dim3((unsigned)count), dim3(kBT), lds_cycles, s,
-                       dd, arena);
-  else
-    hipLaunchKernelGGL(k_amg2v_cycles<false>, dim3((unsigned)count), dim3(kBT), lds_cycles, s,
-                       dd, arena);
+  if (phased) {
+    // cycle k = launches A_k (second half of cycle k - 1, first half of cycle k) and B_k (the
+    // coarse solve); A_max_iter ends it. Every launch after the one that met the tolerance
+    // returns at once; with a tolerance the host queues batches of cycles and reads the done
+    // flag of the batch before the one it just queued, so the GPU never waits for the host.
+    auto launch_a = [&]() {
+      if (r_lds)
+        hipLaunchKernelGGL((k_amg2v_cycles<true, true>), dim3(1), dim3(kBT), lds_cycles, s, dd,
+                           arena);
+      else
+        hipLaunchKernelGGL((k_amg2v_cycles<false, true>), dim3(1), dim3(kBT), lds_cycles, s, dd,
+                           arena);
+    };
+    const unsigned coarse_blocks = (unsigned)((desc[0].nc + 3) / 4);
+    const int total_a = max_iter + 1;
+    static thread_local int32_t* flag_host = nullptr;
+    static thread_local hipEvent_t flag_ev[2] = {nullptr, nullptr};
+    if (!flag_host) {
+      MLAMG_HIP(hipHostMalloc(&flag_host, 2 * sizeof(int32_t), hipHostMallocDefault));
+      for (auto& e : flag_ev) MLAMG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    const int32_t* done_dev = reinterpret_cast<const int32_t*>(arena + desc[0].stat_out) + 3;
+    constexpr int kPhaseBatch = 4;
+    int a = 0;
+    for (int batch = 0; a < total_a; ++batch) {
+      const int na = tol >= 0.0 ? std::min(kPhaseBatch, total_a - a) : total_a - a;
+      for (int q = 0; q < na; ++q, ++a) {
+        launch_a();
+        if (a < max_iter)
+          hipLaunchKernelGGL(k_amg2v_coarse, dim3(coarse_blocks), dim3(256), 0, s, dd, arena);
+      }
+      MLAMG_HIP(hipGetLastError());
+      if (tol < 0.0 || a >= total_a) break;
+      MLAMG_HIP(hipMemcpyAsync(flag_host + (batch & 1), done_dev, sizeof(int32_t),
+                               hipMemcpyDeviceToHost, s));
+      MLAMG_HIP(hipEventRecord(flag_ev[batch & 1], s));
+      if (batch > 0) {
+        MLAMG_HIP(hipEventSynchronize(flag_ev[(batch - 1) & 1]));
+        if (flag_host[(batch - 1) & 1]) break;
+      }
+    }
+  } else if (r_lds) {
+    hipLaunchKernelGGL((k_amg2v_cycles<true, false>), dim3((unsigned)count), dim3(kBT),
+                       lds_cycles, s, dd, arena);
+  } else {
+    hipLaunchKernelGGL((k_amg2v_cycles<false, false>), dim3((unsigned)count), dim3(kBT),
+                       lds_cycles, s, dd, arena);
+  }
   MLAMG_HIP(hipGetLastError());
   // the host staging buffer is reused for the outputs: the copy-in above completed before the
   // kernel (same stream), and the copy-out below is ordered after it

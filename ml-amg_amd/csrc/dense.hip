@@ -156,27 +156,18 @@ __device__ bool panel_factor(const double* __restrict__ M, int64_t n, int64_t k0
   for (int t = 0; t < bw; ++t) {
     const double dtt = Dg[t * ds + t];
     if (!(dtt > 0.0)) return false;
-    const double sq = sqrt(dtt);
-    double nv[E];
-    bool wr[E];
+    // column t: l_rt = a_rt / sqrt(a_tt), one reciprocal per step (a division per element made
+    // this loop the panel launch's whole cost: ~1,000 fp64 divisions per lane)
+    const double sq = sqrt(dtt), isq = 1.0 / sq;
+    if (lane >= t && lane < bw) Dg[lane * ds + t] = lane == t ? sq : Dg[lane * ds + t] * isq;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // trailing block: a_rc -= l_rt l_ct, t < c <= r
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int q = lane + 64 * e, rr = q / kNB, cc = q % kNB;
-      wr[e] = rr < bw && cc <= rr && cc >= t;
-      nv[e] = 0.0;
-      if (wr[e]) {
-        if (cc == t)
-          nv[e] = rr == t ? sq : Dg[rr * ds + t] / sq;
-        else
-          nv[e] = Dg[rr * ds + cc] - (Dg[rr * ds + t] / sq) * (Dg[cc * ds + t] / sq);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int q = lane + 64 * e;
-      if (wr[e]) Dg[(q / kNB) * ds + q % kNB] = nv[e];
+      if (rr < bw && cc <= rr && cc > t)
+        Dg[rr * ds + cc] = Dg[rr * ds + cc] - Dg[rr * ds + t] * Dg[cc * ds + t];
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");

@@ -289,14 +289,15 @@ def _host_problem(A, P, b, x):
 
 
 # Engine choice for engine='auto' (measured on MI355X, profiles/r02/amg2v_timing.json): one
-# workgroup runs a whole fused solve's cycles, so a single call pays its serial sweep levels
-# alone; above n_c = 512 a single call's coarse inverse comes from the device-wide factorisation
-# (csrc/dense.hip) instead of one CU's. It beats the per-operation hierarchy engine up to
-# n_c ~ 1100 (32^2: 1.7 vs 6.1 ms; 64^2, n_c = 484: 5.9 vs 9.3 ms; 96^2, n_c = 1024: 12.4 vs
-# 13.7 ms; 128^2, n_c = 1849: 37.6 vs 20.3 ms — the one-CU dense coarse GEMV per cycle). In a
-# batch the problems run side by side on the CUs, so up to n_c = 1024 the fused launch wins by
-# a wide margin (48 grids 32^2-64^2: 8.8 ms vs 200 ms for 16 threads of the hierarchy engine).
-FUSED_SINGLE_MAX_NC = 1100
+# workgroup runs a whole fused solve's smoothing and transfers, so a single call pays its serial
+# sweep levels alone. Single calls with n_c > 300 factor the coarse operator on the whole GPU
+# (csrc/dense.hip) and run phased cycles, whose coarse solve is spread over every CU. The fused
+# engine then beats the per-operation hierarchy engine at every size the batched solver takes
+# (32^2: 1.8 vs 5.9 ms; 64^2, n_c = 484: 4.1 vs 9.4 ms; 96^2, n_c = 1024: 9.3 vs 13.9 ms;
+# 128^2, n_c = 1849: 19.8 vs 20.4 ms). In a batch the problems run side by side on the CUs, so
+# up to n_c = 1024 the fused launch wins by a wide margin (48 grids 32^2-64^2: 8.8 ms vs 190 ms
+# for 16 threads of the hierarchy engine).
+FUSED_SINGLE_MAX_NC = 2048
 FUSED_BATCH_MAX_NC = 1024
 
 
