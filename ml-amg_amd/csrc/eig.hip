@@ -1,12 +1,16 @@
 // lambda_max(D^-1 A) for the smoothed-aggregation weight omega = (4/3)/lambda_max
 // (ns/lib/multigrid.py:105: ARPACK eigs(Dinv@A, k=1, which='LM')).
 //
-// D^-1 A is similar to the symmetric B = D^-1/2 A D^-1/2 (A symmetric, positive diagonal), so
-// plain Lanczos on B converges to the same extreme eigenvalue. Every iteration is one CSR-stream
-// SpMV (with the D^-1/2 scaling and the Rayleigh dot fused into its epilogue) plus one fused
-// update/norm kernel; alpha_j and beta_j stay on the device and the host only reads them every
-// kCheck iterations to bisect the tridiagonal T_j for its largest eigenvalue. Reductions use a
-// fixed order, so the result is deterministic.
+// D^-1 A is self-adjoint in the D inner product <x, y>_D = x^T D y (A symmetric, positive
+// diagonal), so Lanczos in that inner product converges to its extreme eigenvalue with plain
+// products by A: q_j D-orthonormal, z = A q_j, alpha_j = z . q_j,
+// w = D^-1 z - alpha_j q_j - beta_j q_{j-1}, beta_{j+1} = ||w||_D, q_{j+1} = w / beta_{j+1}.
+// The product z = A q is the operator's own SpMV kernel in whatever format it carries (the C4
+// fine level in the row-pair format: 37 us instead of 250 us for a CSR pass with the scaling
+// fused), the vector work is three streaming kernels and the three Lanczos vectors rotate by
+// pointer. alpha_j and beta_j stay on the device; the host reads them every kCheck iterations
+// to bisect the tridiagonal T_j for its largest eigenvalue. Reductions use a fixed order, so
+// the result is deterministic.
 #include "common.hpp"
 
 #include <cmath>
@@ -28,51 +32,6 @@ __device__ __forceinline__ double block_sum256(double v, double* red) {
   return t;
 }
 
-// w = h .* (A u), partial[b] = sum over the block of w_i * v_i
-__global__ __launch_bounds__(kThreads) void k_lanczos_spmv(
-    const int32_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-    const double* __restrict__ vals, const int32_t* __restrict__ blk,
-    const double* __restrict__ u, const double* __restrict__ h, const double* __restrict__ v,
-    double* __restrict__ w, double* __restrict__ partial) {
-  __shared__ double prod[kBlockNnz];
-  __shared__ int32_t rp[kBlockRows + 1];
-  __shared__ double red[4];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int r0 = blk[b], r1 = blk[b + 1], nr = r1 - r0;
-  const int e0 = indptr[r0], ne = indptr[r1] - e0;
-  double acc = 0.0;
-  if (ne <= kBlockNnz) {
-    for (int t = tid; t <= nr; t += kThreads) rp[t] = indptr[r0 + t] - e0;
-    for (int e = tid; e < ne; e += kThreads) prod[e] = vals[e0 + e] * u[indices[e0 + e]];
-    __syncthreads();
-    for (int t = tid; t < nr; t += kThreads) {
-      double s = 0.0;
-      for (int k = rp[t]; k < rp[t + 1]; ++k) s += prod[k];
-      const int i = r0 + t;
-      const double wi = h[i] * s;
-      w[i] = wi;
-      acc += wi * v[i];
-    }
-  } else {
-    double s = 0.0;
-    for (int c = 0; c < ne; c += kBlockNnz) {
-      const int m = min(kBlockNnz, ne - c);
-      for (int e = tid; e < m; e += kThreads) prod[e] = vals[e0 + c + e] * u[indices[e0 + c + e]];
-      __syncthreads();
-      if (tid == 0)
-        for (int k = 0; k < m; ++k) s += prod[k];
-      __syncthreads();
-    }
-    if (tid == 0) {
-      const double wi = h[r0] * s;
-      w[r0] = wi;
-      acc = wi * v[r0];
-    }
-  }
-  const double t = block_sum256(acc, red);
-  if (tid == 0) partial[b] = t;
-}
-
 __global__ __launch_bounds__(1024) void k_reduce_to(const double* __restrict__ partial, int n,
                                                     double* __restrict__ out, int take_sqrt) {
   __shared__ double red[16];
@@ -88,40 +47,47 @@ __global__ __launch_bounds__(1024) void k_reduce_to(const double* __restrict__ p
   }
 }
 
-// w -= alpha*v + beta*vprev ; partial = sum w^2
-__global__ __launch_bounds__(256) void k_lanczos_update(double* __restrict__ w,
-                                                        const double* __restrict__ v,
-                                                        const double* __restrict__ vprev,
-                                                        const double* __restrict__ alpha,
-                                                        const double* __restrict__ beta,
-                                                        int64_t n, double* __restrict__ partial) {
+// partial[b] = sum over the block's entries of z_i q_i
+__global__ __launch_bounds__(256) void k_lz_dot(const double* __restrict__ z,
+                                                const double* __restrict__ q, int64_t n,
+                                                double* __restrict__ partial) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    acc += z[i] * q[i];
+  const double t = block_sum256(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+// w = D^-1 z - alpha q - beta q_prev ; partial = sum d_i w_i^2 (the D-norm)
+__global__ __launch_bounds__(256) void k_lz_update(const double* __restrict__ z,
+                                                   const double* __restrict__ dinv,
+                                                   const double* __restrict__ d,
+                                                   const double* __restrict__ q,
+                                                   const double* __restrict__ qprev,
+                                                   const double* __restrict__ alpha,
+                                                   const double* __restrict__ beta, int64_t n,
+                                                   double* __restrict__ w,
+                                                   double* __restrict__ partial) {
   __shared__ double red[4];
   const double a = *alpha, bt = *beta;
   double acc = 0.0;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const double wi = (w[i] - a * v[i]) - bt * vprev[i];
+    const double wi = (dinv[i] * z[i] - a * q[i]) - bt * qprev[i];
     w[i] = wi;
-    acc += wi * wi;
+    acc += d[i] * (wi * wi);
   }
   const double t = block_sum256(acc, red);
   if (threadIdx.x == 0) partial[blockIdx.x] = t;
 }
 
-// vprev <- v ; v <- w / beta ; u <- h .* v
-__global__ __launch_bounds__(256) void k_lanczos_next(double* __restrict__ vprev,
-                                                      double* __restrict__ v,
-                                                      const double* __restrict__ w,
-                                                      const double* __restrict__ h,
-                                                      double* __restrict__ u,
-                                                      const double* __restrict__ beta, int64_t n) {
+// w <- w / beta (beta = 0: breakdown, w = 0)
+__global__ __launch_bounds__(256) void k_lz_scale(double* __restrict__ w,
+                                                  const double* __restrict__ beta, int64_t n) {
   const double bt = *beta;
   const double inv = bt > 0.0 ? 1.0 / bt : 0.0;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    vprev[i] = v[i];
-    const double vi = w[i] * inv;
-    v[i] = vi;
-    u[i] = h[i] * vi;
-  }
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    w[i] = w[i] * inv;
 }
 
 __device__ __forceinline__ uint64_t splitmix(uint64_t x) {
@@ -131,25 +97,26 @@ __device__ __forceinline__ uint64_t splitmix(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-// h_i = 1/sqrt(a_ii); v = random; partial = sum v^2
-__global__ __launch_bounds__(256) void k_lanczos_init(const int32_t* __restrict__ indptr,
-                                                      const int32_t* __restrict__ indices,
-                                                      const double* __restrict__ vals,
-                                                      int64_t n, uint64_t seed,
-                                                      double* __restrict__ h,
-                                                      double* __restrict__ w,
-                                                      double* __restrict__ partial) {
+// d_i = a_ii (sum of the stored diagonal entries), dinv = 1/d; q = random; partial = sum d q^2
+__global__ __launch_bounds__(256) void k_lz_init(const int32_t* __restrict__ indptr,
+                                                 const int32_t* __restrict__ indices,
+                                                 const double* __restrict__ vals, int64_t n,
+                                                 uint64_t seed, double* __restrict__ d,
+                                                 double* __restrict__ dinv,
+                                                 double* __restrict__ q,
+                                                 double* __restrict__ partial) {
   __shared__ double red[4];
   double acc = 0.0;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    double d = 0.0;
+    double di = 0.0;
     for (int k = indptr[i]; k < indptr[i + 1]; ++k)
-      if (indices[k] == (int32_t)i) d += vals[k];
-    h[i] = 1.0 / sqrt(d);
+      if (indices[k] == (int32_t)i) di += vals[k];
+    d[i] = di;
+    dinv[i] = 1.0 / di;
     const uint64_t r = splitmix(seed * 0x100000001B3ull + (uint64_t)i);
     const double x = (double)(r >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
-    w[i] = x;
-    acc += x * x;
+    q[i] = x;
+    acc += di * (x * x);
   }
   const double t = block_sum256(acc, red);
   if (threadIdx.x == 0) partial[blockIdx.x] = t;
@@ -203,30 +170,27 @@ extern "C" int mlamg_lambda_max_dinvA(const mlamg_csr* A, int max_iter, double t
     return MLAMG_OK;
   }
   const int nbv = (int)std::min<int64_t>(1024, (n + 255) / 256);
-  const int npart = std::max<int>(A->n_blocks, nbv);
   const int m_max = (int)std::min<int64_t>(max_iter, n);
-  double *h, *u, *v, *vprev, *w, *partial, *alpha, *beta;
-  MLAMG_HIP(hipMalloc(&h, sizeof(double) * n * 5 + sizeof(double) * (npart + 2 * (m_max + 2))));
-  u = h + n;
-  v = u + n;
-  vprev = v + n;
-  w = vprev + n;
-  partial = w + n;
-  alpha = partial + npart;
-  beta = alpha + (m_max + 2);
+  double* base = nullptr;
+  MLAMG_HIP(hipMalloc(&base, sizeof(double) * (n * 6 + nbv + 2 * (m_max + 2) + 1)));
   struct Free {
     double* p;
     ~Free() { (void)hipFree(p); }
-  } guard{h};
-  MLAMG_HIP(hipMemsetAsync(vprev, 0, sizeof(double) * n, s));
+  } guard{base};
+  double* z = base;
+  double* d = z + n;
+  double* dinv = d + n;
+  double* Q[3] = {dinv + n, dinv + 2 * n, dinv + 3 * n};  // q_prev, q, w
+  double* partial = dinv + 4 * n;
+  double* alpha = partial + nbv;
+  double* beta = alpha + (m_max + 2);
+  double* nrm0 = beta + (m_max + 2);
+  MLAMG_HIP(hipMemsetAsync(Q[0], 0, sizeof(double) * n, s));
   MLAMG_HIP(hipMemsetAsync(beta, 0, sizeof(double) * (m_max + 2), s));
-  hipLaunchKernelGGL(k_lanczos_init, dim3(nbv), dim3(256), 0, s, A->indptr, A->indices, A->data,
-                     n, seed, h, w, partial);
-  hipLaunchKernelGGL(k_reduce_to, dim3(1), dim3(1024), 0, s, partial, nbv, beta + 0, 1);
-  // v1 = w / ||w||  (beta[0] is reset to 0 after use)
-  hipLaunchKernelGGL(k_lanczos_next, dim3(nbv), dim3(256), 0, s, vprev, v, w, h, u, beta + 0, n);
-  MLAMG_HIP(hipMemsetAsync(vprev, 0, sizeof(double) * n, s));
-  MLAMG_HIP(hipMemsetAsync(beta, 0, sizeof(double), s));
+  hipLaunchKernelGGL(k_lz_init, dim3(nbv), dim3(256), 0, s, A->indptr, A->indices, A->data, n,
+                     seed, d, dinv, Q[1], partial);
+  hipLaunchKernelGGL(k_reduce_to, dim3(1), dim3(1024), 0, s, partial, nbv, nrm0, 1);
+  hipLaunchKernelGGL(k_lz_scale, dim3(nbv), dim3(256), 0, s, Q[1], nrm0, n);
   MLAMG_HIP(hipGetLastError());
 
   const int kCheck = 32;
@@ -237,16 +201,18 @@ extern "C" int mlamg_lambda_max_dinvA(const mlamg_csr* A, int max_iter, double t
   while (!done) {
     const int jend = std::min(m_max, j + kCheck);
     for (; j < jend; ++j) {
-      hipLaunchKernelGGL(k_lanczos_spmv, dim3(A->n_blocks), dim3(kThreads), 0, s, A->indptr,
-                         A->indices, A->data, A->blk, u, h, v, w, partial);
-      hipLaunchKernelGGL(k_reduce_to, dim3(1), dim3(1024), 0, s, partial, A->n_blocks, alpha + j,
-                         0);
-      // beta[j] couples v_j and v_{j-1}; beta[j+1] is the new norm
-      hipLaunchKernelGGL(k_lanczos_update, dim3(nbv), dim3(256), 0, s, w, v, vprev, alpha + j,
-                         beta + j, n, partial);
+      MLAMG_TRY(launch_spmv_plain(A, Q[1], z, s));
+      hipLaunchKernelGGL(k_lz_dot, dim3(nbv), dim3(256), 0, s, z, Q[1], n, partial);
+      hipLaunchKernelGGL(k_reduce_to, dim3(1), dim3(1024), 0, s, partial, nbv, alpha + j, 0);
+      // beta[j] couples q_j and q_{j-1}; beta[j+1] is the new norm
+      hipLaunchKernelGGL(k_lz_update, dim3(nbv), dim3(256), 0, s, z, dinv, d, Q[1], Q[0],
+                         alpha + j, beta + j, n, Q[2], partial);
       hipLaunchKernelGGL(k_reduce_to, dim3(1), dim3(1024), 0, s, partial, nbv, beta + j + 1, 1);
-      hipLaunchKernelGGL(k_lanczos_next, dim3(nbv), dim3(256), 0, s, vprev, v, w, h, u,
-                         beta + j + 1, n);
+      hipLaunchKernelGGL(k_lz_scale, dim3(nbv), dim3(256), 0, s, Q[2], beta + j + 1, n);
+      double* old = Q[0];  // q_prev <- q, q <- w, w <- (old q_prev)
+      Q[0] = Q[1];
+      Q[1] = Q[2];
+      Q[2] = old;
     }
     MLAMG_HIP(hipGetLastError());
     MLAMG_HIP(hipMemcpyAsync(ha.data(), alpha, sizeof(double) * j, hipMemcpyDeviceToHost, s));

@@ -292,6 +292,14 @@ class Hierarchy:
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             if P_given is None or jacobi_weight == "sa":
+                if lvl == 0 and fine_format in ("autotune", "rowpat"):
+                    # Lanczos runs on the operator's own SpMV: a constant stencil gets its
+                    # row-pair format now (the autotune below reuses or replaces it)
+                    try:
+                        A_dev.set_format("rowpat")
+                    except _lib.MlamgError as e:
+                        if e.code != _lib.MLAMG_EUNSUPPORTED:
+                            raise
                 L.lam, L.lanczos_iters = lambda_max_dinv_a(A_dev, max_iter=lanczos_iter,
                                                            tol=lanczos_tol)
                 L.omega = (4.0 / 3.0) / abs(L.lam)
