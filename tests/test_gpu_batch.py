@@ -24,8 +24,9 @@ def _problems(ml, oracle, count):
 
 @pytest.mark.parametrize("smoother", ("gauss_seidel", "jacobi"))
 def test_batch_equals_sequential(oracle, smoother, monkeypatch):
-    # single calls with n_c > 512 factor the coarse operator device-wide (own roundings, see
-    # test_fused_single_device_wide_coarse); here both sides take the one-workgroup factor
+    # single calls with n_c > 300 factor the coarse operator device-wide and run phased cycles
+    # (own roundings, see test_fused_single_device_wide_coarse); here both sides take the
+    # one-workgroup path
     monkeypatch.setenv("MLAMG_BATCH_NO_EXT", "1")
     import torch
     if not torch.cuda.is_available():
@@ -225,7 +226,7 @@ def test_fused_wide_coarse(oracle, monkeypatch):
 
 @pytest.mark.parametrize("m,agg", ((48, 2), (96, 3)))
 def test_fused_single_device_wide_coarse(oracle, monkeypatch, m, agg):
-    """A single fused call with n_c > 512 (576, 1024) builds its coarse inverse with the
+    """A single fused call with n_c > 300 (576, 1024) builds its coarse inverse with the
     device-wide inverse Cholesky factor (csrc/dense.hip) instead of one workgroup's: same
     iteration count and histories as the one-workgroup factor and the oracle (SuperLU) to
     rounding (rtol 1e-10), iterates within 1e-9 of their max."""
@@ -250,3 +251,52 @@ def test_fused_single_device_wide_coarse(oracle, monkeypatch, m, agg):
         assert np.allclose(e, er, rtol=1e-10, atol=0)
     scale = np.abs(xr).max()
     assert np.abs(xe - xr).max() <= 1e-9 * scale and np.abs(xe - xw).max() <= 1e-9 * scale
+
+
+def test_fused_phased_edge_cases(oracle):
+    """The phased single-call path (n_c > 300: device-wide Galerkin and factor, cycles split
+    into workgroup half-cycles and an all-CU coarse solve) on the edge cases of the one-launch
+    path: a singular Galerkin operator (the reference's early return), max_iter 0 / 1 / 2, rows
+    with a zero diagonal (not SPD: the Gauss-Jordan setup is relaunched), and a non-symmetric
+    operator (no device-wide factor; Gauss-Jordan in the setup kernel)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import scipy.sparse as sp
+    import mlamg.multigrid
+    import mlamg.problems
+    import mlamg as ml
+    m = 40
+    A = ml.problems.poisson_2d_5pt(m)
+    Agg = ml.problems.box_aggregates_2d(m, m, 2)
+    assert Agg.shape[1] > 300
+    x0 = np.random.RandomState(4).randn(A.shape[0])
+    z = np.zeros(A.shape[0])
+    # singular: an empty coarse column
+    Ps = sp.hstack([sp.csr_matrix(Agg, dtype=np.float64), sp.csr_matrix((A.shape[0], 1))]).tocsr()
+    x, c, e, it = ml.multigrid.amg_2_v(A, Ps, z, x0, res_tol=1e-10, engine="fused")
+    assert (it, c) == (0, 1.0) and np.array_equal(x, x0) and not np.any(e)
+    P, _ = oracle.smoothed_aggregation_jacobi(A, Agg, omega=2.0 / 3.0)
+    for mi in (0, 1, 2):
+        got = ml.multigrid.amg_2_v(A, P, z, x0, res_tol=1e-300, max_iter=mi, engine="fused")
+        ref = oracle.amg_2_v(A, P, z, x0, res_tol=1e-300, max_iter=mi)
+        assert got[3] == ref[3] == mi and len(got[2]) == mi
+        assert np.allclose(got[2], ref[2], rtol=1e-10, atol=0)
+        assert np.abs(got[0] - ref[0]).max() <= 1e-9 * np.abs(ref[0]).max()
+    # zero diagonal rows (A_H no longer SPD in floating point: relaunched Gauss-Jordan)
+    Az = A.copy()
+    for i in (0, 55, 777, A.shape[0] - 1):
+        lo, hi = Az.indptr[i], Az.indptr[i + 1]
+        Az.data[lo + np.flatnonzero(Az.indices[lo:hi] == i)] = 0.0
+    b = np.random.RandomState(5).randn(A.shape[0])
+    # a non-symmetric operator (host check: no device-wide factor at all)
+    An = A.copy().tolil()
+    An[3, 4] = -1.5
+    An = An.tocsr()
+    for M in (Az, An):
+        xr, cr, er, ir = oracle.amg_2_v(M, P, b, x0, res_tol=1e-300, max_iter=6)
+        xf, cf, ef, itf = ml.multigrid.amg_2_v(M, P, b, x0, res_tol=1e-300, max_iter=6,
+                                               engine="fused")
+        assert itf == ir == 6
+        assert np.allclose(ef, er, rtol=1e-10, atol=0), (ef, er)
+        assert np.abs(xf - xr).max() <= 1e-9 * np.abs(xr).max()
