@@ -118,19 +118,19 @@ __global__ __launch_bounds__(256) void k_gemv(const double* __restrict__ M, int6
   const double* r = M + row * n;
   double s = 0.0;
   // same order as a plain lane-strided loop, with 8 row/b loads of a lane in flight at once (the
-  // loop is otherwise a chain of dependent memory round trips: ~10 us for n = 1008)
-  int64_t j = lane;
-  for (; j + 7 * 64 < n; j += 8 * 64) {
+  // loop is otherwise a chain of dependent memory round trips: ~10 us for n = 1008); the tail
+  // is one more predicated batch (a past-the-end slot adds 0 * 0), not a dependent loop
+  for (int64_t j = lane; j < n; j += 8 * 64) {
     double m[8], v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      m[u] = r[j + u * 64];
-      v[u] = b[j + u * 64];
+      const int64_t k = j + u * 64;
+      m[u] = k < n ? r[k] : 0.0;
+      v[u] = k < n ? b[k] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += m[u] * v[u];
   }
-  for (; j < n; j += 64) s += r[j] * b[j];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   if (lane == 0) x[row] = s;
