@@ -68,6 +68,7 @@ struct BDesc {
   int32_t gs_rw;  // one-wave sweep (rows of K = 4 or 8 slots, levels <= 64 * gs_rw rows), 1 or 2
                   // rows per lane; 0: the workgroup sweeps each level
   int32_t gs_db;   // one-wave sweep: double-buffered chunk staging (chunks of >= 3 levels)
+  int32_t gs_rp;   // one-wave sweep, one buffer: the next chunk prefetched into registers
   int32_t phased;  // single large problem: each cycle is two launches, the workgroup's half
                    // cycles and the coarse solve on every CU (k_amg2v_coarse); r_H, e_H global
   double tol, omega;
@@ -820,7 +821,9 @@ __global__ __launch_bounds__(256) void k_amg2v_coarse(const BDesc* __restrict__ 
 // k_amg2v_coarse, post-smoothing, norm, tolerance test) and the first half of cycle k
 // (pre-smoothing, residual, r_H = P^T r), x kept in x_out between launches; stat[3] = done,
 // tstat[7] = launches so far
-template <bool R_LDS, bool PHASED>
+// RP: the one-wave sweep's register-prefetched staging (gs_rp), instantiated for single phased
+// problems only (its registers would otherwise add spills to every other variant)
+template <bool R_LDS, bool PHASED, bool RP>
 __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ descs,
                                                       char* __restrict__ arena) {
   extern __shared__ double lds[];
@@ -1066,8 +1069,15 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
         for (int q = t0; q <= l1 - l0; q += nt) wl[q] = lptr[l0 + q] - P0;
       };
       const bool db = D.gs_db != 0;
+      constexpr bool rp = RP;
+      // gs_rp (one buffer, chunks of <= 959 positions and <= 1920 slots): waves 1-15 load chunk
+      // ch + 1 into registers while wave 0 sweeps ch, and write it into the buffer after the
+      // sweep's barrier, so only an LDS copy separates two sweeps
+      int rg_c[2] = {0, 0}, rg_r = 0, rg_l = 0;
+      double rg_v[2] = {0.0, 0.0}, rg_d = 0.0, rg_b = 0.0;
       // half-steps h = 2 ch - 1 (staging of chunk 0), 2 ch (wave 0 sweeps ch; with db, waves
-      // 1-15 stage ch + 1 meanwhile), 2 ch + 1 (without db: waves 1-15 stage ch + 1)
+      // 1-15 stage ch + 1 meanwhile; with rp they load it), 2 ch + 1 (without db: waves 1-15
+      // stage ch + 1, with rp from their registers)
       for (int h = -1; h < 2 * D.n_chunks; ++h) {
         const int ch = h < 0 ? -1 : h >> 1;
         const bool sweep_half = h >= 0 && (h & 1) == 0;
@@ -1086,10 +1096,62 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
           else
             wave_sweep(std::integral_constant<int, 8>(), std::integral_constant<int, 1>(), cur,
                        l1 - l0, cnt);
-        } else if (nx < D.n_chunks && (sweep_half == db || h < 0) && (tid >= 64 || !db)) {
+        } else if (RP && h >= 0 && nx < D.n_chunks && tid >= 64) {
+          const int t0 = tid - 64;
+          const int l0 = clev[nx], l1 = clev[nx + 1];
+          const int P0 = lptr[l0], cnt = lptr[l1] - P0;
+          if (sweep_half) {  // global -> registers, under the sweep
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int q = t0 + u * (kBT - 64);
+              if (q < cnt * K) {
+                rg_c[u] = pkc[(int64_t)P0 * K + q];
+                rg_v[u] = pkv[(int64_t)P0 * K + q];
+              }
+            }
+            if (t0 < cnt) {
+              rg_d = pkd[P0 + t0];
+              rg_b = bl[P0 + t0];
+              rg_r = pkr[P0 + t0];
+            }
+            if (t0 <= l1 - l0) rg_l = lptr[l0 + t0] - P0;
+          } else {  // registers -> the buffer (the sweep of ch is done)
+            double* wv = stage;
+            double* wd = wv + (int64_t)(cap + 1) * K;
+            double* wb = wd + (cap + 1);
+            int32_t* wc = reinterpret_cast<int32_t*>(wb + (cap + 1));
+            int32_t* wr = wc + (int64_t)(cap + 1) * K;
+            int32_t* wl = wr + (cap + 1);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int q = t0 + u * (kBT - 64);
+              if (q < cnt * K) {
+                wc[q] = rg_c[u];
+                wv[q] = rg_v[u];
+              }
+            }
+            if (t0 < cnt) {
+              wd[t0] = rg_d;
+              wb[t0] = rg_b;
+              wr[t0] = rg_r;
+            }
+            if (t0 <= l1 - l0) wl[t0] = rg_l;
+            if (t0 < K) {  // the dummy position
+              wc[cnt * K + t0] = n;
+              wv[cnt * K + t0] = 0.0;
+            }
+            if (t0 == 0) {
+              wd[cnt] = 1.0;
+              wb[cnt] = 0.0;
+              wr[cnt] = n + 1;
+            }
+          }
+        } else if (!rp && nx < D.n_chunks && (sweep_half == db || h < 0) && (tid >= 64 || !db)) {
           // without db wave 0 is idle here and stages too
           stage_chunk(nx, stage + (db ? (nx & 1) * buf_doubles : 0), db ? tid - 64 : tid,
                       db ? kBT - 64 : kBT);
+        } else if (rp && h < 0) {
+          stage_chunk(0, stage, tid, kBT);
         }
         __syncthreads();
       }
@@ -1373,7 +1435,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     std::vector<double> pkv, pkd, akv, ppv, ptv, blv;  // blv: b in sweep (level) order
     int K = 1, KA = 1, KP = 1, KT = 1, nlev = 0, panel = 8, cap = 0;
     bool spd = false;
-    int chol_nb = 4, gs_rw = 0, gs_db = 0;
+    int chol_nb = 4, gs_rw = 0, gs_db = 0, gs_rp = 0;
     size_t lds_setup = 0, lds_cycles = 0;
     int code = MLAMG_OK;  // analysis failure: code + message (reported for the first problem)
     std::string err;
@@ -1554,6 +1616,10 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
         L.clev.push_back(l);
       }
     }
+    static const bool no_rp = std::getenv("MLAMG_BATCH_NO_RP") != nullptr;  // A/B knob
+    if (phased && gs_rw && !L.gs_db && !no_rp && L.cap + 1 <= kBT - 64 &&
+        L.cap * L.K <= 2 * (kBT - 64))
+      L.gs_rp = 1;
     L.lds_setup = std::max(L.lds_setup, setup_lds(pb));
     L.lds_cycles = vec_lds + 16 + (size_t)(L.cap + 1) * (12 * L.K + 24) * (L.gs_db ? 2 : 1) + 40;
     L.spd = spd;
@@ -1596,6 +1662,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     D.chol_nb = L.chol_nb;
     D.gs_rw = L.gs_rw;
     D.gs_db = L.gs_db;
+    D.gs_rp = L.gs_rp;
     D.phased = phased ? 1 : 0;
     D.tol = tol;
     D.omega = jacobi_weight;
@@ -1712,13 +1779,20 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     // coarse solve); A_max_iter ends it. Every launch after the one that met the tolerance
     // returns at once; with a tolerance the host queues batches of cycles and reads the done
     // flag of the batch before the one it just queued, so the GPU never waits for the host.
+    const bool rp = desc[0].gs_rp != 0;
     auto launch_a = [&]() {
-      if (r_lds)
-        hipLaunchKernelGGL((k_amg2v_cycles<true, true>), dim3(1), dim3(kBT), lds_cycles, s, dd,
-                           arena);
+      if (r_lds && rp)
+        hipLaunchKernelGGL((k_amg2v_cycles<true, true, true>), dim3(1), dim3(kBT), lds_cycles, s,
+                           dd, arena);
+      else if (r_lds)
+        hipLaunchKernelGGL((k_amg2v_cycles<true, true, false>), dim3(1), dim3(kBT), lds_cycles, s,
+                           dd, arena);
+      else if (rp)
+        hipLaunchKernelGGL((k_amg2v_cycles<false, true, true>), dim3(1), dim3(kBT), lds_cycles,
+                           s, dd, arena);
       else
-        hipLaunchKernelGGL((k_amg2v_cycles<false, true>), dim3(1), dim3(kBT), lds_cycles, s, dd,
-                           arena);
+        hipLaunchKernelGGL((k_amg2v_cycles<false, true, false>), dim3(1), dim3(kBT), lds_cycles,
+                           s, dd, arena);
     };
     const unsigned coarse_blocks = (unsigned)((desc[0].nc + 3) / 4);
     const int total_a = max_iter + 1;
@@ -1749,10 +1823,10 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       }
     }
   } else if (r_lds) {
-    hipLaunchKernelGGL((k_amg2v_cycles<true, false>), dim3((unsigned)count), dim3(kBT),
+    hipLaunchKernelGGL((k_amg2v_cycles<true, false, false>), dim3((unsigned)count), dim3(kBT),
                        lds_cycles, s, dd, arena);
   } else {
-    hipLaunchKernelGGL((k_amg2v_cycles<false, false>), dim3((unsigned)count), dim3(kBT),
+    hipLaunchKernelGGL((k_amg2v_cycles<false, false, false>), dim3((unsigned)count), dim3(kBT),
                        lds_cycles, s, dd, arena);
   }
   MLAMG_HIP(hipGetLastError());
