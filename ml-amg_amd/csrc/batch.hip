@@ -81,7 +81,8 @@ struct BDesc {
   int64_t AH, AI, rg, dinv;                // Galerkin / un-pivoted inverse / r when not in
                                            // LDS / weighted-Jacobi weights
   int64_t x_out, err_out, stat_out;
-  int64_t rcg, eg;  // phased: r_H and e_H in the arena
+  int64_t rcg, eg, yg;  // phased: r_H, e_H and L^-1 r_H in the arena
+  int64_t done_ctr;     // phased: problems finished (one counter for the launch)
 };
 
 template <class T>
@@ -786,34 +787,51 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
   }
 }
 
-// e_H = A_H^-1 r_H of a phased problem on every CU: a wave per row, the order and operations of
-// rows_dot<0> (lane l sums columns l, l + 64, ... with fma, then the butterfly), so the result
-// is the one-workgroup cycle's bit for bit
+// The coarse solve of phased problems on every CU, a wave per row; block b belongs to problem q
+// with cblk[q] <= b < cblk[q + 1]. Each row is the one-workgroup rows_dot's: lane l sums the
+// columns l, l + 64, ... of its span with fma (masked slots add 0 * x), then the butterfly, so
+// the result is the one-workgroup cycle's bit for bit.
+//   PH 1: mode 0 (full inverse in AI): e_H = A_H^-1 r_H; mode 1: y = L^-1 r_H (AH's rows, [0, j])
+//   PH 2: mode 1 only: e_H = L^-T y (AI's rows, [j, n_c))
+template <int PH>
 __global__ __launch_bounds__(256) void k_amg2v_coarse(const BDesc* __restrict__ descs,
-                                                      char* __restrict__ arena) {
-  const BDesc D = descs[0];
-  const int32_t* stat = at<int32_t>(arena, D.stat_out);
+                                                      char* __restrict__ arena,
+                                                      const int32_t* __restrict__ cblk,
+                                                      int count) {
+  int lo = 0, hi = count;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (cblk[mid] <= (int)blockIdx.x) lo = mid;
+    else hi = mid;
+  }
+  const BDesc* D = descs + lo;
+  const int32_t* stat = at<int32_t>(arena, D->stat_out);
   if (stat[3]) return;
-  const int nc = D.nc;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int mode = stat[2];
+  if (PH == 2 && mode != 1) return;
+  const int nc = D->nc;
+  const int row = ((int)blockIdx.x - cblk[lo]) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= nc) return;
-  const double* __restrict__ M = at<double>(arena, D.AI) + (int64_t)row * nc;
-  const double* __restrict__ v = at<double>(arena, D.rcg);
-  // rows_dot's steps of 4 x 64 columns, zero-padded past nc exactly as there (fma(0, 0, s))
+  const bool tri = mode == 1;
+  const double* __restrict__ M =
+      at<double>(arena, PH == 1 && tri ? D->AH : D->AI) + (int64_t)row * nc;
+  const double* __restrict__ v = at<double>(arena, PH == 1 ? D->rcg : D->yg);
+  double* out = at<double>(arena, PH == 1 && tri ? D->yg : D->eg);
+  const int k0 = PH == 2 ? row : 0, k1 = PH == 1 && tri ? row + 1 : nc;
   double s = 0.0;
-  for (int o = 0; o < nc; o += 4 * 64) {
+  for (int o = k0 & ~63; o < k1; o += 4 * 64) {
     double m[4], x[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int k = o + u * 64 + lane;
-      m[u] = k < nc ? M[k] : 0.0;
+      m[u] = (k >= k0 && k < k1) ? M[k] : 0.0;
       x[u] = k < nc ? v[k] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) s = fma(m[u], x[u], s);
   }
   s = bw_sum(s);
-  if (lane == 0) at<double>(arena, D.eg)[row] = s;
+  if (lane == 0) out[row] = s;
 }
 
 // one workgroup per problem: the cycles (reads the setup kernel's inverse and status).
@@ -894,6 +912,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
     if (tid == 0) {
       stat[0] = 0;
       stat[3] = 1;
+      if (PHASED) atomicAdd(at<int32_t>(arena, D.done_ctr), 1);
     }
     return;
   }
@@ -1268,6 +1287,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
       if (fin) {
         stat[0] = k;
         stat[3] = 1;
+        atomicAdd(at<int32_t>(arena, D.done_ctr), 1);
       }
     }
     return;
@@ -1451,7 +1471,14 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     return e ? std::atoi(e) : kExtCoarseMin;
   }();
   const bool ext_ok = count == 1 && probs[0].n_c > ext_min && !std::getenv("MLAMG_BATCH_NO_EXT");
-  const bool phased = ext_ok && !std::getenv("MLAMG_BATCH_NO_PHASED");
+  // batches whose largest coarse operator is above the same size run phased too (each problem's
+  // cycles on its workgroup, every problem's coarse solve spread over the CUs); their coarse
+  // inverses stay the one-workgroup factors, so a batch's results equal the non-phased launch's
+  int64_t max_nc = 0;
+  for (int q = 0; q < count; ++q) max_nc = std::max<int64_t>(max_nc, probs[q].n_c);
+  const bool phased_batch = count > 1 && max_nc > ext_min && !std::getenv("MLAMG_BATCH_NO_EXT") &&
+                            !std::getenv("MLAMG_BATCH_NO_PHASED_BATCH");
+  const bool phased = (ext_ok || phased_batch) && !std::getenv("MLAMG_BATCH_NO_PHASED");
   // residual in LDS when every problem leaves room for it (phased: r_H, e_H live in the arena)
   bool r_lds = true;
   for (int q = 0; q < count; ++q) {
@@ -1617,7 +1644,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       }
     }
     static const bool no_rp = std::getenv("MLAMG_BATCH_NO_RP") != nullptr;  // A/B knob
-    if (phased && gs_rw && !L.gs_db && !no_rp && L.cap + 1 <= kBT - 64 &&
+    if (phased && count == 1 && gs_rw && !L.gs_db && !no_rp && L.cap + 1 <= kBT - 64 &&
         L.cap * L.K <= 2 * (kBT - 64))
       L.gs_rp = 1;
     L.lds_setup = std::max(L.lds_setup, setup_lds(pb));
@@ -1683,6 +1710,10 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     D.x0 = lay.take(8 * n);
   }
 #undef REQ
+  // phased: each problem's first coarse-solve block (k_amg2v_coarse), a row per wave
+  const int64_t cblk_off = phased ? lay.take(4 * (size_t)(count + 1)) : 0;
+  std::vector<int32_t> cblk(count + 1, 0);
+  for (int q = 0; q < count; ++q) cblk[q + 1] = cblk[q] + (int32_t)((desc[q].nc + 3) / 4);
   MLAMG_REQUIRE(lds_setup <= kBLdsBytes + 1024 && lds_cycles <= kBLdsBytes + 1024,
                 "LDS budget exceeded");
   const size_t in_bytes = lay.off;
@@ -1695,8 +1726,11 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     if (phased) {
       D.rcg = lay.take(8 * (size_t)D.nc);
       D.eg = lay.take(8 * (size_t)D.nc);
+      D.yg = lay.take(8 * (size_t)D.nc);
     }
   }
+  const int64_t done_off = phased ? lay.take(sizeof(int32_t)) : 0;
+  for (int q = 0; q < count; ++q) desc[q].done_ctr = done_off;
   const size_t out_begin = lay.off;
   for (int q = 0; q < count; ++q) {
     BDesc& D = desc[q];
@@ -1722,6 +1756,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   char* hb = static_cast<char*>(H.p);
   const auto t_pinned = std::chrono::steady_clock::now();
   std::memcpy(hb + desc_off, desc.data(), sizeof(BDesc) * count);
+  if (phased) std::memcpy(hb + cblk_off, cblk.data(), 4 * (size_t)(count + 1));
   auto put = [&](int64_t off, const void* src, size_t bytes) {
     if (bytes) std::memcpy(hb + off, src, bytes);
   };
@@ -1779,22 +1814,28 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     // coarse solve); A_max_iter ends it. Every launch after the one that met the tolerance
     // returns at once; with a tolerance the host queues batches of cycles and reads the done
     // flag of the batch before the one it just queued, so the GPU never waits for the host.
-    const bool rp = desc[0].gs_rp != 0;
+    const bool rp = count == 1 && desc[0].gs_rp != 0;
+    const dim3 ga((unsigned)count);
     auto launch_a = [&]() {
       if (r_lds && rp)
-        hipLaunchKernelGGL((k_amg2v_cycles<true, true, true>), dim3(1), dim3(kBT), lds_cycles, s,
-                           dd, arena);
+        hipLaunchKernelGGL((k_amg2v_cycles<true, true, true>), ga, dim3(kBT), lds_cycles, s, dd,
+                           arena);
       else if (r_lds)
-        hipLaunchKernelGGL((k_amg2v_cycles<true, true, false>), dim3(1), dim3(kBT), lds_cycles, s,
-                           dd, arena);
+        hipLaunchKernelGGL((k_amg2v_cycles<true, true, false>), ga, dim3(kBT), lds_cycles, s, dd,
+                           arena);
       else if (rp)
-        hipLaunchKernelGGL((k_amg2v_cycles<false, true, true>), dim3(1), dim3(kBT), lds_cycles,
-                           s, dd, arena);
+        hipLaunchKernelGGL((k_amg2v_cycles<false, true, true>), ga, dim3(kBT), lds_cycles, s,
+                           dd, arena);
       else
-        hipLaunchKernelGGL((k_amg2v_cycles<false, true, false>), dim3(1), dim3(kBT), lds_cycles,
-                           s, dd, arena);
+        hipLaunchKernelGGL((k_amg2v_cycles<false, true, false>), ga, dim3(kBT), lds_cycles, s,
+                           dd, arena);
     };
-    const unsigned coarse_blocks = (unsigned)((desc[0].nc + 3) / 4);
+    const unsigned coarse_blocks = (unsigned)cblk[count];
+    const int32_t* cb = reinterpret_cast<const int32_t*>(arena + cblk_off);
+    // mode-1 problems (one-workgroup inverse Cholesky factor) need the second, L^-T, pass
+    bool two_pass = false;
+    for (int q = 0; q < count; ++q) two_pass = two_pass || (plans[q].spd && !ext_coarse);
+    MLAMG_HIP(hipMemsetAsync(arena + done_off, 0, sizeof(int32_t), s));
     const int total_a = max_iter + 1;
     static thread_local int32_t* flag_host = nullptr;
     static thread_local hipEvent_t flag_ev[2] = {nullptr, nullptr};
@@ -1802,15 +1843,20 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       MLAMG_HIP(hipHostMalloc(&flag_host, 2 * sizeof(int32_t), hipHostMallocDefault));
       for (auto& e : flag_ev) MLAMG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    const int32_t* done_dev = reinterpret_cast<const int32_t*>(arena + desc[0].stat_out) + 3;
+    const int32_t* done_dev = reinterpret_cast<const int32_t*>(arena + done_off);
     constexpr int kPhaseBatch = 4;
     int a = 0;
     for (int batch = 0; a < total_a; ++batch) {
       const int na = tol >= 0.0 ? std::min(kPhaseBatch, total_a - a) : total_a - a;
       for (int q = 0; q < na; ++q, ++a) {
         launch_a();
-        if (a < max_iter)
-          hipLaunchKernelGGL(k_amg2v_coarse, dim3(coarse_blocks), dim3(256), 0, s, dd, arena);
+        if (a < max_iter) {
+          hipLaunchKernelGGL(k_amg2v_coarse<1>, dim3(coarse_blocks), dim3(256), 0, s, dd, arena,
+                             cb, count);
+          if (two_pass)
+            hipLaunchKernelGGL(k_amg2v_coarse<2>, dim3(coarse_blocks), dim3(256), 0, s, dd,
+                               arena, cb, count);
+        }
       }
       MLAMG_HIP(hipGetLastError());
       if (tol < 0.0 || a >= total_a) break;
@@ -1819,7 +1865,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       MLAMG_HIP(hipEventRecord(flag_ev[batch & 1], s));
       if (batch > 0) {
         MLAMG_HIP(hipEventSynchronize(flag_ev[(batch - 1) & 1]));
-        if (flag_host[(batch - 1) & 1]) break;
+        if (flag_host[(batch - 1) & 1] >= count) break;
       }
     }
   } else if (r_lds) {

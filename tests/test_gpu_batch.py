@@ -300,3 +300,30 @@ def test_fused_phased_edge_cases(oracle):
         assert itf == ir == 6
         assert np.allclose(ef, er, rtol=1e-10, atol=0), (ef, er)
         assert np.abs(xf - xr).max() <= 1e-9 * np.abs(xr).max()
+
+
+@pytest.mark.parametrize("smoother", ("gauss_seidel", "jacobi"))
+def test_phased_batch_equals_one_launch(oracle, monkeypatch, smoother):
+    """A batch whose largest coarse operator has n_c > 300 runs phased (each problem's cycles on
+    its workgroup, every problem's coarse solve — L^-1 then L^-T passes, or the Gauss-Jordan
+    inverse — spread over the CUs, a done counter ending the launches): the same arithmetic as
+    the one-launch batch, so the same bits, problems finishing at different cycles included."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mlamg.multigrid
+    import mlamg.problems
+    import mlamg as ml
+    probs = _problems(ml, oracle, 14)
+    assert max(P.shape[1] for _, P, _, _ in probs) > 300
+    # a non-symmetric operator (Gauss-Jordan inverse, mode 0) in the mix
+    A, P, b, x = probs[3]
+    A = A.tolil()
+    A[3, 4] = -1.5
+    probs[3] = (A.tocsr(), P, b, x)
+    ph = ml.multigrid.amg_2_v_batch(probs, res_tol=1e-10, smoother=smoother)
+    monkeypatch.setenv("MLAMG_BATCH_NO_PHASED_BATCH", "1")
+    one = ml.multigrid.amg_2_v_batch(probs, res_tol=1e-10, smoother=smoother)
+    assert len({r[3] for r in ph}) > 1  # not all problems stop at the same cycle
+    for i, (a, c) in enumerate(zip(ph, one)):
+        assert a[3] == c[3] and np.array_equal(a[2], c[2]) and np.array_equal(a[0], c[0]), i
