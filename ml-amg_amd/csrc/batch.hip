@@ -39,6 +39,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <type_traits>
@@ -63,8 +64,9 @@ struct BDesc {
   int32_t K, KA, KP, KT, nlev, panel, n_chunks, cap, timing;
   int32_t spd;    // A symmetric: try the inverse Cholesky factor before Gauss-Jordan
   int32_t chol_nb;  // its panel width (4..16, from n_c)
-  int32_t setup_mode;  // 0: Galerkin + coarse inverse here; 1: Galerkin only (the inverse is
-                       // built by the device-wide factorisation, dense.hip)
+  int32_t setup_mode;  // 0: Galerkin + coarse inverse here; 1: neither (k_galerkin_rows and the
+                       // device-wide factorisation of dense.hip); 2: Galerkin only (the batched
+                       // device-wide factorisation follows); 3: nothing (a relaunch's bystander)
   int32_t gs_rw;  // one-wave sweep (rows of K = 4 or 8 slots, levels <= 64 * gs_rw rows), 1 or 2
                   // rows per lane; 0: the workgroup sweeps each level
   int32_t gs_db;   // one-wave sweep: double-buffered chunk staging (chunks of >= 3 levels)
@@ -588,6 +590,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
       t_mark = t;
     }
   };
+  if (D.setup_mode == 3) return;
   if (D.timing && tid == 0)
     for (int q = 0; q < 8; ++q) tstat[q] = 0;
   if (tid == 0) {  // phased cycles: done flag, half cycles run
@@ -604,6 +607,13 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
   }
   dense_galerkin(D, arena, AH, tid);
   stamp(0);
+  if (D.setup_mode == 2) {  // the inverse from dense.hip's batched factorisation
+    if (tid == 0) {
+      stat[1] = 0;
+      stat[2] = 0;
+    }
+    return;
+  }
 
   if (D.spd) {
     // the panel width is the problem's own (a function of n_c alone): a problem's roundings do
@@ -1742,6 +1752,11 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   // a single problem with a large SPD coarse operator takes the device-wide coarse factorisation
   const bool ext_coarse = ext_ok && plans[0].spd;
   if (ext_coarse) desc[0].setup_mode = 1;
+  // a phased batch factors its SPD operators device-wide too, all in one launch sequence
+  const bool batch_ext = phased && count > 1 && !std::getenv("MLAMG_BATCH_NO_BATCH_EXT");
+  if (batch_ext)
+    for (int q = 0; q < count; ++q)
+      if (plans[q].spd) desc[q].setup_mode = 2;
   // ---- pack the inputs into pinned host memory, one copy in
   HostPinned& H = g_batch_host;
   const size_t host_need = std::max(in_bytes, total - out_begin);
@@ -1809,6 +1824,37 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       hipLaunchKernelGGL(k_amg2v_setup, dim3(1), dim3(kBT), lds_setup, s, dd, arena);
     }
   }
+  if (batch_ext) {
+    std::vector<DenseJob> jobs;
+    std::vector<int> who;
+    for (int q = 0; q < count; ++q)
+      if (desc[q].setup_mode == 2) {
+        DenseJob J{};
+        J.M = reinterpret_cast<double*>(arena + desc[q].AH);
+        J.inv = reinterpret_cast<double*>(arena + desc[q].AI);
+        J.n = desc[q].nc;
+        jobs.push_back(J);
+        who.push_back(q);
+      }
+    std::unique_ptr<bool[]> ok(new bool[std::max<size_t>(jobs.size(), 1)]);
+    MLAMG_TRY(dense_chol_inverse_batch(jobs.data(), (int)jobs.size(), ok.get(), s));
+    bool any_failed = false;
+    for (size_t j = 0; j < jobs.size(); ++j) any_failed = any_failed || !ok[j];
+    if (any_failed) {  // Gauss-Jordan in the setup kernel for those, the others untouched
+      BDesc* Dh = reinterpret_cast<BDesc*>(hb + desc_off);
+      for (int q = 0; q < count; ++q) Dh[q].setup_mode = 3;
+      for (size_t j = 0; j < jobs.size(); ++j)
+        if (!ok[j]) {
+          Dh[who[j]].setup_mode = 0;
+          Dh[who[j]].spd = 0;
+        }
+      MLAMG_HIP(hipMemcpyAsync(arena + desc_off, hb + desc_off, sizeof(BDesc) * count,
+                               hipMemcpyHostToDevice, s));
+      MLAMG_HIP(hipStreamSynchronize(s));
+      hipLaunchKernelGGL(k_amg2v_setup, dim3((unsigned)count), dim3(kBT), lds_setup, s, dd,
+                         arena);
+    }
+  }
   if (phased) {
     // cycle k = launches A_k (second half of cycle k - 1, first half of cycle k) and B_k (the
     // coarse solve); A_max_iter ends it. Every launch after the one that met the tolerance
@@ -1834,7 +1880,8 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     const int32_t* cb = reinterpret_cast<const int32_t*>(arena + cblk_off);
     // mode-1 problems (one-workgroup inverse Cholesky factor) need the second, L^-T, pass
     bool two_pass = false;
-    for (int q = 0; q < count; ++q) two_pass = two_pass || (plans[q].spd && !ext_coarse);
+    for (int q = 0; q < count; ++q)
+      two_pass = two_pass || (plans[q].spd && desc[q].setup_mode == 0);
     MLAMG_HIP(hipMemsetAsync(arena + done_off, 0, sizeof(int32_t), s));
     const int total_a = max_iter + 1;
     static thread_local int32_t* flag_host = nullptr;

@@ -222,6 +222,16 @@ int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int
 // A^-1 of a dense row-major n x n operator (destroyed) through its inverse Cholesky factor on the
 // whole GPU (dense.hip); *spd = false: not symmetric to rounding / not SPD, inv not written
 int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t s);
+// the same for many operators in one launch sequence (Lp, Zd, flag filled in here); spd[j] per job
+struct DenseJob {
+  double* M;
+  double* inv;
+  double* Lp;
+  double* Zd;
+  int32_t* flag;
+  int64_t n;
+};
+int dense_chol_inverse_batch(const DenseJob* jobs, int count, bool* spd, hipStream_t s);
 int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
                       hipStream_t s);
 int32_t* hier_done_flag(mlamg_hier* H);

@@ -179,10 +179,10 @@ __device__ bool panel_factor(const double* __restrict__ M, int64_t n, int64_t k0
 // Panel k0: block b of the grid takes rows below the panel (L21 = A21 L11^-T into Lp, row-major
 // (n - k1) x kNB) and columns < k1 of the panel's rows (Z = L11^-1 [X_top | I], written into M's
 // rows k0..k1-1: the final rows of X), a row / column per thread with its values in registers.
-__global__ __launch_bounds__(256) void k_chol_panel(double* __restrict__ M, int64_t n, int64_t k0,
-                                                    double* __restrict__ Lp,
-                                                    double* __restrict__ Zd,
-                                                    int32_t* __restrict__ fail) {
+__device__ __forceinline__ void chol_panel_body(double* __restrict__ M, int64_t n, int64_t k0,
+                                                double* __restrict__ Lp,
+                                                double* __restrict__ Zd,
+                                                int32_t* __restrict__ fail) {
   __shared__ double Dg[kNB * (kNB + 1)];
   __shared__ double rd[kNB];
   __shared__ int ok_s;
@@ -241,10 +241,10 @@ __global__ __launch_bounds__(256) void k_chol_panel(double* __restrict__ M, int6
 // Trailing update of panel k0, a wave per 16 x 16 tile of rows [k1, n) x columns [0, i]:
 //   M[i, j] <- (j in [k0, k1) ? 0 : M[i, j]) - sum_t L21[i][t] W[t][j],
 //   W = the panel's rows of X (j < k1) or L21^T (j >= k1).
-__global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ M, int64_t n,
-                                                     int64_t k0, const double* __restrict__ Lp,
-                                                     const double* __restrict__ Zd,
-                                                     const int32_t* __restrict__ fail) {
+__device__ __forceinline__ void chol_update_body(double* __restrict__ M, int64_t n, int64_t k0,
+                                                 const double* __restrict__ Lp,
+                                                 const double* __restrict__ Zd,
+                                                 const int32_t* __restrict__ fail) {
   if (*fail) return;
   const int64_t k1 = min<int64_t>(k0 + kNB, n);
   if (blockIdx.x == 0)  // L11^-1 into M's diagonal block (no tile of this launch reads it there)
@@ -294,8 +294,8 @@ __global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ M, int
 
 // A^-1 = X^T X from X = L^-1 (lower triangle of X; its upper triangle is not read): a wave per
 // 16 x 16 tile, C_ij = sum over k >= max(i, j) of X_ki X_kj.
-__global__ __launch_bounds__(256) void k_xtx(const double* __restrict__ X, int64_t n,
-                                             double* __restrict__ Cm) {
+__device__ __forceinline__ void xtx_body(const double* __restrict__ X, int64_t n,
+                                         double* __restrict__ Cm) {
   const int64_t nb = (n + 15) / 16;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nb * nb) return;
@@ -319,13 +319,111 @@ __global__ __launch_bounds__(256) void k_xtx(const double* __restrict__ X, int64
 // A symmetric up to rounding, checked on the device: |a_ij - a_ji| <= 1e-12 max(|a_ii|, |a_jj|)
 // (a Galerkin P^T A P of a symmetric A is symmetric up to its SpGEMM's summation order; a
 // genuinely unsymmetric operator differs by far more). bad[0] counts violations.
-__global__ void k_asym(const double* __restrict__ M, int64_t n, int32_t* __restrict__ bad) {
+__device__ __forceinline__ void asym_body(const double* __restrict__ M, int64_t n,
+                                          int32_t* __restrict__ bad) {
   const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (q >= n * n) return;
   const int64_t i = q / n, j = q - i * n;
   if (j >= i) return;
   const double d = fmax(fabs(M[i * n + i]), fabs(M[j * n + j]));
   if (!(fabs(M[i * n + j] - M[j * n + i]) <= 1e-12 * d)) atomicAdd(bad, 1);
+}
+
+__global__ __launch_bounds__(256) void k_chol_panel(double* __restrict__ M, int64_t n, int64_t k0,
+                                                    double* __restrict__ Lp,
+                                                    double* __restrict__ Zd,
+                                                    int32_t* __restrict__ fail) {
+  chol_panel_body(M, n, k0, Lp, Zd, fail);
+}
+__global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ M, int64_t n,
+                                                     int64_t k0, const double* __restrict__ Lp,
+                                                     const double* __restrict__ Zd,
+                                                     const int32_t* __restrict__ fail) {
+  chol_update_body(M, n, k0, Lp, Zd, fail);
+}
+__global__ __launch_bounds__(256) void k_xtx(const double* __restrict__ X, int64_t n,
+                                             double* __restrict__ Cm) {
+  xtx_body(X, n, Cm);
+}
+__global__ void k_asym(const double* __restrict__ M, int64_t n, int32_t* __restrict__ bad) {
+  asym_body(M, n, bad);
+}
+
+// Many operators at once (the phased batch of batch.hip): job blockIdx.y, each launch sized for
+// the largest job; blocks beyond a job's work return. flag[0] = failed pivot, flag[1] = asymmetry
+// count: either stops the job's remaining launches.
+__global__ __launch_bounds__(256) void k_chol_panel_b(const DenseJob* __restrict__ jobs,
+                                                      int64_t k0) {
+  const DenseJob J = jobs[blockIdx.y];
+  if (k0 >= J.n || (int64_t)blockIdx.x * 256 >= J.n || J.flag[1]) return;
+  chol_panel_body(J.M, J.n, k0, J.Lp, J.Zd, J.flag);
+}
+__global__ __launch_bounds__(256) void k_chol_update_b(const DenseJob* __restrict__ jobs,
+                                                       int64_t k0) {
+  const DenseJob J = jobs[blockIdx.y];
+  if (k0 >= J.n || J.flag[1]) return;
+  chol_update_body(J.M, J.n, k0, J.Lp, J.Zd, J.flag);
+}
+__global__ __launch_bounds__(256) void k_xtx_b(const DenseJob* __restrict__ jobs) {
+  const DenseJob J = jobs[blockIdx.y];
+  if (J.flag[0] || J.flag[1]) return;
+  xtx_body(J.M, J.n, J.inv);
+}
+__global__ void k_asym_b(const DenseJob* __restrict__ jobs) {
+  const DenseJob J = jobs[blockIdx.y];
+  asym_body(J.M, J.n, J.flag + 1);
+}
+
+int dense_chol_inverse_batch(const DenseJob* jobs_host, int count, bool* spd, hipStream_t s) {
+  if (count <= 0) return MLAMG_OK;
+  int64_t max_n = 0, lp = 0;
+  for (int j = 0; j < count; ++j) {
+    max_n = std::max(max_n, jobs_host[j].n);
+    lp += ((std::max<int64_t>(jobs_host[j].n, 1) + kNB) * kNB + kNB * kNB + 31) & ~int64_t(31);
+  }
+  // job table | flags (2 per job) | Lp + Zd per job
+  const size_t tab = ((sizeof(DenseJob) * count + 255) & ~size_t(255));
+  const size_t fl = ((sizeof(int32_t) * 2 * count + 255) & ~size_t(255));
+  char* base = static_cast<char*>(scratch(tab + fl + sizeof(double) * lp, 12));
+  MLAMG_REQUIRE(base, "dense batch: scratch allocation failed");
+  std::vector<DenseJob> jobs(jobs_host, jobs_host + count);
+  int32_t* flags = reinterpret_cast<int32_t*>(base + tab);
+  double* work = reinterpret_cast<double*>(base + tab + fl);
+  for (int j = 0; j < count; ++j) {
+    jobs[j].flag = flags + 2 * j;
+    jobs[j].Lp = work;
+    jobs[j].Zd = work + (std::max<int64_t>(jobs[j].n, 1) + kNB) * kNB;
+    work += ((std::max<int64_t>(jobs[j].n, 1) + kNB) * kNB + kNB * kNB + 31) & ~int64_t(31);
+  }
+  MLAMG_HIP(hipMemcpyAsync(base, jobs.data(), sizeof(DenseJob) * count, hipMemcpyHostToDevice,
+                           s));
+  MLAMG_HIP(hipMemsetAsync(flags, 0, sizeof(int32_t) * 2 * count, s));
+  const DenseJob* dj = reinterpret_cast<const DenseJob*>(base);
+  const unsigned cy = (unsigned)count;
+  hipLaunchKernelGGL(k_asym_b, dim3((unsigned)((max_n * max_n + 255) / 256), cy), dim3(256), 0, s,
+                     dj);
+  for (int64_t k0 = 0; k0 < max_n; k0 += kNB) {
+    hipLaunchKernelGGL(k_chol_panel_b, dim3((unsigned)((max_n + 255) / 256), cy), dim3(256), 0, s,
+                       dj, k0);
+    int64_t T = 1;
+    for (int j = 0; j < count; ++j) {
+      const int64_t n = jobs[j].n, k1 = std::min<int64_t>(k0 + kNB, n);
+      if (k0 >= n || k1 >= n) continue;
+      const int64_t a16 = (k1 + 15) / 16, nrb = (n - k1 + 15) / 16;
+      T = std::max<int64_t>(T, nrb * (a16 + 1) + nrb * (nrb - 1) / 2);
+    }
+    hipLaunchKernelGGL(k_chol_update_b, dim3((unsigned)((T + 3) / 4), cy), dim3(256), 0, s, dj,
+                       k0);
+  }
+  const int64_t nb = (max_n + 15) / 16;
+  hipLaunchKernelGGL(k_xtx_b, dim3((unsigned)((nb * nb + 3) / 4), cy), dim3(256), 0, s, dj);
+  MLAMG_HIP(hipGetLastError());
+  std::vector<int32_t> h(2 * (size_t)count);
+  MLAMG_HIP(hipMemcpyAsync(h.data(), flags, sizeof(int32_t) * 2 * count, hipMemcpyDeviceToHost,
+                           s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  for (int j = 0; j < count; ++j) spd[j] = h[2 * j] == 0 && h[2 * j + 1] == 0;
+  return MLAMG_OK;
 }
 
 // the inverse Cholesky path; *spd false when A is not symmetric to rounding or not SPD in

@@ -306,8 +306,11 @@ def test_fused_phased_edge_cases(oracle):
 def test_phased_batch_equals_one_launch(oracle, monkeypatch, smoother):
     """A batch whose largest coarse operator has n_c > 300 runs phased (each problem's cycles on
     its workgroup, every problem's coarse solve — L^-1 then L^-T passes, or the Gauss-Jordan
-    inverse — spread over the CUs, a done counter ending the launches): the same arithmetic as
-    the one-launch batch, so the same bits, problems finishing at different cycles included."""
+    inverse — spread over the CUs, a done counter ending the launches). With the one-workgroup
+    factors (MLAMG_BATCH_NO_BATCH_EXT) it is the same arithmetic as the one-launch batch, so the
+    same bits, problems finishing at different cycles included; by default its SPD operators are
+    factored device-wide in one batched launch sequence (dense.hip): same iteration counts,
+    histories within rtol 1e-10 (+ 1e-12 of the first norm), iterates within 1e-9 of their max."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -321,9 +324,15 @@ def test_phased_batch_equals_one_launch(oracle, monkeypatch, smoother):
     A = A.tolil()
     A[3, 4] = -1.5
     probs[3] = (A.tocsr(), P, b, x)
+    ext = ml.multigrid.amg_2_v_batch(probs, res_tol=1e-10, smoother=smoother)
+    monkeypatch.setenv("MLAMG_BATCH_NO_BATCH_EXT", "1")
     ph = ml.multigrid.amg_2_v_batch(probs, res_tol=1e-10, smoother=smoother)
     monkeypatch.setenv("MLAMG_BATCH_NO_PHASED_BATCH", "1")
     one = ml.multigrid.amg_2_v_batch(probs, res_tol=1e-10, smoother=smoother)
     assert len({r[3] for r in ph}) > 1  # not all problems stop at the same cycle
     for i, (a, c) in enumerate(zip(ph, one)):
         assert a[3] == c[3] and np.array_equal(a[2], c[2]) and np.array_equal(a[0], c[0]), i
+    for i, (a, c) in enumerate(zip(ext, one)):
+        # (b != 0 problems reach the residual's rounding floor near res_tol: atol 1e-12 err_0)
+        assert a[3] == c[3] and np.allclose(a[2], c[2], rtol=1e-10, atol=1e-12 * c[2][0]), i
+        assert np.abs(a[0] - c[0]).max() <= 1e-9 * np.abs(c[0]).max(), i
