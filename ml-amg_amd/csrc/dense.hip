@@ -430,14 +430,15 @@ int dense_chol_inverse_batch(const DenseJob* jobs_host, int count, bool* spd, hi
 // floating point (M destroyed, inv untouched garbage)
 int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t s) {
   *spd = false;
-  double* Lp = nullptr;
-  int32_t* flag = nullptr;
-  if (hipMalloc(&Lp, sizeof(double) * (std::max<int64_t>(n, 1) + kNB) * kNB) != hipSuccess ||
-      hipMalloc(&flag, sizeof(int32_t) * 2) != hipSuccess) {
-    if (Lp) (void)hipFree(Lp);
-    set_error("dense_create: hipMalloc failed");
+  // L21 panel + the diagonal block's L11^-1 + flags from a cached scratch slot (no per-call
+  // hipMalloc / hipFree: the fused single-call path factors once per amg_2_v call)
+  const size_t lp_doubles = (size_t)(std::max<int64_t>(n, 1) + kNB) * kNB + kNB * kNB;
+  double* Lp = static_cast<double*>(scratch(sizeof(double) * lp_doubles + 256, 13));
+  if (!Lp) {
+    set_error("dense_create: scratch allocation failed");
     return MLAMG_ENOMEM;
   }
+  int32_t* flag = reinterpret_cast<int32_t*>(Lp + lp_doubles);
   (void)hipMemsetAsync(flag, 0, sizeof(int32_t) * 2, s);
   hipLaunchKernelGGL(k_asym, dim3((unsigned)((n * n + 255) / 256)), dim3(256), 0, s, M, n,
                      flag + 1);
@@ -468,8 +469,6 @@ int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t
       *spd = e == hipSuccess;
     }
   }
-  (void)hipFree(Lp);
-  (void)hipFree(flag);
   if (e != hipSuccess) {
     set_error(std::string("dense_create: ") + hipGetErrorString(e));
     return MLAMG_EHIP;
