@@ -1483,8 +1483,7 @@ class HostPool {
   pid_t pid_ = getpid();
 };
 
-template <class F>
-void parallel_for(int count, F&& f) {
+int host_threads() {
   static const int max_threads = [] {
     int t = 16;
     cpu_set_t set;
@@ -1492,13 +1491,22 @@ void parallel_for(int count, F&& f) {
     if (const char* e = std::getenv("MLAMG_HOST_THREADS")) t = std::max(1, std::atoi(e));
     return std::max(1, t);
   }();
-  if (max_threads <= 1 || count < 4) {
+  return max_threads;
+}
+
+HostPool& host_pool() {  // one pool for every parallel_for of the process
+  static HostPool pool(host_threads() - 1);
+  return pool;
+}
+
+template <class F>
+void parallel_for(int count, F&& f) {
+  if (host_threads() <= 1 || count < 4) {
     for (int q = 0; q < count; ++q) f(q);
     return;
   }
-  static HostPool pool(max_threads - 1);
   const std::function<void(int)> fn = [&](int q) { f(q); };
-  if (!pool.run(count, fn))
+  if (!host_pool().run(count, fn))
     for (int q = 0; q < count; ++q) f(q);
 }
 
@@ -1950,12 +1958,23 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       two_pass = two_pass || (plans[q].spd && desc[q].setup_mode == 0);
     MLAMG_HIP(hipMemsetAsync(arena + done_off, 0, sizeof(int32_t), s));
     const int total_a = max_iter + 1;
-    static thread_local int32_t* flag_host = nullptr;
-    static thread_local hipEvent_t flag_ev[2] = {nullptr, nullptr};
-    if (!flag_host) {
-      MLAMG_HIP(hipHostMalloc(&flag_host, 2 * sizeof(int32_t), hipHostMallocDefault));
-      for (auto& e : flag_ev) MLAMG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // per host thread: two pinned done-count slots and their events (freed at thread exit)
+    struct PhaseFlags {
+      int32_t* host = nullptr;
+      hipEvent_t ev[2] = {nullptr, nullptr};
+      ~PhaseFlags() {
+        for (auto e : ev)
+          if (e) (void)hipEventDestroy(e);
+        if (host) (void)hipHostFree(host);
+      }
+    };
+    static thread_local PhaseFlags pf;
+    if (!pf.host) {
+      MLAMG_HIP(hipHostMalloc(&pf.host, 2 * sizeof(int32_t), hipHostMallocDefault));
+      for (auto& e : pf.ev) MLAMG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
+    int32_t* flag_host = pf.host;
+    hipEvent_t* flag_ev = pf.ev;
     const int32_t* done_dev = reinterpret_cast<const int32_t*>(arena + done_off);
     constexpr int kPhaseBatch = 4;
     int a = 0;
