@@ -27,6 +27,14 @@ struct mlamg_gs {
   double* pk_diag = nullptr;
   double* b_lvl = nullptr;
   int32_t max_off = 0;  // longest off-diagonal count
+  // windowed one-wave sweep (k_gs_win): x by level-order position in an LDS ring of 2^ring_log2
+  // slots; wcol = the packed columns as positions (pads -1); chunks of levels staged into two
+  // LDS buffers of win_cap + 1 positions; win_w = the widest level distance of a coupling
+  int32_t win_rw = 0;  // rows per lane (0: no windowed sweep)
+  int32_t ring_log2 = 0, win_cap = 0, win_w = 0, n_chunks = 0;
+  int32_t* wcol = nullptr;
+  int32_t* d_clev = nullptr;
+  size_t win_lds = 0;
 };
 
 namespace mlamg {
@@ -199,6 +207,169 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_lds(const int32_t* __restrict__
   for (int64_t i = threadIdx.x; i < n; i += kGsBlock) x[i] = xs[i];
 }
 
+// Windowed one-wave sweep for levels of <= 64 * RW rows: wave 0 walks the levels with x held by
+// level-order position in an LDS ring (a level's rows read positions at most W levels away, so
+// levels [l - W, l + W] are all a step needs); waves 1-15 meanwhile stage the next chunk of
+// levels (structure + the old x of the levels entering the window, loaded past L1) into the other
+// buffer. Consecutive levels need only a wavefront fence; a chunk ends with a workgroup barrier.
+// Pads point at the ring's zero slot (+0.0 products: the sum starts at +0.0 and never becomes
+// -0.0, so bitwise neutral); a zero-diagonal row is left alone, as the sequential sweep does.
+// Updated values go to the ring and to x. Same products, order and division: bitwise gs_row.
+// 256 lanes: wave 0 gets the registers of RW rows x KM slots (+ the next level's) without spills;
+// the 3 other waves stage
+constexpr int kGsWinBlock = 256;
+
+template <int KM, int RW>
+__global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restrict__ rows,
+                                                     const int32_t* __restrict__ lptr,
+                                                     int32_t nlev,
+                                                     const int32_t* __restrict__ clev,
+                                                     int32_t nchunks,
+                                                     const int32_t* __restrict__ wcol,
+                                                     const double* __restrict__ pval,
+                                                     const double* __restrict__ pdiag,
+                                                     const double* __restrict__ blvl,
+                                                     int ring_log2, int cap, int W,
+                                                     int iterations, double* x,
+                                                     const int32_t* done) {
+  extern __shared__ double lds[];
+  if (done && *done) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int RS = 1 << ring_log2, RM = RS - 1;
+  double* ring = lds;  // RS slots + the zero slot (RS) + the sink slot (RS + 1)
+  // per buffer (position-major, 16-byte aligned): vals cap+1 x KM | diag | b | cols (ring slots)
+  // cap+1 x KM | target slot | row | level starts
+  // (cap + 1) x (2 KM + 4) words of doubles + (cap + 1) x (KM + 4) words of ints, in doubles
+  const int64_t buf = (((int64_t)(cap + 1) * (3 * KM + 8) + 1) / 2 + 1) & ~int64_t(1);
+  double* bufs = lds + ((RS + 2 + 1) & ~1);
+  if (tid == 0) ring[RS] = 0.0;
+  auto stage = [&](int ch, double* wv, int t0, int nt) {
+    double* wd = wv + (int64_t)(cap + 1) * KM;
+    double* wb = wd + (cap + 1);
+    int32_t* wc = reinterpret_cast<int32_t*>(wb + (cap + 1));
+    int32_t* wt = wc + (int64_t)(cap + 1) * KM;
+    int32_t* wr = wt + (cap + 1);
+    int32_t* wl = wr + (cap + 1);
+    const int l0 = clev[ch], l1 = clev[ch + 1];
+    const int P0 = lptr[l0], cnt = lptr[l1] - P0;
+    for (int q = t0; q < cnt * KM; q += nt) {
+      const int32_t c = wcol[(int64_t)P0 * KM + q];
+      wc[q] = c >= 0 ? (c & RM) : RS;
+      wv[q] = pval[(int64_t)P0 * KM + q];
+    }
+    for (int q = t0; q < cnt; q += nt) {
+      const double d = pdiag[P0 + q];
+      wd[q] = d != 0.0 ? d : 1.0;
+      wb[q] = blvl[P0 + q];
+      wt[q] = d != 0.0 ? ((P0 + q) & RM) : RS + 1;  // zero diagonal: left alone (sink)
+      wr[q] = d != 0.0 ? rows[P0 + q] : -1;
+    }
+    for (int q = t0; q <= l1 - l0; q += nt) wl[q] = lptr[l0 + q] - P0;
+    if (t0 < KM) {  // the dummy position of lanes past a level's end
+      wc[cnt * KM + t0] = RS;
+      wv[cnt * KM + t0] = 0.0;
+    }
+    if (t0 == 0) {
+      wd[cnt] = 1.0;
+      wb[cnt] = 0.0;
+      wt[cnt] = RS + 1;
+      wr[cnt] = -1;
+    }
+    // the old x of the levels entering the window with this chunk (past L1: the previous
+    // sweep of this launch wrote them from wave 0)
+    const int la = ch == 0 ? 0 : min(nlev, l0 + W), lb = min(nlev, l1 + W);
+    for (int p = lptr[la] + t0; p < lptr[lb]; p += nt)
+      ring[p & RM] = __hip_atomic_load(x + rows[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  for (int it = 0; it < iterations; ++it) {
+    stage(0, bufs, tid, kGsWinBlock);
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+      double* cur = bufs + (ch & 1) * buf;
+      if (tid < 64) {
+        const double* sv = cur;
+        const double* sd = sv + (int64_t)(cap + 1) * KM;
+        const double* sb = sd + (cap + 1);
+        const int32_t* sc = reinterpret_cast<const int32_t*>(sb + (cap + 1));
+        const int32_t* st = sc + (int64_t)(cap + 1) * KM;
+        const int32_t* sr = st + (cap + 1);
+        const int32_t* sl = sr + (cap + 1);
+        const int nl = clev[ch + 1] - clev[ch];
+        const int cnt = sl[nl];
+        int c[RW][KM], tg[RW], rw[RW];
+        double v[RW][KM], d[RW], bv[RW];
+        auto load = [&](int l, int (&cc)[RW][KM], double (&vv)[RW][KM], double* dd, double* bb,
+                        int* tt, int* rr) {
+          const int a = sl[l], z = sl[l + 1];
+#pragma unroll
+          for (int u = 0; u < RW; ++u) {
+            const int p = a + lane + 64 * u < z ? a + lane + 64 * u : cnt;
+#pragma unroll
+            for (int k = 0; k < KM; k += 4) {
+              const int4 c4 = *reinterpret_cast<const int4*>(sc + (int64_t)p * KM + k);
+              cc[u][k] = c4.x;
+              cc[u][k + 1] = c4.y;
+              cc[u][k + 2] = c4.z;
+              cc[u][k + 3] = c4.w;
+            }
+#pragma unroll
+            for (int k = 0; k < KM; k += 2) {
+              const double2 v2 = *reinterpret_cast<const double2*>(sv + (int64_t)p * KM + k);
+              vv[u][k] = v2.x;
+              vv[u][k + 1] = v2.y;
+            }
+            dd[u] = sd[p];
+            bb[u] = sb[p];
+            tt[u] = st[p];
+            rr[u] = sr[p];
+          }
+        };
+        load(0, c, v, d, bv, tg, rw);
+        #pragma unroll 1
+        for (int l = 0; l < nl; ++l) {
+          double g[RW][KM];
+#pragma unroll
+          for (int u = 0; u < RW; ++u)
+#pragma unroll
+            for (int k = 0; k < KM; ++k) g[u][k] = ring[c[u][k]];
+          int c2[RW][KM], tg2[RW], rw2[RW];
+          double v2[RW][KM], d2[RW], bv2[RW];
+          load(l + 1 < nl ? l + 1 : l, c2, v2, d2, bv2, tg2, rw2);
+#pragma unroll
+          for (int u = 0; u < RW; ++u) {
+            double y = 0.0;
+#pragma unroll
+            for (int k = 0; k < KM; ++k) y += v[u][k] * g[u][k];
+            const double xi = (bv[u] - y) / d[u];
+            ring[tg[u]] = xi;
+            if (rw[u] >= 0) x[rw[u]] = xi;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+          for (int u = 0; u < RW; ++u) {
+#pragma unroll
+            for (int k = 0; k < KM; ++k) {
+              c[u][k] = c2[u][k];
+              v[u][k] = v2[u][k];
+            }
+            d[u] = d2[u];
+            bv[u] = bv2[u];
+            tg[u] = tg2[u];
+            rw[u] = rw2[u];
+          }
+        }
+      } else if (ch + 1 < nchunks) {
+        stage(ch + 1, bufs + ((ch + 1) & 1) * buf, tid - 64, kGsWinBlock - 64);
+      }
+      __syncthreads();
+    }
+    __threadfence();  // this sweep's x stores before the next sweep's window loads
+    __syncthreads();
+  }
+}
+
 __global__ void k_gs_b_level(const int32_t* __restrict__ rows, int64_t n,
                              const double* __restrict__ b, double* __restrict__ blvl,
                              const int32_t* done) {
@@ -230,6 +401,23 @@ static void launch_gs_pipe(const mlamg_gs* G, double* x, const double* b, int it
                      done);
 }
 
+static bool gs_win_disabled() {  // MLAMG_GS_NO_WIN=1: A/B runs, tests
+  const char* e = std::getenv("MLAMG_GS_NO_WIN");
+  return e && e[0] == '1';
+}
+
+template <int KM, int RW>
+static void launch_gs_win(const mlamg_gs* G, double* x, const double* b, int iterations,
+                          const int32_t* done, hipStream_t s) {
+  const int64_t n = G->A->n_rows;
+  hipLaunchKernelGGL(k_gs_b_level, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
+                     n, b, G->b_lvl, done);
+  hipLaunchKernelGGL((k_gs_win<KM, RW>), dim3(1), dim3(kGsWinBlock), G->win_lds, s, G->rows,
+                     G->d_level_ptr, G->n_levels, G->d_clev, G->n_chunks, G->wcol, G->pk_val,
+                     G->pk_diag, G->b_lvl, G->ring_log2, G->win_cap, G->win_w, iterations, x,
+                     done);
+}
+
 int64_t gs_rows(const mlamg_gs* G) { return G->A->n_rows; }
 
 int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
@@ -237,7 +425,19 @@ int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
   const mlamg_csr* A = G->A;
   if (A->n_rows == 0 || iterations <= 0) return MLAMG_OK;
   const bool pipe = G->pk_k > 0 && G->n_levels > 4;
-  if (pipe && G->max_level_rows <= 2 * kGsBlock) {
+  if (pipe && G->win_rw > 0 && !gs_win_disabled()) {
+    if (G->pk_k == 4) {
+      switch (G->win_rw) {
+        case 1: launch_gs_win<4, 1>(G, x, b, iterations, done, s); break;
+        case 2: launch_gs_win<4, 2>(G, x, b, iterations, done, s); break;
+        case 3: launch_gs_win<4, 3>(G, x, b, iterations, done, s); break;
+        default: launch_gs_win<4, 4>(G, x, b, iterations, done, s); break;
+      }
+    } else {
+      if (G->win_rw == 1) launch_gs_win<8, 1>(G, x, b, iterations, done, s);
+      else launch_gs_win<8, 2>(G, x, b, iterations, done, s);
+    }
+  } else if (pipe && G->max_level_rows <= 2 * kGsBlock) {
     const bool one = G->max_level_rows <= kGsBlock;
     if (G->pk_k == 4) {
       if (one) launch_gs_pipe<1, 4>(G, x, b, iterations, done, s);
@@ -265,6 +465,67 @@ int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
 }  // namespace mlamg
 
 using namespace mlamg;
+
+// The windowed one-wave sweep's plan: W = the widest level distance of a coupling, chunks of
+// levels that fit a staging buffer, and the ring that holds every position a step and the
+// concurrent staging of the next chunk touch. Optional: win_rw stays 0 when levels are wider
+// than 64 * RW rows or the ring and buffers do not fit the LDS budget.
+static void setup_window(mlamg_gs* G, const std::vector<int32_t>& ip,
+                         const std::vector<int32_t>& ij, const std::vector<int32_t>& level,
+                         const std::vector<int32_t>& rows, const std::vector<int32_t>& pcol,
+                         int K) {
+  const int64_t n = G->A->n_rows;
+  const int nlev = G->n_levels;
+  const int rw_max = K == 4 ? 4 : 2;
+  const int rw = (G->max_level_rows + 63) / 64;
+  if (rw < 1 || rw > rw_max || nlev <= 4) return;
+  int W = 0;
+  for (int64_t i = 0; i < n; ++i)
+    for (int k = ip[i]; k < ip[i + 1]; ++k)
+      if (ij[k] != i) W = std::max(W, std::abs(level[ij[k]] - level[i]));
+  const std::vector<int32_t>& lp = G->level_ptr;
+  const size_t budget = 150 * 1024;
+  const size_t per_pos = (size_t)(12 * K + 32);
+  for (int cap = 4096; cap >= G->max_level_rows; cap = cap * 3 / 4) {
+    std::vector<int32_t> clev{0};
+    for (int l = 0; l < nlev;) {
+      const int start = l;
+      while (l < nlev && (l == start || lp[l + 1] - lp[start] <= cap)) ++l;
+      clev.push_back(l);
+    }
+    const int nch = (int)clev.size() - 1;
+    int64_t span = 0;
+    for (int ch = 0; ch < nch; ++ch) {
+      const int lo = std::max(0, clev[ch] - W);
+      const int hi = std::min(nlev, clev[std::min(ch + 2, nch)] + W);
+      span = std::max<int64_t>(span, lp[hi] - lp[lo]);
+    }
+    int lg = 0;
+    while ((int64_t(1) << lg) < span) ++lg;
+    const size_t ring = ((size_t(1) << lg) + 4) * 8;
+    const size_t bufs = 2 * ((size_t)(cap + 1) * per_pos + 32);
+    if (ring + bufs > budget) continue;
+    std::vector<int32_t> pos(n), wcol((size_t)n * K, -1);
+    for (int64_t p = 0; p < n; ++p) pos[rows[p]] = (int32_t)p;
+    for (size_t q = 0; q < (size_t)n * K; ++q)
+      if (pcol[q] >= 0) wcol[q] = pos[pcol[q]];
+    if (hipMalloc(&G->wcol, sizeof(int32_t) * std::max<size_t>((size_t)n * K, 1)) != hipSuccess ||
+        hipMalloc(&G->d_clev, sizeof(int32_t) * clev.size()) != hipSuccess) {
+      if (G->wcol) (void)hipFree(G->wcol);
+      G->wcol = nullptr;
+      return;
+    }
+    (void)hipMemcpy(G->wcol, wcol.data(), sizeof(int32_t) * (size_t)n * K, hipMemcpyHostToDevice);
+    (void)hipMemcpy(G->d_clev, clev.data(), sizeof(int32_t) * clev.size(), hipMemcpyHostToDevice);
+    G->win_w = W;
+    G->win_cap = cap;
+    G->ring_log2 = lg;
+    G->n_chunks = nch;
+    G->win_lds = ring + bufs + 64;
+    G->win_rw = rw;
+    return;
+  }
+}
 
 extern "C" {
 
@@ -357,6 +618,7 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
           (void)hipMemcpy(G->pk_diag, pdiag.data(), sizeof(double) * n, hipMemcpyHostToDevice);
         }
         G->pk_k = K;
+        setup_window(G, ip, ij, level, rows, pcol, K);
       } else {  // optional: the sweep falls back to the plain kernels
         for (void* q : {(void*)G->pk_col, (void*)G->pk_val, (void*)G->pk_diag, (void*)G->b_lvl})
           if (q) (void)hipFree(q);
@@ -372,7 +634,7 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
 int mlamg_gs_destroy(mlamg_gs* G) {
   if (G) {
     for (void* q : {(void*)G->rows, (void*)G->d_level_ptr, (void*)G->pk_col, (void*)G->pk_val,
-                    (void*)G->pk_diag, (void*)G->b_lvl})
+                    (void*)G->pk_diag, (void*)G->b_lvl, (void*)G->wcol, (void*)G->d_clev})
       if (q) (void)hipFree(q);
     delete G;
   }

@@ -130,7 +130,7 @@ class Hierarchy:
         L.dinv = L.A.diag_inv(omega) if dinv_w is None else to_device_vec(dinv_w)
         H.levels.append(L)
         H.Ac = galerkin(L.R, L.A, L.P)
-        H._finalize(nu_pre, nu_post)
+        H._finalize(nu_pre, nu_post, dense_max=cls.TWO_LEVEL_DENSE_MAX)
         if smoother == "gauss_seidel":
             L.gs = GaussSeidel(L.A)
             call("mlamg_hier_set_level_smoother", H.handle, 0, L.gs.handle)
@@ -362,6 +362,9 @@ class Hierarchy:
     # coarsest solve: a dense inverse up to this many rows (its setup is O(n_c^3)), above it
     # PCG preconditioned by an inner hierarchy of the coarse operator (csrc/pcg.hip)
     DENSE_MAX = 4096
+    # the reference's two-level solve factors A_H once for ~30 cycles: there the O(n_c^3) dense
+    # factor (device-wide, fp64 matrix cores) beats a PCG solve per cycle up to larger n_c
+    TWO_LEVEL_DENSE_MAX = 12288
     COARSE_RTOL = 1e-12
 
     def _finalize(self, nu_pre, nu_post, dense_max=None, coarse_rtol=None):

@@ -343,13 +343,17 @@ def _P1(golden):
 
 
 @pytest.mark.parametrize("case", ("wide_levels", "grid_200", "grid_1100", "cube_24",
-                                  "long_rows", "unsorted_zero_diag", "grid_60_lds", "cube_12_lds"))
+                                  "long_rows", "unsorted_zero_diag", "grid_60_lds", "cube_12_lds",
+                                  "grid_256", "nine_point_48"))
 def test_gauss_seidel_both_schedules(ml, oracle, torch_cuda, case):
     """Level-scheduled GS through every schedule: the pipelined one-workgroup kernel (levels of
     <= 1024 rows: grid_200; <= 2048: grid_1100 diagonals; cube_24 planes), the plain
     one-workgroup kernel (rows with more than 8 off-diagonals), the per-level launches (a level
-    wider than 8192 rows) — bitwise the sequential pyamg sweep, including rows stored in
-    non-ascending order, a zero diagonal (row left unchanged) and a duplicated diagonal entry."""
+    wider than 8192 rows), the windowed one-wave sweep (levels of <= 256 rows with <= 4
+    off-diagonals, <= 128 with <= 8: grid_200, grid_256, grid_60, cube_12, nine_point_48 whose
+    couplings span 2 levels, the unsorted / zero-diagonal case) — bitwise the sequential pyamg
+    sweep, including rows stored in non-ascending order, a zero diagonal (row left unchanged)
+    and a duplicated diagonal entry; three sweeps per launch."""
     rs = np.random.RandomState(11)
     if case == "wide_levels":
         n = 30000  # diagonal + a sparse upper band: a few levels of ~10^4 independent rows
@@ -361,6 +365,12 @@ def test_gauss_seidel_both_schedules(ml, oracle, torch_cuda, case):
         A = ml.problems.poisson_2d_5pt(1100)
     elif case == "cube_24":
         A = ml.problems.poisson_3d_7pt(24)
+    elif case == "grid_256":
+        A = ml.problems.poisson_2d_5pt(256)
+    elif case == "nine_point_48":
+        m = 48
+        T = sp.diags([1.0, 1.0, 1.0], [-1, 0, 1], shape=(m, m))
+        A = (sp.kron(T, T) * -1.0 + sp.eye(m * m) * 9.0).tocsr()
     elif case == "grid_60_lds":  # n <= 8192: x held in LDS for the whole sweep
         A = ml.problems.poisson_2d_5pt(60)
     elif case == "cube_12_lds":
