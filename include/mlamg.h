@@ -274,8 +274,10 @@ int mlamg_gs_sweep(const mlamg_gs* G, double* x, const double* b, int iterations
  * dense GEMV. Returns MLAMG_EINVAL if the matrix is numerically singular. */
 int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream);
 int mlamg_dense_destroy(mlamg_dense* D);
-/* which inverse was built: 1 = inverse Cholesky factor (symmetric positive definite), 0 =
- * Gauss-Jordan with partial pivoting (any other nonsingular operator) */
+/* which inverse was built: 1 = inverse Cholesky factor X = L^-1 with A^-1 = X^T X formed
+ * (symmetric positive definite), 2 = the same factor kept and applied as X^T (X b), two
+ * triangular passes (SPD operators of >= 2048 rows: no O(n^3) product), 0 = Gauss-Jordan with
+ * partial pivoting (any other nonsingular operator) */
 int mlamg_dense_info(const mlamg_dense* D, int* method, int64_t* n);
 int mlamg_dense_solve(const mlamg_dense* D, const double* b, double* x, void* stream);
 

@@ -147,7 +147,9 @@ struct mlamg_csr {
 struct mlamg_dense {
   int64_t n = 0;
   double* inv = nullptr;  // row-major n x n
-  int method = 0;         // 0 Gauss-Jordan, 1 inverse Cholesky factor (dense.hip)
+  int method = 0;  // 0 Gauss-Jordan, 1 inverse Cholesky factor (A^-1 = X^T X), 2 the factor X
+                   // (lower) with X^T (strict upper) applied as two triangular passes (dense.hip)
+  double* y = nullptr;  // method 2: the intermediate X b
 };
 
 namespace mlamg {

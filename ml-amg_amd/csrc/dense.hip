@@ -136,6 +136,55 @@ __global__ __launch_bounds__(256) void k_gemv(const double* __restrict__ M, int6
   if (lane == 0) x[row] = s;
 }
 
+// One of the two triangular passes of A^-1 b = X^T (X b) with X = L^-1 kept in M's lower triangle
+// and X^T in its strict upper one (method 2): row i of M over columns [0, i] (UP false: y = X b)
+// or [i, n) (UP true: x = X^T y, since (X^T)_ij = X_ji = M_ij for j > i). Same wave-per-row
+// batches as k_gemv; together the two passes read M once.
+template <bool UP>
+__global__ __launch_bounds__(256) void k_gemv_tri(const double* __restrict__ M, int64_t n,
+                                                  const double* __restrict__ b,
+                                                  double* __restrict__ x, const int32_t* done) {
+  if (done && *done) return;
+  const int64_t row = blockIdx.x * 4ll + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const double* r = M + row * n;
+  const int64_t j0 = UP ? row : 0, j1 = UP ? n : row + 1;
+  double s = 0.0;
+  for (int64_t j = j0 + lane; j < j1; j += 8 * 64) {
+    double m[8], v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t k = j + u * 64;
+      m[u] = k < j1 ? r[k] : 0.0;
+      v[u] = k < j1 ? b[k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += m[u] * v[u];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) x[row] = s;
+}
+
+// M's strict upper triangle <- the transpose of its strict lower one, 32 x 32 tiles through LDS
+// (a workgroup per lower tile: coalesced reads along rows, coalesced writes along rows)
+__global__ __launch_bounds__(256) void k_sym_upper(double* __restrict__ M, int64_t n) {
+  __shared__ double t[32][33];
+  const int64_t bi = blockIdx.y, bj = blockIdx.x;
+  if (bj > bi) return;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < 32; r += 8) {
+    const int64_t i = bi * 32 + r, j = bj * 32 + tx;
+    t[r][tx] = (i < n && j < n && j < i) ? M[i * n + j] : 0.0;
+  }
+  __syncthreads();
+  for (int c = ty; c < 32; c += 8) {
+    const int64_t i = bj * 32 + c, j = bi * 32 + tx;  // (i, j) = transposed (j, i), j > i
+    if (i < n && j < n && j > i) M[i * n + j] = t[tx][c];
+  }
+}
+
 // ------------------------------------------------------------ inverse Cholesky factor
 constexpr int kNB = 32;
 typedef double d4v __attribute__((ext_vector_type(4)));
@@ -427,7 +476,8 @@ int dense_chol_inverse_batch(const DenseJob* jobs_host, int count, bool* spd, hi
 }
 
 // the inverse Cholesky path; *spd false when A is not symmetric to rounding or not SPD in
-// floating point (M destroyed, inv untouched garbage)
+// floating point (M destroyed, inv untouched garbage). inv null: no X^T X product; M keeps
+// X = L^-1 in its lower triangle and X^T in its strict upper one (method 2)
 int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t s) {
   *spd = false;
   // L21 panel + the diagonal block's L11^-1 + flags from a cached scratch slot (no per-call
@@ -463,8 +513,14 @@ int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t
     e = hipMemcpyAsync(h, flag, sizeof(int32_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e == hipSuccess && h[0] == 0) {
-      const int64_t nb = (n + 15) / 16;
-      hipLaunchKernelGGL(k_xtx, dim3((unsigned)((nb * nb + 3) / 4)), dim3(256), 0, s, M, n, inv);
+      if (inv) {
+        const int64_t nb = (n + 15) / 16;
+        hipLaunchKernelGGL(k_xtx, dim3((unsigned)((nb * nb + 3) / 4)), dim3(256), 0, s, M, n,
+                           inv);
+      } else {  // keep X and mirror it: the two triangular passes of method 2
+        const unsigned nt = (unsigned)((n + 31) / 32);
+        hipLaunchKernelGGL(k_sym_upper, dim3(nt, nt), dim3(256), 0, s, M, n);
+      }
       e = hipStreamSynchronize(s);
       *spd = e == hipSuccess;
     }
@@ -479,7 +535,14 @@ int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t
 int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int32_t* done,
                      hipStream_t s) {
   if (D->n == 0) return MLAMG_OK;
-  hipLaunchKernelGGL(k_gemv, dim3((D->n + 3) / 4), dim3(256), 0, s, D->inv, D->n, b, x, done);
+  if (D->method == 2) {
+    hipLaunchKernelGGL(k_gemv_tri<false>, dim3((D->n + 3) / 4), dim3(256), 0, s, D->inv, D->n, b,
+                       D->y, done);
+    hipLaunchKernelGGL(k_gemv_tri<true>, dim3((D->n + 3) / 4), dim3(256), 0, s, D->inv, D->n,
+                       D->y, x, done);
+  } else {
+    hipLaunchKernelGGL(k_gemv, dim3((D->n + 3) / 4), dim3(256), 0, s, D->inv, D->n, b, x, done);
+  }
   MLAMG_HIP(hipGetLastError());
   return MLAMG_OK;
 }
@@ -489,6 +552,12 @@ int dense_solve_impl(const mlamg_dense* D, const double* b, double* x, const int
 using namespace mlamg;
 
 extern "C" {
+
+// operators of at least this many rows keep the factor (method 2); MLAMG_DENSE_TRI_MIN overrides
+static int64_t dense_tri_min() {
+  const char* e = std::getenv("MLAMG_DENSE_TRI_MIN");
+  return e ? std::atoll(e) : 2048;
+}
 
 int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream) {
   MLAMG_REQUIRE(A && out, "NULL argument");
@@ -516,7 +585,31 @@ int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream) {
     set_error("dense_create: hipMalloc failed");
     return MLAMG_ENOMEM;
   }
-  if (n >= 2 * kNB && !std::getenv("MLAMG_DENSE_GJ")) {
+  if (n >= dense_tri_min() && !std::getenv("MLAMG_DENSE_GJ") &&
+      hipMalloc(&D->y, sizeof(double) * n) == hipSuccess) {
+    // large operators: the inverse Cholesky factor in place, applied as two triangular passes
+    // (no O(n^3) X^T X product; the same n^2 doubles read per solve)
+    (void)hipMemsetAsync(D->inv, 0, sizeof(double) * n * n, s);
+    hipLaunchKernelGGL(k_densify, dim3((n + 255) / 256), dim3(256), 0, s, A->indptr, A->indices,
+                       A->data, n, D->inv);
+    bool spd = false;
+    const int rc = dense_chol_inverse(D->inv, n, nullptr, &spd, s);
+    if (rc != MLAMG_OK) {
+      cleanup();
+      (void)hipFree(D->inv);
+      (void)hipFree(D->y);
+      delete D;
+      return rc;
+    }
+    if (spd) {
+      cleanup();
+      D->method = 2;
+      *out = D;
+      return MLAMG_OK;
+    }
+    (void)hipFree(D->y);  // not SPD: Gauss-Jordan below (the matrix is densified again)
+    D->y = nullptr;
+  } else if (n >= 2 * kNB && !std::getenv("MLAMG_DENSE_GJ")) {
     // inverse Cholesky factor in a scratch copy, the inverse into D->inv
     double* M = nullptr;
     if (hipMalloc(&M, sizeof(double) * n * n) == hipSuccess) {
@@ -588,6 +681,7 @@ int mlamg_dense_info(const mlamg_dense* D, int* method, int64_t* n) {
 int mlamg_dense_destroy(mlamg_dense* D) {
   if (D) {
     if (D->inv) (void)hipFree(D->inv);
+    if (D->y) (void)hipFree(D->y);
     delete D;
   }
   return MLAMG_OK;

@@ -33,7 +33,8 @@ struct mlamg_gs {
   int32_t win_rw = 0;  // rows per lane (0: no windowed sweep)
   int32_t ring_log2 = 0, win_cap = 0, win_w = 0, n_chunks = 0;
   int32_t* wcol = nullptr;
-  int32_t* d_clev = nullptr;
+  int32_t* d_clev = nullptr;  // the chunk plan (8 ints per chunk) + level starts
+  double* win_xl = nullptr;  // x in level order (the window's old-x source)
   size_t win_lds = 0;
 };
 
@@ -209,122 +210,186 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_lds(const int32_t* __restrict__
 
 // Windowed one-wave sweep for levels of <= 64 * RW rows: wave 0 walks the levels with x held by
 // level-order position in an LDS ring (a level's rows read positions at most W levels away, so
-// levels [l - W, l + W] are all a step needs); waves 1-15 meanwhile stage the next chunk of
-// levels (structure + the old x of the levels entering the window, loaded past L1) into the other
-// buffer. Consecutive levels need only a wavefront fence; a chunk ends with a workgroup barrier.
+// levels [l - W, l + W] are all a step needs); the 7 other waves meanwhile stage the next chunk
+// of levels into the other buffer: the structure (values, columns as ring slots, diagonal, b,
+// row id) and the old x of the levels entering the window, read from xl, a level-ordered copy of
+// x (one independent load per position instead of rows[p] then x[rows[p]]), every load of a
+// thread's positions issued before its first LDS store. Consecutive levels need only a wavefront
+// fence; a chunk ends with a workgroup barrier.
 // Pads point at the ring's zero slot (+0.0 products: the sum starts at +0.0 and never becomes
-// -0.0, so bitwise neutral); a zero-diagonal row is left alone, as the sequential sweep does.
-// Updated values go to the ring and to x. Same products, order and division: bitwise gs_row.
-// 256 lanes: wave 0 gets the registers of RW rows x KM slots (+ the next level's) without spills;
-// the 3 other waves stage
-constexpr int kGsWinBlock = 256;
+// -0.0, so bitwise neutral); a zero-diagonal row is left alone, as the sequential sweep does (its
+// quotient goes to the sink slot). Updated values go to the ring, to x and to xl. Same products,
+// order and division: bitwise gs_row.
+constexpr int kGsWinBlock = 512;
+#ifndef MLAMG_GSWIN_LAB  // timing variants (tools/gs_win_lab.py): 1 = no sweep, 2 = no staging
+#define MLAMG_GSWIN_LAB 0
+#endif
+constexpr int kGsWinStageU = 4;  // positions per staging thread with all loads in flight
+
+// one staging buffer of cap + 1 positions (the last: the dummy of lanes past a level's end),
+// 16-byte aligned sections: vals (cap+1) x KM | diag | b (doubles) | row (int32) | level starts
+// (cap + 2 int32) | columns (cap+1) x KM (uint16 ring slots), after a 16-byte header (levels,
+// first position, positions)
+__host__ __device__ constexpr int64_t win_a16(int64_t b) { return (b + 15) & ~int64_t(15); }
+__host__ __device__ constexpr int64_t win_buf_bytes(int64_t cap, int KM) {
+  return 16 + win_a16(8 * (cap + 1) * KM) + 2 * win_a16(8 * (cap + 1)) + win_a16(4 * (cap + 1)) +
+         win_a16(4 * (cap + 2)) + win_a16(2 * (cap + 1) * KM);
+}
+
+template <int KM>
+struct WinBuf {
+  double* v;
+  double* d;
+  double* b;
+  int32_t* r;
+  int32_t* l;
+  uint16_t* c;
+  int32_t* h;
+  __device__ WinBuf(char* base, int cap) {
+    char* p = base + 16;
+    h = reinterpret_cast<int32_t*>(base);
+    v = reinterpret_cast<double*>(p);
+    p += win_a16(8 * (int64_t)(cap + 1) * KM);
+    d = reinterpret_cast<double*>(p);
+    p += win_a16(8 * (int64_t)(cap + 1));
+    b = reinterpret_cast<double*>(p);
+    p += win_a16(8 * (int64_t)(cap + 1));
+    r = reinterpret_cast<int32_t*>(p);
+    p += win_a16(4 * (int64_t)(cap + 1));
+    l = reinterpret_cast<int32_t*>(p);
+    p += win_a16(4 * (int64_t)(cap + 2));
+    c = reinterpret_cast<uint16_t*>(p);
+  }
+};
+
+template <int KM>
+struct WinCols {  // KM uint16 slots: one 8-byte (KM 4) or 16-byte (KM 8) LDS access
+  typedef typename std::conditional<KM == 4, uint2, uint4>::type T;
+};
 
 template <int KM, int RW>
 __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restrict__ rows,
-                                                     const int32_t* __restrict__ lptr,
-                                                     int32_t nlev,
-                                                     const int32_t* __restrict__ clev,
+                                                     const int4* __restrict__ cdesc,
+                                                     const int32_t* __restrict__ wlev,
                                                      int32_t nchunks,
                                                      const int32_t* __restrict__ wcol,
                                                      const double* __restrict__ pval,
                                                      const double* __restrict__ pdiag,
                                                      const double* __restrict__ blvl,
-                                                     int ring_log2, int cap, int W,
-                                                     int iterations, double* x,
+                                                     int ring_log2, int cap,
+                                                     int iterations, double* x, double* xl,
                                                      const int32_t* done) {
   extern __shared__ double lds[];
   if (done && *done) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int RS = 1 << ring_log2, RM = RS - 1;
   double* ring = lds;  // RS slots + the zero slot (RS) + the sink slot (RS + 1)
-  // per buffer (position-major, 16-byte aligned): vals cap+1 x KM | diag | b | cols (ring slots)
-  // cap+1 x KM | target slot | row | level starts
-  // (cap + 1) x (2 KM + 4) words of doubles + (cap + 1) x (KM + 4) words of ints, in doubles
-  const int64_t buf = (((int64_t)(cap + 1) * (3 * KM + 8) + 1) / 2 + 1) & ~int64_t(1);
-  double* bufs = lds + ((RS + 2 + 1) & ~1);
+  char* bufs = reinterpret_cast<char*>(lds + ((RS + 2 + 1) & ~1));
+  const int64_t bb = win_buf_bytes(cap, KM);
   if (tid == 0) ring[RS] = 0.0;
-  auto stage = [&](int ch, double* wv, int t0, int nt) {
-    double* wd = wv + (int64_t)(cap + 1) * KM;
-    double* wb = wd + (cap + 1);
-    int32_t* wc = reinterpret_cast<int32_t*>(wb + (cap + 1));
-    int32_t* wt = wc + (int64_t)(cap + 1) * KM;
-    int32_t* wr = wt + (cap + 1);
-    int32_t* wl = wr + (cap + 1);
-    const int l0 = clev[ch], l1 = clev[ch + 1];
-    const int P0 = lptr[l0], cnt = lptr[l1] - P0;
-    for (int q = t0; q < cnt * KM; q += nt) {
-      const int32_t c = wcol[(int64_t)P0 * KM + q];
-      wc[q] = c >= 0 ? (c & RM) : RS;
-      wv[q] = pval[(int64_t)P0 * KM + q];
-    }
-    for (int q = t0; q < cnt; q += nt) {
-      const double d = pdiag[P0 + q];
-      wd[q] = d != 0.0 ? d : 1.0;
-      wb[q] = blvl[P0 + q];
-      wt[q] = d != 0.0 ? ((P0 + q) & RM) : RS + 1;  // zero diagonal: left alone (sink)
-      wr[q] = d != 0.0 ? rows[P0 + q] : -1;
-    }
-    for (int q = t0; q <= l1 - l0; q += nt) wl[q] = lptr[l0 + q] - P0;
-    if (t0 < KM) {  // the dummy position of lanes past a level's end
-      wc[cnt * KM + t0] = RS;
-      wv[cnt * KM + t0] = 0.0;
-    }
+  typedef typename WinCols<KM>::T CT;
+  auto stage = [&](int ch, char* base, int t0, int nt) {
+    WinBuf<KM> w(base, cap);
+    // the chunk's plan (host-built): levels, first position and count, the old-x range entering
+    // the window (levels [l0 + W, l1 + W) clipped; chunk 0: [0, l1 + W)) and its level starts
+    const int4 c0 = cdesc[2 * ch], c1 = cdesc[2 * ch + 1];
+    const int nl = c0.x, P0 = c0.y, cnt = c0.z, X0 = c0.w, xcnt = c1.x, woff = c1.y;
     if (t0 == 0) {
-      wd[cnt] = 1.0;
-      wb[cnt] = 0.0;
-      wt[cnt] = RS + 1;
-      wr[cnt] = -1;
+      w.h[0] = nl;
+      w.h[1] = P0;
+      w.h[2] = cnt;
     }
-    // the old x of the levels entering the window with this chunk (past L1: the previous
-    // sweep of this launch wrote them from wave 0)
-    const int la = ch == 0 ? 0 : min(nlev, l0 + W), lb = min(nlev, l1 + W);
-    for (int p = lptr[la] + t0; p < lptr[lb]; p += nt)
-      ring[p & RM] = __hip_atomic_load(x + rows[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int tot = max(cnt + 1, xcnt);
+    for (int q0 = t0; q0 < tot; q0 += nt * kGsWinStageU) {
+      double v[kGsWinStageU][KM], d[kGsWinStageU], bv[kGsWinStageU], xo[kGsWinStageU];
+      int32_t c[kGsWinStageU][KM], r[kGsWinStageU], ls[kGsWinStageU];
+#pragma unroll
+      for (int u = 0; u < kGsWinStageU; ++u) {
+        const int q = q0 + u * nt;
+        ls[u] = wlev[woff + min(q, nl)];
+        const bool in = q < cnt;
+        const int64_t pp = in ? (int64_t)(P0 + q) : 0;
+#pragma unroll
+        for (int k = 0; k < KM; k += 4) {
+          const int4 c4 = *reinterpret_cast<const int4*>(wcol + pp * KM + k);
+          c[u][k] = c4.x;
+          c[u][k + 1] = c4.y;
+          c[u][k + 2] = c4.z;
+          c[u][k + 3] = c4.w;
+        }
+#pragma unroll
+        for (int k = 0; k < KM; k += 2) {
+          const double2 v2 = *reinterpret_cast<const double2*>(pval + pp * KM + k);
+          v[u][k] = v2.x;
+          v[u][k + 1] = v2.y;
+        }
+        d[u] = pdiag[pp];
+        bv[u] = blvl[pp];
+        r[u] = rows[pp];
+        // written by wave 0 in the previous sweep of this launch: past L1
+        xo[u] = q < xcnt ? __hip_atomic_load(xl + X0 + q, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+                         : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kGsWinStageU; ++u) {
+        const int q = q0 + u * nt;
+        if (q <= cnt) {
+          const bool dummy = q == cnt;  // lanes past a level's end: zero slots, sink target
+          uint16_t cs[KM];
+#pragma unroll
+          for (int k = 0; k < KM; ++k)
+            cs[k] = (uint16_t)(!dummy && c[u][k] >= 0 ? (c[u][k] & RM) : RS);
+          *reinterpret_cast<CT*>(w.c + (int64_t)q * KM) = *reinterpret_cast<const CT*>(cs);
+#pragma unroll
+          for (int k = 0; k < KM; k += 2) {
+            double2 v2;
+            v2.x = dummy ? 0.0 : v[u][k];
+            v2.y = dummy ? 0.0 : v[u][k + 1];
+            *reinterpret_cast<double2*>(w.v + (int64_t)q * KM + k) = v2;
+          }
+          w.d[q] = dummy ? 0.0 : d[u];
+          w.b[q] = dummy ? 0.0 : bv[u];
+          w.r[q] = r[u];
+        }
+        if (q < xcnt) ring[(X0 + q) & RM] = xo[u];
+        if (q <= nl) w.l[q] = ls[u];
+      }
+    }
   };
   for (int it = 0; it < iterations; ++it) {
     stage(0, bufs, tid, kGsWinBlock);
     __syncthreads();
     for (int ch = 0; ch < nchunks; ++ch) {
-      double* cur = bufs + (ch & 1) * buf;
-      if (tid < 64) {
-        const double* sv = cur;
-        const double* sd = sv + (int64_t)(cap + 1) * KM;
-        const double* sb = sd + (cap + 1);
-        const int32_t* sc = reinterpret_cast<const int32_t*>(sb + (cap + 1));
-        const int32_t* st = sc + (int64_t)(cap + 1) * KM;
-        const int32_t* sr = st + (cap + 1);
-        const int32_t* sl = sr + (cap + 1);
-        const int nl = clev[ch + 1] - clev[ch];
-        const int cnt = sl[nl];
-        int c[RW][KM], tg[RW], rw[RW];
+      char* cur = bufs + (MLAMG_GSWIN_LAB == 2 ? 0 : (ch & 1) * bb);
+      if (tid < 64 && MLAMG_GSWIN_LAB != 1) {
+        const WinBuf<KM> w(cur, cap);
+        const int nl = w.h[0], P0 = w.h[1], cnt = w.h[2];
+        int c[RW][KM], p[RW], rw[RW];
         double v[RW][KM], d[RW], bv[RW];
-        auto load = [&](int l, int (&cc)[RW][KM], double (&vv)[RW][KM], double* dd, double* bb,
-                        int* tt, int* rr) {
-          const int a = sl[l], z = sl[l + 1];
+        auto load = [&](int l, int (&cc)[RW][KM], double (&vv)[RW][KM], double* dd, double* bq,
+                        int* pq, int* rr) {
+          const int a = w.l[l], z = w.l[l + 1];
 #pragma unroll
           for (int u = 0; u < RW; ++u) {
-            const int p = a + lane + 64 * u < z ? a + lane + 64 * u : cnt;
+            const int q = a + lane + 64 * u < z ? a + lane + 64 * u : cnt;
+            const CT c4 = *reinterpret_cast<const CT*>(w.c + (int64_t)q * KM);
+            const uint16_t* cs = reinterpret_cast<const uint16_t*>(&c4);
 #pragma unroll
-            for (int k = 0; k < KM; k += 4) {
-              const int4 c4 = *reinterpret_cast<const int4*>(sc + (int64_t)p * KM + k);
-              cc[u][k] = c4.x;
-              cc[u][k + 1] = c4.y;
-              cc[u][k + 2] = c4.z;
-              cc[u][k + 3] = c4.w;
-            }
+            for (int k = 0; k < KM; ++k) cc[u][k] = cs[k];
 #pragma unroll
             for (int k = 0; k < KM; k += 2) {
-              const double2 v2 = *reinterpret_cast<const double2*>(sv + (int64_t)p * KM + k);
+              const double2 v2 = *reinterpret_cast<const double2*>(w.v + (int64_t)q * KM + k);
               vv[u][k] = v2.x;
               vv[u][k + 1] = v2.y;
             }
-            dd[u] = sd[p];
-            bb[u] = sb[p];
-            tt[u] = st[p];
-            rr[u] = sr[p];
+            dd[u] = w.d[q];
+            bq[u] = w.b[q];
+            rr[u] = w.r[q];
+            pq[u] = q;
           }
         };
-        load(0, c, v, d, bv, tg, rw);
+        load(0, c, v, d, bv, p, rw);
         #pragma unroll 1
         for (int l = 0; l < nl; ++l) {
           double g[RW][KM];
@@ -332,18 +397,28 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
           for (int u = 0; u < RW; ++u)
 #pragma unroll
             for (int k = 0; k < KM; ++k) g[u][k] = ring[c[u][k]];
-          int c2[RW][KM], tg2[RW], rw2[RW];
+          int c2[RW][KM], p2[RW], rw2[RW];
           double v2[RW][KM], d2[RW], bv2[RW];
-          load(l + 1 < nl ? l + 1 : l, c2, v2, d2, bv2, tg2, rw2);
+          load(l + 1 < nl ? l + 1 : l, c2, v2, d2, bv2, p2, rw2);
+          // the RW rows' sums and divisions first, as one block (their dependency chains
+          // interleave), then the stores
+          double xi[RW];
 #pragma unroll
           for (int u = 0; u < RW; ++u) {
             double y = 0.0;
 #pragma unroll
             for (int k = 0; k < KM; ++k) y += v[u][k] * g[u][k];
-            const double xi = (bv[u] - y) / d[u];
-            ring[tg[u]] = xi;
-            if (rw[u] >= 0) x[rw[u]] = xi;
+            xi[u] = (bv[u] - y) / d[u];
           }
+#pragma unroll
+          for (int u = 0; u < RW; ++u)  // zero diagonal (and the dummy): left alone
+            ring[d[u] != 0.0 ? ((P0 + p[u]) & RM) : RS + 1] = xi[u];
+#pragma unroll
+          for (int u = 0; u < RW; ++u)
+            if (d[u] != 0.0) {
+              x[rw[u]] = xi[u];
+              xl[P0 + p[u]] = xi[u];
+            }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -356,16 +431,16 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
             }
             d[u] = d2[u];
             bv[u] = bv2[u];
-            tg[u] = tg2[u];
+            p[u] = p2[u];
             rw[u] = rw2[u];
           }
         }
-      } else if (ch + 1 < nchunks) {
-        stage(ch + 1, bufs + ((ch + 1) & 1) * buf, tid - 64, kGsWinBlock - 64);
+      } else if (tid >= 64 && MLAMG_GSWIN_LAB != 2 && ch + 1 < nchunks) {
+        stage(ch + 1, bufs + ((ch + 1) & 1) * bb, tid - 64, kGsWinBlock - 64);
       }
       __syncthreads();
     }
-    __threadfence();  // this sweep's x stores before the next sweep's window loads
+    __threadfence();  // this sweep's x / xl stores before the next sweep's window loads
     __syncthreads();
   }
 }
@@ -401,6 +476,19 @@ static void launch_gs_pipe(const mlamg_gs* G, double* x, const double* b, int it
                      done);
 }
 
+__global__ void k_gs_win_prep(const int32_t* __restrict__ rows, int64_t n,
+                              const double* __restrict__ b, double* __restrict__ blvl,
+                              const double* __restrict__ x, double* __restrict__ xl,
+                              const int32_t* done) {
+  if (done && *done) return;
+  const int64_t p = blockIdx.x * 256ll + threadIdx.x;
+  if (p < n) {
+    const int32_t i = rows[p];
+    blvl[p] = b[i];
+    xl[p] = x[i];
+  }
+}
+
 static bool gs_win_disabled() {  // MLAMG_GS_NO_WIN=1: A/B runs, tests
   const char* e = std::getenv("MLAMG_GS_NO_WIN");
   return e && e[0] == '1';
@@ -410,12 +498,12 @@ template <int KM, int RW>
 static void launch_gs_win(const mlamg_gs* G, double* x, const double* b, int iterations,
                           const int32_t* done, hipStream_t s) {
   const int64_t n = G->A->n_rows;
-  hipLaunchKernelGGL(k_gs_b_level, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
-                     n, b, G->b_lvl, done);
+  hipLaunchKernelGGL(k_gs_win_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
+                     n, b, G->b_lvl, x, G->win_xl, done);
   hipLaunchKernelGGL((k_gs_win<KM, RW>), dim3(1), dim3(kGsWinBlock), G->win_lds, s, G->rows,
-                     G->d_level_ptr, G->n_levels, G->d_clev, G->n_chunks, G->wcol, G->pk_val,
-                     G->pk_diag, G->b_lvl, G->ring_log2, G->win_cap, G->win_w, iterations, x,
-                     done);
+                     reinterpret_cast<const int4*>(G->d_clev), G->d_clev + 8 * G->n_chunks,
+                     G->n_chunks, G->wcol, G->pk_val, G->pk_diag, G->b_lvl, G->ring_log2,
+                     G->win_cap, iterations, x, G->win_xl, done);
 }
 
 int64_t gs_rows(const mlamg_gs* G) { return G->A->n_rows; }
@@ -485,8 +573,7 @@ static void setup_window(mlamg_gs* G, const std::vector<int32_t>& ip,
       if (ij[k] != i) W = std::max(W, std::abs(level[ij[k]] - level[i]));
   const std::vector<int32_t>& lp = G->level_ptr;
   const size_t budget = 150 * 1024;
-  const size_t per_pos = (size_t)(12 * K + 32);
-  for (int cap = 4096; cap >= G->max_level_rows; cap = cap * 3 / 4) {
+  for (int cap = 4096; cap >= G->max_level_rows; cap = cap * 7 / 8) {
     std::vector<int32_t> clev{0};
     for (int l = 0; l < nlev;) {
       const int start = l;
@@ -503,20 +590,39 @@ static void setup_window(mlamg_gs* G, const std::vector<int32_t>& ip,
     int lg = 0;
     while ((int64_t(1) << lg) < span) ++lg;
     const size_t ring = ((size_t(1) << lg) + 4) * 8;
-    const size_t bufs = 2 * ((size_t)(cap + 1) * per_pos + 32);
+    const size_t bufs = 2 * (size_t)win_buf_bytes(cap, K);
     if (ring + bufs > budget) continue;
+    // per chunk: {levels, first position, positions, old-x start} {old-x count, level-start
+    // offset, -, -}, then every chunk's level starts relative to its first position
+    std::vector<int32_t> plan(8 * (size_t)nch);
+    for (int ch = 0; ch < nch; ++ch) {
+      const int l0 = clev[ch], l1 = clev[ch + 1];
+      const int la = ch == 0 ? 0 : std::min(nlev, l0 + W), lb = std::min(nlev, l1 + W);
+      int32_t* d = plan.data() + 8 * (size_t)ch;
+      d[0] = l1 - l0;
+      d[1] = lp[l0];
+      d[2] = lp[l1] - lp[l0];
+      d[3] = lp[la];
+      d[4] = lp[lb] - lp[la];
+      d[5] = (int32_t)plan.size() - 8 * nch;
+      for (int l = l0; l <= l1; ++l) plan.push_back(lp[l] - lp[l0]);
+    }
     std::vector<int32_t> pos(n), wcol((size_t)n * K, -1);
     for (int64_t p = 0; p < n; ++p) pos[rows[p]] = (int32_t)p;
     for (size_t q = 0; q < (size_t)n * K; ++q)
       if (pcol[q] >= 0) wcol[q] = pos[pcol[q]];
     if (hipMalloc(&G->wcol, sizeof(int32_t) * std::max<size_t>((size_t)n * K, 1)) != hipSuccess ||
-        hipMalloc(&G->d_clev, sizeof(int32_t) * clev.size()) != hipSuccess) {
-      if (G->wcol) (void)hipFree(G->wcol);
+        hipMalloc(&G->d_clev, sizeof(int32_t) * plan.size()) != hipSuccess ||
+        hipMalloc(&G->win_xl, sizeof(double) * std::max<int64_t>(n, 1)) != hipSuccess) {
+      for (void* q : {(void*)G->wcol, (void*)G->d_clev, (void*)G->win_xl})
+        if (q) (void)hipFree(q);
       G->wcol = nullptr;
+      G->d_clev = nullptr;
+      G->win_xl = nullptr;
       return;
     }
     (void)hipMemcpy(G->wcol, wcol.data(), sizeof(int32_t) * (size_t)n * K, hipMemcpyHostToDevice);
-    (void)hipMemcpy(G->d_clev, clev.data(), sizeof(int32_t) * clev.size(), hipMemcpyHostToDevice);
+    (void)hipMemcpy(G->d_clev, plan.data(), sizeof(int32_t) * plan.size(), hipMemcpyHostToDevice);
     G->win_w = W;
     G->win_cap = cap;
     G->ring_log2 = lg;
@@ -634,7 +740,8 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
 int mlamg_gs_destroy(mlamg_gs* G) {
   if (G) {
     for (void* q : {(void*)G->rows, (void*)G->d_level_ptr, (void*)G->pk_col, (void*)G->pk_val,
-                    (void*)G->pk_diag, (void*)G->b_lvl, (void*)G->wcol, (void*)G->d_clev})
+                    (void*)G->pk_diag, (void*)G->b_lvl, (void*)G->wcol, (void*)G->d_clev,
+                    (void*)G->win_xl})
       if (q) (void)hipFree(q);
     delete G;
   }

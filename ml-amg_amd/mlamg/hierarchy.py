@@ -364,7 +364,7 @@ class Hierarchy:
     DENSE_MAX = 4096
     # the reference's two-level solve factors A_H once for ~30 cycles: there the O(n_c^3) dense
     # factor (device-wide, fp64 matrix cores) beats a PCG solve per cycle up to larger n_c
-    TWO_LEVEL_DENSE_MAX = 12288
+    TWO_LEVEL_DENSE_MAX = 10240
     COARSE_RTOL = 1e-12
 
     def _finalize(self, nu_pre, nu_post, dense_max=None, coarse_rtol=None):

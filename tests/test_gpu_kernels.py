@@ -285,12 +285,12 @@ def test_dense_coarse_solve(golden, ml, torch_cuda):
     assert np.allclose(host(x), ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
 
 
-@pytest.mark.parametrize("n", (64, 97, 300, 1025))
+@pytest.mark.parametrize("n", (64, 97, 300, 1025, 2100))
 def test_dense_inverse_cholesky(ml, torch_cuda, n):
     """Symmetric positive definite coarse operators take the device-wide inverse Cholesky
-    factor (dense.hip: 32-column panels, MFMA trailing updates, A^-1 = X^T X); an unsymmetric
-    one takes Gauss-Jordan. Both against numpy's inverse at fp64 tolerance (sizes straddle the
-    panel and tile edges)."""
+    factor (dense.hip: 32-column panels, MFMA trailing updates, A^-1 = X^T X, or from 2048 rows
+    the factor kept and applied as X^T (X b)); an unsymmetric one takes Gauss-Jordan. Both
+    against numpy's inverse at fp64 tolerance (sizes straddle the panel and tile edges)."""
     torch = torch_cuda
     import ctypes
     from mlamg._lib import call, ptr, stream_ptr
@@ -298,7 +298,7 @@ def test_dense_inverse_cholesky(ml, torch_cuda, n):
     B = sp.random(n, n, density=min(1.0, 12.0 / n), random_state=rs, format="csr")
     S = (B + B.T).tocsr()
     A = (S + sp.diags(np.asarray(abs(S).sum(axis=1)).ravel() + 1.0)).tocsr()  # SPD (diag. dom.)
-    for M, method in ((A, 1), ((A + sp.triu(B, 1) * 0.5).tocsr(), 0)):
+    for M, method in ((A, 1 if n < 2048 else 2), ((A + sp.triu(B, 1) * 0.5).tocsr(), 0)):
         Md = ml.sparse.DeviceCSR.from_scipy(M)
         h = ctypes.c_void_p()
         call("mlamg_dense_create", Md.handle, ctypes.byref(h), stream_ptr())
