@@ -30,7 +30,7 @@ struct mlamg_gs {
   // windowed one-wave sweep (k_gs_win): x by level-order position in an LDS ring of 2^ring_log2
   // slots; wcol = the packed columns as positions (pads -1); chunks of levels staged into two
   // LDS buffers of win_cap + 1 positions; win_w = the widest level distance of a coupling
-  int32_t win_rw = 0;  // rows per lane (0: no windowed sweep)
+  int32_t win_rw = 0;  // 64-row slots per level (0: no windowed sweep)
   int32_t ring_log2 = 0, win_cap = 0, win_w = 0, n_chunks = 0;
   int32_t* wcol = nullptr;
   int32_t* d_clev = nullptr;  // the chunk plan (8 ints per chunk) + level starts
@@ -218,7 +218,8 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_lds(const int32_t* __restrict__
 // fence; a chunk ends with a workgroup barrier.
 // Pads point at the ring's zero slot (+0.0 products: the sum starts at +0.0 and never becomes
 // -0.0, so bitwise neutral); a zero-diagonal row is left alone, as the sequential sweep does (its
-// quotient goes to the sink slot). Updated values go to the ring, to x and to xl. Same products,
+// quotient goes to the sink slot). Updated values go to the ring and to xl (copied back to x by
+// one coalesced pass after the launch: no scattered stores in the sweep). Same products,
 // order and division: bitwise gs_row.
 constexpr int kGsWinBlock = 512;
 #ifndef MLAMG_GSWIN_LAB  // timing variants (tools/gs_win_lab.py): 1 = no sweep, 2 = no staging
@@ -227,13 +228,13 @@ constexpr int kGsWinBlock = 512;
 constexpr int kGsWinStageU = 4;  // positions per staging thread with all loads in flight
 
 // one staging buffer of cap + 1 positions (the last: the dummy of lanes past a level's end),
-// 16-byte aligned sections: vals (cap+1) x KM | diag | b (doubles) | row (int32) | level starts
+// 16-byte aligned sections: vals (cap+1) x KM | diag | b (doubles) | level starts
 // (cap + 2 int32) | columns (cap+1) x KM (uint16 ring slots), after a 16-byte header (levels,
 // first position, positions)
 __host__ __device__ constexpr int64_t win_a16(int64_t b) { return (b + 15) & ~int64_t(15); }
 __host__ __device__ constexpr int64_t win_buf_bytes(int64_t cap, int KM) {
-  return 16 + win_a16(8 * (cap + 1) * KM) + 2 * win_a16(8 * (cap + 1)) + win_a16(4 * (cap + 1)) +
-         win_a16(4 * (cap + 2)) + win_a16(2 * (cap + 1) * KM);
+  return 16 + win_a16(8 * (cap + 1) * KM) + 2 * win_a16(8 * (cap + 1)) + win_a16(4 * (cap + 2)) +
+         win_a16(2 * (cap + 1) * KM);
 }
 
 template <int KM>
@@ -241,7 +242,6 @@ struct WinBuf {
   double* v;
   double* d;
   double* b;
-  int32_t* r;
   int32_t* l;
   uint16_t* c;
   int32_t* h;
@@ -254,8 +254,6 @@ struct WinBuf {
     p += win_a16(8 * (int64_t)(cap + 1));
     b = reinterpret_cast<double*>(p);
     p += win_a16(8 * (int64_t)(cap + 1));
-    r = reinterpret_cast<int32_t*>(p);
-    p += win_a16(4 * (int64_t)(cap + 1));
     l = reinterpret_cast<int32_t*>(p);
     p += win_a16(4 * (int64_t)(cap + 2));
     c = reinterpret_cast<uint16_t*>(p);
@@ -267,9 +265,8 @@ struct WinCols {  // KM uint16 slots: one 8-byte (KM 4) or 16-byte (KM 8) LDS ac
   typedef typename std::conditional<KM == 4, uint2, uint4>::type T;
 };
 
-template <int KM, int RW>
-__global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restrict__ rows,
-                                                     const int4* __restrict__ cdesc,
+template <int KM, int RW, int CW>
+__global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int4* __restrict__ cdesc,
                                                      const int32_t* __restrict__ wlev,
                                                      int32_t nchunks,
                                                      const int32_t* __restrict__ wcol,
@@ -277,14 +274,18 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
                                                      const double* __restrict__ pdiag,
                                                      const double* __restrict__ blvl,
                                                      int ring_log2, int cap,
-                                                     int iterations, double* x, double* xl,
+                                                     int iterations, double* xl,
                                                      const int32_t* done) {
   extern __shared__ double lds[];
   if (done && *done) return;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int RS = 1 << ring_log2, RM = RS - 1;
   double* ring = lds;  // RS slots + the zero slot (RS) + the sink slot (RS + 1)
-  char* bufs = reinterpret_cast<char*>(lds + ((RS + 2 + 1) & ~1));
+  // the sweeping waves' level counters (CW > 1), then the staging buffers
+  int32_t* flags = reinterpret_cast<int32_t*>(lds + RS + 2);
+  char* bufs = reinterpret_cast<char*>(lds + ((RS + 4 + 1) & ~1));
+  if (tid < 4) flags[tid] = 0;
+  int seq = 0;
   const int64_t bb = win_buf_bytes(cap, KM);
   if (tid == 0) ring[RS] = 0.0;
   typedef typename WinCols<KM>::T CT;
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
     const int tot = max(cnt + 1, xcnt);
     for (int q0 = t0; q0 < tot; q0 += nt * kGsWinStageU) {
       double v[kGsWinStageU][KM], d[kGsWinStageU], bv[kGsWinStageU], xo[kGsWinStageU];
-      int32_t c[kGsWinStageU][KM], r[kGsWinStageU], ls[kGsWinStageU];
+      int32_t c[kGsWinStageU][KM], ls[kGsWinStageU];
 #pragma unroll
       for (int u = 0; u < kGsWinStageU; ++u) {
         const int q = q0 + u * nt;
@@ -325,7 +326,6 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
         }
         d[u] = pdiag[pp];
         bv[u] = blvl[pp];
-        r[u] = rows[pp];
         // written by wave 0 in the previous sweep of this launch: past L1
         xo[u] = q < xcnt ? __hip_atomic_load(xl + X0 + q, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT)
@@ -350,7 +350,6 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
           }
           w.d[q] = dummy ? 0.0 : d[u];
           w.b[q] = dummy ? 0.0 : bv[u];
-          w.r[q] = r[u];
         }
         if (q < xcnt) ring[(X0 + q) & RM] = xo[u];
         if (q <= nl) w.l[q] = ls[u];
@@ -362,17 +361,18 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
     __syncthreads();
     for (int ch = 0; ch < nchunks; ++ch) {
       char* cur = bufs + (MLAMG_GSWIN_LAB == 2 ? 0 : (ch & 1) * bb);
-      if (tid < 64 && MLAMG_GSWIN_LAB != 1) {
+      if (tid < 64 * CW && MLAMG_GSWIN_LAB != 1) {
         const WinBuf<KM> w(cur, cap);
         const int nl = w.h[0], P0 = w.h[1], cnt = w.h[2];
-        int c[RW][KM], p[RW], rw[RW];
+        int c[RW][KM], p[RW];
         double v[RW][KM], d[RW], bv[RW];
         auto load = [&](int l, int (&cc)[RW][KM], double (&vv)[RW][KM], double* dd, double* bq,
-                        int* pq, int* rr) {
+                        int* pq) {
           const int a = w.l[l], z = w.l[l + 1];
 #pragma unroll
           for (int u = 0; u < RW; ++u) {
-            const int q = a + lane + 64 * u < z ? a + lane + 64 * u : cnt;
+            const int q0 = a + lane + 64 * (wv + CW * u);
+            const int q = q0 < z ? q0 : cnt;
             const CT c4 = *reinterpret_cast<const CT*>(w.c + (int64_t)q * KM);
             const uint16_t* cs = reinterpret_cast<const uint16_t*>(&c4);
 #pragma unroll
@@ -385,11 +385,10 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
             }
             dd[u] = w.d[q];
             bq[u] = w.b[q];
-            rr[u] = w.r[q];
             pq[u] = q;
           }
         };
-        load(0, c, v, d, bv, p, rw);
+        load(0, c, v, d, bv, p);
         #pragma unroll 1
         for (int l = 0; l < nl; ++l) {
           double g[RW][KM];
@@ -397,9 +396,9 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
           for (int u = 0; u < RW; ++u)
 #pragma unroll
             for (int k = 0; k < KM; ++k) g[u][k] = ring[c[u][k]];
-          int c2[RW][KM], p2[RW], rw2[RW];
+          int c2[RW][KM], p2[RW];
           double v2[RW][KM], d2[RW], bv2[RW];
-          load(l + 1 < nl ? l + 1 : l, c2, v2, d2, bv2, p2, rw2);
+          load(l + 1 < nl ? l + 1 : l, c2, v2, d2, bv2, p2);
           // the RW rows' sums and divisions first, as one block (their dependency chains
           // interleave), then the stores
           double xi[RW];
@@ -415,13 +414,26 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
             ring[d[u] != 0.0 ? ((P0 + p[u]) & RM) : RS + 1] = xi[u];
 #pragma unroll
           for (int u = 0; u < RW; ++u)
-            if (d[u] != 0.0) {
-              x[rw[u]] = xi[u];
-              xl[P0 + p[u]] = xi[u];
-            }
+            if (d[u] != 0.0) xl[P0 + p[u]] = xi[u];
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (CW > 1) {
+            // the level's other sweeping waves: a wave's LDS operations complete in issue
+            // order, so a counter stored after the ring stores is seen after them; the spin
+            // reads all counters until each has reached this level
+            ++seq;
+            asm volatile("" ::: "memory");
+            if (lane == 0) *reinterpret_cast<volatile int32_t*>(flags + wv) = seq;
+            for (;;) {
+              bool ok = true;
+#pragma unroll
+              for (int w2 = 0; w2 < CW; ++w2)
+                ok = ok && *reinterpret_cast<volatile int32_t*>(flags + w2) >= seq;
+              if (ok) break;
+            }
+            asm volatile("" ::: "memory");
+          }
 #pragma unroll
           for (int u = 0; u < RW; ++u) {
 #pragma unroll
@@ -432,15 +444,14 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int32_t* __restric
             d[u] = d2[u];
             bv[u] = bv2[u];
             p[u] = p2[u];
-            rw[u] = rw2[u];
           }
         }
-      } else if (tid >= 64 && MLAMG_GSWIN_LAB != 2 && ch + 1 < nchunks) {
-        stage(ch + 1, bufs + ((ch + 1) & 1) * bb, tid - 64, kGsWinBlock - 64);
+      } else if (tid >= 64 * CW && MLAMG_GSWIN_LAB != 2 && ch + 1 < nchunks) {
+        stage(ch + 1, bufs + ((ch + 1) & 1) * bb, tid - 64 * CW, kGsWinBlock - 64 * CW);
       }
       __syncthreads();
     }
-    __threadfence();  // this sweep's x / xl stores before the next sweep's window loads
+    __threadfence();  // this sweep's xl stores before the next sweep's window loads
     __syncthreads();
   }
 }
@@ -476,6 +487,16 @@ static void launch_gs_pipe(const mlamg_gs* G, double* x, const double* b, int it
                      done);
 }
 
+// x <- xl after the window sweeps (rows in level order: coalesced reads of xl; a zero-diagonal
+// row's xl still holds its old x)
+__global__ void k_gs_win_post(const int32_t* __restrict__ rows, int64_t n,
+                              const double* __restrict__ xl, double* __restrict__ x,
+                              const int32_t* done) {
+  if (done && *done) return;
+  const int64_t p = blockIdx.x * 256ll + threadIdx.x;
+  if (p < n) x[rows[p]] = xl[p];
+}
+
 __global__ void k_gs_win_prep(const int32_t* __restrict__ rows, int64_t n,
                               const double* __restrict__ b, double* __restrict__ blvl,
                               const double* __restrict__ x, double* __restrict__ xl,
@@ -494,16 +515,18 @@ static bool gs_win_disabled() {  // MLAMG_GS_NO_WIN=1: A/B runs, tests
   return e && e[0] == '1';
 }
 
-template <int KM, int RW>
+template <int KM, int RW, int CW>
 static void launch_gs_win(const mlamg_gs* G, double* x, const double* b, int iterations,
                           const int32_t* done, hipStream_t s) {
   const int64_t n = G->A->n_rows;
   hipLaunchKernelGGL(k_gs_win_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
                      n, b, G->b_lvl, x, G->win_xl, done);
-  hipLaunchKernelGGL((k_gs_win<KM, RW>), dim3(1), dim3(kGsWinBlock), G->win_lds, s, G->rows,
+  hipLaunchKernelGGL((k_gs_win<KM, RW, CW>), dim3(1), dim3(kGsWinBlock), G->win_lds, s,
                      reinterpret_cast<const int4*>(G->d_clev), G->d_clev + 8 * G->n_chunks,
                      G->n_chunks, G->wcol, G->pk_val, G->pk_diag, G->b_lvl, G->ring_log2,
-                     G->win_cap, iterations, x, G->win_xl, done);
+                     G->win_cap, iterations, G->win_xl, done);
+  hipLaunchKernelGGL(k_gs_win_post, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
+                     n, G->win_xl, x, done);
 }
 
 int64_t gs_rows(const mlamg_gs* G) { return G->A->n_rows; }
@@ -514,16 +537,23 @@ int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
   if (A->n_rows == 0 || iterations <= 0) return MLAMG_OK;
   const bool pipe = G->pk_k > 0 && G->n_levels > 4;
   if (pipe && G->win_rw > 0 && !gs_win_disabled()) {
+    // win_rw = 64-row slots per level: up to 4 sweeping waves, then 2 rows per lane
     if (G->pk_k == 4) {
       switch (G->win_rw) {
-        case 1: launch_gs_win<4, 1>(G, x, b, iterations, done, s); break;
-        case 2: launch_gs_win<4, 2>(G, x, b, iterations, done, s); break;
-        case 3: launch_gs_win<4, 3>(G, x, b, iterations, done, s); break;
-        default: launch_gs_win<4, 4>(G, x, b, iterations, done, s); break;
+        case 1: launch_gs_win<4, 1, 1>(G, x, b, iterations, done, s); break;
+        case 2: launch_gs_win<4, 1, 2>(G, x, b, iterations, done, s); break;
+        case 3: launch_gs_win<4, 1, 3>(G, x, b, iterations, done, s); break;
+        case 4: launch_gs_win<4, 1, 4>(G, x, b, iterations, done, s); break;
+        default: launch_gs_win<4, 2, 4>(G, x, b, iterations, done, s); break;
       }
     } else {
-      if (G->win_rw == 1) launch_gs_win<8, 1>(G, x, b, iterations, done, s);
-      else launch_gs_win<8, 2>(G, x, b, iterations, done, s);
+      switch (G->win_rw) {
+        case 1: launch_gs_win<8, 1, 1>(G, x, b, iterations, done, s); break;
+        case 2: launch_gs_win<8, 1, 2>(G, x, b, iterations, done, s); break;
+        case 3: launch_gs_win<8, 1, 3>(G, x, b, iterations, done, s); break;
+        case 4: launch_gs_win<8, 1, 4>(G, x, b, iterations, done, s); break;
+        default: launch_gs_win<8, 2, 4>(G, x, b, iterations, done, s); break;
+      }
     }
   } else if (pipe && G->max_level_rows <= 2 * kGsBlock) {
     const bool one = G->max_level_rows <= kGsBlock;
@@ -564,9 +594,8 @@ static void setup_window(mlamg_gs* G, const std::vector<int32_t>& ip,
                          int K) {
   const int64_t n = G->A->n_rows;
   const int nlev = G->n_levels;
-  const int rw_max = K == 4 ? 4 : 2;
-  const int rw = (G->max_level_rows + 63) / 64;
-  if (rw < 1 || rw > rw_max || nlev <= 4) return;
+  const int rw = (G->max_level_rows + 63) / 64;  // 64-row slots: <= 4 waves x 2 rows per lane
+  if (rw < 1 || rw > 8 || nlev <= 4) return;
   int W = 0;
   for (int64_t i = 0; i < n; ++i)
     for (int k = ip[i]; k < ip[i + 1]; ++k)

@@ -344,14 +344,16 @@ def _P1(golden):
 
 @pytest.mark.parametrize("case", ("wide_levels", "grid_200", "grid_1100", "cube_24",
                                   "long_rows", "unsorted_zero_diag", "grid_60_lds", "cube_12_lds",
-                                  "grid_256", "nine_point_48"))
+                                  "grid_256", "nine_point_48", "grid_160", "grid_400",
+                                  "nine_point_300"))
 def test_gauss_seidel_both_schedules(ml, oracle, torch_cuda, case):
     """Level-scheduled GS through every schedule: the pipelined one-workgroup kernel (levels of
     <= 1024 rows: grid_200; <= 2048: grid_1100 diagonals; cube_24 planes), the plain
     one-workgroup kernel (rows with more than 8 off-diagonals), the per-level launches (a level
-    wider than 8192 rows), the windowed one-wave sweep (levels of <= 256 rows with <= 4
-    off-diagonals, <= 128 with <= 8: grid_200, grid_256, grid_60, cube_12, nine_point_48 whose
-    couplings span 2 levels, the unsorted / zero-diagonal case) — bitwise the sequential pyamg
+    wider than 8192 rows), the windowed sweep (levels of <= 512 rows with <= 8 off-diagonals on
+    1-4 sweeping waves: grid_60, cube_12, nine_point_48 whose couplings span 2 levels and the
+    unsorted / zero-diagonal case on one, nine_point_300 on 3 with 8 slots per row, grid_160
+    on 3, grid_200 and grid_256 on 4, grid_400 on 4 with 2 rows per lane) — bitwise the sequential pyamg
     sweep, including rows stored in non-ascending order, a zero diagonal (row left unchanged)
     and a duplicated diagonal entry; three sweeps per launch."""
     rs = np.random.RandomState(11)
@@ -367,8 +369,10 @@ def test_gauss_seidel_both_schedules(ml, oracle, torch_cuda, case):
         A = ml.problems.poisson_3d_7pt(24)
     elif case == "grid_256":
         A = ml.problems.poisson_2d_5pt(256)
-    elif case == "nine_point_48":
-        m = 48
+    elif case in ("grid_160", "grid_400"):
+        A = ml.problems.poisson_2d_5pt(int(case[5:]))
+    elif case in ("nine_point_48", "nine_point_300"):
+        m = int(case[11:])
         T = sp.diags([1.0, 1.0, 1.0], [-1, 0, 1], shape=(m, m))
         A = (sp.kron(T, T) * -1.0 + sp.eye(m * m) * 9.0).tocsr()
     elif case == "grid_60_lds":  # n <= 8192: x held in LDS for the whole sweep
