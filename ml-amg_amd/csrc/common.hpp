@@ -115,7 +115,8 @@ struct mlamg_csr {
   // (col - srt_base[block]) << kSrtPosBits | slot (its CSR position inside the block)
   int32_t srt_nb = 0;
   int32_t* srt_blk = nullptr;   // srt_nb+1 row boundaries
-  int32_t* srt_base = nullptr;  // per block {lo, hi, split}: column windows of the sorted entries
+  int32_t* srt_base = nullptr;  // per block {r0, r1, e0, nnz, lo, hi, split, 0}: rows, entries
+                                // and the column windows of the sorted entries
   uint32_t* srt_pk = nullptr;
   double* srt_val = nullptr;
   // value dictionary of the sorted copy (<= 256 distinct values, e.g. SA prolongators of

@@ -694,12 +694,15 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   }
   const int b = (int)xcd_block(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x;
-  const int r0 = blk[b], r1 = blk[b + 1], nr = r1 - r0;
-  const int e0 = indptr[r0];
-  const int ne = indptr[r1] - e0;
+  // the block's record {r0, r1, e0, nnz, lo, hi, split, -} in one 32-byte load: the entry
+  // stream's addresses then wait for one round trip, not two (blk, then indptr)
+  const int4 m0 = reinterpret_cast<const int4*>(base)[2 * b];
+  const int4 m1 = reinterpret_cast<const int4*>(base)[2 * b + 1];
+  const int r0 = m0.x, r1 = m0.y, nr = r1 - r0;
+  const int e0 = m0.z, ne = m0.w;
   // two column windows per block: sorted entries [0, split) are offsets from lo, the rest from
   // hi (a halo-extended local matrix has its ghost columns far from the owned ones)
-  const int lo = base[3 * b], hi = base[3 * b + 1], split = base[3 * b + 2];
+  const int lo = m1.x, hi = m1.y, split = m1.z;
   for (int t = tid; t <= nr; t += kSrtThreads) rp[t] = indptr[r0 + t] - e0;
   constexpr int RPT = kSrtRows / kSrtThreads;  // rows per thread in phase 2
   static_assert(RPT * kSrtThreads == kSrtRows, "whole rows per thread in phase 2");
@@ -723,7 +726,11 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int cb = tid + u * kSrtThreads < split ? lo : hi;
+#ifdef MLAMG_SRT_LAB_NOGATHER  // timing variant only (tools/p0r0_time.py): no x gathers
+    xv[u] = (double)(cb + (int)(w[u] >> kSrtPosBits));
+#else
     xv[u] = w[u] != kNone ? x[cb + (int)(w[u] >> kSrtPosBits)] : 0.0;
+#endif
   }
   if constexpr (VD) {
     __syncthreads();  // value table staged (the gathers above are already in flight)
@@ -1263,7 +1270,7 @@ __global__ __launch_bounds__(256) void k_srt_pack(const int32_t* __restrict__ ip
   const int a = ip[blk[b]], z = ip[blk[b + 1]];
   const int m = z - a;
   if (m == 0) {
-    if (threadIdx.x == 0) base[3 * b] = base[3 * b + 1] = base[3 * b + 2] = 0;
+    if (threadIdx.x == 0) base[8 * b + 4] = base[8 * b + 5] = base[8 * b + 6] = 0;
     return;
   }
   auto col = [&](int e) { return (int64_t)(key[a + e] & cmask); };
@@ -1291,9 +1298,9 @@ __global__ __launch_bounds__(256) void k_srt_pack(const int32_t* __restrict__ ip
   }
   const int lo = (int)col(0), hi = split < m ? (int)col(split) : lo;
   if (threadIdx.x == 0) {
-    base[3 * b] = lo;
-    base[3 * b + 1] = hi;
-    base[3 * b + 2] = split;
+    base[8 * b + 4] = lo;
+    base[8 * b + 5] = hi;
+    base[8 * b + 6] = split;
   }
   for (int e = (int)threadIdx.x; e < m; e += 256) {
     const int src = idx[a + e];
@@ -1443,7 +1450,7 @@ static int build_sorted(mlamg_csr* A, hipStream_t s) {
   };
   const size_t m = (size_t)std::max<int64_t>(nnz, 1);
   if (hipMalloc(&A->srt_blk, sizeof(int32_t) * (nb + 1)) != hipSuccess ||
-      hipMalloc(&A->srt_base, sizeof(int32_t) * 3 * std::max(nb, 1)) != hipSuccess ||
+      hipMalloc(&A->srt_base, sizeof(int32_t) * 8 * std::max(nb, 1)) != hipSuccess ||
       hipMalloc(&A->srt_pk, sizeof(uint32_t) * m) != hipSuccess ||
       hipMalloc(&A->srt_val, sizeof(double) * m) != hipSuccess ||
       hipMalloc(&k0, sizeof(uint64_t) * m) != hipSuccess ||
@@ -1452,9 +1459,19 @@ static int build_sorted(mlamg_csr* A, hipStream_t s) {
       hipMalloc(&i1, sizeof(int32_t) * m) != hipSuccess ||
       hipMalloc(&wide, sizeof(int32_t)) != hipSuccess)
     fail("out of device memory");
+  // per block {r0, r1, e0, nnz, lo, hi, split, 0}; k_srt_pack fills the column windows
+  std::vector<int32_t> meta(8 * (size_t)std::max(nb, 1), 0);
+  for (int b = 0; b < nb; ++b) {
+    meta[8 * b] = blk[b];
+    meta[8 * b + 1] = blk[b + 1];
+    meta[8 * b + 2] = ip[blk[b]];
+    meta[8 * b + 3] = ip[blk[b + 1]] - ip[blk[b]];
+  }
   if (rc == MLAMG_OK &&
       (hipMemcpyAsync(A->srt_blk, blk.data(), sizeof(int32_t) * (nb + 1), hipMemcpyHostToDevice,
                       s) != hipSuccess ||
+       hipMemcpyAsync(A->srt_base, meta.data(), sizeof(int32_t) * meta.size(),
+                      hipMemcpyHostToDevice, s) != hipSuccess ||
        hipMemsetAsync(wide, 0, sizeof(int32_t), s) != hipSuccess))
     fail("upload");
   if (rc == MLAMG_OK && nb > 0 && nnz > 0) {
@@ -2094,8 +2111,7 @@ int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
   } else if (A->rp_pid) {
     b += 1.0 * ((A->n_rows + 1) / 2) + 4.0 * 257 + 32.0 * A->rp_n_ent;  // pair ids + tables
   } else if (A->srt_pk) {
-    b += (A->srt_vi ? 5.0 : 12.0) * A->nnz + 4.0 * (n + 1) + 4.0 * (A->srt_nb + 1) +
-         12.0 * A->srt_nb;
+    b += (A->srt_vi ? 5.0 : 12.0) * A->nnz + 4.0 * (n + 1) + 32.0 * A->srt_nb;
   } else if (A->dict_code) {
     int64_t n_codes = 0;
     MLAMG_HIP(hipMemcpy(&n_codes, A->dict_ptr + A->n_slices, sizeof(int64_t), hipMemcpyDeviceToHost));
