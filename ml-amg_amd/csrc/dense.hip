@@ -189,39 +189,53 @@ __global__ __launch_bounds__(256) void k_sym_upper(double* __restrict__ M, int64
 constexpr int kNB = 32;
 typedef double d4v __attribute__((ext_vector_type(4)));
 
-// wave 0 of a workgroup: the diagonal block of panel k0 (lower part of M) into Dg (ld kNB + 1),
-// factorised L11 (right-looking, wave-synchronous), and 1/diag(L11) into rd. Returns false on a
-// non-positive pivot (same in every lane).
+// a lane's double, read by the whole wave (two 32-bit lane reads: no LDS round trip)
+__device__ __forceinline__ double read_lane(double v, int l) {
+  const int2 h = __builtin_bit_cast(int2, v);
+  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readlane(h.x, l),
+                                              __builtin_amdgcn_readlane(h.y, l)));
+}
+
+// wave 0 of a workgroup: the diagonal block of panel k0 (lower part of M) factorised L11
+// (right-looking), each lane holding its row of the block in registers and reading the other
+// rows' column-t entries by lane reads; L11 into Dg (ld kNB + 1), 1/diag(L11) into rd. Returns
+// false on a non-positive pivot (same in every lane). Per element the same operations in the
+// same order as a right-looking sweep over an LDS copy (l_rt = a_rt * (1 / sqrt(a_tt)),
+// a_rc -= l_rt l_ct), without its two wave barriers and LDS round trips per step.
 __device__ bool panel_factor(const double* __restrict__ M, int64_t n, int64_t k0, int bw,
                              double* Dg, double* rd) {
-  constexpr int ds = kNB + 1, E = kNB * kNB / 64;
+  constexpr int ds = kNB + 1;
   const int lane = threadIdx.x & 63;
-  for (int q = lane; q < kNB * kNB; q += 64) {
-    const int rr = q / kNB, cc = q % kNB;
-    Dg[rr * ds + cc] = (rr < bw && cc <= rr) ? M[(k0 + rr) * n + k0 + cc] : 0.0;
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  for (int t = 0; t < bw; ++t) {
-    const double dtt = Dg[t * ds + t];
-    if (!(dtt > 0.0)) return false;
-    // column t: l_rt = a_rt / sqrt(a_tt), one reciprocal per step (a division per element made
-    // this loop the panel launch's whole cost: ~1,000 fp64 divisions per lane)
-    const double sq = sqrt(dtt), isq = 1.0 / sq;
-    if (lane >= t && lane < bw) Dg[lane * ds + t] = lane == t ? sq : Dg[lane * ds + t] * isq;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // trailing block: a_rc -= l_rt l_ct, t < c <= r
+  const bool own = lane < bw;
+  double a[kNB];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int q = lane + 64 * e, rr = q / kNB, cc = q % kNB;
-      if (rr < bw && cc <= rr && cc > t)
-        Dg[rr * ds + cc] = Dg[rr * ds + cc] - Dg[rr * ds + t] * Dg[cc * ds + t];
+  for (int c = 0; c < kNB; ++c) a[c] = (own && c <= lane) ? M[(k0 + lane) * n + k0 + c] : 0.0;
+  bool ok = true;
+  // fully unrolled (a[] stays in registers): steps past bw or after a failed pivot do nothing
+#pragma unroll
+  for (int t = 0; t < kNB; ++t) {
+    const double dtt = read_lane(a[t], t);
+    const bool live = ok && t < bw;
+    if (live && !(dtt > 0.0)) ok = false;
+    if (live && ok) {
+      // column t: l_rt = a_rt / sqrt(a_tt), one reciprocal per step
+      const double sq = sqrt(dtt), isq = 1.0 / sq;
+      if (lane == t) a[t] = sq;
+      else if (lane > t && own) a[t] = a[t] * isq;
+      if (lane == 0) rd[t] = isq;
+      // trailing block: a_rc -= l_rt l_ct, t < c <= r
+#pragma unroll
+      for (int c = t + 1; c < kNB; ++c) {
+        const double lct = read_lane(a[t], c);
+        if (c <= lane && own && c < bw) a[c] = a[c] - a[t] * lct;
+      }
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   }
-  if (lane < bw) rd[lane] = 1.0 / Dg[lane * ds + lane];
+  if (!ok) return false;
+#pragma unroll
+  for (int c = 0; c < kNB; ++c)
+    if (lane < kNB) Dg[lane * ds + c] = (own && c <= lane) ? a[c] : 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   return true;
 }
 
@@ -238,8 +252,11 @@ __device__ __forceinline__ void chol_panel_body(double* __restrict__ M, int64_t 
   if (*fail) return;
   const int bw = (int)min<int64_t>(kNB, n - k0);
   const int64_t k1 = k0 + bw;
+#ifndef MLAMG_DENSE_LAB  // timing builds only (tools/dense_lab.py): 1 = no row part, 2 = no factor
+#define MLAMG_DENSE_LAB 0
+#endif
   if (threadIdx.x < 64) {
-    const bool ok = panel_factor(M, n, k0, bw, Dg, rd);
+    const bool ok = MLAMG_DENSE_LAB == 2 ? true : panel_factor(M, n, k0, bw, Dg, rd);
     if (threadIdx.x == 0) ok_s = ok ? 1 : 0;
   }
   __syncthreads();
@@ -249,7 +266,7 @@ __device__ __forceinline__ void chol_panel_body(double* __restrict__ M, int64_t 
   }
   constexpr int ds = kNB + 1;
   const int64_t nrows = n - k1;  // rows below: bw == kNB whenever there are any
-  const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t item = MLAMG_DENSE_LAB == 1 ? INT64_MAX / 2 : (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (item < nrows) {
     const int64_t i = k1 + item;
     double a[kNB];
