@@ -304,9 +304,13 @@ __device__ __forceinline__ void chol_panel_body(double* __restrict__ M, int64_t 
   }
 }
 
-// Trailing update of panel k0, a wave per 16 x 16 tile of rows [k1, n) x columns [0, i]:
+// Trailing update of panel k0, a wave per 32 x 32 tile (2 x 2 MFMA blocks: per k step two A and
+// two B operand loads feed four MFMAs) of rows [k1, n) x columns [0, i]:
 //   M[i, j] <- (j in [k0, k1) ? 0 : M[i, j]) - sum_t L21[i][t] W[t][j],
 //   W = the panel's rows of X (j < k1) or L21^T (j >= k1).
+// Row blocks of 32 from k1 (a multiple of 32 whenever rows remain); row block rb spans column
+// tiles 0 .. k1/32 + rb.
+constexpr int kUpd = 32;
 __device__ __forceinline__ void chol_update_body(double* __restrict__ M, int64_t n, int64_t k0,
                                                  const double* __restrict__ Lp,
                                                  const double* __restrict__ Zd,
@@ -319,43 +323,67 @@ __device__ __forceinline__ void chol_update_body(double* __restrict__ M, int64_t
       if (k0 + t < n && c <= t) M[(k0 + t) * n + k0 + c] = Zd[q];
     }
   if (k1 >= n) return;
-  const int64_t a16 = (k1 + 15) / 16, nrb = (n - k1 + 15) / 16;
-  auto C = [&](int64_t rb) { return rb * (a16 + 1) + rb * (rb - 1) / 2; };
+  const int64_t a32 = k1 / kUpd, nrb = (n - k1 + kUpd - 1) / kUpd;
+  auto C = [&](int64_t rb) { return rb * (a32 + 1) + rb * (rb - 1) / 2; };
   const int64_t T = C(nrb);
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= T) return;
   const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
-  const double bq = (double)a16 + 0.5;
+  const double bq = (double)a32 + 0.5;
   int64_t rb = (int64_t)(-bq + sqrt(bq * bq + 2.0 * (double)q));
   while (rb > 0 && C(rb) > q) --rb;
   while (C(rb + 1) <= q) ++rb;
-  const int64_t i0 = k1 + 16 * rb, j0 = 16 * (q - C(rb));
+  const int64_t i0 = k1 + kUpd * rb, j0 = kUpd * (q - C(rb));
   const int64_t last = n - k1 - 1;
-  const int64_t jc = j0 + lr;
-  const bool zero = jc >= k0 && jc < k1;
-  d4v acc;
+  d4v acc[2][2];
+  const double* arow[2];
+  const double* brow[2];
+  bool from_x[2];
+  int64_t jz[2];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int64_t i = i0 + lk + 4 * r;
-    acc[r] = (!zero && i < n && jc < n) ? M[i * n + jc] : 0.0;
+  for (int tj = 0; tj < 2; ++tj) {
+    const int64_t jc = j0 + 16 * tj + lr;
+    const bool zero = jc >= k0 && jc < k1;
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = i0 + 16 * ti + lk + 4 * r;
+        acc[ti][tj][r] = (!zero && i < n && jc < n) ? M[i * n + jc] : 0.0;
+      }
+    from_x[tj] = jc < k1;
+    brow[tj] = Lp + min(max(jc - k1, (int64_t)0), last) * kNB;
+    jz[tj] = min(jc, k1 - 1);
   }
-  const double* arow = Lp + min(i0 + lr - k1, last) * kNB;
-  const bool from_x = jc < k1;
-  const double* brow = Lp + min(max(jc - k1, (int64_t)0), last) * kNB;
-  const int64_t jz = min(jc, k1 - 1);
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti) arow[ti] = Lp + min(i0 + 16 * ti + lr - k1, last) * kNB;
 #pragma unroll
   for (int kk = 0; kk < kNB; kk += 4) {
     const int k = kk + lk;
-    const double av = -arow[k];
-    const double bv = from_x ? (jz >= k0 ? Zd[k * kNB + (jz - k0)] : M[(k0 + k) * n + jz])
-                             : brow[k];
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    double av[2], bv[2];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti) av[ti] = -arow[ti][k];
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+      bv[tj] = from_x[tj] ? (jz[tj] >= k0 ? Zd[k * kNB + (jz[tj] - k0)] : M[(k0 + k) * n + jz[tj]])
+                          : brow[tj][k];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj)
+        acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti], bv[tj], acc[ti][tj], 0, 0, 0);
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int64_t i = i0 + lk + 4 * r;
-    if (i < n && jc < n) M[i * n + jc] = acc[r];
-  }
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj) {
+      const int64_t jc = j0 + 16 * tj + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = i0 + 16 * ti + lk + 4 * r;
+        if (i < n && jc < n) M[i * n + jc] = acc[ti][tj][r];
+      }
+    }
 }
 
 // A^-1 = X^T X from X = L^-1 (lower triangle of X; its upper triangle is not read): a wave per
@@ -475,8 +503,8 @@ int dense_chol_inverse_batch(const DenseJob* jobs_host, int count, bool* spd, hi
     for (int j = 0; j < count; ++j) {
       const int64_t n = jobs[j].n, k1 = std::min<int64_t>(k0 + kNB, n);
       if (k0 >= n || k1 >= n) continue;
-      const int64_t a16 = (k1 + 15) / 16, nrb = (n - k1 + 15) / 16;
-      T = std::max<int64_t>(T, nrb * (a16 + 1) + nrb * (nrb - 1) / 2);
+      const int64_t a32 = k1 / kUpd, nrb = (n - k1 + kUpd - 1) / kUpd;
+      T = std::max<int64_t>(T, nrb * (a32 + 1) + nrb * (nrb - 1) / 2);
     }
     hipLaunchKernelGGL(k_chol_update_b, dim3((unsigned)((T + 3) / 4), cy), dim3(256), 0, s, dj,
                        k0);
@@ -521,8 +549,8 @@ int dense_chol_inverse(double* M, int64_t n, double* inv, bool* spd, hipStream_t
                          n, k0, Lp, Zd, flag);
       int64_t T = 0;
       if (k1 < n) {
-        const int64_t a16 = (k1 + 15) / 16, nrb = (n - k1 + 15) / 16;
-        T = nrb * (a16 + 1) + nrb * (nrb - 1) / 2;
+        const int64_t a32 = k1 / kUpd, nrb = (n - k1 + kUpd - 1) / kUpd;
+        T = nrb * (a32 + 1) + nrb * (nrb - 1) / 2;
       }
       hipLaunchKernelGGL(k_chol_update, dim3((unsigned)std::max<int64_t>(1, (T + 3) / 4)),
                          dim3(256), 0, s, M, n, k0, Lp, Zd, flag);
