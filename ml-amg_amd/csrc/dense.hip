@@ -186,7 +186,12 @@ __global__ __launch_bounds__(256) void k_sym_upper(double* __restrict__ M, int64
 }
 
 // ------------------------------------------------------------ inverse Cholesky factor
-constexpr int kNB = 32;
+#ifndef MLAMG_DENSE_NB  // panel width (A/B builds; 64: n 11449 factor 109 -> 88 ms, but 26 -> 28 ms
+                        // at 7396 and slower fused singles / batches, so 32)
+#define MLAMG_DENSE_NB 32
+#endif
+constexpr int kNB = MLAMG_DENSE_NB;
+static_assert(kNB == 32 || kNB == 64, "panel width: 32 or 64 (lane-per-row diagonal factor)");
 typedef double d4v __attribute__((ext_vector_type(4)));
 
 // a lane's double, read by the whole wave (two 32-bit lane reads: no LDS round trip)
@@ -654,7 +659,7 @@ int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream) {
     }
     (void)hipFree(D->y);  // not SPD: Gauss-Jordan below (the matrix is densified again)
     D->y = nullptr;
-  } else if (n >= 2 * kNB && !std::getenv("MLAMG_DENSE_GJ")) {
+  } else if (n >= 64 && !std::getenv("MLAMG_DENSE_GJ")) {
     // inverse Cholesky factor in a scratch copy, the inverse into D->inv
     double* M = nullptr;
     if (hipMalloc(&M, sizeof(double) * n * n) == hipSuccess) {
