@@ -140,7 +140,10 @@ __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restri
     static_assert(kBlockRows <= kThreads, "one row per thread in phase 2");
     EpiIn pre;
     if (tid < nr) pre = epi_load<OP>(r0 + tid, ep);
-    for (int t = tid; t <= nr; t += kThreads) rp[t] = indptr[r0 + t] - e0;
+    // row pointers to registers now, to LDS after the gathers (an LDS store waits for its load,
+    // which would hold back the entry loads behind it)
+    const int rpa = indptr[r0 + min(tid, nr)];
+    const int rpb = tid == 0 ? indptr[r1] : 0;  // t = kThreads when nr == kBlockRows == kThreads
     const int32_t* ci = indices + e0;
     const double* cv = vals + e0;
     // all kBlockNnz/kThreads loads of a lane issued back to back: the x gathers depend on the
@@ -156,6 +159,8 @@ __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restri
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
+    if (tid <= nr) rp[tid] = rpa - e0;
+    if (tid == 0 && nr == kThreads) rp[kThreads] = rpb - e0;
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (tid + u * kThreads < ne) prod[tid + u * kThreads] = vv[u] * xv[u];
@@ -689,11 +694,13 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   __shared__ double red[kSrtThreads / 64];
   __shared__ double valt[VD ? 256 : 1];
   if (ep.done && *ep.done) return;
-  if constexpr (VD) {
-    if (threadIdx.x < 256) valt[threadIdx.x] = vtab[threadIdx.x];
-  }
   const int b = (int)xcd_block(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x;
+  // every global load of the block is issued before the first LDS store that needs one (a
+  // store waits for its load, and a load placed after it would wait too): the value table and
+  // the row pointers go to registers first and to LDS just before the barrier
+  double tv = 0.0;
+  if constexpr (VD) tv = vtab[tid & 255];
   // the block's record {r0, r1, e0, nnz, lo, hi, split, -} in one 32-byte load: the entry
   // stream's addresses then wait for one round trip, not two (blk, then indptr)
   const int4 m0 = reinterpret_cast<const int4*>(base)[2 * b];
@@ -703,7 +710,13 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   // two column windows per block: sorted entries [0, split) are offsets from lo, the rest from
   // hi (a halo-extended local matrix has its ghost columns far from the owned ones)
   const int lo = m1.x, hi = m1.y, split = m1.z;
-  for (int t = tid; t <= nr; t += kSrtThreads) rp[t] = indptr[r0 + t] - e0;
+  constexpr int RPQ = kSrtRows / kSrtThreads + 1;  // row pointers per thread (nr + 1 <= kSrtRows + 1)
+  int rpv[RPQ];
+#pragma unroll
+  for (int q = 0; q < RPQ; ++q) {
+    const int t = tid + q * kSrtThreads;
+    rpv[q] = t <= nr ? indptr[r0 + t] : 0;
+  }
   constexpr int RPT = kSrtRows / kSrtThreads;  // rows per thread in phase 2
   static_assert(RPT * kSrtThreads == kSrtRows, "whole rows per thread in phase 2");
   EpiIn pre[RPT];
@@ -732,7 +745,13 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
     xv[u] = w[u] != kNone ? x[cb + (int)(w[u] >> kSrtPosBits)] : 0.0;
 #endif
   }
+#pragma unroll
+  for (int q = 0; q < RPQ; ++q) {
+    const int t = tid + q * kSrtThreads;
+    if (t <= nr) rp[t] = rpv[q] - e0;
+  }
   if constexpr (VD) {
+    if (tid < 256) valt[tid] = tv;
     __syncthreads();  // value table staged (the gathers above are already in flight)
 #pragma unroll
     for (int u = 0; u < U; ++u) vv[u] = w[u] != kNone ? valt[(int)vv[u]] : 0.0;
