@@ -9,6 +9,10 @@
 // independent. Results are therefore bit for bit those of the sequential sweep.
 #include "common.hpp"
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 struct mlamg_gs {
   const mlamg_csr* A = nullptr;
   int32_t n_levels = 0;
@@ -669,11 +673,22 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
   MLAMG_REQUIRE(A->n_rows == A->n_cols, "square matrix required");
   hipStream_t s = S(stream);
   const int64_t n = A->n_rows;
+  // MLAMG_TIMING=1: host phase times of the schedule analysis on stderr
+  static const bool timing = std::getenv("MLAMG_TIMING") != nullptr;
+  auto t_prev = std::chrono::steady_clock::now();
+  auto phase = [&](const char* name) {
+    if (!timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[gs_create] %s %.3f ms\n", name,
+                 std::chrono::duration<double, std::milli>(t - t_prev).count());
+    t_prev = t;
+  };
   std::vector<int32_t> ip(n + 1), ij(A->nnz);
   MLAMG_HIP(hipMemcpyAsync(ip.data(), A->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, s));
   if (A->nnz)
     MLAMG_HIP(hipMemcpyAsync(ij.data(), A->indices, sizeof(int32_t) * A->nnz, hipMemcpyDeviceToHost, s));
   MLAMG_HIP(hipStreamSynchronize(s));
+  phase("copy_in");
   std::vector<int32_t> level(n, 0), req(n, 0);
   int32_t nlev = 0;
   for (int64_t i = 0; i < n; ++i) {
@@ -705,6 +720,7 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
   if (n) (void)hipMemcpy(G->rows, rows.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice);
   for (int32_t l = 0; l < nlev; ++l)
     G->max_level_rows = std::max(G->max_level_rows, G->level_ptr[l + 1] - G->level_ptr[l]);
+  phase("levels");
   if (hipMalloc(&G->d_level_ptr, sizeof(int32_t) * (nlev + 1)) != hipSuccess) {
     (void)hipFree(G->rows);
     delete G;
@@ -742,6 +758,7 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
           }
         }
       }
+      phase("pack");
       const size_t m = std::max<size_t>((size_t)n * K, 1), nn = std::max<int64_t>(n, 1);
       if (hipMalloc(&G->pk_col, sizeof(int32_t) * m) == hipSuccess &&
           hipMalloc(&G->pk_val, sizeof(double) * m) == hipSuccess &&
@@ -753,7 +770,9 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
           (void)hipMemcpy(G->pk_diag, pdiag.data(), sizeof(double) * n, hipMemcpyHostToDevice);
         }
         G->pk_k = K;
+        phase("pack_upload");
         setup_window(G, ip, ij, level, rows, pcol, K);
+        phase("window");
       } else {  // optional: the sweep falls back to the plain kernels
         for (void* q : {(void*)G->pk_col, (void*)G->pk_val, (void*)G->pk_diag, (void*)G->b_lvl})
           if (q) (void)hipFree(q);

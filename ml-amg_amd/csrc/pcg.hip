@@ -15,7 +15,7 @@
 // once. Eagerly launched solves poll the flag every few iterations and stop launching; inside a
 // stream capture every iteration up to maxit is recorded (the V-cycle executor therefore runs
 // hierarchies with a PCG coarse solver eagerly). Reductions are fixed-order (partials over a
-// fixed grid, one-workgroup finalisation), so a solve is deterministic.
+// fixed grid, summed in order by the last-arriving workgroup), so a solve is deterministic.
 #include "common.hpp"
 
 #include <cmath>
@@ -26,14 +26,16 @@ struct mlamg_pcg {
   int64_t n = 0;
   double rtol = 1e-12;
   int maxit = 200;
-  int poll = 4;
+  int poll = 2;
   void* mem = nullptr;
   double *r = nullptr, *p = nullptr, *q = nullptr, *partial = nullptr;
   double* scal = nullptr;     // [0] rho, [1] alpha, [2] beta, [3] ||b||^2, [4] ||r||^2 (last),
                               // [5] largest final ||r||/||b|| over solves
   int32_t* flags = nullptr;   // [0] iterations of the last solve, [1] solves not converged,
                               // [2] total iterations
-  int32_t* done_host = nullptr;
+  int32_t* ctr = nullptr;     // arrival counter of the reduction kernels (re-armed to 0)
+  int32_t* done_host = nullptr;  // two pinned slots of the polled done flag
+  hipEvent_t ev[2] = {nullptr, nullptr};
   int nb = 1;
 };
 
@@ -56,23 +58,44 @@ __device__ __forceinline__ void block_partial(double s, double* partial) {
   if (threadIdx.x == 0) partial[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-// one workgroup: fixed-order sum of nb partials
-__device__ __forceinline__ double block_total(const double* __restrict__ partial, int nb) {
-  __shared__ double red[16];
-  double s = strided_sum(partial, nb, threadIdx.x, 1024);
+// Each reduction kernel finishes its own scalar step: every workgroup writes its partial, and the
+// workgroup that arrives last at the solver's counter (release / acquire at agent scope, so the
+// other XCDs' partials are visible to it) sums the partials in fixed order and updates the
+// scalars — one launch per dot product instead of a partials launch plus a one-workgroup
+// finalisation launch. The counter is re-armed by that same workgroup.
+__device__ __forceinline__ bool arrive_last(int32_t* ctr) {
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (int)gridDim.x - 1;
+    if (last) {
+      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence();
+    }
+  }
+  __syncthreads();
+  return last != 0;
+}
+
+// fixed-order sum of nb partials by one kPcgThreads workgroup (all threads get the total)
+__device__ __forceinline__ double last_total(const double* __restrict__ partial, int nb) {
+  __shared__ double red[kPcgThreads / 64];
+  double s = strided_sum(partial, nb, threadIdx.x, kPcgThreads);
   s = pcg_wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  double t = 0.0;
-  for (int i = 0; i < 16; ++i) t += red[i];
-  return t;
+  return ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-// x = 0, r = b, partials of b.b; done := outer done (a finished outer iteration skips the solve)
+// x = 0, r = b, ||b||^2; done := outer done (a finished outer iteration skips the solve); a zero
+// right-hand side is solved by x = 0
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_init(const double* __restrict__ b,
                                                           double* __restrict__ x,
                                                           double* __restrict__ r, int64_t n,
                                                           double* __restrict__ partial,
+                                                          int32_t* ctr, double* scal,
                                                           int32_t* done, const int32_t* outer,
                                                           int32_t* flags) {
   const bool skip = outer && *outer;
@@ -90,37 +113,45 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_init(const double* __restri
     s += v * v;
   }
   block_partial(s, partial);
-}
-
-// ||b||^2; a zero right-hand side is solved by x = 0
-__global__ __launch_bounds__(1024) void k_pcg_bnorm(const double* __restrict__ partial, int nb,
-                                                    double* scal, int32_t* done) {
-  if (*done) return;
-  const double t = block_total(partial, nb);
+  if (!arrive_last(ctr)) return;
+  const double t = last_total(partial, gridDim.x);
   if (threadIdx.x == 0) {
     scal[3] = t;
     if (!(t > 0.0)) *done = 1;
   }
 }
 
-// partials of u.v
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_dot(const double* __restrict__ u,
-                                                         const double* __restrict__ v, int64_t n,
-                                                         double* __restrict__ partial,
-                                                         const int32_t* done) {
+// alpha = rho / (p.q)
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_alpha(const double* __restrict__ p,
+                                                           const double* __restrict__ q, int64_t n,
+                                                           double* __restrict__ partial,
+                                                           int32_t* ctr, double* scal,
+                                                           const int32_t* done) {
   if (*done) return;
   double s = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kPcgThreads)
-    s += u[i] * v[i];
+    s += p[i] * q[i];
   block_partial(s, partial);
+  if (!arrive_last(ctr)) return;
+  const double t = last_total(partial, gridDim.x);
+  if (threadIdx.x == 0) scal[1] = scal[0] / t;
 }
 
-// rho = r.z (first: p = z as well, done by k_pcg_p with beta = 0)
-__global__ __launch_bounds__(1024) void k_pcg_rho(const double* __restrict__ partial, int nb,
-                                                  double* scal, const int32_t* done, int first) {
+// rho = r.z, beta = rho / rho_old (first: beta = 0, so k_pcg_p sets p = z)
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_rho(const double* __restrict__ r,
+                                                         const double* __restrict__ z, int64_t n,
+                                                         double* __restrict__ partial,
+                                                         int32_t* ctr, double* scal,
+                                                         const int32_t* done, int first) {
   if (*done) return;
-  const double t = block_total(partial, nb);
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kPcgThreads)
+    s += r[i] * z[i];
+  block_partial(s, partial);
+  if (!arrive_last(ctr)) return;
+  const double t = last_total(partial, gridDim.x);
   if (threadIdx.x == 0) {
     scal[2] = first ? 0.0 : t / scal[0];
     scal[0] = t;
@@ -138,22 +169,15 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_p(const double* __restrict_
     p[i] = z[i] + beta * p[i];
 }
 
-// alpha = rho / (p.q)
-__global__ __launch_bounds__(1024) void k_pcg_alpha(const double* __restrict__ partial, int nb,
-                                                    double* scal, const int32_t* done) {
-  if (*done) return;
-  const double t = block_total(partial, nb);
-  if (threadIdx.x == 0) scal[1] = scal[0] / t;
-}
-
-// x += alpha p, r -= alpha q, partials of r.r
+// x += alpha p, r -= alpha q; ||r||^2 <= rtol^2 ||b||^2 -> done; iteration count
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(double* __restrict__ x,
                                                             double* __restrict__ r,
                                                             const double* __restrict__ p,
                                                             const double* __restrict__ q,
-                                                            int64_t n, const double* scal,
+                                                            int64_t n, double* scal,
                                                             double* __restrict__ partial,
-                                                            const int32_t* done) {
+                                                            int32_t* ctr, int32_t* done,
+                                                            int32_t* flags, double rtol) {
   if (*done) return;
   const double alpha = scal[1];
   double s = 0.0;
@@ -165,14 +189,8 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(double* __restrict__
     s += v * v;
   }
   block_partial(s, partial);
-}
-
-// ||r||^2 <= rtol^2 ||b||^2 -> done; iteration count
-__global__ __launch_bounds__(1024) void k_pcg_check(const double* __restrict__ partial, int nb,
-                                                    double* scal, int32_t* done, int32_t* flags,
-                                                    double rtol) {
-  if (*done) return;
-  const double t = block_total(partial, nb);
+  if (!arrive_last(ctr)) return;
+  const double t = last_total(partial, gridDim.x);
   if (threadIdx.x == 0) {
     scal[4] = t;
     flags[0] += 1;
@@ -203,17 +221,14 @@ static int pcg_iteration(mlamg_pcg* C, double* x, int32_t* done, hipStream_t s) 
   const int nb = C->nb;
   const int64_t n = C->n;
   MLAMG_TRY(spmv_set(C->A, C->p, C->q, done, s));
-  hipLaunchKernelGGL(k_pcg_dot, dim3(nb), dim3(kPcgThreads), 0, s, C->p, C->q, n, C->partial,
-                     done);
-  hipLaunchKernelGGL(k_pcg_alpha, dim3(1), dim3(1024), 0, s, C->partial, nb, C->scal, done);
+  hipLaunchKernelGGL(k_pcg_alpha, dim3(nb), dim3(kPcgThreads), 0, s, C->p, C->q, n, C->partial,
+                     C->ctr, C->scal, done);
   hipLaunchKernelGGL(k_pcg_update, dim3(nb), dim3(kPcgThreads), 0, s, x, C->r, C->p, C->q, n,
-                     C->scal, C->partial, done);
-  hipLaunchKernelGGL(k_pcg_check, dim3(1), dim3(1024), 0, s, C->partial, nb, C->scal, done,
-                     C->flags, C->rtol);
+                     C->scal, C->partial, C->ctr, done, C->flags, C->rtol);
   double* z = nullptr;
   MLAMG_TRY(hier_coarse_cycle(C->M, C->r, &z, 0, s));
-  hipLaunchKernelGGL(k_pcg_dot, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, n, C->partial, done);
-  hipLaunchKernelGGL(k_pcg_rho, dim3(1), dim3(1024), 0, s, C->partial, nb, C->scal, done, 0);
+  hipLaunchKernelGGL(k_pcg_rho, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, n, C->partial,
+                     C->ctr, C->scal, done, 0);
   hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(kPcgThreads), 0, s, z, C->p, n, C->scal, done);
   MLAMG_HIP(hipGetLastError());
   return MLAMG_OK;
@@ -229,20 +244,28 @@ int pcg_solve_impl(mlamg_pcg* C, const double* b, double* x, const int32_t* oute
   MLAMG_HIP(hipStreamIsCapturing(s, &cap));
   const bool poll = cap == hipStreamCaptureStatusNone && C->done_host;
   hipLaunchKernelGGL(k_pcg_init, dim3(nb), dim3(kPcgThreads), 0, s, b, x, C->r, C->n, C->partial,
-                     done, outer_done, C->flags);
-  hipLaunchKernelGGL(k_pcg_bnorm, dim3(1), dim3(1024), 0, s, C->partial, nb, C->scal, done);
+                     C->ctr, C->scal, done, outer_done, C->flags);
   double* z = nullptr;
   MLAMG_TRY(hier_coarse_cycle(C->M, C->r, &z, 0, s));
-  hipLaunchKernelGGL(k_pcg_dot, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, C->n, C->partial,
-                     done);
-  hipLaunchKernelGGL(k_pcg_rho, dim3(1), dim3(1024), 0, s, C->partial, nb, C->scal, done, 1);
+  hipLaunchKernelGGL(k_pcg_rho, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, C->n, C->partial,
+                     C->ctr, C->scal, done, 1);
   hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(kPcgThreads), 0, s, z, C->p, C->n, C->scal, done);
+  // The host polls the done flag without draining the queue: after queueing group g of `poll`
+  // iterations it copies the flag into pinned slot g % 2 and then waits for group g - 1's copy,
+  // so the device always has the next group queued while the host reads the previous one.
+  int g = 0;
   for (int it = 0; it < C->maxit; ++it) {
     MLAMG_TRY(pcg_iteration(C, x, done, s));
     if (poll && (it + 1) % C->poll == 0 && it + 1 < C->maxit) {
-      MLAMG_HIP(hipMemcpyAsync(C->done_host, done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-      MLAMG_HIP(hipStreamSynchronize(s));
-      if (*C->done_host) break;
+      const int slot = g & 1;
+      MLAMG_HIP(hipMemcpyAsync(C->done_host + slot, done, sizeof(int32_t), hipMemcpyDeviceToHost,
+                               s));
+      MLAMG_HIP(hipEventRecord(C->ev[slot], s));
+      if (g > 0) {
+        MLAMG_HIP(hipEventSynchronize(C->ev[slot ^ 1]));
+        if (C->done_host[slot ^ 1]) break;
+      }
+      ++g;
     }
   }
   hipLaunchKernelGGL(k_pcg_end, dim3(1), dim3(64), 0, s, C->scal, done, C->flags, outer_done);
@@ -286,10 +309,15 @@ int mlamg_pcg_create(const mlamg_csr* A, mlamg_hier* M, double rtol, int maxit,
   C->partial = reinterpret_cast<double*>(p + 3 * vec);
   C->scal = reinterpret_cast<double*>(p + 3 * vec + sizeof(double) * kPcgMaxBlocks);
   C->flags = reinterpret_cast<int32_t*>(p + 3 * vec + sizeof(double) * kPcgMaxBlocks + 256);
+  C->ctr = C->flags + 8;
   if (hipMemset(C->mem, 0, total) != hipSuccess ||
-      hipHostMalloc(&C->done_host, sizeof(int32_t), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&C->done_host, 2 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&C->ev[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&C->ev[1], hipEventDisableTiming) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     if (C->done_host) (void)hipHostFree(C->done_host);
+    for (hipEvent_t e : C->ev)
+      if (e) (void)hipEventDestroy(e);
     (void)hipFree(C->mem);
     delete C;
     set_error("pcg_create: allocation failed");
@@ -303,6 +331,8 @@ int mlamg_pcg_destroy(mlamg_pcg* C) {
   if (C) {
     if (C->mem) (void)hipFree(C->mem);
     if (C->done_host) (void)hipHostFree(C->done_host);
+    for (hipEvent_t e : C->ev)
+      if (e) (void)hipEventDestroy(e);
     delete C;
   }
   return MLAMG_OK;

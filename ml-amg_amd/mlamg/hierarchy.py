@@ -124,18 +124,28 @@ class Hierarchy:
         from .multigrid import GaussSeidel
         H = cls()
         H.jacobi_weight = omega
+        tm, t0 = {}, time.perf_counter()
         L = Level(as_device(A))
         L.P = as_device(P)
         L.R = L.P.transpose()
         L.dinv = L.A.diag_inv(omega) if dinv_w is None else to_device_vec(dinv_w)
         H.levels.append(L)
+        torch.cuda.synchronize()
+        tm["upload"], t0 = time.perf_counter() - t0, time.perf_counter()
         H.Ac = galerkin(L.R, L.A, L.P)
+        torch.cuda.synchronize()
+        tm["galerkin"], t0 = time.perf_counter() - t0, time.perf_counter()
         H._finalize(nu_pre, nu_post, dense_max=cls.TWO_LEVEL_DENSE_MAX)
+        torch.cuda.synchronize()
+        tm["coarse_solver"], t0 = time.perf_counter() - t0, time.perf_counter()
         if smoother == "gauss_seidel":
             L.gs = GaussSeidel(L.A)
             call("mlamg_hier_set_level_smoother", H.handle, 0, L.gs.handle)
+            torch.cuda.synchronize()
+            tm["gauss_seidel"] = time.perf_counter() - t0
         elif smoother != "jacobi":
             raise ValueError(f"unknown smoother {smoother!r}")
+        H.timings = tm
         if norm not in ("residual", "x"):
             raise ValueError(f"unknown norm {norm!r}")
         call("mlamg_hier_set_norm", H.handle, 0 if norm == "residual" else 1)
@@ -366,6 +376,10 @@ class Hierarchy:
     # factor (device-wide, fp64 matrix cores) beats a PCG solve per cycle up to larger n_c
     TWO_LEVEL_DENSE_MAX = 10240
     COARSE_RTOL = 1e-12
+    # the PCG preconditioner's hierarchy stops coarsening at this size (its coarsest operator is
+    # then solved by the dense inverse)
+    PCG_INNER_MAX_COARSE = 4096
+    PCG_INNER_NU = 2  # V(nu, nu) preconditioner cycle (symmetric for any nu)
 
     def _finalize(self, nu_pre, nu_post, dense_max=None, coarse_rtol=None):
         self.nu_pre, self.nu_post = nu_pre, nu_post
@@ -394,7 +408,10 @@ class Hierarchy:
         ||r|| <= rtol ||b||. The inner hierarchy smooths with the per-level SA weight
         w = (4/3)/lambda_max(D^-1 A) (w * lambda_max < 2: a convergent, symmetric V-cycle, i.e.
         an SPD preconditioner for an SPD A_c)."""
-        self.inner = Hierarchy.build(self.Ac, alpha=0.1, max_coarse=1000, jacobi_weight="sa",
+        self.inner = Hierarchy.build(self.Ac, alpha=0.1, max_coarse=self.PCG_INNER_MAX_COARSE,
+                                     jacobi_weight="sa", lanczos_tol=1e-8,
+                                     nu_pre=self.PCG_INNER_NU,
+                                     nu_post=self.PCG_INNER_NU,
                                      fine_format="csr_stream", coarse_format="exact")
         h = ctypes.c_void_p()
         call("mlamg_pcg_create", self.Ac.handle, self.inner.handle, float(rtol), int(maxit),
