@@ -168,6 +168,11 @@ int mlamg_spgemm(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out, void* 
 /* setup scratch: SpGEMM temporaries are cached device blocks reused across calls; this frees
  * the cached (unused) blocks. freed_bytes nullable. */
 int mlamg_scratch_trim(size_t* freed_bytes);
+/* device allocation cache (csrc/runtime.cpp): every library buffer comes from size-class lists
+ * of released blocks (a hipFree unmaps pages, ~1 ms per buffer). trim really frees the cached
+ * blocks; stats reports the cached bytes and the hit / miss counts. Pointers nullable. */
+int mlamg_device_cache_trim(size_t* freed_bytes);
+int mlamg_device_cache_stats(size_t* cached_bytes, int64_t* hits, int64_t* misses);
 /* accumulated wall times (ms) of the Galerkin/SpGEMM phases since the last reset, in the order
  * count, alloc, expand, sort, runsum, emit, finalize, free (n <= 8 entries written) */
 int mlamg_setup_phase_times(double* ms_out, int n, int reset);

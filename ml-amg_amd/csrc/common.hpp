@@ -46,6 +46,22 @@ const char* get_error();
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---------------------------------------------------------------- device allocations
+// Every device buffer of the library comes from a size-class cache (runtime.cpp): a hipFree
+// unmaps the pages, ~1 ms per buffer on MI355X, and one two-level amg_2_v call creates and
+// drops ~60 buffers (55 ms of hipFree at 320^2 against a 95 ms call). A released block keeps
+// hipFree's ordering (the device is synchronised before the block can be handed out again)
+// and stays mapped for the next allocation of its size class; the cache holds at most
+// MLAMG_DEVICE_CACHE_MB (default 8192) MiB and is flushed when an allocation fails.
+hipError_t cached_malloc(void** p, size_t bytes);
+hipError_t cached_free(void* p);
+template <class T>
+inline hipError_t cached_malloc_t(T** p, size_t bytes) {
+  return cached_malloc(reinterpret_cast<void**>(p), bytes);
+}
+#define hipMalloc(p, bytes) ::mlamg::cached_malloc_t((p), (bytes))
+#define hipFree(p) ::mlamg::cached_free((void*)(p))
+
 // ---------------------------------------------------------------- CSR-stream geometry
 // A row block = up to kBlockRows consecutive rows whose nonzeros (<= kBlockNnz) are staged
 // through LDS by one 256-thread workgroup; a row longer than kBlockNnz gets a block of its own

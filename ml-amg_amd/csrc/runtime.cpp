@@ -5,14 +5,131 @@
 #include <atomic>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <unordered_map>
 
 namespace mlamg {
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 const char* get_error() { return g_last_error.c_str(); }
+
+// ---------------------------------------------------------------- device allocation cache
+// Size classes: powers of two up to 1 MiB, then 8 steps per power of two (<= 12.5 % slack).
+namespace {
+size_t size_class(size_t b) {
+  b = std::max<size_t>(b, 256);
+  size_t p2 = 256;
+  while (p2 < b) p2 <<= 1;
+  if (p2 <= (size_t(1) << 20)) return p2;
+  const size_t step = p2 >> 4;  // p2 / 2 < b <= p2: steps of p2 / 16
+  return (b + step - 1) / step * step;
+}
+struct DevCache {
+  std::mutex mu;
+  std::unordered_map<void*, std::pair<int, size_t>> live;         // ptr -> (device, class)
+  std::map<std::pair<int, size_t>, std::vector<void*>> free_list;  // (device, class) -> blocks
+  size_t cached = 0, limit = 0;
+  int64_t hits = 0, misses = 0;
+  DevCache() {
+    const char* e = std::getenv("MLAMG_DEVICE_CACHE_MB");
+    limit = (e ? (size_t)std::strtoull(e, nullptr, 10) : size_t(8192)) << 20;
+  }
+  // really free every cached block (caller holds mu)
+  size_t flush() {
+    size_t n = 0;
+    for (auto& kv : free_list) {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      (void)hipSetDevice(kv.first.first);
+      for (void* q : kv.second) {
+        (void)(hipFree)(q);
+        n += kv.first.second;
+      }
+      (void)hipSetDevice(cur);
+    }
+    free_list.clear();
+    cached = 0;
+    return n;
+  }
+};
+DevCache& dev_cache() {
+  static DevCache* c = new DevCache();  // never destroyed: thread-exit frees may come late
+  return *c;
+}
+}  // namespace
+
+hipError_t cached_malloc(void** p, size_t bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const size_t cls = size_class(bytes);
+  DevCache& c = dev_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.free_list.find({dev, cls});
+  if (it != c.free_list.end() && !it->second.empty()) {
+    *p = it->second.back();
+    it->second.pop_back();
+    c.cached -= cls;
+    c.live[*p] = {dev, cls};
+    ++c.hits;
+    return hipSuccess;
+  }
+  e = (hipMalloc)(p, cls);
+  if (e != hipSuccess) {  // out of memory: give the cached blocks back and retry once
+    (void)hipGetLastError();
+    if (c.flush() == 0) return e;
+    e = (hipMalloc)(p, cls);
+    if (e != hipSuccess) return e;
+  }
+  c.live[*p] = {dev, cls};
+  ++c.misses;
+  return hipSuccess;
+}
+
+hipError_t cached_free(void* p) {
+  if (!p) return hipSuccess;
+  DevCache& c = dev_cache();
+  std::pair<int, size_t> key;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) return (hipFree)(p);  // not ours
+    key = it->second;
+    c.live.erase(it);
+  }
+  // hipFree's ordering: no kernel still in flight may see the block handed out again. The
+  // lock is not held here, so other host threads (one per rank in the loopback executor) keep
+  // allocating and launching while this one waits.
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (cur != key.first) (void)hipSetDevice(key.first);
+  hipError_t e = hipDeviceSynchronize();
+  if (cur != key.first) (void)hipSetDevice(cur);
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (e != hipSuccess || c.cached + key.second > c.limit) return (hipFree)(p);
+  c.free_list[key].push_back(p);
+  c.cached += key.second;
+  return hipSuccess;
+}
+
+size_t device_cache_trim() {
+  DevCache& c = dev_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  (void)hipDeviceSynchronize();
+  return c.flush();
+}
+
+void device_cache_stats(size_t* cached, int64_t* hits, int64_t* misses) {
+  DevCache& c = dev_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (cached) *cached = c.cached;
+  if (hits) *hits = c.hits;
+  if (misses) *misses = c.misses;
+}
 
 // ---------------------------------------------------------------- scratch
 // Per host thread: work submitted from different threads (one stream each, e.g. concurrent
@@ -288,3 +405,14 @@ static std::atomic<uint64_t> g_format_epoch{0};
 uint64_t format_epoch() { return g_format_epoch.load(); }
 void bump_format_epoch() { g_format_epoch.fetch_add(1); }
 }  // namespace mlamg
+
+extern "C" int mlamg_device_cache_trim(size_t* freed_bytes) {
+  const size_t n = mlamg::device_cache_trim();
+  if (freed_bytes) *freed_bytes = n;
+  return MLAMG_OK;
+}
+
+extern "C" int mlamg_device_cache_stats(size_t* cached_bytes, int64_t* hits, int64_t* misses) {
+  mlamg::device_cache_stats(cached_bytes, hits, misses);
+  return MLAMG_OK;
+}

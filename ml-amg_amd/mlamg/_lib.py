@@ -92,6 +92,10 @@ SIGNATURES = {
     "mlamg_spgemm": (c_int, [c_vp, c_vp, c_vpp, c_vp]),
     "mlamg_galerkin": (c_int, [c_vp, c_vp, c_vp, c_vpp, c_vp]),
     "mlamg_scratch_trim": (c_int, [ctypes.POINTER(ctypes.c_size_t)]),
+    "mlamg_device_cache_trim": (c_int, [ctypes.POINTER(ctypes.c_size_t)]),
+    "mlamg_device_cache_stats": (c_int, [ctypes.POINTER(ctypes.c_size_t),
+                                         ctypes.POINTER(ctypes.c_int64),
+                                         ctypes.POINTER(ctypes.c_int64)]),
     "mlamg_setup_phase_times": (c_int, [P_dbl, c_int, c_int]),
     "mlamg_sa_smoother": (c_int, [c_vp, c_dbl, c_vpp, c_vp]),
     "mlamg_csr_scale_rows": (c_int, [c_vp, c_vp, c_int, c_vpp, c_vp]),

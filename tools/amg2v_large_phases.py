@@ -1,5 +1,6 @@
 """Setup / cycle split of the large two-level amg_2_v (hierarchy engine, PCG coarse solve when
 n_c > TWO_LEVEL_DENSE_MAX): where the 320^2 call's time goes (last table)."""
+import gc
 import json
 import os
 import sys
@@ -32,8 +33,17 @@ for m in [int(a) for a in sys.argv[1:]] or (320,):
     x0 = np.random.RandomState(0).randn(A.shape[0])
     b = np.zeros(A.shape[0])
     multigrid.amg_2_v(A, P, b, x0, res_tol=1e-10)
+    H = out = None
     for rep in range(2):
+        tf = T()
+        H = out = None  # free the previous rep's device objects outside the timed phases
+        td = T()
+        gc.collect()
+        tg = T()
+        gc.collect()
         t0 = T()
+        free_ms = {"del": round((td - tf) * 1e3, 2), "gc": round((tg - td) * 1e3, 2),
+                   "gc_again": round((t0 - tg) * 1e3, 2)}
         H = Hierarchy.two_level(A, P, omega=2.0 / 3.0, smoother="gauss_seidel")
         t1 = T()
         xd = to_device_vec(x0).clone()
@@ -52,7 +62,7 @@ for m in [int(a) for a in sys.argv[1:]] or (320,):
                "setup_phases_ms": {k: round(v * 1e3, 2) for k, v in H.timings.items()},
                "inner_build_ms": ({k: round(v * 1e3, 2) for k, v in H.inner.timings.items()
                                    if isinstance(v, float)} if H.inner is not None else None),
-               "setup_ms": round((t1 - t0) * 1e3, 2), "cycle_ms": round((t3 - t2) * 1e3, 2),
+               "setup_ms": round((t1 - t0) * 1e3, 2), "free_prev_ms": free_ms, "cycle_ms": round((t3 - t2) * 1e3, 2),
                "cycles": len(err) if hasattr(err, "__len__") else None,
                "amg_2_v_ms": round((t5 - t4) * 1e3, 2), "iters": out[3]}
         print(json.dumps(row), flush=True)
