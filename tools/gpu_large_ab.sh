@@ -1,0 +1,8 @@
+# two-level amg_2_v beyond the fused engine: device allocation cache off vs on (same box).
+# Each GPU step has its own time limit; a failure ends the script.
+set -u
+mkdir -p gpurun_out; export TMPDIR=/tmp
+MLAMG_DEVICE_CACHE_MB=0 timeout -k 10 400 python -u tools/amg2v_large.py 160 256 320 512 1024 > gpurun_out/large_nocache.log 2>&1 || { echo fail1; tail -20 gpurun_out/large_nocache.log; exit 1; }
+grep grid gpurun_out/large_nocache.log
+timeout -k 10 400 python -u tools/amg2v_large.py 160 256 320 512 1024 > gpurun_out/large_cache.log 2>&1 || { echo fail2; tail -20 gpurun_out/large_cache.log; exit 1; }
+grep grid gpurun_out/large_cache.log
