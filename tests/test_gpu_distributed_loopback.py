@@ -173,7 +173,10 @@ def test_loopback_c4_world8_bench_partition():
         # the interior part's kernel is an autotune pick among exact-order formats, timed while
         # 8 rank threads share the GPU: which one wins is noise-dependent, the result is not
         assert s0 and s0[0]["formats"][1] is not None, D.splits
-    assert Ds[0].tuning[0]["chosen"].startswith("rowpat")  # fine local operator stays rowpat
+    # the row-pair encoder accepts every rank's fine local operator (it is timed; the pick
+    # itself is the same noise-dependent contest as above)
+    for D in Ds:
+        assert any(k.startswith("rowpat") for k in D.tuning[0].get("us", {})), D.tuning[0]
     for D, (x_own, h) in zip(Ds, out):
         assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank}"
         np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
