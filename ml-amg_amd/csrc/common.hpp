@@ -52,7 +52,8 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // drops ~60 buffers (55 ms of hipFree at 320^2 against a 95 ms call). A released block keeps
 // hipFree's ordering (the device is synchronised before the block can be handed out again)
 // and stays mapped for the next allocation of its size class; the cache holds at most
-// MLAMG_DEVICE_CACHE_MB (default 8192) MiB and is flushed when an allocation fails.
+// MLAMG_DEVICE_CACHE_MB (default 8192) MiB and is flushed when an allocation fails; blocks above
+// MLAMG_DEVICE_CACHE_MAX_BLOCK_MB (default 16) MiB are plain hipMalloc / hipFree.
 hipError_t cached_malloc(void** p, size_t bytes);
 hipError_t cached_free(void* p);
 template <class T>

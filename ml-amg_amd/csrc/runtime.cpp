@@ -32,11 +32,17 @@ struct DevCache {
   std::mutex mu;
   std::unordered_map<void*, std::pair<int, size_t>> live;         // ptr -> (device, class)
   std::map<std::pair<int, size_t>, std::vector<void*>> free_list;  // (device, class) -> blocks
-  size_t cached = 0, limit = 0;
+  size_t cached = 0, limit = 0, max_block = 0;
   int64_t hits = 0, misses = 0;
   DevCache() {
     const char* e = std::getenv("MLAMG_DEVICE_CACHE_MB");
     limit = (e ? (size_t)std::strtoull(e, nullptr, 10) : size_t(8192)) << 20;
+    // blocks above this size bypass the cache (allocated at their exact size, really freed):
+    // the hierarchy's large operators and vectors then sit where a plain hipMalloc puts them
+    // (the C4 bench cycle measured 1-3 % slower on recycled, class-rounded blocks), while the
+    // many small buffers of a two-level call, whose hipFree cost dominates, are cached
+    const char* m = std::getenv("MLAMG_DEVICE_CACHE_MAX_BLOCK_MB");
+    max_block = (m ? (size_t)std::strtoull(m, nullptr, 10) : size_t(16)) << 20;
   }
   // really free every cached block (caller holds mu)
   size_t flush() {
@@ -66,8 +72,9 @@ hipError_t cached_malloc(void** p, size_t bytes) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  const size_t cls = size_class(bytes);
   DevCache& c = dev_cache();
+  if (bytes > c.max_block) return (hipMalloc)(p, bytes);  // not tracked: cached_free frees it
+  const size_t cls = size_class(bytes);
   std::lock_guard<std::mutex> lk(c.mu);
   auto it = c.free_list.find({dev, cls});
   if (it != c.free_list.end() && !it->second.empty()) {
