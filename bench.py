@@ -216,6 +216,9 @@ def main():
                     help="skip the unstructured (C3) fine-SpMV roofline line")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="launch the ranks, rendezvous over gloo and report them; no GPU work")
+    ap.add_argument("--verify-selftest", action="store_true",
+                    help="run the distributed verification chain over gloo (mismatch injected "
+                         "by MLAMG_INJECT_MISMATCH_RANK); no GPU work")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -228,6 +231,8 @@ def main():
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}")
     if args.launch_selftest:
         return launch_selftest(world, rank)
+    if args.verify_selftest:
+        return verify_selftest(world, rank)
     if os.environ.get("MLAMG_ONE_DEVICE") == "1":
         local_rank = 0  # rehearsal only: every rank on GPU 0 (checks the RCCL code path on 1 GPU)
     torch.cuda.set_device(local_rank)
@@ -424,10 +429,56 @@ def c3_spmv_roofline(device):
             "csr_stream_frac": res["csr_stream"]["frac"], "formats": res}
 
 
+EXIT_DIST_MISMATCH = 4
+
+
+def refuse_mismatch(e):
+    """A distributed run whose iterate differs from the single-GPU one prints no value line and
+    exits non-zero (every rank: the verification result is reduced over ranks)."""
+    log(f"REFUSED: {e}")
+    sys.exit(EXIT_DIST_MISMATCH)
+
+
+def verify_selftest(world, rank):
+    """--verify-selftest (CPU, gloo): the distributed verification chain with a mismatch
+    injected on rank 1 (MLAMG_INJECT_MISMATCH_RANK) — the same decision and exit path as a
+    real run whose iterate is wrong; no GPU work."""
+    import torch.distributed as dist
+    from mlamg import distributed
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", world_size=world, rank=rank)
+    bad = os.environ.get("MLAMG_INJECT_MISMATCH_RANK") == str(rank)
+
+    class _Paths:
+        def set_overlap(self, on):
+            pass
+
+        def set_cycle_graph(self, on):
+            pass
+
+    def check():
+        ok = torch.tensor([0.0 if bad else 1.0])
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        return bool(ok.item() == 1.0)
+
+    try:
+        graph_on, overlap_on = distributed.verify_paths(check, _Paths(), True, True)
+    except distributed.DistributedMismatch as e:
+        dist.destroy_process_group()
+        refuse_mismatch(e)
+    if rank == 0:
+        print(json.dumps({"verify_selftest": True, "value": 1.0, "cycle_graph": graph_on,
+                          "overlap": overlap_on}), flush=True)
+    dist.destroy_process_group()
+
+
 def run_distributed(args, world, rank, local_rank):
     from mlamg import distributed
-    out, H, x0, teardown = distributed.bench_main(args, world, rank, local_rank, METRIC,
-                                                  HBM_PEAK_GBPS)
+    try:
+        out, H, x0, teardown = distributed.bench_main(args, world, rank, local_rank, METRIC,
+                                                      HBM_PEAK_GBPS)
+    except distributed.DistributedMismatch as e:
+        refuse_mismatch(e)
     if rank == 0:
         if not args.no_cpu_baseline:
             # rank 0 only, on the same (replicated) hierarchy; the other ranks wait in teardown

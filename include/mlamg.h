@@ -284,6 +284,9 @@ int mlamg_dense_destroy(mlamg_dense* D);
  * triangular passes (SPD operators of >= 2048 rows: no O(n^3) product), 0 = Gauss-Jordan with
  * partial pivoting (any other nonsingular operator) */
 int mlamg_dense_info(const mlamg_dense* D, int* method, int64_t* n);
+/* x = A^-1 b (device vectors), async on the stream. NOT reentrant on one handle: method 2 keeps
+ * its intermediate X b in the handle's own buffer, so two solves with the same handle must be
+ * ordered (same stream, or synchronised); use one handle per concurrent stream. */
 int mlamg_dense_solve(const mlamg_dense* D, const double* b, double* x, void* stream);
 
 /* Least squares by LSQR: x = argmin ||A x - b||_2 from x0 = 0, scipy.sparse.linalg.lsqr
@@ -329,6 +332,13 @@ int mlamg_pcg_solve(mlamg_pcg* C, const double* b, double* x, void* stream);
  * relative residual over all solves (each nullable); syncs */
 int mlamg_pcg_stats(const mlamg_pcg* C, int32_t* last_iters, int32_t* not_converged,
                     int32_t* total_iters, double* max_rel_residual, void* stream);
+/* solves ended by a breakdown (p.Ap <= 0, r.z <= 0 or a NaN residual: A or the preconditioner
+ * not positive definite; the solve stops with the iterate it had); syncs */
+int mlamg_pcg_breakdowns(const mlamg_pcg* C, int32_t* breakdowns, void* stream);
+/* *symmetric = 1 when A is square and |a_ij - a_ji| <= rtol * max(|a_ii|, |a_jj|) for every
+ * stored entry (a missing a_ji counts as 0; rtol = 0: exact symmetry); the PCG coarse solve is
+ * only chosen for such operators. Syncs. */
+int mlamg_csr_symmetric(const mlamg_csr* A, double rtol, int* symmetric, void* stream);
 /* use the PCG solver C (size = A_coarse rows) as H's coarsest solve instead of a dense inverse;
  * cycles of such a hierarchy run eagerly (use_graph is ignored) */
 int mlamg_hier_set_coarse_pcg(mlamg_hier* H, const mlamg_csr* A_coarse, mlamg_pcg* C);

@@ -853,7 +853,10 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
   MLAMG_TRY(jacobi_sweep(A, L.dinv, b, x_ext, L.t_ext, false, done, s));
   // r = b - A t with per-block ||r||^2 partials, x <- t; then the global norm
   // (r itself is not stored: the next cycle starts with its own residual). Split: the parts'
-  // partials lie in part order (0, 1, 2), whatever order the parts ran in
+  // partials lie in part order (0, 1, 2), whatever order the parts ran in. The parts' row
+  // blocks are cut differently from the unsplit operator's, so the NORM (history, tolerance
+  // stop) matches overlap-off / single-GPU runs to rounding, not bitwise; the iterate itself is
+  // bitwise unchanged (every row is summed in its stored order)
   int64_t poff[3] = {0, 0, 0};
   int nb = (int)A->n_part;
   if (D->overlap && L.sA.on() && !L.hx->nbr.empty()) {

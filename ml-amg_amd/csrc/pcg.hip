@@ -32,7 +32,9 @@ struct mlamg_pcg {
   double* scal = nullptr;     // [0] rho, [1] alpha, [2] beta, [3] ||b||^2, [4] ||r||^2 (last),
                               // [5] largest final ||r||/||b|| over solves
   int32_t* flags = nullptr;   // [0] iterations of the last solve, [1] solves not converged,
-                              // [2] total iterations
+                              // [2] total iterations, [3] solves ended by a breakdown
+                              // (p.Ap <= 0, r.z <= 0 or a NaN: A_c or the preconditioner
+                              // not positive definite)
   int32_t* ctr = nullptr;     // arrival counter of the reduction kernels (re-armed to 0)
   int32_t* done_host = nullptr;  // two pinned slots of the polled done flag
   hipEvent_t ev[2] = {nullptr, nullptr};
@@ -121,12 +123,18 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_init(const double* __restri
   }
 }
 
+// a breakdown ends the solve (done) and is counted; the iterate stays as it was
+__device__ __forceinline__ void breakdown(int32_t* done, int32_t* flags) {
+  *done = 1;
+  flags[3] += 1;
+}
+
 // alpha = rho / (p.q)
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_alpha(const double* __restrict__ p,
                                                            const double* __restrict__ q, int64_t n,
                                                            double* __restrict__ partial,
                                                            int32_t* ctr, double* scal,
-                                                           const int32_t* done) {
+                                                           int32_t* done, int32_t* flags) {
   if (*done) return;
   double s = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
@@ -135,7 +143,10 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_alpha(const double* __restr
   block_partial(s, partial);
   if (!arrive_last(ctr)) return;
   const double t = last_total(partial, gridDim.x);
-  if (threadIdx.x == 0) scal[1] = scal[0] / t;
+  if (threadIdx.x == 0) {
+    scal[1] = scal[0] / t;
+    if (!(t > 0.0)) breakdown(done, flags);  // p.Ap <= 0 or NaN: A_c not positive definite
+  }
 }
 
 // rho = r.z, beta = rho / rho_old (first: beta = 0, so k_pcg_p sets p = z)
@@ -143,7 +154,8 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_rho(const double* __restric
                                                          const double* __restrict__ z, int64_t n,
                                                          double* __restrict__ partial,
                                                          int32_t* ctr, double* scal,
-                                                         const int32_t* done, int first) {
+                                                         int32_t* done, int32_t* flags,
+                                                         int first) {
   if (*done) return;
   double s = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
@@ -155,6 +167,9 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_rho(const double* __restric
   if (threadIdx.x == 0) {
     scal[2] = first ? 0.0 : t / scal[0];
     scal[0] = t;
+    // r != 0 here (a zero residual ended the solve), so r.z <= 0 means the preconditioner is
+    // not positive definite
+    if (!(t > 0.0)) breakdown(done, flags);
   }
 }
 
@@ -199,6 +214,8 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(double* __restrict__
       *done = 1;
       const double rel = sqrt(t / scal[3]);
       if (rel > scal[5]) scal[5] = rel;
+    } else if (!(t >= 0.0)) {
+      breakdown(done, flags);  // NaN residual
     }
   }
 }
@@ -222,13 +239,13 @@ static int pcg_iteration(mlamg_pcg* C, double* x, int32_t* done, hipStream_t s) 
   const int64_t n = C->n;
   MLAMG_TRY(spmv_set(C->A, C->p, C->q, done, s));
   hipLaunchKernelGGL(k_pcg_alpha, dim3(nb), dim3(kPcgThreads), 0, s, C->p, C->q, n, C->partial,
-                     C->ctr, C->scal, done);
+                     C->ctr, C->scal, done, C->flags);
   hipLaunchKernelGGL(k_pcg_update, dim3(nb), dim3(kPcgThreads), 0, s, x, C->r, C->p, C->q, n,
                      C->scal, C->partial, C->ctr, done, C->flags, C->rtol);
   double* z = nullptr;
   MLAMG_TRY(hier_coarse_cycle(C->M, C->r, &z, 0, s));
   hipLaunchKernelGGL(k_pcg_rho, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, n, C->partial,
-                     C->ctr, C->scal, done, 0);
+                     C->ctr, C->scal, done, C->flags, 0);
   hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(kPcgThreads), 0, s, z, C->p, n, C->scal, done);
   MLAMG_HIP(hipGetLastError());
   return MLAMG_OK;
@@ -248,7 +265,7 @@ int pcg_solve_impl(mlamg_pcg* C, const double* b, double* x, const int32_t* oute
   double* z = nullptr;
   MLAMG_TRY(hier_coarse_cycle(C->M, C->r, &z, 0, s));
   hipLaunchKernelGGL(k_pcg_rho, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, C->n, C->partial,
-                     C->ctr, C->scal, done, 1);
+                     C->ctr, C->scal, done, C->flags, 1);
   hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(kPcgThreads), 0, s, z, C->p, C->n, C->scal, done);
   // The host polls the done flag without draining the queue: after queueing group g of `poll`
   // iterations it copies the flag into pinned slot g % 2 and then waits for group g - 1's copy,
@@ -271,6 +288,36 @@ int pcg_solve_impl(mlamg_pcg* C, const double* b, double* x, const int32_t* oute
   hipLaunchKernelGGL(k_pcg_end, dim3(1), dim3(64), 0, s, C->scal, done, C->flags, outer_done);
   MLAMG_HIP(hipGetLastError());
   return MLAMG_OK;
+}
+
+// Symmetry to rounding of a square CSR (any column order, no duplicates): thread per row i,
+// every stored a_ij is looked up in row j (linear scan: Galerkin rows are short and unsorted);
+// a missing a_ji counts as 0. Violation: |a_ij - a_ji| > rtol * max(|a_ii|, |a_jj|) (rtol = 0:
+// exact symmetry). bad[0] is set by plain stores (benign race, any violation wins).
+__device__ __forceinline__ double row_entry(const int32_t* __restrict__ ip,
+                                            const int32_t* __restrict__ ij,
+                                            const double* __restrict__ v, int r, int c) {
+  for (int k = ip[r]; k < ip[r + 1]; ++k)
+    if (ij[k] == c) return v[k];
+  return 0.0;
+}
+
+__global__ __launch_bounds__(256) void k_sym_check(const int32_t* __restrict__ ip,
+                                                   const int32_t* __restrict__ ij,
+                                                   const double* __restrict__ v, int64_t n,
+                                                   double rtol, int32_t* bad) {
+  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (i >= n) return;
+  const double dii = fabs(row_entry(ip, ij, v, (int)i, (int)i));
+  bool ok = true;
+  for (int k = ip[i]; k < ip[i + 1] && ok; ++k) {
+    const int j = ij[k];
+    if (j == (int)i) continue;
+    const double a = v[k], b = row_entry(ip, ij, v, j, (int)i);
+    const double scale = fmax(dii, fabs(row_entry(ip, ij, v, j, j)));
+    ok = fabs(a - b) <= rtol * scale;
+  }
+  if (!ok) bad[0] = 1;
 }
 
 int64_t pcg_rows(const mlamg_pcg* C) { return C->n; }
@@ -342,6 +389,40 @@ int mlamg_pcg_solve(mlamg_pcg* C, const double* b, double* x, void* stream) {
   MLAMG_REQUIRE(C && (C->n == 0 || (b && x)), "NULL argument");
   MLAMG_REQUIRE(b != x, "b and x must differ");
   return pcg_solve_impl(C, b, x, nullptr, S(stream));
+}
+
+int mlamg_pcg_breakdowns(const mlamg_pcg* C, int32_t* breakdowns, void* stream) {
+  MLAMG_REQUIRE(C && breakdowns, "NULL argument");
+  int32_t f[4] = {0, 0, 0, 0};
+  hipStream_t s = S(stream);
+  MLAMG_HIP(hipMemcpyAsync(f, C->flags, sizeof(f), hipMemcpyDeviceToHost, s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  *breakdowns = f[3];
+  return MLAMG_OK;
+}
+
+int mlamg_csr_symmetric(const mlamg_csr* A, double rtol, int* symmetric, void* stream) {
+  MLAMG_REQUIRE(A && symmetric, "NULL argument");
+  MLAMG_REQUIRE(rtol >= 0.0, "rtol >= 0 required");
+  if (A->n_rows != A->n_cols) {
+    *symmetric = 0;
+    return MLAMG_OK;
+  }
+  hipStream_t s = S(stream);
+  int32_t* bad = static_cast<int32_t*>(scratch(sizeof(int32_t), 14));
+  MLAMG_REQUIRE(bad, "csr_symmetric: scratch allocation failed");
+  MLAMG_HIP(hipMemsetAsync(bad, 0, sizeof(int32_t), s));
+  if (A->n_rows > 0) {
+    const unsigned nb = (unsigned)((A->n_rows + 255) / 256);
+    hipLaunchKernelGGL(k_sym_check, dim3(nb), dim3(256), 0, s, A->indptr, A->indices, A->data,
+                       A->n_rows, rtol, bad);
+    MLAMG_HIP(hipGetLastError());
+  }
+  int32_t h = 0;
+  MLAMG_HIP(hipMemcpyAsync(&h, bad, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  *symmetric = h == 0;
+  return MLAMG_OK;
 }
 
 int mlamg_pcg_stats(const mlamg_pcg* C, int32_t* last_iters, int32_t* not_converged,

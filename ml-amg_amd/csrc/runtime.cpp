@@ -36,7 +36,9 @@ struct DevCache {
   int64_t hits = 0, misses = 0;
   DevCache() {
     const char* e = std::getenv("MLAMG_DEVICE_CACHE_MB");
-    limit = (e ? (size_t)std::strtoull(e, nullptr, 10) : size_t(8192)) << 20;
+    // bounded well below what a torch process may need: torch's allocator cannot reclaim these
+    // blocks (mlamg_device_cache_trim gives them back; an OOM in this library flushes them)
+    limit = (e ? (size_t)std::strtoull(e, nullptr, 10) : size_t(2048)) << 20;
     // blocks above this size bypass the cache (allocated at their exact size, really freed):
     // the hierarchy's large operators and vectors then sit where a plain hipMalloc puts them
     // (the C4 bench cycle measured 1-3 % slower on recycled, class-rounded blocks), while the
@@ -73,7 +75,15 @@ hipError_t cached_malloc(void** p, size_t bytes) {
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   DevCache& c = dev_cache();
-  if (bytes > c.max_block) return (hipMalloc)(p, bytes);  // not tracked: cached_free frees it
+  if (bytes > c.max_block) {  // not tracked: cached_free frees it
+    e = (hipMalloc)(p, bytes);
+    if (e == hipSuccess) return e;
+    // out of memory: the cached small blocks (up to the cap) may be what is missing
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (c.flush() == 0) return e;
+    return (hipMalloc)(p, bytes);
+  }
   const size_t cls = size_class(bytes);
   std::lock_guard<std::mutex> lk(c.mu);
   auto it = c.free_list.find({dev, cls});

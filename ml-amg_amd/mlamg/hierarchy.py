@@ -46,6 +46,19 @@ def strength(A_dev, mode="invabs", rho=None):
     return DeviceCSR(h)
 
 
+class CoarseSolveError(RuntimeError):
+    """The coarsest solve cannot be done as asked (PCG on a non-symmetric operator too large
+    for the dense solver) or a PCG coarse solve broke down (operator not positive definite)."""
+    code = MLAMG_EUNSUPPORTED
+
+
+def csr_symmetric(M, rtol=0.0):
+    """True when the device CSR M is symmetric to `rtol` (mlamg_csr_symmetric)."""
+    ok = ctypes.c_int()
+    call("mlamg_csr_symmetric", M.handle, float(rtol), ctypes.byref(ok), stream_ptr())
+    return bool(ok.value)
+
+
 class Level:
     __slots__ = ("A", "dinv", "P", "R", "Agg", "omega", "lam", "lanczos_iters", "n_seeds",
                  "bf_sweeps", "seeds", "gs")
@@ -113,6 +126,7 @@ class Hierarchy:
         self.timings = {}
         self.pcg = None
         self.inner = None
+        self._breakdowns_seen = 0
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -381,10 +395,24 @@ class Hierarchy:
     PCG_INNER_MAX_COARSE = 4096
     PCG_INNER_NU = 2  # V(nu, nu) preconditioner cycle (symmetric for any nu)
 
+    # the dense solver's size limit (dense.hip mlamg_dense_create): an operator PCG may not take
+    # (not symmetric) still gets an exact inverse up to this size
+    DENSE_LIMIT = 32768
+    SYMMETRY_RTOL = 1e-12  # dense.hip's "symmetric to rounding" test
+
     def _finalize(self, nu_pre, nu_post, dense_max=None, coarse_rtol=None):
         self.nu_pre, self.nu_post = nu_pre, nu_post
         dense_max = self.DENSE_MAX if dense_max is None else dense_max
-        if self.Ac.shape[0] <= dense_max:
+        n_c = self.Ac.shape[0]
+        if n_c > dense_max and not csr_symmetric(self.Ac, self.SYMMETRY_RTOL):
+            # PCG needs an SPD A_c (a Galerkin P^T A P of an SPD A is symmetric to rounding);
+            # SuperLU, which the reference uses, takes any nonsingular A_H
+            if n_c > self.DENSE_LIMIT:
+                raise CoarseSolveError(f"coarse operator of {n_c} rows is not symmetric: the "
+                                       "PCG coarse solve needs an SPD operator and the dense "
+                                       f"solver is limited to {self.DENSE_LIMIT} rows")
+            dense_max = n_c
+        if n_c <= dense_max:
             h = ctypes.c_void_p()
             call("mlamg_dense_create", self.Ac.handle, ctypes.byref(h), stream_ptr())
             self.dense = h
@@ -426,10 +454,21 @@ class Hierarchy:
             return None
         a, b, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         d = ctypes.c_double()
+        e = ctypes.c_int32()
         call("mlamg_pcg_stats", self.pcg, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
              ctypes.byref(d), stream_ptr())
+        call("mlamg_pcg_breakdowns", self.pcg, ctypes.byref(e), stream_ptr())
         return {"last_iters": a.value, "not_converged": b.value, "total_iters": c.value,
-                "max_rel_residual": d.value}
+                "max_rel_residual": d.value, "breakdowns": e.value}
+
+    def check_coarse(self):
+        """Raise if a PCG coarse solve broke down (A_c or its preconditioner not positive
+        definite: the iterate is not a solve of the coarse system). Syncs."""
+        st = self.coarse_stats()
+        if st is not None and st["breakdowns"] > self._breakdowns_seen:
+            self._breakdowns_seen = st["breakdowns"]
+            raise CoarseSolveError(f"PCG coarse solve broke down ({st['breakdowns']} solves): "
+                                   "the coarse operator is not positive definite")
 
     # ------------------------------------------------------------------ cycling
     def cycle(self, b, x, n_cycles, tol=None, use_graph=True, history=True):
@@ -441,6 +480,8 @@ class Hierarchy:
         done = ctypes.c_int32()
         call("mlamg_hier_vcycle", self.handle, ptr(b), ptr(x), int(n_cycles), _tol_arg(tol),
              ptr(hist), ctypes.byref(done), int(bool(use_graph)), stream_ptr())
+        if self.pcg is not None:
+            self.check_coarse()
         if not history:
             return None
         return hist[: int(done.value)].cpu().numpy()

@@ -411,7 +411,14 @@ def amg_2_v(A, P, b, x,
     dev_x = to_device_vec(x).clone()  # x = x.copy()  (:171)
     dev_b = to_device_vec(b)
     # err[i]; stops after the first e <= tol
-    err = H.cycle(dev_b, dev_x, max_iter, tol=tol, use_graph=use_graph)
+    from .hierarchy import CoarseSolveError
+    try:
+        err = H.cycle(dev_b, dev_x, max_iter, tol=tol, use_graph=use_graph)
+    except CoarseSolveError:
+        # the PCG coarse solve broke down: A_H is not positive definite (singular, e.g. a P
+        # with an empty column) — the case where the reference's factorisation fails, so the
+        # reference's failure return (multigrid.py:167-170)
+        return x, np.float64(1.), np.zeros(max_iter), 0
     return dev_x.cpu().numpy(), conv_factor(err), err, len(err)
 
 

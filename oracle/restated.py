@@ -480,44 +480,54 @@ def vcycle_omp(levels, Ainv, b, x, n_cycles, threads):
 # symmetrize_measure=True), as called by utils/common.py:27,30. The scipy steps are pyamg's own
 # scipy calls; its three amg_core kernels are restated below.
 
+def _pyamg_norm(x):
+    """pyamg.util.linalg.norm: sqrt(inner(conj(x), x).real) of the raveled vector."""
+    x = np.ravel(x)
+    return np.sqrt(np.inner(x.conj(), x).real)
+
+
 def approximate_spectral_radius(A, tol=0.01, maxiter=15, restart=5):
-    """pyamg.util.linalg.approximate_spectral_radius (nonsymmetric Arnoldi with modified
-    Gram-Schmidt, restarted from the Ritz vector; initial vector np.random.rand)."""
+    """pyamg.util.linalg.approximate_spectral_radius(A) with its _approximate_eigenvalues
+    (pyamg 4.x/5.x; symmetric=False is forced there): v0 = np.random.rand(n, 1) from the GLOBAL
+    generator (n draws), Arnoldi with modified Gram-Schmidt (H[i, j] = dot(conj(v_i), w),
+    breakdown below eps*1e6), scipy.linalg.eig of H[:m, :m], restart from the dominant Ritz
+    vector (complex if eig returned complex vectors — pyamg keeps it complex) until
+    |H[m, m-1] y_m| / |ev| < tol. A@v is scipy's csr_matvec. Returns |ev_max| (float)."""
+    import scipy.linalg
     n = A.shape[0]
-    maxiter = min(n, maxiter)
     v0 = np.random.rand(n, 1)
-    ev_max = 0.0
+    maxiter = min(n, maxiter)
+    breakdown = np.finfo(np.float64).eps * 1e6
+    ev = None
+    max_index = 0
     for _ in range(restart + 1):
-        v = v0 / la.norm(v0)
-        H = np.zeros((maxiter + 1, maxiter))
-        V = [v]
-        breakdown = np.finfo(float).eps * 1e6
+        v0 = v0 / _pyamg_norm(v0)
+        H = np.zeros((maxiter + 1, maxiter), dtype=np.result_type(v0.dtype, A.dtype))
+        V = [v0]
         flag = False
         j = 0
         for j in range(maxiter):
             w = A @ V[-1]
             for i, vi in enumerate(V):
-                H[i, j] = np.dot(vi.ravel(), w.ravel())
+                H[i, j] = np.dot(np.conjugate(vi.ravel()), w.ravel())
                 w = w - H[i, j] * vi
-            H[j + 1, j] = la.norm(w)
+            H[j + 1, j] = _pyamg_norm(w)
             if H[j + 1, j] < breakdown:
                 flag = True
-                if H[j + 1, j] != 0.0:
+                if H[j + 1, j] != 0:
                     w = w / H[j + 1, j]
                 V.append(w)
                 break
             w = w / H[j + 1, j]
             V.append(w)
-        import scipy.linalg
-        ev, evect = scipy.linalg.eig(H[:j + 1, :j + 1])
-        k = int(np.abs(ev).argmax())
-        ev_max = abs(ev[k])
-        err = H[j + 1, j] * evect[-1, k]
-        v0 = np.hstack(V[:j + 1]) @ evect[:, k].reshape(-1, 1)
-        v0 = np.real(v0)
-        if abs(err) / abs(ev[k]) < tol or flag:
+        ev, evect = scipy.linalg.eig(H[:j + 1, :j + 1], left=False, right=True)
+        nvecs = ev.shape[0]
+        max_index = np.abs(ev).argmax()
+        err = H[nvecs, nvecs - 1] * evect[-1, max_index]
+        v0 = np.dot(np.hstack(V[:-1]), evect[:, max_index].reshape(-1, 1))
+        if np.abs(err) / np.abs(ev[max_index]) < tol or flag:
             break
-    return float(ev_max)
+    return float(np.abs(ev[max_index]))
 
 
 def _incomplete_mat_mult(T, mask):

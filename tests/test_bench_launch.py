@@ -48,6 +48,25 @@ def test_launcher_world_size_must_match():
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus=4" in r.stderr
 
 
+@pytest.mark.parametrize("n", (2, 3))
+def test_distributed_mismatch_is_refused(n):
+    """A distributed iterate that differs from the single-GPU one on every executor path
+    (mismatch injected on rank 1 through the real verification chain,
+    mlamg.distributed.verify_paths) ends the run non-zero with no value line."""
+    r = _run(["--gpus", str(n), "--verify-selftest"],
+             env_extra={"MLAMG_INJECT_MISMATCH_RANK": "1"})
+    assert r.returncode == 4, (r.returncode, r.stderr[-2000:])
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "REFUSED" in r.stderr
+
+
+def test_distributed_verification_passes_without_mismatch():
+    r = _run(["--gpus", "2", "--verify-selftest"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["verify_selftest"] and out["cycle_graph"] and out["overlap"]
+
+
 def test_failing_rank_fails_the_launch():
     """A rank that dies makes the launcher stop the others and exit with its status (rank 0
     would otherwise wait in the rendezvous)."""

@@ -106,3 +106,71 @@ def test_amg_2_v_large_coarse_1024(ml, oracle, torch_cuda):
         assert np.allclose(e, er, rtol=1e-10, atol=0), (smoother, e, er)
         assert abs(c - cr) <= 1e-8
         assert np.abs(x - xr).max() <= 1e-8 * np.abs(xr).max()
+
+
+def test_csr_symmetric_check(ml, torch_cuda):
+    """mlamg_csr_symmetric: exact and to-rounding symmetry of unsorted Galerkin-like rows."""
+    import scipy.sparse as sp
+    from mlamg.hierarchy import csr_symmetric
+    from mlamg.sparse import DeviceCSR
+    A = ml.problems.poisson_2d_5pt(20).tocsr()
+    assert csr_symmetric(DeviceCSR.from_scipy(A))
+    B = A.copy()
+    B.data = B.data.copy()
+    B.data[5] *= 1 + 1e-14  # symmetric to rounding only
+    assert not csr_symmetric(DeviceCSR.from_scipy(B), 0.0)
+    assert csr_symmetric(DeviceCSR.from_scipy(B), 1e-12)
+    C = A.tolil()
+    C[0, 7] = 0.5  # no mirror entry: a_70 counts as 0
+    assert not csr_symmetric(DeviceCSR.from_scipy(C.tocsr()), 1e-12)
+    # unsorted rows (scipy's csr_matmat order) are fine
+    P = _sa_P(ml, A)
+    Ac = ml.sparse.galerkin(ml.sparse.DeviceCSR.from_scipy(P.T.tocsr()),
+                            DeviceCSR.from_scipy(A), DeviceCSR.from_scipy(P))
+    assert csr_symmetric(Ac, 1e-12)
+    assert not csr_symmetric(DeviceCSR.from_scipy(sp.random(6, 7, 0.5, format="csr")), 1.0)
+
+
+def test_nonsymmetric_coarse_takes_dense_or_refuses(ml, torch_cuda, monkeypatch):
+    """A coarse operator that is not symmetric never goes to PCG: dense inverse up
+    to DENSE_LIMIT rows, CoarseSolveError above."""
+    import scipy.sparse as sp
+    H_ = ml.hierarchy.Hierarchy
+    A = ml.problems.poisson_2d_5pt(48).tocsr()
+    n = A.shape[0]
+    # upwind convection: A + c * (I - shift) is not symmetric
+    A = (A + 0.5 * (sp.eye(n) - sp.eye(n, k=-1))).tocsr()
+    P = _sa_P(ml, ml.problems.poisson_2d_5pt(48))
+    monkeypatch.setattr(H_, "TWO_LEVEL_DENSE_MAX", 16)
+    H = H_.two_level(A, P)
+    assert H.pcg is None and H.dense is not None
+    monkeypatch.setattr(H_, "DENSE_LIMIT", 64)
+    with pytest.raises(ml.hierarchy.CoarseSolveError):
+        H_.two_level(A, P)
+
+
+def test_pcg_breakdown_is_reported(ml, torch_cuda, monkeypatch):
+    """An indefinite symmetric coarse operator (tridiag(1, 1, 1): spectrum (-1, 3), positive
+    diagonal; P = I so A_H = A) passes the symmetry test, so PCG is chosen, and breaks down
+    (p.Ap or r.z not positive). The breakdown is counted, the cycle raises CoarseSolveError, and
+    amg_2_v maps it to the reference's factorisation-failure return (x, 1.0, zeros, 0),
+    ns/lib/multigrid.py:167-170."""
+    import scipy.sparse as sp
+    torch = torch_cuda
+    H_ = ml.hierarchy.Hierarchy
+    n = 20000
+    A = sp.diags([np.ones(n - 1), np.ones(n), np.ones(n - 1)], [-1, 0, 1], format="csr")
+    P = sp.eye(n, format="csr")
+    monkeypatch.setattr(H_, "TWO_LEVEL_DENSE_MAX", 64)
+    H = H_.two_level(A, P, smoother="jacobi")
+    assert H.pcg is not None
+    b = torch.as_tensor(np.random.RandomState(1).randn(n)).cuda()
+    xd = torch.zeros(n, dtype=torch.float64, device="cuda")
+    with pytest.raises(ml.hierarchy.CoarseSolveError):
+        H.cycle(b, xd, 3)
+    assert H.coarse_stats()["breakdowns"] >= 1
+    x0 = np.random.RandomState(0).randn(n)
+    x, c, e, it = ml.multigrid.amg_2_v(A, P, np.random.RandomState(1).randn(n), x0,
+                                       res_tol=1e-10, max_iter=7, engine="hierarchy",
+                                       smoother="jacobi")
+    assert c == 1.0 and it == 0 and np.array_equal(e, np.zeros(7)) and x is x0

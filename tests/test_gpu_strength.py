@@ -59,11 +59,10 @@ def test_evolution_bitwise_vs_oracle(oracle, torch_cuda, name, mode):
     assert np.array_equal(got.data, ref.data), np.abs(got.data - ref.data).max()
 
 
-def test_device_rho_and_default_path(oracle, torch_cuda):
-    """The mirror's default rho (device Lanczos) vs the exact spectral radius, pyamg's Arnoldi
-    estimate within its tolerance, and the default-path measure feeding lloyd_aggregation like
-    utils/common.py:53-56."""
-    from mlamg import graph, strength
+def test_device_lanczos_rho(oracle, torch_cuda):
+    """The opt-in rho='lanczos' (device Lanczos) vs the exact spectral radius; pyamg's Arnoldi
+    estimate within its own 1e-2 tolerance of it."""
+    from mlamg import strength
     from mlamg.sparse import DeviceCSR
     A = _matrix("jump2d")
     Dinv_A = sp.diags(1.0 / A.diagonal()) @ A
@@ -73,11 +72,52 @@ def test_device_rho_and_default_path(oracle, torch_cuda):
     np.random.seed(0)
     rho_pyamg = oracle.approximate_spectral_radius(Dinv_A.tocsr())
     assert abs(rho_pyamg - lam) <= 1e-2 * lam
-    C = strength.strength_measure_funcs["olson"](A)
+    got = strength.olson(A, rho="lanczos")
     ref = oracle.strength_measure(A, "olson", rho=rho)
-    assert np.array_equal(C.indices, ref.indices) and np.array_equal(C.data, ref.data)
-    AggOp, roots, seeds = graph.lloyd_aggregation(C, ratio=0.1, distance="same", rand=0)
-    assert AggOp.shape == (A.shape[0], int(np.ceil(0.1 * A.shape[0])))
+    assert np.array_equal(got.indices, ref.indices) and np.array_equal(got.data, ref.data)
+
+
+@pytest.mark.parametrize("name", ("poisson2d", "lap3d_grid", "c3_mesh", "jump2d"))
+@pytest.mark.parametrize("mode", ("olson", "evolution"))
+def test_default_path_reproduces_reference_call(oracle, torch_cuda, name, mode):
+    """utils/evaluate_model.py:53-55 / utils/common.py:51-58 exactly: np.random.seed(0), then
+    strength_measure_funcs[mode](A) — pyamg's seeded Arnoldi estimate of rho(D^-1 A) draws n
+    numbers from the global generator —, then lloyd_aggregation(C, ratio, 'same') with
+    rand=None, whose seeds come from the state the measure left behind (graph.py:215-216,231).
+    Mirror vs oracle: rho, C, the generator state, seeds and AggOp all bitwise."""
+    from mlamg import graph, strength
+    A = _matrix(name).tocsr()
+    np.random.seed(0)
+    Dinv_A = A.copy()
+    Dinv_A.data = Dinv_A.data * np.repeat(strength.pyamg_dinv(A), np.diff(A.indptr))
+    rho_ref = oracle.approximate_spectral_radius(Dinv_A)
+    np.random.seed(0)
+    rho_got = strength.spectral_radius_pyamg(A)
+    assert rho_got == rho_ref
+
+    np.random.seed(0)
+    C_ref = sp.csr_matrix(oracle.strength_measure(A, mode))
+    st_ref = np.random.get_state()
+    Agg_ref, roots_ref, seeds_ref = oracle.lloyd_aggregation(C_ref, ratio=0.1, distance="same",
+                                                             canon=True)
+    st_ref_after = np.random.get_state()
+
+    np.random.seed(0)
+    C = strength.strength_measure_funcs[mode](A)
+    st = np.random.get_state()
+    Agg, roots, seeds = graph.lloyd_aggregation(C, ratio=0.1, distance="same")
+    st_after = np.random.get_state()
+
+    C_ref.sort_indices()
+    assert np.array_equal(C.indptr, C_ref.indptr) and np.array_equal(C.indices, C_ref.indices)
+    assert np.array_equal(C.data, C_ref.data)
+    for s, r in ((st, st_ref), (st_after, st_ref_after)):
+        assert s[0] == r[0] and np.array_equal(s[1], r[1]) and s[2:] == r[2:]
+    assert np.array_equal(seeds, seeds_ref)
+    assert np.array_equal(roots, roots_ref)
+    assert np.array_equal(Agg.indptr, Agg_ref.indptr)
+    assert np.array_equal(Agg.indices, Agg_ref.indices)
+    assert Agg.dtype == Agg_ref.dtype == np.int8
 
 
 @pytest.mark.parametrize("mode", ("olson", "evolution"))

@@ -67,6 +67,21 @@ def test_arnoldi_estimate_within_its_tolerance(oracle):
     assert abs(rho - lam) <= 1e-2 * lam
 
 
+def test_arnoldi_consumes_n_global_draws(oracle):
+    """pyamg draws its start vector as np.random.rand(n, 1) from the global generator and
+    nothing else: after the estimate the state equals a seed(0) generator advanced by n
+    doubles (what lloyd_aggregation(..., rand=None) then permutes from, ns/lib/graph.py:215)."""
+    A = _mats()["random_m"]
+    Dinv_A = (sp.diags(1.0 / A.diagonal()) @ A).tocsr()
+    np.random.seed(0)
+    oracle.approximate_spectral_radius(Dinv_A)
+    after = np.random.get_state()
+    rs = np.random.RandomState(0)
+    rs.rand(A.shape[0], 1)
+    want = rs.get_state()
+    assert np.array_equal(after[1], want[1]) and after[2:] == want[2:]
+
+
 @pytest.mark.parametrize("name", ("evolution", "olson"))
 def test_measures_add_their_second_term(oracle, name):
     A = _mats()["poisson2d"]
