@@ -185,8 +185,10 @@ int mlamg_galerkin(const mlamg_csr* R, const mlamg_csr* A, const mlamg_csr* P, m
 /* S = I - (omega*Dinv)@A with scipy rounding/zero-dropping (multigrid.py:104-106). */
 int mlamg_sa_smoother(const mlamg_csr* A, double omega, mlamg_csr** out, void* stream);
 
-/* M = diag(d)@A (row scaling) with zeros dropped; reverse!=0 stores each row's columns in
- * descending order — the order scipy's csr_matmat emits for dia@csr (multigrid.py:44). */
+/* M = diag(d)@A (row scaling). reverse=1: zeros dropped, each row's columns in descending
+ * order — the order scipy's csr_matmat emits for dia@csr (multigrid.py:44). reverse=0: A's
+ * pattern and stored order kept, nothing dropped — sparsetools csr_scale_rows (pyamg
+ * scale_rows, the D^-1 A of evolution_strength_of_connection). */
 int mlamg_csr_scale_rows(const mlamg_csr* A, const double* d, int reverse, mlamg_csr** out,
                          void* stream);
 

@@ -742,6 +742,8 @@ int spgemm_impl(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out, int ord
 // mode 0: M = diag(d)@A, reversed stored order, zeros dropped (csr_matmat of dia@csr)
 // mode 1: S = I - diag(d)@A in csr_binop_csr_general order (A's stored order sans diagonal,
 //         then the diagonal), zeros dropped
+// mode 2: M = diag(d)@A in place of A's values (csr_scale_rows: same pattern, same order,
+//         nothing dropped — pyamg's scale_rows(A, d, copy=True))
 __global__ void k_scale_count(const int32_t* __restrict__ ap, const int32_t* __restrict__ aj,
                               const double* __restrict__ ax, const double* __restrict__ d,
                               int64_t n, int mode, int32_t* __restrict__ cnt) {
@@ -749,7 +751,9 @@ __global__ void k_scale_count(const int32_t* __restrict__ ap, const int32_t* __r
   if (i >= n) return;
   const double di = d[i];
   int32_t c = 0;
-  if (mode == 0) {
+  if (mode == 2) {
+    c = ap[i + 1] - ap[i];
+  } else if (mode == 0) {
     for (int k = ap[i]; k < ap[i + 1]; ++k) c += (di * ax[k] != 0.0);
   } else {
     double mdiag = 0.0;
@@ -774,7 +778,12 @@ __global__ void k_scale_fill(const int32_t* __restrict__ ap, const int32_t* __re
   if (i >= n) return;
   const double di = d[i];
   int32_t o = cp[i];
-  if (mode == 0) {
+  if (mode == 2) {
+    for (int k = ap[i]; k < ap[i + 1]; ++k, ++o) {
+      cj[o] = aj[k];
+      cx[o] = ax[k] * di;  // csr_scale_rows: Ax[jj] *= Xx[i]
+    }
+  } else if (mode == 0) {
     for (int k = ap[i + 1] - 1; k >= ap[i]; --k) {
       const double m = di * ax[k];
       if (m != 0.0) {
@@ -914,8 +923,8 @@ int mlamg_galerkin(const mlamg_csr* R, const mlamg_csr* A, const mlamg_csr* P, m
 int mlamg_csr_scale_rows(const mlamg_csr* A, const double* d, int reverse, mlamg_csr** out,
                          void* stream) {
   MLAMG_REQUIRE(A && d && out, "NULL argument");
-  MLAMG_REQUIRE(reverse == 1, "only the scipy dia@csr (reverse=1) order is implemented");
-  return scale_rows_impl(A, d, 0, out, S(stream));
+  MLAMG_REQUIRE(reverse == 0 || reverse == 1, "reverse must be 0 or 1");
+  return scale_rows_impl(A, d, reverse ? 0 : 2, out, S(stream));
 }
 
 int mlamg_sa_smoother(const mlamg_csr* A, double omega, mlamg_csr** out, void* stream) {

@@ -16,7 +16,7 @@ import ctypes
 import numpy as np
 import scipy.sparse as sp
 
-from ._lib import call, stream_ptr
+from ._lib import call, ptr, stream_ptr
 from .sparse import DeviceCSR
 
 

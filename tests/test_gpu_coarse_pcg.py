@@ -124,6 +124,7 @@ def test_csr_symmetric_check(ml, torch_cuda):
     C[0, 7] = 0.5  # no mirror entry: a_70 counts as 0
     assert not csr_symmetric(DeviceCSR.from_scipy(C.tocsr()), 1e-12)
     # unsorted rows (scipy's csr_matmat order) are fine
+    A = ml.problems.poisson_2d_5pt(48).tocsr()
     P = _sa_P(ml, A)
     Ac = ml.sparse.galerkin(ml.sparse.DeviceCSR.from_scipy(P.T.tocsr()),
                             DeviceCSR.from_scipy(A), DeviceCSR.from_scipy(P))
