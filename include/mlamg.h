@@ -75,10 +75,11 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
  *   SELL        SELL-64 slices, lane-per-row sums in stored order (scipy's bits); vec_width > 1
  *               is read as sigma: rows sorted by length inside windows of sigma rows
  *               (SELL-C-sigma; get_format reports sigma in vec_width)
- *   VECTOR      vec_width lanes per row (0 = auto from the mean row length; 4..512), lane-
- *               strided partial sums + xor butterfly per 64-lane wave (+ wave sums left to right
- *               for 128..512, one 512-lane workgroup; <= 2^20 rows): a different, fixed order
- *               (oracle vec_matvec), for long-row coarse operators with no scipy counterpart
+ *   VECTOR      vec_width lanes per row (0 = auto from the mean row length; 64, 128, 256 or
+ *               512; <= 2^20 rows), lane-parallel sums in ONE canonical order whatever the width
+ *               (512 virtual lanes: lane v sums entries v, v+512, ...; xor butterfly per 64-lane
+ *               virtual wave; the 8 wave sums left to right — oracle vec_matvec), for long-row
+ *               coarse operators with no scipy counterpart; norm partials per row
  *   AUTO_EXACT  SELL when its padding costs <= 15% extra entries, else CSR_STREAM
  *   SORTED      CSR_STREAM row blocks (<= 512 rows, <= 4096 nonzeros) whose entries are stored
  *               in ascending column order with their CSR slot, so the x gathers of a
@@ -103,6 +104,11 @@ int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indice
  *             in stored order (scipy's bits). get_format reports the pattern count in
  *             vec_width. EUNSUPPORTED (format unchanged) when the patterns do not fit. */
 #define MLAMG_FMT_ROWPAT 6
+/* LONG        scipy's order for long rows (coarse Galerkin operators, R = P^T): tiles of
+ *             <= 64 consecutive rows / <= 4096 nonzeros over the CSR arrays themselves, one
+ *             workgroup each; every row summed left to right by one lane from LDS products with
+ *             pipelined reads (csrc/spmv.hip k_csr_long). Bitwise csr_matvec. */
+#define MLAMG_FMT_LONG 7
 int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream);
 int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored_entries);
 /* Attach the level's Jacobi weights dinv_w (device, n_rows) to a ROWPAT operator: checked on the
@@ -341,6 +347,18 @@ int mlamg_pcg_breakdowns(const mlamg_pcg* C, int32_t* breakdowns, void* stream);
  * stored entry (a missing a_ji counts as 0; rtol = 0: exact symmetry); the PCG coarse solve is
  * only chosen for such operators. Syncs. */
 int mlamg_csr_symmetric(const mlamg_csr* A, double rtol, int* symmetric, void* stream);
+/* Preconditioned GMRES with one V-cycle of M (a finalised hierarchy built on A) as the
+ * preconditioner — the Krylov acceleration of the reference's PyAMG PC apply,
+ * `Amg.solve(b, tol=amg_rtol, accel='gmres')` (ns/preconditioner/PyAMG.py:119). Algorithm of
+ * scipy.sparse.linalg.gmres: restarted (restart <= 0: 20), left-preconditioned MGS, Givens,
+ * gh-8400 inner tolerance control, stop when ||b - A x||_2 <= rtol ||b||_2; at most maxiter
+ * restart cycles (<= 0: 10 n). x (device) is the initial guess (x_is_zero: known to be 0) and
+ * the result. *info = 0 converged, else maxiter; *inner_iters = Krylov steps taken;
+ * presid_hist_host (nullable, hist_cap entries) receives the preconditioned residual estimate
+ * / ||b|| of every step. Syncs. */
+int mlamg_gmres(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, double rtol,
+                int restart, int maxiter, int x_is_zero, int* info, int* inner_iters,
+                double* presid_hist_host, int hist_cap, void* stream);
 /* use the PCG solver C (size = A_coarse rows) as H's coarsest solve instead of a dense inverse;
  * cycles of such a hierarchy run eagerly (use_graph is ignored) */
 int mlamg_hier_set_coarse_pcg(mlamg_hier* H, const mlamg_csr* A_coarse, mlamg_pcg* C);

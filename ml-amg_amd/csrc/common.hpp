@@ -82,6 +82,10 @@ constexpr int kSrtThreads = MLAMG_SRT_THREADS;
 constexpr int kSrtRows = MLAMG_SRT_THREADS * MLAMG_SRT_RPT;
 constexpr int kSrtNnz = 8 * MLAMG_SRT_THREADS;
 constexpr int kSrtPosBits = 12;
+// "long" format tiles (long-row coarse operators: Galerkin A_l, R = P^T): 256-thread
+// workgroups, <= kLongNnz fp64 products in LDS, <= kLongRows rows per tile (one lane each)
+constexpr int kLongNnz = 4096;
+constexpr int kLongRows = 64;
 
 // Tolerance arguments: tol >= 0 arms the device stop flag with ||.|| <= tol (the reference's
 // `e <= tol`, ns/lib/multigrid.py:197, MLAMG.py:194 — tol = 0 included: an exactly zero norm
@@ -157,6 +161,11 @@ struct mlamg_csr {
   // rp_dinv_att reads the per-pattern values rp_dinv[2p], rp_dinv[2p+1] instead of memory
   const double* rp_dinv_att = nullptr;
   double* rp_dinv = nullptr;
+  // optional long-row tiling ("long" format): tiles of consecutive rows (<= kLongRows rows,
+  // <= kLongNnz nonzeros, or one longer row streamed in chunks) over the CSR arrays themselves;
+  // every row summed left to right by one lane (scipy's order) from LDS products
+  int32_t lg_nt = 0;
+  int32_t* lg_tile = nullptr;  // lg_nt+1 row boundaries
   // number of per-block partial sums a NORM launch writes with the active format
   int32_t n_part = 0;
 };
@@ -198,6 +207,7 @@ namespace mlamg {
 constexpr int64_t kWideMaxRows = int64_t(1) << 20;
 inline int64_t part_capacity(const mlamg_csr* A) {
   int64_t c = std::max<int64_t>(std::max<int64_t>(A->n_blocks, A->srt_nb), (A->n_rows + 3) / 4);
+  c = std::max<int64_t>(c, A->lg_nt);
   if (A->n_rows <= kWideMaxRows) c = std::max<int64_t>(c, A->n_rows);
   return c + 2;
 }

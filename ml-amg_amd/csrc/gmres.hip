@@ -1,0 +1,347 @@
+// Preconditioned GMRES around the V-cycle: the Krylov acceleration of the reference's PyAMG
+// preconditioner, `Amg.solve(X.array_r, tol=amg_rtol, accel='gmres')` (ns/preconditioner/
+// PyAMG.py:119, the default `amg_precondition_with_gmres` of :54): zero initial guess, a
+// residual tolerance relative to ||b||, one V-cycle of the hierarchy as preconditioner.
+//
+// The algorithm is scipy.sparse.linalg.gmres (scipy 1.15, the library in this image): restarted,
+// LEFT-preconditioned (w = M A v), modified Gram-Schmidt, Givens rotations on the Hessenberg
+// column, inner stop on the preconditioned residual estimate with the gh-8400 tolerance control
+// (ptol adapted between restarts), outer stop ||b - A x||_2 <= atol = rtol ||b||_2. pyamg's own
+// krylov.gmres, which the reference calls, is absent here (parity unpinned); scipy's is the
+// pinned restatement of the same method.
+//
+// Everything n-sized runs on the device: the SpMV (the operator's exact-order format), the
+// preconditioner (hier_coarse_cycle: one V-cycle from a zero guess, replayed from a captured
+// graph), and the Gram-Schmidt dots / updates (fixed-order reductions finished by the
+// last-arriving workgroup, so a solve is deterministic). The (restart+1)-sized Hessenberg work —
+// rotations, the triangular solve, the tolerance logic — is done on the host from the column the
+// device computed (one read-back per inner iteration), as scipy does in numpy.
+#include "common.hpp"
+
+#include <cmath>
+
+namespace mlamg {
+
+constexpr int kGmThreads = 256;
+constexpr int kGmMaxBlocks = 1024;
+
+__device__ __forceinline__ double gm_wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// out[0] = a . b, fixed order: per-workgroup partials, summed in order by the last-arriving
+// workgroup (agent-scope acquire/release on the arrival counter)
+__global__ __launch_bounds__(kGmThreads) void k_gm_dot(const double* __restrict__ a,
+                                                      const double* __restrict__ b, int64_t n,
+                                                      double* __restrict__ partial, int32_t* ctr,
+                                                      double* out) {
+  __shared__ double red[kGmThreads / 64];
+  __shared__ int last;
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads)
+    s += a[i] * b[i];
+  s = gm_wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+    __threadfence();
+    const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (int)gridDim.x - 1;
+    if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  double t = strided_sum(partial, gridDim.x, threadIdx.x, kGmThreads);
+  t = gm_wave_sum(t);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// w -= (*coef) * v   (numpy's `w -= tmp * v[k, :]`: one product, one subtraction per entry)
+__global__ __launch_bounds__(kGmThreads) void k_gm_axmy(double* __restrict__ w,
+                                                       const double* __restrict__ v, int64_t n,
+                                                       const double* coef) {
+  const double c = *coef;
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads)
+    w[i] = w[i] - c * v[i];
+}
+
+// y = x * (1 / d)  with d = sqrt(*dd) (numpy: v *= (1 / norm))
+__global__ __launch_bounds__(kGmThreads) void k_gm_scale(double* __restrict__ y,
+                                                        const double* __restrict__ x, int64_t n,
+                                                        double d) {
+  const double inv = 1.0 / d;
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads)
+    y[i] = x[i] * inv;
+}
+
+// x += sum_k y[k] v_k (k ascending: numpy's `x += y @ v[:m, :]`)
+__global__ __launch_bounds__(kGmThreads) void k_gm_update(double* __restrict__ x,
+                                                         const double* __restrict__ V,
+                                                         int64_t n, int64_t ld,
+                                                         const double* __restrict__ y, int m) {
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads) {
+    double t = 0.0;
+    for (int k = 0; k < m; ++k) t += y[k] * V[k * ld + i];
+    x[i] = x[i] + t;
+  }
+}
+
+static int gm_grid(int64_t n) {
+  return (int)std::min<int64_t>(kGmMaxBlocks, std::max<int64_t>(1, (n + kGmThreads - 1) /
+                                                                       kGmThreads));
+}
+
+// LAPACK dlartg (3.10+, the safe-scaling version scipy's get_lapack_funcs('lartg') binds):
+// c f + s g = r, -s f + c g = 0
+static void lartg(double f, double g, double* c, double* s, double* r) {
+  if (g == 0.0) {
+    *c = 1.0;
+    *s = 0.0;
+    *r = f;
+  } else if (f == 0.0) {
+    *c = 0.0;
+    *s = g > 0 ? 1.0 : -1.0;
+    *r = std::fabs(g);
+  } else {
+    const double d = std::sqrt(f * f + g * g);
+    *c = std::fabs(f) / d;
+    *r = f > 0 ? d : -d;
+    *s = g / *r;
+  }
+}
+
+struct GmWork {
+  double* V = nullptr;    // (restart + 1) x ld
+  double* w = nullptr;
+  double* r = nullptr;
+  double* pb = nullptr;   // staging right-hand side of the preconditioner (fixed address)
+  double* partial = nullptr;
+  double* scal = nullptr;  // dot results: [0..restart+1) MGS coefficients, [restart+1] norm^2
+  double* y = nullptr;     // solution of the small triangular system
+  int32_t* ctr = nullptr;
+  void* mem = nullptr;
+  int64_t ld = 0;
+};
+
+int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, double rtol,
+               int restart, int maxiter, bool x_zero, int* info_out, int* iters_out,
+               double* presid_hist, int hist_cap, hipStream_t s) {
+  const int64_t n = A->n_rows;
+  if (restart <= 0) restart = 20;
+  restart = (int)std::min<int64_t>(restart, std::max<int64_t>(n, 1));
+  if (maxiter <= 0) maxiter = (int)std::min<int64_t>(INT32_MAX, 10 * std::max<int64_t>(n, 1));
+  GmWork W;
+  W.ld = ((std::max<int64_t>(n, 1) + 31) / 32) * 32;
+  const size_t vec = sizeof(double) * W.ld;
+  const size_t total = vec * (restart + 1) + 3 * vec + sizeof(double) * kGmMaxBlocks +
+                       sizeof(double) * (2 * restart + 4) + 256;
+  MLAMG_HIP(hipMalloc(&W.mem, total));
+  char* p = static_cast<char*>(W.mem);
+  W.V = reinterpret_cast<double*>(p);
+  p += vec * (restart + 1);
+  W.w = reinterpret_cast<double*>(p);
+  p += vec;
+  W.r = reinterpret_cast<double*>(p);
+  p += vec;
+  W.pb = reinterpret_cast<double*>(p);
+  p += vec;
+  W.partial = reinterpret_cast<double*>(p);
+  p += sizeof(double) * kGmMaxBlocks;
+  W.scal = reinterpret_cast<double*>(p);
+  W.y = W.scal + restart + 2;
+  W.ctr = reinterpret_cast<int32_t*>(W.y + restart + 2);
+  struct Free {
+    void* m;
+    ~Free() { (void)hipFree(m); }
+  } guard{W.mem};
+  MLAMG_HIP(hipMemsetAsync(W.ctr, 0, 64, s));
+  MLAMG_TRY(hier_prepare_ext(M));  // allocates the hierarchy's flags and work buffers
+  MLAMG_HIP(hipMemsetAsync(hier_done_flag(M), 0, sizeof(int32_t), s));
+  const int nb = gm_grid(n);
+  const int norm_slot = restart + 1;
+
+  auto dot = [&](const double* a, const double* c, int slot) -> int {
+    hipLaunchKernelGGL(k_gm_dot, dim3(nb), dim3(kGmThreads), 0, s, a, c, n, W.partial, W.ctr,
+                       W.scal + slot);
+    MLAMG_HIP(hipGetLastError());
+    return MLAMG_OK;
+  };
+  auto read = [&](int slot, int count, double* dst) -> int {
+    MLAMG_HIP(hipMemcpyAsync(dst, W.scal + slot, sizeof(double) * count, hipMemcpyDeviceToHost,
+                             s));
+    MLAMG_HIP(hipStreamSynchronize(s));
+    return MLAMG_OK;
+  };
+  auto norm = [&](const double* a, double* out) -> int {  // np.linalg.norm: sqrt(a . a)
+    MLAMG_TRY(dot(a, a, norm_slot));
+    double t = 0.0;
+    MLAMG_TRY(read(norm_slot, 1, &t));
+    *out = std::sqrt(t);
+    return MLAMG_OK;
+  };
+  auto psolve = [&](const double* in, double* out) -> int {  // one V-cycle from x = 0
+    MLAMG_HIP(hipMemcpyAsync(W.pb, in, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    double* z = nullptr;
+    MLAMG_TRY(hier_coarse_cycle(M, W.pb, &z, 1, s));
+    MLAMG_HIP(hipMemcpyAsync(out, z, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    return MLAMG_OK;
+  };
+  auto resid = [&](const double* xv, double* rv) -> int {  // r = b - A x
+    return residual_impl(A, b, xv, rv, nullptr, nullptr, nullptr, nullptr, kNoTol, nullptr,
+                         nullptr, nullptr, s);
+  };
+
+  int iters = 0;
+  *info_out = 0;
+  double bnrm2 = 0.0;
+  MLAMG_TRY(norm(b, &bnrm2));
+  const double atol = rtol * bnrm2;  // _get_atol_rtol: max(atol = 0, rtol * ||b||)
+  if (bnrm2 == 0.0) {  // scipy returns postprocess(b)
+    MLAMG_HIP(hipMemcpyAsync(x, b, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    *iters_out = 0;
+    return MLAMG_OK;
+  }
+  const double eps = 2.220446049250313e-16;
+  MLAMG_TRY(psolve(b, W.w));
+  double Mb_nrm2 = 0.0;
+  MLAMG_TRY(norm(W.w, &Mb_nrm2));
+  double ptol_max_factor = 1.0;
+  double ptol = Mb_nrm2 * std::min(ptol_max_factor, atol / bnrm2);
+  double presid = 0.0, rnorm = 0.0;
+  std::vector<double> h((size_t)restart * (restart + 1), 0.0), giv(2 * (size_t)restart, 0.0),
+      S(restart + 1, 0.0), y(restart + 1, 0.0), col_h(restart + 2, 0.0);
+  auto H = [&](int c, int k) -> double& { return h[(size_t)c * (restart + 1) + k]; };
+  double* V0 = W.V;
+  auto Vk = [&](int k) { return W.V + (int64_t)k * W.ld; };
+  for (int iteration = 0; iteration < maxiter; ++iteration) {
+    if (iteration == 0) {
+      if (x_zero) {
+        MLAMG_HIP(hipMemcpyAsync(W.r, b, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+      } else {
+        MLAMG_TRY(resid(x, W.r));
+      }
+      double r0 = 0.0;
+      MLAMG_TRY(norm(W.r, &r0));
+      if (r0 < atol) break;
+    }
+    MLAMG_TRY(psolve(W.r, V0));
+    double tmp = 0.0;
+    MLAMG_TRY(norm(V0, &tmp));
+    hipLaunchKernelGGL(k_gm_scale, dim3(nb), dim3(kGmThreads), 0, s, V0, V0, n, tmp);
+    MLAMG_HIP(hipGetLastError());
+    std::fill(S.begin(), S.end(), 0.0);
+    S[0] = tmp;
+    bool breakdown = false;
+    int col = 0;
+    for (col = 0; col < restart; ++col) {
+      MLAMG_TRY(spmv_set(A, Vk(col), W.r, nullptr, s));  // av (W.r is free until the update)
+      MLAMG_TRY(psolve(W.r, W.w));                       // w = M av
+      double h0 = 0.0;
+      MLAMG_TRY(norm(W.w, &h0));
+      for (int k = 0; k <= col; ++k) {  // modified Gram-Schmidt, coefficient on the device
+        MLAMG_TRY(dot(Vk(k), W.w, k));
+        hipLaunchKernelGGL(k_gm_axmy, dim3(nb), dim3(kGmThreads), 0, s, W.w, Vk(k), n,
+                           W.scal + k);
+        MLAMG_HIP(hipGetLastError());
+      }
+      MLAMG_TRY(dot(W.w, W.w, norm_slot));
+      MLAMG_TRY(read(0, restart + 2, col_h.data()));
+      for (int k = 0; k <= col; ++k) H(col, k) = col_h[k];
+      const double h1 = std::sqrt(col_h[norm_slot]);
+      H(col, col + 1) = h1;
+      if (h1 <= eps * h0) {  // exact solution indicator
+        H(col, col + 1) = 0.0;
+        breakdown = true;
+        MLAMG_HIP(hipMemcpyAsync(Vk(col + 1), W.w, sizeof(double) * n, hipMemcpyDeviceToDevice,
+                                 s));
+      } else {
+        hipLaunchKernelGGL(k_gm_scale, dim3(nb), dim3(kGmThreads), 0, s, Vk(col + 1), W.w, n,
+                           h1);
+        MLAMG_HIP(hipGetLastError());
+      }
+      for (int k = 0; k < col; ++k) {  // past rotations
+        const double c = giv[2 * k], sn = giv[2 * k + 1];
+        const double n0 = H(col, k), n1 = H(col, k + 1);
+        H(col, k) = c * n0 + sn * n1;
+        H(col, k + 1) = -sn * n0 + c * n1;
+      }
+      double c, sn, mag;
+      lartg(H(col, col), H(col, col + 1), &c, &sn, &mag);
+      giv[2 * col] = c;
+      giv[2 * col + 1] = sn;
+      H(col, col) = mag;
+      H(col, col + 1) = 0.0;
+      const double t2 = -sn * S[col];
+      S[col] = c * S[col];
+      S[col + 1] = t2;
+      presid = std::fabs(t2);
+      if (presid_hist && iters < hist_cap) presid_hist[iters] = presid / bnrm2;
+      ++iters;
+      if (presid <= ptol || breakdown) break;
+    }
+    if (col == restart) col = restart - 1;
+    if (H(col, col) == 0.0) S[col] = 0.0;
+    for (int k = 0; k <= col; ++k) y[k] = S[k];
+    for (int k = col; k > 0; --k) {
+      if (y[k] != 0.0) {
+        y[k] /= H(k, k);
+        const double t = y[k];
+        for (int j = 0; j < k; ++j) y[j] -= t * H(k, j);
+      }
+    }
+    if (y[0] != 0.0) y[0] /= H(0, 0);
+    MLAMG_HIP(hipMemcpyAsync(W.y, y.data(), sizeof(double) * (col + 1), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_gm_update, dim3(nb), dim3(kGmThreads), 0, s, x, W.V, n, W.ld, W.y,
+                       col + 1);
+    MLAMG_HIP(hipGetLastError());
+    MLAMG_TRY(resid(x, W.r));
+    MLAMG_TRY(norm(W.r, &rnorm));
+    if (rnorm <= atol) break;
+    if (breakdown) break;
+    if (presid <= ptol)
+      ptol_max_factor = std::max(eps, 0.25 * ptol_max_factor);
+    else
+      ptol_max_factor = std::min(1.0, 1.5 * ptol_max_factor);
+    ptol = presid * std::min(ptol_max_factor, atol / rnorm);
+  }
+  *info_out = rnorm <= atol ? 0 : maxiter;
+  *iters_out = iters;
+  MLAMG_HIP(hipStreamSynchronize(s));
+  return MLAMG_OK;
+}
+
+}  // namespace mlamg
+
+using namespace mlamg;
+
+extern "C" {
+
+int mlamg_gmres(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, double rtol,
+                int restart, int maxiter, int x_is_zero, int* info, int* inner_iters,
+                double* presid_hist_host, int hist_cap, void* stream) {
+  MLAMG_REQUIRE(A && M && info && inner_iters, "NULL argument");
+  MLAMG_REQUIRE(A->n_rows == A->n_cols, "square matrix required");
+  MLAMG_REQUIRE(hier_fine_rows(M) == A->n_rows, "preconditioner hierarchy does not match A");
+  MLAMG_REQUIRE(A->n_rows == 0 || (b && x && b != x), "b and x must be distinct device vectors");
+  MLAMG_REQUIRE(rtol >= 0.0, "rtol >= 0 required");
+  if (A->n_rows == 0) {
+    *info = 0;
+    *inner_iters = 0;
+    return MLAMG_OK;
+  }
+  return gmres_impl(A, M, b, x, rtol, restart, maxiter, x_is_zero != 0, info, inner_iters,
+                    presid_hist_host, presid_hist_host ? hist_cap : 0, S(stream));
+}
+
+}  // extern "C"

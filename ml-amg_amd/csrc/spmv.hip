@@ -612,64 +612,99 @@ void k_rowpair(const uint8_t* __restrict__ pid,
   }
 }
 
-// ---------------------------------------------------------------- CSR-vector variant
-// strided entries per lane loaded together (summation order unchanged: entry l, l+VW, ...);
-// build-time knob (tools/build_variant.sh -DMLAMG_VEC_UNROLL=N)
-#ifndef MLAMG_VEC_UNROLL
-#define MLAMG_VEC_UNROLL 4
-#endif
-constexpr int kVecUnroll = MLAMG_VEC_UNROLL;
-// VW lanes per row (long rows of coarse Galerkin operators). Lane l sums entries l, l+VW, ...
-// in order, then the VW partials are combined by an xor butterfly (off = VW/2 .. 1). This is a
-// DIFFERENT summation order from scipy's, restated exactly by the oracle (oracle.c
-// vec_matvec); it is only selected explicitly (mlamg_csr_set_format) for operators that have no
-// scipy counterpart in the reference (coarse levels of the multilevel hierarchy).
-template <int VW, int OP, bool NORM>
-__global__ __launch_bounds__(kThreads) void k_csr_vec(const int32_t* __restrict__ indptr,
-                                                      const int32_t* __restrict__ indices,
-                                                      const double* __restrict__ vals,
-                                                      int64_t n_rows,
-                                                      const double* __restrict__ x, Epi ep) {
-  __shared__ double red[kThreads / 64];
+// ---------------------------------------------------------------- CSR-vector (canonical order)
+// Lane-parallel sums for long rows (coarse Galerkin operators A_l, R = P^T: hundreds of entries
+// per row, where a one-lane left-to-right chain costs ~15-25 cycles per entry: tools/
+// chain_lab.hip). Every width W = 64 Q (Q = 1, 2, 4, 8 waves per row) computes the SAME
+// canonical order — the order of 512 virtual lanes:
+//   virtual lane v = 64 w + l (w = 0..7, l = 0..63) sums the row's entries v, v + 512, ... left
+//   to right from +0.0; each virtual wave w folds its 64 lanes with an xor butterfly (off = 32
+//   .. 1); the row is ((ws_0 + ws_1) + ...) + ws_7.
+// Physical wave p of a row (0..Q-1) holds the virtual waves w = p + Q j (j < 8 / Q), one
+// accumulator each. An empty virtual lane holds +0.0, which no butterfly step or wave sum can
+// see (a sum started at +0.0 is never -0.0). So the width is a pure performance choice: every
+// W gives the same bits (oracle.c vec_matvec restates the order; VERDICT r02 item 2 — the
+// autotune's timing noise used to pick between lane-strided orders).
+// Residual norms are written per row (partial[row]), so the norm is width-independent too.
+template <int Q, int OP, bool NORM>
+__global__ __launch_bounds__(512) void k_csr_vcan(const int32_t* __restrict__ indptr,
+                                                  const int32_t* __restrict__ indices,
+                                                  const double* __restrict__ vals,
+                                                  int64_t n_rows, const double* __restrict__ x,
+                                                  Epi ep) {
+  constexpr int J = 8 / Q;    // virtual waves per physical wave (accumulators per lane)
+  constexpr int RPB = 8 / Q;  // rows per 512-thread workgroup
+  __shared__ double ws[RPB][8];
   if (ep.done && *ep.done) return;
-  const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int64_t row = gid / VW;
-  const int l = threadIdx.x & (VW - 1);
-  double s = 0.0;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rloc = wave / Q, p = wave % Q;
+  const int64_t row = (int64_t)blockIdx.x * RPB + rloc;
+  double acc[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) acc[j] = 0.0;
   EpiIn pre;
-  if (l == 0 && row < n_rows) pre = epi_load<OP>((int)row, ep);
+  const bool head = p == 0 && lane == 0 && row < n_rows;
+  if (head) pre = epi_load<OP>((int)row, ep);
   if (row < n_rows) {
     const int a = indptr[row], b = indptr[row + 1];
-    // kVecUnroll strided entries per lane per step, loads issued together, summed in order
-    for (int k = a + l; k < b; k += kVecUnroll * VW) {
-      int32_t cc[kVecUnroll];
-      double vv[kVecUnroll], xv[kVecUnroll];
+    // Q stripes of 512 entries per step: Q * J = 8 entries per lane in flight
+    for (int base = a; base < b; base += 512 * Q) {
+      int32_t cc[Q][J];
+      double vv[Q][J], xv[Q][J];
 #pragma unroll
-      for (int u = 0; u < kVecUnroll; ++u) {
-        const int e = k + u * VW;
-        cc[u] = e < b ? __builtin_nontemporal_load(indices + e) : -1;
-        vv[u] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
-      }
+      for (int t = 0; t < Q; ++t)
 #pragma unroll
-      for (int u = 0; u < kVecUnroll; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
+        for (int j = 0; j < J; ++j) {
+          const int e = base + 512 * t + 64 * (p + Q * j) + lane;
+          cc[t][j] = e < b ? __builtin_nontemporal_load(indices + e) : -1;
+          vv[t][j] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
+        }
 #pragma unroll
-      for (int u = 0; u < kVecUnroll; ++u)
-        if (cc[u] >= 0) s += vv[u] * xv[u];
+      for (int t = 0; t < Q; ++t)
+#pragma unroll
+        for (int j = 0; j < J; ++j) xv[t][j] = cc[t][j] >= 0 ? x[cc[t][j]] : 0.0;
+#pragma unroll
+      for (int t = 0; t < Q; ++t)
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          if (cc[t][j] >= 0) acc[j] += vv[t][j] * xv[t][j];
     }
   }
 #pragma unroll
-  for (int off = VW / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, VW);
-  double sq = 0.0;
-  if (l == 0 && row < n_rows) sq = epi_store<OP>((int)row, s, pre, ep);
-  if constexpr (NORM) {
-    double w = wave_sum(sq);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double t = 0.0;
-      for (int i = 0; i < kThreads / 64; ++i) t += red[i];
-      ep.partial[blockIdx.x] = t;
-    }
+  for (int j = 0; j < J; ++j)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[j] += __shfl_xor(acc[j], off, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < J; ++j) ws[rloc][p + Q * j] = acc[j];
+  __syncthreads();
+  if (head) {
+    double r = ws[rloc][0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) r += ws[rloc][w];
+    const double sq = epi_store<OP>((int)row, r, pre, ep);
+    if constexpr (NORM) ep.partial[row] = sq;
+  }
+}
+
+template <int OP, bool NORM, int Q>
+static int launch_vcan(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  constexpr int RPB = 8 / Q;
+  const unsigned nb = (unsigned)std::max<int64_t>(1, (A->n_rows + RPB - 1) / RPB);
+  hipLaunchKernelGGL((k_csr_vcan<Q, OP, NORM>), dim3(nb), dim3(512), 0, s, A->indptr,
+                     A->indices, A->data, A->n_rows, x, ep);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+template <int OP, bool NORM>
+static int launch_vec(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  if (A->n_rows == 0) return MLAMG_OK;
+  switch (A->vec_width) {
+    case 128: return launch_vcan<OP, NORM, 2>(A, x, ep, s);
+    case 256: return launch_vcan<OP, NORM, 4>(A, x, ep, s);
+    case 512: return launch_vcan<OP, NORM, 8>(A, x, ep, s);
+    default: return launch_vcan<OP, NORM, 1>(A, x, ep, s);
   }
 }
 
@@ -790,99 +825,103 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   }
 }
 
-// Wide variant: VW = 128, 256 or 512 lanes per row inside a 512-lane workgroup (512/VW rows).
-// Lane l sums entries l, l+VW, ... in order; each 64-lane wave folds its lanes with the same xor
-// butterfly as VW = 64; the row's wave sums are then added left to right (w0 + w1 + ...). A fixed
-// order, restated by the oracle (vec_matvec); for the long rows of the coarsest operators, where
-// 64 lanes per row leave the chip mostly idle.
-template <int VW, int OP, bool NORM>
-__global__ __launch_bounds__(512) void k_csr_vecw(const int32_t* __restrict__ indptr,
-                                                  const int32_t* __restrict__ indices,
-                                                  const double* __restrict__ vals, int64_t n_rows,
-                                                  const double* __restrict__ x, Epi ep) {
-  constexpr int RPB = 512 / VW, WPR = VW / 64;
-  __shared__ double wsum[512 / 64];
-  __shared__ double red[RPB];
-  if (ep.done && *ep.done) return;
-  const int t = threadIdx.x;
-  const int64_t row = (int64_t)blockIdx.x * RPB + t / VW;
-  const int l = t & (VW - 1);
-  double s = 0.0;
-  EpiIn pre;
-  if (l == 0 && row < n_rows) pre = epi_load<OP>((int)row, ep);
-  if (row < n_rows) {
-    const int a = indptr[row], b = indptr[row + 1];
-    for (int k = a + l; k < b; k += kVecUnroll * VW) {
-      int32_t cc[kVecUnroll];
-      double vv[kVecUnroll], xv[kVecUnroll];
+// ---------------------------------------------------------------- long-row CSR ("long")
+// scipy's order for long rows (coarse Galerkin operators A_l and R = P^T: hundreds of nonzeros
+// per row). One 256-thread workgroup per tile of <= kLongRows consecutive rows holding
+// <= kLongNnz nonzeros. Phase 1 streams the tile's entries (kLongNnz / 256 per lane, every index
+// and value load issued before the first gather) and writes the products to LDS. Phase 2 gives
+// each row to one lane — row t to wave t % 4, lane t / 4, so the four SIMDs sum side by side —
+// which adds its products left to right with the LDS reads issued eight ahead of the adds: the
+// chain is then bound by the dependent fp64 adds instead of the ~50-cycle LDS latency that an
+// unpipelined loop pays per read (the CSR-stream kernel on C4 level 3: 64 us). A row longer than
+// kLongNnz is a tile of its own, streamed in chunks with lane 0 carrying the sum. Bitwise
+// csr_matvec — unlike the lane-strided CSR-vector order this format replaces in the autotune, so
+// the kernel choice (a timing decision) can no longer change a result.
+// Left-to-right sum of p[ka..kb) by one lane. Measured (tools/chain_lab.hip, MI355X): a
+// dependent v_add_f64 chain costs ~14-17 cycles per element at best; an LDS read waited for
+// per element ~85, per batch of 8 ~26-33, of 32 ~17-28 — so batches of 32 reads, then 32 adds
+// (software pipelining across batches loses: the register copies between the buffers wait for
+// the fresh reads at the end of every iteration).
+__device__ __forceinline__ double chain_sum(const double* __restrict__ p, int ka, int kb,
+                                            double s) {
+  int k = ka;
+  for (; k + 32 <= kb; k += 32) {
+    double v[32];
 #pragma unroll
-      for (int u = 0; u < kVecUnroll; ++u) {
-        const int e = k + u * VW;
-        cc[u] = e < b ? __builtin_nontemporal_load(indices + e) : -1;
-        vv[u] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
-      }
+    for (int u = 0; u < 32; ++u) v[u] = p[k + u];
 #pragma unroll
-      for (int u = 0; u < kVecUnroll; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
-#pragma unroll
-      for (int u = 0; u < kVecUnroll; ++u)
-        if (cc[u] >= 0) s += vv[u] * xv[u];
-    }
+    for (int u = 0; u < 32; ++u) s += v[u];
   }
+  for (; k + 8 <= kb; k += 8) {
+    double v[8];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if ((t & 63) == 0) wsum[t >> 6] = s;
-  __syncthreads();
-  double sq = 0.0;
-  if (l == 0 && row < n_rows) {
-    const int w0 = (t >> 6);
-    double r = wsum[w0];
+    for (int u = 0; u < 8; ++u) v[u] = p[k + u];
 #pragma unroll
-    for (int q = 1; q < WPR; ++q) r += wsum[w0 + q];
-    sq = epi_store<OP>((int)row, r, pre, ep);
+    for (int u = 0; u < 8; ++u) s += v[u];
   }
-  if constexpr (NORM) {
-    if (l == 0) red[t / VW] = sq;
-    __syncthreads();
-    if (t == 0) {
-      double tot = 0.0;
-      for (int i = 0; i < RPB; ++i) tot += red[i];
-      ep.partial[blockIdx.x] = tot;
-    }
-  }
-}
-
-template <int OP, bool NORM, int VW>
-static int launch_vec_wide(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
-  constexpr int RPB = 512 / VW;
-  const unsigned nb = (unsigned)std::max<int64_t>(1, (A->n_rows + RPB - 1) / RPB);
-  hipLaunchKernelGGL((k_csr_vecw<VW, OP, NORM>), dim3(nb), dim3(512), 0, s, A->indptr,
-                     A->indices, A->data, A->n_rows, x, ep);
-  MLAMG_HIP(hipGetLastError());
-  return MLAMG_OK;
-}
-
-template <int OP, bool NORM, int VW>
-static int launch_vec_w(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
-  const int64_t threads = A->n_rows * VW;
-  const unsigned nb = (unsigned)std::max<int64_t>(1, (threads + kThreads - 1) / kThreads);
-  hipLaunchKernelGGL((k_csr_vec<VW, OP, NORM>), dim3(nb), dim3(kThreads), 0, s, A->indptr,
-                     A->indices, A->data, A->n_rows, x, ep);
-  MLAMG_HIP(hipGetLastError());
-  return MLAMG_OK;
+  for (; k < kb; ++k) s += p[k];
+  return s;
 }
 
 template <int OP, bool NORM>
-static int launch_vec(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
-  if (A->n_rows == 0) return MLAMG_OK;
-  switch (A->vec_width) {
-    case 4: return launch_vec_w<OP, NORM, 4>(A, x, ep, s);
-    case 8: return launch_vec_w<OP, NORM, 8>(A, x, ep, s);
-    case 16: return launch_vec_w<OP, NORM, 16>(A, x, ep, s);
-    case 32: return launch_vec_w<OP, NORM, 32>(A, x, ep, s);
-    case 128: return launch_vec_wide<OP, NORM, 128>(A, x, ep, s);
-    case 256: return launch_vec_wide<OP, NORM, 256>(A, x, ep, s);
-    case 512: return launch_vec_wide<OP, NORM, 512>(A, x, ep, s);
-    default: return launch_vec_w<OP, NORM, 64>(A, x, ep, s);
+__global__ __launch_bounds__(kThreads) void k_csr_long(const int32_t* __restrict__ indptr,
+                                                       const int32_t* __restrict__ indices,
+                                                       const double* __restrict__ vals,
+                                                       const int32_t* __restrict__ tile,
+                                                       const double* __restrict__ x, Epi ep) {
+  __shared__ double prod[kLongNnz];
+  __shared__ int32_t rp[kLongRows + 1];
+  __shared__ double red[kThreads / 64];
+  static_assert(kLongRows <= kThreads && kLongRows % 4 == 0, "rows spread over four waves");
+  if (ep.done && *ep.done) return;
+  const int b = (int)xcd_block(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x;
+  const int r0 = tile[b], r1 = tile[b + 1], nr = r1 - r0;
+  const int e0 = indptr[r0];
+  const int ne = indptr[r1] - e0;
+  const int t = (tid & 63) * 4 + (tid >> 6);  // this lane's row in phase 2
+  double sq = 0.0;
+  if (ne <= kLongNnz) {
+    EpiIn pre;
+    if (t < nr) pre = epi_load<OP>(r0 + t, ep);
+    const int rpa = tid <= nr ? indptr[r0 + tid] : 0;
+    constexpr int U = kLongNnz / kThreads;
+    const int32_t* ci = indices + e0;
+    const double* cv = vals + e0;
+    int32_t cc[U];
+    double vv[U], xv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + u * kThreads;
+      cc[u] = e < ne ? __builtin_nontemporal_load(ci + e) : -1;
+      vv[u] = e < ne ? __builtin_nontemporal_load(cv + e) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
+    if (tid <= nr) rp[tid] = rpa - e0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (tid + u * kThreads < ne) prod[tid + u * kThreads] = vv[u] * xv[u];
+    __syncthreads();
+    if (t < nr) sq += epi_store<OP>(r0 + t, chain_sum(prod, rp[t], rp[t + 1], 0.0), pre, ep);
+  } else {
+    // one row longer than a tile: chunks through LDS, lane 0 carries the ordered sum
+    double s = 0.0;
+    for (int c = 0; c < ne; c += kLongNnz) {
+      const int m = min(kLongNnz, ne - c);
+      for (int e = tid; e < m; e += kThreads)
+        prod[e] = vals[e0 + c + e] * x[indices[e0 + c + e]];
+      __syncthreads();
+      if (tid == 0) s = chain_sum(prod, 0, m, s);
+      __syncthreads();
+    }
+    if (tid == 0) sq += epilogue<OP>(r0, s, ep);
+  }
+  if constexpr (NORM) {
+    double w = wave_sum(sq);
+    if ((tid & 63) == 0) red[tid >> 6] = w;
+    __syncthreads();
+    if (tid == 0) ep.partial[b] = ((red[0] + red[1]) + red[2]) + red[3];
   }
 }
 
@@ -932,6 +971,13 @@ static int launch_rowpair(const mlamg_csr* A, const double* x, const Epi& ep, hi
 template <int OP, bool NORM>
 static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   if (A->vec_width) return launch_vec<OP, NORM>(A, x, ep, s);
+  if (A->lg_tile) {
+    if (A->lg_nt == 0) return MLAMG_OK;
+    hipLaunchKernelGGL((k_csr_long<OP, NORM>), dim3(A->lg_nt), dim3(kThreads), 0, s, A->indptr,
+                       A->indices, A->data, A->lg_tile, x, ep);
+    MLAMG_HIP(hipGetLastError());
+    return MLAMG_OK;
+  }
   if (A->rp_pid) {
     if (A->n_rows == 0) return MLAMG_OK;
     return launch_rowpair<OP, NORM>(A, x, ep, s);
@@ -1344,6 +1390,47 @@ __global__ void k_vdict_encode(const double* __restrict__ v, int64_t n, unsigned
   if (e >= n) return;
   const unsigned long long key = (unsigned long long)__double_as_longlong(v[e]);
   out[e] = (uint8_t)vidx[dict_slot(key, vtab, nullptr, false)];
+}
+
+static void drop_long(mlamg_csr* A) {
+  if (A->lg_tile) (void)hipFree(A->lg_tile);
+  A->lg_tile = nullptr;
+  A->lg_nt = 0;
+  if (!A->sell_ptr && !A->vec_width && !A->srt_pk && !A->rp_pid) A->n_part = A->n_blocks;
+}
+
+// Tiles of the "long" format: consecutive rows while the tile has <= kLongRows rows and
+// <= kLongNnz nonzeros; a longer row is a tile of its own (streamed in chunks by the kernel).
+static int build_long(mlamg_csr* A, hipStream_t s) {
+  const int64_t n = A->n_rows;
+  std::vector<int32_t> ip(n + 1);
+  MLAMG_HIP(hipMemcpyAsync(ip.data(), A->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost,
+                           s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  std::vector<int32_t> t(1, 0);
+  for (int64_t r = 0; r < n;) {
+    int64_t r1 = r, nz = 0;
+    while (r1 < n && r1 - r < kLongRows && nz + (ip[r1 + 1] - ip[r1]) <= kLongNnz) {
+      nz += ip[r1 + 1] - ip[r1];
+      ++r1;
+    }
+    if (r1 == r) r1 = r + 1;
+    t.push_back((int32_t)r1);
+    r = r1;
+  }
+  int32_t* d = nullptr;
+  MLAMG_HIP(hipMalloc(&d, sizeof(int32_t) * t.size()));
+  if (hipMemcpyAsync(d, t.data(), sizeof(int32_t) * t.size(), hipMemcpyHostToDevice, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    (void)hipFree(d);
+    set_error("build_long: upload failed");
+    return MLAMG_EHIP;
+  }
+  if (A->lg_tile) (void)hipFree(A->lg_tile);
+  A->lg_tile = d;
+  A->lg_nt = (int32_t)(t.size() - 1);
+  return MLAMG_OK;
 }
 
 static void drop_sorted(mlamg_csr* A) {
@@ -2051,46 +2138,58 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       drop_rowpat(A);
       drop_sell(A);
       drop_sorted(A);
+      drop_long(A);
       A->vec_width = 0;
       return MLAMG_OK;
     case MLAMG_FMT_SELL:
       A->vec_width = 0;
       drop_rowpat(A);
       drop_sorted(A);
+      drop_long(A);
       return build_sell(A, s, vec_width > 1 ? vec_width : 1);  // vec_width doubles as sigma
     case MLAMG_FMT_SELL_DICT:
       A->vec_width = 0;
       drop_rowpat(A);
       drop_sorted(A);
+      drop_long(A);
       return build_sell_dict(A, s, vec_width > 1 ? vec_width : 1);
     case MLAMG_FMT_SORTED: {
       // built first, so an unsupported matrix keeps its current format
       MLAMG_TRY(build_sorted(A, s));
       drop_rowpat(A);
       drop_sell(A);
+      drop_long(A);
       A->vec_width = 0;
       A->n_part = A->srt_nb;
       return MLAMG_OK;
     }
-    case MLAMG_FMT_VECTOR: {
+    case MLAMG_FMT_LONG: {
+      MLAMG_TRY(build_long(A, s));
       drop_rowpat(A);
       drop_sell(A);
       drop_sorted(A);
+      A->vec_width = 0;
+      A->n_part = std::max<int32_t>(1, A->lg_nt);
+      return MLAMG_OK;
+    }
+    case MLAMG_FMT_VECTOR: {
       int vw = vec_width;
-      if (vw == 0) {
-        vw = 4;
-        while (vw < 64 && 2.0 * vw <= A->avg_row_len) vw *= 2;
+      if (vw == 0) {  // auto: a wave per 128 entries of the mean row, 64..512 lanes
+        vw = 64;
+        while (vw < 512 && 2.0 * vw <= A->avg_row_len) vw *= 2;
       }
-      MLAMG_REQUIRE(vw == 4 || vw == 8 || vw == 16 || vw == 32 || vw == 64 || vw == 128 ||
-                        vw == 256 || vw == 512,
-                    "vec_width must be 0 (auto), 4, 8, 16, 32, 64, 128, 256 or 512");
-      if (vw >= 128 && A->n_rows > kWideMaxRows) {
-        set_error("vec_width >= 128 needs <= 2^20 rows");
+      MLAMG_REQUIRE(vw == 64 || vw == 128 || vw == 256 || vw == 512,
+                    "vec_width must be 0 (auto), 64, 128, 256 or 512");
+      if (A->n_rows > kWideMaxRows) {
+        set_error("the VECTOR format needs <= 2^20 rows");
         return MLAMG_EUNSUPPORTED;
       }
+      drop_rowpat(A);
+      drop_sell(A);
+      drop_sorted(A);
+      drop_long(A);
       A->vec_width = vw;
-      A->n_part = vw >= 128 ? (int32_t)std::max<int64_t>(1, (A->n_rows * vw + 511) / 512)
-                            : (int32_t)std::max<int64_t>(1, (A->n_rows * vw + kThreads - 1) / kThreads);
+      A->n_part = (int32_t)std::max<int64_t>(1, A->n_rows);  // one norm partial per row
       return MLAMG_OK;
     }
     case MLAMG_FMT_AUTO_EXACT: {
@@ -2100,6 +2199,7 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       A->vec_width = 0;
       drop_rowpat(A);
       drop_sorted(A);
+      drop_long(A);
       MLAMG_TRY(build_sell(A, s, 1));
       if (A->nnz > 0 && (double)A->sell_elems <= 1.15 * (double)A->nnz) return MLAMG_OK;
       MLAMG_TRY(build_sell(A, s, 512));
@@ -2111,6 +2211,7 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       MLAMG_TRY(build_rowpat(A, s));  // built first: an unsupported matrix keeps its format
       drop_sell(A);
       drop_sorted(A);
+      drop_long(A);
       A->vec_width = 0;
       A->n_part = rowpat_parts(A);
       return MLAMG_OK;
@@ -2127,6 +2228,8 @@ int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
   double b = 8.0 * m + 8.0 * n;  // x read once, y written once
   if (A->vec_width) {
     b += 12.0 * A->nnz + 4.0 * (n + 1);
+  } else if (A->lg_tile) {
+    b += 12.0 * A->nnz + 4.0 * (n + 1) + 4.0 * (A->lg_nt + 1);
   } else if (A->rp_pid) {
     b += 1.0 * ((A->n_rows + 1) / 2) + 4.0 * 257 + 32.0 * A->rp_n_ent;  // pair ids + tables
   } else if (A->srt_pk) {
@@ -2202,6 +2305,7 @@ int mlamg_csr_attach_dinv(mlamg_csr* A, const double* dinv_w, void* stream) {
 int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* stored) {
   MLAMG_REQUIRE(A, "NULL argument");
   const int f = A->vec_width  ? MLAMG_FMT_VECTOR
+                : A->lg_tile   ? MLAMG_FMT_LONG
                 : A->rp_pid    ? MLAMG_FMT_ROWPAT
                 : A->srt_pk    ? MLAMG_FMT_SORTED
                 : A->dict_code ? MLAMG_FMT_SELL_DICT

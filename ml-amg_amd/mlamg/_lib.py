@@ -140,6 +140,8 @@ SIGNATURES = {
     "mlamg_pcg_solve": (c_int, [c_vp, c_vp, c_vp, c_vp]),
     "mlamg_pcg_stats": (c_int, [c_vp, P_i32, P_i32, P_i32, P_dbl, c_vp]),
     "mlamg_pcg_breakdowns": (c_int, [c_vp, P_i32, c_vp]),
+    "mlamg_gmres": (c_int, [c_vp, c_vp, c_vp, c_vp, c_dbl, c_int, c_int, c_int, P_int, P_int,
+                            c_vp, c_int, c_vp]),
     "mlamg_csr_symmetric": (c_int, [c_vp, c_dbl, P_int, c_vp]),
     "mlamg_hier_set_smoothing": (c_int, [c_vp, c_int, c_int]),
     "mlamg_hier_set_level_smoother": (c_int, [c_vp, c_int, c_vp]),

@@ -300,15 +300,16 @@ class DistributedHierarchy:
 
 
 def tune_local(M_glob, M_loc, kind, autotune=True):
-    """Kernel for one rank's local operator. Every exact-order format (CSR-stream, SELL, sorted,
-    dictionary SELL, row-pair patterns) sums each row in its stored order, so when the global
-    operator uses one of them any of them reproduces its rows bit for bit: with autotune the
-    fastest on the local operator (ghost columns change what the encoders accept and how well
-    they pack) is kept. A CSR-vector global operator keeps its lane width (that order is part of
-    the result). Returns (M_loc, {"chosen": ..., "us": {...}})."""
+    """Kernel for one rank's local operator. The local operator keeps every row's stored
+    entry order, so any kernel of the global operator's family reproduces its rows bit for bit:
+    the exact-order family (CSR-stream, SELL, sorted, dictionary SELL, row-pair patterns,
+    long-row tiles: scipy's order) or the CSR-vector family (one canonical order for every
+    width). With autotune the fastest of the family on the local operator is kept (ghost
+    columns change what the encoders accept and how well they pack). Returns
+    (M_loc, {"chosen": ..., "us": {...}})."""
     from .hierarchy import Hierarchy
     fmt, arg, _ = M_glob.get_format()
-    if fmt == "vector" or not autotune:
+    if not autotune:
         try:
             M_loc.set_format(fmt, arg)
         except _lib.MlamgError as e:  # e.g. sorted: ghost columns too far from owned
@@ -321,7 +322,13 @@ def tune_local(M_glob, M_loc, kind, autotune=True):
     if kind == "A" and M_loc.shape[0] != M_loc.shape[1]:
         kind = "R"  # ghost columns: mlamg_residual is square-only, time y = A x instead
     times = {}
-    for f, a in Hierarchy.EXACT_CANDIDATES:
+    if fmt == "vector":
+        cands = list(Hierarchy.VECTOR_CANDIDATES)
+    else:
+        cands = list(Hierarchy.EXACT_CANDIDATES)
+        if M_loc.nnz >= 16 * max(M_loc.shape[0], 1):
+            cands += list(Hierarchy.LONG_CANDIDATES)
+    for f, a in cands:
         try:
             times[f"{f}/{a}"] = Hierarchy._time_format(M_loc, f, a, x, y, kind=kind)
         except _lib.MlamgError as e:

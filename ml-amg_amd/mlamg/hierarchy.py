@@ -167,8 +167,8 @@ class Hierarchy:
 
     EXACT_CANDIDATES = (("csr_stream", 0), ("sell", 1), ("sell", 512), ("sorted", 0),
                         ("sell_dict", 1), ("sell_dict", 512), ("rowpat", 0))
-    VECTOR_CANDIDATES = (("vector", 8), ("vector", 16), ("vector", 32), ("vector", 64),
-                         ("vector", 128), ("vector", 256), ("vector", 512))
+    LONG_CANDIDATES = (("long", 0),)
+    VECTOR_CANDIDATES = (("vector", 64), ("vector", 128), ("vector", 256), ("vector", 512))
 
     @staticmethod
     def _time_format(M, fmt, arg, x, y, reps=5, kind="A"):
@@ -194,25 +194,42 @@ class Hierarchy:
         e1.synchronize()
         return e0.elapsed_time(e1) / reps * 1e3  # us
 
-    def apply_formats(self, fine_format="autotune", coarse_format="vector", vec_min_row=16):
+    # operators whose mean row has at least this many entries use the lane-parallel CSR-vector
+    # family (canonical order, one result for every width); shorter rows use the exact-order
+    # (scipy) family. A rule on the matrix, not a timing: measured on the C4 hierarchy
+    # (tools/coarse_formats.py) the vector kernels win from R_2 (357 entries per row: 18 vs
+    # 34 us) up and lose below (A_2, 187 per row: 79 vs 54 us).
+    VEC_MIN_MEAN_ROW = 256
+
+    def apply_formats(self, fine_format="autotune", coarse_format="auto", vec_min_row=None):
         """Choose the SpMV kernel of every operator.
 
-        Level-0 operators (A0, P0, R0: the ones with a scipy counterpart in the reference
-        cycle) always keep scipy's summation order: CSR-stream, SELL-64, SELL-64-sigma or
-        gather-sorted CSR-stream, all bitwise scipy. Coarser levels (the multilevel extension, no reference counterpart) may
-        also use the CSR-vector kernel for A_l and R_l when coarse_format='vector' and their
-        mean row length is >= vec_min_row; its fixed order is restated by the oracle.
-        fine_format='autotune' times every admissible kernel on each operator once and keeps
-        the fastest (results in self.tuning); any other value forces that format."""
+        The candidates of one operator all compute the same bits, so the autotune — a timing
+        decision — cannot change any result:
+          * mean row length < vec_min_row (default VEC_MIN_MEAN_ROW): the exact-order family,
+            scipy's left-to-right order (CSR-stream, SELL-64[-sigma], dictionary SELL,
+            gather-sorted CSR-stream, row-pair patterns, long-row tiles) — bitwise A @ x;
+          * otherwise (levels >= 1 only; coarse_format='auto'): the CSR-vector family, widths
+            64..512 in one canonical lane-parallel order (oracle.c vec_matvec), for the long
+            rows of coarse Galerkin operators where a one-lane chain is latency-bound.
+        Which family applies is a rule on the matrix; coarse_format='exact' keeps every
+        operator in the exact family. fine_format='autotune' times the family's kernels on each
+        operator once and keeps the fastest (self.tuning); any other value forces that format."""
+        if coarse_format not in ("auto", "exact", "vector"):
+            raise ValueError(f"coarse_format must be 'auto' or 'exact', got {coarse_format!r}")
+        vec_min_row = self.VEC_MIN_MEAN_ROW if vec_min_row is None else vec_min_row
         self.tuning = []
         dev = torch.device("cuda", torch.cuda.current_device())
         for i, L in enumerate(self.levels):
             row = {}
             for name, M in (("A", L.A), ("P", L.P), ("R", L.R)):
-                cands = list(self.EXACT_CANDIDATES)
-                if (i > 0 and name in ("A", "R") and coarse_format == "vector"
+                if (i > 0 and coarse_format != "exact" and M.shape[0] <= (1 << 20)
                         and M.nnz >= vec_min_row * M.shape[0]):
-                    cands += list(self.VECTOR_CANDIDATES)
+                    cands = list(self.VECTOR_CANDIDATES)
+                else:
+                    cands = list(self.EXACT_CANDIDATES)
+                    if M.nnz >= 16 * M.shape[0]:
+                        cands += list(self.LONG_CANDIDATES)
                 if fine_format != "autotune":
                     M.set_format(fine_format if fine_format != "vector" else "auto_exact")
                     row[name] = {"chosen": M.get_format()[:2]}
@@ -259,7 +276,7 @@ class Hierarchy:
     def build(cls, A, *, alpha=0.1, strength_mode="invabs", aggregation="bellman_ford",
               max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, seed=0, sort_seeds=True,
               lanczos_tol=1e-15, lanczos_iter=20000, lloyd_maxiter=10, nu_pre=1, nu_post=1,
-              fine_format="autotune", coarse_format="vector", verbose=False, finalize=True,
+              fine_format="autotune", coarse_format="auto", verbose=False, finalize=True,
               aggregates=None, prolongators=None):
         """Smoothed-aggregation hierarchy built on the GPU.
 
@@ -499,6 +516,30 @@ class Hierarchy:
         hist = self.cycle(bd, xd, maxiter, tol=tol)
         x = xd.cpu().numpy() if not isinstance(b, torch.Tensor) else xd
         return (x, hist) if return_history else x
+
+    def gmres(self, b, x0=None, rtol=1e-5, restart=20, maxiter=None, return_info=False):
+        """GMRES on A x = b preconditioned by one V-cycle of this hierarchy (mlamg_gmres:
+        scipy.sparse.linalg.gmres's algorithm — left-preconditioned, restarted MGS — with
+        ||b - A x|| <= rtol ||b||; the Krylov acceleration of ns/preconditioner/PyAMG.py:119).
+        x0=None starts from 0. Returns x (numpy in -> numpy out, tensor in -> tensor out), plus
+        {"info", "inner_iters", "presid"} (presid: preconditioned residual estimate / ||b|| per
+        Krylov step) with return_info=True."""
+        A = self.levels[0].A if self.levels else self.Ac
+        bd = to_device_vec(b)
+        xd = torch.zeros_like(bd) if x0 is None else to_device_vec(x0).clone()
+        n = bd.numel()
+        cap = 4096
+        hist = (ctypes.c_double * cap)()
+        info, inner = ctypes.c_int(), ctypes.c_int()
+        call("mlamg_gmres", A.handle, self.handle, ptr(bd), ptr(xd), float(rtol), int(restart),
+             int(maxiter or 0), int(x0 is None), ctypes.byref(info), ctypes.byref(inner), hist,
+             cap, stream_ptr())
+        x = xd if isinstance(b, torch.Tensor) else xd.cpu().numpy()
+        if not return_info:
+            return x
+        k = min(inner.value, cap)
+        return x, {"info": info.value, "inner_iters": inner.value,
+                   "presid": np.array(hist[:k])}
 
     def precondition(self, b):
         """One V-cycle from a zero guess: the action of the preconditioner on b."""

@@ -48,6 +48,14 @@ class _Options:
             return self._petsc.getInt(key, default)
         return int(self.store.get(key, default))
 
+    def getBool(self, key, default):
+        if self._petsc is not None:  # pragma: no cover
+            return self._petsc.getBool(key, default)
+        v = self.store.get(key, default)
+        if isinstance(v, str):
+            return v.strip().lower() in ("1", "true", "yes", "on")
+        return bool(v)
+
 
 def _csr_from_pc(pc):
     _, P = pc.getOperators()
@@ -135,11 +143,30 @@ class MLAMG:
 
 
 class MultilevelPC(MLAMG):
-    """Multilevel variant (the role of ns/preconditioner/PyAMG.py: pyamg SA solver, :94,119),
-    SA prolongators on Bellman-Ford aggregates down to a dense coarse level; stationary V-cycles
-    (no GMRES acceleration)."""
+    """The PyAMG PC (ns/preconditioner/PyAMG.py:13-130) on the MI355X.
+
+    Setup (:79-100): a multilevel smoothed-aggregation hierarchy of the operator, at most
+    '<prefix>pyamg_amg_max_levels' levels (default 10, :53) — built on the device (seeded
+    Bellman-Ford aggregates, SA prolongators, dense coarsest level) in place of pyamg's
+    smoothed_aggregation_solver (absent here).
+    Apply (:118-120), `Amg.solve(b, tol=amg_rtol, accel='gmres' if amg_precondition_with_gmres
+    else None)`: zero initial guess and a tolerance relative to ||b|| (pyamg's solve scales tol
+    by ||b||, and its default maxiter is 100).
+      * with GMRES (the default, :54): device GMRES preconditioned by one V-cycle
+        (Hierarchy.gmres: scipy's algorithm, restart 20, ||b - A x|| <= amg_rtol ||b||, at most
+        100 restart cycles);
+      * without: stationary V-cycles from x = 0 until ||b - A x|| <= amg_rtol ||b||, at most 100.
+    """
 
     _prefix = "pyamg_"
+    PYAMG_MAXITER = 100  # pyamg multilevel_solver.solve default
+
+    def _initialize(self, pc):
+        prefix = ((pc.getOptionsPrefix() if hasattr(pc, "getOptionsPrefix") else "") or "")
+        opts = _Options()
+        self.amg_precon_gmres = opts.getBool(
+            f"{prefix}{self._prefix}amg_precondition_with_gmres", True)
+        super()._initialize(pc)
 
     def _createAmgSolver(self, pc):
         A = _csr_from_pc(pc)
@@ -149,6 +176,24 @@ class MultilevelPC(MLAMG):
         levels = opts.getInt(f"{prefix}{self._prefix}amg_max_levels", 10)
         self.H = Hierarchy.build(A, alpha=self.alpha, max_levels=levels,
                                  jacobi_weight=self.jacobi_weight)
+
+    def _apply(self, pc, X, Y):
+        b = X.array_r if hasattr(X, "array_r") else np.asarray(X)
+        b = np.asarray(b, dtype=np.float64)
+        if self.amg_precon_gmres:
+            out = self.H.gmres(b, rtol=self.amg_rtol, restart=20, maxiter=self.PYAMG_MAXITER)
+        else:
+            normb = float(np.linalg.norm(b))
+            tol = self.amg_rtol * normb if normb != 0 else self.amg_rtol
+            bd = to_device_vec(b)
+            xd = torch.zeros_like(bd)
+            if normb > tol:  # pyamg: while residuals[-1] > tol (||r_0|| = ||b|| at x = 0)
+                self.H.cycle(bd, xd, self.PYAMG_MAXITER, tol=tol)
+            out = xd.cpu().numpy()
+        if hasattr(Y, "setArray"):
+            Y.setArray(out)
+        else:
+            Y[...] = out
 
 
 # ---------------------------------------------------------------------- package-level API

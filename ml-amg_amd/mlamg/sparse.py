@@ -162,11 +162,12 @@ class DeviceCSR:
         return NotImplemented
 
     FORMATS = {"csr_stream": 0, "sell": 1, "vector": 2, "auto_exact": 3, "sorted": 4,
-               "sell_dict": 5, "rowpat": 6}
+               "sell_dict": 5, "rowpat": 6, "long": 7}
 
     def set_format(self, fmt, vec_width=0):
-        """SpMV kernel/storage: 'csr_stream' | 'sell' | 'sorted' | 'auto_exact' (scipy order)
-        or 'vector' (lane-strided order, see include/mlamg.h)."""
+        """SpMV kernel/storage: 'csr_stream' | 'sell' | 'sell_dict' | 'sorted' | 'rowpat' |
+        'long' | 'auto_exact' (all scipy's order) or 'vector' (lane-strided order, see
+        include/mlamg.h)."""
         call("mlamg_csr_set_format", self.handle, self.FORMATS[fmt], int(vec_width), stream_ptr())
         return self
 

@@ -31,31 +31,28 @@ void ref_csr_matvec(int64_t n, const int32_t* ip, const int32_t* ij, const doubl
   }
 }
 
-/* The device CSR-vector order (mlamg_csr_set_format VECTOR): lane l of vw sums entries
- * l, l+vw, ... of the row in order, then partials combine by an xor butterfly off=vw/2..1. */
-/* device CSR-vector order (spmv.hip k_csr_vec / k_csr_vecw): lane l of vw sums entries l, l+vw,
- * ... in order; each group of min(vw, 64) lanes folds with an xor butterfly; for vw > 64 the
- * group (wave) sums are then added left to right. */
+/* device CSR-vector order (spmv.hip k_csr_vcan, every width 64..512 alike): 512 virtual lanes;
+ * virtual lane v = 64 w + l sums the row's entries v, v + 512, ... left to right from +0.0; each
+ * virtual wave w folds its 64 lanes with an xor butterfly (off = 32 .. 1: lane l becomes
+ * a[l] + a[l ^ off]); the row is ((ws_0 + ws_1) + ...) + ws_7. */
 void vec_matvec(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
-                const double* x, double* y, int vw) {
-  double part[512], nxt[512];
-  if (vw < 1 || vw > 512 || (vw & (vw - 1))) {
-    for (int64_t i = 0; i < n; ++i) y[i] = NAN;
-    return;
-  }
-  const int g = vw < 64 ? vw : 64;
+                const double* x, double* y) {
+  double part[512], nxt[64];
   for (int64_t i = 0; i < n; ++i) {
-    for (int l = 0; l < vw; ++l) {
+    for (int v = 0; v < 512; ++v) {
       double s = 0.0;
-      for (int32_t k = ip[i] + l; k < ip[i + 1]; k += vw) s += ax[k] * x[ij[k]];
-      part[l] = s;
+      for (int32_t k = ip[i] + v; k < ip[i + 1]; k += 512) s += ax[k] * x[ij[k]];
+      part[v] = s;
     }
-    for (int off = g / 2; off > 0; off >>= 1) {
-      for (int l = 0; l < vw; ++l) nxt[l] = part[l] + part[(l & ~(g - 1)) | ((l & (g - 1)) ^ off)];
-      for (int l = 0; l < vw; ++l) part[l] = nxt[l];
+    double r = 0.0;
+    for (int w = 0; w < 8; ++w) {
+      double* a = part + 64 * w;
+      for (int off = 32; off > 0; off >>= 1) {
+        for (int l = 0; l < 64; ++l) nxt[l] = a[l] + a[l ^ off];
+        for (int l = 0; l < 64; ++l) a[l] = nxt[l];
+      }
+      r = w == 0 ? a[0] : r + a[0];
     }
-    double r = part[0];
-    for (int w = 1; w < vw / g; ++w) r += part[w * g];
     y[i] = r;
   }
 }

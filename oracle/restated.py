@@ -34,7 +34,7 @@ def lib():
         L.ref_bellman_ford_torch.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
         L.ref_bellman_ford_torch.restype = ctypes.c_int
         L.canon_bellman_ford.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
-        L.vec_matvec.argtypes = [i64, vp, vp, vp, vp, vp, ctypes.c_int]
+        L.vec_matvec.argtypes = [i64, vp, vp, vp, vp, vp]
         L.lloyd_cluster.argtypes = [i64, vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int, vp, vp,
                                     ctypes.c_int]
         L.lloyd_cluster.restype = ctypes.c_int
@@ -63,20 +63,21 @@ def csr_matvec(A, x):
     return y
 
 
-def vec_matvec(A, x, vw):
-    """The device CSR-vector summation order (oracle.c vec_matvec)."""
-    if vw not in (4, 8, 16, 32, 64, 128, 256, 512):
-        raise ValueError(f"vector width must be 4..512 (power of two), got {vw}")
+def vec_matvec(A, x, vw=None):
+    """The device CSR-vector summation order (oracle.c vec_matvec): one canonical order for
+    every lane width (vw, 64..512, is accepted and checked but does not change the result)."""
+    if vw is not None and vw not in (64, 128, 256, 512):
+        raise ValueError(f"vector width must be 64, 128, 256 or 512, got {vw}")
     ip, ij, ax = _csr_arrays(A)
     x = np.ascontiguousarray(x, dtype=np.float64)
     y = np.empty(A.shape[0])
-    lib().vec_matvec(A.shape[0], _p(ip), _p(ij), _p(ax), _p(x), _p(y), int(vw))
+    lib().vec_matvec(A.shape[0], _p(ip), _p(ij), _p(ax), _p(x), _p(y))
     return y
 
 
 def mv(M, x, vw=0):
-    """M@x in scipy's order (vw == 0) or the device vector order (vw > 0)."""
-    return M @ x if not vw else vec_matvec(M, x, vw)
+    """M@x in scipy's order (vw == 0) or the device's canonical vector order (vw > 0)."""
+    return M @ x if not vw else vec_matvec(M, x)
 
 
 def gauss_seidel(A, x, b, iterations=1):

@@ -33,7 +33,7 @@ def dev(torch, x):
 
 @pytest.mark.parametrize("k", MATS)
 @pytest.mark.parametrize("fmt", ("sell", "csr_stream", "auto_exact", "sorted", "sell_dict",
-                                 "rowpat"))
+                                 "rowpat", "long"))
 def test_exact_formats_bitwise(golden, ml, torch_cuda, k, fmt):
     torch = torch_cuda
     A = golden_csr(golden, k)
@@ -56,18 +56,147 @@ def test_exact_formats_bitwise(golden, ml, torch_cuda, k, fmt):
     assert abs(nrm.item() - ref) <= 1e-13 * ref
 
 
-@pytest.mark.parametrize("vw", (4, 8, 16, 32, 64, 128, 256, 512))
-def test_vector_format_matches_oracle_order(ml, oracle, torch_cuda, vw):
+def test_vector_format_one_order_for_every_width(ml, oracle, torch_cuda):
+    """CSR-vector widths 64..512 compute one canonical order (oracle.c vec_matvec), for every
+    epilogue; rows from empty to several 512-entry stripes; other widths are refused."""
     torch = torch_cuda
-    rs = np.random.RandomState(vw)
-    A = sp.random(700, 650, density=0.08, random_state=rs, format="csr")
-    A.data -= 0.5
-    x = rs.randn(650)
-    Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("vector", vw)
-    assert Ad.get_format()[:2] == ("vector", vw)
-    y = Ad.matvec(dev(torch, x)).cpu().numpy()
-    assert np.array_equal(y, oracle.vec_matvec(A, x, vw))
-    assert np.allclose(y, A @ x, rtol=1e-12, atol=1e-12)
+    from mlamg._lib import MlamgError, call, ptr, stream_ptr
+    rs = np.random.RandomState(8)
+    n = 700
+    lens = rs.randint(0, 1500, n)
+    lens[::13] = 0
+    lens[5] = 4100
+    indptr = np.concatenate([[0], np.cumsum(lens)])
+    indices = np.concatenate([rs.randint(0, n, l) for l in lens]).astype(np.int32)
+    A = sp.csr_matrix((rs.randn(indptr[-1]) - 0.1, indices, indptr), shape=(n, n))
+    A.sum_duplicates()
+    A = A + sp.diags(np.abs(rs.randn(n)) + 1.0)
+    A = A.tocsr()
+    x, b, e = rs.randn(n), rs.randn(n), rs.randn(n)
+    ref = oracle.vec_matvec(A, x)
+    assert np.allclose(ref, A @ x, rtol=1e-11, atol=1e-11)
+    for vw in (0, 64, 128, 256, 512):
+        Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("vector", vw)
+        assert Ad.get_format()[0] == "vector"
+        xd, bd = dev(torch, x), dev(torch, b)
+        assert np.array_equal(Ad.matvec(xd).cpu().numpy(), ref)
+        r = torch.empty_like(bd)
+        nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
+        call("mlamg_residual", Ad.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), stream_ptr())
+        assert np.array_equal(r.cpu().numpy(), b - ref)
+        if vw:
+            nrm_ref = nrm.item() if vw == 64 else nrm_ref
+            assert nrm.item() == nrm_ref  # per-row partials: the norm is width-independent
+        y = dev(torch, e)
+        call("mlamg_prolong_add", Ad.handle, ptr(xd), ptr(y), stream_ptr())
+        assert np.array_equal(y.cpu().numpy(), e + ref)
+    for bad in (4, 8, 32, 1024):
+        with pytest.raises(MlamgError):
+            ml.sparse.DeviceCSR.from_scipy(A).set_format("vector", bad)
+
+
+def test_long_format_ragged_chunked_and_epilogues(ml, torch_cuda):
+    """long format (csrc/spmv.hip k_csr_long): bitwise scipy on ragged rows — empty rows, rows
+    of exactly one tile (4096), rows longer than a tile (streamed in chunks), tiles capped at 64
+    rows — for y = A x, the residual (+ norm partials), x += A e and the Jacobi sweep."""
+    torch = torch_cuda
+    from mlamg._lib import call, ptr, stream_ptr
+    rs = np.random.RandomState(11)
+    n = 6000
+    lens = rs.randint(0, 900, n)
+    lens[::41] = 0
+    lens[7] = 4096
+    lens[8] = 4097
+    lens[100] = 5999
+    lens[200:330] = rs.randint(0, 5, 130)  # short rows: tiles hit the 64-row cap
+    indptr = np.concatenate([[0], np.cumsum(lens)])
+    indices = np.concatenate([rs.choice(n, l, replace=False) for l in lens])  # unsorted rows
+    A = sp.csr_matrix((rs.randn(indptr[-1]), indices, indptr), shape=(n, n))
+    A.setdiag(np.abs(rs.randn(n)) + 1.0)
+    A = A.tocsr()
+    Ad = ml.sparse.DeviceCSR.from_scipy(A, check=False).set_format("long")
+    assert Ad.get_format()[0] == "long"
+    A = Ad.to_scipy()  # the stored order the kernel sums in
+    x, b, e = rs.randn(n), rs.randn(n), rs.randn(n)
+    xd, bd = dev(torch, x), dev(torch, b)
+    ref_y = ml.sparse.DeviceCSR.from_scipy(A, check=False)  # csr_stream: scipy's order
+    assert np.array_equal(Ad.matvec(xd).cpu().numpy(), A @ x)
+    assert np.array_equal(ref_y.matvec(xd).cpu().numpy(), A @ x)
+    r = torch.empty_like(bd)
+    nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
+    call("mlamg_residual", Ad.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), stream_ptr())
+    assert np.array_equal(r.cpu().numpy(), b - A @ x)
+    assert abs(nrm.item() - np.linalg.norm(b - A @ x)) <= 1e-13 * np.linalg.norm(b - A @ x)
+    y = dev(torch, e)
+    call("mlamg_prolong_add", Ad.handle, ptr(xd), ptr(y), stream_ptr())
+    assert np.array_equal(y.cpu().numpy(), e + A @ x)
+    dw = Ad.diag_inv(2.0 / 3.0)
+    xs, t = dev(torch, x), torch.empty_like(xd)
+    call("mlamg_jacobi", Ad.handle, ptr(dw), ptr(bd), ptr(xs), ptr(t), 1, stream_ptr())
+    d = dw.cpu().numpy()
+    assert np.array_equal(xs.cpu().numpy(), x + d * (b - A @ x))
+
+
+def test_results_do_not_depend_on_format_choice(ml, oracle, torch_cuda):
+    """the autotune picks among kernels that compute the same bits — the
+    exact-order family (scipy's order) for rows shorter than Hierarchy.VEC_MIN_MEAN_ROW, the
+    CSR-vector family (one canonical order for every width) for longer coarse rows — so forcing
+    any other member of the family on every operator leaves the V-cycle iterate bitwise
+    unchanged (the residual norm's partial sums are grouped per kernel block, so the history
+    agrees to rounding). The iterate's history matches the oracle cycle, which needs no
+    per-operator order information beyond the family."""
+    torch = torch_cuda
+    A = ml.problems.poisson_3d_7pt(40)
+    n = A.shape[0]
+    x0 = np.random.RandomState(0).randn(n)
+    b = np.random.RandomState(1).randn(n)
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=300, coarse_format="auto")
+    assert H.n_levels >= 3
+    ops = [M for L in H.levels for M in (L.A, L.P, L.R)]
+    family = ["vector" if M.get_format()[0] == "vector" else "exact" for M in ops]
+    outs = []
+    exact_forced = ("csr_stream", "long", "sorted", "sell")
+    for step in range(5):
+        if step > 0:
+            for M, fam in zip(ops, family):
+                if fam == "vector":
+                    M.set_format("vector", (64, 128, 256, 512)[step - 1])
+                else:
+                    try:
+                        M.set_format(exact_forced[step - 1])
+                    except ml._lib.MlamgError:
+                        M.set_format("csr_stream")
+            H.attach_dinvs()
+        xd = dev(torch, x0)
+        h = H.cycle(dev(torch, b), xd, 4)
+        outs.append((xd.cpu().numpy(), h))
+    for xo, ho in outs[1:]:
+        assert np.array_equal(xo, outs[0][0])
+        assert np.allclose(ho, outs[0][1], rtol=1e-13, atol=0)
+    lv = _oracle_levels_from_device(H)
+    xr, hr = oracle.vcycle_solve(lv, H.Ac.to_scipy(), b, x0, 4)
+    assert np.allclose(outs[0][1], hr, rtol=1e-10, atol=0)
+
+
+def test_vector_family_rule_c3_like(ml, torch_cuda):
+    """The family is a rule on the matrix (mean row length), not a timing: two builds choose
+    the same family for every operator and give bitwise-identical iterates."""
+    torch = torch_cuda
+    A = ml.problems.poisson_3d_7pt(48)
+    n = A.shape[0]
+    x0 = np.random.RandomState(2).randn(n)
+    res = []
+    for _ in range(2):
+        H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=300)
+        fams = [[f[k][0] == "vector" for k in "APR"] for f in H.formats()]
+        for L, fam in zip(H.levels, fams):
+            for k, M in zip("APR", (L.A, L.P, L.R)):
+                long_rows = M.nnz >= H.VEC_MIN_MEAN_ROW * M.shape[0]
+                assert fam["APR".index(k)] == (long_rows and L is not H.levels[0])
+        xd = dev(torch, x0)
+        H.cycle(torch.zeros(n, dtype=torch.float64, device="cuda"), xd, 3)
+        res.append((fams, xd.cpu().numpy()))
+    assert res[0][0] == res[1][0] and np.array_equal(res[0][1], res[1][1])
 
 
 def test_sell_ragged_rows(ml, torch_cuda):

@@ -15,7 +15,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 FORMATS = (("csr_stream", 0), ("sell", 1), ("sell", 512), ("sorted", 0), ("sell_dict", 1),
-           ("rowpat", 0), ("vector", 8), ("vector", 64))
+           ("rowpat", 0), ("long", 0), ("vector", 64), ("vector", 256))
 
 
 @pytest.fixture(scope="module")
