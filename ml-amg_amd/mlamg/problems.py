@@ -80,6 +80,38 @@ def poisson_3d_7pt(nx, ny=None, nz=None):
     return _csr_from_stencil(n, cols, vals)
 
 
+def random_coeff_3d_7pt(nx, seed=0, decades=1.0):
+    """7-point finite-volume diffusion -div(k grad u) on an nx^3 interior grid (Dirichlet), with
+    an independent coefficient k = 10^U(-decades, decades) on every cell face (RandomState(seed)),
+    boundary faces included: a symmetric M-matrix with the C4 sparsity (nnz 70,263,936 at 216^3)
+    whose values are all distinct, so no stencil re-encoding (row-pair patterns, dictionary
+    SELL) applies — the generic-operator counterpart of the C4 headline."""
+    n = nx ** 3
+    rs = np.random.RandomState(seed)
+    # face coefficients: kx[i] couples cell i with its +x neighbour (or the boundary)
+    kx = 10.0 ** rs.uniform(-decades, decades, n)
+    ky = 10.0 ** rs.uniform(-decades, decades, n)
+    kz = 10.0 ** rs.uniform(-decades, decades, n)
+    # the -x / -y / -z faces of the first cells of each line are boundary faces of their own
+    kx0 = 10.0 ** rs.uniform(-decades, decades, n)
+    ky0 = 10.0 ** rs.uniform(-decades, decades, n)
+    kz0 = 10.0 ** rs.uniform(-decades, decades, n)
+    idx = np.arange(n, dtype=np.int64)
+    x = idx % nx
+    y = (idx // nx) % nx
+    z = idx // (nx * nx)
+    pl = nx * nx
+    kxm = np.where(x > 0, kx[np.maximum(idx - 1, 0)], kx0)
+    kym = np.where(y > 0, ky[np.maximum(idx - nx, 0)], ky0)
+    kzm = np.where(z > 0, kz[np.maximum(idx - pl, 0)], kz0)
+    diag = kxm + kx + kym + ky + kzm + kz
+    cols = [np.where(z > 0, idx - pl, -1), np.where(y > 0, idx - nx, -1),
+            np.where(x > 0, idx - 1, -1), idx, np.where(x < nx - 1, idx + 1, -1),
+            np.where(y < nx - 1, idx + nx, -1), np.where(z < nx - 1, idx + pl, -1)]
+    vals = [-kzm, -kym, -kxm, diag, -kx, -ky, -kz]
+    return _csr_from_stencil(n, cols, vals)
+
+
 def voronoi_jumps(rand, ns=None):
     """Jump seeds [x, y, d] like utils/create_data.py:69-78 (d = 10^U(-4,4), ptp > 1e3)."""
     ns = rand.randint(2, 4) if ns is None else ns

@@ -1,6 +1,8 @@
 """GPU parity on the BASELINE.json configurations other than the bench line:
 C2 (2D 5-point 1024^2), C3 (P1 Laplacian on the reference's cylflow-highres mesh, also x4^2
-refined), C5 (Voronoi jump coefficients, on the C2-style grid and on the C3 mesh).
+refined), C5 (Voronoi jump coefficients, on the C2-style grid and on the C3 mesh), and the
+variable-coefficient 3D 7-point operator of bench.py's second line (at 64^3: no stencil
+re-encoding applies, values all distinct).
 
 For each: the device hierarchy (seeded Bellman-Ford aggregates, SA prolongators, Galerkin) is
 compared level by level, bit for bit, with the oracle's CPU restatement of the same recipe (fed
@@ -55,6 +57,8 @@ def _matrix(name):
     if name == "lap3d_grid":  # the reference's own demos/laplace_3d.grid (1331 DoF, aniso P1)
         g = np.load(os.path.join(HERE, "golden", "laplace_3d_grid.npz"))
         return sp.csr_matrix((g["data"], g["indices"], g["indptr"]))
+    if name == "varcoef3d_64":  # bench.py's variable-coefficient C4 line at 64^3
+        return problems.random_coeff_3d_7pt(64, seed=0)
     if name == "aniso3d_48":  # utils/create_3d_laplace.py family at 47^3 interior DoF
         return mesh.aniso_laplace_3d(48, 48, 48, theta_y=1.0, theta_z=0.5, eps_x=1e-2,
                                      eps_y=10.0)[0]
@@ -62,7 +66,7 @@ def _matrix(name):
 
 
 @pytest.mark.parametrize("name", ("c2_1024", "c3", "c3_r2", "c5_grid", "c5_mesh", "lap3d_grid",
-                                  "aniso3d_48"))
+                                  "aniso3d_48", "varcoef3d_64"))
 def test_config_hierarchy_and_cycle_parity(ml, oracle, torch_cuda, name):
     torch = torch_cuda
     A = _matrix(name)
@@ -106,3 +110,15 @@ def test_config_hierarchy_and_cycle_parity(ml, oracle, torch_cuda, name):
     assert np.allclose(hd, ho, rtol=1e-11, atol=0), (hd, ho)
     assert np.allclose(xd.cpu().numpy(), xo, rtol=1e-9, atol=1e-11 * np.abs(xo).max())
     assert hd[-1] < hd[0]
+
+
+def test_varcoef_refuses_stencil_encodings(ml, torch_cuda):
+    """The variable-coefficient operator is a generic CSR: rowpat and dictionary SELL refuse it,
+    so the bench line beside the headline streams 12 B per nonzero."""
+    from mlamg._lib import MLAMG_EUNSUPPORTED, MlamgError
+    from mlamg.sparse import DeviceCSR
+    Ad = DeviceCSR.from_scipy(_matrix("varcoef3d_64"))
+    for fmt in ("rowpat", "sell_dict"):
+        with pytest.raises(MlamgError) as e:
+            Ad.set_format(fmt)
+        assert e.value.code == MLAMG_EUNSUPPORTED

@@ -177,6 +177,15 @@ def test_loopback_c4_world8_bench_partition():
     # itself is the same noise-dependent contest as above)
     for D in Ds:
         assert any(k.startswith("rowpat") for k in D.tuning[0].get("us", {})), D.tuning[0]
+    # every rank's local kernel is a member of its global operator's family (exact order or
+    # canonical vector order), so the per-rank timing contest cannot change a bit
+    def fam(f):
+        return "vector" if f.startswith("vector") else "exact"
+    for D in Ds:
+        for l in range(D.K):
+            glob = {"A": H.levels[l].A, "P": H.levels[l].P, "R": H.levels[l].R}
+            for k, t in zip("APR", D.tuning[3 * l:3 * l + 3]):
+                assert fam(t["chosen"]) == fam(glob[k].get_format()[0]), (l, k, t["chosen"])
     for D, (x_own, h) in zip(Ds, out):
         assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank}"
         np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
