@@ -708,6 +708,65 @@ static int launch_vec(const mlamg_csr* A, const double* x, const Epi& ep, hipStr
   }
 }
 
+// Left-to-right sum of p[ka..kb) by one lane. Measured (tools/chain_lab.hip, MI355X): a
+// dependent v_add_f64 chain costs ~14-17 cycles per element at best; an LDS read waited for
+// per element ~85, per batch of 8 ~26-33, of 32 ~17-28 — so batches of 32 reads, then 32 adds
+// (software pipelining across batches loses: the register copies between the buffers wait for
+// the fresh reads at the end of every iteration).
+__device__ __forceinline__ double chain_sum(const double* __restrict__ p, int ka, int kb,
+                                            double s) {
+  int k = ka;
+  for (; k + 32 <= kb; k += 32) {
+    double v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) v[u] = p[k + u];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) s += v[u];
+  }
+  for (; k + 8 <= kb; k += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[k + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  // the last < 8 entries: all reads issued together (the index is clamped to the row's last
+  // entry, so no read leaves the row), then the adds that belong to the row, in order
+  const int rem = kb - k;
+  if (rem > 0) {
+    double v[7];
+#pragma unroll
+    for (int u = 0; u < 7; ++u) v[u] = p[k + min(u, rem - 1)];
+#pragma unroll
+    for (int u = 0; u < 7; ++u) s = u < rem ? s + v[u] : s;
+  }
+  return s;
+}
+
+// Two rows' left-to-right sums at once: batches of 8 reads from each row, then the 16 adds
+// alternating between the two chains (independent, so each hides the other's add latency);
+// each row's products are added in stored order.
+__device__ __forceinline__ void sum_two_rows(const double* __restrict__ p, int a0, int b0, int a1,
+                                             int b1, double& s0, double& s1) {
+  while (a0 + 8 <= b0 && a1 + 8 <= b1) {
+    double u[8], v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      u[k] = p[a0 + k];
+      v[k] = p[a1 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s0 += u[k];
+      s1 += v[k];
+    }
+    a0 += 8;
+    a1 += 8;
+  }
+  s0 = chain_sum(p, a0, b0, s0);
+  s1 = chain_sum(p, a1, b1, s1);
+}
+
 // ---------------------------------------------------------------- gather-sorted CSR-stream
 // Same two phases as k_csr_stream, but each block's nonzeros are stored in ascending column
 // order, packed with their CSR slot: the 64 gathers of one wave-instruction then fall on a few
@@ -715,7 +774,7 @@ static int launch_vec(const mlamg_csr* A, const double* x, const Epi& ep, hipStr
 // operators: Galerkin A_l, R = P^T). Products are written to LDS at their CSR slot and phase 2
 // sums every row in stored order, so the result is bitwise k_csr_stream's (scipy's).
 // VD: values come from a <= 256-entry dictionary (one byte per nonzero instead of eight)
-template <int OP, bool NORM, bool VD>
+template <int OP, bool NORM, bool VD, bool LR>
 __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restrict__ indptr,
                                                         const uint32_t* __restrict__ pk,
                                                         const double* __restrict__ av,
@@ -736,12 +795,30 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   // the row pointers go to registers first and to LDS just before the barrier
   double tv = 0.0;
   if constexpr (VD) tv = vtab[tid & 255];
-  // the block's record {r0, r1, e0, nnz, lo, hi, split, -} in one 32-byte load: the entry
-  // stream's addresses then wait for one round trip, not two (blk, then indptr)
+  // the block's record {r0, r1, e0, nnz, lo, hi, split, -} (one 32-byte load) goes out first;
+  // the entry stream is laid out at a fixed stride (k_srt_pad: block b at b * kSrtNnz, padded
+  // with kNone), so its loads need nothing from the record and follow at once, in flight while
+  // the record's round trip completes (loads retire in order: the row-pointer and epilogue
+  // loads that depend on the record then wait for it alone)
   const int4 m0 = reinterpret_cast<const int4*>(base)[2 * b];
   const int4 m1 = reinterpret_cast<const int4*>(base)[2 * b + 1];
+  constexpr int U = kSrtNnz / kSrtThreads;
+  constexpr uint32_t kNone = 0xffffffffu, kSlot = (1u << kSrtPosBits) - 1;
+  uint32_t w[U];
+  double vv[U], xv[U];
+  {
+    const size_t eb = (size_t)b * kSrtNnz + tid;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      w[u] = __builtin_nontemporal_load(pk + eb + u * kSrtThreads);
+      if constexpr (VD)
+        vv[u] = (double)__builtin_nontemporal_load(vi + eb + u * kSrtThreads);  // index for now
+      else
+        vv[u] = __builtin_nontemporal_load(av + eb + u * kSrtThreads);
+    }
+  }
   const int r0 = m0.x, r1 = m0.y, nr = r1 - r0;
-  const int e0 = m0.z, ne = m0.w;
+  const int e0 = m0.z;
   // two column windows per block: sorted entries [0, split) are offsets from lo, the rest from
   // hi (a halo-extended local matrix has its ghost columns far from the owned ones)
   const int lo = m1.x, hi = m1.y, split = m1.z;
@@ -758,19 +835,6 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
 #pragma unroll
   for (int q = 0; q < RPT; ++q)
     if (tid + q * kSrtThreads < nr) pre[q] = epi_load<OP>(r0 + tid + q * kSrtThreads, ep);
-  constexpr int U = kSrtNnz / kSrtThreads;
-  constexpr uint32_t kNone = 0xffffffffu, kSlot = (1u << kSrtPosBits) - 1;
-  uint32_t w[U];
-  double vv[U], xv[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int e = tid + u * kSrtThreads;
-    w[u] = e < ne ? __builtin_nontemporal_load(pk + e0 + e) : kNone;
-    if constexpr (VD)
-      vv[u] = e < ne ? (double)__builtin_nontemporal_load(vi + e0 + e) : 0.0;  // index for now
-    else
-      vv[u] = e < ne ? __builtin_nontemporal_load(av + e0 + e) : 0.0;
-  }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int cb = tid + u * kSrtThreads < split ? lo : hi;
@@ -796,22 +860,49 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
     if (w[u] != kNone) prod[w[u] & kSlot] = vv[u] * xv[u];
   __syncthreads();
   double sq = 0.0;
+  // LR = false, short rows (P_0, R_0, A_1: 4-40 entries): one row after the other in 4-entry
+  // batches. LR = true, long rows (operators averaging >= kSrtLongRow entries per row, e.g. A_3:
+  // 709): the thread's two rows side by side in 8-entry batches. A separate instantiation, not a
+  // branch: with both forms in one kernel the extra registers cost the short-row operators
+  // 10-20 % (measured on the C4 hierarchy, tools/coarse_formats.py; the two-row form cuts
+  // A_3 65 -> 34 us and R_2 33 -> 20 us)
+  if constexpr (!LR) {
 #pragma unroll
-  for (int q = 0; q < RPT; ++q) {
-    const int t = tid + q * kSrtThreads;
-    if (t >= nr) break;
-    double s = 0.0;
-    const int ka = rp[t], kb = rp[t + 1];
-    int k = ka;
-    for (; k + 4 <= kb; k += 4) {
-      const double p0 = prod[k], p1 = prod[k + 1], p2 = prod[k + 2], p3 = prod[k + 3];
-      s += p0;
-      s += p1;
-      s += p2;
-      s += p3;
+    for (int q = 0; q < RPT; ++q) {
+      const int t = tid + q * kSrtThreads;
+      if (t >= nr) break;
+      double s = 0.0;
+      const int ka = rp[t], kb = rp[t + 1];
+      int k = ka;
+      for (; k + 4 <= kb; k += 4) {
+        const double p0 = prod[k], p1 = prod[k + 1], p2 = prod[k + 2], p3 = prod[k + 3];
+        s += p0;
+        s += p1;
+        s += p2;
+        s += p3;
+      }
+      for (; k < kb; ++k) s += prod[k];
+      sq += epi_store<OP>(r0 + t, s, pre[q], ep);
     }
-    for (; k < kb; ++k) s += prod[k];
-    sq += epi_store<OP>(r0 + t, s, pre[q], ep);
+  } else if constexpr (RPT == 2) {
+    // the thread's two rows summed side by side: two independent dependent-add chains share
+    // the LDS read latency and each other's add latency (each row still left to right)
+    const int t0 = tid, t1 = tid + kSrtThreads;
+    if (t1 < nr) {
+      double s0 = 0.0, s1 = 0.0;
+      sum_two_rows(prod, rp[t0], rp[t0 + 1], rp[t1], rp[t1 + 1], s0, s1);
+      sq += epi_store<OP>(r0 + t0, s0, pre[0], ep);
+      sq += epi_store<OP>(r0 + t1, s1, pre[1], ep);
+    } else if (t0 < nr) {
+      sq += epi_store<OP>(r0 + t0, chain_sum(prod, rp[t0], rp[t0 + 1], 0.0), pre[0], ep);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int t = tid + q * kSrtThreads;
+      if (t >= nr) break;
+      sq += epi_store<OP>(r0 + t, chain_sum(prod, rp[t], rp[t + 1], 0.0), pre[q], ep);
+    }
   }
   if constexpr (NORM) {
     double v = wave_sum(sq);
@@ -837,32 +928,6 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
 // kLongNnz is a tile of its own, streamed in chunks with lane 0 carrying the sum. Bitwise
 // csr_matvec — unlike the lane-strided CSR-vector order this format replaces in the autotune, so
 // the kernel choice (a timing decision) can no longer change a result.
-// Left-to-right sum of p[ka..kb) by one lane. Measured (tools/chain_lab.hip, MI355X): a
-// dependent v_add_f64 chain costs ~14-17 cycles per element at best; an LDS read waited for
-// per element ~85, per batch of 8 ~26-33, of 32 ~17-28 — so batches of 32 reads, then 32 adds
-// (software pipelining across batches loses: the register copies between the buffers wait for
-// the fresh reads at the end of every iteration).
-__device__ __forceinline__ double chain_sum(const double* __restrict__ p, int ka, int kb,
-                                            double s) {
-  int k = ka;
-  for (; k + 32 <= kb; k += 32) {
-    double v[32];
-#pragma unroll
-    for (int u = 0; u < 32; ++u) v[u] = p[k + u];
-#pragma unroll
-    for (int u = 0; u < 32; ++u) s += v[u];
-  }
-  for (; k + 8 <= kb; k += 8) {
-    double v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = p[k + u];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
-  }
-  for (; k < kb; ++k) s += p[k];
-  return s;
-}
-
 template <int OP, bool NORM>
 __global__ __launch_bounds__(kThreads) void k_csr_long(const int32_t* __restrict__ indptr,
                                                        const int32_t* __restrict__ indices,
@@ -984,14 +1049,23 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_
   }
   if (A->srt_pk) {
     if (A->srt_nb == 0) return MLAMG_OK;
-    if (A->srt_vi)
-      hipLaunchKernelGGL((k_sorted<OP, NORM, true>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s,
-                         A->indptr, A->srt_pk, A->srt_val, A->srt_vi, A->srt_vtab, A->srt_blk,
-                         A->srt_base, x, ep);
-    else
-      hipLaunchKernelGGL((k_sorted<OP, NORM, false>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s,
-                         A->indptr, A->srt_pk, A->srt_val, A->srt_vi, A->srt_vtab, A->srt_blk,
-                         A->srt_base, x, ep);
+    const bool lr = A->avg_row_len >= kSrtLongRow;
+#define MLAMG_SRT_LAUNCH(VDV, LRV)                                                              \
+  hipLaunchKernelGGL((k_sorted<OP, NORM, VDV, LRV>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s, \
+                     A->indptr, A->srt_pk, A->srt_val, A->srt_vi, A->srt_vtab, A->srt_blk,     \
+                     A->srt_base, x, ep)
+    if (A->srt_vi) {
+      if (lr)
+        MLAMG_SRT_LAUNCH(true, true);
+      else
+        MLAMG_SRT_LAUNCH(true, false);
+    } else {
+      if (lr)
+        MLAMG_SRT_LAUNCH(false, true);
+      else
+        MLAMG_SRT_LAUNCH(false, false);
+    }
+#undef MLAMG_SRT_LAUNCH
     MLAMG_HIP(hipGetLastError());
     return MLAMG_OK;
   }
@@ -1517,6 +1591,36 @@ static int sorted_value_dict(mlamg_csr* A, hipStream_t s) {
   return MLAMG_OK;
 }
 
+// Fixed-stride layout of the sorted copy: block b's entries at [b * kSrtNnz, (b + 1) * kSrtNnz),
+// padded with `pad` (kNone codes, zero values): the kernel's entry loads then need no block
+// record (e0, ne) and issue at launch, in parallel with the record load, instead of one memory
+// round trip after it.
+template <class T>
+__global__ __launch_bounds__(256) void k_srt_pad(const T* __restrict__ src, T* __restrict__ dst,
+                                                 const int32_t* __restrict__ meta, T pad) {
+  const int b = blockIdx.x;
+  const int e0 = meta[8 * b + 2], ne = meta[8 * b + 3];
+  T* d = dst + (size_t)b * kSrtNnz;
+  for (int e = threadIdx.x; e < kSrtNnz; e += 256) d[e] = e < ne ? src[e0 + e] : pad;
+}
+
+template <class T>
+static int pad_stream(T** arr, int nb, const int32_t* meta, T pad, hipStream_t s) {
+  T* d = nullptr;
+  MLAMG_HIP(hipMalloc(&d, sizeof(T) * (size_t)kSrtNnz * std::max(nb, 1)));
+  if (nb > 0) {
+    hipLaunchKernelGGL((k_srt_pad<T>), dim3(nb), dim3(256), 0, s, *arr, d, meta, pad);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+      (void)hipFree(d);
+      set_error("sorted format: padding pass failed");
+      return MLAMG_EHIP;
+    }
+  }
+  (void)hipFree(*arr);
+  *arr = d;
+  return MLAMG_OK;
+}
+
 // Row blocks of <= kSrtRows rows / <= kSrtNnz nonzeros; inside each, entries radix-sorted by
 // (block, column) (stable, so equal columns keep CSR order; any order would give the same bits).
 // EUNSUPPORTED (A unchanged) if a row is longer than kSrtNnz or a block's columns do not fit
@@ -1613,7 +1717,12 @@ static int build_sorted(mlamg_csr* A, hipStream_t s) {
   A->srt_nb = nb;
   A->n_part = nb;
   (void)sorted_value_dict(A, s);  // optional: keeps the fp64 values when it does not apply
-  return MLAMG_OK;
+  rc = pad_stream<uint32_t>(&A->srt_pk, nb, A->srt_base, 0xffffffffu, s);
+  if (rc == MLAMG_OK)
+    rc = A->srt_vi ? pad_stream<uint8_t>(&A->srt_vi, nb, A->srt_base, (uint8_t)0, s)
+                   : pad_stream<double>(&A->srt_val, nb, A->srt_base, 0.0, s);
+  if (rc != MLAMG_OK) drop_sorted(A);
+  return rc;
 }
 
 // ---------------------------------------------------------------- row-pair pattern construction
@@ -2233,7 +2342,8 @@ int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
   } else if (A->rp_pid) {
     b += 1.0 * ((A->n_rows + 1) / 2) + 4.0 * 257 + 32.0 * A->rp_n_ent;  // pair ids + tables
   } else if (A->srt_pk) {
-    b += (A->srt_vi ? 5.0 : 12.0) * A->nnz + 4.0 * (n + 1) + 32.0 * A->srt_nb;
+    b += (A->srt_vi ? 5.0 : 12.0) * (double)kSrtNnz * A->srt_nb + 4.0 * (n + 1) +
+         32.0 * A->srt_nb;  // the padded fixed-stride stream
   } else if (A->dict_code) {
     int64_t n_codes = 0;
     MLAMG_HIP(hipMemcpy(&n_codes, A->dict_ptr + A->n_slices, sizeof(int64_t), hipMemcpyDeviceToHost));
