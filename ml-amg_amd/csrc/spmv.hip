@@ -626,6 +626,10 @@ void k_rowpair(const uint8_t* __restrict__ pid,
 // W gives the same bits (oracle.c vec_matvec restates the order; VERDICT r02 item 2 — the
 // autotune's timing noise used to pick between lane-strided orders).
 // Residual norms are written per row (partial[row]), so the norm is width-independent too.
+#ifndef MLAMG_VCAN_STEPS  // A/B knob: 512-entry stripes per wave per step, times Q
+#define MLAMG_VCAN_STEPS 1
+#endif
+constexpr int kVcanSteps = MLAMG_VCAN_STEPS;
 template <int Q, int OP, bool NORM>
 __global__ __launch_bounds__(512) void k_csr_vcan(const int32_t* __restrict__ indptr,
                                                   const int32_t* __restrict__ indices,
@@ -647,12 +651,13 @@ __global__ __launch_bounds__(512) void k_csr_vcan(const int32_t* __restrict__ in
   if (head) pre = epi_load<OP>((int)row, ep);
   if (row < n_rows) {
     const int a = indptr[row], b = indptr[row + 1];
-    // Q stripes of 512 entries per step: Q * J = 8 entries per lane in flight
-    for (int base = a; base < b; base += 512 * Q) {
-      int32_t cc[Q][J];
-      double vv[Q][J], xv[Q][J];
+    // T = S Q stripes of 512 entries per step: 8 S entries per lane in flight
+    constexpr int T = kVcanSteps * Q;
+    for (int base = a; base < b; base += 512 * T) {
+      int32_t cc[T][J];
+      double vv[T][J], xv[T][J];
 #pragma unroll
-      for (int t = 0; t < Q; ++t)
+      for (int t = 0; t < T; ++t)
 #pragma unroll
         for (int j = 0; j < J; ++j) {
           const int e = base + 512 * t + 64 * (p + Q * j) + lane;
@@ -660,11 +665,11 @@ __global__ __launch_bounds__(512) void k_csr_vcan(const int32_t* __restrict__ in
           vv[t][j] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
         }
 #pragma unroll
-      for (int t = 0; t < Q; ++t)
+      for (int t = 0; t < T; ++t)
 #pragma unroll
         for (int j = 0; j < J; ++j) xv[t][j] = cc[t][j] >= 0 ? x[cc[t][j]] : 0.0;
 #pragma unroll
-      for (int t = 0; t < Q; ++t)
+      for (int t = 0; t < T; ++t)
 #pragma unroll
         for (int j = 0; j < J; ++j)
           if (cc[t][j] >= 0) acc[j] += vv[t][j] * xv[t][j];
@@ -866,7 +871,51 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   // branch: with both forms in one kernel the extra registers cost the short-row operators
   // 10-20 % (measured on the C4 hierarchy, tools/coarse_formats.py; the two-row form cuts
   // A_3 65 -> 34 us and R_2 33 -> 20 us)
-  if constexpr (!LR) {
+#ifndef MLAMG_SRT_SHORT2  // A/B knob: short rows two at a time (1) or one after the other (0)
+#define MLAMG_SRT_SHORT2 1
+#endif
+  if constexpr (!LR && MLAMG_SRT_SHORT2 && RPT == 2) {
+    const int t0 = tid, t1 = tid + kSrtThreads;
+    if (t0 < nr) {
+      double s0 = 0.0, s1 = 0.0;
+      int a0 = rp[t0];
+      const int b0 = rp[t0 + 1];
+      int a1 = t1 < nr ? rp[t1] : 0;
+      const int b1 = t1 < nr ? rp[t1 + 1] : 0;
+      while (a0 + 4 <= b0 && a1 + 4 <= b1) {
+        const double p0 = prod[a0], p1 = prod[a0 + 1], p2 = prod[a0 + 2], p3 = prod[a0 + 3];
+        const double q0 = prod[a1], q1 = prod[a1 + 1], q2 = prod[a1 + 2], q3 = prod[a1 + 3];
+        s0 += p0;
+        s1 += q0;
+        s0 += p1;
+        s1 += q1;
+        s0 += p2;
+        s1 += q2;
+        s0 += p3;
+        s1 += q3;
+        a0 += 4;
+        a1 += 4;
+      }
+      for (; a0 + 4 <= b0; a0 += 4) {
+        const double p0 = prod[a0], p1 = prod[a0 + 1], p2 = prod[a0 + 2], p3 = prod[a0 + 3];
+        s0 += p0;
+        s0 += p1;
+        s0 += p2;
+        s0 += p3;
+      }
+      for (; a0 < b0; ++a0) s0 += prod[a0];
+      for (; a1 + 4 <= b1; a1 += 4) {
+        const double q0 = prod[a1], q1 = prod[a1 + 1], q2 = prod[a1 + 2], q3 = prod[a1 + 3];
+        s1 += q0;
+        s1 += q1;
+        s1 += q2;
+        s1 += q3;
+      }
+      for (; a1 < b1; ++a1) s1 += prod[a1];
+      sq += epi_store<OP>(r0 + t0, s0, pre[0], ep);
+      if (t1 < nr) sq += epi_store<OP>(r0 + t1, s1, pre[1], ep);
+    }
+  } else if constexpr (!LR) {
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int t = tid + q * kSrtThreads;
