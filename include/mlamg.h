@@ -258,6 +258,19 @@ int mlamg_gnn_topk(const float* scores, int64_t n, int64_t k, float* vec, int32_
 int mlamg_bellman_ford(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* dist_f32,
                        int32_t* cluster, int32_t* iters_host, void* stream);
 
+/* pyamg 4.x graph.bellman_ford(G, seeds) exactly (the aggregation step of FullAggNet.forward,
+ * ns/model/agg_interp.py:475; replaces that call): sequential in-place pull sweeps
+ * x_i <- min(x_i, G_ij + x_j) over rows 0..n-1 in stored order, strict <, nearest seed from the
+ * first strictly better neighbour, repeated until a sweep changes no distance; run
+ * level-scheduled in one workgroup, so distances AND nearest seeds (ties included) are bitwise
+ * pyamg's. Arithmetic in the graph's dtype: fp64 = 0 -> float32 (G's values must be exactly
+ * representable, e.g. widened CNet weights; dist is float*), 1 -> float64 (dist is double*).
+ * dist[n] (unreached: the dtype's max), nearest[n] (seed node id, -1 unreached), *sweeps_host =
+ * pyamg's sweep count (the last one changes nothing). EINVAL if no fixed point after n + 2
+ * sweeps (a negative cycle: pyamg would not return). Syncs. */
+int mlamg_bellman_ford_pyamg(const mlamg_csr* G, const int32_t* seeds, int32_t k, int fp64,
+                             void* dist, int32_t* nearest, int32_t* sweeps_host, void* stream);
+
 /* Agg (n x k, values 1.0) from a per-node column assignment col[n] (-1 = no aggregate):
  * graph.py:56-86 nearest_center_to_agg and graph.py:234-238 AggOp. */
 int mlamg_aggregate_op(const int32_t* col, int64_t n, int64_t k, mlamg_csr** out, void* stream);

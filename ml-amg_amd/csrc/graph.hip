@@ -234,6 +234,77 @@ __global__ void k_mark_seeds(const int32_t* __restrict__ s, int32_t k, int32_t* 
   if (t < k) f[s[t]] = 1;
 }
 
+// ---------------------------------------------------------------- pyamg 4.x bellman_ford (exact)
+// pyamg.graph.bellman_ford (the aggregation step of FullAggNet.forward, ns/model/agg_interp.py
+// :475): amg_core sweeps rows 0..n-1 in place, x_i <- min(x_i, fl(G_ij + x_j)) in the graph's
+// dtype with a strict <, nearest seed taken from the first strictly better neighbour, until a
+// sweep changes no distance. Labels then depend on the sweep order, so this is the sequential
+// sweep itself, run level-scheduled in one workgroup: level(i) = 1 + max level(j) over j < i
+// coupled to i in either direction (the Gauss-Seidel schedule of gs.hip). A level's rows see the
+// final values of every earlier-coupled row and the old values of every later-coupled one, and
+// rows of a level touch no common entry: every (x, z) is bit for bit the sequential sweep's.
+constexpr int kBfBlock = 1024;
+
+template <typename T>
+__global__ void k_bfp_init(T* __restrict__ x, int32_t* __restrict__ z, int64_t n, T big) {
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  x[i] = big;
+  z[i] = -1;
+}
+template <typename T>
+__global__ void k_bfp_seeds(const int32_t* __restrict__ s, int32_t k, T* __restrict__ x,
+                            int32_t* __restrict__ z) {
+  int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= k) return;
+  x[s[t]] = T(0);
+  z[s[t]] = s[t];
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBfBlock) void k_bf_pyamg(const int32_t* __restrict__ ip,
+                                                       const int32_t* __restrict__ ij,
+                                                       const double* __restrict__ ax,
+                                                       const int32_t* __restrict__ rows,
+                                                       const int32_t* __restrict__ lptr,
+                                                       int32_t n_levels, int32_t max_sweeps, T* x,
+                                                       int32_t* z, int32_t* __restrict__ out) {
+  __shared__ int32_t changed;
+  int32_t sweeps = 0, c = 0;
+  do {
+    if (threadIdx.x == 0) changed = 0;
+    __syncthreads();
+    for (int32_t l = 0; l < n_levels; ++l) {
+      const int32_t a = lptr[l], e = lptr[l + 1];
+      for (int32_t t = a + (int32_t)threadIdx.x; t < e; t += kBfBlock) {
+        const int32_t i = rows[t];
+        const T x0 = x[i];
+        T xi = x0;
+        int32_t zi = z[i];
+        for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
+          const int32_t j = ij[k];
+          const T d = (T)ax[k] + x[j];  // the row's own entry reads the old x_i, as amg_core
+          if (d < xi) {
+            xi = d;
+            zi = z[j];
+          }
+        }
+        if (xi != x0) changed = 1;  // pyamg: (old_distances == distances).all()
+        x[i] = xi;
+        z[i] = zi;
+      }
+      __syncthreads();
+    }
+    ++sweeps;
+    c = changed;
+    __syncthreads();  // every thread has read the flag before it is reset
+  } while (c && sweeps < max_sweeps);
+  if (threadIdx.x == 0) {
+    out[0] = sweeps;
+    out[1] = c;
+  }
+}
+
 static inline dim3 g1(int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n + 255) / 256)); }
 
 static int read_flag(int32_t* dflag, hipStream_t s, int32_t* out) {
@@ -294,6 +365,77 @@ int mlamg_bellman_ford(const mlamg_csr* G, const int32_t* seeds, int32_t k, floa
   if (n) hipLaunchKernelGGL(k_lab_finish, g1(n), dim3(256), 0, s, cluster, n);
   MLAMG_HIP(hipStreamSynchronize(s));
   if (iters_host) *iters_host = sweeps;
+  return MLAMG_OK;
+}
+
+int mlamg_bellman_ford_pyamg(const mlamg_csr* G, const int32_t* seeds, int32_t k, int fp64,
+                             void* dist, int32_t* nearest, int32_t* sweeps_host, void* stream) {
+  MLAMG_REQUIRE(G && dist && nearest && (k == 0 || seeds), "NULL argument");
+  MLAMG_REQUIRE(G->n_rows == G->n_cols, "graph must be square");
+  MLAMG_REQUIRE(fp64 == 0 || fp64 == 1, "fp64 must be 0 (float32 graph) or 1 (float64 graph)");
+  MLAMG_REQUIRE(k >= 0, "negative seed count");
+  hipStream_t s = S(stream);
+  const int64_t n = G->n_rows;
+  MLAMG_REQUIRE(n < INT32_MAX, "graph too large for int32 rows");
+  int64_t bad = 0;
+  MLAMG_TRY(count_out_of_range(seeds, k, 0, n, s, &bad));
+  MLAMG_REQUIRE(bad == 0, "seed index out of range [0, n)");
+  // level schedule of the sequential sweep (host, O(nnz))
+  std::vector<int32_t> ip(n + 1), ij(G->nnz);
+  MLAMG_HIP(hipMemcpyAsync(ip.data(), G->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, s));
+  if (G->nnz)
+    MLAMG_HIP(hipMemcpyAsync(ij.data(), G->indices, sizeof(int32_t) * G->nnz, hipMemcpyDeviceToHost, s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  std::vector<int32_t> level(n, 0), req(n, 0);
+  int32_t nlev = n ? 1 : 0;
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t L = req[i];
+    for (int32_t q = ip[i]; q < ip[i + 1]; ++q)
+      if (ij[q] < i) L = std::max(L, level[ij[q]] + 1);
+    level[i] = L;
+    for (int32_t q = ip[i]; q < ip[i + 1]; ++q)
+      if (ij[q] > i) req[ij[q]] = std::max(req[ij[q]], L + 1);
+    nlev = std::max(nlev, L + 1);
+  }
+  std::vector<int32_t> plan((size_t)nlev + 1 + n + 2, 0);  // lptr | rows | out
+  int32_t* lp = plan.data();
+  for (int64_t i = 0; i < n; ++i) lp[level[i] + 1]++;
+  for (int32_t l = 0; l < nlev; ++l) lp[l + 1] += lp[l];
+  std::vector<int32_t> fill(lp, lp + nlev);
+  int32_t* rows = lp + nlev + 1;
+  for (int64_t i = 0; i < n; ++i) rows[fill[level[i]]++] = (int32_t)i;
+  int32_t* dplan = nullptr;
+  MLAMG_HIP(hipMalloc(&dplan, sizeof(int32_t) * plan.size()));
+  struct Free {
+    void* a;
+    ~Free() { (void)hipFree(a); }
+  } guard{dplan};
+  MLAMG_HIP(hipMemcpyAsync(dplan, plan.data(), sizeof(int32_t) * plan.size(), hipMemcpyHostToDevice, s));
+  int32_t* dout = dplan + nlev + 1 + n;
+  // nonnegative weights converge within n + 1 sweeps; more means a negative cycle, on which
+  // pyamg would never return
+  const int32_t max_sweeps = (int32_t)std::min<int64_t>(n + 2, INT32_MAX);
+  if (fp64) {
+    double* x = static_cast<double*>(dist);
+    if (n) hipLaunchKernelGGL(k_bfp_init<double>, g1(n), dim3(256), 0, s, x, nearest, n, DBL_MAX);
+    if (k) hipLaunchKernelGGL(k_bfp_seeds<double>, g1(k), dim3(256), 0, s, seeds, k, x, nearest);
+    if (n)
+      hipLaunchKernelGGL(k_bf_pyamg<double>, dim3(1), dim3(kBfBlock), 0, s, G->indptr, G->indices,
+                         G->data, dplan + nlev + 1, dplan, nlev, max_sweeps, x, nearest, dout);
+  } else {
+    float* x = static_cast<float*>(dist);
+    if (n) hipLaunchKernelGGL(k_bfp_init<float>, g1(n), dim3(256), 0, s, x, nearest, n, FLT_MAX);
+    if (k) hipLaunchKernelGGL(k_bfp_seeds<float>, g1(k), dim3(256), 0, s, seeds, k, x, nearest);
+    if (n)
+      hipLaunchKernelGGL(k_bf_pyamg<float>, dim3(1), dim3(kBfBlock), 0, s, G->indptr, G->indices,
+                         G->data, dplan + nlev + 1, dplan, nlev, max_sweeps, x, nearest, dout);
+  }
+  MLAMG_HIP(hipGetLastError());
+  int32_t res[2] = {n ? 0 : 1, 0};
+  if (n) MLAMG_HIP(hipMemcpyAsync(res, dout, sizeof(res), hipMemcpyDeviceToHost, s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  MLAMG_REQUIRE(res[1] == 0, "bellman_ford: no fixed point after n + 2 sweeps (negative cycle)");
+  if (sweeps_host) *sweeps_host = res[0];
   return MLAMG_OK;
 }
 

@@ -319,23 +319,44 @@ class FullAggNet(nn.Module):
         return next(self.parameters()).device
 
     @torch.no_grad()
-    def forward(self, A, alpha):
+    def forward(self, A, alpha, aggregation="pyamg", x=None):
         """Returns (agg, P, bf_weights, cluster_centers, node_weights) like :442-486: agg and P
         as torch sparse COO (n x k, fp32), bf_weights as torch sparse COO (the CNet edge
-        values), cluster_centers the seed nodes (ascending), node_weights the 0/1 scores."""
-        from .graph import aggregate_op_device, bellman_ford_device, labels_to_columns
+        values C, edge (i, j) = A's entry (i, j)), cluster_centers the seed nodes (ascending),
+        node_weights the 0/1 scores.
+
+        aggregation: "pyamg" (default) is the reference's step, pyamg.graph.bellman_ford(C,
+        top_k) (:475): pull sweeps x_i <- min(x_i, C_ij + x_j) in float32, emulated exactly
+        on the device (graph.bellman_ford_pyamg_device), so every node's nearest seed is pyamg's,
+        ties included; a node no seed reaches raises KeyError like nearest_center_to_agg's dict
+        lookup (ns/lib/graph.py:83). "parallel" runs the same distances with the multi-workgroup
+        order-independent Bellman-Ford (graph.hip k_bf_sweep, on C^T so the direction is
+        pyamg's): nearest seeds equal pyamg's whenever shortest paths are unique, ties go to the
+        smallest seed id, unreached nodes get no aggregate. x: node features replacing the
+        reference graph's constant 1/n (graph_from_matrix_basic, ns/model/data.py:22-31) —
+        not in the reference's signature; a test hook for well-conditioned inputs."""
+        from .graph import (aggregate_op_device, bellman_ford_device, bellman_ford_pyamg_device,
+                            labels_to_columns)
+        if aggregation not in ("pyamg", "parallel"):
+            raise ValueError(f"aggregation must be 'pyamg' or 'parallel', got {aggregation!r}")
         A = sp.csr_matrix(A)
         m = A.shape[0]
         k = int(np.ceil(alpha * m))
         g = Graph(A, device=self.device)
+        if x is not None:
+            g.x = torch.as_tensor(x, dtype=torch.float32).reshape(m, 1).to(self.device)
         node_scores = self.AggNet.run(g, k).reshape(-1)
         top_k = torch.nonzero(node_scores == 1).reshape(-1)
-        # Bellman-Ford over the CNet edge weights from the seeds (pyamg.graph.bellman_ford,
-        # :466-473), all on the device
+        # Bellman-Ford over the CNet edge weights from the seeds (:466-475), on the device
         _, bf_edges = self.CNet.run(g)
         C = g.csr(bf_edges)
         seeds = top_k.to(torch.int32)
-        _, lab, _ = bellman_ford_device(C, seeds)
+        if aggregation == "pyamg":
+            _, lab, _ = bellman_ford_pyamg_device(C, seeds)
+            if bool((lab < 0).any()):
+                raise KeyError(-1)
+        else:
+            _, lab, _ = bellman_ford_device(C.T, seeds)
         col = labels_to_columns(lab, seeds)
         Agg = aggregate_op_device(col, k)
         # P_hat from PNet on graph_from_matrix(A, Agg), P = P_hat Agg (:476-484)

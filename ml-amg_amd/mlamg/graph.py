@@ -1,15 +1,19 @@
 """Drop-in mirror of ns/lib/graph.py (aggregation) running on the MI355X.
 
   modified_bellman_ford   ns/lib/graph.py:7-53     seeded Bellman-Ford, fp32 (torch) arithmetic
+  bellman_ford            pyamg 4.x graph.bellman_ford (ns/model/agg_interp.py:475, the
+                          aggregation step of FullAggNet.forward): sequential sweeps emulated
+                          exactly, so nearest seeds are bitwise pyamg's, ties included
   nearest_center_to_agg   ns/lib/graph.py:56-86    aggregate matrix from assignments
   lloyd_aggregation       ns/lib/graph.py:156-239  seeds + pyamg 4.x lloyd_cluster + AggOp
   num_connected_components, check_aggregates_connected   ns/lib/graph.py:89-153 (host-side
                           graph checks, kept so an alias of ns.lib.graph to this module is whole)
 
-Distances are bit-exact with the reference for any input (order-independent fixed point, see
-csrc/graph.hip). Seed labels are bit-exact whenever shortest paths are unique; on exact ties the
-device uses the order-independent rule "smallest seed id among tight predecessors" where the
-reference keeps whichever its sequential sweep found first.
+modified_bellman_ford: distances are bit-exact with the reference for any input (order-independent
+fixed point, see csrc/graph.hip). Seed labels are bit-exact whenever shortest paths are unique; on
+exact ties the device uses the order-independent rule "smallest seed id among tight predecessors"
+where the reference keeps whichever its sequential sweep found first. bellman_ford (pyamg's) is
+bit-exact in both outputs for every input: its sweeps are level-scheduled, not reordered.
 """
 from __future__ import annotations
 
@@ -47,6 +51,44 @@ def bellman_ford_device(G, seeds_dev):
     call("mlamg_bellman_ford", G.handle, ptr(seeds_dev), int(seeds_dev.numel()), ptr(dist),
          ptr(lab), ctypes.byref(sweeps), stream_ptr())
     return dist, lab, int(sweeps.value)
+
+
+def bellman_ford_pyamg_device(G, seeds_dev, fp64=False):
+    """pyamg 4.x graph.bellman_ford on a DeviceCSR (pull form: x_i <- min(x_i, G[i, j] + x_j)).
+
+    Returns (distances float32/float64 tensor (unreached: the dtype's max), nearest seed int32
+    tensor (seed node id, -1 unreached), sweeps)."""
+    n = G.shape[0]
+    dev = _device()
+    dist = torch.empty(n, dtype=torch.float64 if fp64 else torch.float32, device=dev)
+    near = torch.empty(n, dtype=torch.int32, device=dev)
+    sweeps = ctypes.c_int32()
+    call("mlamg_bellman_ford_pyamg", G.handle, ptr(seeds_dev), int(seeds_dev.numel()),
+         1 if fp64 else 0, ptr(dist), ptr(near), ctypes.byref(sweeps), stream_ptr())
+    return dist, near, int(sweeps.value)
+
+
+def bellman_ford(G, seeds, maxiter=None):
+    """Drop-in for pyamg.graph.bellman_ford (pyamg 4.x, as ns/model/agg_interp.py:475 calls it).
+
+    G: scipy sparse graph (asgraph: anything but CSR/CSC becomes csr_matrix, duplicates summed;
+    a CSC graph's arrays are walked as CSR, like amg_core does), float32 or float64 weights;
+    seeds: node ids. Returns numpy (distances in G's dtype, nearest_seed intc). maxiter only
+    validated: pyamg 4.x never advances its counter, so it sweeps to the fixed point anyway."""
+    if maxiter is not None and maxiter < 0:
+        raise ValueError('maxiter must be positive')
+    if not (sp.isspmatrix_csr(G) or sp.isspmatrix_csc(G)):
+        G = sp.csr_matrix(G)
+    if G.dtype == complex:
+        raise ValueError('Bellman-Ford algorithm only defined for real weights')
+    if G.dtype not in (np.float32, np.float64):
+        raise TypeError(f'graph weights must be float32 or float64, got {G.dtype}')
+    Gc = sp.csr_matrix((G.data.astype(np.float64), G.indices, G.indptr), shape=G.shape)
+    Gd = DeviceCSR.from_scipy(Gc, check=False)
+    seeds = np.asarray(seeds, dtype=np.intc).reshape(-1)
+    seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
+    d, z, _ = bellman_ford_pyamg_device(Gd, seeds_dev, fp64=G.dtype == np.float64)
+    return d.cpu().numpy(), z.cpu().numpy().astype(np.intc)
 
 
 def modified_bellman_ford(S_T, centers):

@@ -116,3 +116,36 @@ def aggnet(mod, g, k):
     for layer in mod.layers:
         x = topk_vec(agg_layer_raw(layer, g, x), k)
     return x
+
+
+@torch.no_grad()
+def full_forward(net, A, alpha, x=None):
+    """FullAggNet.forward (agg_interp.py:458-486) restated on a module's parameters: AggNet
+    scores and top-k seeds, CNet edge weights C (sp.coo_matrix over the graph's edges, :469-471),
+    pyamg 4.x bellman_ford(C, top_k) (restated.pyamg_bellman_ford, the oracle's C restatement),
+    nearest_center_to_agg (dict lookup: KeyError on an unreached node), PNet on
+    graph_from_matrix(A, Agg) and P = P_hat Agg. x replaces the constant 1/n node input.
+    Returns (Agg scipy CSR n x k, P scipy CSR, C scipy CSR, top_k tensor, scores tensor)."""
+    from . import restated
+    A = sp.csr_matrix(A)
+    m = A.shape[0]
+    k = int(np.ceil(alpha * m))
+    g = RefGraph(A)
+    if x is not None:
+        g.x = torch.as_tensor(np.asarray(x), dtype=torch.float32).reshape(-1)
+    scores = aggnet(net.AggNet, g, k).reshape(-1)
+    top_k = torch.where(scores == 1)[0]
+    _, bfe = mpnn(net.CNet, g)
+    ei = g.edge_index.numpy()
+    C = sp.coo_matrix((bfe.reshape(-1).numpy(), (ei[0], ei[1])), shape=(m, m))
+    _, nearest, _ = restated.pyamg_bellman_ford(C, top_k.numpy())
+    pos = {int(s): t for t, s in enumerate(top_k.tolist())}
+    col = np.array([pos[int(c)] for c in nearest], dtype=np.int64)
+    Agg = sp.csr_matrix((np.ones(m), (np.arange(m), col)), shape=(m, len(pos)))
+    gp = RefGraph(A, agg=Agg)
+    if x is not None:
+        gp.x = g.x
+    _, pe = mpnn(net.PNet, gp)
+    P_hat = sp.csr_matrix((pe.reshape(-1).numpy().astype(np.float64), A.indices, A.indptr),
+                          shape=A.shape)
+    return Agg, (P_hat @ Agg).tocsr(), C.tocsr(), top_k, scores

@@ -11,6 +11,9 @@
  *                           over coalesced COO order, strict <)
  *   canon_bellman_ford      same distances (order-independent fixed point) with the device's
  *                           order-independent label rule (min seed id over tight edges)
+ *   pyamg_bellman_ford      pyamg 4.x graph.bellman_ford (ns/model/agg_interp.py:475): amg_core
+ *                           pull sweeps over the rows in order, in place, strict <, in the
+ *                           graph's dtype (float32: the CNet weights), until no distance changes
  *   ref_lloyd_cluster       pyamg 4.x amg_core lloyd_cluster + graph.lloyd_cluster driver loop
  *                           (called at ns/lib/graph.py:232), sequential
  *   canon_lloyd_cluster     same with the device's label rule (min cluster index over tight
@@ -247,4 +250,45 @@ int lloyd_cluster(int64_t n, const int32_t* ip, const int32_t* ij, const double*
   free(last);
   free(is_seed);
   return it;
+}
+
+/* pyamg 4.x pyamg.graph.bellman_ford(G, seeds) with its amg_core.bellman_ford kernel, for a
+ * float32 G (ns/model/agg_interp.py:469-475 builds G from the CNet's float32 edge weights, so
+ * amg_core runs its <int, float> instantiation: every sum rounds to float). distances start at
+ * FLT_MAX (max_value(float32)), 0 at the seeds; nearest_seed starts at -1, seeds[s] at seeds;
+ * each sweep visits rows 0..n-1 in order and, in place, takes the first strictly smaller
+ * w_ij + d_j over the row's stored entries (and the nearest seed of that j); sweeps repeat
+ * until a sweep leaves every distance unchanged. Returns the number of sweeps (>= 1). */
+int pyamg_bellman_ford(int64_t n, const int32_t* ip, const int32_t* ij, const float* w,
+                       const int32_t* seeds, int64_t k, float* dist, int32_t* nearest) {
+  for (int64_t i = 0; i < n; ++i) {
+    dist[i] = FLT_MAX;
+    nearest[i] = -1;
+  }
+  for (int64_t s = 0; s < k; ++s) {
+    dist[seeds[s]] = 0.0f;
+    nearest[seeds[s]] = seeds[s];
+  }
+  int sweeps = 0;
+  int changed = 1;
+  while (changed) {
+    changed = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      float xi = dist[i];
+      int32_t zi = nearest[i];
+      for (int32_t jj = ip[i]; jj < ip[i + 1]; ++jj) {
+        const int32_t j = ij[jj];
+        const float d = w[jj] + dist[j];
+        if (d < xi) {
+          xi = d;
+          zi = nearest[j];
+        }
+      }
+      if (xi != dist[i]) changed = 1;
+      dist[i] = xi;
+      nearest[i] = zi;
+    }
+    ++sweeps;
+  }
+  return sweeps;
 }

@@ -34,6 +34,8 @@ def lib():
         L.ref_bellman_ford_torch.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
         L.ref_bellman_ford_torch.restype = ctypes.c_int
         L.canon_bellman_ford.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
+        L.pyamg_bellman_ford.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
+        L.pyamg_bellman_ford.restype = ctypes.c_int
         L.vec_matvec.argtypes = [i64, vp, vp, vp, vp, vp]
         L.lloyd_cluster.argtypes = [i64, vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int, vp, vp,
                                     ctypes.c_int]
@@ -244,6 +246,24 @@ def canon_bellman_ford(C, seeds):
     lab = np.empty(n, dtype=np.int32)
     lib().canon_bellman_ford(n, _p(ip), _p(ij), _p(w), _p(s), len(s), _p(d), _p(lab))
     return d, lab
+
+
+def pyamg_bellman_ford(G, seeds):
+    """pyamg 4.x graph.bellman_ford(G, seeds) as ns/model/agg_interp.py:471-475 calls it: G a
+    scipy COO/CSR of float32 weights (asgraph -> csr_matrix: duplicates summed, rows sorted),
+    amg_core sweeps in float32. Returns (distances float32, nearest_seed int32 seed node id or
+    -1, sweeps)."""
+    G = sp.csr_matrix(G)
+    G.sum_duplicates()
+    ip = np.ascontiguousarray(G.indptr, dtype=np.int32)
+    ij = np.ascontiguousarray(G.indices, dtype=np.int32)
+    w = np.ascontiguousarray(G.data, dtype=np.float32)
+    s = np.ascontiguousarray(seeds, dtype=np.int32)
+    n = G.shape[0]
+    d = np.empty(n, dtype=np.float32)
+    z = np.empty(n, dtype=np.int32)
+    sweeps = lib().pyamg_bellman_ford(n, _p(ip), _p(ij), _p(w), _p(s), len(s), _p(d), _p(z))
+    return d, z, sweeps
 
 
 def nearest_center_to_agg(top_k, nearest_center):

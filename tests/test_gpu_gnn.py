@@ -113,26 +113,38 @@ def test_aggnet_scores_and_topk(torch_cuda):
     assert idx.cpu().tolist() == [1, 2, 4] and v.cpu().tolist() == [0, 1, 1, 0, 1, 0]
 
 
-def test_fullaggnet_forward(torch_cuda, oracle):
-    """FullAggNet.forward on the device: k seeds, every reachable node in one aggregate, and P =
-    PNet(graph_from_matrix(A, Agg)) Agg against the oracle's PNet on the device's aggregates."""
+def _to_csr(T, shape):
+    return sp.csr_matrix((T.values().cpu().numpy(), T.indices().cpu().numpy()), shape=shape)
+
+
+@pytest.mark.parametrize("aggregation", ("pyamg", "parallel"))
+def test_fullaggnet_forward(torch_cuda, oracle, aggregation):
+    """FullAggNet.forward on the device: k seeds, every node in one aggregate, the aggregates
+    those of the aggregation rule on the device's own CNet weights C — "pyamg": pyamg 4.x
+    bellman_ford(C, top_k) (oracle restatement, pull sweeps, strict <; bitwise, ties included:
+    the ReLU-ended CNet leaves many exact-zero weights); "parallel": the order-independent
+    rule on the same pull direction (oracle.canon_bellman_ford pushes, so on C^T) — and P =
+    PNet(graph_from_matrix(A, Agg)) Agg against the oracle's product on the device's P_hat."""
     torch = torch_cuda
     from mlamg import gnn
-    from oracle import gnn_ref
     torch.manual_seed(2)
     net = gnn.FullAggNet(dim=64, num_conv=2, iterations=2).cuda()
     A = _A(14)
     n = A.shape[0]
-    agg, P, C, top_k, scores = net.forward(A, 0.1)
+    agg, P, C, top_k, scores = net.forward(A, 0.1, aggregation=aggregation)
     k = int(np.ceil(0.1 * n))
     assert agg.shape == (n, k) and P.shape == (n, k) and len(top_k) == k
     assert torch.equal(torch.nonzero(scores == 1).reshape(-1), top_k)
-    Agg = sp.csr_matrix((agg.values().cpu().numpy(), agg.indices().cpu().numpy()), shape=(n, k))
+    Agg = _to_csr(agg, (n, k))
     assert np.all(np.diff(Agg.indptr) <= 1)
-    # the aggregates are the device Bellman-Ford's over the CNet weights from the seeds
-    Cs = sp.csr_matrix((C.values().cpu().numpy(), C.indices().cpu().numpy()), shape=(n, n))
-    _, lab = oracle.canon_bellman_ford(Cs.astype(np.float64), top_k.cpu().numpy())
-    pos = {int(s): t for t, s in enumerate(top_k.cpu().numpy())}
+    Cs = _to_csr(C, (n, n))
+    seeds = top_k.cpu().numpy()
+    if aggregation == "pyamg":
+        _, lab, _ = oracle.pyamg_bellman_ford(Cs.astype(np.float32), seeds)
+        assert np.all(lab >= 0) and np.all(np.diff(Agg.indptr) == 1)
+    else:
+        _, lab = oracle.canon_bellman_ford(Cs.T.tocsr().astype(np.float64), seeds)
+    pos = {int(s): t for t, s in enumerate(seeds)}
     col = np.array([pos.get(int(l), -1) if l >= 0 else -1 for l in lab])
     rows = np.nonzero(col >= 0)[0]
     Agg_ref = sp.csr_matrix((np.ones(len(rows)), (rows, col[rows])), shape=(n, k))
@@ -142,6 +154,122 @@ def test_fullaggnet_forward(torch_cuda, oracle):
     P_hat = sp.csr_matrix((pe.reshape(-1).double().cpu().numpy(), A.indices, A.indptr),
                           shape=A.shape)
     P_ref = (P_hat @ Agg).toarray().astype(np.float32)
-    Pd = sp.csr_matrix((P.values().cpu().numpy(), P.indices().cpu().numpy()),
-                       shape=(n, k)).toarray()
+    Pd = _to_csr(P, (n, k)).toarray()
     assert np.abs(Pd - P_ref).max() <= 1e-6 * max(np.abs(P_ref).max(), 1e-30)
+
+
+def test_fullaggnet_forward_end_to_end(torch_cuda):
+    """The whole FullAggNet.forward (agg_interp.py:458-486) on the device against
+    oracle/gnn_ref.full_forward — the torch restatement of every layer plus the oracle's
+    pyamg.graph.bellman_ford — at the same seeded weights, on a well-conditioned non-constant
+    node input (x ~ U(0.5, 1.5): InstanceNorm of the reference's constant 1/n input turns fp32
+    rounding into O(1) differences). ~70% of the CNet weights are exact ReLU zeros, so pyamg's
+    sweep order decides many nearest seeds. Preconditions checked on the oracle side: every AggNet
+    layer separates its k-th and (k+1)-th score. Then the seeds and the aggregates are equal,
+    C and P agree to rtol 1e-4 of their scale (fp32, different summation orders)."""
+    torch = torch_cuda
+    from mlamg import gnn
+    from oracle import gnn_ref
+    torch.manual_seed(0)
+    net = gnn.FullAggNet(dim=32, num_conv=2, iterations=2)
+    for mod in net.modules():  # positive biases: a live network (default init leaves the
+        if isinstance(mod, torch.nn.Linear) and mod.bias is not None:  # ReLU stacks dead)
+            mod.bias.data.uniform_(0.05, 0.3)
+    netd = gnn.FullAggNet(dim=32, num_conv=2, iterations=2)
+    netd.load_state_dict(net.state_dict())
+    netd = netd.cuda()
+    A = _A(16)
+    n = A.shape[0]
+    alpha = 0.1
+    k = int(np.ceil(alpha * n))
+    x = np.random.RandomState(3).uniform(0.5, 1.5, n).astype(np.float32)
+    g = gnn_ref.RefGraph(A)
+    g.x = torch.as_tensor(x)
+    xx = g.x
+    for layer in net.AggNet.layers:
+        raw = gnn_ref.agg_layer_raw(layer, g, xx).reshape(-1)
+        srt = torch.sort(raw, descending=True).values
+        assert float(srt[k - 1] - srt[k]) > 1e-4 * float(srt.abs().max()), "ill-conditioned seed"
+        xx = gnn_ref.topk_vec(raw, k)
+    Agg_r, P_r, C_r, top_r, s_r = gnn_ref.full_forward(net, A, alpha, x=x)
+    agg, P, C, top_k, scores = netd.forward(A, alpha, x=x)
+    assert torch.equal(top_k.cpu(), top_r) and torch.equal(scores.cpu(), s_r)
+    Cd = _to_csr(C, (n, n))
+    assert np.array_equal(Cd.indptr, C_r.indptr) and np.array_equal(Cd.indices, C_r.indices)
+    assert np.abs(Cd.data - C_r.data).max() <= 1e-4 * np.abs(C_r.data).max()
+    Agg = _to_csr(agg, (n, k))
+    assert (abs(Agg - Agg_r) > 0).nnz == 0
+    Pd = _to_csr(P, (n, k)).toarray()
+    Pr = P_r.toarray()
+    assert np.abs(Pd - Pr).max() <= 1e-4 * np.abs(Pr).max()
+
+
+def test_bellman_ford_pyamg_device(torch_cuda, oracle):
+    """graph.bellman_ford (the drop-in for pyamg.graph.bellman_ford) against the oracle
+    restatement, bitwise in distances and nearest seeds: random and all-equal (tie-rich)
+    float32 weights, a float64 graph, duplicates in a COO input (summed by asgraph), a
+    disconnected graph (unreached: FLT_MAX / -1), no seeds, a non-symmetric pattern, and
+    a larger 3-D grid whose level schedule is deep."""
+    from mlamg import graph, problems
+    rs = np.random.RandomState(11)
+
+    def check(G, seeds, dtype=np.float32):
+        d, z = graph.bellman_ford(G, seeds)
+        if dtype == np.float32:
+            dr, zr, _ = oracle.pyamg_bellman_ford(G, seeds)
+        else:
+            dr, zr = _pyamg_bf_f64(G, seeds)
+        assert d.dtype == dtype and np.array_equal(d, dr) and np.array_equal(z, zr)
+        return d, z
+
+    A = problems.poisson_2d_5pt(23).tocoo()
+    for w in (rs.uniform(0.1, 2.0, A.nnz), np.ones(A.nnz)):
+        G = sp.coo_matrix((w.astype(np.float32), (A.row, A.col)), shape=A.shape)
+        check(G, np.sort(rs.permutation(A.shape[0])[:40]))
+    # float64 graph
+    G = sp.csr_matrix((rs.uniform(0.1, 2.0, A.nnz), (A.row, A.col)), shape=A.shape)
+    check(G, [0, 100, 300], np.float64)
+    # duplicates summed
+    r = np.concatenate([A.row, A.row[:50]])
+    c = np.concatenate([A.col, A.col[:50]])
+    G = sp.coo_matrix((rs.uniform(0, 1, len(r)).astype(np.float32), (r, c)), shape=A.shape)
+    check(G, [5, 77])
+    # disconnected + no seeds + non-symmetric
+    keep = (A.row < 200) == (A.col < 200)
+    G = sp.coo_matrix((np.ones(keep.sum(), np.float32), (A.row[keep], A.col[keep])), shape=A.shape)
+    d, z = check(G, [3])
+    assert np.all(z[200:] == -1) and np.all(d[200:] == np.finfo(np.float32).max)
+    d, z = check(G, np.array([], dtype=np.int32))
+    assert np.all(z == -1)
+    up = A.col >= A.row
+    G = sp.coo_matrix((rs.uniform(0, 1, up.sum()).astype(np.float32), (A.row[up], A.col[up])),
+                      shape=A.shape)
+    check(G, [400, 17])
+    B = problems.poisson_3d_7pt(18).tocoo()
+    G = sp.coo_matrix((rs.randint(0, 3, B.nnz).astype(np.float32), (B.row, B.col)), shape=B.shape)
+    check(G, np.sort(rs.permutation(B.shape[0])[:60]))
+
+
+def _pyamg_bf_f64(G, seeds):
+    """pyamg 4.x bellman_ford in float64 (small graphs): the same sweeps as the oracle's float32
+    restatement, in the graph's dtype."""
+    G = sp.csr_matrix(G)
+    G.sum_duplicates()
+    n = G.shape[0]
+    x = np.full(n, np.finfo(np.float64).max)
+    z = np.full(n, -1, dtype=np.int32)
+    x[seeds] = 0
+    z[seeds] = seeds
+    ip, ij, w = G.indptr, G.indices, G.data
+    while True:
+        changed = False
+        for i in range(n):
+            xi, zi = x[i], z[i]
+            for q in range(ip[i], ip[i + 1]):
+                d = w[q] + x[ij[q]]
+                if d < xi:
+                    xi, zi = d, z[ij[q]]
+            changed |= xi != x[i]
+            x[i], z[i] = xi, zi
+        if not changed:
+            return x, z

@@ -149,3 +149,65 @@ def test_amg_2_v_singular_driver(golden_singular, oracle, key):
     assert np.array_equal(err, g[f"{key}_err"])
     assert conv == g[f"{key}_conv"]
     assert np.array_equal(x, g[f"{key}_x"])
+
+
+def _pyamg_bf_literal(G, seeds):
+    """pyamg 4.x graph.bellman_ford + amg_core.bellman_ford, transcribed line by line (numpy
+    float32 scalars: every sum rounds to float32 like the <int, float> instantiation)."""
+    import scipy.sparse as sp
+    G = sp.csr_matrix(G)
+    G.sum_duplicates()
+    n = G.shape[0]
+    x = np.full(n, np.finfo(np.float32).max, dtype=np.float32)
+    x[seeds] = 0
+    z = np.full(n, -1, dtype=np.int32)
+    z[seeds] = seeds
+    w = G.data.astype(np.float32)
+    sweeps = 0
+    while True:
+        old = x.copy()
+        for i in range(n):
+            xi, zi = x[i], z[i]
+            for jj in range(G.indptr[i], G.indptr[i + 1]):
+                j = G.indices[jj]
+                d = np.float32(w[jj] + x[j])
+                if d < xi:
+                    xi, zi = d, z[j]
+            x[i], z[i] = xi, zi
+        sweeps += 1
+        if (old == x).all():
+            return x, z, sweeps
+
+
+@pytest.mark.parametrize("kind", ("random", "unit_ties", "disconnected"))
+def test_oracle_pyamg_bellman_ford(oracle, kind):
+    """oracle.pyamg_bellman_ford (the restatement of the aggregation step FullAggNet runs,
+    ns/model/agg_interp.py:475) against a literal transcription of pyamg 4.x: distances, nearest
+    seeds (first strictly better in sweep order — ties included) and the sweep count; its
+    distances are the order-independent fixed point the device's own Bellman-Ford computes."""
+    import scipy.sparse as sp
+    from mlamg import problems
+    rs = np.random.RandomState(7)
+    A = problems.poisson_2d_5pt(11).tocoo()
+    if kind == "random":
+        w = rs.uniform(0.1, 2.0, A.nnz).astype(np.float32)
+    elif kind == "unit_ties":
+        w = np.ones(A.nnz, dtype=np.float32)
+    else:
+        w = rs.uniform(0.1, 2.0, A.nnz).astype(np.float32)
+        cut = (A.row < 60) != (A.col < 60)  # two components
+        w = w[~cut]
+        A = sp.coo_matrix((np.ones(len(w)), (A.row[~cut], A.col[~cut])), shape=A.shape)
+    G = sp.coo_matrix((w, (A.row, A.col)), shape=A.shape)
+    seeds = np.sort(rs.permutation(A.shape[0])[:12]).astype(np.int32)
+    if kind == "disconnected":
+        seeds = seeds[seeds < 60]
+    d, z, sw = oracle.pyamg_bellman_ford(G, seeds)
+    dl, zl, swl = _pyamg_bf_literal(G, seeds)
+    assert np.array_equal(d, dl) and np.array_equal(z, zl) and sw == swl
+    # canon_bellman_ford pushes along C[i, j] (i -> j); pyamg pulls d_i = min_j G[i, j] + d_j
+    dc, _ = oracle.canon_bellman_ford(sp.csr_matrix(G).T.tocsr().astype(np.float64), seeds)
+    reach = z >= 0
+    assert np.array_equal(d[reach], dc[reach])
+    if kind == "disconnected":
+        assert not reach.all() and np.all(d[~reach] == np.finfo(np.float32).max)
