@@ -80,8 +80,28 @@ def _compile(src, hdr_digest, verbose):
     return obj, True
 
 
+def build_hostext(verbose: bool = False) -> str:
+    """mlamg/_hostptr: the CPython helper of the batched amg_2_v entry (csrc/hostptr.c)."""
+    import sysconfig
+    src = os.path.join(CSRC, "hostptr.c")
+    out = os.path.join(HERE, "mlamg", "_hostptr" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+        return out
+    cc = os.environ.get("CC", shutil.which("gcc") or "cc")
+    cmd = [cc, "-O2", "-shared", "-fPIC", "-Wall", f"-I{sysconfig.get_paths()['include']}", src,
+           "-o", out + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"building _hostptr failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build(verbose: bool = False, jobs: int | None = None) -> str:
     os.makedirs(BUILD, exist_ok=True)
+    build_hostext(verbose)
     dig = _headers_digest()
     srcs = _sources()
     jobs = jobs or min(8, len(srcs))

@@ -89,6 +89,15 @@ struct BDesc {
   int64_t x_out, err_out, stat_out;
   int64_t rcg, eg, yg;  // phased: r_H, e_H and L^-1 r_H in the arena
   int64_t done_ctr;     // phased: problems finished (one counter for the launch)
+  // the problem's values as the caller stores them (A.data, P.data) and its shape's gather maps
+  // (shared by every problem with the same sparsity): the packed value arrays above are
+  // gathered from them on the device (gather_values), so only the caller's values travel
+  int64_t a_raw, p_raw;
+  int64_t a_map, p_map, t_map, g_map, d_map, pk_row0;
+  // banded coarse solve (band_ld = half-bandwidth + 1, 0: dense): the factor in the band
+  // solve's lane layouts F (forward) and G (backward), reciprocal diagonal
+  int32_t band_ld, pad0;
+  int64_t lc, lr, rinv;
 };
 
 template <class T>
@@ -493,6 +502,297 @@ __device__ bool chol_inverse(double* __restrict__ M, int nc, double* lds, int ti
   return true;
 }
 
+// The packed value arrays of one problem from its raw CSR values and its shape's maps (index
+// into A.data / P.data, -1 = pad -> 0.0): exactly the values the host packing used to store.
+// Four independent map loads per thread before their gathers. The sweep's diagonal and row
+// order are value dependent: a zero diagonal under the one-wave sweep writes the sink slot.
+__device__ void gather_values(const BDesc& D, char* arena, int tid) {
+  const double* __restrict__ av = at<double>(arena, D.a_raw);
+  const double* __restrict__ pv = at<double>(arena, D.p_raw);
+  auto gather = [&](int64_t map_off, int64_t out_off, int64_t cnt, const double* __restrict__ src) {
+    const int32_t* __restrict__ m = at<int32_t>(arena, map_off);
+    double* __restrict__ o = at<double>(arena, out_off);
+    #pragma unroll 1
+    for (int64_t q0 = tid; q0 < cnt; q0 += 4 * kBT) {
+      int32_t k[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) k[u] = q0 + u * kBT < cnt ? m[q0 + u * kBT] : -1;
+      double v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = k[u] >= 0 ? src[k[u]] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (q0 + u * kBT < cnt) o[q0 + u * kBT] = v[u];
+    }
+  };
+  gather(D.a_map, D.ak_val, (int64_t)D.KA * D.n, av);
+  gather(D.p_map, D.pp_val, (int64_t)D.KP * D.n, pv);
+  gather(D.t_map, D.pt_val, (int64_t)D.KT * D.nc, pv);
+  if (D.smoother == 0) {
+    gather(D.g_map, D.pk_val, (int64_t)D.K * D.n, av);
+    const int32_t* __restrict__ dm = at<int32_t>(arena, D.d_map);
+    const int32_t* __restrict__ r0 = at<int32_t>(arena, D.pk_row0);
+    const double* __restrict__ b = at<double>(arena, D.b);
+    double* __restrict__ pkd = at<double>(arena, D.pk_diag);
+    double* __restrict__ bl = at<double>(arena, D.b_lvl);
+    int32_t* __restrict__ pkr = at<int32_t>(arena, D.pk_row);
+    #pragma unroll 1
+    for (int p = tid; p < D.n; p += kBT) {
+      const int32_t k = dm[p], r = r0[p];
+      double d = k >= 0 ? av[k] : 0.0;  // the last stored diagonal entry, as the sweep takes it
+      bl[p] = b[r];
+      int32_t row = r;
+      if (D.gs_rw && d == 0.0) {  // pyamg leaves x_i alone: write the sink slot
+        d = 1.0;
+        row = D.n + 1;
+      }
+      pkd[p] = d;
+      pkr[p] = row;
+    }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- banded coarse operators
+// The coarse operators of the reference's grids are narrow-banded: aggregates numbered along
+// the grid couple only to neighbours, so A_H = P^T A P has half-bandwidth b = (aggregates per
+// grid row) + 1 (23 at 64^2 with 3 x 3 boxes, 44 at 128^2). For b < 64 the coarse solve is a
+// banded Cholesky factor A_H = L L^T (n_c b^2 / 2 multiply-adds instead of the dense inverse's
+// n_c^3 / 3 + ...) and two band substitutions per cycle (4 n_c b bytes instead of 8 n_c^2).
+// Held, like the dense paths, to fp64 rounding of a direct solve; chosen per problem from its own
+// pattern, so a problem's results do not depend on its batch.
+constexpr int kBandMax = 63;  // half-bandwidth limit: rows (j, j + b] within the 64 lanes
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)x, l);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// pointers in a given address space (1 global, 3 LDS): loads through them are global / LDS
+// instructions, not flat ones, so the compiler counts them on their own counters and a
+// prefetch stays in flight (a flat load in a non-inlined function waits on every counter)
+template <int AS>
+using as_ptr = __attribute__((address_space(AS))) double*;
+template <int AS>
+using as_cptr = const __attribute__((address_space(AS))) double*;
+
+// Right-looking banded Cholesky of AH (dense n_c x n_c, only |i - k| <= b read) over a sliding
+// window of the b + 1 active rows in LDS (row i in slot i mod (b + 1), its entries k in
+// [i - b, i) in column slots k mod (b + 1); diagonals in their own ring, slot i mod (b + 2)).
+// Column j: l_i = a_ij / l_jj for i in (j, j + b], a_ik -= l_i l_k for j < k <= i <= j + b,
+// and row j + b + 1 enters the slots row j leaves: one barrier per column (the entering row and
+// every update touch slots column j does not read). The entering rows are loaded from AH two
+// columns ahead. Out, in the band solve's lane layout (step j's 64 lane values contiguous, steps
+// padded by kBandPad zero steps on either side, see band_solve): F[j][i mod 64] = L[i][j] / L[j][j]
+// for i in (j, j + b], G[i][j mod 64] = L[i][j], RI[j] = 1 / L[j][j]. Returns false
+// (uniformly) on a non-positive pivot.
+constexpr int kBandPad = 32;  // zero steps before and after the band solve's lane layout
+__device__ __forceinline__ int64_t band_at(int j, int l) { return (int64_t)(j + kBandPad) * 64 + l; }
+
+__device__ bool band_chol(const double* __restrict__ AH_, int nc, int b, double* lds,
+                          double* __restrict__ F_, double* __restrict__ G_,
+                          double* __restrict__ RI_, int tid) {
+  const as_cptr<1> AH = (as_cptr<1>)AH_;
+  const as_ptr<1> F = (as_ptr<1>)F_, G = (as_ptr<1>)G_, RI = (as_ptr<1>)RI_;
+  const int w = b + 1, wd = b + 2;
+  // zeros outside the band, and on the padding steps
+  for (int64_t q = tid; q < (int64_t)(nc + 2 * kBandPad) * 64; q += kBT) {
+    F[q] = 0.0;
+    G[q] = 0.0;
+  }
+  for (int q = tid; q < nc + 2 * kBandPad; q += kBT) RI[q] = 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  const as_ptr<3> off = (as_ptr<3>)lds;  // w x w
+  const as_ptr<3> dg = off + w * w;      // wd
+  for (int q = tid; q < w * w; q += kBT) {
+    const int i = q / w, k = q - (q / w) * w;
+    if (i < nc && k < i) off[(i % w) * w + k % w] = AH[(int64_t)i * nc + k];
+  }
+  for (int i = tid; i < w && i < nc; i += kBT) dg[i % wd] = AH[(int64_t)i * nc + i];
+  // this thread's pairs (di, dk), 1 <= dk <= di <= b (rows j + di, j + dk): b <= 63 gives at
+  // most 2016 pairs, two per thread
+  int pdi[2] = {0, 0}, pdk[2] = {0, 0};
+  const int npairs = b * (b + 1) / 2;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int p = tid + m * kBT;
+    if (p < npairs) {
+      int di = (int)((1.0 + sqrt(1.0 + 8.0 * (double)p)) * 0.5);
+      while (di * (di - 1) / 2 > p) --di;
+      while (di * (di + 1) / 2 <= p) ++di;
+      pdi[m] = di;
+      pdk[m] = p - di * (di - 1) / 2 + 1;
+    }
+  }
+  // entering-row entries of this thread (kk = tid <= b): row j + b + 1, column j + 1 + kk
+  auto enter_val = [&](int j) -> double {
+    const int ni = j + b + 1, k = j + 1 + tid;
+    return tid <= b && ni < nc ? AH[(int64_t)ni * nc + (k < ni ? k : ni)] : 0.0;
+  };
+  double pre0 = enter_val(0), pre1 = enter_val(1);
+  __syncthreads();
+  for (int j = 0; j < nc; ++j) {
+    const double d = dg[j % wd];
+    if (!(d > 0.0)) return false;  // every thread read the same pivot
+    const double ljj = sqrt(d), r = 1.0 / ljj;
+    const int cj = j % w;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int di = pdi[m], dk = pdk[m];
+      const int i = j + di, k = j + dk;
+      if (di == 0 || i >= nc) continue;
+      const double li = off[(i % w) * w + cj] * r;
+      if (dk == di) {
+        dg[i % wd] = dg[i % wd] - li * li;
+        F[band_at(j, i & 63)] = li * r;
+        G[band_at(i, j & 63)] = li;
+      } else {
+        const double lk = off[(k % w) * w + cj] * r;
+        off[(i % w) * w + k % w] = off[(i % w) * w + k % w] - li * lk;
+      }
+    }
+    if (tid == 0) RI[j + kBandPad] = r;
+    // the entering row (raw A_H: no column <= j has reached it), loaded two columns ago
+    const int ni = j + b + 1;
+    const double v = (j & 1) ? pre1 : pre0;
+    if (ni < nc && tid <= b) {
+      const int k = j + 1 + tid;
+      if (k < ni) off[(ni % w) * w + k % w] = v;
+      else dg[ni % wd] = v;
+    }
+    if (j & 1) pre1 = enter_val(j + 2);
+    else pre0 = enter_val(j + 2);
+    __syncthreads();
+  }
+  return true;
+}
+
+// e = A_H^-1 r by L y = r, L^T e = y on ONE wave (the caller's wave 0): right-looking
+// substitution over a window of 64 rows, row i on lane i mod 64. Step j: every lane reads the
+// owner lane's partial sum s_j (readlane) and each window row i in (j, j + b] takes
+// s_i -= (L_ij / l_jj) s_j, the band factor's value for (step j, this lane) read straight from
+// the lane layout (zeros outside the band and on the padding steps: no index arithmetic, no
+// conditions), so a step is readlane -> fused multiply-add. Row j's lane then holds row j + 64:
+// after the step (any b < 64), or, when b <= 64 - D (LATE), for the D owners of a block at its
+// end (row j + 64 takes its first update D or more steps later; an owner's sum is final from
+// its step on). A block's values (D steps) are loaded one block ahead, so they stay in flight
+// while the previous block computes; the owners store y_j = s_j / l_jj at the block's end.
+// Backward the same over rows descending with G (L's rows) scaled by 1 / l_jj at load. r, y, e
+// live in address spaces RS, YS, ES (1 global, 3 LDS). (Not inlined: its own registers; the
+// cycle kernel saves its registers around the call once per coarse solve instead of spilling
+// in its sweeps.)
+template <int RS, int YS, int ES, bool LATE>
+__device__ __noinline__ void band_solve(const double* __restrict__ F_,
+                                        const double* __restrict__ G_,
+                                        const double* __restrict__ RI_, int nc,
+                                        const double* r_, double* y_, double* e_, int lane) {
+  constexpr int D = 8;
+  const as_cptr<1> F = (as_cptr<1>)F_, G = (as_cptr<1>)G_, RI = (as_cptr<1>)RI_;
+  const as_cptr<RS> r = (as_cptr<RS>)r_;
+  const as_ptr<YS> y = (as_ptr<YS>)y_;
+  const as_ptr<ES> e = (as_ptr<ES>)e_;
+  const int last = nc - 1;
+  const int nblk = (nc + D - 1) / D;  // blocks of D steps; padding steps are exact no-ops
+  // ---- forward: step j = q D + d; lane holds the row = lane (mod 64) in [j, j + 64)
+  {
+    double s = lane < nc ? r[lane] : 0.0;
+    // block q: c[d] = F[j][lane]; p[0] = 1 / l of this lane's row in the block (owners);
+    // p[1] = the row entering this lane (LATE: after the block; else lane d: at step j0 + d)
+    double cf[2][D], pv[2][2];
+    auto load = [&](int q, double (&c)[D], double (&p)[2]) {
+      const int j0 = q * D;
+      const int own = (j0 & ~63) + lane;
+      p[0] = RI[min(own, nc) + kBandPad];
+      const int nr = LATE ? own + 64 : j0 + lane + 64;
+      p[1] = r[min(nr, last)];
+      if (!(nr < nc && (LATE || lane < D))) p[1] = 0.0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) c[d] = F[band_at(j0 + d, lane)];
+    };
+    auto steps = [&](int q, const double (&c)[D], const double (&p)[2]) {
+      const int j0 = q * D;
+      const bool mine = lane >= (j0 & 63) && lane < (j0 & 63) + D;
+      double keep = 0.0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int j = j0 + d;
+        const double sj = readlane_d(s, j & 63);
+        if (LATE) {
+          s = __builtin_fma(-c[d], sj, s);
+        } else {
+          const bool own = lane == (j & 63);
+          keep = own ? sj : keep;
+          s = own ? readlane_d(p[1], d) : __builtin_fma(-c[d], sj, s);
+        }
+      }
+      if (LATE) keep = s;
+      const int jj = (j0 & ~63) + lane;
+      if (mine && jj < nc) y[jj] = keep * p[0];
+      if (LATE && mine) s = p[1];
+    };
+    load(0, cf[0], pv[0]);
+    for (int q = 0; q < nblk; q += 2) {
+      load(q + 1, cf[1], pv[1]);
+      steps(q, cf[0], pv[0]);
+      load(q + 2, cf[0], pv[0]);
+      steps(q + 1, cf[1], pv[1]);
+    }
+  }
+  // y stored by the owner lanes, read by every lane below
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // ---- backward: step j = last - (q D + d); lane holds the row = lane (mod 64) in (j - 64, j]
+  {
+    const int k0 = last - ((last - lane) & 63);
+    double s = k0 >= 0 ? y[k0] : 0.0;
+    double cf[2][D], pv[2][2];
+    auto load = [&](int q, double (&c)[D], double (&p)[2]) {
+      const int hi = last - q * D;
+      const int own = hi - ((hi - lane) & 63);  // this lane's row in (hi - 64, hi]
+      p[0] = RI[max(own, -1) + kBandPad];
+      const int nr = LATE ? own - 64 : hi - lane - 64;
+      p[1] = y[max(nr, 0)];
+      if (!(nr >= 0 && (LATE || lane < D))) p[1] = 0.0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int j = hi - d;
+        c[d] = G[band_at(j, lane)] * RI[j + kBandPad];
+      }
+    };
+    auto steps = [&](int q, const double (&c)[D], const double (&p)[2]) {
+      const int hi = last - q * D;
+      const int jj = hi - ((hi - lane) & 63);
+      const bool mine = jj > hi - D;
+      double keep = 0.0;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int j = hi - d;
+        const double sj = readlane_d(s, j & 63);
+        if (LATE) {
+          s = __builtin_fma(-c[d], sj, s);
+        } else {
+          const bool own = lane == (j & 63);
+          keep = own ? sj : keep;
+          s = own ? readlane_d(p[1], d) : __builtin_fma(-c[d], sj, s);
+        }
+      }
+      if (LATE) keep = s;
+      if (mine && jj >= 0) e[jj] = keep * p[0];
+      if (LATE && mine) s = p[1];
+    };
+    load(0, cf[0], pv[0]);
+    for (int q = 0; q < nblk; q += 2) {
+      load(q + 1, cf[1], pv[1]);
+      steps(q, cf[0], pv[0]);
+      load(q + 2, cf[0], pv[0]);
+      steps(q + 1, cf[1], pv[1]);
+    }
+  }
+}
+
 // A_H = P^T A P (dense, row j = coarse row j; accumulation order of the packed rows)
 __device__ void dense_galerkin(const BDesc& D, char* arena, double* AH, int tid) {
   const int n = D.n, nc = D.nc, KA = D.KA, KP = D.KP, KT = D.KT;
@@ -572,7 +872,7 @@ __global__ __launch_bounds__(256) void k_galerkin_rows(const BDesc* __restrict__
 // 1 = inverse Cholesky factor L^-1 in AH's lower triangle and its transpose in AI's upper
 // triangle, 0 = the Gauss-Jordan inverse in AI)
 __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ descs,
-                                                     char* __restrict__ arena) {
+                                                     char* __restrict__ arena, int band_pass) {
   extern __shared__ double lds[];
   __shared__ double redv[kBWaves];
   __shared__ int redi[kBWaves];
@@ -595,31 +895,38 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
     }
   };
   if (D.setup_mode == 3) return;
-  if (D.timing && tid == 0)
-    for (int q = 0; q < 8; ++q) tstat[q] = 0;
-  if (tid == 0) {  // phased cycles: done flag, half cycles run
-    stat[3] = 0;
-    tstat[7] = 0;
+  if (band_pass) {
+    // after k_amg2v_band: only a band factor that met a non-positive pivot continues, to
+    // Gauss-Jordan on its A_H (which the band factor only read)
+    if (D.band_ld == 0 || stat[2] == 2) return;
+  } else {
+    gather_values(D, arena, tid);
+    if (D.timing && tid == 0)
+      for (int q = 0; q < 8; ++q) tstat[q] = 0;
+    if (tid == 0) {  // phased cycles: done flag, half cycles run
+      stat[3] = 0;
+      tstat[7] = 0;
+    }
+    if (D.setup_mode == 1) {  // A_H from k_galerkin_rows, the inverse from dense.hip
+      if (tid == 0) {
+        stat[1] = 0;
+        stat[2] = 0;
+      }
+      return;
+    }
+    dense_galerkin(D, arena, AH, tid);
+    stamp(0);
+    if (D.setup_mode == 2 || D.band_ld > 0) {
+      // the inverse from dense.hip's batched factorisation, or the band factor of k_amg2v_band
+      if (tid == 0) {
+        stat[1] = 0;
+        stat[2] = D.band_ld > 0 ? 2 : 0;
+      }
+      return;
+    }
   }
 
-  if (D.setup_mode == 1) {  // A_H from k_galerkin_rows, the inverse from dense.hip
-    if (tid == 0) {
-      stat[1] = 0;
-      stat[2] = 0;
-    }
-    return;
-  }
-  dense_galerkin(D, arena, AH, tid);
-  stamp(0);
-  if (D.setup_mode == 2) {  // the inverse from dense.hip's batched factorisation
-    if (tid == 0) {
-      stat[1] = 0;
-      stat[2] = 0;
-    }
-    return;
-  }
-
-  if (D.spd) {
+  if (D.spd && !band_pass) {
     // the panel width is the problem's own (a function of n_c alone): a problem's roundings do
     // not depend on the batch it is launched with
     const bool ok = D.chol_nb == 16   ? chol_inverse<16>(AH, nc, lds, tid, stamp)
@@ -801,6 +1108,26 @@ __global__ __launch_bounds__(kBT) void k_amg2v_setup(const BDesc* __restrict__ d
   }
 }
 
+// The banded Cholesky factor of every problem with a band (one workgroup each, after
+// k_amg2v_setup's Galerkin product); a non-positive pivot sets stat[2] = 0, and the band pass of
+// k_amg2v_setup that follows inverts that A_H by Gauss-Jordan instead.
+__global__ __launch_bounds__(kBT) void k_amg2v_band(const BDesc* __restrict__ descs,
+                                                    char* __restrict__ arena) {
+  extern __shared__ double lds[];
+  const BDesc D = descs[blockIdx.x];
+  if (D.setup_mode == 3 || D.band_ld == 0) return;
+  int32_t* stat = at<int32_t>(arena, D.stat_out);
+  int64_t* tstat = at<int64_t>(arena, D.stat_out + 16);
+  const int64_t t0 = D.timing ? wall_clock64() : 0;
+  const bool ok = band_chol(at<double>(arena, D.AH), D.nc, D.band_ld - 1, lds,
+                            at<double>(arena, D.lc), at<double>(arena, D.lr),
+                            at<double>(arena, D.rinv), threadIdx.x);
+  if (threadIdx.x == 0) {
+    if (!ok) stat[2] = 0;
+    if (D.timing) tstat[1] += wall_clock64() - t0;
+  }
+}
+
 // The coarse solve of phased problems on every CU, a wave per row; block b belongs to problem q
 // with cblk[q] <= b < cblk[q + 1]. Each row is the one-workgroup rows_dot's: lane l sums the
 // columns l, l + 64, ... of its span with fma (masked slots add 0 * x), then the butterfly, so
@@ -822,6 +1149,7 @@ __global__ __launch_bounds__(256) void k_amg2v_coarse(const BDesc* __restrict__ 
   const int32_t* stat = at<int32_t>(arena, D->stat_out);
   if (stat[3]) return;
   const int mode = stat[2];
+  if (mode == 2) return;  // banded: solved by the problem's own workgroup (k_amg2v_cycles)
   if (PH == 2 && mode != 1) return;
   const int nc = D->nc;
   const int row = ((int)blockIdx.x - cblk[lo]) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1231,6 +1559,20 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
     }
   };
 
+  // the banded coarse solve on wave 0 (the band's rows need not fit the LDS)
+  // (r_H, e_H: LDS, or global when PHASED; the intermediate in r's storage: LDS when R_LDS)
+  auto band_coarse = [&](const double* rh, double* yv, double* ev) {
+    if (tid < 64) {
+      const int bw = D.band_ld - 1;
+      const double* F = at<double>(arena, D.lc);
+      const double* G = at<double>(arena, D.lr);
+      const double* ri = at<double>(arena, D.rinv);
+      constexpr int VS = PHASED ? 1 : 3, YS = R_LDS ? 3 : 1;
+      if (bw <= 56) band_solve<VS, YS, VS, true>(F, G, ri, nc, rh, yv, ev, tid);
+      else band_solve<VS, YS, VS, false>(F, G, ri, nc, rh, yv, ev, tid);
+    }
+  };
+
   auto smooth = [&](int nu) {
     stamp(3);
     for (int it = 0; it < nu; ++it) {
@@ -1292,6 +1634,11 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
       }
       __syncthreads();
       stamp(3);
+      if (mode == 2) {  // banded: this workgroup's wave 0 solves (k_amg2v_coarse skips it)
+        band_coarse(rcs, ys, es);
+        __syncthreads();
+        stamp(6);
+      }
     }
     #pragma unroll 1
     for (int i = tid; i < n; i += kBT) x_out[i] = xs[i];
@@ -1321,7 +1668,9 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
       }
       __syncthreads();
       stamp(3);
-      if (mode == 1) {  // e = L^-T (L^-1 r_H)
+      if (mode == 2) {  // banded: L y = r_H, L^T e = y on wave 0
+        band_coarse(rcs, ys, es);
+      } else if (mode == 1) {  // e = L^-T (L^-1 r_H)
         rows_dot<1>(AH, nc, rcs, ys, tid);
         __syncthreads();
         rows_dot<2>(AI, nc, ys, es, tid);
@@ -1395,22 +1744,6 @@ bool csr_symmetric(int64_t n, const int32_t* ip, const int32_t* ij, const double
       if (row[q].first != ti[tp[i] + q] || !(row[q].second == tv[tp[i] + q])) return false;
   }
   return true;
-}
-
-// rows of a CSR into a slot-major fixed-width layout (col -1 / value 0 pads); width = the
-// longest row (>= 1)
-int pack_rows(int64_t rows, const int32_t* ip, const int32_t* ij, const double* v,
-              std::vector<int32_t>& col, std::vector<double>& val) {
-  int w = 1;
-  for (int64_t i = 0; i < rows; ++i) w = std::max(w, ip[i + 1] - ip[i]);
-  col.assign((size_t)w * rows, -1);
-  val.assign((size_t)w * rows, 0.0);
-  for (int64_t i = 0; i < rows; ++i)
-    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
-      col[(size_t)(k - ip[i]) * rows + i] = ij[k];
-      val[(size_t)(k - ip[i]) * rows + i] = v[k];
-    }
-  return w;
 }
 
 // f(0 .. count-1) on up to MLAMG_HOST_THREADS (default: the CPUs this process may run on, at
@@ -1510,6 +1843,401 @@ void parallel_for(int count, F&& f) {
     for (int q = 0; q < count; ++q) f(q);
 }
 
+// ---------------------------------------------------------------- problem patterns and shapes
+// Everything the host derives from a problem's index arrays alone is computed once per distinct
+// sparsity pattern and kept across calls (a dataset's grids share few patterns: the reference's
+// farms loop over grids of a handful of sizes); per problem only the caller's values travel
+// (A.data, P.data, b, x0) and are placed into the packed layouts on the device.
+//   Pattern: the arrays (for the exact match), the exact-symmetry pairing of A's entries and the
+//            half-bandwidth of A_H = P^T A P — independent of the batch's flags;
+//   Shape:   a pattern's level schedule, packed column layouts and value maps for one set of
+//            batch flags (smoother, phased, residual in LDS, single call).
+struct Pattern {
+  int64_t n = 0, nc = 0, annz = 0, pnnz = 0;
+  uint64_t key = 0;
+  std::vector<int32_t> aip, aij, pip, pij;
+  // sym[k] = index of entry (j, i) for entry k = (i, j); sym_ok false when an entry has no
+  // mirror; dups when a row repeats a column (the value test then sorts, csr_symmetric)
+  std::vector<int32_t> sym;
+  bool sym_ok = false, dups = false;
+  int band = 0;  // half-bandwidth of A_H's structure (lower part)
+  size_t bytes() const { return 4 * (aip.size() + aij.size() + pip.size() + pij.size() + sym.size()); }
+};
+
+struct Shape {
+  std::shared_ptr<const Pattern> pat;
+  int smoother = 0, phased = 0, r_lds = 0, single = 0;
+  // slot-major packed columns (-1 pads) and, per slot, the index of its value in A.data /
+  // P.data (-1: pad, value 0.0)
+  std::vector<int32_t> akc, amap, ppc, pmap, ptc, tmap;
+  // Gauss-Seidel sweep in level order: lev/clev (level and chunk starts), pkc/gmap the
+  // off-diagonal slots (position-major for the one-wave sweep), dmap the last stored diagonal
+  // entry of each position (-1: none), pkr0 the position's row
+  std::vector<int32_t> lev, clev, pkc, gmap, dmap, pkr0;
+  bool chol_fits = false;
+  int K = 1, KA = 1, KP = 1, KT = 1, nlev = 0, panel = 8, cap = 0, chol_nb = 4;
+  int gs_rw = 0, gs_db = 0, gs_rp = 0;
+  size_t lds_base = 0, lds_chol = 0, lds_cycles = 0;
+  int code = MLAMG_OK;
+  std::string err;
+  size_t bytes() const {
+    size_t b = 0;
+    for (const auto* v : {&akc, &amap, &ppc, &pmap, &ptc, &tmap, &lev, &clev, &pkc, &gmap, &dmap,
+                          &pkr0})
+      b += 4 * v->size();
+    return b;
+  }
+};
+
+uint64_t mix_bytes(const void* data, size_t bytes, uint64_t h) {
+  const unsigned char* p = static_cast<const unsigned char*>(data);
+  constexpr uint64_t M1 = 0x9E3779B97F4A7C15ull, M2 = 0xC2B2AE3D27D4EB4Full;
+  uint64_t a = h ^ M1, b = h + M2, c = h * M1 + 1, d = h ^ M2;
+  size_t i = 0;
+  for (; i + 32 <= bytes; i += 32) {  // four independent lanes
+    uint64_t w[4];
+    std::memcpy(w, p + i, 32);
+    a = (a ^ w[0]) * M1;
+    b = (b ^ w[1]) * M2;
+    c = (c ^ w[2]) * M1;
+    d = (d ^ w[3]) * M2;
+    a ^= a >> 29;
+    b ^= b >> 31;
+    c ^= c >> 27;
+    d ^= d >> 33;
+  }
+  for (; i < bytes; ++i) a = (a ^ p[i]) * M1;
+  uint64_t r = a ^ (b * M1) ^ (c * M2) ^ (d + M1) ^ bytes;
+  r ^= r >> 32;
+  return r * M2;
+}
+
+uint64_t pattern_key(const mlamg_amg2v_problem& P) {
+  int64_t hdr[4] = {P.n, P.n_c, P.A_nnz, P.P_nnz};
+  uint64_t h = mix_bytes(hdr, sizeof(hdr), 0x5A17u);
+  h = mix_bytes(P.A_indptr, 4 * (size_t)(P.n + 1), h);
+  h = mix_bytes(P.A_indices, 4 * (size_t)P.A_nnz, h);
+  h = mix_bytes(P.P_indptr, 4 * (size_t)(P.n + 1), h);
+  return mix_bytes(P.P_indices, 4 * (size_t)P.P_nnz, h);
+}
+
+bool same_pattern(const mlamg_amg2v_problem& a, const mlamg_amg2v_problem& b) {
+  if (a.n != b.n || a.n_c != b.n_c || a.A_nnz != b.A_nnz || a.P_nnz != b.P_nnz) return false;
+  auto eq = [](const int32_t* x, const int32_t* y, int64_t cnt) {
+    return x == y || cnt == 0 || std::memcmp(x, y, 4 * (size_t)cnt) == 0;
+  };
+  return eq(a.A_indptr, b.A_indptr, a.n + 1) && eq(a.A_indices, b.A_indices, a.A_nnz) &&
+         eq(a.P_indptr, b.P_indptr, a.n + 1) && eq(a.P_indices, b.P_indices, a.P_nnz);
+}
+
+bool pattern_matches(const Pattern& S, const mlamg_amg2v_problem& P) {
+  mlamg_amg2v_problem q{};
+  q.n = S.n;
+  q.n_c = S.nc;
+  q.A_nnz = S.annz;
+  q.P_nnz = S.pnnz;
+  q.A_indptr = S.aip.data();
+  q.A_indices = S.aij.data();
+  q.P_indptr = S.pip.data();
+  q.P_indices = S.pij.data();
+  return same_pattern(q, P);
+}
+
+// bounded most-recently-used lists (count and bytes); one lock for both
+std::mutex g_shape_mu;
+std::vector<std::shared_ptr<const Pattern>> g_patterns;
+std::vector<std::shared_ptr<const Shape>> g_shapes;
+constexpr size_t kCacheCount = 64;
+constexpr size_t kCacheBytes = size_t(256) << 20;
+
+template <class T>
+void cache_trim(std::vector<std::shared_ptr<const T>>& v) {
+  size_t total = 0;
+  for (const auto& t : v) total += t->bytes();
+  while (v.size() > 1 && (v.size() > kCacheCount || total > kCacheBytes)) {
+    total -= v.front()->bytes();
+    v.erase(v.begin());
+  }
+}
+
+std::shared_ptr<const Pattern> pattern_lookup(uint64_t key, const mlamg_amg2v_problem& P) {
+  std::lock_guard<std::mutex> lk(g_shape_mu);
+  for (size_t i = g_patterns.size(); i-- > 0;)
+    if (g_patterns[i]->key == key && pattern_matches(*g_patterns[i], P)) {
+      auto s = g_patterns[i];
+      g_patterns.erase(g_patterns.begin() + (long)i);
+      g_patterns.push_back(s);
+      return s;
+    }
+  return nullptr;
+}
+
+std::shared_ptr<const Shape> shape_lookup(const Pattern* pat, int smoother, int phased,
+                                          int r_lds, int single) {
+  std::lock_guard<std::mutex> lk(g_shape_mu);
+  for (size_t i = g_shapes.size(); i-- > 0;) {
+    const Shape& S = *g_shapes[i];
+    if (S.pat.get() == pat && S.smoother == smoother && S.phased == phased &&
+        S.r_lds == r_lds && S.single == single) {
+      auto s = g_shapes[i];
+      g_shapes.erase(g_shapes.begin() + (long)i);
+      g_shapes.push_back(s);
+      return s;
+    }
+  }
+  return nullptr;
+}
+
+void pattern_insert(const std::shared_ptr<const Pattern>& s) {
+  std::lock_guard<std::mutex> lk(g_shape_mu);
+  g_patterns.push_back(s);
+  cache_trim(g_patterns);
+}
+
+void shape_insert(const std::shared_ptr<const Shape>& s) {
+  std::lock_guard<std::mutex> lk(g_shape_mu);
+  g_shapes.push_back(s);
+  cache_trim(g_shapes);
+}
+
+// rows of a CSR pattern into a slot-major fixed-width layout: col (-1 pads) and the index of
+// each slot's value (-1 pads); width = the longest row (>= 1)
+int pack_map(int64_t rows, const int32_t* ip, const int32_t* ij, std::vector<int32_t>& col,
+             std::vector<int32_t>& map) {
+  int w = 1;
+  for (int64_t i = 0; i < rows; ++i) w = std::max(w, ip[i + 1] - ip[i]);
+  col.assign((size_t)w * rows, -1);
+  map.assign((size_t)w * rows, -1);
+  for (int64_t i = 0; i < rows; ++i)
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
+      col[(size_t)(k - ip[i]) * rows + i] = ij[k];
+      map[(size_t)(k - ip[i]) * rows + i] = k;
+    }
+  return w;
+}
+
+std::shared_ptr<Pattern> analyse_pattern(const mlamg_amg2v_problem& P, uint64_t key) {
+  auto Sp = std::make_shared<Pattern>();
+  Pattern& S = *Sp;
+  const int64_t n = P.n, nnz = P.A_nnz;
+  const int32_t *ip = P.A_indptr, *ij = P.A_indices;
+  S.n = n;
+  S.nc = P.n_c;
+  S.annz = nnz;
+  S.pnnz = P.P_nnz;
+  S.key = key;
+  S.aip.assign(ip, ip + n + 1);
+  S.aij.assign(ij, ij + nnz);
+  S.pip.assign(P.P_indptr, P.P_indptr + n + 1);
+  S.pij.assign(P.P_indices, P.P_indices + P.P_nnz);
+  // A's structural transpose pairing
+  std::vector<int32_t> tp(n + 1, 0), tk(nnz), tr(nnz);
+  for (int64_t k = 0; k < nnz; ++k) tp[ij[k] + 1]++;
+  for (int64_t j = 0; j < n; ++j) tp[j + 1] += tp[j];
+  std::vector<int32_t> fill(tp.begin(), tp.end() - 1);
+  for (int64_t i = 0; i < n; ++i)
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {  // column j: rows ascending
+      tr[fill[ij[k]]] = (int32_t)i;
+      tk[fill[ij[k]]++] = k;
+    }
+  S.sym.assign(nnz, -1);
+  S.sym_ok = true;
+  std::vector<std::pair<int32_t, int32_t>> row;
+  for (int64_t i = 0; i < n; ++i) {
+    row.clear();
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) row.emplace_back(ij[k], k);
+    std::sort(row.begin(), row.end());
+    for (size_t q = 1; q < row.size(); ++q)
+      if (row[q].first == row[q - 1].first) S.dups = true;
+    if (ip[i + 1] - ip[i] != tp[i + 1] - tp[i]) {
+      S.sym_ok = false;
+      continue;
+    }
+    // column i of A (entries (r, i), r ascending) against row i's columns ascending
+    for (size_t q = 0; q < row.size(); ++q) {
+      if (tr[tp[i] + q] != row[q].first) S.sym_ok = false;
+      S.sym[row[q].second] = tk[tp[i] + q];
+    }
+  }
+  if (S.dups) S.sym_ok = false;
+  // half-bandwidth of A_H: (P^T A P)_IJ != 0 needs P_iI, A_ik, P_kJ != 0, so the lowest J of
+  // any coarse row I of fine row i is the lowest P column over i's A neighbours
+  std::vector<int32_t> pmin(n, INT32_MAX);
+  for (int64_t i = 0; i < n; ++i)
+    for (int32_t k = P.P_indptr[i]; k < P.P_indptr[i + 1]; ++k)
+      pmin[i] = std::min(pmin[i], P.P_indices[k]);
+  int band = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t am = INT32_MAX;
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) am = std::min(am, pmin[ij[k]]);
+    if (am == INT32_MAX) continue;
+    for (int32_t k = P.P_indptr[i]; k < P.P_indptr[i + 1]; ++k)
+      band = std::max(band, P.P_indices[k] - am);
+  }
+  S.band = band;
+  return Sp;
+}
+
+// chol_lds / setup_lds: LDS bytes of the inverse-Cholesky factor (two NB x (NB+1) blocks, the
+// L21 panel and the Z rows) and of the Gauss-Jordan panel (n_c x (b+1), pivots, permutation)
+size_t chol_lds(int nb, int64_t nc) {
+  return (size_t)8 * (2 * nb * (nb + 1) + (size_t)nc * (nb + 1) + (size_t)nb * nc);
+}
+size_t band_lds(int b) { return (size_t)8 * ((size_t)(b + 1) * (b + 1) + (b + 2)); }
+size_t gj_lds(int b, int64_t nc) { return (size_t)nc * (b + 1) * 8 + 16 * b + (size_t)nc * 12; }
+
+// the structure analysis of one pattern (P already validated)
+std::shared_ptr<Shape> analyse_shape(const mlamg_amg2v_problem& P,
+                                     const std::shared_ptr<const Pattern>& pat, int smoother,
+                                     int phased, int r_lds, int single) {
+  auto Sp = std::make_shared<Shape>();
+  Shape& L = *Sp;
+  const int64_t n = P.n, nc = P.n_c;
+  L.pat = pat;
+  L.smoother = smoother;
+  L.phased = phased;
+  L.r_lds = r_lds;
+  L.single = single;
+  L.KA = pack_map(n, P.A_indptr, P.A_indices, L.akc, L.amap);
+  L.KP = pack_map(n, P.P_indptr, P.P_indices, L.ppc, L.pmap);
+  {  // P^T: entries of coarse column j in ascending fine row
+    std::vector<int32_t> tp(nc + 1, 0);
+    for (int64_t k = 0; k < P.P_nnz; ++k) tp[P.P_indices[k] + 1]++;
+    for (int64_t j = 0; j < nc; ++j) tp[j + 1] += tp[j];
+    std::vector<int32_t> ti(P.P_nnz), tk(P.P_nnz);
+    std::vector<int32_t> fill(tp.begin(), tp.end() - 1);
+    for (int64_t i = 0; i < n; ++i)
+      for (int32_t k = P.P_indptr[i]; k < P.P_indptr[i + 1]; ++k) {
+        const int32_t j = P.P_indices[k];
+        ti[fill[j]] = (int32_t)i;
+        tk[fill[j]++] = k;
+      }
+    L.KT = pack_map(nc, tp.data(), ti.data(), L.ptc, L.tmap);
+    // pack_map stored positions into ti/tk; map them back to P.data indices
+    for (auto& m : L.tmap)
+      if (m >= 0) m = tk[m];
+  }
+  if (L.KA > kBMaxK + 1 || L.KP > kBMaxKP || L.KT > kBMaxKT) {
+    L.code = MLAMG_EUNSUPPORTED;
+    L.err = "amg2v_batch: rows of A, P or P^T longer than the batched solver's slots";
+    return Sp;
+  }
+  int chol_nb = 16;  // the widest panel that fits (wider panels lengthen the per-thread
+                     // triangular solves more than they save in trailing passes)
+  while (chol_nb > 4 && chol_lds(chol_nb, nc) > kBLdsBytes) chol_nb >>= 1;
+  L.chol_nb = chol_nb;
+  L.chol_fits = chol_lds(chol_nb, nc) <= kBLdsBytes;
+  L.lds_chol = chol_lds(chol_nb, nc);
+  // cycle vectors in LDS: x (+ zero and sink slots), r when it fits (L^-1 r_H shares it), r_H,
+  // e_H; the sweep's staging area gets the rest
+  const size_t vec_lds = (size_t)n * 8 * (r_lds ? 2 : 1) + 16 + (phased ? 0 : (size_t)nc * 16);
+  const size_t room = kBLdsBytes > vec_lds + 64 ? kBLdsBytes - vec_lds - 64 : 0;
+  int gs_rw = 0;
+  if (smoother == 0) {
+    // level schedule of the forward sweep (gs.hip): level(i) = 1 + max level(j) over j < i
+    // coupled in either direction; rows ascending within a level
+    std::vector<int32_t> level(n, 0), req(n, 0);
+    int maxoff = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      int32_t lv = req[i];
+      int off = 0;
+      for (int32_t k = P.A_indptr[i]; k < P.A_indptr[i + 1]; ++k) {
+        const int32_t j = P.A_indices[k];
+        if (j < i) lv = std::max(lv, level[j] + 1);
+        if (j != i) ++off;
+      }
+      level[i] = lv;
+      maxoff = std::max(maxoff, off);
+      for (int32_t k = P.A_indptr[i]; k < P.A_indptr[i + 1]; ++k) {
+        const int32_t j = P.A_indices[k];
+        if (j > i) req[j] = std::max(req[j], lv + 1);
+      }
+      L.nlev = std::max(L.nlev, lv + 1);
+    }
+    if (maxoff > kBMaxK) {
+      L.code = MLAMG_EUNSUPPORTED;
+      L.err = "amg2v_batch: a row of A has more than 32 off-diagonal entries";
+      return Sp;
+    }
+    L.lev.assign(L.nlev + 1, 0);
+    for (int64_t i = 0; i < n; ++i) L.lev[level[i] + 1]++;
+    for (int l = 0; l < L.nlev; ++l) L.lev[l + 1] += L.lev[l];
+    int wmax = 0;
+    for (int l = 0; l < L.nlev; ++l) wmax = std::max(wmax, L.lev[l + 1] - L.lev[l]);
+    // one-wave sweep: rows of 4 slots and levels of <= 128 rows, or 8 slots and <= 64 rows,
+    // and a staging area that holds the widest level (+ the dummy position)
+    const int km = maxoff <= 4 ? 4 : maxoff <= 8 ? 8 : 0;
+    if (km == 4 && wmax <= 128) gs_rw = wmax <= 64 ? 1 : 2;
+    if (km == 8 && wmax <= 64) gs_rw = 1;
+    if (gs_rw && (int)std::min<size_t>(4096, room / (12 * km + 24)) - 1 < wmax) gs_rw = 0;
+    // two staging buffers when each still holds >= 3 of the widest levels
+    static const bool no_db = std::getenv("MLAMG_BATCH_NO_DB") != nullptr;  // A/B knob
+    if (gs_rw && !no_db &&
+        (int)std::min<size_t>(4096, room / (2 * (12 * km + 24) + 16)) - 1 >= 3 * wmax)
+      L.gs_db = 1;
+    L.K = gs_rw ? km : std::max(maxoff, 1);
+    const int64_t K = L.K;
+    L.pkr0.resize(n);
+    L.pkc.assign((size_t)n * K, gs_rw ? (int32_t)n : -1);
+    L.gmap.assign((size_t)n * K, -1);
+    L.dmap.assign(n, -1);
+    std::vector<int32_t> fill(L.lev.begin(), L.lev.end() - 1);
+    for (int64_t i = 0; i < n; ++i) {
+      const int32_t p = fill[level[i]]++;
+      L.pkr0[p] = (int32_t)i;
+      int s2 = 0;
+      for (int32_t k = P.A_indptr[i]; k < P.A_indptr[i + 1]; ++k) {
+        if (P.A_indices[k] == i) {
+          L.dmap[p] = k;  // the last stored diagonal entry, as the sweep takes it
+        } else {
+          // slot-major for the workgroup sweep, position-major for the one-wave sweep
+          const size_t at = gs_rw ? (size_t)p * K + s2 : (size_t)s2 * n + p;
+          L.pkc[at] = P.A_indices[k];
+          L.gmap[at] = k;
+          ++s2;
+        }
+      }
+    }
+  }
+  // panel width: the widest power of two <= 16 whose n_c x (b+1) panel (+ pivots and the
+  // final column permutation) fits
+  int pb = kBMaxPanel;
+  while (pb > 4 && gj_lds(pb, nc) > kBLdsBytes) pb >>= 1;
+  if (gj_lds(pb, nc) > kBLdsBytes) {
+    L.code = MLAMG_EINVAL;
+    L.err = "coarse too large";
+    return Sp;
+  }
+  L.panel = pb;
+  // GS staging chunks: runs of consecutive levels with <= cap rows, cap from the LDS left
+  // after the cycle vectors, one position kept for the one-wave sweep's dummy (a level wider
+  // than cap is swept by the workgroup straight from the arena)
+  if (smoother == 0) {
+    const size_t per_pos = (12 * (size_t)L.K + 24) * (L.gs_db ? 2 : 1);
+    const size_t slack = L.gs_db ? 32 : 0;
+    L.cap = (int)std::min<size_t>(4096, (room > slack ? room - slack : 0) / per_pos) - 1;
+    L.clev.push_back(0);
+    int l = 0;
+    while (l < L.nlev) {
+      const int start = l;
+      int cnt = 0;
+      while (l < L.nlev && (l == start || cnt + (L.lev[l + 1] - L.lev[l]) <= L.cap)) {
+        cnt += L.lev[l + 1] - L.lev[l];
+        ++l;
+      }
+      L.clev.push_back(l);
+    }
+  }
+  static const bool no_rp = std::getenv("MLAMG_BATCH_NO_RP") != nullptr;  // A/B knob
+  if (phased && single && gs_rw && !L.gs_db && !no_rp && L.cap + 1 <= kBT - 64 &&
+      L.cap * L.K <= 2 * (kBT - 64))
+    L.gs_rp = 1;
+  L.lds_base = gj_lds(pb, nc);
+  L.lds_cycles = vec_lds + 16 + (size_t)(L.cap + 1) * (12 * L.K + 24) * (L.gs_db ? 2 : 1) + 40;
+  L.gs_rw = gs_rw;
+  return Sp;
+}
+
 }  // namespace
 }  // namespace mlamg
 
@@ -1533,34 +2261,96 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   MLAMG_REQUIRE(nu_pre >= 0 && nu_post >= 0 && max_iter >= 0, "negative count");
   if (count == 0) return MLAMG_OK;
   hipStream_t s = S(stream);
-  // ---- host: validation, structure analysis, layout
-  struct Plan {
-    std::vector<int32_t> lev, pkr, pkc, clev, akc, ppc, ptc;
-    std::vector<double> pkv, pkd, akv, ppv, ptv, blv;  // blv: b in sweep (level) order
-    int K = 1, KA = 1, KP = 1, KT = 1, nlev = 0, panel = 8, cap = 0;
-    bool spd = false;
-    int chol_nb = 4, gs_rw = 0, gs_db = 0, gs_rp = 0;
-    size_t lds_setup = 0, lds_cycles = 0;
-    int code = MLAMG_OK;  // analysis failure: code + message (reported for the first problem)
-    std::string err;
-  };
+  // ---- host: validation, patterns (flag-independent analysis), per-problem value checks, the
+  // batch's strategy, shapes (flag-dependent analysis); patterns and shapes cached across calls
   static const bool timing = std::getenv("MLAMG_BATCH_TIMING") != nullptr;
   const auto t_begin = std::chrono::steady_clock::now();
-  std::vector<Plan> plans(count);
   std::vector<BDesc> desc(count);
-  // a single problem with a large coarse operator: the coarse inverse from the device-wide
-  // factorisation (dense.hip) and phased cycles, the coarse solve on every CU
+  const bool no_cache = std::getenv("MLAMG_BATCH_NO_SHAPE_CACHE") != nullptr;  // A/B knob
+  const bool no_band = std::getenv("MLAMG_BATCH_NO_BAND") != nullptr;         // A/B knob
+  // 1. validation and the pattern key of every problem (host threads)
+  std::vector<int> vcode(count, MLAMG_OK);
+  std::vector<const char*> verr(count, nullptr);
+  std::vector<uint64_t> key(count, 0);
+  parallel_for(count, [&](int q) {
+    const mlamg_amg2v_problem& P = probs[q];
+    auto fail = [&](const char* m) {
+      vcode[q] = MLAMG_EINVAL;
+      verr[q] = m;
+    };
+    const int64_t n = P.n, nc = P.n_c;
+    if (!(n >= 1 && n <= kBMaxN)) return fail("problem rows out of range for the batched solver");
+    if (!(nc >= 1 && nc <= kBMaxNc && nc <= n)) return fail("coarse size out of range");
+    if (!(valid_csr(n, n, P.A_nnz, P.A_indptr, P.A_indices) && P.A_data))
+      return fail("A is not a valid n x n CSR");
+    if (!(valid_csr(n, nc, P.P_nnz, P.P_indptr, P.P_indices) && P.P_data))
+      return fail("P is not a valid n x n_c CSR");
+    if (!(P.b && P.x0 && P.x_out && (max_iter == 0 || P.err_out))) return fail("NULL vector");
+    key[q] = pattern_key(P);
+  });
+  for (int q = 0; q < count; ++q)
+    if (vcode[q] != MLAMG_OK) {
+      set_error(std::string(verr[q]) + " (problem " + std::to_string(q) + ")");
+      return vcode[q];
+    }
+  // 2. group by key (a representative per distinct key), members compared in full (a key
+  // collision leaves the member its own pattern); patterns from the cache or analysed
+  std::vector<int> rep(count);
+  {
+    std::vector<std::pair<uint64_t, int>> order(count);
+    for (int q = 0; q < count; ++q) order[q] = {key[q], q};
+    std::sort(order.begin(), order.end());
+    for (int t = 0; t < count; ++t)
+      rep[order[t].second] = t > 0 && order[t].first == order[t - 1].first
+                                 ? rep[order[t - 1].second]
+                                 : order[t].second;
+  }
+  parallel_for(count, [&](int q) {
+    if (rep[q] != q && !same_pattern(probs[q], probs[rep[q]])) rep[q] = q;
+  });
+  std::vector<std::shared_ptr<const Pattern>> pat(count);
+  std::vector<int> todo;
+  for (int q = 0; q < count; ++q)
+    if (rep[q] == q) {
+      if (!no_cache) pat[q] = pattern_lookup(key[q], probs[q]);
+      if (!pat[q]) todo.push_back(q);
+    }
+  parallel_for((int)todo.size(), [&](int t) {
+    const int q = todo[t];
+    auto S = analyse_pattern(probs[q], key[q]);
+    if (!no_cache) pattern_insert(S);
+    pat[q] = S;
+  });
+  for (int q = 0; q < count; ++q) pat[q] = pat[rep[q]];
+  // 3. per problem: A == A^T exactly (values included) -> an SPD coarse operator, factored as a
+  // band when its structure is narrow, else as a dense inverse Cholesky factor
+  std::vector<char> sym(count, 0), band(count, 0);
+  parallel_for(count, [&](int q) {
+    const Pattern& S = *pat[q];
+    const mlamg_amg2v_problem& P = probs[q];
+    bool s = false;
+    if (S.sym_ok) {
+      s = true;
+      for (int64_t k = 0; k < S.annz && s; ++k) s = P.A_data[k] == P.A_data[S.sym[k]];
+    } else if (S.dups) {
+      s = csr_symmetric(P.n, P.A_indptr, P.A_indices, P.A_data);
+    }
+    sym[q] = s ? 1 : 0;
+    band[q] = s && !no_band && S.band <= kBandMax && band_lds(S.band) <= kBLdsBytes ? 1 : 0;
+  });
+  // 4. strategy. A single problem with a large dense coarse operator: the coarse inverse from
+  // the device-wide factorisation (dense.hip) and phased cycles, the coarse solve on every CU.
+  // Batches holding such problems run phased too (each problem's cycles on its workgroup, the
+  // dense coarse solves spread over the CUs; banded problems solve on their own workgroup)
   static const int ext_min = [] {
     const char* e = std::getenv("MLAMG_BATCH_EXT_MIN");
     return e ? std::atoi(e) : kExtCoarseMin;
   }();
-  const bool ext_ok = count == 1 && probs[0].n_c > ext_min && !std::getenv("MLAMG_BATCH_NO_EXT");
-  // batches whose largest coarse operator is above the same size run phased too (each problem's
-  // cycles on its workgroup, every problem's coarse solve spread over the CUs); their coarse
-  // inverses stay the one-workgroup factors, so a batch's results equal the non-phased launch's
-  int64_t max_nc = 0;
-  for (int q = 0; q < count; ++q) max_nc = std::max<int64_t>(max_nc, probs[q].n_c);
-  const bool phased_batch = count > 1 && max_nc > ext_min && !std::getenv("MLAMG_BATCH_NO_EXT") &&
+  const bool no_ext = std::getenv("MLAMG_BATCH_NO_EXT") != nullptr;
+  bool big_dense = false;
+  for (int q = 0; q < count; ++q) big_dense = big_dense || (!band[q] && probs[q].n_c > ext_min);
+  const bool ext_ok = count == 1 && big_dense && !no_ext;
+  const bool phased_batch = count > 1 && big_dense && !no_ext &&
                             !std::getenv("MLAMG_BATCH_NO_PHASED_BATCH");
   const bool phased = (ext_ok || phased_batch) && !std::getenv("MLAMG_BATCH_NO_PHASED");
   // residual in LDS when every problem leaves room for it (phased: r_H, e_H live in the arena)
@@ -1570,191 +2360,78 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
                         16 * 1024;
     if (need > kBLdsBytes) r_lds = false;
   }
+  const int single = count == 1 ? 1 : 0;
+  // 5. shapes for these flags (cached per pattern)
+  std::vector<std::shared_ptr<const Shape>> shape(count);
+  todo.clear();
+  for (int q = 0; q < count; ++q)
+    if (rep[q] == q) {
+      if (!no_cache) shape[q] = shape_lookup(pat[q].get(), smoother, phased, r_lds, single);
+      if (!shape[q]) todo.push_back(q);
+    }
+  parallel_for((int)todo.size(), [&](int t) {
+    const int q = todo[t];
+    auto S = analyse_shape(probs[q], pat[q], smoother, phased, r_lds, single);
+    if (S->code == MLAMG_OK && !no_cache) shape_insert(S);
+    shape[q] = S;
+  });
+  for (int q = 0; q < count; ++q) shape[q] = shape[rep[q]];
+  for (int q = 0; q < count; ++q)
+    if (shape[q]->code != MLAMG_OK) {
+      set_error(shape[q]->err + " (problem " + std::to_string(q) + ")");
+      return shape[q]->code;
+    }
+  // the dense inverse Cholesky factor where no band is taken and it fits one workgroup's LDS
+  std::vector<char> spd(count, 0);
+  for (int q = 0; q < count; ++q) spd[q] = sym[q] && !band[q] && shape[q]->chol_fits ? 1 : 0;
+  const auto t_analysed = std::chrono::steady_clock::now();
+  // ---- layout: each distinct shape's structure once, then every problem's values
   Layout lay;
   const int64_t desc_off = lay.take(sizeof(BDesc) * count);
-  size_t lds_setup = 0, lds_cycles = 0;
-  // inverse-Cholesky LDS: two NB x (NB+1) blocks, the L21 panel and the Z rows
-  auto chol_lds = [](int nb, int64_t nc) {
-    return (size_t)8 * (2 * nb * (nb + 1) + (size_t)nc * (nb + 1) + (size_t)nb * nc);
+  size_t lds_setup = 0, lds_cycles = 0, lds_band = 0;
+  bool any_band = false;
+  for (int q = 0; q < count; ++q) any_band = any_band || band[q];
+  struct ShapeOffs {
+    int64_t akc, amap, ppc, pmap, ptc, tmap, lev, clev, pkc, gmap, dmap, pkr0;
   };
-  auto analyse = [&](int q) {
-    mlamg_amg2v_problem& P = probs[q];
-    Plan& L = plans[q];
-#define REQ(cond, msg)       \
-  do {                       \
-    if (!(cond)) {           \
-      L.code = MLAMG_EINVAL; \
-      L.err = (msg);         \
-      return;                \
-    }                        \
-  } while (0)
-    const int64_t n = P.n, nc = P.n_c;
-    REQ(n >= 1 && n <= kBMaxN, "problem rows out of range for the batched solver");
-    REQ(nc >= 1 && nc <= kBMaxNc && nc <= n, "coarse size out of range");
-    REQ(valid_csr(n, n, P.A_nnz, P.A_indptr, P.A_indices) && P.A_data,
-        "A is not a valid n x n CSR");
-    REQ(valid_csr(n, nc, P.P_nnz, P.P_indptr, P.P_indices) && P.P_data,
-        "P is not a valid n x n_c CSR");
-    REQ(P.b && P.x0 && P.x_out && (max_iter == 0 || P.err_out), "NULL vector");
-    L.KA = pack_rows(n, P.A_indptr, P.A_indices, P.A_data, L.akc, L.akv);
-    L.KP = pack_rows(n, P.P_indptr, P.P_indices, P.P_data, L.ppc, L.ppv);
-    {  // P^T: entries of coarse column j in ascending fine row
-      std::vector<int32_t> tp(nc + 1, 0);
-      for (int64_t k = 0; k < P.P_nnz; ++k) tp[P.P_indices[k] + 1]++;
-      for (int64_t j = 0; j < nc; ++j) tp[j + 1] += tp[j];
-      std::vector<int32_t> ti(P.P_nnz);
-      std::vector<double> tv(P.P_nnz);
-      std::vector<int32_t> fill(tp.begin(), tp.end() - 1);
-      for (int64_t i = 0; i < n; ++i)
-        for (int32_t k = P.P_indptr[i]; k < P.P_indptr[i + 1]; ++k) {
-          const int32_t j = P.P_indices[k];
-          ti[fill[j]] = (int32_t)i;
-          tv[fill[j]++] = P.P_data[k];
-        }
-      L.KT = pack_rows(nc, tp.data(), ti.data(), tv.data(), L.ptc, L.ptv);
-    }
-    if (L.KA > kBMaxK + 1 || L.KP > kBMaxKP || L.KT > kBMaxKT) {
-      L.code = MLAMG_EUNSUPPORTED;
-      L.err = "amg2v_batch: rows of A, P or P^T longer than the batched solver's slots";
-      return;
-    }
-    int chol_nb = 16;  // the widest panel that fits (wider panels lengthen the per-thread
-                       // triangular solves more than they save in trailing passes)
-    while (chol_nb > 4 && chol_lds(chol_nb, nc) > kBLdsBytes) chol_nb >>= 1;
-    const bool spd = csr_symmetric(n, P.A_indptr, P.A_indices, P.A_data) &&
-                     chol_lds(chol_nb, nc) <= kBLdsBytes;
-    if (spd) L.lds_setup = chol_lds(chol_nb, nc);
-    // cycle vectors in LDS: x (+ zero and sink slots), r when it fits (L^-1 r_H shares it), r_H,
-    // e_H; the sweep's staging area gets the rest
-    const size_t vec_lds = (size_t)n * 8 * (r_lds ? 2 : 1) + 16 + (phased ? 0 : (size_t)nc * 16);
-    const size_t room = kBLdsBytes > vec_lds + 64 ? kBLdsBytes - vec_lds - 64 : 0;
-    int gs_rw = 0;
-    if (smoother == 0) {
-      // level schedule of the forward sweep (gs.hip): level(i) = 1 + max level(j) over j < i
-      // coupled in either direction; rows ascending within a level
-      std::vector<int32_t> level(n, 0), req(n, 0);
-      int maxoff = 0;
-      for (int64_t i = 0; i < n; ++i) {
-        int32_t lv = req[i];
-        int off = 0;
-        for (int32_t k = P.A_indptr[i]; k < P.A_indptr[i + 1]; ++k) {
-          const int32_t j = P.A_indices[k];
-          if (j < i) lv = std::max(lv, level[j] + 1);
-          if (j != i) ++off;
-        }
-        level[i] = lv;
-        maxoff = std::max(maxoff, off);
-        for (int32_t k = P.A_indptr[i]; k < P.A_indptr[i + 1]; ++k) {
-          const int32_t j = P.A_indices[k];
-          if (j > i) req[j] = std::max(req[j], lv + 1);
-        }
-        L.nlev = std::max(L.nlev, lv + 1);
-      }
-      if (maxoff > kBMaxK) {
-        L.code = MLAMG_EUNSUPPORTED;
-        L.err = "amg2v_batch: a row of A has more than 32 off-diagonal entries";
-        return;
-      }
-      L.lev.assign(L.nlev + 1, 0);
-      for (int64_t i = 0; i < n; ++i) L.lev[level[i] + 1]++;
-      for (int l = 0; l < L.nlev; ++l) L.lev[l + 1] += L.lev[l];
-      int wmax = 0;
-      for (int l = 0; l < L.nlev; ++l) wmax = std::max(wmax, L.lev[l + 1] - L.lev[l]);
-      // one-wave sweep: rows of 4 slots and levels of <= 128 rows, or 8 slots and <= 64 rows,
-      // and a staging area that holds the widest level (+ the dummy position)
-      const int km = maxoff <= 4 ? 4 : maxoff <= 8 ? 8 : 0;
-      if (km == 4 && wmax <= 128) gs_rw = wmax <= 64 ? 1 : 2;
-      if (km == 8 && wmax <= 64) gs_rw = 1;
-      if (gs_rw && (int)std::min<size_t>(4096, room / (12 * km + 24)) - 1 < wmax) gs_rw = 0;
-      // two staging buffers when each still holds >= 3 of the widest levels
-      static const bool no_db = std::getenv("MLAMG_BATCH_NO_DB") != nullptr;  // A/B knob
-      if (gs_rw && !no_db &&
-          (int)std::min<size_t>(4096, room / (2 * (12 * km + 24) + 16)) - 1 >= 3 * wmax)
-        L.gs_db = 1;
-      L.K = gs_rw ? km : std::max(maxoff, 1);
-      const int64_t K = L.K;
-      L.pkr.resize(n);
-      L.pkc.assign((size_t)n * K, gs_rw ? (int32_t)n : -1);
-      L.pkv.assign((size_t)n * K, 0.0);
-      L.pkd.assign(n, 0.0);
-      std::vector<int32_t> fill(L.lev.begin(), L.lev.end() - 1);
-      L.blv.resize(n);
-      for (int64_t i = 0; i < n; ++i) {
-        const int32_t p = fill[level[i]]++;
-        L.pkr[p] = (int32_t)i;
-        L.blv[p] = P.b[i];
-        int s2 = 0;
-        for (int32_t k = P.A_indptr[i]; k < P.A_indptr[i + 1]; ++k) {
-          if (P.A_indices[k] == i) {
-            L.pkd[p] = P.A_data[k];  // the last stored diagonal entry, as the sweep takes it
-          } else {
-            // slot-major for the workgroup sweep, position-major for the one-wave sweep
-            const size_t at = gs_rw ? (size_t)p * K + s2 : (size_t)s2 * n + p;
-            L.pkc[at] = P.A_indices[k];
-            L.pkv[at] = P.A_data[k];
-            ++s2;
-          }
-        }
-        if (gs_rw && L.pkd[p] == 0.0) {  // pyamg leaves x_i alone: write the sink slot
-          L.pkd[p] = 1.0;
-          L.pkr[p] = (int32_t)n + 1;
-        }
-      }
-    }
-    // panel width: the widest power of two <= 16 whose n_c x (b+1) panel (+ pivots and the
-    // final column permutation) fits
-    int pb = kBMaxPanel;
-    auto setup_lds = [&](int b) { return (size_t)nc * (b + 1) * 8 + 16 * b + (size_t)nc * 12; };
-    while (pb > 4 && setup_lds(pb) > kBLdsBytes) pb >>= 1;
-    REQ(setup_lds(pb) <= kBLdsBytes, "coarse too large");
-    L.panel = pb;
-    // GS staging chunks: runs of consecutive levels with <= cap rows, cap from the LDS left
-    // after the cycle vectors, one position kept for the one-wave sweep's dummy (a level wider
-    // than cap is swept by the workgroup straight from the arena)
-    if (smoother == 0) {
-      const size_t per_pos = (12 * (size_t)L.K + 24) * (L.gs_db ? 2 : 1);
-      const size_t slack = L.gs_db ? 32 : 0;
-      L.cap = (int)std::min<size_t>(4096, (room > slack ? room - slack : 0) / per_pos) - 1;
-      L.clev.push_back(0);
-      int l = 0;
-      while (l < L.nlev) {
-        const int start = l;
-        int cnt = 0;
-        while (l < L.nlev && (l == start || cnt + (L.lev[l + 1] - L.lev[l]) <= L.cap)) {
-          cnt += L.lev[l + 1] - L.lev[l];
-          ++l;
-        }
-        L.clev.push_back(l);
-      }
-    }
-    static const bool no_rp = std::getenv("MLAMG_BATCH_NO_RP") != nullptr;  // A/B knob
-    if (phased && count == 1 && gs_rw && !L.gs_db && !no_rp && L.cap + 1 <= kBT - 64 &&
-        L.cap * L.K <= 2 * (kBT - 64))
-      L.gs_rp = 1;
-    L.lds_setup = std::max(L.lds_setup, setup_lds(pb));
-    L.lds_cycles = vec_lds + 16 + (size_t)(L.cap + 1) * (12 * L.K + 24) * (L.gs_db ? 2 : 1) + 40;
-    L.spd = spd;
-    L.chol_nb = chol_nb;
-    L.gs_rw = gs_rw;
-    L.panel = pb;
-  };
-  // per-problem analysis on the host's cores (one problem per task)
-  parallel_for(count, analyse);
-  const auto t_analysed = std::chrono::steady_clock::now();
+  std::vector<const Shape*> uniq;
+  std::vector<ShapeOffs> uoff;
+  std::vector<int> uidx(count, -1);
   for (int q = 0; q < count; ++q) {
-    const Plan& L = plans[q];
-    if (L.code != MLAMG_OK) {
-      set_error(L.err + " (problem " + std::to_string(q) + ")");
-      return L.code;
+    if (rep[q] != q) {
+      uidx[q] = uidx[rep[q]];
+      continue;
     }
-    lds_setup = std::max(lds_setup, L.lds_setup);
+    const Shape& S = *shape[q];
+    ShapeOffs o;
+    o.akc = lay.take(4 * S.akc.size());
+    o.amap = lay.take(4 * S.amap.size());
+    o.ppc = lay.take(4 * S.ppc.size());
+    o.pmap = lay.take(4 * S.pmap.size());
+    o.ptc = lay.take(4 * S.ptc.size());
+    o.tmap = lay.take(4 * S.tmap.size());
+    o.lev = lay.take(4 * S.lev.size());
+    o.clev = lay.take(4 * S.clev.size());
+    o.pkc = lay.take(4 * S.pkc.size());
+    o.gmap = lay.take(4 * S.gmap.size());
+    o.dmap = lay.take(4 * S.dmap.size());
+    o.pkr0 = lay.take(4 * S.pkr0.size());
+    uidx[q] = (int)uniq.size();
+    uniq.push_back(&S);
+    uoff.push_back(o);
+  }
+  for (int q = 0; q < count; ++q) {
+    const Shape& L = *shape[q];
+    const ShapeOffs& o = uoff[uidx[q]];
+    lds_setup = std::max(lds_setup, std::max(L.lds_base, spd[q] ? L.lds_chol : size_t(0)));
+    if (band[q]) lds_band = std::max(lds_band, band_lds(pat[q]->band));
     lds_cycles = std::max(lds_cycles, L.lds_cycles);
     const mlamg_amg2v_problem& P = probs[q];
-    const int64_t n = P.n, nc = P.n_c;
+    const int64_t n = P.n;
     BDesc& D = desc[q];
     std::memset(&D, 0, sizeof(D));
     D.n = (int32_t)n;
-    D.nc = (int32_t)nc;
+    D.nc = (int32_t)P.n_c;
     D.smoother = smoother;
     D.nu_pre = nu_pre;
     D.nu_post = nu_post;
@@ -1769,7 +2446,8 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     D.n_chunks = L.clev.empty() ? 0 : (int32_t)L.clev.size() - 1;
     D.cap = L.cap;
     D.timing = timing ? 1 : 0;
-    D.spd = L.spd ? 1 : 0;
+    D.spd = spd[q];
+    D.band_ld = band[q] ? pat[q]->band + 1 : 0;
     D.chol_nb = L.chol_nb;
     D.gs_rw = L.gs_rw;
     D.gs_db = L.gs_db;
@@ -1777,23 +2455,23 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     D.phased = phased ? 1 : 0;
     D.tol = tol;
     D.omega = jacobi_weight;
-    D.ak_col = lay.take(4 * L.akc.size());
-    D.ak_val = lay.take(8 * L.akv.size());
-    D.pp_col = lay.take(4 * L.ppc.size());
-    D.pp_val = lay.take(8 * L.ppv.size());
-    D.pt_row = lay.take(4 * L.ptc.size());
-    D.pt_val = lay.take(8 * L.ptv.size());
-    D.lev_ptr = lay.take(4 * L.lev.size());
-    D.chunk_lev = lay.take(4 * L.clev.size());
-    D.pk_row = lay.take(4 * L.pkr.size());
-    D.pk_col = lay.take(4 * L.pkc.size());
-    D.pk_val = lay.take(8 * L.pkv.size());
-    D.pk_diag = lay.take(8 * L.pkd.size());
-    D.b_lvl = lay.take(8 * L.pkr.size());
+    D.ak_col = o.akc;
+    D.a_map = o.amap;
+    D.pp_col = o.ppc;
+    D.p_map = o.pmap;
+    D.pt_row = o.ptc;
+    D.t_map = o.tmap;
+    D.lev_ptr = o.lev;
+    D.chunk_lev = o.clev;
+    D.pk_col = o.pkc;
+    D.g_map = o.gmap;
+    D.d_map = o.dmap;
+    D.pk_row0 = o.pkr0;
+    D.a_raw = lay.take(8 * (size_t)P.A_nnz);
+    D.p_raw = lay.take(8 * (size_t)P.P_nnz);
     D.b = lay.take(8 * n);
     D.x0 = lay.take(8 * n);
   }
-#undef REQ
   // phased: each problem's first coarse-solve block (k_amg2v_coarse), a row per wave
   const int64_t cblk_off = phased ? lay.take(4 * (size_t)(count + 1)) : 0;
   std::vector<int32_t> cblk(count + 1, 0);
@@ -1803,10 +2481,24 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   const size_t in_bytes = lay.off;
   for (int q = 0; q < count; ++q) {
     BDesc& D = desc[q];
+    const Shape& L = *shape[q];
+    // the packed values, gathered on the device (gather_values)
+    D.ak_val = lay.take(8 * L.akc.size());
+    D.pp_val = lay.take(8 * L.ppc.size());
+    D.pt_val = lay.take(8 * L.ptc.size());
+    D.pk_val = lay.take(8 * L.pkc.size());
+    D.pk_diag = lay.take(8 * L.pkr0.size());
+    D.pk_row = lay.take(4 * L.pkr0.size());
+    D.b_lvl = lay.take(8 * L.pkr0.size());
     D.AH = lay.take((size_t)8 * D.nc * D.nc);
     D.AI = lay.take((size_t)8 * D.nc * D.nc);
     D.rg = lay.take(8 * (size_t)D.n);
     D.dinv = lay.take(8 * (size_t)D.n);
+    if (D.band_ld > 0) {  // the band solve's lane layouts (band_chol), padded
+      D.lc = lay.take((size_t)8 * 64 * (D.nc + 2 * kBandPad));
+      D.lr = lay.take((size_t)8 * 64 * (D.nc + 2 * kBandPad));
+      D.rinv = lay.take((size_t)8 * (D.nc + 2 * kBandPad));
+    }
     if (phased) {
       D.rcg = lay.take(8 * (size_t)D.nc);
       D.eg = lay.take(8 * (size_t)D.nc);
@@ -1824,13 +2516,16 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   }
   const size_t total = lay.off;
   // a single problem with a large SPD coarse operator takes the device-wide coarse factorisation
-  const bool ext_coarse = ext_ok && plans[0].spd;
+  const bool ext_coarse = ext_ok && spd[0];
   if (ext_coarse) desc[0].setup_mode = 1;
-  // a phased batch factors its SPD operators device-wide too, all in one launch sequence
+  // a phased batch factors its large SPD operators device-wide too, all in one launch sequence.
+  // The factor is chosen by the problem's own n_c, as a single call chooses it (the batched and
+  // the single device-wide factors run the same code per operator): a problem's results do not
+  // depend on the batch it is launched with
   const bool batch_ext = phased && count > 1 && !std::getenv("MLAMG_BATCH_NO_BATCH_EXT");
   if (batch_ext)
     for (int q = 0; q < count; ++q)
-      if (plans[q].spd) desc[q].setup_mode = 2;
+      if (spd[q] && desc[q].nc > ext_min) desc[q].setup_mode = 2;
   // ---- pack the inputs into pinned host memory, one copy in
   HostPinned& H = g_batch_host;
   const size_t host_need = std::max(in_bytes, total - out_begin);
@@ -1849,26 +2544,32 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   auto put = [&](int64_t off, const void* src, size_t bytes) {
     if (bytes) std::memcpy(hb + off, src, bytes);
   };
-  parallel_for(count, [&](int q) {
+  const int nu = (int)uniq.size();
+  parallel_for(nu + count, [&](int t) {
+    if (t < nu) {  // a shape's structure
+      const Shape& S = *uniq[t];
+      const ShapeOffs& o = uoff[t];
+      put(o.akc, S.akc.data(), 4 * S.akc.size());
+      put(o.amap, S.amap.data(), 4 * S.amap.size());
+      put(o.ppc, S.ppc.data(), 4 * S.ppc.size());
+      put(o.pmap, S.pmap.data(), 4 * S.pmap.size());
+      put(o.ptc, S.ptc.data(), 4 * S.ptc.size());
+      put(o.tmap, S.tmap.data(), 4 * S.tmap.size());
+      put(o.lev, S.lev.data(), 4 * S.lev.size());
+      put(o.clev, S.clev.data(), 4 * S.clev.size());
+      put(o.pkc, S.pkc.data(), 4 * S.pkc.size());
+      put(o.gmap, S.gmap.data(), 4 * S.gmap.size());
+      put(o.dmap, S.dmap.data(), 4 * S.dmap.size());
+      put(o.pkr0, S.pkr0.data(), 4 * S.pkr0.size());
+      return;
+    }
+    const int q = t - nu;  // a problem's values
     const mlamg_amg2v_problem& P = probs[q];
     const BDesc& D = desc[q];
-    const Plan& L = plans[q];
-    const int64_t n = P.n;
-    put(D.ak_col, L.akc.data(), 4 * L.akc.size());
-    put(D.ak_val, L.akv.data(), 8 * L.akv.size());
-    put(D.pp_col, L.ppc.data(), 4 * L.ppc.size());
-    put(D.pp_val, L.ppv.data(), 8 * L.ppv.size());
-    put(D.pt_row, L.ptc.data(), 4 * L.ptc.size());
-    put(D.pt_val, L.ptv.data(), 8 * L.ptv.size());
-    put(D.lev_ptr, L.lev.data(), 4 * L.lev.size());
-    put(D.chunk_lev, L.clev.data(), 4 * L.clev.size());
-    put(D.pk_row, L.pkr.data(), 4 * L.pkr.size());
-    put(D.pk_col, L.pkc.data(), 4 * L.pkc.size());
-    put(D.pk_val, L.pkv.data(), 8 * L.pkv.size());
-    put(D.pk_diag, L.pkd.data(), 8 * L.pkd.size());
-    put(D.b_lvl, L.blv.data(), 8 * L.blv.size());
-    put(D.b, P.b, 8 * n);
-    put(D.x0, P.x0, 8 * n);
+    put(D.a_raw, P.A_data, 8 * (size_t)P.A_nnz);
+    put(D.p_raw, P.P_data, 8 * (size_t)P.P_nnz);
+    put(D.b, P.b, 8 * (size_t)P.n);
+    put(D.x0, P.x0, 8 * (size_t)P.n);
   });
   const auto t_filled = std::chrono::steady_clock::now();
   char* arena = static_cast<char*>(scratch(total, 11));
@@ -1876,7 +2577,11 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
   const auto t_packed = std::chrono::steady_clock::now();
   MLAMG_HIP(hipMemcpyAsync(arena, hb, in_bytes, hipMemcpyHostToDevice, s));
   const BDesc* dd = reinterpret_cast<const BDesc*>(arena + desc_off);
-  hipLaunchKernelGGL(k_amg2v_setup, dim3((unsigned)count), dim3(kBT), lds_setup, s, dd, arena);
+  hipLaunchKernelGGL(k_amg2v_setup, dim3((unsigned)count), dim3(kBT), lds_setup, s, dd, arena, 0);
+  if (any_band) {  // band factors, then Gauss-Jordan for any that met a non-positive pivot
+    hipLaunchKernelGGL(k_amg2v_band, dim3((unsigned)count), dim3(kBT), lds_band, s, dd, arena);
+    hipLaunchKernelGGL(k_amg2v_setup, dim3((unsigned)count), dim3(kBT), lds_setup, s, dd, arena, 1);
+  }
   if (ext_coarse) {
     const int nc = desc[0].nc;
     const int R = std::max(1, std::min(64, (int)((size_t)128 * 1024 / (8 * (size_t)nc))));
@@ -1895,7 +2600,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       MLAMG_HIP(hipMemcpyAsync(arena + desc_off, hb + desc_off, sizeof(BDesc),
                                hipMemcpyHostToDevice, s));
       MLAMG_HIP(hipStreamSynchronize(s));
-      hipLaunchKernelGGL(k_amg2v_setup, dim3(1), dim3(kBT), lds_setup, s, dd, arena);
+      hipLaunchKernelGGL(k_amg2v_setup, dim3(1), dim3(kBT), lds_setup, s, dd, arena, 0);
     }
   }
   if (batch_ext) {
@@ -1926,7 +2631,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
                                hipMemcpyHostToDevice, s));
       MLAMG_HIP(hipStreamSynchronize(s));
       hipLaunchKernelGGL(k_amg2v_setup, dim3((unsigned)count), dim3(kBT), lds_setup, s, dd,
-                         arena);
+                         arena, 0);
     }
   }
   if (phased) {
@@ -1955,7 +2660,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
     // mode-1 problems (one-workgroup inverse Cholesky factor) need the second, L^-T, pass
     bool two_pass = false;
     for (int q = 0; q < count; ++q)
-      two_pass = two_pass || (plans[q].spd && desc[q].setup_mode == 0);
+      two_pass = two_pass || (spd[q] && desc[q].setup_mode == 0);
     MLAMG_HIP(hipMemsetAsync(arena + done_off, 0, sizeof(int32_t), s));
     const int total_a = max_iter + 1;
     // per host thread: two pinned done-count slots and their events (freed at thread exit)
@@ -2036,7 +2741,7 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
                    "(%s) %.3f ms (panels %.3f, updates %.3f), smoothing (%s) %.3f ms, rest of "
                    "cycles %.3f ms (coarse solve %.3f ms)\n",
                    q, (long long)P.n, (long long)P.n_c, st[0], ts[0] * 1e-5,
-                   st[2] == 1 ? "cholesky" : "gauss-jordan", 
+                   st[2] == 2 ? "band cholesky" : st[2] == 1 ? "cholesky" : "gauss-jordan",
                    (ts[1] + ts[4] + ts[5]) * 1e-5, ts[4] * 1e-5, ts[5] * 1e-5,
                    D.gs_rw ? "one wave" : "workgroup", ts[2] * 1e-5, (ts[3] + ts[6]) * 1e-5,
                    ts[6] * 1e-5);

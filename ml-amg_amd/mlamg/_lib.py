@@ -11,6 +11,7 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
 import torch  # noqa: F401  (must be loaded before the HIP library, see module doc)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -58,6 +59,12 @@ class Amg2vProblem(ctypes.Structure):
                 ("b", ctypes.c_void_p), ("x0", ctypes.c_void_p),
                 ("x_out", ctypes.c_void_p), ("err_out", ctypes.c_void_p),
                 ("iters_out", ctypes.c_int32), ("status_out", ctypes.c_int32)]
+
+
+# the same record as a numpy dtype: a batch's problem list is filled column-wise
+AMG2V_DTYPE = np.dtype([(name, {ctypes.c_int64: "<i8", ctypes.c_void_p: "<u8",
+                                ctypes.c_int32: "<i4"}[t]) for name, t in Amg2vProblem._fields_])
+assert AMG2V_DTYPE.itemsize == ctypes.sizeof(Amg2vProblem)
 
 
 # name -> (restype, argtypes); every symbol of include/mlamg.h

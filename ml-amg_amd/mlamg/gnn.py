@@ -332,13 +332,16 @@ class FullAggNet(nn.Module):
         lookup (ns/lib/graph.py:83). "parallel" runs the same distances with the multi-workgroup
         order-independent Bellman-Ford (graph.hip k_bf_sweep, on C^T so the direction is
         pyamg's): nearest seeds equal pyamg's whenever shortest paths are unique, ties go to the
-        smallest seed id, unreached nodes get no aggregate. x: node features replacing the
+        smallest seed id, unreached nodes get no aggregate. "pyamg64": pyamg's sweeps in float64
+        on the widened weights (what a pyamg build binding only double computes; the pyamg
+        version is unpinned). x: node features replacing the
         reference graph's constant 1/n (graph_from_matrix_basic, ns/model/data.py:22-31) —
         not in the reference's signature; a test hook for well-conditioned inputs."""
         from .graph import (aggregate_op_device, bellman_ford_device, bellman_ford_pyamg_device,
                             labels_to_columns)
-        if aggregation not in ("pyamg", "parallel"):
-            raise ValueError(f"aggregation must be 'pyamg' or 'parallel', got {aggregation!r}")
+        if aggregation not in ("pyamg", "pyamg64", "parallel"):
+            raise ValueError("aggregation must be 'pyamg', 'pyamg64' or 'parallel', got "
+                             f"{aggregation!r}")
         A = sp.csr_matrix(A)
         m = A.shape[0]
         k = int(np.ceil(alpha * m))
@@ -351,8 +354,8 @@ class FullAggNet(nn.Module):
         _, bf_edges = self.CNet.run(g)
         C = g.csr(bf_edges)
         seeds = top_k.to(torch.int32)
-        if aggregation == "pyamg":
-            _, lab, _ = bellman_ford_pyamg_device(C, seeds)
+        if aggregation != "parallel":
+            _, lab, _ = bellman_ford_pyamg_device(C, seeds, fp64=aggregation == "pyamg64")
             if bool((lab < 0).any()):
                 raise KeyError(-1)
         else:

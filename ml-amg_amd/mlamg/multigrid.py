@@ -270,22 +270,45 @@ def _batch_limits():
     return _BATCH_LIMITS
 
 
-def _host_problem(A, P, b, x):
-    """Host CSR / vector arrays of one amg_2_v problem in the layout the batched kernel takes
-    (int32 indices, fp64 values, duplicate-free rows in their stored order)."""
+_CSR_TYPES = (sp.csr_matrix,) + ((sp.csr_array,) if hasattr(sp, "csr_array") else ())
+_F64, _I32 = np.dtype(np.float64), np.dtype(np.int32)
+
+
+def _fused_arrays(A, P, b, x, max_nc=None):
+    """The fused solver's host arrays of one amg_2_v problem, or None outside its limits:
+    (n, n_c, [A.indptr, A.indices, A.data, P.indptr, P.indices, P.data, b, x]) with int32
+    indices, fp64 values, C-contiguous, A's rows duplicate-free in their stored order.
+    Canonical int32 / fp64 CSR inputs (what the reference's generators produce) are used as
+    they are, without copies."""
     from .sparse import canonical_rows
-    if sp.issparse(A) and sp.issparse(P):
+    if not (sp.issparse(A) and sp.issparse(P)):
+        return None
+    max_n, lim_nc, _ = _batch_limits()
+    max_nc = lim_nc if max_nc is None else min(max_nc, lim_nc)
+    n, m = A.shape
+    n2, nc = P.shape
+    if not (n == m == n2 and 1 <= n <= max_n and 1 <= nc <= max_nc and nc <= n):
+        return None
+    if A.__class__ not in _CSR_TYPES or not A.has_canonical_format:
         A = canonical_rows(A)
-        P = sp.csr_matrix(P) if not sp.isspmatrix_csr(P) else P
-        arrs = []
-        for M in (A, P):
-            arrs.append((np.ascontiguousarray(M.indptr, dtype=np.int32),
-                         np.ascontiguousarray(M.indices, dtype=np.int32),
-                         np.ascontiguousarray(M.data, dtype=np.float64)))
-        bv = np.ascontiguousarray(np.asarray(b, dtype=np.float64).ravel())
-        xv = np.ascontiguousarray(np.asarray(x, dtype=np.float64).ravel())
-        return A.shape, P.shape, arrs, bv, xv
-    return None
+    if P.__class__ not in _CSR_TYPES:
+        P = sp.csr_matrix(P)
+    if A.nnz >= 2**31 or P.nnz >= 2**31:
+        return None
+    arrs = []
+    for v, dt in ((A.indptr, _I32), (A.indices, _I32), (A.data, _F64), (P.indptr, _I32),
+                  (P.indices, _I32), (P.data, _F64)):
+        if v.dtype != dt or not v.flags.c_contiguous:
+            v = np.ascontiguousarray(v, dtype=dt)
+        arrs.append(v)
+    for v in (b, x):
+        if (v.__class__ is not np.ndarray or v.dtype != _F64 or v.ndim != 1
+                or not v.flags.c_contiguous):
+            v = np.ascontiguousarray(np.asarray(v, dtype=np.float64).ravel())
+        if v.size != n:
+            raise ValueError(f"amg_2_v: vector of size {v.size} for a system of {n} rows")
+        arrs.append(v)
+    return n, nc, arrs
 
 
 # Engine choice for engine='auto' (measured on MI355X, profiles/r02/amg2v_timing.json): one
@@ -301,59 +324,57 @@ FUSED_SINGLE_MAX_NC = 2048
 FUSED_BATCH_MAX_NC = 1024
 
 
-def _fused_eligible(A, P, singular, max_nc=None):
-    if singular or not (sp.issparse(A) and sp.issparse(P)):
-        return False
-    max_n, lim_nc, _ = _batch_limits()
-    max_nc = lim_nc if max_nc is None else min(max_nc, lim_nc)
-    n, nc = A.shape[0], P.shape[1]
-    return (A.shape[0] == A.shape[1] == P.shape[0] and 1 <= n <= max_n and 1 <= nc <= max_nc
-            and nc <= n and A.nnz < 2**31 and P.nnz < 2**31)
-
-
-def _amg_2_v_fused(items, pre, post, jacobi_weight, res_tol, error_tol, max_iter, smoother):
-    """Run amg_2_v on every (A, P, b, x) of `items` in ONE device launch (csrc/batch.hip): one
-    workgroup per problem does its Galerkin product, coarse inverse, cycles and tolerance test.
-    Returns a list of (x, conv_factor, err, iters), or None when a problem is outside the
-    kernel's limits (the caller then takes the hierarchy path)."""
-    from ._lib import Amg2vProblem
+def _amg_2_v_fused(prepared, xs, pre, post, jacobi_weight, res_tol, error_tol, max_iter,
+                   smoother):
+    """Run amg_2_v on every problem of `prepared` (_fused_arrays outputs; xs the caller's initial
+    guesses) in ONE device launch (csrc/batch.hip): one workgroup per problem does its Galerkin
+    product, coarse inverse, cycles and tolerance test. Returns a list of (x, conv_factor, err,
+    iters), or None when a problem is outside the kernel's limits (the caller then takes the
+    hierarchy path)."""
+    from ._hostptr import data_ptrs
     tol = res_tol if res_tol is not None else error_tol
-    probs = (Amg2vProblem * len(items))()
-    keep = []
-    outs = []
-    for q, (A, P, b, x) in enumerate(items):
-        hp = _host_problem(A, P, b, x)
-        if hp is None:
-            return None
-        (n, _), (_, nc), ((aip, aij, av), (pip, pij, pv)), bv, xv = hp
-        xo = np.empty(n)
-        eo = np.empty(max(max_iter, 1))
-        keep.append((aip, aij, av, pip, pij, pv, bv, xv))
-        outs.append((xo, eo))
-        pr = probs[q]
-        pr.n, pr.n_c = n, nc
-        pr.A_indptr, pr.A_indices, pr.A_data = aip.ctypes.data, aij.ctypes.data, av.ctypes.data
-        pr.A_nnz = int(aij.size)
-        pr.P_indptr, pr.P_indices, pr.P_data = pip.ctypes.data, pij.ctypes.data, pv.ctypes.data
-        pr.P_nnz = int(pij.size)
-        pr.b, pr.x0 = bv.ctypes.data, xv.ctypes.data
-        pr.x_out, pr.err_out = xo.ctypes.data, eo.ctypes.data
-    rc = _lib.lib.mlamg_amg2v_batch(probs, len(items), 0 if smoother == "gauss_seidel" else 1,
+    count = len(prepared)
+    rec = np.zeros(count, dtype=_lib.AMG2V_DTYPE)  # mlamg_amg2v_problem[count], filled by column
+    # the eight host buffers of every problem, their addresses in one call
+    flat = [a for _, _, arrs in prepared for a in arrs]
+    ptrs = np.empty(8 * count, dtype=np.uint64)
+    data_ptrs(flat, ptrs)
+    ptrs = ptrs.reshape(count, 8)
+    for c, k in enumerate(("A_indptr", "A_indices", "A_data", "P_indptr", "P_indices", "P_data",
+                           "b", "x0")):
+        rec[k] = ptrs[:, c]
+    ns = np.fromiter((p[0] for p in prepared), dtype=np.int64, count=count)
+    rec["n"] = ns
+    rec["n_c"] = np.fromiter((p[1] for p in prepared), dtype=np.int64, count=count)
+    rec["A_nnz"] = np.fromiter((p[2][1].size for p in prepared), dtype=np.int64, count=count)
+    rec["P_nnz"] = np.fromiter((p[2][4].size for p in prepared), dtype=np.int64, count=count)
+    # outputs: one block for every x and one for every history
+    xoff = np.zeros(count + 1, dtype=np.int64)
+    np.cumsum(ns, out=xoff[1:])
+    xbuf = np.empty(int(xoff[-1]))
+    hlen = max(max_iter, 1)
+    ebuf = np.empty((count, hlen))
+    rec["x_out"] = xbuf.ctypes.data + 8 * xoff[:-1]
+    rec["err_out"] = ebuf.ctypes.data + 8 * hlen * np.arange(count, dtype=np.int64)
+    rc = _lib.lib.mlamg_amg2v_batch(rec.ctypes.data, count,
+                                    0 if smoother == "gauss_seidel" else 1,
                                     int(pre), int(post), float(jacobi_weight),
                                     0 if res_tol is not None else 1, float(tol), int(max_iter),
                                     stream_ptr())
+    del flat
     if rc == _lib.MLAMG_EUNSUPPORTED:
         return None
     _lib.check(rc, "mlamg_amg2v_batch")
     res = []
-    for q, (A, P, b, x) in enumerate(items):
-        xo, eo = outs[q]
-        if probs[q].status_out == 1:  # factorisation failure: multigrid.py:167-170
-            res.append((x, np.float64(1.), np.zeros(max_iter), 0))
+    status = rec["status_out"].tolist()
+    iters = rec["iters_out"].tolist()
+    xo = xoff.tolist()
+    for q in range(count):
+        if status[q] == 1:  # factorisation failure: multigrid.py:167-170
+            res.append((xs[q], np.float64(1.), np.zeros(max_iter), 0))
             continue
-        it = int(probs[q].iters_out)
-        err = eo[:it].copy() if it < max_iter else eo[:max_iter].copy()
-        res.append((xo, conv_factor(err), err, len(err)))
+        err = ebuf[q, :min(iters[q], max_iter)].copy()
+        res.append((xbuf[xo[q]:xo[q + 1]], conv_factor(err), err, len(err)))
     return res
 
 
@@ -385,9 +406,11 @@ def amg_2_v(A, P, b, x,
         raise ValueError(f"unknown smoother {smoother!r}")
     if engine not in ("auto", "fused", "hierarchy"):
         raise ValueError(f"unknown engine {engine!r}")
-    if engine != "hierarchy" and _fused_eligible(
-            A, P, singular, None if engine == "fused" else FUSED_SINGLE_MAX_NC):
-        out = _amg_2_v_fused([(A, P, b, x)], pre_smoothing_steps, post_smoothing_steps,
+    prep = None
+    if engine != "hierarchy" and not singular:
+        prep = _fused_arrays(A, P, b, x, None if engine == "fused" else FUSED_SINGLE_MAX_NC)
+    if prep is not None:
+        out = _amg_2_v_fused([prep], [x], pre_smoothing_steps, post_smoothing_steps,
                              jacobi_weight, res_tol, error_tol, max_iter, smoother)
         if out is not None:
             return out[0]
@@ -448,12 +471,18 @@ def amg_2_v_batch(problems, workers=8, **kw):
         opts.update({k: v for k, v in kw.items() if k in opts})
         if opts["res_tol"] is None and opts["error_tol"] is None:
             raise RuntimeError('One of res_tol or error_tol must be set!')
-        idx = [i for i, (A, P, b, x) in enumerate(problems)
-               if _fused_eligible(A, P, opts["singular"],
-                                  None if engine == "fused" else FUSED_BATCH_MAX_NC)]
+        idx, prepared = [], []
+        if not opts["singular"]:
+            lim = None if engine == "fused" else FUSED_BATCH_MAX_NC
+            for i, (A, P, b, x) in enumerate(problems):
+                h = _fused_arrays(A, P, b, x, lim)
+                if h is not None:
+                    idx.append(i)
+                    prepared.append(h)
         results = [None] * len(problems)
         if idx:
-            out = _amg_2_v_fused([problems[i] for i in idx], opts["pre_smoothing_steps"],
+            out = _amg_2_v_fused(prepared, [problems[i][3] for i in idx],
+                                 opts["pre_smoothing_steps"],
                                  opts["post_smoothing_steps"], opts["jacobi_weight"],
                                  opts["res_tol"], opts["error_tol"], opts["max_iter"],
                                  opts["smoother"])

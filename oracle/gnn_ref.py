@@ -119,12 +119,13 @@ def aggnet(mod, g, k):
 
 
 @torch.no_grad()
-def full_forward(net, A, alpha, x=None):
+def full_forward(net, A, alpha, x=None, bf_dtype=np.float32):
     """FullAggNet.forward (agg_interp.py:458-486) restated on a module's parameters: AggNet
     scores and top-k seeds, CNet edge weights C (sp.coo_matrix over the graph's edges, :469-471),
     pyamg 4.x bellman_ford(C, top_k) (restated.pyamg_bellman_ford, the oracle's C restatement),
     nearest_center_to_agg (dict lookup: KeyError on an unreached node), PNet on
-    graph_from_matrix(A, Agg) and P = P_hat Agg. x replaces the constant 1/n node input.
+    graph_from_matrix(A, Agg) and P = P_hat Agg. x replaces the constant 1/n node input;
+    bf_dtype the Bellman-Ford arithmetic (float32: the weights' dtype; float64 widened).
     Returns (Agg scipy CSR n x k, P scipy CSR, C scipy CSR, top_k tensor, scores tensor)."""
     from . import restated
     A = sp.csr_matrix(A)
@@ -138,7 +139,7 @@ def full_forward(net, A, alpha, x=None):
     _, bfe = mpnn(net.CNet, g)
     ei = g.edge_index.numpy()
     C = sp.coo_matrix((bfe.reshape(-1).numpy(), (ei[0], ei[1])), shape=(m, m))
-    _, nearest, _ = restated.pyamg_bellman_ford(C, top_k.numpy())
+    _, nearest, _ = restated.pyamg_bellman_ford(C, top_k.numpy(), dtype=bf_dtype)
     pos = {int(s): t for t, s in enumerate(top_k.tolist())}
     col = np.array([pos[int(c)] for c in nearest], dtype=np.int64)
     Agg = sp.csr_matrix((np.ones(m), (np.arange(m), col)), shape=(m, len(pos)))

@@ -259,36 +259,40 @@ int lloyd_cluster(int64_t n, const int32_t* ip, const int32_t* ij, const double*
  * each sweep visits rows 0..n-1 in order and, in place, takes the first strictly smaller
  * w_ij + d_j over the row's stored entries (and the nearest seed of that j); sweeps repeat
  * until a sweep leaves every distance unchanged. Returns the number of sweeps (>= 1). */
-int pyamg_bellman_ford(int64_t n, const int32_t* ip, const int32_t* ij, const float* w,
-                       const int32_t* seeds, int64_t k, float* dist, int32_t* nearest) {
-  for (int64_t i = 0; i < n; ++i) {
-    dist[i] = FLT_MAX;
-    nearest[i] = -1;
+/* in the graph's dtype: float (the CNet weights as pyamg 4.x receives them) or double (a
+ * pyamg build that binds only double would widen them first) */
+#define PYAMG_BF(NAME, T, TMAX)                                                                \
+  int NAME(int64_t n, const int32_t* ip, const int32_t* ij, const T* w, const int32_t* seeds,  \
+           int64_t k, T* dist, int32_t* nearest) {                                             \
+    for (int64_t i = 0; i < n; ++i) {                                                          \
+      dist[i] = TMAX;                                                                          \
+      nearest[i] = -1;                                                                         \
+    }                                                                                          \
+    for (int64_t s = 0; s < k; ++s) {                                                          \
+      dist[seeds[s]] = 0;                                                                      \
+      nearest[seeds[s]] = seeds[s];                                                            \
+    }                                                                                          \
+    int sweeps = 0, changed = 1;                                                               \
+    while (changed) {                                                                          \
+      changed = 0;                                                                             \
+      for (int64_t i = 0; i < n; ++i) {                                                        \
+        T xi = dist[i];                                                                        \
+        int32_t zi = nearest[i];                                                               \
+        for (int32_t jj = ip[i]; jj < ip[i + 1]; ++jj) {                                       \
+          const int32_t j = ij[jj];                                                            \
+          const T d = w[jj] + dist[j];                                                         \
+          if (d < xi) {                                                                        \
+            xi = d;                                                                            \
+            zi = nearest[j];                                                                   \
+          }                                                                                    \
+        }                                                                                      \
+        if (xi != dist[i]) changed = 1;                                                        \
+        dist[i] = xi;                                                                          \
+        nearest[i] = zi;                                                                       \
+      }                                                                                        \
+      ++sweeps;                                                                                \
+    }                                                                                          \
+    return sweeps;                                                                             \
   }
-  for (int64_t s = 0; s < k; ++s) {
-    dist[seeds[s]] = 0.0f;
-    nearest[seeds[s]] = seeds[s];
-  }
-  int sweeps = 0;
-  int changed = 1;
-  while (changed) {
-    changed = 0;
-    for (int64_t i = 0; i < n; ++i) {
-      float xi = dist[i];
-      int32_t zi = nearest[i];
-      for (int32_t jj = ip[i]; jj < ip[i + 1]; ++jj) {
-        const int32_t j = ij[jj];
-        const float d = w[jj] + dist[j];
-        if (d < xi) {
-          xi = d;
-          zi = nearest[j];
-        }
-      }
-      if (xi != dist[i]) changed = 1;
-      dist[i] = xi;
-      nearest[i] = zi;
-    }
-    ++sweeps;
-  }
-  return sweeps;
-}
+PYAMG_BF(pyamg_bellman_ford, float, FLT_MAX)
+PYAMG_BF(pyamg_bellman_ford_f64, double, DBL_MAX)

@@ -34,8 +34,9 @@ def lib():
         L.ref_bellman_ford_torch.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
         L.ref_bellman_ford_torch.restype = ctypes.c_int
         L.canon_bellman_ford.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
-        L.pyamg_bellman_ford.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
-        L.pyamg_bellman_ford.restype = ctypes.c_int
+        for f in (L.pyamg_bellman_ford, L.pyamg_bellman_ford_f64):
+            f.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
+            f.restype = ctypes.c_int
         L.vec_matvec.argtypes = [i64, vp, vp, vp, vp, vp]
         L.lloyd_cluster.argtypes = [i64, vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int, vp, vp,
                                     ctypes.c_int]
@@ -248,21 +249,23 @@ def canon_bellman_ford(C, seeds):
     return d, lab
 
 
-def pyamg_bellman_ford(G, seeds):
+def pyamg_bellman_ford(G, seeds, dtype=None):
     """pyamg 4.x graph.bellman_ford(G, seeds) as ns/model/agg_interp.py:471-475 calls it: G a
-    scipy COO/CSR of float32 weights (asgraph -> csr_matrix: duplicates summed, rows sorted),
-    amg_core sweeps in float32. Returns (distances float32, nearest_seed int32 seed node id or
-    -1, sweeps)."""
+    scipy COO/CSR (asgraph -> csr_matrix: duplicates summed, rows sorted), amg_core sweeps in
+    the graph's dtype (float32 for the CNet weights; dtype=np.float64 widens them first).
+    Returns (distances, nearest_seed int32 seed node id or -1, sweeps)."""
     G = sp.csr_matrix(G)
     G.sum_duplicates()
+    dt = np.dtype(dtype or (np.float64 if G.dtype == np.float64 else np.float32))
     ip = np.ascontiguousarray(G.indptr, dtype=np.int32)
     ij = np.ascontiguousarray(G.indices, dtype=np.int32)
-    w = np.ascontiguousarray(G.data, dtype=np.float32)
+    w = np.ascontiguousarray(G.data, dtype=dt)
     s = np.ascontiguousarray(seeds, dtype=np.int32)
     n = G.shape[0]
-    d = np.empty(n, dtype=np.float32)
+    d = np.empty(n, dtype=dt)
     z = np.empty(n, dtype=np.int32)
-    sweeps = lib().pyamg_bellman_ford(n, _p(ip), _p(ij), _p(w), _p(s), len(s), _p(d), _p(z))
+    f = lib().pyamg_bellman_ford_f64 if dt == np.float64 else lib().pyamg_bellman_ford
+    sweeps = f(n, _p(ip), _p(ij), _p(w), _p(s), len(s), _p(d), _p(z))
     return d, z, sweeps
 
 

@@ -22,12 +22,15 @@ def _problems(ml, oracle, count):
     return out
 
 
+@pytest.mark.parametrize("ext", (False, True))
 @pytest.mark.parametrize("smoother", ("gauss_seidel", "jacobi"))
-def test_batch_equals_sequential(oracle, smoother, monkeypatch):
-    # single calls with n_c > 300 factor the coarse operator device-wide and run phased cycles
-    # (own roundings, see test_fused_single_device_wide_coarse); here both sides take the
-    # one-workgroup path
-    monkeypatch.setenv("MLAMG_BATCH_NO_EXT", "1")
+def test_batch_equals_sequential(oracle, smoother, ext, monkeypatch):
+    """Every problem of a batch equals its own single call bit for bit. ext=True (the default
+    engine): problems with n_c > 300 take the device-wide coarse factor both alone and in the
+    batch (the batch then runs phased; the others keep the one-workgroup factor, chosen by their
+    own n_c); ext=False: everything on the one-workgroup path."""
+    if not ext:
+        monkeypatch.setenv("MLAMG_BATCH_NO_EXT", "1")
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -133,6 +136,107 @@ def test_fused_batch_mixed_sizes_bitwise_single(oracle, monkeypatch):
     bat = ml.multigrid.amg_2_v_batch(probs, res_tol=1e-10)
     for i, (a, c) in enumerate(zip(one, bat)):
         assert a[3] == c[3] and np.array_equal(a[2], c[2]) and np.array_equal(a[0], c[0]), i
+
+
+@pytest.mark.parametrize("smoother", ("gauss_seidel", "jacobi"))
+def test_shared_shapes_values_differ(oracle, monkeypatch, smoother):
+    """Problems with one sparsity pattern and different values (Voronoi jump coefficients, a
+    value-nonsymmetric A on a symmetric pattern, a zero diagonal entry, separate or shared index
+    arrays): the batch analyses each pattern once and gathers every problem's values on the
+    device. Results equal one call per problem bit for bit, on a first call (patterns analysed),
+    a second (patterns from the cache) and with the cache off."""
+    monkeypatch.setenv("MLAMG_BATCH_NO_EXT", "1")
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import scipy.sparse as sp
+    import mlamg.multigrid
+    import mlamg as ml
+    probs = []
+    for i in range(12):
+        m = (30, 37)[i % 2]
+        A = ml.problems.jump_2d(m, ml.problems.voronoi_jumps(np.random.RandomState(i)))
+        if i % 4 == 1:  # same pattern, values no longer symmetric: Gauss-Jordan coarse inverse
+            A = A.copy()
+            A.data[A.indptr[5] + 1] *= 1.5
+        if i == 6 and smoother == "gauss_seidel":  # a zero diagonal: the sweep skips the row
+            A = A.copy()
+            A.data[(A.indices == 7) & (np.repeat(np.arange(A.shape[0]), np.diff(A.indptr)) == 7)] = 0.0
+        if i % 3 == 2:  # shares its index arrays with the previous problem of its size
+            B = probs[i - 2][0]
+            A = sp.csr_matrix((A.data.copy(), B.indices, B.indptr), shape=A.shape)
+        Agg = ml.problems.box_aggregates_2d(m, m, 3)
+        P, _ = oracle.smoothed_aggregation_jacobi(ml.problems.poisson_2d_5pt(m), Agg,
+                                                  omega=2.0 / 3.0)
+        x0 = np.random.RandomState(50 + i).randn(A.shape[0])
+        probs.append((A, P, np.zeros(A.shape[0]), x0))
+    one = [ml.multigrid.amg_2_v(A, P, b, x, res_tol=1e-10, smoother=smoother, engine="fused",
+                                max_iter=60) for A, P, b, x in probs]
+    runs = [ml.multigrid.amg_2_v_batch(probs, res_tol=1e-10, smoother=smoother, max_iter=60),
+            ml.multigrid.amg_2_v_batch(probs, res_tol=1e-10, smoother=smoother, max_iter=60)]
+    monkeypatch.setenv("MLAMG_BATCH_NO_SHAPE_CACHE", "1")
+    runs.append(ml.multigrid.amg_2_v_batch(probs, res_tol=1e-10, smoother=smoother, max_iter=60))
+    for r, bat in enumerate(runs):
+        for i, (a, c) in enumerate(zip(one, bat)):
+            assert a[3] == c[3] and np.array_equal(a[2], c[2]), (r, i)
+            assert np.array_equal(a[0], c[0]), (r, i)
+    # and the values matter: two problems of one pattern converge differently
+    assert not np.array_equal(one[0][2], one[2][2])
+
+
+@pytest.mark.parametrize("smoother", ("gauss_seidel", "jacobi"))
+def test_band_coarse_solve(oracle, monkeypatch, smoother):
+    """Narrow-banded coarse operators (aggregates numbered along the grid: half-bandwidth
+    kx + 1 <= 63) take the banded Cholesky factor and band substitutions: the same iteration
+    counts as the dense coarse inverse (MLAMG_BATCH_NO_BAND) and as the oracle (SuperLU), and
+    histories within fp64 rounding of both. Permuted aggregate numbers (wide band) keep the
+    dense path; a symmetric indefinite A (the band factor meets a negative pivot) falls back
+    to Gauss-Jordan, bitwise the dense path's fallback."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import scipy.sparse as sp
+    import mlamg.multigrid
+    import mlamg as ml
+    cases = []
+    for m, box, perm in ((20, 2, False), (45, 3, False), (64, 3, False), (96, 3, False),
+                         (40, 3, True)):
+        A = ml.problems.poisson_2d_5pt(m)
+        Agg = ml.problems.box_aggregates_2d(m, m, box)
+        if perm:
+            Agg = sp.csr_matrix(Agg[:, np.random.RandomState(m).permutation(Agg.shape[1])])
+        P, _ = oracle.smoothed_aggregation_jacobi(A, Agg, omega=2.0 / 3.0)
+        x0 = np.random.RandomState(m).randn(A.shape[0])
+        cases.append((A, P, np.zeros(A.shape[0]), x0 / np.linalg.norm(x0)))
+    kw = dict(res_tol=1e-10, smoother=smoother, max_iter=100)
+    band = [ml.multigrid.amg_2_v(*c, engine="fused", **kw) for c in cases]
+    bat = ml.multigrid.amg_2_v_batch(cases, **kw)
+    monkeypatch.setenv("MLAMG_BATCH_NO_BAND", "1")
+    dense = [ml.multigrid.amg_2_v(*c, engine="fused", **kw) for c in cases]
+    monkeypatch.delenv("MLAMG_BATCH_NO_BAND")
+    for i, c in enumerate(cases):
+        xr, cr, er, ir = oracle.amg_2_v(*c, jacobi_weight=0.666, **kw)
+        assert band[i][3] == dense[i][3] == ir, (i, band[i][3], dense[i][3], ir)
+        assert np.allclose(band[i][2], er, rtol=1e-10, atol=1e-14 * er[0]), i
+        assert np.allclose(band[i][2], dense[i][2], rtol=1e-10, atol=1e-14 * er[0]), i
+        scale = np.abs(xr).max()
+        assert np.abs(band[i][0] - xr).max() <= 1e-9 * scale + 1e-14, i
+        # the batch is bitwise its single calls
+        assert bat[i][3] == band[i][3] and np.array_equal(bat[i][2], band[i][2]), i
+        assert np.array_equal(bat[i][0], band[i][0]), i
+    # symmetric indefinite: the band factor fails, Gauss-Jordan takes over (both paths alike)
+    A = (ml.problems.poisson_2d_5pt(30) - 1.0 * sp.eye(900)).tocsr()
+    A.sort_indices()
+    P, _ = oracle.smoothed_aggregation_jacobi(ml.problems.poisson_2d_5pt(30),
+                                              ml.problems.box_aggregates_2d(30, 30, 3),
+                                              omega=2.0 / 3.0)
+    c = (A, P, np.zeros(900), np.random.RandomState(1).randn(900))
+    kw2 = dict(res_tol=1e-10, smoother=smoother, max_iter=20)
+    a = ml.multigrid.amg_2_v(*c, engine="fused", **kw2)
+    monkeypatch.setenv("MLAMG_BATCH_NO_BAND", "1")
+    d = ml.multigrid.amg_2_v(*c, engine="fused", **kw2)
+    assert a[3] == d[3] and np.array_equal(a[2], d[2], equal_nan=True)
+    assert np.array_equal(a[0], d[0], equal_nan=True)
 
 
 def test_fused_edge_cases(oracle):

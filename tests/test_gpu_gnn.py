@@ -117,7 +117,7 @@ def _to_csr(T, shape):
     return sp.csr_matrix((T.values().cpu().numpy(), T.indices().cpu().numpy()), shape=shape)
 
 
-@pytest.mark.parametrize("aggregation", ("pyamg", "parallel"))
+@pytest.mark.parametrize("aggregation", ("pyamg", "pyamg64", "parallel"))
 def test_fullaggnet_forward(torch_cuda, oracle, aggregation):
     """FullAggNet.forward on the device: k seeds, every node in one aggregate, the aggregates
     those of the aggregation rule on the device's own CNet weights C — "pyamg": pyamg 4.x
@@ -139,8 +139,10 @@ def test_fullaggnet_forward(torch_cuda, oracle, aggregation):
     assert np.all(np.diff(Agg.indptr) <= 1)
     Cs = _to_csr(C, (n, n))
     seeds = top_k.cpu().numpy()
-    if aggregation == "pyamg":
-        _, lab, _ = oracle.pyamg_bellman_ford(Cs.astype(np.float32), seeds)
+    if aggregation != "parallel":
+        _, lab, _ = oracle.pyamg_bellman_ford(
+            Cs.astype(np.float32), seeds,
+            dtype=np.float64 if aggregation == "pyamg64" else np.float32)
         assert np.all(lab >= 0) and np.all(np.diff(Agg.indptr) == 1)
     else:
         _, lab = oracle.canon_bellman_ford(Cs.T.tocsr().astype(np.float64), seeds)
@@ -158,7 +160,8 @@ def test_fullaggnet_forward(torch_cuda, oracle, aggregation):
     assert np.abs(Pd - P_ref).max() <= 1e-6 * max(np.abs(P_ref).max(), 1e-30)
 
 
-def test_fullaggnet_forward_end_to_end(torch_cuda):
+@pytest.mark.parametrize("aggregation", ("pyamg", "pyamg64"))
+def test_fullaggnet_forward_end_to_end(torch_cuda, aggregation):
     """The whole FullAggNet.forward (agg_interp.py:458-486) on the device against
     oracle/gnn_ref.full_forward — the torch restatement of every layer plus the oracle's
     pyamg.graph.bellman_ford — at the same seeded weights, on a well-conditioned non-constant
@@ -191,8 +194,9 @@ def test_fullaggnet_forward_end_to_end(torch_cuda):
         srt = torch.sort(raw, descending=True).values
         assert float(srt[k - 1] - srt[k]) > 1e-4 * float(srt.abs().max()), "ill-conditioned seed"
         xx = gnn_ref.topk_vec(raw, k)
-    Agg_r, P_r, C_r, top_r, s_r = gnn_ref.full_forward(net, A, alpha, x=x)
-    agg, P, C, top_k, scores = netd.forward(A, alpha, x=x)
+    bf_dtype = np.float64 if aggregation == "pyamg64" else np.float32
+    Agg_r, P_r, C_r, top_r, s_r = gnn_ref.full_forward(net, A, alpha, x=x, bf_dtype=bf_dtype)
+    agg, P, C, top_k, scores = netd.forward(A, alpha, x=x, aggregation=aggregation)
     assert torch.equal(top_k.cpu(), top_r) and torch.equal(scores.cpu(), s_r)
     Cd = _to_csr(C, (n, n))
     assert np.array_equal(Cd.indptr, C_r.indptr) and np.array_equal(Cd.indices, C_r.indices)
@@ -215,10 +219,7 @@ def test_bellman_ford_pyamg_device(torch_cuda, oracle):
 
     def check(G, seeds, dtype=np.float32):
         d, z = graph.bellman_ford(G, seeds)
-        if dtype == np.float32:
-            dr, zr, _ = oracle.pyamg_bellman_ford(G, seeds)
-        else:
-            dr, zr = _pyamg_bf_f64(G, seeds)
+        dr, zr, _ = oracle.pyamg_bellman_ford(G, seeds)
         assert d.dtype == dtype and np.array_equal(d, dr) and np.array_equal(z, zr)
         return d, z
 
@@ -249,27 +250,3 @@ def test_bellman_ford_pyamg_device(torch_cuda, oracle):
     G = sp.coo_matrix((rs.randint(0, 3, B.nnz).astype(np.float32), (B.row, B.col)), shape=B.shape)
     check(G, np.sort(rs.permutation(B.shape[0])[:60]))
 
-
-def _pyamg_bf_f64(G, seeds):
-    """pyamg 4.x bellman_ford in float64 (small graphs): the same sweeps as the oracle's float32
-    restatement, in the graph's dtype."""
-    G = sp.csr_matrix(G)
-    G.sum_duplicates()
-    n = G.shape[0]
-    x = np.full(n, np.finfo(np.float64).max)
-    z = np.full(n, -1, dtype=np.int32)
-    x[seeds] = 0
-    z[seeds] = seeds
-    ip, ij, w = G.indptr, G.indices, G.data
-    while True:
-        changed = False
-        for i in range(n):
-            xi, zi = x[i], z[i]
-            for q in range(ip[i], ip[i + 1]):
-                d = w[q] + x[ij[q]]
-                if d < xi:
-                    xi, zi = d, z[ij[q]]
-            changed |= xi != x[i]
-            x[i], z[i] = xi, zi
-        if not changed:
-            return x, z

@@ -151,18 +151,18 @@ def test_amg_2_v_singular_driver(golden_singular, oracle, key):
     assert np.array_equal(x, g[f"{key}_x"])
 
 
-def _pyamg_bf_literal(G, seeds):
+def _pyamg_bf_literal(G, seeds, dt=np.float32):
     """pyamg 4.x graph.bellman_ford + amg_core.bellman_ford, transcribed line by line (numpy
     float32 scalars: every sum rounds to float32 like the <int, float> instantiation)."""
     import scipy.sparse as sp
     G = sp.csr_matrix(G)
     G.sum_duplicates()
     n = G.shape[0]
-    x = np.full(n, np.finfo(np.float32).max, dtype=np.float32)
+    x = np.full(n, np.finfo(dt).max, dtype=dt)
     x[seeds] = 0
     z = np.full(n, -1, dtype=np.int32)
     z[seeds] = seeds
-    w = G.data.astype(np.float32)
+    w = G.data.astype(dt)
     sweeps = 0
     while True:
         old = x.copy()
@@ -170,7 +170,7 @@ def _pyamg_bf_literal(G, seeds):
             xi, zi = x[i], z[i]
             for jj in range(G.indptr[i], G.indptr[i + 1]):
                 j = G.indices[jj]
-                d = np.float32(w[jj] + x[j])
+                d = dt(w[jj] + x[j])
                 if d < xi:
                     xi, zi = d, z[j]
             x[i], z[i] = xi, zi
@@ -205,6 +205,10 @@ def test_oracle_pyamg_bellman_ford(oracle, kind):
     d, z, sw = oracle.pyamg_bellman_ford(G, seeds)
     dl, zl, swl = _pyamg_bf_literal(G, seeds)
     assert np.array_equal(d, dl) and np.array_equal(z, zl) and sw == swl
+    d64, z64, sw64 = oracle.pyamg_bellman_ford(G, seeds, dtype=np.float64)
+    dl, zl, swl = _pyamg_bf_literal(G, seeds, np.float64)
+    assert d64.dtype == np.float64
+    assert np.array_equal(d64, dl) and np.array_equal(z64, zl) and sw64 == swl
     # canon_bellman_ford pushes along C[i, j] (i -> j); pyamg pulls d_i = min_j G[i, j] + d_j
     dc, _ = oracle.canon_bellman_ford(sp.csr_matrix(G).T.tocsr().astype(np.float64), seeds)
     reach = z >= 0
