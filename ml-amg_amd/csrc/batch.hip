@@ -562,6 +562,11 @@ __device__ void gather_values(const BDesc& D, char* arena, int tid) {
 // Held, like the dense paths, to fp64 rounding of a direct solve; chosen per problem from its own
 // pattern, so a problem's results do not depend on its batch.
 constexpr int kBandMax = 63;  // half-bandwidth limit: rows (j, j + b] within the 64 lanes
+// coarse size limit: the substitutions run on one wave, ~45 ns per row and direction; a single
+// call with a larger coarse operator is faster with the device-wide dense factor and its coarse
+// solve spread over the CUs (128^2: 13 vs 26 ms). Every batch-eligible size (n_c <= 1024, the
+// Python engine's FUSED_BATCH_MAX_NC) is below it, so batches and single calls choose alike.
+constexpr int kBandMaxNc = 1024;
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const long long x = __double_as_longlong(v);
@@ -591,80 +596,100 @@ using as_cptr = const __attribute__((address_space(AS))) double*;
 constexpr int kBandPad = 32;  // zero steps before and after the band solve's lane layout
 __device__ __forceinline__ int64_t band_at(int j, int l) { return (int64_t)(j + kBandPad) * 64 + l; }
 
+// LDS ordering between the lanes of one wave: its LDS operations complete in issue order, so a
+// wavefront-scope fence (no wait on global memory: prefetches and stores stay in flight) only
+// keeps the compiler from moving LDS accesses across it
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One workgroup, a (row, column) pair of column j's update per thread: rings of power-of-two
+// sizes (slot = index & mask, no integer division), >= b + 2 rows and diagonals, rows stored
+// with an odd stride (conflict-free LDS columns).
 __device__ bool band_chol(const double* __restrict__ AH_, int nc, int b, double* lds,
                           double* __restrict__ F_, double* __restrict__ G_,
                           double* __restrict__ RI_, int tid) {
   const as_cptr<1> AH = (as_cptr<1>)AH_;
   const as_ptr<1> F = (as_ptr<1>)F_, G = (as_ptr<1>)G_, RI = (as_ptr<1>)RI_;
-  const int w = b + 1, wd = b + 2;
+  int w = 1;
+  while (w < b + 2) w <<= 1;
+  const int m = w - 1, ws = w + 1;
+  const as_ptr<3> off = (as_ptr<3>)lds;  // w rows of stride ws
+  const as_ptr<3> dg = off + w * ws;     // w
   // zeros outside the band, and on the padding steps
   for (int64_t q = tid; q < (int64_t)(nc + 2 * kBandPad) * 64; q += kBT) {
     F[q] = 0.0;
     G[q] = 0.0;
   }
   for (int q = tid; q < nc + 2 * kBandPad; q += kBT) RI[q] = 0.0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  const as_ptr<3> off = (as_ptr<3>)lds;  // w x w
-  const as_ptr<3> dg = off + w * w;      // wd
-  for (int q = tid; q < w * w; q += kBT) {
-    const int i = q / w, k = q - (q / w) * w;
-    if (i < nc && k < i) off[(i % w) * w + k % w] = AH[(int64_t)i * nc + k];
+  for (int q = tid; q < (b + 1) * (b + 1); q += kBT) {
+    const int i = q / (b + 1), k = q - i * (b + 1);
+    if (i < nc && k < i) off[(i & m) * ws + (k & m)] = AH[(int64_t)i * nc + k];
   }
-  for (int i = tid; i < w && i < nc; i += kBT) dg[i % wd] = AH[(int64_t)i * nc + i];
+  for (int i = tid; i <= b && i < nc; i += kBT) dg[i & m] = AH[(int64_t)i * nc + i];
   // this thread's pairs (di, dk), 1 <= dk <= di <= b (rows j + di, j + dk): b <= 63 gives at
   // most 2016 pairs, two per thread
   int pdi[2] = {0, 0}, pdk[2] = {0, 0};
   const int npairs = b * (b + 1) / 2;
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    const int p = tid + m * kBT;
+  for (int u = 0; u < 2; ++u) {
+    const int p = tid + u * kBT;
     if (p < npairs) {
       int di = (int)((1.0 + sqrt(1.0 + 8.0 * (double)p)) * 0.5);
       while (di * (di - 1) / 2 > p) --di;
       while (di * (di + 1) / 2 <= p) ++di;
-      pdi[m] = di;
-      pdk[m] = p - di * (di - 1) / 2 + 1;
+      pdi[u] = di;
+      pdk[u] = p - di * (di - 1) / 2 + 1;
     }
   }
-  // entering-row entries of this thread (kk = tid <= b): row j + b + 1, column j + 1 + kk
+  // entering-row entries of this thread (tid <= b): row j + b + 1, column j + 1 + tid
   auto enter_val = [&](int j) -> double {
     const int ni = j + b + 1, k = j + 1 + tid;
     return tid <= b && ni < nc ? AH[(int64_t)ni * nc + (k < ni ? k : ni)] : 0.0;
   };
   double pre0 = enter_val(0), pre1 = enter_val(1);
   __syncthreads();
-  for (int j = 0; j < nc; ++j) {
-    const double d = dg[j % wd];
+  auto column = [&](int j, double v) -> bool {
+    const double d = dg[j & m];
     if (!(d > 0.0)) return false;  // every thread read the same pivot
     const double ljj = sqrt(d), r = 1.0 / ljj;
-    const int cj = j % w;
+    const int cj = j & m;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int di = pdi[m], dk = pdk[m];
+    for (int u = 0; u < 2; ++u) {
+      const int di = pdi[u], dk = pdk[u];
       const int i = j + di, k = j + dk;
       if (di == 0 || i >= nc) continue;
-      const double li = off[(i % w) * w + cj] * r;
+      const double li = off[(i & m) * ws + cj] * r;
       if (dk == di) {
-        dg[i % wd] = dg[i % wd] - li * li;
+        dg[i & m] = dg[i & m] - li * li;
         F[band_at(j, i & 63)] = li * r;
         G[band_at(i, j & 63)] = li;
       } else {
-        const double lk = off[(k % w) * w + cj] * r;
-        off[(i % w) * w + k % w] = off[(i % w) * w + k % w] - li * lk;
+        const double lk = off[(k & m) * ws + cj] * r;
+        off[(i & m) * ws + (k & m)] = off[(i & m) * ws + (k & m)] - li * lk;
       }
     }
     if (tid == 0) RI[j + kBandPad] = r;
-    // the entering row (raw A_H: no column <= j has reached it), loaded two columns ago
+    // the entering row (raw A_H: no column <= j has reached it), loaded two columns before
     const int ni = j + b + 1;
-    const double v = (j & 1) ? pre1 : pre0;
     if (ni < nc && tid <= b) {
       const int k = j + 1 + tid;
-      if (k < ni) off[(ni % w) * w + k % w] = v;
-      else dg[ni % wd] = v;
+      if (k < ni) off[(ni & m) * ws + (k & m)] = v;
+      else dg[ni & m] = v;
     }
-    if (j & 1) pre1 = enter_val(j + 2);
-    else pre0 = enter_val(j + 2);
     __syncthreads();
+    return true;
+  };
+  for (int j = 0; j < nc; j += 2) {  // two columns per trip: each prefetch has a column to land
+    const double v0 = pre0;
+    pre0 = enter_val(j + 2);
+    if (!column(j, v0)) return false;
+    if (j + 1 >= nc) break;
+    const double v1 = pre1;
+    pre1 = enter_val(j + 3);
+    if (!column(j + 1, v1)) return false;
   }
   return true;
 }
@@ -2083,7 +2108,11 @@ std::shared_ptr<Pattern> analyse_pattern(const mlamg_amg2v_problem& P, uint64_t 
 size_t chol_lds(int nb, int64_t nc) {
   return (size_t)8 * (2 * nb * (nb + 1) + (size_t)nc * (nb + 1) + (size_t)nb * nc);
 }
-size_t band_lds(int b) { return (size_t)8 * ((size_t)(b + 1) * (b + 1) + (b + 2)); }
+size_t band_lds(int b) {  // band_chol's rings: w x (w + 1) window, w diagonals
+  size_t w = 1;
+  while (w < (size_t)b + 2) w <<= 1;
+  return 8 * (w * (w + 1) + w);
+}
 size_t gj_lds(int b, int64_t nc) { return (size_t)nc * (b + 1) * 8 + 16 * b + (size_t)nc * 12; }
 
 // the structure analysis of one pattern (P already validated)
@@ -2336,7 +2365,8 @@ int mlamg_amg2v_batch(mlamg_amg2v_problem* probs, int count, int smoother, int n
       s = csr_symmetric(P.n, P.A_indptr, P.A_indices, P.A_data);
     }
     sym[q] = s ? 1 : 0;
-    band[q] = s && !no_band && S.band <= kBandMax && band_lds(S.band) <= kBLdsBytes ? 1 : 0;
+    band[q] = s && !no_band && S.band <= kBandMax && S.nc <= kBandMaxNc &&
+              band_lds(S.band) <= kBLdsBytes ? 1 : 0;
   });
   // 4. strategy. A single problem with a large dense coarse operator: the coarse inverse from
   // the device-wide factorisation (dense.hip) and phased cycles, the coarse solve on every CU.
