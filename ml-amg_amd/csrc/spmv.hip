@@ -35,7 +35,16 @@ struct Epi {
   const double* copy_from;
   double* partial;     // RESID: per-block sum of r^2 (nullable)
   const int32_t* done; // nullable: device flag; nonzero -> kernel is a no-op
+  int cached;          // set by launch(): 1 = cached loads of the nonzero stream (see kCachedNnz)
 };
+
+// A level operator (square) of at most kCachedNnz entries (~100 MB in CSR) is read with ordinary
+// (cached) loads, so its stream stays in the 256 MB MALL from its pre-smoothing to its
+// post-smoothing pass (C4 level-3 A: second pass 28 -> 22 us). Everything else — larger streams,
+// and P / R, read once per cycle — uses non-temporal loads, which leave the MALL to the vectors
+// the next kernel reads (cached P_2 / P_3 / R_3 streams measured 1-3 us slower each).
+constexpr int64_t kCachedNnz = 8 << 20;
+
 
 // The per-row operands an epilogue reads, fetched apart from the store so kernels can issue
 // these loads at the start (before the nonzero stream) and keep their latency off the tail.
@@ -151,11 +160,20 @@ __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restri
     constexpr int U = kBlockNnz / kThreads;
     int32_t cc[U];
     double vv[U], xv[U];
+    if (ep.cached) {  // uniform: one unrolled load sequence or the other
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = tid + u * kThreads;
-      cc[u] = e < ne ? __builtin_nontemporal_load(ci + e) : -1;
-      vv[u] = e < ne ? __builtin_nontemporal_load(cv + e) : 0.0;
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kThreads;
+        cc[u] = e < ne ? ci[e] : -1;
+        vv[u] = e < ne ? cv[e] : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kThreads;
+        cc[u] = e < ne ? __builtin_nontemporal_load(ci + e) : -1;
+        vv[u] = e < ne ? __builtin_nontemporal_load(cv + e) : 0.0;
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
@@ -656,14 +674,25 @@ __global__ __launch_bounds__(512) void k_csr_vcan(const int32_t* __restrict__ in
     for (int base = a; base < b; base += 512 * T) {
       int32_t cc[T][J];
       double vv[T][J], xv[T][J];
+      if (ep.cached) {  // uniform: one unrolled load sequence or the other
 #pragma unroll
-      for (int t = 0; t < T; ++t)
+        for (int t = 0; t < T; ++t)
 #pragma unroll
-        for (int j = 0; j < J; ++j) {
-          const int e = base + 512 * t + 64 * (p + Q * j) + lane;
-          cc[t][j] = e < b ? __builtin_nontemporal_load(indices + e) : -1;
-          vv[t][j] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
-        }
+          for (int j = 0; j < J; ++j) {
+            const int e = base + 512 * t + 64 * (p + Q * j) + lane;
+            cc[t][j] = e < b ? indices[e] : -1;
+            vv[t][j] = e < b ? vals[e] : 0.0;
+          }
+      } else {
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int j = 0; j < J; ++j) {
+            const int e = base + 512 * t + 64 * (p + Q * j) + lane;
+            cc[t][j] = e < b ? __builtin_nontemporal_load(indices + e) : -1;
+            vv[t][j] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
+          }
+      }
 #pragma unroll
       for (int t = 0; t < T; ++t)
 #pragma unroll
@@ -813,13 +842,24 @@ __global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restric
   double vv[U], xv[U];
   {
     const size_t eb = (size_t)b * kSrtNnz + tid;
+    if (ep.cached) {  // uniform: one unrolled load sequence or the other
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      w[u] = __builtin_nontemporal_load(pk + eb + u * kSrtThreads);
-      if constexpr (VD)
-        vv[u] = (double)__builtin_nontemporal_load(vi + eb + u * kSrtThreads);  // index for now
-      else
-        vv[u] = __builtin_nontemporal_load(av + eb + u * kSrtThreads);
+      for (int u = 0; u < U; ++u) {
+        w[u] = pk[eb + u * kSrtThreads];
+        if constexpr (VD)
+          vv[u] = (double)vi[eb + u * kSrtThreads];  // index for now
+        else
+          vv[u] = av[eb + u * kSrtThreads];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        w[u] = __builtin_nontemporal_load(pk + eb + u * kSrtThreads);
+        if constexpr (VD)
+          vv[u] = (double)__builtin_nontemporal_load(vi + eb + u * kSrtThreads);  // index for now
+        else
+          vv[u] = __builtin_nontemporal_load(av + eb + u * kSrtThreads);
+      }
     }
   }
   const int r0 = m0.x, r1 = m0.y, nr = r1 - r0;
@@ -1004,11 +1044,20 @@ __global__ __launch_bounds__(kThreads) void k_csr_long(const int32_t* __restrict
     const double* cv = vals + e0;
     int32_t cc[U];
     double vv[U], xv[U];
+    if (ep.cached) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = tid + u * kThreads;
-      cc[u] = e < ne ? __builtin_nontemporal_load(ci + e) : -1;
-      vv[u] = e < ne ? __builtin_nontemporal_load(cv + e) : 0.0;
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kThreads;
+        cc[u] = e < ne ? ci[e] : -1;
+        vv[u] = e < ne ? cv[e] : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kThreads;
+        cc[u] = e < ne ? __builtin_nontemporal_load(ci + e) : -1;
+        vv[u] = e < ne ? __builtin_nontemporal_load(cv + e) : 0.0;
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) xv[u] = cc[u] >= 0 ? x[cc[u]] : 0.0;
@@ -1082,8 +1131,16 @@ static int launch_rowpair(const mlamg_csr* A, const double* x, const Epi& ep, hi
 }
 
 // ---------------------------------------------------------------- launch helpers
+// MLAMG_NO_CACHED_LOADS=1: every nonzero stream non-temporal (A/B runs)
+static bool cached_loads_off() {
+  static const bool off = std::getenv("MLAMG_NO_CACHED_LOADS") != nullptr;
+  return off;
+}
+
 template <int OP, bool NORM>
-static int launch(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+static int launch(const mlamg_csr* A, const double* x, const Epi& ep_in, hipStream_t s) {
+  Epi ep = ep_in;
+  ep.cached = A->n_rows == A->n_cols && A->nnz <= kCachedNnz && !cached_loads_off() ? 1 : 0;
   if (A->vec_width) return launch_vec<OP, NORM>(A, x, ep, s);
   if (A->lg_tile) {
     if (A->lg_nt == 0) return MLAMG_OK;
