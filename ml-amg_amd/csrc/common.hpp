@@ -131,9 +131,11 @@ struct mlamg_csr {
   int32_t* dict_off = nullptr;   // 256 offsets
   double* dict_val = nullptr;    // 256 values
   int32_t dict_n_off = 0, dict_n_val = 0;
-  // CSR-vector format (lane-strided partial sums + butterfly, NOT scipy's order): 0 = off,
-  // else the number of lanes per row (4..64)
+  // CSR-vector format (the canonical 512-virtual-lane order, spmv.hip k_csr_vcan): 0 = off,
+  // else the number of lanes per row (64..512)
   int32_t vec_width = 0;
+  // its column indices as 16-bit copies when n_cols <= 65536 (10 instead of 12 B per nonzero)
+  uint16_t* vec_idx16 = nullptr;
   // optional gather-sorted copy ("sorted" format): row blocks of <= kSrtRows rows and
   // <= kSrtNnz nonzeros whose entries are stored in ascending column order, each packed as
   // (col - srt_base[block]) << kSrtPosBits | slot (its CSR position inside the block)

@@ -235,6 +235,7 @@ void csr_free(mlamg_csr* A) {
   if (A->srt_val) (void)hipFree(A->srt_val);
   if (A->srt_vi) (void)hipFree(A->srt_vi);
   if (A->srt_vtab) (void)hipFree(A->srt_vtab);
+  if (A->vec_idx16) (void)hipFree(A->vec_idx16);
   if (A->rp_pid) (void)hipFree(A->rp_pid);
   if (A->rp_ptr) (void)hipFree(A->rp_ptr);
   if (A->rp_off) (void)hipFree(A->rp_off);

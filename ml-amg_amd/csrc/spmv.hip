@@ -648,9 +648,9 @@ void k_rowpair(const uint8_t* __restrict__ pid,
 #define MLAMG_VCAN_STEPS 1
 #endif
 constexpr int kVcanSteps = MLAMG_VCAN_STEPS;
-template <int Q, int OP, bool NORM>
+template <int Q, int OP, bool NORM, typename IT>
 __global__ __launch_bounds__(512) void k_csr_vcan(const int32_t* __restrict__ indptr,
-                                                  const int32_t* __restrict__ indices,
+                                                  const IT* __restrict__ indices,
                                                   const double* __restrict__ vals,
                                                   int64_t n_rows, const double* __restrict__ x,
                                                   Epi ep) {
@@ -680,7 +680,7 @@ __global__ __launch_bounds__(512) void k_csr_vcan(const int32_t* __restrict__ in
 #pragma unroll
           for (int j = 0; j < J; ++j) {
             const int e = base + 512 * t + 64 * (p + Q * j) + lane;
-            cc[t][j] = e < b ? indices[e] : -1;
+            cc[t][j] = e < b ? (int32_t)indices[e] : -1;
             vv[t][j] = e < b ? vals[e] : 0.0;
           }
       } else {
@@ -689,7 +689,7 @@ __global__ __launch_bounds__(512) void k_csr_vcan(const int32_t* __restrict__ in
 #pragma unroll
           for (int j = 0; j < J; ++j) {
             const int e = base + 512 * t + 64 * (p + Q * j) + lane;
-            cc[t][j] = e < b ? __builtin_nontemporal_load(indices + e) : -1;
+            cc[t][j] = e < b ? (int32_t)__builtin_nontemporal_load(indices + e) : -1;
             vv[t][j] = e < b ? __builtin_nontemporal_load(vals + e) : 0.0;
           }
       }
@@ -725,8 +725,12 @@ template <int OP, bool NORM, int Q>
 static int launch_vcan(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   constexpr int RPB = 8 / Q;
   const unsigned nb = (unsigned)std::max<int64_t>(1, (A->n_rows + RPB - 1) / RPB);
-  hipLaunchKernelGGL((k_csr_vcan<Q, OP, NORM>), dim3(nb), dim3(512), 0, s, A->indptr,
-                     A->indices, A->data, A->n_rows, x, ep);
+  if (A->vec_idx16)
+    hipLaunchKernelGGL((k_csr_vcan<Q, OP, NORM, uint16_t>), dim3(nb), dim3(512), 0, s, A->indptr,
+                       A->vec_idx16, A->data, A->n_rows, x, ep);
+  else
+    hipLaunchKernelGGL((k_csr_vcan<Q, OP, NORM, int32_t>), dim3(nb), dim3(512), 0, s, A->indptr,
+                       A->indices, A->data, A->n_rows, x, ep);
   MLAMG_HIP(hipGetLastError());
   return MLAMG_OK;
 }
@@ -1572,6 +1576,32 @@ __global__ void k_vdict_encode(const double* __restrict__ v, int64_t n, unsigned
   out[e] = (uint8_t)vidx[dict_slot(key, vtab, nullptr, false)];
 }
 
+static void drop_vec16(mlamg_csr* A) {
+  if (A->vec_idx16) (void)hipFree(A->vec_idx16);
+  A->vec_idx16 = nullptr;
+}
+
+__global__ void k_idx16(const int32_t* __restrict__ in, uint16_t* __restrict__ out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (uint16_t)in[i];
+}
+
+// 16-bit column copies for the VECTOR format (n_cols <= 65536; env MLAMG_NO_IDX16 = A/B knob)
+static int build_vec16(mlamg_csr* A, hipStream_t s) {
+  drop_vec16(A);
+  if (A->n_cols > 65536 || A->nnz == 0 || getenv("MLAMG_NO_IDX16")) return MLAMG_OK;
+  uint16_t* d = nullptr;
+  if (hipMalloc(&d, sizeof(uint16_t) * (size_t)A->nnz) != hipSuccess) {
+    (void)hipGetLastError();
+    return MLAMG_OK;  // optional copy: the 32-bit indices serve
+  }
+  hipLaunchKernelGGL(k_idx16, dim3((unsigned)((A->nnz + 255) / 256)), dim3(256), 0, s, A->indices,
+                     d, A->nnz);
+  MLAMG_HIP(hipGetLastError());
+  A->vec_idx16 = d;
+  return MLAMG_OK;
+}
+
 static void drop_long(mlamg_csr* A) {
   if (A->lg_tile) (void)hipFree(A->lg_tile);
   A->lg_tile = nullptr;
@@ -2355,15 +2385,18 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       drop_sorted(A);
       drop_long(A);
       A->vec_width = 0;
+      drop_vec16(A);
       return MLAMG_OK;
     case MLAMG_FMT_SELL:
       A->vec_width = 0;
+      drop_vec16(A);
       drop_rowpat(A);
       drop_sorted(A);
       drop_long(A);
       return build_sell(A, s, vec_width > 1 ? vec_width : 1);  // vec_width doubles as sigma
     case MLAMG_FMT_SELL_DICT:
       A->vec_width = 0;
+      drop_vec16(A);
       drop_rowpat(A);
       drop_sorted(A);
       drop_long(A);
@@ -2375,6 +2408,7 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       drop_sell(A);
       drop_long(A);
       A->vec_width = 0;
+      drop_vec16(A);
       A->n_part = A->srt_nb;
       return MLAMG_OK;
     }
@@ -2384,6 +2418,7 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       drop_sell(A);
       drop_sorted(A);
       A->vec_width = 0;
+      drop_vec16(A);
       A->n_part = std::max<int32_t>(1, A->lg_nt);
       return MLAMG_OK;
     }
@@ -2404,6 +2439,7 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       drop_sorted(A);
       drop_long(A);
       A->vec_width = vw;
+      MLAMG_TRY(build_vec16(A, s));
       A->n_part = (int32_t)std::max<int64_t>(1, A->n_rows);  // one norm partial per row
       return MLAMG_OK;
     }
@@ -2412,6 +2448,7 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       // SELL-64-sigma (rows sorted by length inside windows of 512) if that does, else
       // CSR-stream
       A->vec_width = 0;
+      drop_vec16(A);
       drop_rowpat(A);
       drop_sorted(A);
       drop_long(A);
@@ -2428,6 +2465,7 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       drop_sorted(A);
       drop_long(A);
       A->vec_width = 0;
+      drop_vec16(A);
       A->n_part = rowpat_parts(A);
       return MLAMG_OK;
     }
@@ -2442,7 +2480,7 @@ int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
   const double n = (double)A->n_rows, m = (double)A->n_cols;
   double b = 8.0 * m + 8.0 * n;  // x read once, y written once
   if (A->vec_width) {
-    b += 12.0 * A->nnz + 4.0 * (n + 1);
+    b += (A->vec_idx16 ? 10.0 : 12.0) * A->nnz + 4.0 * (n + 1);
   } else if (A->lg_tile) {
     b += 12.0 * A->nnz + 4.0 * (n + 1) + 4.0 * (A->lg_nt + 1);
   } else if (A->rp_pid) {

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import statistics
 import time
 
 import numpy as np
@@ -170,10 +171,19 @@ class Hierarchy:
     LONG_CANDIDATES = (("long", 0),)
     VECTOR_CANDIDATES = (("vector", 64), ("vector", 128), ("vector", 256), ("vector", 512))
 
+    # bytes read between two timed launches of the autotune, so each one starts with the
+    # operator and x out of the caches (L2 4 MB per XCD, MALL 256 MB) as in the cycle, where the
+    # other levels' streams pass in between; a read leaves no dirty lines to write back during
+    # the timed launch
+    FLUSH_BYTES = 512 << 20
+
     @staticmethod
-    def _time_format(M, fmt, arg, x, y, reps=5, kind="A"):
-        """Average time of M's cycle operation in format fmt: the residual epilogue for A
-        (r = b - A x, as in the cycle; here b = y), y += M x for P, y = M x for R."""
+    def _time_format(M, fmt, arg, x, y, reps=5, kind="A", flush=None):
+        """Median time of M's cycle operation in format fmt over `reps` launches, each after a
+        cache flush (a read of `flush`): the residual epilogue for A (r = b - A x, as in the
+        cycle; here b = y), y += M x for P, y = M x for R. Timing a launch repeated back to back
+        measures cache-resident operators (any operator up to the MALL's size), which
+        favoured formats that are not the fastest in the cycle."""
         M.set_format(fmt, arg)
         if kind == "A":
             def op():
@@ -186,13 +196,17 @@ class Hierarchy:
                 M.matvec(x, out=y)
         op()
         s = torch.cuda.current_stream()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(reps):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        sink = torch.empty((), dtype=flush.dtype, device=flush.device) if flush is not None else None
+        for e0, e1 in ev:
+            if flush is not None:
+                torch.sum(flush, dim=0, out=sink)
+            e0.record(s)
             op()
-        e1.record(s)
-        e1.synchronize()
-        return e0.elapsed_time(e1) / reps * 1e3  # us
+            e1.record(s)
+        ev[-1][1].synchronize()
+        return statistics.median(e0.elapsed_time(e1) for e0, e1 in ev) * 1e3  # us
 
     # operators whose mean row has at least this many entries use the lane-parallel CSR-vector
     # family (canonical order, one result for every width); shorter rows use the exact-order
@@ -220,6 +234,8 @@ class Hierarchy:
         vec_min_row = self.VEC_MIN_MEAN_ROW if vec_min_row is None else vec_min_row
         self.tuning = []
         dev = torch.device("cuda", torch.cuda.current_device())
+        flush = (torch.ones(self.FLUSH_BYTES // 8, dtype=torch.float64, device=dev)
+                 if fine_format == "autotune" else None)
         for i, L in enumerate(self.levels):
             row = {}
             for name, M in (("A", L.A), ("P", L.P), ("R", L.R)):
@@ -240,7 +256,7 @@ class Hierarchy:
                 for fmt, arg in cands:
                     try:
                         times[f"{fmt}/{arg}"] = self._time_format(M, fmt, arg, x, y,
-                                                                  kind=name)
+                                                                  kind=name, flush=flush)
                     except MlamgError as e:  # format limits (e.g. sorted: row > 4096 nnz)
                         if e.code != MLAMG_EUNSUPPORTED:
                             raise

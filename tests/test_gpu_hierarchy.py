@@ -56,23 +56,32 @@ def test_exact_formats_bitwise(golden, ml, torch_cuda, k, fmt):
     assert abs(nrm.item() - ref) <= 1e-13 * ref
 
 
-def test_vector_format_one_order_for_every_width(ml, oracle, torch_cuda):
+@pytest.mark.parametrize("n_cols,idx16", [(700, True), (700, False), (65536, True),
+                                          (70000, False)])
+def test_vector_format_one_order_for_every_width(ml, oracle, torch_cuda, monkeypatch, n_cols,
+                                                 idx16):
     """CSR-vector widths 64..512 compute one canonical order (oracle.c vec_matvec), for every
-    epilogue; rows from empty to several 512-entry stripes; other widths are refused."""
+    epilogue; rows from empty to several 512-entry stripes; other widths are refused. With
+    16-bit column copies (n_cols <= 65536) and with the 32-bit indices (env MLAMG_NO_IDX16,
+    or more than 65536 columns: the last column 65535 / 69999 is always referenced)."""
     torch = torch_cuda
     from mlamg._lib import MlamgError, call, ptr, stream_ptr
+    if not idx16:
+        monkeypatch.setenv("MLAMG_NO_IDX16", "1")
     rs = np.random.RandomState(8)
     n = 700
     lens = rs.randint(0, 1500, n)
     lens[::13] = 0
     lens[5] = 4100
     indptr = np.concatenate([[0], np.cumsum(lens)])
-    indices = np.concatenate([rs.randint(0, n, l) for l in lens]).astype(np.int32)
-    A = sp.csr_matrix((rs.randn(indptr[-1]) - 0.1, indices, indptr), shape=(n, n))
+    indices = np.concatenate([rs.randint(0, n_cols, l) for l in lens]).astype(np.int32)
+    indices[-1] = n_cols - 1
+    A = sp.csr_matrix((rs.randn(indptr[-1]) - 0.1, indices, indptr), shape=(n, n_cols))
     A.sum_duplicates()
-    A = A + sp.diags(np.abs(rs.randn(n)) + 1.0)
-    A = A.tocsr()
-    x, b, e = rs.randn(n), rs.randn(n), rs.randn(n)
+    A = (A + sp.diags(np.abs(rs.randn(n)) + 1.0) @ sp.eye(n, n_cols)).tocsr()
+    A.sort_indices()
+    assert A.indices.max() == n_cols - 1
+    x, b, e = rs.randn(n_cols), rs.randn(n), rs.randn(n)
     ref = oracle.vec_matvec(A, x)
     assert np.allclose(ref, A @ x, rtol=1e-11, atol=1e-11)
     for vw in (0, 64, 128, 256, 512):
@@ -80,13 +89,14 @@ def test_vector_format_one_order_for_every_width(ml, oracle, torch_cuda):
         assert Ad.get_format()[0] == "vector"
         xd, bd = dev(torch, x), dev(torch, b)
         assert np.array_equal(Ad.matvec(xd).cpu().numpy(), ref)
-        r = torch.empty_like(bd)
-        nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
-        call("mlamg_residual", Ad.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), stream_ptr())
-        assert np.array_equal(r.cpu().numpy(), b - ref)
-        if vw:
-            nrm_ref = nrm.item() if vw == 64 else nrm_ref
-            assert nrm.item() == nrm_ref  # per-row partials: the norm is width-independent
+        if n_cols == n:  # the residual epilogue needs a square operator
+            r = torch.empty_like(bd)
+            nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
+            call("mlamg_residual", Ad.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), stream_ptr())
+            assert np.array_equal(r.cpu().numpy(), b - ref)
+            if vw:
+                nrm_ref = nrm.item() if vw == 64 else nrm_ref
+                assert nrm.item() == nrm_ref  # per-row partials: the norm is width-independent
         y = dev(torch, e)
         call("mlamg_prolong_add", Ad.handle, ptr(xd), ptr(y), stream_ptr())
         assert np.array_equal(y.cpu().numpy(), e + ref)

@@ -1,30 +1,44 @@
-"""Per-kernel breakdown of one V-cycle from a rocprofv3 kernel trace (host-side analysis).
+"""Per-kernel breakdown of the V-cycle from a rocprofv3 kernel trace (host-side analysis).
 
-  python tools/cycle_trace.py gpurun_out/prof/bench_kernel_trace.csv [cycle_index_from_end]
+  python tools/cycle_trace.py gpurun_out/prof/bench_kernel_trace.csv [n_cycles]
 
-Cycles are delimited by the end-of-cycle norm kernel (k_finalize_norm); prints each kernel's
-duration and the idle gap before it, then the cycle's span and busy time.
+Cycles are delimited by the end-of-cycle norm kernel (k_finalize_norm). Over the last n_cycles
+cycles (default 10) that launch the same kernel sequence as the last one, prints each
+position's median duration and median idle gap before it, then the median span and busy time
+(a single cycle's numbers scatter by a few microseconds per kernel).
 """
 import csv
+import statistics
 import sys
+
+
+def cycles(rows):
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "k_finalize_norm" in r["Kernel_Name"]]
+    return [rows[a + 1:b + 1] for a, b in zip(idx, idx[1:])]
 
 
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
-    k = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "k_finalize_norm" in r["Kernel_Name"]]
-    i0, i1 = idx[-k - 1], idx[-k]
-    seg = rows[i0 + 1:i1 + 1]
-    t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
-    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg)
-    prev = None
-    for r in seg:
-        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        gap = (s - prev) / 1e3 if prev else 0.0
-        print(f"{gap:7.2f} {(e - s) / 1e3:8.2f}  {r['Kernel_Name'][:100]}")
-        prev = e
-    print(f"kernels {len(seg)}  span {(t1 - t0) / 1e3:.1f} us  busy {busy / 1e3:.1f} us")
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    cyc = cycles(rows)
+    names = [r["Kernel_Name"] for r in cyc[-1]]
+    same = [c for c in cyc if [r["Kernel_Name"] for r in c] == names][-n:]
+    durs, gaps, spans, busys = [], [], [], []
+    for c in same:
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in c]
+        g = [0.0] + [(int(c[i]["Start_Timestamp"]) - int(c[i - 1]["End_Timestamp"])) / 1e3
+                     for i in range(1, len(c))]
+        durs.append(d)
+        gaps.append(g)
+        spans.append((int(c[-1]["End_Timestamp"]) - int(c[0]["Start_Timestamp"])) / 1e3)
+        busys.append(sum(d))
+    for i, name in enumerate(names):
+        md = statistics.median(d[i] for d in durs)
+        mg = statistics.median(g[i] for g in gaps)
+        print(f"{mg:7.2f} {md:8.2f}  {name[:100]}")
+    print(f"cycles {len(same)}  kernels {len(names)}  median span {statistics.median(spans):.1f} us"
+          f"  busy {statistics.median(busys):.1f} us")
 
 
 if __name__ == "__main__":
