@@ -90,6 +90,17 @@ constexpr double kSrtLongRow = 48.0;
 constexpr int kLongNnz = 4096;
 constexpr int kLongRows = 64;
 
+// Row-pair pattern LDS windows (spmv.hip k_rowpair_win): cluster k of the wide entries' offsets
+// is staged as rows [R0 + s[k], R0 + s[k] + len[k]) of x at window row base[k]
+constexpr int kRpWinMax = 4;
+constexpr int kRpWinNT = 256;        // pairs (threads) per workgroup
+constexpr int kRpWinMaxRows = 4096;  // 32 KiB of LDS
+struct RpWin {
+  int32_t n = 0, rows = -1, nt = 256, woff0 = -1;
+  int32_t s[kRpWinMax] = {0, 0, 0, 0}, len[kRpWinMax] = {0, 0, 0, 0},
+          base[kRpWinMax] = {0, 0, 0, 0};
+};
+
 // Tolerance arguments: tol >= 0 arms the device stop flag with ||.|| <= tol (the reference's
 // `e <= tol`, ns/lib/multigrid.py:197, MLAMG.py:194 — tol = 0 included: an exactly zero norm
 // stops); a negative tol means "no tolerance" (run every requested cycle).
@@ -161,6 +172,9 @@ struct mlamg_csr {
   double* rp_val = nullptr;      // per entry (row 2i's value, row 2i+1's value)
   int32_t rp_n_pat = 0, rp_n_ent = 0;
   int32_t rp_k = 8;                    // entries per kernel step (patterns padded to multiples)
+  mlamg::RpWin rp_win;                 // LDS row windows of k_rowpair_win (rows < 0: none)
+  uint16_t* rp_slot = nullptr;         // its slot order: pattern | local pair << 8, per workgroup
+                                       // sorted by pattern
   std::vector<int32_t> rp_rep;         // representative pair of each pattern (host)
   // attached Jacobi weights (mlamg_csr_attach_dinv): an epilogue whose dinv pointer equals
   // rp_dinv_att reads the per-pattern values rp_dinv[2p], rp_dinv[2p+1] instead of memory

@@ -439,21 +439,23 @@ __device__ __forceinline__ void st2(double* p, int i, bool both, double v0, doub
 
 // epi_load for rows r, r+1
 // (no_dinv: the dinv operand comes from the caller's pattern table instead of memory)
+// (no_x: the x operand — JACOBI's xin, RESID's copy_from — equals the SpMV's x and comes from
+// the caller's LDS window instead of memory)
 template <int OP>
 __device__ __forceinline__ void epi_load2(int r, bool both, const Epi& e, EpiIn& u, EpiIn& w,
-                                          bool no_dinv) {
+                                          bool no_dinv, bool no_x = false) {
   if constexpr (OP == EPI_AXPBY) {
     if (e.beta != 0.0) ld2(e.y, r, both, u.a, w.a);
     if (e.copy_to && !no_dinv) ld2(e.dinv, r, both, u.c, w.c);
   } else if constexpr (OP == EPI_RESID) {
     ld2(e.b, r, both, u.a, w.a);
     if (e.copy_to) {
-      ld2(e.copy_from, r, both, u.b, w.b);
+      if (!no_x) ld2(e.copy_from, r, both, u.b, w.b);
       if (e.dinv && !no_dinv) ld2(e.dinv, r, both, u.c, w.c);
     }
   } else if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) {
     ld2(e.b, r, both, u.a, w.a);
-    ld2(e.xin, r, both, u.b, w.b);
+    if (!no_x) ld2(e.xin, r, both, u.b, w.b);
     if (!no_dinv) ld2(e.dinv, r, both, u.c, w.c);
   } else {  // EPI_ADD
     ld2(e.y, r, both, u.a, w.a);
@@ -630,6 +632,201 @@ void k_rowpair(const uint8_t* __restrict__ pid,
   }
 }
 
+// Row-pair patterns with LDS row windows (C4 A_0: the x gathers, not HBM, bound k_rowpair —
+// 7 16-byte loads per pair through the texture path, 36-38 us; tools/stencil_lab.hip: a 216^3
+// 7-point stencil 32.6 us with every neighbour a global load, 24.4 us with x staged per
+// workgroup, against 23.2 us for a copy of x into y). A workgroup owns NT pairs (rows
+// [R0, R0 + 2 NT)); the wide entries' offsets form <= kRpWinMax clusters (C4: -n^2 | -n..n |
+// +n^2), and for each cluster the rows of x the workgroup's pairs read through it are staged in
+// LDS with 16-byte loads, all issued up front. The sums then read every operand from LDS; x is
+// kept as two arrays of the even and the odd window rows (8-byte reads of one array at a
+// 16-byte lane stride had 4.4 M bank conflicts per C4 pass). Values, masks and order are
+// k_rowpair's, so the bits are scipy's; an epilogue operand equal to x (Jacobi's xin, the fused
+// sweep's copy_from) is read from the window too. Edge pairs keep the global-load path.
+// One wave's lanes of pattern p (uniform): its entries' records and values are scalar loads,
+// each lane reads its two x values per entry from the window (row lr + woff), masks them and
+// adds the products in the pattern's (CSR) order. K entries in flight per step.
+// One wave's lanes of pattern p (uniform): its entries' records and values are scalar loads,
+// all issued before the first is used (an SMEM result is waited for with lgkmcnt(0), which
+// drains the window reads too); each lane reads its two x values per entry from the window
+// (row lr + woff), masks them and adds the products in the pattern's (CSR) order.
+// One wave's lanes of pattern p (uniform): its entries' records and values are scalar loads,
+// all issued before the first is used (an SMEM result is waited for with lgkmcnt(0), which
+// drains the window reads too). An entry of the staged cluster reads its two x values from the
+// window (row lr + woff), any other (flag 8) is one 16-byte global load, issued first; each is
+// masked and the products are added in the pattern's (CSR) order.
+template <int K>
+__device__ __forceinline__ void rowpair_win_uniform(int p, const int32_t* pst,
+                                                    const int4* __restrict__ pat_of,
+                                                    const dbl2* __restrict__ pat_vv,
+                                                    __amdgpu_buffer_rsrc_t rs, int r,
+                                                    const double* __restrict__ we,
+                                                    const double* __restrict__ wo, int lr,
+                                                    double& s0, double& s1) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const int a = __builtin_amdgcn_readfirstlane(pst[p]);
+  const int len = __builtin_amdgcn_readfirstlane(pst[p + 1]) - a;
+  const int* fi = reinterpret_cast<const int*>(pat_of);  // (offset, -, -, flags | woff << 8)
+  for (int k = 0; k < len; k += K) {
+    int fl[K], fo[K];
+    double v0[K], v1[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      fl[q] = __builtin_amdgcn_readfirstlane(fi[4 * (a + k + q) + 3]);
+      fo[q] = __builtin_amdgcn_readfirstlane(fi[4 * (a + k + q)]);
+      const dbl2 v = pat_vv[a + k + q];
+      v0[q] = v.x;
+      v1[q] = v.y;
+    }
+    u32x4 g[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+      if (fl[q] & 8)  // uniform: a scalar branch; rows outside x read zeros
+        g[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(r + fo[q]) * 8u, 0, 0);
+    double x0[K], x1[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      // window row m (parity = the entry's woff parity, lr is even): even m is
+      // (we[m/2], wo[m/2]), odd m (wo[m/2], we[m/2 + 1]); base pointers selected, one read
+      // each (a branch per parity made the compiler wait for every earlier LDS read)
+      const int wf = (fl[q] & 8) ? 0 : fl[q] >> 8;
+      const int odd = wf & 1;
+      const double* b0 = odd ? wo : we;
+      const double* b1 = odd ? we : wo;
+      const int j = (lr + wf) >> 1;
+      x0[q] = b0[j];
+      x1[q] = b1[j + odd];
+    }
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      const bool gl = fl[q] & 8;
+      const double t0 = gl ? __builtin_bit_cast(double, (uint64_t)g[q].x | ((uint64_t)g[q].y << 32))
+                           : x0[q];
+      const double t1 = gl ? __builtin_bit_cast(double, (uint64_t)g[q].z | ((uint64_t)g[q].w << 32))
+                           : x1[q];
+      // an entry a row does not have: +0.0 (its value is 0.0 too), as in rowpair_sums
+      const double y0 = (fl[q] & 1) ? t0 : 0.0;
+      const double y1 = (fl[q] & 2) ? t1 : 0.0;
+      s0 += v0[q] * y0;
+      s1 += v1[q] * y1;
+    }
+  }
+}
+
+template <int OP, bool NORM, int K>
+__global__ __launch_bounds__(kRpWinNT) void k_rowpair_win(const uint16_t* __restrict__ slot,
+                                                          const int32_t* __restrict__ pat_ptr,
+                                                          const int4* __restrict__ pat_of,
+                                                          const dbl2* __restrict__ pat_vv,
+                                                          int64_t n_rows, int64_t n_cols,
+                                                          const double* __restrict__ dinv_att,
+                                                          const dbl2* __restrict__ pat_dinv,
+                                                          RpWin W, const double* __restrict__ x,
+                                                          Epi ep) {
+  constexpr int NT = kRpWinNT;
+  // LDS: even / odd window rows we[W.rows / 2], wo[W.rows / 2]
+  extern __shared__ double rp_win_lds[];
+  __shared__ double red[NT / 64];
+  __shared__ int32_t pst[257];  // pattern starts
+  if (ep.done && *ep.done) return;
+  const int half = W.rows >> 1;
+  double* we = rp_win_lds;
+  double* wo = we + half;
+  const bool tab_dinv = ep.dinv != nullptr && ep.dinv == dinv_att;
+  bool x_op = false;  // the epilogue's x operand is x itself, in the window
+  if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) x_op = ep.xin == x && W.woff0 >= 0;
+  if constexpr (OP == EPI_RESID)
+    x_op = ep.copy_to != nullptr && ep.copy_from == x && W.woff0 >= 0;
+  const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t R0 = lb * 2 * NT;
+  const int64_t sl = lb * NT + threadIdx.x;
+  const int n_pairs_blk = (int)min<int64_t>(NT, (n_rows + 1) / 2 - lb * NT);
+  const bool live = threadIdx.x < n_pairs_blk;
+  const int sv = live ? (int)slot[sl] : 0;
+  const int p = sv & 0xff;
+  const int64_t pr = lb * NT + (sv >> 8);
+  const bool both = 2 * pr + 1 < n_rows;
+  const int r = (int)(2 * pr);
+  EpiIn u, w;
+  if (live) epi_load2<OP>(r, both, ep, u, w, tab_dinv, x_op);
+  dbl2 dv = {0.0, 0.0};
+  if (live && tab_dinv) dv = pat_dinv[p];
+  // windows: 16-byte buffer loads, slots before row 0 or past n_cols read zeros; all issued
+  // before the first LDS store
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(n_cols * 8), 0x00020000);
+  auto wload = [&](int i) {
+    const int t = 2 * i;
+    int k = 0;
+#pragma unroll
+    for (int c = 1; c < kRpWinMax; ++c) k += (c < W.n && t >= W.base[c]) ? 1 : 0;
+    const int64_t g = R0 + W.s[k] + (t - W.base[k]);
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, g >= 0 ? (uint32_t)(g * 8) : ~15u, 0, 0);
+  };
+  auto wstore = [&](int i, const u32x4& t) {
+    we[i] = __builtin_bit_cast(double, (uint64_t)t.x | ((uint64_t)t.y << 32));
+    wo[i] = __builtin_bit_cast(double, (uint64_t)t.z | ((uint64_t)t.w << 32));
+  };
+#ifndef MLAMG_RPW_DBG  // timing variants only (tools/build_variant.sh): 1 no sums, 2 no staging
+#define MLAMG_RPW_DBG 0
+#endif
+  constexpr int WQ = 4;  // slots per thread in registers (C4: 3.9)
+  if (!(MLAMG_RPW_DBG & 2)) {
+    u32x4 wv[WQ];
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+      const int i = threadIdx.x + q * NT;
+      if (i < half) wv[q] = wload(i);
+    }
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+      const int i = threadIdx.x + q * NT;
+      if (i < half) wstore(i, wv[q]);
+    }
+    for (int i = threadIdx.x + WQ * NT; i < half; i += NT) wstore(i, wload(i));
+  }
+  for (int i = threadIdx.x; i < 257; i += NT) pst[i] = pat_ptr[i];
+  __syncthreads();
+  double sq = 0.0;
+  if (live) {
+    if (tab_dinv) {
+      u.c = dv.x;
+      w.c = dv.y;
+    }
+    const int lr = (int)(r - R0);
+    if (x_op) {  // window row lr + woff0 (even: lr and woff0 are)
+      const int j = (lr + W.woff0) >> 1;
+      u.b = we[j];
+      w.b = both ? wo[j] : 0.0;
+    }
+  }
+  // one pass per distinct pattern of the wave (sorted slots: one, at a pattern boundary two or
+  // three), the pattern's records as scalar loads. Every pair reads its operands from the
+  // windows, the matrix's first and last pairs too: rows outside x were staged as zeros and
+  // are masked like every entry a row does not have.
+  double s0 = 0.0, s1 = 0.0;
+  uint64_t todo = (MLAMG_RPW_DBG & 1) ? 0 : __ballot(live);
+  while (todo) {
+    const int p0 = __builtin_amdgcn_readlane(p, (int)__builtin_ctzll(todo));
+    const bool mine = live && p == p0;
+    todo &= ~__ballot(mine);
+    if (mine)
+      rowpair_win_uniform<K>(p0, pst, pat_of, pat_vv, rs, r, we, wo, (int)(r - R0), s0, s1);
+  }
+  if (live && !(MLAMG_RPW_DBG & 4)) sq = epi_store2<OP>(r, both, s0, s1, u, w, ep);
+  if constexpr (NORM) {
+    double v = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int i = 0; i < NT / 64; ++i) t += red[i];
+      ep.partial[lb] = t;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- CSR-vector (canonical order)
 // Lane-parallel sums for long rows (coarse Galerkin operators A_l, R = P^T: hundreds of entries
 // per row, where a one-lane left-to-right chain costs ~15-25 cycles per entry: tools/
@@ -735,9 +932,224 @@ static int launch_vcan(const mlamg_csr* A, const double* x, const Epi& ep, hipSt
   return MLAMG_OK;
 }
 
+// The same canonical order for the long-row coarse operators where k_csr_vcan is latency-bound
+// (C4 level 3: 10,078 rows of ~709 entries; a 512-thread workgroup per 1-2 rows issues its loads
+// once and drains: 22-27 us for a 71 MB stream; a wave that walks whole rows one after another
+// pays a chain of memory round trips per row instead). A 1024-thread workgroup owns a contiguous
+// range of rows (their bounds staged in LDS), dealt to its 16 waves. A wave walks its rows'
+// 512-entry stripes (virtual wave j of a stripe = entry 64 j + lane, one accumulator each) as a
+// software pipeline: the loads of the next stripe are in flight while the current one is
+// gathered and summed, across row ends too. x is staged in LDS once per workgroup when it fits
+// (XL), so the gathers leave the texture address unit (TA busy 51 % on A_3 with x gathered from
+// L2). Bitwise k_csr_vcan's order at every width: entry e of a row goes to
+// virtual lane (e - start) mod 512 and each virtual lane sums its entries left to right.
+constexpr int kVwThreads = 1024;
+constexpr int64_t kVwMaxX = 16384;     // doubles of x in LDS (128 KiB)
+constexpr int64_t kVwMaxRows = 4096;   // rows per workgroup (bounds in LDS, 16 KiB)
+
+// one stripe of a wave: 8 entries per lane (virtual waves j = 0..7), every load unconditional
+// (buffer loads, out-of-range offsets read 0) and masked by selects, so the loop body has no
+// divergent branch and the compiler's wait counts keep the next stripe's loads in flight
+struct VwStripe {
+  int32_t c[8];
+  double v[8];
+  EpiIn pre;  // epilogue operands of the stripe's row (loaded with every stripe: same lines)
+  int row;    // local row
+  int e0, lb; // stripe start and row end: the mask is applied when the stripe is consumed (a
+              // select right after the load would wait for it)
+  bool last;  // last stripe of the row
+};
+
+template <int OP, bool NORM, typename IT, bool XL, bool NT>
+__global__ __launch_bounds__(kVwThreads) void k_vcan_wave(const int32_t* __restrict__ indptr,
+                                                          const IT* __restrict__ indices,
+                                                          const double* __restrict__ vals,
+                                                          int64_t n_rows, int64_t n_cols,
+                                                          int64_t nnz, int64_t rows_per_block,
+                                                          const double* __restrict__ x, Epi ep) {
+  extern __shared__ double lds[];
+  if (ep.done && *ep.done) return;
+  constexpr int kAux = NT ? 2 : 0;  // nt: non-temporal stream (see kCachedNnz)
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int nr = (int)min<int64_t>(rows_per_block, n_rows - r0);
+  const int64_t xw = XL ? ((n_cols + 1) & ~int64_t(1)) : 0;
+  int32_t* rp = reinterpret_cast<int32_t*>(lds + xw);
+  for (int i = threadIdx.x; i <= nr; i += kVwThreads) rp[i] = indptr[r0 + i];
+  if constexpr (XL) {
+    for (int64_t i = threadIdx.x; i < n_cols; i += 8 * kVwThreads) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t k = i + u * kVwThreads;
+        v[u] = k < n_cols ? x[k] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t k = i + u * kVwThreads;
+        if (k < n_cols) lds[k] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rsI =
+      __builtin_amdgcn_make_buffer_rsrc((void*)indices, 0, (int)(nnz * sizeof(IT)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsV =
+      __builtin_amdgcn_make_buffer_rsrc((void*)vals, 0, (int)(nnz * 8), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsX =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(n_cols * 8), 0x00020000);
+  // load cursor (wave-uniform): row lr (local), its bounds [la, lb), next stripe start le; a row
+  // of any length (empty included) is at least one stripe; past the last row the cursor reads
+  // an empty range
+  int lr = wave;
+  if (lr >= nr) return;
+  int la = __builtin_amdgcn_readfirstlane(rp[lr]);
+  int lb = __builtin_amdgcn_readfirstlane(rp[lr + 1]);
+  int le = la;
+  auto load = [&](VwStripe& s) {
+    s.row = lr;
+    s.e0 = le;
+    s.lb = lb;
+    s.last = le + 512 >= lb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = le + 64 * j + lane;
+      if constexpr (sizeof(IT) == 2)
+        s.c[j] = (int32_t)__builtin_amdgcn_raw_buffer_load_b16(rsI, e * 2, 0, kAux);
+      else
+        s.c[j] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rsI, e * 4, 0, kAux);
+      s.v[j] =
+          __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsV, e * 8, 0, kAux));
+    }
+    s.pre = epi_load<OP>((int)min<int64_t>(r0 + lr, n_rows - 1), ep);
+    le += 512;
+    if (le >= lb) {
+      lr += kVwThreads / 64;
+      const bool in = lr < nr;
+      la = in ? __builtin_amdgcn_readfirstlane(rp[lr]) : 0;
+      lb = in ? __builtin_amdgcn_readfirstlane(rp[lr + 1]) : 0;
+      le = la;
+    }
+  };
+  double acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.0;
+  auto gather = [&](const VwStripe& s, double* xv) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = s.e0 + 64 * j + lane < s.lb;
+      if constexpr (XL)
+        xv[j] = lds[ok ? s.c[j] : 0];
+      else  // past the row: offset 0xfffffff8, out of range, reads 0
+        xv[j] = __builtin_bit_cast(
+            double, __builtin_amdgcn_raw_buffer_load_b64(rsX, ok ? (uint32_t)s.c[j] * 8u : ~7u,
+                                                         0, 0));
+    }
+  };
+  auto sum = [&](const VwStripe& s, const double* xv) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      acc[j] = s.e0 + 64 * j + lane < s.lb ? acc[j] + s.v[j] * xv[j] : acc[j];
+    if (s.last) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc[j] += __shfl_xor(acc[j], off, 64);
+      if (lane == 0) {
+        double r = acc[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) r += acc[j];
+        const double sq = epi_store<OP>((int)(r0 + s.row), r, s.pre, ep);
+        if constexpr (NORM) ep.partial[r0 + s.row] = sq;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.0;
+    }
+  };
+  // x in LDS: issue the next stripe's loads, then gather and sum this one; x in memory: gather
+  // this one first (vmcnt is in order: its gathers must not queue behind the next stripe)
+  auto step = [&](VwStripe& cur, VwStripe& nxt) -> bool {
+    double xv[8];
+    const bool more = lr < nr;
+    if constexpr (XL) {
+      load(nxt);
+      gather(cur, xv);
+    } else {
+      gather(cur, xv);
+      load(nxt);
+    }
+    sum(cur, xv);
+    return more;
+  };
+  VwStripe sa, sb;
+  load(sa);
+  while (step(sa, sb) && step(sb, sa)) {
+  }
+}
+
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// MLAMG_VCAN_WAVE=1 takes k_vcan_wave (x in LDS when it fits), =2 without the LDS copy of x;
+// unset / 0 keeps k_csr_vcan, which measured as fast or faster on every C4 operator.
+// Read at every launch (a host getenv, not a device cost) so one process can compare them.
+static int vcan_wave_mode() {
+  const char* e = std::getenv("MLAMG_VCAN_WAVE");
+  return e ? std::atoi(e) : 0;
+}
+
+template <int OP, bool NORM, typename IT, bool XL>
+static void launch_vcan_wave_nt(const mlamg_csr* A, const IT* idx, const double* x,
+                                const Epi& ep, hipStream_t s, unsigned nb, size_t lds,
+                                int64_t rpb) {
+  if (ep.cached)
+    hipLaunchKernelGGL((k_vcan_wave<OP, NORM, IT, XL, false>), dim3(nb), dim3(kVwThreads), lds, s,
+                       A->indptr, idx, A->data, A->n_rows, A->n_cols, A->nnz, rpb, x, ep);
+  else
+    hipLaunchKernelGGL((k_vcan_wave<OP, NORM, IT, XL, true>), dim3(nb), dim3(kVwThreads), lds, s,
+                       A->indptr, idx, A->data, A->n_rows, A->n_cols, A->nnz, rpb, x, ep);
+}
+
+template <int OP, bool NORM, typename IT>
+static void launch_vcan_wave(const mlamg_csr* A, const IT* idx, const double* x, const Epi& ep,
+                             hipStream_t s) {
+  const bool xl = A->n_cols <= kVwMaxX && vcan_wave_mode() != 2;
+  // one workgroup per CU with x in LDS (up to 144 KiB with the row bounds); two without
+  const int64_t slots = (int64_t)device_cus() * (xl ? 1 : 2);
+  const int64_t rpb = std::min<int64_t>(kVwMaxRows,
+                                        std::max<int64_t>(1, (A->n_rows + slots - 1) / slots));
+  const unsigned nb = (unsigned)((A->n_rows + rpb - 1) / rpb);
+  const size_t rows_lds = sizeof(int32_t) * (size_t)(rpb + 1);
+  if (xl)
+    launch_vcan_wave_nt<OP, NORM, IT, true>(
+        A, idx, x, ep, s, nb, sizeof(double) * ((A->n_cols + 1) & ~int64_t(1)) + rows_lds, rpb);
+  else
+    launch_vcan_wave_nt<OP, NORM, IT, false>(A, idx, x, ep, s, nb, rows_lds, rpb);
+}
+
 template <int OP, bool NORM>
 static int launch_vec(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   if (A->n_rows == 0) return MLAMG_OK;
+  // buffer offsets are 32-bit: the wave kernel takes streams below 2 GiB
+  if (vcan_wave_mode() != 0 && A->nnz < (int64_t(1) << 28) && A->n_cols < (int64_t(1) << 28)) {
+    if (A->vec_idx16)
+      launch_vcan_wave<OP, NORM, uint16_t>(A, A->vec_idx16, x, ep, s);
+    else
+      launch_vcan_wave<OP, NORM, int32_t>(A, A->indices, x, ep, s);
+    MLAMG_HIP(hipGetLastError());
+    return MLAMG_OK;
+  }
   switch (A->vec_width) {
     case 128: return launch_vcan<OP, NORM, 2>(A, x, ep, s);
     case 256: return launch_vcan<OP, NORM, 4>(A, x, ep, s);
@@ -1131,6 +1543,26 @@ static int launch_rowpair_ch(const mlamg_csr* A, const double* x, const Epi& ep,
 
 template <int OP, bool NORM>
 static int launch_rowpair(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  if (A->rp_win.rows >= 0 && A->rp_slot) {
+    const int64_t n_pairs = (A->n_rows + 1) / 2;
+    const unsigned nb = (unsigned)((n_pairs + kRpWinNT - 1) / kRpWinNT);
+    const size_t lds = sizeof(double) * (size_t)A->rp_win.rows;
+#define MLAMG_RPW(KV)                                                                           \
+  hipLaunchKernelGGL((k_rowpair_win<OP, NORM, KV>), dim3(nb), dim3(kRpWinNT), lds, s,            \
+                     A->rp_slot, A->rp_ptr, reinterpret_cast<const int4*>(A->rp_off),           \
+                     reinterpret_cast<const dbl2*>(A->rp_val), A->n_rows, A->n_cols,            \
+                     A->rp_dinv_att, reinterpret_cast<const dbl2*>(A->rp_dinv), A->rp_win, x,   \
+                     ep)
+    switch (A->rp_k) {
+      case 5: MLAMG_RPW(5); break;
+      case 6: MLAMG_RPW(6); break;
+      case 7: MLAMG_RPW(7); break;
+      default: MLAMG_RPW(8); break;
+    }
+#undef MLAMG_RPW
+    MLAMG_HIP(hipGetLastError());
+    return MLAMG_OK;
+  }
   return launch_rowpair_ch<OP, NORM, kRpChunks>(A, x, ep, s);
 }
 
@@ -1975,14 +2407,16 @@ __global__ void k_rp_assign(const int32_t* __restrict__ ip, const int32_t* __res
 
 static void drop_rowpat(mlamg_csr* A) {
   for (void* p : {(void*)A->rp_pid, (void*)A->rp_ptr, (void*)A->rp_off, (void*)A->rp_val,
-                  (void*)A->rp_dinv})
+                  (void*)A->rp_dinv, (void*)A->rp_slot})
     if (p) (void)hipFree(p);
+  A->rp_slot = nullptr;
   A->rp_dinv = nullptr;
   A->rp_dinv_att = nullptr;
   A->rp_rep.clear();
   A->rp_pid = nullptr;
   A->rp_ptr = nullptr;
   A->rp_off = nullptr;
+  A->rp_win = RpWin{};
   A->rp_val = nullptr;
   A->rp_n_pat = A->rp_n_ent = 0;
   if (!A->sell_ptr && !A->vec_width && !A->srt_pk) A->n_part = A->n_blocks;
@@ -2040,6 +2474,7 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
   if (rc == MLAMG_OK && (hc[2] != 0 || hc[0] > 255))
     fail(MLAMG_EUNSUPPORTED, "more than 255 distinct row-pair patterns");
   std::vector<int32_t> hptr(257, 0), hoff, reps;
+  RpWin win{};
   int kstep = 8;
   std::vector<double> hv0, hv1;
   std::vector<uint8_t> hfl;
@@ -2160,6 +2595,61 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
       hptr[k + 1] = (int32_t)hoff.size();
     }
     for (size_t k = pats.size() + 1; k < 257; ++k) hptr[k] = (int32_t)hoff.size();
+    // LDS windows of k_rowpair_win: the entries' offsets grouped into <= kRpWinMax
+    // clusters (a gap of more than 2 NT rows starts a new one); cluster k is staged as rows
+    // [R0 + s_k, R0 + s_k + L_k) of x, the clusters concatenated; an entry's window row is then
+    // (r - R0) + woff, woff = base_k + off - s_k, kept in bits 8.. of its flags word
+    std::vector<int32_t> hwoff(hoff.size(), 0);
+    {
+      const char* ev = std::getenv("MLAMG_RP_WIN");
+      win.nt = kRpWinNT;
+      std::vector<int32_t> offs;
+      for (size_t e = 0; e < hoff.size(); ++e) offs.push_back(hoff[e]);
+      std::sort(offs.begin(), offs.end());
+      offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
+      // opt-in (MLAMG_RP_WIN=1): on C4 this kernel measured slower than k_rowpair
+      bool ok = ev && ev[0] == '1' && !offs.empty();
+      std::vector<std::pair<int32_t, int32_t>> cl;  // (lo, hi) offsets
+      for (int32_t o : offs) {
+        if (cl.empty() || (int64_t)o - cl.back().second > 2 * win.nt)
+          cl.push_back({o, o});
+        else
+          cl.back().second = o;
+      }
+      ok = ok && cl.size() <= (size_t)kRpWinMax;
+      int32_t total = 0;
+      for (size_t k = 0; ok && k < cl.size(); ++k) {
+        const int32_t s0 = cl[k].first & ~1;                               // even start
+        const int32_t len = ((2 * win.nt + cl[k].second - s0) + 1) & ~1;   // even length
+        win.s[k] = s0;
+        win.len[k] = len;
+        win.base[k] = total;
+        total += len;
+      }
+      // only the cluster holding offset 0 is staged (the workgroup's own rows and their
+      // near neighbours); entries of the other clusters (C4: +-n^2) stay 16-byte global loads,
+      // marked by flag 8 (staging them as well cost more than it saved: 3.9 rows staged per
+      // row of x)
+      int kc = -1;
+      for (size_t k = 0; ok && k < cl.size(); ++k)
+        if (cl[k].first <= 0 && 0 <= cl[k].second) kc = (int)k;
+      ok = ok && kc >= 0 && win.len[kc] <= kRpWinMaxRows;
+      win.n = ok ? 1 : 0;
+      if (ok) {
+        win.s[0] = win.s[kc];
+        win.len[0] = win.len[kc];
+        win.base[0] = 0;
+      }
+      win.rows = ok ? win.len[0] : -1;
+      win.woff0 = ok ? -win.s[0] : -1;
+      if (ok)
+        for (size_t e = 0; e < hoff.size(); ++e) {
+          if (cl[kc].first <= hoff[e] && hoff[e] <= cl[kc].second)
+            hwoff[e] = hoff[e] - win.s[0];
+          else
+            hfl[e] |= 8;
+        }
+    }
     const size_t ne = hoff.size(), na = std::max<size_t>(ne, 1);
     // interleaved records: (offset, flags) and (row 2i value, row 2i+1 value)
     std::vector<int32_t> hof(4 * ne);
@@ -2168,7 +2658,7 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
       hof[4 * e] = hoff[e];
       hof[4 * e + 1] = (hfl[e] & 1) ? -1 : 0;
       hof[4 * e + 2] = (hfl[e] & 2) ? -1 : 0;
-      hof[4 * e + 3] = hfl[e];
+      hof[4 * e + 3] = hfl[e] | (win.rows >= 0 ? hwoff[e] << 8 : 0);
       hvv[2 * e] = hv0[e];
       hvv[2 * e + 1] = hv1[e];
     }
@@ -2201,7 +2691,34 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
       if (p) (void)hipFree(p);
     return rc;
   }
+  // k_rowpair_win's slot order: within each workgroup's 256 pairs, the pairs sorted (stably) by
+  // pattern, each slot a uint16 (pattern | local pair << 8), so a wave's lanes share a pattern
+  // and read its records with scalar loads
+  uint16_t* pslot = nullptr;
+  if (win.rows >= 0 && n_pairs > 0) {
+    std::vector<uint8_t> hp((size_t)n_pairs);
+    std::vector<uint16_t> hs((size_t)n_pairs);
+    bool okc = hipMemcpy(hp.data(), pid, (size_t)n_pairs, hipMemcpyDeviceToHost) == hipSuccess;
+    for (int64_t c0 = 0; okc && c0 < n_pairs; c0 += kRpWinNT) {
+      const int64_t c1 = std::min<int64_t>(n_pairs, c0 + kRpWinNT);
+      int cnt[257] = {0};
+      for (int64_t i = c0; i < c1; ++i) ++cnt[hp[i] + 1];
+      for (int k = 0; k < 256; ++k) cnt[k + 1] += cnt[k];
+      for (int64_t i = c0; i < c1; ++i)
+        hs[c0 + cnt[hp[i]]++] = (uint16_t)(hp[i] | ((i - c0) << 8));
+    }
+    okc = okc && hipMalloc(&pslot, sizeof(uint16_t) * (size_t)n_pairs) == hipSuccess &&
+          hipMemcpy(pslot, hs.data(), sizeof(uint16_t) * (size_t)n_pairs,
+                    hipMemcpyHostToDevice) == hipSuccess;
+    if (!okc) {
+      if (pslot) (void)hipFree(pslot);
+      pslot = nullptr;
+      win = RpWin{};
+    }
+  }
   drop_rowpat(A);
+  A->rp_win = win;
+  A->rp_slot = pslot;
   A->rp_pid = pid;
   A->rp_ptr = pptr;
   A->rp_off = poff;
@@ -2226,7 +2743,9 @@ __global__ void k_rp_dinv_check(const uint8_t* __restrict__ pid, const double* _
 }
 
 static int32_t rowpat_parts(const mlamg_csr* A) {
-  const int64_t n_pairs = (A->n_rows + 1) / 2, per = (int64_t)kRpChunks * kThreads;
+  const int64_t n_pairs = (A->n_rows + 1) / 2,
+                per = (A->rp_win.rows >= 0 && A->rp_slot) ? (int64_t)kRpWinNT
+                                                           : (int64_t)kRpChunks * kThreads;
   return (int32_t)std::max<int64_t>(1, (n_pairs + per - 1) / per);
 }
 

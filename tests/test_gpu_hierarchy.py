@@ -84,7 +84,10 @@ def test_vector_format_one_order_for_every_width(ml, oracle, torch_cuda, monkeyp
     x, b, e = rs.randn(n_cols), rs.randn(n), rs.randn(n)
     ref = oracle.vec_matvec(A, x)
     assert np.allclose(ref, A @ x, rtol=1e-11, atol=1e-11)
-    for vw in (0, 64, 128, 256, 512):
+    # every kernel of the family: k_vcan_wave with x in LDS (MLAMG_VCAN_WAVE=1, n_cols <= 16384)
+    # and from global memory (=2), k_csr_vcan at each width (=0, the default)
+    for mode, vw in [(m, w) for m in ("1", "2", "0") for w in (0, 64, 128, 256, 512)]:
+        monkeypatch.setenv("MLAMG_VCAN_WAVE", mode)
         Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("vector", vw)
         assert Ad.get_format()[0] == "vector"
         xd, bd = dev(torch, x), dev(torch, b)
@@ -95,7 +98,7 @@ def test_vector_format_one_order_for_every_width(ml, oracle, torch_cuda, monkeyp
             call("mlamg_residual", Ad.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), stream_ptr())
             assert np.array_equal(r.cpu().numpy(), b - ref)
             if vw:
-                nrm_ref = nrm.item() if vw == 64 else nrm_ref
+                nrm_ref = nrm.item() if (mode, vw) == ("1", 64) else nrm_ref
                 assert nrm.item() == nrm_ref  # per-row partials: the norm is width-independent
         y = dev(torch, e)
         call("mlamg_prolong_add", Ad.handle, ptr(xd), ptr(y), stream_ptr())
@@ -624,6 +627,46 @@ def test_rowpat_format(ml, torch_cuda):
     xs2 = dev(torch, x)
     call("mlamg_jacobi", Ad.handle, ptr(d2), ptr(bd), ptr(xs2), ptr(t1), 1, stream_ptr())
     assert torch.equal(xs, xs2)
+
+
+@pytest.mark.parametrize("win", ["1", "0"])
+def test_rowpat_window(ml, torch_cuda, monkeypatch, win):
+    """Row-pair kernel with the LDS row window (k_rowpair_win, opt-in MLAMG_RP_WIN=1) and
+    without (k_rowpair, the default): bitwise scipy for y = A x, the residual, Jacobi with xin == x (window
+    operand) and xin != x, the cycle's fused end residual; 48^3 puts the +-n^2 entries beyond the
+    largest halo (global loads beside window reads), 24^3 and 2D 37^2 keep them all in it."""
+    torch = torch_cuda
+    from mlamg._lib import call, ptr, stream_ptr
+    monkeypatch.setenv("MLAMG_RP_WIN", win)
+    rs = np.random.RandomState(12)
+    for A in (ml.problems.poisson_3d_7pt(48), ml.problems.poisson_3d_7pt(24),
+              ml.problems.poisson_2d_5pt(37)):
+        n = A.shape[0]
+        x, b, d = rs.randn(n), rs.randn(n), rs.rand(n) + 0.5
+        xd, bd, dd = dev(torch, x), dev(torch, b), dev(torch, d)
+        Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("rowpat")
+        y = A @ x
+        assert np.array_equal(Ad.matvec(xd).cpu().numpy(), y)
+        r = torch.empty(n, dtype=torch.float64, device="cuda")
+        call("mlamg_residual", Ad.handle, ptr(bd), ptr(xd), ptr(r), None, stream_ptr())
+        assert np.array_equal(r.cpu().numpy(), b - y)
+        xs = dev(torch, x)
+        t = torch.empty_like(xs)
+        call("mlamg_jacobi", Ad.handle, ptr(dd), ptr(bd), ptr(xs), ptr(t), 1, stream_ptr())
+        assert np.array_equal(xs.cpu().numpy(), x + d * (b - y))
+    A = ml.problems.poisson_3d_7pt(48)
+    bd = dev(torch, rs.randn(A.shape[0]))
+    x0 = rs.randn(A.shape[0])
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=500, fine_format="csr_stream")
+    H2 = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=500, fine_format="csr_stream")
+    H2.levels[0].A.set_format("rowpat")
+    assert H2.levels[0].A.attach_dinv(H2.levels[0].dinv)
+    for use_graph in (False, True):
+        x1, x2 = dev(torch, x0), dev(torch, x0)
+        h1 = H.cycle(bd, x1, 4, use_graph=use_graph)
+        h2 = H2.cycle(bd, x2, 4, use_graph=use_graph)
+        assert torch.equal(x1, x2)
+        assert np.allclose(h1, h2, rtol=1e-14, atol=0)
 
 
 def test_supplied_aggregates_and_prolongator(ml, oracle, torch_cuda):

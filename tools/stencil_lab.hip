@@ -180,6 +180,64 @@ __global__ __launch_bounds__(256) void k_pair_ind(const double* __restrict__ x,
   *reinterpret_cast<dbl2*>(y + r) = out;
 }
 
+// LDS row window: a workgroup owns CH * 512 consecutive rows and stages x over them plus a
+// halo of H >= n rows on each side with 16-byte loads (one fetch per element + 2H), so the
+// in-plane neighbours (+-1, +-n) come from LDS; the +-n^2 neighbours are global 16-byte loads
+// issued before the window is staged. TA instructions per 64 pairs: ~1.2 (window) + 2 (z) + 1
+// (store) instead of 7 + 1.
+template <int CH, int ZP>
+__global__ __launch_bounds__(256) void k_pair_tile(const double* __restrict__ x,
+                                                   double* __restrict__ y, int n, int64_t N) {
+  extern __shared__ dbl2 win[];
+  const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const int H = (n + 1) & ~1;
+  const int64_t R0 = lb * CH * 512;
+  const int64_t T0 = R0 - H;
+  const int wlen = (CH * 512 + 2 * H) / 2;  // dbl2 slots
+  const int64_t n2 = (int64_t)n * n;
+  dbl2 zm[CH], zp[CH];
+  auto zload = [&]() {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int64_t r = R0 + 2 * (c * 256 + threadIdx.x);
+      zm[c] = (r - n2 >= 0 && r + 1 < N) ? *reinterpret_cast<const dbl2u*>(x + r - n2) : dbl2{0.0, 0.0};
+      zp[c] = (r + n2 + 1 < N) ? *reinterpret_cast<const dbl2u*>(x + r + n2) : dbl2{0.0, 0.0};
+    }
+  };
+  if (ZP) zload();
+  for (int i = threadIdx.x; i < wlen; i += 256) {
+    const int64_t g = T0 + 2 * i;
+    win[i] = (g >= 0 && g + 1 < N) ? *reinterpret_cast<const dbl2u*>(x + g) : dbl2{0.0, 0.0};
+  }
+  __syncthreads();
+  if (!ZP) zload();
+  const double* w = reinterpret_cast<const double*>(win);
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int64_t r = R0 + 2 * (c * 256 + threadIdx.x);
+    if (r + 1 >= N) break;
+    const int l = (int)(r - T0);
+    const double c0 = w[l], c1 = w[l + 1];
+    double s0 = 6.0 * c0, s1 = 6.0 * c1;
+    s0 -= w[l - 1];
+    s1 -= c0;
+    s0 -= c1;
+    s1 -= w[l + 2];
+    s0 -= w[l - n];
+    s1 -= w[l + 1 - n];
+    s0 -= w[l + n];
+    s1 -= w[l + 1 + n];
+    s0 -= zm[c].x;
+    s1 -= zm[c].y;
+    s0 -= zp[c].x;
+    s1 -= zp[c].y;
+    dbl2 o;
+    o.x = s0;
+    o.y = s1;
+    *reinterpret_cast<dbl2*>(y + r) = o;
+  }
+}
+
 template <class F>
 static float timeit(F f, int reps) {
   hipEvent_t a, b;
@@ -244,6 +302,22 @@ int main(int argc, char** argv) {
     float us1 = timeit([&] { hipLaunchKernelGGL((k_pair_ind<1>), dim3(nb), dim3(256), 0, 0, x, y, pid, n, N); }, reps);
     float us2 = timeit([&] { hipLaunchKernelGGL((k_pair_ind<2>), dim3(nb), dim3(256), 0, 0, x, y, pid, n, N); }, reps);
     printf("pair + pid load      : %7.1f us\npair + pid + LDS offs: %7.1f us\n", us1, us2);
+  }
+  for (int ch : {1, 2, 4, 11, 12}) {
+    const int H = (n + 1) & ~1;
+    const unsigned nb = (unsigned)((N + ch * 512 - 1) / (ch * 512));
+    const size_t lds = sizeof(double) * (ch * 512 + 2 * H);
+    const int c2 = ch % 10;  // 11, 12: CH 1, 2 with the z loads after the barrier
+    const unsigned nb2 = (unsigned)((N + c2 * 512 - 1) / (c2 * 512));
+    const size_t lds2 = sizeof(double) * (c2 * 512 + 2 * H);
+    float us = timeit([&] {
+      if (ch == 1) hipLaunchKernelGGL((k_pair_tile<1, 1>), dim3(nb), dim3(256), lds, 0, x, y, n, N);
+      if (ch == 2) hipLaunchKernelGGL((k_pair_tile<2, 1>), dim3(nb), dim3(256), lds, 0, x, y, n, N);
+      if (ch == 4) hipLaunchKernelGGL((k_pair_tile<4, 1>), dim3(nb), dim3(256), lds, 0, x, y, n, N);
+      if (ch == 11) hipLaunchKernelGGL((k_pair_tile<1, 0>), dim3(nb2), dim3(256), lds2, 0, x, y, n, N);
+      if (ch == 12) hipLaunchKernelGGL((k_pair_tile<2, 0>), dim3(nb2), dim3(256), lds2, 0, x, y, n, N);
+    }, reps);
+    printf("pair LDS window CH=%d: %7.1f us  %6.0f GB/s (x+y)\n", ch, us, 16.0 * N / us / 1e3);
   }
   run_row<0, 0>(x, y, n, N, reps);
   run_row<7, 0>(x, y, n, N, reps);
