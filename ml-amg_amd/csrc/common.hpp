@@ -94,6 +94,7 @@ constexpr int kLongRows = 64;
 // is staged as rows [R0 + s[k], R0 + s[k] + len[k]) of x at window row base[k]
 constexpr int kRpWinMax = 4;
 constexpr int kRpWinNT = 256;        // pairs (threads) per workgroup
+constexpr int kRpWinG = 2;           // global (unstaged) entries per kernel step at most
 constexpr int kRpWinMaxRows = 4096;  // 32 KiB of LDS
 struct RpWin {
   int32_t n = 0, rows = -1, nt = 256, woff0 = -1;

@@ -644,17 +644,11 @@ void k_rowpair(const uint8_t* __restrict__ pid,
 // k_rowpair's, so the bits are scipy's; an epilogue operand equal to x (Jacobi's xin, the fused
 // sweep's copy_from) is read from the window too. Edge pairs keep the global-load path.
 // One wave's lanes of pattern p (uniform): its entries' records and values are scalar loads,
-// each lane reads its two x values per entry from the window (row lr + woff), masks them and
-// adds the products in the pattern's (CSR) order. K entries in flight per step.
-// One wave's lanes of pattern p (uniform): its entries' records and values are scalar loads,
-// all issued before the first is used (an SMEM result is waited for with lgkmcnt(0), which
-// drains the window reads too); each lane reads its two x values per entry from the window
-// (row lr + woff), masks them and adds the products in the pattern's (CSR) order.
-// One wave's lanes of pattern p (uniform): its entries' records and values are scalar loads,
 // all issued before the first is used (an SMEM result is waited for with lgkmcnt(0), which
 // drains the window reads too). An entry of the staged cluster reads its two x values from the
-// window (row lr + woff), any other (flag 8) is one 16-byte global load, issued first; each is
-// masked and the products are added in the pattern's (CSR) order.
+// window (row lr + woff); the others (flag 8, at most kRpWinG per step: C4's +-n^2) are 16-byte
+// global loads issued first into kRpWinG registers; each value is masked and the products are
+// added in the pattern's (CSR) order.
 template <int K>
 __device__ __forceinline__ void rowpair_win_uniform(int p, const int32_t* pst,
                                                     const int4* __restrict__ pat_of,
@@ -678,11 +672,33 @@ __device__ __forceinline__ void rowpair_win_uniform(int p, const int32_t* pst,
       v0[q] = v.x;
       v1[q] = v.y;
     }
-    u32x4 g[K];
+    // the step's global entries (scalar bookkeeping): entry qg[t] goes to register g[t]; an
+    // unused register reads an out-of-range slot (zeros)
+    int qg[kRpWinG], og[kRpWinG];
 #pragma unroll
-    for (int q = 0; q < K; ++q)
-      if (fl[q] & 8)  // uniform: a scalar branch; rows outside x read zeros
-        g[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(r + fo[q]) * 8u, 0, 0);
+    for (int t = 0; t < kRpWinG; ++t) {
+      qg[t] = -1;
+      og[t] = 0;
+    }
+    {
+      int t = 0;
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+        if (fl[q] & 8) {
+#pragma unroll
+          for (int u2 = 0; u2 < kRpWinG; ++u2)
+            if (u2 == t) {
+              qg[u2] = q;
+              og[u2] = fo[q];
+            }
+          ++t;
+        }
+    }
+    u32x4 g[kRpWinG];
+#pragma unroll
+    for (int t = 0; t < kRpWinG; ++t)
+      g[t] = __builtin_amdgcn_raw_buffer_load_b128(
+          rs, qg[t] >= 0 ? (uint32_t)(r + og[t]) * 8u : ~15u, 0, 0);
     double x0[K], x1[K];
 #pragma unroll
     for (int q = 0; q < K; ++q) {
@@ -699,11 +715,13 @@ __device__ __forceinline__ void rowpair_win_uniform(int p, const int32_t* pst,
     }
 #pragma unroll
     for (int q = 0; q < K; ++q) {
-      const bool gl = fl[q] & 8;
-      const double t0 = gl ? __builtin_bit_cast(double, (uint64_t)g[q].x | ((uint64_t)g[q].y << 32))
-                           : x0[q];
-      const double t1 = gl ? __builtin_bit_cast(double, (uint64_t)g[q].z | ((uint64_t)g[q].w << 32))
-                           : x1[q];
+      double t0 = x0[q], t1 = x1[q];
+#pragma unroll
+      for (int t = 0; t < kRpWinG; ++t)
+        if (qg[t] == q) {  // scalar condition
+          t0 = __builtin_bit_cast(double, (uint64_t)g[t].x | ((uint64_t)g[t].y << 32));
+          t1 = __builtin_bit_cast(double, (uint64_t)g[t].z | ((uint64_t)g[t].w << 32));
+        }
       // an entry a row does not have: +0.0 (its value is 0.0 too), as in rowpair_sums
       const double y0 = (fl[q] & 1) ? t0 : 0.0;
       const double y1 = (fl[q] & 2) ? t1 : 0.0;
@@ -742,17 +760,9 @@ __global__ __launch_bounds__(kRpWinNT) void k_rowpair_win(const uint16_t* __rest
   const int64_t sl = lb * NT + threadIdx.x;
   const int n_pairs_blk = (int)min<int64_t>(NT, (n_rows + 1) / 2 - lb * NT);
   const bool live = threadIdx.x < n_pairs_blk;
-  const int sv = live ? (int)slot[sl] : 0;
-  const int p = sv & 0xff;
-  const int64_t pr = lb * NT + (sv >> 8);
-  const bool both = 2 * pr + 1 < n_rows;
-  const int r = (int)(2 * pr);
-  EpiIn u, w;
-  if (live) epi_load2<OP>(r, both, ep, u, w, tab_dinv, x_op);
-  dbl2 dv = {0.0, 0.0};
-  if (live && tab_dinv) dv = pat_dinv[p];
-  // windows: 16-byte buffer loads, slots before row 0 or past n_cols read zeros; all issued
-  // before the first LDS store
+  // windows: 16-byte buffer loads, slots before row 0 or past n_cols read zeros; issued first
+  // (they need nothing but the block index), before the slot load and the epilogue loads that
+  // depend on it, and all before the first LDS store
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(n_cols * 8), 0x00020000);
@@ -771,14 +781,25 @@ __global__ __launch_bounds__(kRpWinNT) void k_rowpair_win(const uint16_t* __rest
 #ifndef MLAMG_RPW_DBG  // timing variants only (tools/build_variant.sh): 1 no sums, 2 no staging
 #define MLAMG_RPW_DBG 0
 #endif
-  constexpr int WQ = 4;  // slots per thread in registers (C4: 3.9)
+  constexpr int WQ = 4;  // slots per thread in registers (C4: 3.9 with every cluster staged)
+  u32x4 wv[WQ];
   if (!(MLAMG_RPW_DBG & 2)) {
-    u32x4 wv[WQ];
 #pragma unroll
     for (int q = 0; q < WQ; ++q) {
       const int i = threadIdx.x + q * NT;
       if (i < half) wv[q] = wload(i);
     }
+  }
+  const int sv = live ? (int)slot[sl] : 0;
+  const int p = sv & 0xff;
+  const int64_t pr = lb * NT + (sv >> 8);
+  const bool both = 2 * pr + 1 < n_rows;
+  const int r = (int)(2 * pr);
+  EpiIn u, w;
+  if (live) epi_load2<OP>(r, both, ep, u, w, tab_dinv, x_op);
+  dbl2 dv = {0.0, 0.0};
+  if (live && tab_dinv) dv = pat_dinv[p];
+  if (!(MLAMG_RPW_DBG & 2)) {
 #pragma unroll
     for (int q = 0; q < WQ; ++q) {
       const int i = threadIdx.x + q * NT;
@@ -2649,6 +2670,17 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
           else
             hfl[e] |= 8;
         }
+      // the kernel holds at most kRpWinG global entries per step (of kstep entries)
+      for (size_t e0 = 0; ok && e0 < hoff.size(); e0 += kstep) {
+        int ng = 0;
+        for (size_t e = e0; e < std::min(hoff.size(), e0 + kstep); ++e) ng += (hfl[e] & 8) ? 1 : 0;
+        ok = ng <= kRpWinG;
+      }
+      if (!ok) {
+        for (auto& f : hfl) f &= ~8;
+        win.n = 0;
+        win.rows = -1;
+      }
     }
     const size_t ne = hoff.size(), na = std::max<size_t>(ne, 1);
     // interleaved records: (offset, flags) and (row 2i value, row 2i+1 value)
