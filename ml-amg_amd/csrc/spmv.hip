@@ -43,7 +43,10 @@ struct Epi {
 // post-smoothing pass (C4 level-3 A: second pass 28 -> 22 us). Everything else — larger streams,
 // and P / R, read once per cycle — uses non-temporal loads, which leave the MALL to the vectors
 // the next kernel reads (cached P_2 / P_3 / R_3 streams measured 1-3 us slower each).
-constexpr int64_t kCachedNnz = 8 << 20;
+#ifndef MLAMG_CACHED_NNZ  // build-time A/B knob
+#define MLAMG_CACHED_NNZ (8 << 20)
+#endif
+constexpr int64_t kCachedNnz = MLAMG_CACHED_NNZ;
 
 
 // The per-row operands an epilogue reads, fetched apart from the store so kernels can issue

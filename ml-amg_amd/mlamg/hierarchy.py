@@ -208,6 +208,22 @@ class Hierarchy:
         ev[-1][1].synchronize()
         return statistics.median(e0.elapsed_time(e1) for e0, e1 in ev) * 1e3  # us
 
+    # Autotune pruning: the fewest bytes per stored nonzero a format can stream (sorted: 4-byte
+    # packed index + a 1-byte value code when the values fit a dictionary; sell_dict: a 2-byte
+    # code; rowpat: ~0, one byte per pair of rows; vector: 16-bit indices) at the 8 TB/s HBM
+    # peak: no candidate can beat that from a cold cache (the autotune reads 512 MB, twice the
+    # MALL, before each timed launch). A pruned candidate costs nothing but a timing chance:
+    # every format of the family computes the same bits.
+    FORMAT_MIN_BYTES_PER_NNZ = {"csr_stream": 12.0, "sell": 12.0, "sorted": 5.0, "sell_dict": 2.0,
+                                "rowpat": 0.0, "long": 12.0, "vector": 10.0}
+    LB_PEAK_BPS = 8e12
+
+    @classmethod
+    def _lower_bound_us(cls, M, kind, fmt):
+        n_rows, n_cols = M.shape
+        vec = 8.0 * (n_cols + n_rows + (n_rows if kind in ("A", "P") else 0))  # x, y (+ b / y in)
+        return (cls.FORMAT_MIN_BYTES_PER_NNZ[fmt] * M.nnz + vec) / cls.LB_PEAK_BPS * 1e6
+
     # operators whose mean row has at least this many entries use the lane-parallel CSR-vector
     # family (canonical order, one result for every width); shorter rows use the exact-order
     # (scipy) family. A rule on the matrix, not a timing: measured on the C4 hierarchy
@@ -253,7 +269,16 @@ class Hierarchy:
                 x = torch.randn(M.shape[1], dtype=torch.float64, device=dev)
                 y = torch.zeros(M.shape[0], dtype=torch.float64, device=dev)
                 times = {}
+                # most compact formats first; a candidate whose bytes could not move in less
+                # than the best time so far, even at LB_PEAK_BPS, is neither built nor timed
+                # (a timing rule only: every candidate of the family computes the same bits)
+                lbs = {c: self._lower_bound_us(M, name, c[0]) for c in cands}
+                cands.sort(key=lambda c: lbs[c])
+                pruned = []
                 for fmt, arg in cands:
+                    if times and lbs[(fmt, arg)] >= min(times.values()):
+                        pruned.append(f"{fmt}/{arg}")
+                        continue
                     try:
                         times[f"{fmt}/{arg}"] = self._time_format(M, fmt, arg, x, y,
                                                                   kind=name, flush=flush)
@@ -263,7 +288,8 @@ class Hierarchy:
                 best = min(times, key=times.get)
                 fmt, arg = best.split("/")
                 M.set_format(fmt, int(arg))
-                row[name] = {"chosen": best, "us": {k: round(v, 2) for k, v in times.items()}}
+                row[name] = {"chosen": best, "us": {k: round(v, 2) for k, v in times.items()},
+                             "pruned": pruned}
             self.tuning.append(row)
         self.attach_dinvs()
 
