@@ -1187,15 +1187,23 @@ static int launch_vec(const mlamg_csr* A, const double* x, const Epi& ep, hipStr
 // per element ~85, per batch of 8 ~26-33, of 32 ~17-28 — so batches of 32 reads, then 32 adds
 // (software pipelining across batches loses: the register copies between the buffers wait for
 // the fresh reads at the end of every iteration).
+// Batches of 16 (round 3): the 32-read batch needed 64 VGPRs for the batch alone, so the
+// sorted kernel's long-row instantiation (R_1, A_2, P_3 on C4) ran at 80-92 VGPRs, 5 waves per
+// SIMD, i.e. 2 resident 512-thread blocks per CU instead of 4: with 16 it fits 55-60 VGPRs, and
+// the C4 cycle went 0.80 -> 0.77 ms (same box, alternating: 1,225-1,253 -> 1,288-1,307 V-cycles/s).
+#ifndef MLAMG_CHAIN_BATCH  // build-time A/B knob: LDS reads per batch (registers: 2 per read)
+#define MLAMG_CHAIN_BATCH 16
+#endif
 __device__ __forceinline__ double chain_sum(const double* __restrict__ p, int ka, int kb,
                                             double s) {
+  constexpr int CB = MLAMG_CHAIN_BATCH;
   int k = ka;
-  for (; k + 32 <= kb; k += 32) {
-    double v[32];
+  for (; k + CB <= kb; k += CB) {
+    double v[CB];
 #pragma unroll
-    for (int u = 0; u < 32; ++u) v[u] = p[k + u];
+    for (int u = 0; u < CB; ++u) v[u] = p[k + u];
 #pragma unroll
-    for (int u = 0; u < 32; ++u) s += v[u];
+    for (int u = 0; u < CB; ++u) s += v[u];
   }
   for (; k + 8 <= kb; k += 8) {
     double v[8];
@@ -1248,8 +1256,13 @@ __device__ __forceinline__ void sum_two_rows(const double* __restrict__ p, int a
 // operators: Galerkin A_l, R = P^T). Products are written to LDS at their CSR slot and phase 2
 // sums every row in stored order, so the result is bitwise k_csr_stream's (scipy's).
 // VD: values come from a <= 256-entry dictionary (one byte per nonzero instead of eight)
+#ifndef MLAMG_SRT_WAVES  // minimum waves per SIMD the register allocation must allow (0: free)
+#define MLAMG_SRT_WAVES 0
+#endif
 template <int OP, bool NORM, bool VD, bool LR>
-__global__ __launch_bounds__(kSrtThreads) void k_sorted(const int32_t* __restrict__ indptr,
+__global__ __launch_bounds__(kSrtThreads)
+__attribute__((amdgpu_waves_per_eu(MLAMG_SRT_WAVES > 0 ? MLAMG_SRT_WAVES : 1, 8)))
+void k_sorted(const int32_t* __restrict__ indptr,
                                                         const uint32_t* __restrict__ pk,
                                                         const double* __restrict__ av,
                                                         const uint8_t* __restrict__ vi,
