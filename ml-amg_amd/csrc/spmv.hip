@@ -563,8 +563,12 @@ __device__ __forceinline__ void rowpair_sums(const double* __restrict__ x, int64
 // CH chunks of 256 pairs per workgroup (tables staged once; the next chunk's pattern ids are
 // fetched while the current chunk gathers). MLAMG_RP_WAVES: minimum waves per SIMD the register
 // allocation must leave room for (0 = compiler's choice; build-time knob for A/B runs)
+// 5 (round 3): the end-of-cycle instantiation (residual + norm + fused next sweep) took 115
+// VGPRs, 4 waves per SIMD; at 5 it fits 96 with no spill (the others 91-94): that kernel 67 -> 58
+// us, the cycle 813 -> 802 us traced, bench +0.6-1.2 % alternating on one box (6: spills, 10 %
+// slower; profiles/r03/final/ab_rowpair_waves*.txt)
 #ifndef MLAMG_RP_WAVES
-#define MLAMG_RP_WAVES 0
+#define MLAMG_RP_WAVES 5
 #endif
 template <int OP, bool NORM, int CH, int K>
 __global__ __launch_bounds__(kThreads)
