@@ -251,12 +251,24 @@ int mlamg_gnn_edge_mlp(const int32_t* src, const int32_t* tgt, const float* X, i
 int mlamg_gnn_topk(const float* scores, int64_t n, int64_t k, float* vec, int32_t* idx,
                    void* stream);
 
-/* Seeded Bellman-Ford (ns/lib/graph.py:7-53) on edge weights G (row i -> col j, weight g_ij,
- * evaluated in fp32 like the torch reference). dist_f32[n], cluster[n] (node id of the nearest
- * seed, -1 if unreachable). Ties broken deterministically by the smallest seed node id.
- * *iters_host = number of synchronous sweeps. Syncs. */
+/* Seeded Bellman-Ford exactly as the reference's modified_bellman_ford (ns/lib/graph.py:7-53;
+ * replaces that call at utils/evaluate_model.py:57, utils/evaluate_dataset.py:87): sweeps over
+ * the edges (i -> j, weight g_ij rounded to fp32 like the torch COO values, ns/lib/sparse.py:28)
+ * in row-major order, in place, `if d_i + g_ij < d_j: d_j = d_i + g_ij; nearest_j = nearest_i`
+ * in fp32, until a sweep updates nothing. Run level-scheduled (csrc/graph.hip), so distances
+ * AND nearest seeds, ties included, are bitwise the reference's. dist_f32[n] (+inf unreached),
+ * nearest[n] (seed node id, -1 unreached: the reference leaves 0 there), *sweeps_host = the
+ * reference's sweep count (the last one updates nothing). EINVAL on a negative self-loop or no
+ * fixed point after n + 2 sweeps (the reference would never return). Syncs. */
 int mlamg_bellman_ford(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* dist_f32,
-                       int32_t* cluster, int32_t* iters_host, void* stream);
+                       int32_t* nearest, int32_t* sweeps_host, void* stream);
+
+/* Order-independent seeded Bellman-Ford (the multilevel / distributed hierarchy's aggregation,
+ * which has no reference counterpart): the same fp32 distances (the order-independent fixed
+ * point), label = smallest seed node id over tight in-edges; = mlamg_bellman_ford's labels
+ * whenever shortest paths are unique. Multi-workgroup sweeps. *iters_host = synchronous sweeps. */
+int mlamg_bellman_ford_canon(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* dist_f32,
+                             int32_t* cluster, int32_t* iters_host, void* stream);
 
 /* pyamg 4.x graph.bellman_ford(G, seeds) exactly (the aggregation step of FullAggNet.forward,
  * ns/model/agg_interp.py:475; replaces that call): sequential in-place pull sweeps
@@ -279,11 +291,19 @@ int mlamg_aggregate_op(const int32_t* col, int64_t n, int64_t k, mlamg_csr** out
 int mlamg_labels_to_columns(const int32_t* label, int64_t n, const int32_t* seeds, int32_t k,
                             int32_t* col, void* stream);
 
-/* pyamg 4.x lloyd_cluster (called at ns/lib/graph.py:232): up to maxiter rounds of
- * {outward Bellman-Ford, boundary detection, inward Bellman-Ford, recentre}, fp64 distances.
- * seeds (DEVICE, k) updated in place; dist[n], cluster[n] (aggregate index, -1 none). Syncs. */
+/* pyamg 4.x lloyd_cluster (called at ns/lib/graph.py:232 and behind
+ * pyamg.aggregation.lloyd_aggregation, utils/common.py:91): up to maxiter rounds of {outward
+ * Bellman-Ford, boundary detection, inward Bellman-Ford, recentre}, fp64 distances, the outward
+ * pass in amg_core's sequential sweep order, so clusters and new seeds are bitwise pyamg's,
+ * ties included. seeds (DEVICE, k) updated in place; dist[n], cluster[n] (aggregate index,
+ * -1 none); *iters_host = rounds run (stops early when no seed moves). Syncs. */
 int mlamg_lloyd_cluster(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxiter, double* dist,
                         int32_t* cluster, int32_t* iters_host, void* stream);
+
+/* The same with the order-independent label rule (min cluster index over tight pull
+ * neighbours) and multi-workgroup sweeps: the hierarchy's Lloyd option. */
+int mlamg_lloyd_cluster_canon(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxiter,
+                              double* dist, int32_t* cluster, int32_t* iters_host, void* stream);
 
 /* ---------------------------------------------------------------- Gauss-Seidel
  * pyamg relaxation.gauss_seidel (forward lexicographic, in place) used by the reference driver

@@ -1,18 +1,24 @@
 // Aggregation kernels: seeded Bellman-Ford (ns/lib/graph.py:7-53), aggregate operator
-// (graph.py:56-86, 234-238) and pyamg 4.x lloyd_cluster (called at graph.py:232).
+// (graph.py:56-86, 234-238), pyamg 4.x lloyd_cluster (called at graph.py:232) and pyamg 4.x
+// graph.bellman_ford (ns/model/agg_interp.py:475).
 //
-// Distances. The reference relaxes edges sequentially in place; every relaxation is the
-// monotone map d_j <- min(d_j, fl(d_i + w_ij)). Any fair order of monotone relaxations from the
-// same start reaches the same (greatest) common fixed point, so the parallel in-place sweeps
-// here (atomicMin on the order-preserving bit pattern of non-negative floats) end on exactly
-// the reference distances, bit for bit, in fp32 (torch) or fp64 (pyamg) arithmetic.
-// Labels. Which seed wins a node whose shortest path is not unique depends on the sequential
-// sweep order, which a parallel sweep cannot reproduce. The rule here is order-independent:
-// label(j) = min over tight in-edges (fl(d_i + w_ij) == d_j) of label(i), seeds labelled by
-// themselves. With unique shortest paths (tie-free weights) it equals the reference's label.
+// Two label rules.
+// * Reference order (the drop-in entry points mlamg_bellman_ford, mlamg_lloyd_cluster,
+//   mlamg_bellman_ford_pyamg). The reference sweeps are sequential and in place, so which seed
+//   wins a node whose shortest path is not unique depends on the sweep order. These entry points
+//   run that order itself, level-scheduled (below), so distances AND labels are bitwise the
+//   reference's on every input, ties included.
+// * Order-independent (mlamg_bellman_ford_canon, mlamg_lloyd_cluster_canon; the multilevel and
+//   distributed hierarchy, which have no reference counterpart). Every relaxation is the monotone
+//   map d_j <- min(d_j, fl(d_i + w_ij)); any fair order of monotone relaxations from the same
+//   start reaches the same (greatest) common fixed point, so parallel in-place sweeps (atomicMin
+//   on the order-preserving bit pattern of non-negative floats) end on exactly the reference
+//   distances. label(j) = min over tight in-edges (fl(d_i + w_ij) == d_j) of label(i), seeds
+//   labelled by themselves; with unique shortest paths it equals the reference's label.
 #include "common.hpp"
 
 #include <cfloat>
+#include <limits>
 
 namespace mlamg {
 
@@ -136,7 +142,7 @@ __global__ void k_ll_seeds(const int32_t* __restrict__ s, int32_t k, double* __r
   int t = blockIdx.x * 256 + threadIdx.x;
   if (t >= k) return;
   d[s[t]] = 0.0;
-  c[s[t]] = t;
+  atomicMax(c + s[t], t);  // c starts at -1; a repeated seed keeps its last index, as amg_core
 }
 
 __global__ void k_ll_pull(const int32_t* __restrict__ ip, const int32_t* __restrict__ ij,
@@ -234,16 +240,28 @@ __global__ void k_mark_seeds(const int32_t* __restrict__ s, int32_t k, int32_t* 
   if (t < k) f[s[t]] = 1;
 }
 
-// ---------------------------------------------------------------- pyamg 4.x bellman_ford (exact)
-// pyamg.graph.bellman_ford (the aggregation step of FullAggNet.forward, ns/model/agg_interp.py
-// :475): amg_core sweeps rows 0..n-1 in place, x_i <- min(x_i, fl(G_ij + x_j)) in the graph's
-// dtype with a strict <, nearest seed taken from the first strictly better neighbour, until a
-// sweep changes no distance. Labels then depend on the sweep order, so this is the sequential
-// sweep itself, run level-scheduled in one workgroup: level(i) = 1 + max level(j) over j < i
-// coupled to i in either direction (the Gauss-Seidel schedule of gs.hip). A level's rows see the
-// final values of every earlier-coupled row and the old values of every later-coupled one, and
-// rows of a level touch no common entry: every (x, z) is bit for bit the sequential sweep's.
+// ---------------------------------------------------------------- sequential sweeps (exact)
+// pyamg's pull sweep (amg_core bellman_ford: graph.bellman_ford at ns/model/agg_interp.py:475,
+// and the outward pass of lloyd_cluster behind ns/lib/graph.py:232): rows 0..n-1 in place,
+// x_i <- min(x_i, fl(G_ij + x_j)) over the row's stored entries with a strict <, the label taken
+// from the first strictly better neighbour, until a sweep changes no distance. Run
+// level-scheduled: level(i) = 1 + max level(j) over j < i coupled to i in either direction (the
+// Gauss-Seidel schedule of gs.hip). A level's rows see the final values of every earlier-coupled
+// row and the old values of every later-coupled one, and rows of a level touch no common entry:
+// every (x, z) is bit for bit the sequential sweep's.
+//
+// The reference's push sweep (ns/lib/graph.py:40-51, modified_bellman_ford): for every edge
+// (i, j) of the coalesced COO in row-major order, in place, fp32, strict <,
+// `if d[i] + w_ij < d[j]: d[j] = d[i] + w_ij; nearest[j] = nearest[i]`. Row i's pushes use d[i]
+// as it stands when row i is reached: its value at the end of the previous sweep folded with the
+// pushes of the rows k < i into it, in ascending k. Call that mid_i. Node j ends the sweep at
+// mid_j folded further with the pushes of the rows k > j, which also carry their mid_k, again in
+// ascending k. So a sweep is two passes over the in-edge lists (transpose, sources ascending):
+// mid, level-scheduled on in-edges from lower rows (level(j) = 1 + max level(k), k < j, k -> j),
+// then end, fully parallel. A self-loop never pushes when w_jj >= 0; a negative one makes the
+// reference loop forever and is refused.
 constexpr int kBfBlock = 1024;
+constexpr int64_t kSeqOneBlockMax = 1 << 18;  // wider graphs: one launch per level
 
 template <typename T>
 __global__ void k_bfp_init(T* __restrict__ x, int32_t* __restrict__ z, int64_t n, T big) {
@@ -261,6 +279,27 @@ __global__ void k_bfp_seeds(const int32_t* __restrict__ s, int32_t k, T* __restr
   z[s[t]] = s[t];
 }
 
+// one row of the pull sweep; returns whether x_i changed
+template <typename T>
+__device__ inline int pull_row(int32_t i, const int32_t* __restrict__ ip,
+                               const int32_t* __restrict__ ij, const double* __restrict__ ax,
+                               T* x, int32_t* z) {
+  const T x0 = x[i];
+  T xi = x0;
+  int32_t zi = z[i];
+  for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
+    const int32_t j = ij[k];
+    const T d = (T)ax[k] + x[j];  // the row's own entry reads the old x_i, as amg_core
+    if (d < xi) {
+      xi = d;
+      zi = z[j];
+    }
+  }
+  x[i] = xi;
+  z[i] = zi;
+  return xi != x0;  // pyamg: (old_distances == distances).all()
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBfBlock) void k_bf_pyamg(const int32_t* __restrict__ ip,
                                                        const int32_t* __restrict__ ij,
@@ -274,27 +313,15 @@ __global__ __launch_bounds__(kBfBlock) void k_bf_pyamg(const int32_t* __restrict
   do {
     if (threadIdx.x == 0) changed = 0;
     __syncthreads();
+    int any = 0;
     for (int32_t l = 0; l < n_levels; ++l) {
       const int32_t a = lptr[l], e = lptr[l + 1];
-      for (int32_t t = a + (int32_t)threadIdx.x; t < e; t += kBfBlock) {
-        const int32_t i = rows[t];
-        const T x0 = x[i];
-        T xi = x0;
-        int32_t zi = z[i];
-        for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
-          const int32_t j = ij[k];
-          const T d = (T)ax[k] + x[j];  // the row's own entry reads the old x_i, as amg_core
-          if (d < xi) {
-            xi = d;
-            zi = z[j];
-          }
-        }
-        if (xi != x0) changed = 1;  // pyamg: (old_distances == distances).all()
-        x[i] = xi;
-        z[i] = zi;
-      }
+      for (int32_t t = a + (int32_t)threadIdx.x; t < e; t += kBfBlock)
+        any |= pull_row<T>(rows[t], ip, ij, ax, x, z);
       __syncthreads();
     }
+    if (any) changed = 1;
+    __syncthreads();
     ++sweeps;
     c = changed;
     __syncthreads();  // every thread has read the flag before it is reset
@@ -305,11 +332,302 @@ __global__ __launch_bounds__(kBfBlock) void k_bf_pyamg(const int32_t* __restrict
   }
 }
 
+// one level of the pull sweep over the whole GPU (graphs above kSeqOneBlockMax rows)
+template <typename T>
+__global__ void k_bfp_level(const int32_t* __restrict__ ip, const int32_t* __restrict__ ij,
+                            const double* __restrict__ ax, const int32_t* __restrict__ rows,
+                            int32_t cnt, T* x, int32_t* z, int32_t* __restrict__ changed) {
+  const int32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= cnt) return;
+  if (pull_row<T>(rows[t], ip, ij, ax, x, z)) *changed = 1;
+}
+
+// push sweep: mid_j (in-edges from rows k < j) and end_j (then rows k > j), see above
+__device__ inline void push_mid(int32_t j, const int32_t* __restrict__ tip,
+                                const int32_t* __restrict__ tsrc, const float* __restrict__ tw,
+                                const float* d, const int32_t* z, float* dm, int32_t* zm) {
+  float cur = d[j];
+  int32_t lab = z[j];
+  for (int32_t e = tip[j]; e < tip[j + 1]; ++e) {
+    const int32_t k = tsrc[e];
+    if (k >= j) break;
+    const float cand = dm[k] + tw[e];
+    if (cand < cur) {
+      cur = cand;
+      lab = zm[k];
+    }
+  }
+  dm[j] = cur;
+  zm[j] = lab;
+}
+__device__ inline int push_end(int32_t j, const int32_t* __restrict__ tip,
+                               const int32_t* __restrict__ tsrc, const float* __restrict__ tw,
+                               float* d, int32_t* z, const float* dm, const int32_t* zm) {
+  float cur = dm[j];
+  int32_t lab = zm[j];
+  int32_t e0 = tip[j];
+  while (e0 < tip[j + 1] && tsrc[e0] <= j) ++e0;
+  for (int32_t e = e0; e < tip[j + 1]; ++e) {
+    const int32_t k = tsrc[e];
+    const float cand = dm[k] + tw[e];
+    if (cand < cur) {
+      cur = cand;
+      lab = zm[k];
+    }
+  }
+  const int ch = cur < d[j];  // distances only decrease: any update leaves end < start
+  d[j] = cur;
+  z[j] = lab;
+  return ch;
+}
+
+__global__ __launch_bounds__(kBfBlock) void k_bf_push(
+    const int32_t* __restrict__ tip, const int32_t* __restrict__ tsrc,
+    const float* __restrict__ tw, const int32_t* __restrict__ rows,
+    const int32_t* __restrict__ lptr, int32_t n_levels, int32_t n, int32_t max_sweeps, float* d,
+    int32_t* z, float* dm, int32_t* zm, int32_t* __restrict__ out) {
+  __shared__ int32_t changed;
+  int32_t sweeps = 0, c = 0;
+  do {
+    if (threadIdx.x == 0) changed = 0;
+    __syncthreads();
+    for (int32_t l = 0; l < n_levels; ++l) {
+      const int32_t a = lptr[l], e = lptr[l + 1];
+      for (int32_t t = a + (int32_t)threadIdx.x; t < e; t += kBfBlock)
+        push_mid(rows[t], tip, tsrc, tw, d, z, dm, zm);
+      __syncthreads();
+    }
+    int any = 0;
+    for (int32_t j = (int32_t)threadIdx.x; j < n; j += kBfBlock)
+      any |= push_end(j, tip, tsrc, tw, d, z, dm, zm);
+    if (any) changed = 1;
+    __syncthreads();
+    ++sweeps;
+    c = changed;
+    __syncthreads();
+  } while (c && sweeps < max_sweeps);
+  if (threadIdx.x == 0) {
+    out[0] = sweeps;
+    out[1] = c;
+  }
+}
+__global__ void k_push_level(const int32_t* __restrict__ tip, const int32_t* __restrict__ tsrc,
+                             const float* __restrict__ tw, const int32_t* __restrict__ rows,
+                             int32_t cnt, const float* d, const int32_t* z, float* dm,
+                             int32_t* zm) {
+  const int32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t < cnt) push_mid(rows[t], tip, tsrc, tw, d, z, dm, zm);
+}
+__global__ void k_push_end(const int32_t* __restrict__ tip, const int32_t* __restrict__ tsrc,
+                           const float* __restrict__ tw, int32_t n, float* d, int32_t* z,
+                           const float* dm, const int32_t* zm, int32_t* __restrict__ changed) {
+  const int32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j < n && push_end(j, tip, tsrc, tw, d, z, dm, zm)) *changed = 1;
+}
+
 static inline dim3 g1(int64_t n) { return dim3((unsigned)std::max<int64_t>(1, (n + 255) / 256)); }
 
 static int read_flag(int32_t* dflag, hipStream_t s, int32_t* out) {
   MLAMG_HIP(hipMemcpyAsync(out, dflag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   MLAMG_HIP(hipStreamSynchronize(s));
+  return MLAMG_OK;
+}
+
+// ---------------------------------------------------------------- sequential-sweep plans (host)
+// lptr[nlev + 1] | rows[n] (level order) | out[2] (sweeps, unconverged) [| tip[n+1] | tsrc[nnz]]
+struct SeqPlan {
+  int32_t* d = nullptr;  // device copy of the int32 plan
+  float* tw = nullptr;   // push plan: in-edge weights (fp32), source order
+  int32_t nlev = 0;
+  int64_t n = 0, nnz = 0;
+  ~SeqPlan() {
+    if (d) (void)hipFree(d);
+    if (tw) (void)hipFree(tw);
+  }
+  const int32_t* lptr() const { return d; }
+  const int32_t* rows() const { return d + nlev + 1; }
+  int32_t* out() const { return d + nlev + 1 + n; }
+  const int32_t* tip() const { return d + nlev + 1 + n + 2; }
+  const int32_t* tsrc() const { return d + nlev + 1 + n + 2 + n + 1; }
+  std::vector<int32_t> h_lptr;  // host copy of lptr (per-level launches)
+};
+
+static int fetch_pattern(const mlamg_csr* G, hipStream_t s, std::vector<int32_t>& ip,
+                         std::vector<int32_t>& ij, std::vector<double>* ax) {
+  const int64_t n = G->n_rows;
+  ip.assign(n + 1, 0);
+  ij.assign(G->nnz, 0);
+  MLAMG_HIP(hipMemcpyAsync(ip.data(), G->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, s));
+  if (G->nnz)
+    MLAMG_HIP(hipMemcpyAsync(ij.data(), G->indices, sizeof(int32_t) * G->nnz, hipMemcpyDeviceToHost, s));
+  if (ax) {
+    ax->assign(G->nnz, 0.0);
+    if (G->nnz)
+      MLAMG_HIP(hipMemcpyAsync(ax->data(), G->data, sizeof(double) * G->nnz, hipMemcpyDeviceToHost, s));
+  }
+  MLAMG_HIP(hipStreamSynchronize(s));
+  return MLAMG_OK;
+}
+
+// rows bucketed by level; extra = trailing int32 words reserved after rows | out
+static void plan_levels(const std::vector<int32_t>& level, int32_t nlev, size_t extra,
+                        std::vector<int32_t>& plan) {
+  const int64_t n = (int64_t)level.size();
+  plan.assign((size_t)nlev + 1 + n + 2 + extra, 0);
+  int32_t* lp = plan.data();
+  for (int64_t i = 0; i < n; ++i) lp[level[i] + 1]++;
+  for (int32_t l = 0; l < nlev; ++l) lp[l + 1] += lp[l];
+  std::vector<int32_t> fill(lp, lp + nlev);
+  int32_t* rows = lp + nlev + 1;
+  for (int64_t i = 0; i < n; ++i) rows[fill[level[i]]++] = (int32_t)i;
+}
+
+// pull sweep (pyamg): level(i) = 1 + max level(j) over j < i coupled either way
+static int build_pull_plan(const mlamg_csr* G, hipStream_t s, SeqPlan& P) {
+  const int64_t n = G->n_rows;
+  std::vector<int32_t> ip, ij;
+  MLAMG_TRY(fetch_pattern(G, s, ip, ij, nullptr));
+  std::vector<int32_t> level(n, 0), req(n, 0);
+  int32_t nlev = n ? 1 : 0;
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t L = req[i];
+    for (int32_t q = ip[i]; q < ip[i + 1]; ++q)
+      if (ij[q] < i) L = std::max(L, level[ij[q]] + 1);
+    level[i] = L;
+    for (int32_t q = ip[i]; q < ip[i + 1]; ++q)
+      if (ij[q] > i) req[ij[q]] = std::max(req[ij[q]], L + 1);
+    nlev = std::max(nlev, L + 1);
+  }
+  std::vector<int32_t> plan;
+  plan_levels(level, nlev, 0, plan);
+  P.n = n;
+  P.nnz = G->nnz;
+  P.nlev = nlev;
+  P.h_lptr.assign(plan.begin(), plan.begin() + nlev + 1);
+  MLAMG_HIP(hipMalloc(&P.d, sizeof(int32_t) * plan.size()));
+  MLAMG_HIP(hipMemcpyAsync(P.d, plan.data(), sizeof(int32_t) * plan.size(), hipMemcpyHostToDevice, s));
+  MLAMG_HIP(hipStreamSynchronize(s));  // `plan` is pageable and goes out of scope
+  return MLAMG_OK;
+}
+
+// pull sweeps to the fixed point on (x, z); *sweeps = pyamg's count (the last changes nothing)
+template <typename T>
+static int run_pull(const mlamg_csr* G, const SeqPlan& P, T* x, int32_t* z, hipStream_t s,
+                    int32_t* sweeps) {
+  const int64_t n = P.n;
+  if (n == 0) {
+    *sweeps = 1;
+    return MLAMG_OK;
+  }
+  // nonnegative weights converge within n + 1 sweeps; more means a negative cycle, on which
+  // pyamg would never return
+  const int32_t max_sweeps = (int32_t)std::min<int64_t>(n + 2, INT32_MAX);
+  int32_t res[2] = {0, 0};
+  if (n <= kSeqOneBlockMax) {
+    hipLaunchKernelGGL(k_bf_pyamg<T>, dim3(1), dim3(kBfBlock), 0, s, G->indptr, G->indices,
+                       G->data, P.rows(), P.lptr(), P.nlev, max_sweeps, x, z, P.out());
+    MLAMG_HIP(hipGetLastError());
+    MLAMG_HIP(hipMemcpyAsync(res, P.out(), sizeof(res), hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipStreamSynchronize(s));
+  } else {
+    int32_t h = 1;
+    while (h && res[0] < max_sweeps) {
+      MLAMG_HIP(hipMemsetAsync(P.out() + 1, 0, sizeof(int32_t), s));
+      for (int32_t l = 0; l < P.nlev; ++l) {
+        const int32_t a = P.h_lptr[l], cnt = P.h_lptr[l + 1] - a;
+        hipLaunchKernelGGL(k_bfp_level<T>, g1(cnt), dim3(256), 0, s, G->indptr, G->indices,
+                           G->data, P.rows() + a, cnt, x, z, P.out() + 1);
+      }
+      MLAMG_HIP(hipGetLastError());
+      MLAMG_TRY(read_flag(P.out() + 1, s, &h));
+      ++res[0];
+    }
+    res[1] = h;
+  }
+  MLAMG_REQUIRE(res[1] == 0, "bellman_ford: no fixed point after n + 2 sweeps (negative cycle)");
+  *sweeps = res[0];
+  return MLAMG_OK;
+}
+
+// push sweep (ns/lib/graph.py:40-51): in-edge lists with sources ascending, fp32 weights, and
+// the mid-pass schedule level(j) = 1 + max level(k) over edges k -> j with k < j
+static int build_push_plan(const mlamg_csr* G, hipStream_t s, SeqPlan& P) {
+  const int64_t n = G->n_rows, nnz = G->nnz;
+  std::vector<int32_t> ip, ij;
+  std::vector<double> ax;
+  MLAMG_TRY(fetch_pattern(G, s, ip, ij, &ax));
+  std::vector<int32_t> level(n, 0);
+  int32_t nlev = n ? 1 : 0;
+  for (int64_t k = 0; k < n; ++k) {
+    nlev = std::max(nlev, level[k] + 1);
+    for (int32_t q = ip[k]; q < ip[k + 1]; ++q) {
+      const int32_t j = ij[q];
+      if (j == k) MLAMG_REQUIRE(!((float)ax[q] < 0.0f),
+                                "negative self-loop weight: the reference sweep never terminates");
+      if (j > k) level[j] = std::max(level[j], level[k] + 1);
+    }
+  }
+  std::vector<int32_t> plan;
+  plan_levels(level, nlev, (size_t)(n + 1 + nnz), plan);
+  int32_t* tip = plan.data() + nlev + 1 + n + 2;
+  int32_t* tsrc = tip + n + 1;
+  std::vector<float> tw(std::max<int64_t>(nnz, 1));
+  for (int64_t q = 0; q < nnz; ++q) tip[ij[q] + 1]++;
+  for (int64_t j = 0; j < n; ++j) tip[j + 1] += tip[j];
+  std::vector<int32_t> fill(tip, tip + n);
+  for (int64_t k = 0; k < n; ++k)  // sources ascending: the reference's row-major push order
+    for (int32_t q = ip[k]; q < ip[k + 1]; ++q) {
+      const int32_t p = fill[ij[q]]++;
+      tsrc[p] = (int32_t)k;
+      tw[p] = (float)ax[q];  // torch COO values are fp32 (ns/lib/sparse.py:28)
+    }
+  P.n = n;
+  P.nnz = nnz;
+  P.nlev = nlev;
+  P.h_lptr.assign(plan.begin(), plan.begin() + nlev + 1);
+  MLAMG_HIP(hipMalloc(&P.d, sizeof(int32_t) * plan.size()));
+  MLAMG_HIP(hipMalloc(&P.tw, sizeof(float) * tw.size()));
+  MLAMG_HIP(hipMemcpyAsync(P.d, plan.data(), sizeof(int32_t) * plan.size(), hipMemcpyHostToDevice, s));
+  MLAMG_HIP(hipMemcpyAsync(P.tw, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice, s));
+  MLAMG_HIP(hipStreamSynchronize(s));
+  return MLAMG_OK;
+}
+
+static int run_push(const SeqPlan& P, float* d, int32_t* z, float* dm, int32_t* zm, hipStream_t s,
+                    int32_t* sweeps) {
+  const int64_t n = P.n;
+  if (n == 0) {
+    *sweeps = 1;
+    return MLAMG_OK;
+  }
+  const int32_t max_sweeps = (int32_t)std::min<int64_t>(n + 2, INT32_MAX);
+  int32_t res[2] = {0, 0};
+  if (n <= kSeqOneBlockMax) {
+    hipLaunchKernelGGL(k_bf_push, dim3(1), dim3(kBfBlock), 0, s, P.tip(), P.tsrc(), P.tw,
+                       P.rows(), P.lptr(), P.nlev, (int32_t)n, max_sweeps, d, z, dm, zm, P.out());
+    MLAMG_HIP(hipGetLastError());
+    MLAMG_HIP(hipMemcpyAsync(res, P.out(), sizeof(res), hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipStreamSynchronize(s));
+  } else {
+    int32_t h = 1;
+    while (h && res[0] < max_sweeps) {
+      MLAMG_HIP(hipMemsetAsync(P.out() + 1, 0, sizeof(int32_t), s));
+      for (int32_t l = 0; l < P.nlev; ++l) {
+        const int32_t a = P.h_lptr[l], cnt = P.h_lptr[l + 1] - a;
+        hipLaunchKernelGGL(k_push_level, g1(cnt), dim3(256), 0, s, P.tip(), P.tsrc(), P.tw,
+                           P.rows() + a, cnt, d, z, dm, zm);
+      }
+      hipLaunchKernelGGL(k_push_end, g1(n), dim3(256), 0, s, P.tip(), P.tsrc(), P.tw, (int32_t)n,
+                         d, z, dm, zm, P.out() + 1);
+      MLAMG_HIP(hipGetLastError());
+      MLAMG_TRY(read_flag(P.out() + 1, s, &h));
+      ++res[0];
+    }
+    res[1] = h;
+  }
+  MLAMG_REQUIRE(res[1] == 0, "modified_bellman_ford: no fixed point after n + 2 sweeps "
+                             "(negative cycle: the reference would not return)");
+  *sweeps = res[0];
   return MLAMG_OK;
 }
 
@@ -319,8 +637,8 @@ using namespace mlamg;
 
 extern "C" {
 
-int mlamg_bellman_ford(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* dist,
-                       int32_t* cluster, int32_t* iters_host, void* stream) {
+int mlamg_bellman_ford_canon(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* dist,
+                             int32_t* cluster, int32_t* iters_host, void* stream) {
   MLAMG_REQUIRE(G && dist && cluster && (k == 0 || seeds), "NULL argument");
   MLAMG_REQUIRE(G->n_rows == G->n_cols, "graph must be square");
   hipStream_t s = S(stream);
@@ -368,6 +686,38 @@ int mlamg_bellman_ford(const mlamg_csr* G, const int32_t* seeds, int32_t k, floa
   return MLAMG_OK;
 }
 
+int mlamg_bellman_ford(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* dist,
+                       int32_t* nearest, int32_t* sweeps_host, void* stream) {
+  MLAMG_REQUIRE(G && dist && nearest && (k == 0 || seeds), "NULL argument");
+  MLAMG_REQUIRE(G->n_rows == G->n_cols, "graph must be square");
+  MLAMG_REQUIRE(k >= 0, "negative seed count");
+  hipStream_t s = S(stream);
+  const int64_t n = G->n_rows;
+  MLAMG_REQUIRE(n < INT32_MAX, "graph too large for int32 rows");
+  int64_t bad = 0;
+  MLAMG_TRY(count_out_of_range(seeds, k, 0, n, s, &bad));
+  MLAMG_REQUIRE(bad == 0, "seed index out of range [0, n)");
+  SeqPlan P;
+  MLAMG_TRY(build_push_plan(G, s, P));
+  float* dm = nullptr;
+  MLAMG_HIP(hipMalloc(&dm, sizeof(float) * 2 * std::max<int64_t>(n, 1)));
+  struct Free {
+    void* a;
+    ~Free() { (void)hipFree(a); }
+  } guard{dm};
+  int32_t* zm = reinterpret_cast<int32_t*>(dm + std::max<int64_t>(n, 1));
+  // graph.py:30-35: distance inf, nearest 0 (here -1: an unreached node never pushes, so the
+  // initial label is only ever read back), centers 0 / themselves
+  if (n) hipLaunchKernelGGL(k_bfp_init<float>, g1(n), dim3(256), 0, s, dist, nearest, n,
+                            std::numeric_limits<float>::infinity());
+  if (k) hipLaunchKernelGGL(k_bfp_seeds<float>, g1(k), dim3(256), 0, s, seeds, k, dist, nearest);
+  MLAMG_HIP(hipGetLastError());
+  int32_t sweeps = 0;
+  MLAMG_TRY(run_push(P, dist, nearest, dm, zm, s, &sweeps));
+  if (sweeps_host) *sweeps_host = sweeps;
+  return MLAMG_OK;
+}
+
 int mlamg_bellman_ford_pyamg(const mlamg_csr* G, const int32_t* seeds, int32_t k, int fp64,
                              void* dist, int32_t* nearest, int32_t* sweeps_host, void* stream) {
   MLAMG_REQUIRE(G && dist && nearest && (k == 0 || seeds), "NULL argument");
@@ -380,62 +730,23 @@ int mlamg_bellman_ford_pyamg(const mlamg_csr* G, const int32_t* seeds, int32_t k
   int64_t bad = 0;
   MLAMG_TRY(count_out_of_range(seeds, k, 0, n, s, &bad));
   MLAMG_REQUIRE(bad == 0, "seed index out of range [0, n)");
-  // level schedule of the sequential sweep (host, O(nnz))
-  std::vector<int32_t> ip(n + 1), ij(G->nnz);
-  MLAMG_HIP(hipMemcpyAsync(ip.data(), G->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, s));
-  if (G->nnz)
-    MLAMG_HIP(hipMemcpyAsync(ij.data(), G->indices, sizeof(int32_t) * G->nnz, hipMemcpyDeviceToHost, s));
-  MLAMG_HIP(hipStreamSynchronize(s));
-  std::vector<int32_t> level(n, 0), req(n, 0);
-  int32_t nlev = n ? 1 : 0;
-  for (int64_t i = 0; i < n; ++i) {
-    int32_t L = req[i];
-    for (int32_t q = ip[i]; q < ip[i + 1]; ++q)
-      if (ij[q] < i) L = std::max(L, level[ij[q]] + 1);
-    level[i] = L;
-    for (int32_t q = ip[i]; q < ip[i + 1]; ++q)
-      if (ij[q] > i) req[ij[q]] = std::max(req[ij[q]], L + 1);
-    nlev = std::max(nlev, L + 1);
-  }
-  std::vector<int32_t> plan((size_t)nlev + 1 + n + 2, 0);  // lptr | rows | out
-  int32_t* lp = plan.data();
-  for (int64_t i = 0; i < n; ++i) lp[level[i] + 1]++;
-  for (int32_t l = 0; l < nlev; ++l) lp[l + 1] += lp[l];
-  std::vector<int32_t> fill(lp, lp + nlev);
-  int32_t* rows = lp + nlev + 1;
-  for (int64_t i = 0; i < n; ++i) rows[fill[level[i]]++] = (int32_t)i;
-  int32_t* dplan = nullptr;
-  MLAMG_HIP(hipMalloc(&dplan, sizeof(int32_t) * plan.size()));
-  struct Free {
-    void* a;
-    ~Free() { (void)hipFree(a); }
-  } guard{dplan};
-  MLAMG_HIP(hipMemcpyAsync(dplan, plan.data(), sizeof(int32_t) * plan.size(), hipMemcpyHostToDevice, s));
-  int32_t* dout = dplan + nlev + 1 + n;
-  // nonnegative weights converge within n + 1 sweeps; more means a negative cycle, on which
-  // pyamg would never return
-  const int32_t max_sweeps = (int32_t)std::min<int64_t>(n + 2, INT32_MAX);
+  SeqPlan P;
+  MLAMG_TRY(build_pull_plan(G, s, P));
+  int32_t sweeps = 0;
   if (fp64) {
     double* x = static_cast<double*>(dist);
     if (n) hipLaunchKernelGGL(k_bfp_init<double>, g1(n), dim3(256), 0, s, x, nearest, n, DBL_MAX);
     if (k) hipLaunchKernelGGL(k_bfp_seeds<double>, g1(k), dim3(256), 0, s, seeds, k, x, nearest);
-    if (n)
-      hipLaunchKernelGGL(k_bf_pyamg<double>, dim3(1), dim3(kBfBlock), 0, s, G->indptr, G->indices,
-                         G->data, dplan + nlev + 1, dplan, nlev, max_sweeps, x, nearest, dout);
+    MLAMG_HIP(hipGetLastError());
+    MLAMG_TRY(run_pull<double>(G, P, x, nearest, s, &sweeps));
   } else {
     float* x = static_cast<float*>(dist);
     if (n) hipLaunchKernelGGL(k_bfp_init<float>, g1(n), dim3(256), 0, s, x, nearest, n, FLT_MAX);
     if (k) hipLaunchKernelGGL(k_bfp_seeds<float>, g1(k), dim3(256), 0, s, seeds, k, x, nearest);
-    if (n)
-      hipLaunchKernelGGL(k_bf_pyamg<float>, dim3(1), dim3(kBfBlock), 0, s, G->indptr, G->indices,
-                         G->data, dplan + nlev + 1, dplan, nlev, max_sweeps, x, nearest, dout);
+    MLAMG_HIP(hipGetLastError());
+    MLAMG_TRY(run_pull<float>(G, P, x, nearest, s, &sweeps));
   }
-  MLAMG_HIP(hipGetLastError());
-  int32_t res[2] = {n ? 0 : 1, 0};
-  if (n) MLAMG_HIP(hipMemcpyAsync(res, dout, sizeof(res), hipMemcpyDeviceToHost, s));
-  MLAMG_HIP(hipStreamSynchronize(s));
-  MLAMG_REQUIRE(res[1] == 0, "bellman_ford: no fixed point after n + 2 sweeps (negative cycle)");
-  if (sweeps_host) *sweeps_host = res[0];
+  if (sweeps_host) *sweeps_host = sweeps;
   return MLAMG_OK;
 }
 
@@ -499,8 +810,8 @@ int mlamg_aggregate_op(const int32_t* col, int64_t n, int64_t k, mlamg_csr** out
   return MLAMG_OK;
 }
 
-int mlamg_lloyd_cluster(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxiter, double* d,
-                        int32_t* c, int32_t* iters_host, void* stream) {
+static int lloyd_impl(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxiter, double* d,
+                      int32_t* c, int32_t* iters_host, void* stream, bool exact) {
   MLAMG_REQUIRE(G && seeds && d && c, "NULL argument");
   MLAMG_REQUIRE(k >= 1, "at least one seed is required");
   MLAMG_REQUIRE(maxiter >= 1, "maxiter must be positive");
@@ -526,6 +837,8 @@ int mlamg_lloyd_cluster(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxit
       (void)hipFree(b);
     }
   } guard{iw, mx};
+  SeqPlan P;
+  if (exact) MLAMG_TRY(build_pull_plan(G, s, P));
   int32_t* is_seed = iw;
   int32_t* mi = iw + n;
   int32_t* flag = iw + n + k;
@@ -536,22 +849,31 @@ int mlamg_lloyd_cluster(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxit
     hipLaunchKernelGGL(k_ll_init, g1(n), dim3(256), 0, s, d, c, n);
     hipLaunchKernelGGL(k_ll_seeds, g1(k), dim3(256), 0, s, seeds, k, d, c);
     int32_t h = 1;
-    while (h) {  // outward distances
-      MLAMG_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s));
-      hipLaunchKernelGGL(k_ll_pull, g1(n), dim3(256), 0, s, G->indptr, G->indices, G->data, n, d,
-                         flag);
-      MLAMG_TRY(read_flag(flag, s, &h));
-    }
-    h = 1;
-    while (h) {  // cluster labels
-      MLAMG_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s));
-      hipLaunchKernelGGL(k_ll_label, g1(n), dim3(256), 0, s, G->indptr, G->indices, G->data, n,
-                         d, c, is_seed, flag);
-      MLAMG_TRY(read_flag(flag, s, &h));
+    if (exact) {  // outward distances and clusters in amg_core's sweep order
+      int32_t sw = 0;
+      MLAMG_TRY(run_pull<double>(G, P, d, c, s, &sw));
+    } else {
+      while (h) {  // outward distances
+        MLAMG_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s));
+        hipLaunchKernelGGL(k_ll_pull, g1(n), dim3(256), 0, s, G->indptr, G->indices, G->data, n,
+                           d, flag);
+        MLAMG_TRY(read_flag(flag, s, &h));
+      }
+      h = 1;
+      while (h) {  // cluster labels
+        MLAMG_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s));
+        hipLaunchKernelGGL(k_ll_label, g1(n), dim3(256), 0, s, G->indptr, G->indices, G->data, n,
+                           d, c, is_seed, flag);
+        MLAMG_TRY(read_flag(flag, s, &h));
+      }
     }
     hipLaunchKernelGGL(k_ll_boundary, g1(n), dim3(256), 0, s, G->indptr, G->indices, n, c, d);
+    // inward distances: the boundary nodes (d = 0) never improve with weights >= 0, and every
+    // other node's neighbours all share its cluster, so amg_core's in-place label updates can
+    // only copy a node's own cluster: clusters are unchanged and the distances are the
+    // order-independent fixed point
     h = 1;
-    while (h) {  // inward distances (clusters cannot change: see header)
+    while (h) {
       MLAMG_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s));
       hipLaunchKernelGGL(k_ll_pull, g1(n), dim3(256), 0, s, G->indptr, G->indices, G->data, n, d,
                          flag);
@@ -571,6 +893,16 @@ int mlamg_lloyd_cluster(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxit
   MLAMG_HIP(hipGetLastError());
   if (iters_host) *iters_host = it;
   return MLAMG_OK;
+}
+
+int mlamg_lloyd_cluster(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxiter, double* d,
+                        int32_t* c, int32_t* iters_host, void* stream) {
+  return lloyd_impl(G, seeds, k, maxiter, d, c, iters_host, stream, true);
+}
+
+int mlamg_lloyd_cluster_canon(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxiter,
+                              double* d, int32_t* c, int32_t* iters_host, void* stream) {
+  return lloyd_impl(G, seeds, k, maxiter, d, c, iters_host, stream, false);
 }
 
 }  // extern "C"

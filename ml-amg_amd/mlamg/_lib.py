@@ -123,10 +123,12 @@ SIGNATURES = {
                                    c_vp, c_vp]),
     "mlamg_gnn_topk": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "mlamg_bellman_ford": (c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, P_i32, c_vp]),
+    "mlamg_bellman_ford_canon": (c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, P_i32, c_vp]),
     "mlamg_bellman_ford_pyamg": (c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp, P_i32, c_vp]),
     "mlamg_aggregate_op": (c_int, [c_vp, c_i64, c_i64, c_vpp, c_vp]),
     "mlamg_labels_to_columns": (c_int, [c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "mlamg_lloyd_cluster": (c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp, P_i32, c_vp]),
+    "mlamg_lloyd_cluster_canon": (c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp, P_i32, c_vp]),
     "mlamg_gs_create": (c_int, [c_vp, c_vpp, c_vp]),
     "mlamg_gs_destroy": (c_int, [c_vp]),
     "mlamg_gs_levels": (c_int, [c_vp, P_i32]),

@@ -339,6 +339,7 @@ class FullAggNet(nn.Module):
         not in the reference's signature; a test hook for well-conditioned inputs."""
         from .graph import (aggregate_op_device, bellman_ford_device, bellman_ford_pyamg_device,
                             labels_to_columns)
+        from .sparse import DeviceCSR
         if aggregation not in ("pyamg", "pyamg64", "parallel"):
             raise ValueError("aggregation must be 'pyamg', 'pyamg64' or 'parallel', got "
                              f"{aggregation!r}")
@@ -354,6 +355,15 @@ class FullAggNet(nn.Module):
         _, bf_edges = self.CNet.run(g)
         C = g.csr(bf_edges)
         seeds = top_k.to(torch.int32)
+        if aggregation != "parallel" and not A.has_canonical_format:
+            # pyamg's asgraph turns the COO C (:471) into csr_matrix: columns sorted, duplicate
+            # edges summed in C's float32; its sweep visits each row in that order
+            Cs = C.to_scipy()
+            Cc = sp.coo_matrix((Cs.data.astype(np.float32), (np.repeat(np.arange(m),
+                                np.diff(Cs.indptr)), Cs.indices)), shape=(m, m)).tocsr()
+            Cc.sum_duplicates()
+            C = DeviceCSR.from_scipy(sp.csr_matrix((Cc.data.astype(np.float64), Cc.indices,
+                                                    Cc.indptr), shape=(m, m)), check=False)
         if aggregation != "parallel":
             _, lab, _ = bellman_ford_pyamg_device(C, seeds, fp64=aggregation == "pyamg64")
             if bool((lab < 0).any()):

@@ -2,18 +2,19 @@
 
   modified_bellman_ford   ns/lib/graph.py:7-53     seeded Bellman-Ford, fp32 (torch) arithmetic
   bellman_ford            pyamg 4.x graph.bellman_ford (ns/model/agg_interp.py:475, the
-                          aggregation step of FullAggNet.forward): sequential sweeps emulated
-                          exactly, so nearest seeds are bitwise pyamg's, ties included
+                          aggregation step of FullAggNet.forward)
   nearest_center_to_agg   ns/lib/graph.py:56-86    aggregate matrix from assignments
   lloyd_aggregation       ns/lib/graph.py:156-239  seeds + pyamg 4.x lloyd_cluster + AggOp
+  lloyd_cluster           pyamg 4.x graph.lloyd_cluster (what graph.py:232 calls)
   num_connected_components, check_aggregates_connected   ns/lib/graph.py:89-153 (host-side
                           graph checks, kept so an alias of ns.lib.graph to this module is whole)
 
-modified_bellman_ford: distances are bit-exact with the reference for any input (order-independent
-fixed point, see csrc/graph.hip). Seed labels are bit-exact whenever shortest paths are unique; on
-exact ties the device uses the order-independent rule "smallest seed id among tight predecessors"
-where the reference keeps whichever its sequential sweep found first. bellman_ford (pyamg's) is
-bit-exact in both outputs for every input: its sweeps are level-scheduled, not reordered.
+All three reference sweeps are sequential and in place, so on equal-length paths the winning
+seed depends on the sweep order. The device runs those orders themselves, level-scheduled
+(csrc/graph.hip): distances and labels are bitwise the reference's on every input, ties
+included. The order-independent variants (bellman_ford_device, lloyd_cluster_device(...,
+exact=False): label = smallest seed among tight predecessors, multi-workgroup sweeps) serve the
+multilevel / distributed hierarchy, which has no reference counterpart.
 """
 from __future__ import annotations
 
@@ -39,10 +40,25 @@ def _coo_to_device_csr(S_T):
 
 
 def bellman_ford_device(G, seeds_dev):
-    """Device Bellman-Ford on G (push form: edge i -> j, weight G[i, j]).
+    """Order-independent device Bellman-Ford on G (push form: edge i -> j, weight G[i, j]) —
+    the hierarchy's aggregation. Labels: smallest seed id among tight predecessors.
 
     Returns (distance fp32 tensor, label int32 tensor (seed node id, -1 unreachable), sweeps).
     """
+    n = G.shape[0]
+    dev = _device()
+    dist = torch.empty(n, dtype=torch.float32, device=dev)
+    lab = torch.empty(n, dtype=torch.int32, device=dev)
+    sweeps = ctypes.c_int32()
+    call("mlamg_bellman_ford_canon", G.handle, ptr(seeds_dev), int(seeds_dev.numel()), ptr(dist),
+         ptr(lab), ctypes.byref(sweeps), stream_ptr())
+    return dist, lab, int(sweeps.value)
+
+
+def modified_bellman_ford_device(G, seeds_dev):
+    """ns/lib/graph.py:40-51 exactly on a DeviceCSR: the reference's row-major in-place push
+    sweeps in fp32, level-scheduled. Returns (distance fp32 tensor, nearest int32 tensor (seed
+    node id, -1 unreachable), sweeps = the reference's count)."""
     n = G.shape[0]
     dev = _device()
     dist = torch.empty(n, dtype=torch.float32, device=dev)
@@ -99,7 +115,7 @@ def modified_bellman_ford(S_T, centers):
     """
     G = _coo_to_device_csr(S_T)
     seeds = torch.as_tensor(centers).to(device=_device(), dtype=torch.int32)
-    dist, lab, _ = bellman_ford_device(G, seeds)
+    dist, lab, _ = modified_bellman_ford_device(G, seeds)
     nearest = lab.to(torch.int64)
     nearest = torch.where(nearest < 0, torch.zeros_like(nearest), nearest)
     dev = centers.device if isinstance(centers, torch.Tensor) else torch.device("cpu")
@@ -142,14 +158,17 @@ def nearest_center_to_agg(top_k, nearest_center):
     return T.coalesce()
 
 
-def lloyd_cluster_device(G, seeds_dev, maxiter=10):
-    """pyamg 4.x lloyd_cluster on the device. Returns (distances, clusters, seeds, iters)."""
+def lloyd_cluster_device(G, seeds_dev, maxiter=10, exact=True):
+    """pyamg 4.x lloyd_cluster on the device (seeds_dev updated in place). exact=True runs the
+    outward pass in amg_core's sweep order (pyamg's clusters, ties included); exact=False the
+    order-independent rule (the hierarchy's option). Returns (distances, clusters, seeds,
+    iters)."""
     n = G.shape[0]
     dev = _device()
     d = torch.empty(n, dtype=torch.float64, device=dev)
     c = torch.empty(n, dtype=torch.int32, device=dev)
     its = ctypes.c_int32()
-    call("mlamg_lloyd_cluster", G.handle, ptr(seeds_dev), int(seeds_dev.numel()), int(maxiter),
+    call("mlamg_lloyd_cluster" if exact else "mlamg_lloyd_cluster_canon", G.handle, ptr(seeds_dev), int(seeds_dev.numel()), int(maxiter),
          ptr(d), ptr(c), ctypes.byref(its), stream_ptr())
     return d, c, seeds_dev, int(its.value)
 
@@ -206,6 +225,71 @@ def lloyd_aggregation(C, ratio=0.03, distance='unit', maxiter=10, rand=None):
                           shape=(G.shape[0], num_seeds))
     roots = roots_dev.cpu().numpy().astype(np.intc)
     return AggOp, roots, seeds
+
+
+def _asgraph(G):
+    """pyamg.graph.asgraph: CSR/CSC kept (amg_core walks either's arrays as CSR), anything else
+    becomes csr_matrix; square required."""
+    if not (sp.isspmatrix_csr(G) or sp.isspmatrix_csc(G)):
+        G = sp.csr_matrix(G)
+    if G.shape[0] != G.shape[1]:
+        raise ValueError('expected square matrix')
+    return G
+
+
+def lloyd_cluster(G, seeds, maxiter=10):
+    """pyamg 4.x pyamg.graph.lloyd_cluster(G, seeds, maxiter) on the device (the call at
+    ns/lib/graph.py:232 and inside pyamg.aggregation.lloyd_aggregation, utils/common.py:91).
+
+    seeds: an int (that many seeds drawn as np.random.permutation(N)[:seeds] from numpy's
+    GLOBAL generator, like pyamg) or an array of seed nodes. Returns (distances float64,
+    clusters intc, seeds intc) like pyamg; clusters and seeds bitwise amg_core's, ties included.
+    Weights are used in float64 (the reference's graphs are float64)."""
+    G = _asgraph(G)
+    N = G.shape[0]
+    if G.dtype.kind == 'c':
+        G = abs(G)
+    if np.isscalar(seeds):
+        seeds = np.random.permutation(N)[:seeds].astype('intc')
+    else:
+        seeds = np.array(seeds, dtype='intc')
+    if len(seeds) < 1:
+        raise ValueError('at least one seed is required')
+    if seeds.min() < 0:
+        raise ValueError('invalid seed index (%d)' % seeds.min())
+    if seeds.max() >= N:
+        raise ValueError('invalid seed index (%d)' % seeds.max())
+    if maxiter < 1:  # pyamg's loop would not run and return uninitialised arrays
+        raise ValueError('maxiter must be >= 1')
+    Gc = sp.csr_matrix((np.asarray(G.data, dtype=np.float64), G.indices, G.indptr),
+                       shape=G.shape)
+    Gd = DeviceCSR.from_scipy(Gc, check=False)
+    seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
+    d, c, s, _ = lloyd_cluster_device(Gd, seeds_dev, maxiter)
+    return d.cpu().numpy(), c.cpu().numpy().astype('intc'), s.cpu().numpy().astype('intc')
+
+
+def pyamg_lloyd_aggregation(C, ratio=0.03, distance='unit', maxiter=10):
+    """pyamg 4.x pyamg.aggregation.lloyd_aggregation (utils/common.py:91,
+    utils/evaluate_dataset.py:77 call it directly): no `rand`; num_seeds = int(min(max(ratio N,
+    1), N)) drawn inside lloyd_cluster from the global generator; returns (AggOp int8 CSR,
+    seeds)."""
+    if ratio <= 0 or ratio > 1:
+        raise ValueError('ratio must be > 0.0 and <= 1.0')
+    if not (sp.isspmatrix_csr(C) or sp.isspmatrix_csc(C)):
+        raise TypeError('expected csr_matrix or csc_matrix')
+    data = distance_data(C, distance)
+    if C.dtype == complex:
+        data = np.real(data)
+    assert data.min() >= 0
+    G = C.__class__((data, C.indices, C.indptr), shape=C.shape)
+    num_seeds = int(min(max(ratio * G.shape[0], 1), G.shape[0]))
+    _, clusters, seeds = lloyd_cluster(G, num_seeds, maxiter=maxiter)
+    row = (clusters >= 0).nonzero()[0]
+    col = clusters[row]
+    AggOp = sp.coo_matrix((np.ones(len(row), dtype='int8'), (row, col)),
+                          shape=(G.shape[0], num_seeds)).tocsr()
+    return AggOp, seeds
 
 
 def num_connected_components(adj):

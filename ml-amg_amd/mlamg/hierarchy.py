@@ -132,10 +132,11 @@ class Hierarchy:
     # ------------------------------------------------------------------ construction
     @classmethod
     def two_level(cls, A, P, omega=2.0 / 3.0, nu_pre=1, nu_post=1, dinv_w=None,
-                  smoother="jacobi", norm="residual"):
+                  smoother="jacobi", norm="residual", coarse="auto"):
         """Two-level cycle with a given P: MLAMG.amg_2_v (ns/preconditioner/MLAMG.py:120-122,
         smoother='jacobi') or multigrid.amg_2_v (multigrid.py:111-210, smoother='gauss_seidel';
-        norm='x' records ||x||_2 per cycle, the error_tol mode)."""
+        norm='x' records ||x||_2 per cycle, the error_tol mode). coarse='dense' forces the
+        dense inverse (up to DENSE_LIMIT rows) where 'auto' would take PCG."""
         from .multigrid import GaussSeidel
         H = cls()
         H.jacobi_weight = omega
@@ -150,7 +151,12 @@ class Hierarchy:
         H.Ac = galerkin(L.R, L.A, L.P)
         torch.cuda.synchronize()
         tm["galerkin"], t0 = time.perf_counter() - t0, time.perf_counter()
-        H._finalize(nu_pre, nu_post, dense_max=cls.TWO_LEVEL_DENSE_MAX)
+        n_c = H.Ac.shape[0]
+        if coarse == "dense" and n_c > cls.DENSE_LIMIT:
+            raise CoarseSolveError(f"coarse operator of {n_c} rows: the dense solver is limited "
+                                   f"to {cls.DENSE_LIMIT} rows")
+        H._finalize(nu_pre, nu_post,
+                    dense_max=n_c if coarse == "dense" else cls.TWO_LEVEL_DENSE_MAX)
         torch.cuda.synchronize()
         tm["coarse_solver"], t0 = time.perf_counter() - t0, time.perf_counter()
         if smoother == "gauss_seidel":
@@ -363,7 +369,8 @@ class Hierarchy:
                     _, lab, L.bf_sweeps = bellman_ford_device(C, seeds_dev)
                     col = labels_to_columns(lab, seeds_dev)
                 elif aggregation == "lloyd":
-                    _, col, _, L.bf_sweeps = lloyd_cluster_device(C, seeds_dev, lloyd_maxiter)
+                    _, col, _, L.bf_sweeps = lloyd_cluster_device(C, seeds_dev, lloyd_maxiter,
+                                                                  exact=False)
                 else:
                     raise ValueError(f"unknown aggregation {aggregation!r}")
                 L.Agg = aggregate_op_device(col, k)
@@ -576,6 +583,8 @@ class Hierarchy:
         call("mlamg_gmres", A.handle, self.handle, ptr(bd), ptr(xd), float(rtol), int(restart),
              int(maxiter or 0), int(x0 is None), ctypes.byref(info), ctypes.byref(inner), hist,
              cap, stream_ptr())
+        if self.pcg is not None:
+            self.check_coarse()  # a broken-down coarse solve inside the preconditioner
         x = xd if isinstance(b, torch.Tensor) else xd.cpu().numpy()
         if not return_info:
             return x

@@ -419,30 +419,38 @@ def amg_2_v(A, P, b, x,
     if singular:
         return _amg_2_v_singular(A, P, b, x, pre_smoothing_steps, post_smoothing_steps,
                                  jacobi_weight, res_tol, tol, max_iter, smoother)
-    err = np.zeros(max_iter)
-    from .hierarchy import Hierarchy
-    try:
+    from .hierarchy import CoarseSolveError, Hierarchy
+
+    def run(coarse):
         # the whole solve is one device call: cycles replayed from a captured graph, the
         # norm and tolerance test on the device (no host round trip per iteration)
         H = Hierarchy.two_level(A, P, omega=jacobi_weight, nu_pre=pre_smoothing_steps,
                                 nu_post=post_smoothing_steps, smoother=smoother,
-                                norm="residual" if res_tol is not None else "x")
+                                norm="residual" if res_tol is not None else "x", coarse=coarse)
+        dev_x = to_device_vec(x).clone()  # x = x.copy()  (:171)
+        dev_b = to_device_vec(b)
+        err = H.cycle(dev_b, dev_x, max_iter, tol=tol, use_graph=use_graph)  # stops at e <= tol
+        return dev_x.cpu().numpy(), conv_factor(err), err, len(err)
+
+    failed = (x, np.float64(1.), np.zeros(max_iter), 0)  # multigrid.py:167-170
+    try:
+        return run("auto")
     except _lib.MlamgError as e:
         if e.code == _lib.MLAMG_EINVAL and "singular" in str(e):
-            return x, np.float64(1.), err, 0  # multigrid.py:167-170
+            return failed  # the dense factorisation failed, as spla.factorized would
         raise
-    dev_x = to_device_vec(x).clone()  # x = x.copy()  (:171)
-    dev_b = to_device_vec(b)
-    # err[i]; stops after the first e <= tol
-    from .hierarchy import CoarseSolveError
-    try:
-        err = H.cycle(dev_b, dev_x, max_iter, tol=tol, use_graph=use_graph)
     except CoarseSolveError:
-        # the PCG coarse solve broke down: A_H is not positive definite (singular, e.g. a P
-        # with an empty column) — the case where the reference's factorisation fails, so the
-        # reference's failure return (multigrid.py:167-170)
-        return x, np.float64(1.), np.zeros(max_iter), 0
-    return dev_x.cpu().numpy(), conv_factor(err), err, len(err)
+        pass
+    # The PCG coarse solve broke down: A_H is not positive definite. SuperLU (the reference's
+    # factorisation) solves any nonsingular A_H, so the coarse operator is inverted densely
+    # instead (Gauss-Jordan with partial pivoting when it is not SPD) and the solve rerun; the
+    # reference's failure return only when that factorisation fails too.
+    try:
+        return run("dense")
+    except _lib.MlamgError as e:
+        if e.code == _lib.MLAMG_EINVAL and "singular" in str(e):
+            return failed
+        raise
 
 
 def amg_2_v_batch(problems, workers=8, **kw):

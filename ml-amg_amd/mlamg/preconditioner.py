@@ -153,8 +153,11 @@ class MultilevelPC(MLAMG):
     else None)`: zero initial guess and a tolerance relative to ||b|| (pyamg's solve scales tol
     by ||b||, and its default maxiter is 100).
       * with GMRES (the default, :54): device GMRES preconditioned by one V-cycle
-        (Hierarchy.gmres: scipy's algorithm, restart 20, ||b - A x|| <= amg_rtol ||b||, at most
-        100 restart cycles);
+        (Hierarchy.gmres), with pyamg's iteration budget: pyamg.krylov.gmres called without a
+        restart value runs ONE outer cycle of at most maxiter = 100 inner steps (each one
+        V-cycle), so this is one cycle of restart min(100, n). Stop test ||b - A x|| <= amg_rtol
+        ||b|| on the true residual; pyamg's Householder GMRES tests the preconditioned one
+        (parity unpinned: pyamg absent);
       * without: stationary V-cycles from x = 0 until ||b - A x|| <= amg_rtol ||b||, at most 100.
     """
 
@@ -181,7 +184,7 @@ class MultilevelPC(MLAMG):
         b = X.array_r if hasattr(X, "array_r") else np.asarray(X)
         b = np.asarray(b, dtype=np.float64)
         if self.amg_precon_gmres:
-            out = self.H.gmres(b, rtol=self.amg_rtol, restart=20, maxiter=self.PYAMG_MAXITER)
+            out = self.H.gmres(b, rtol=self.amg_rtol, restart=self.PYAMG_MAXITER, maxiter=1)
         else:
             normb = float(np.linalg.norm(b))
             tol = self.amg_rtol * normb if normb != 0 else self.amg_rtol

@@ -321,6 +321,42 @@ def lloyd_aggregation(C, ratio=0.03, distance='unit', maxiter=10, rand=None, can
     return AggOp, roots, seeds
 
 
+def pyamg_lloyd_aggregation(C, ratio=0.03, distance='unit', maxiter=10):
+    """pyamg 4.x pyamg.aggregation.lloyd_aggregation (absent here; restated from its published
+    source — the reference's own graph.py:156-239 says it was adapted from it; parity unpinned
+    w.r.t. pyamg itself), as utils/common.py:91 and utils/evaluate_dataset.py:77 call it:
+    num_seeds = int(min(max(ratio*N, 1), N)); pyamg.graph.lloyd_cluster(G, num_seeds, maxiter)
+    draws np.random.permutation(N)[:num_seeds] from the GLOBAL generator; returns (AggOp, seeds)."""
+    if ratio <= 0 or ratio > 1:
+        raise ValueError('ratio must be > 0.0 and <= 1.0')
+    if not (sp.isspmatrix_csr(C) or sp.isspmatrix_csc(C)):
+        raise TypeError('expected csr_matrix or csc_matrix')
+    if distance == 'unit':
+        data = np.ones_like(C.data).astype(float)
+    elif distance == 'abs':
+        data = abs(C.data)
+    elif distance == 'inv':
+        data = 1.0 / abs(C.data)
+    elif distance == 'same':
+        data = C.data
+    elif distance == 'min':
+        data = C.data - C.data.min()
+    else:
+        raise ValueError(distance)
+    G = C.__class__((data, C.indices, C.indptr), shape=C.shape)
+    if sp.isspmatrix_csc(G):
+        G = sp.csr_matrix((G.data, G.indices, G.indptr), shape=G.shape)
+    N = G.shape[0]
+    num_seeds = int(min(max(ratio * N, 1), N))
+    seeds = np.random.permutation(N)[:num_seeds].astype('intc')
+    _, clusters, seeds = lloyd_cluster(G, seeds, maxiter=maxiter)
+    row = (clusters >= 0).nonzero()[0]
+    col = clusters[row]
+    AggOp = sp.coo_matrix((np.ones(len(row), dtype='int8'), (row, col)),
+                          shape=(N, num_seeds)).tocsr()
+    return AggOp, seeds.astype('intc')
+
+
 # ---------------------------------------------------------------- multilevel (device recipe)
 STRENGTH = {
     "abs": lambda A: abs(A),

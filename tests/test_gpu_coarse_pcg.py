@@ -150,12 +150,14 @@ def test_nonsymmetric_coarse_takes_dense_or_refuses(ml, torch_cuda, monkeypatch)
         H_.two_level(A, P)
 
 
-def test_pcg_breakdown_is_reported(ml, torch_cuda, monkeypatch):
+def test_pcg_breakdown_is_reported(ml, oracle, torch_cuda, monkeypatch):
     """An indefinite symmetric coarse operator (tridiag(1, 1, 1): spectrum (-1, 3), positive
     diagonal; P = I so A_H = A) passes the symmetry test, so PCG is chosen, and breaks down
-    (p.Ap or r.z not positive). The breakdown is counted, the cycle raises CoarseSolveError, and
-    amg_2_v maps it to the reference's factorisation-failure return (x, 1.0, zeros, 0),
-    ns/lib/multigrid.py:167-170."""
+    (p.Ap or r.z not positive). The breakdown is counted and the cycle raises CoarseSolveError.
+    amg_2_v then inverts A_H densely (Gauss-Jordan with pivoting, as SuperLU would factor any
+    nonsingular A_H) and reruns: n = 2001 is nonsingular (tridiag(1,1,1) of order n is singular
+    iff 3 | n + 1), so the solve converges and matches the oracle's (scipy factorized) iterate;
+    only a factorisation failure maps to (x, 1.0, zeros, 0), ns/lib/multigrid.py:167-170."""
     import scipy.sparse as sp
     torch = torch_cuda
     H_ = ml.hierarchy.Hierarchy
@@ -170,8 +172,17 @@ def test_pcg_breakdown_is_reported(ml, torch_cuda, monkeypatch):
     with pytest.raises(ml.hierarchy.CoarseSolveError):
         H.cycle(b, xd, 3)
     assert H.coarse_stats()["breakdowns"] >= 1
+    with pytest.raises(ml.hierarchy.CoarseSolveError):  # inside the preconditioner too
+        H.gmres(b, rtol=1e-8, restart=5, maxiter=1)
+    n = 2001
+    A = sp.diags([np.ones(n - 1), np.ones(n), np.ones(n - 1)], [-1, 0, 1], format="csr")
+    P = sp.eye(n, format="csr")
+    assert H_.two_level(A, P).pcg is not None
     x0 = np.random.RandomState(0).randn(n)
-    x, c, e, it = ml.multigrid.amg_2_v(A, P, np.random.RandomState(1).randn(n), x0,
-                                       res_tol=1e-10, max_iter=7, engine="hierarchy",
-                                       smoother="jacobi")
-    assert c == 1.0 and it == 0 and np.array_equal(e, np.zeros(7)) and x is x0
+    bb = np.random.RandomState(1).randn(n)
+    x, c, e, it = ml.multigrid.amg_2_v(A, P, bb, x0, res_tol=1e-10, max_iter=7,
+                                       engine="hierarchy")
+    xr, cr, er, itr = oracle.amg_2_v(A, P, bb, x0, res_tol=1e-10, max_iter=7)
+    assert it >= 1 and x is not x0
+    assert np.linalg.norm(bb - A @ x) <= 1e-10 and e[-1] <= 1e-10
+    assert np.linalg.norm(x - xr) <= 1e-10 * np.linalg.norm(xr)

@@ -117,19 +117,27 @@ def _to_csr(T, shape):
     return sp.csr_matrix((T.values().cpu().numpy(), T.indices().cpu().numpy()), shape=shape)
 
 
-@pytest.mark.parametrize("aggregation", ("pyamg", "pyamg64", "parallel"))
-def test_fullaggnet_forward(torch_cuda, oracle, aggregation):
+@pytest.mark.parametrize("aggregation,unsorted", (("pyamg", False), ("pyamg64", False),
+                                                  ("parallel", False), ("pyamg", True)))
+def test_fullaggnet_forward(torch_cuda, oracle, aggregation, unsorted):
     """FullAggNet.forward on the device: k seeds, every node in one aggregate, the aggregates
     those of the aggregation rule on the device's own CNet weights C — "pyamg": pyamg 4.x
     bellman_ford(C, top_k) (oracle restatement, pull sweeps, strict <; bitwise, ties included:
     the ReLU-ended CNet leaves many exact-zero weights); "parallel": the order-independent
     rule on the same pull direction (oracle.canon_bellman_ford pushes, so on C^T) — and P =
-    PNet(graph_from_matrix(A, Agg)) Agg against the oracle's product on the device's P_hat."""
+    PNet(graph_from_matrix(A, Agg)) Agg against the oracle's product on the device's P_hat.
+    unsorted: A's rows stored in descending column order — pyamg still sweeps the canonical
+    (sorted) CSR its asgraph makes of C, and so must the device."""
     torch = torch_cuda
     from mlamg import gnn
     torch.manual_seed(2)
     net = gnn.FullAggNet(dim=64, num_conv=2, iterations=2).cuda()
     A = _A(14)
+    if unsorted:
+        rows = [A.indices[A.indptr[i]:A.indptr[i + 1]][::-1] for i in range(A.shape[0])]
+        vals = [A.data[A.indptr[i]:A.indptr[i + 1]][::-1] for i in range(A.shape[0])]
+        A = sp.csr_matrix((np.concatenate(vals), np.concatenate(rows), A.indptr), shape=A.shape)
+        assert not A.has_canonical_format
     n = A.shape[0]
     agg, P, C, top_k, scores = net.forward(A, 0.1, aggregation=aggregation)
     k = int(np.ceil(0.1 * n))

@@ -1,6 +1,8 @@
 """GPU parity: every hot-path kernel through the C-ABI against the reference golden vectors and
 the oracle. Bitwise for SpMV / residual / Jacobi / restriction / prolongation / SpGEMM /
 Galerkin / aggregation; fp64 tolerances (stated per test) for eigenvalues, coarse solves, norms."""
+import os
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -26,6 +28,7 @@ def ml(torch_cuda):
     import mlamg.hierarchy
     import mlamg.multigrid
     import mlamg.sparse
+    import mlamg.strength
     return mlamg
 
 
@@ -209,21 +212,102 @@ def test_empty_and_ragged(ml, torch_cuda):
 
 
 # ---------------------------------------------------------------- aggregation
+CALLERS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                       "reference_callers.npz")
+
+
+@pytest.fixture(scope="module")
+def callers():
+    return dict(np.load(CALLERS, allow_pickle=False))
+
+
+def _weights(A, kind):
+    if kind == "invabs":
+        return sp.csr_matrix((1.0 / np.abs(A.data), A.indices, A.indptr), A.shape)
+    return sp.csr_matrix((np.ones_like(A.data), A.indices, A.indptr), A.shape)
+
+
 @pytest.mark.parametrize("k", ("p2d", "rnd", "lap3d"))
 def test_bellman_ford(golden, ml, oracle, k):
+    """modified_bellman_ford (ns/lib/graph.py:7-53): distances AND nearest centers bitwise the
+    reference's own outputs (tests/golden/reference_vectors.npz) — the constant-coefficient p2d
+    and lap3d graphs are tie-rich."""
     import torch
     A = golden_csr(golden, k)
-    C = sp.csr_matrix((1.0 / np.abs(A.data), A.indices, A.indptr), A.shape)
+    C = _weights(A, "invabs")
     seeds = golden[f"{k}_bf_seeds"]
     S_T = ml.sparse.to_torch_sparse(C)
     d, nc = ml.graph.modified_bellman_ford(S_T, torch.as_tensor(seeds))
-    assert np.array_equal(d.numpy(), golden[f"{k}_bf_dist"])  # distances: bitwise vs reference
-    _, lab = oracle.canon_bellman_ford(C, seeds)
-    assert np.array_equal(nc.numpy(), np.where(lab < 0, 0, lab))  # labels: bitwise vs oracle rule
-    agree = float(np.mean(nc.numpy() == golden[f"{k}_bf_nearest"]))
+    assert d.dtype == torch.float32 and nc.dtype == torch.int64
+    assert np.array_equal(d.numpy(), golden[f"{k}_bf_dist"])
+    assert np.array_equal(nc.numpy(), golden[f"{k}_bf_nearest"])
+
+
+@pytest.mark.parametrize("k", ("p2d", "rnd", "lap3d"))
+@pytest.mark.parametrize("seed", (1, 5))
+def test_bellman_ford_unit_weights(golden, ml, oracle, k, seed):
+    """Unit weights (every path length an integer: ties everywhere) and other seed draws,
+    against the oracle's transcription of the reference sweep (itself bitwise the reference on
+    the goldens above, tests/test_oracle_golden.py); the reference's sweep count as well."""
+    import torch
+    from mlamg.sparse import DeviceCSR
+    A = golden_csr(golden, k)
+    C = _weights(A, "unit")
+    n = A.shape[0]
+    seeds = np.random.RandomState(seed).permutation(n)[:int(np.ceil(0.07 * n))]
+    dr, zr, swr = oracle.modified_bellman_ford(C, seeds)
+    d, nc = ml.graph.modified_bellman_ford(ml.sparse.to_torch_sparse(C), torch.as_tensor(seeds))
+    assert np.array_equal(d.numpy(), dr) and np.array_equal(nc.numpy(), zr)
+    sd = torch.as_tensor(seeds.astype(np.int32)).cuda()
+    _, _, sw = ml.graph.modified_bellman_ford_device(DeviceCSR.from_scipy(C), sd)
+    assert sw == swr
+
+
+@pytest.mark.parametrize("k", ("p2d", "rnd", "lap3d"))
+def test_bellman_ford_canon(golden, ml, oracle, k):
+    """The hierarchy's order-independent variant (mlamg_bellman_ford_canon): same distances,
+    labels = the oracle's restatement of its rule; = the reference's labels on tie-free rnd."""
+    import torch
+    from mlamg.sparse import DeviceCSR
+    A = golden_csr(golden, k)
+    C = _weights(A, "invabs")
+    seeds = golden[f"{k}_bf_seeds"]
+    d, lab, _ = ml.graph.bellman_ford_device(
+        DeviceCSR.from_scipy(C), torch.as_tensor(seeds.astype(np.int32)).cuda())
+    dc, labc = oracle.canon_bellman_ford(C, seeds)
+    assert np.array_equal(d.cpu().numpy(), golden[f"{k}_bf_dist"])
+    assert np.array_equal(lab.cpu().numpy(), labc)
+    agree = float(np.mean(np.where(labc < 0, 0, labc) == golden[f"{k}_bf_nearest"]))
     if k == "rnd":
-        assert agree == 1.0  # unique shortest paths -> same labels as the reference
-    print(f"[{k}] label agreement with reference sequential sweep: {agree:.4f}")
+        assert agree == 1.0
+
+
+def test_bellman_ford_wide_graph(ml, oracle):
+    """Graphs above 2^18 nodes take the per-level launches (graph.hip kSeqOneBlockMax): the
+    push sweep and pyamg's pull sweep bitwise against the oracle on a 520^2 unit-weight grid."""
+    import torch
+    from mlamg import problems
+    from mlamg.sparse import DeviceCSR
+    A = problems.poisson_2d_5pt(520)
+    C = _weights(A, "unit")
+    n = A.shape[0]
+    seeds = np.random.RandomState(0).permutation(n)[:int(np.ceil(0.1 * n))]
+    dr, zr, swr = oracle.modified_bellman_ford(C, seeds)
+    sd = torch.as_tensor(seeds.astype(np.int32)).cuda()
+    Cd = DeviceCSR.from_scipy(C)
+    d, z, sw = ml.graph.modified_bellman_ford_device(Cd, sd)
+    zd = z.cpu().numpy().astype(np.int64)
+    assert np.array_equal(d.cpu().numpy(), dr)
+    assert np.array_equal(np.where(zd < 0, 0, zd), zr) and sw == swr
+    dp, zp, swp = oracle.pyamg_bellman_ford(C, seeds)
+    d2, z2, sw2 = ml.graph.bellman_ford_pyamg_device(Cd, sd)
+    assert np.array_equal(d2.cpu().numpy(), dp) and np.array_equal(z2.cpu().numpy(), zp)
+    assert sw2 == swp
+    Cs = C.copy()
+    dl, cl, sl = oracle.lloyd_cluster(Cs, seeds[:2000].copy(), maxiter=3, canon=False)
+    d3, c3, s3, _ = ml.graph.lloyd_cluster_device(Cd, sd[:2000].clone(), maxiter=3)
+    assert np.array_equal(c3.cpu().numpy(), cl) and np.array_equal(s3.cpu().numpy(), sl)
+    assert np.array_equal(d3.cpu().numpy(), dl)
 
 
 @pytest.mark.parametrize("k", ("p2d", "rnd", "lap3d"))
@@ -249,13 +333,49 @@ def test_lloyd_aggregation(golden, ml, oracle):
 
 
 @pytest.mark.parametrize("k", ("p2d", "lap3d"))
-def test_lloyd_tie_rich_matches_oracle_rule(golden, ml, oracle, k):
+@pytest.mark.parametrize("case", ("unit0", "unit3", "olson"))
+def test_lloyd_tie_rich_matches_reference(golden, callers, ml, oracle, k, case):
+    """ns.lib.graph.lloyd_aggregation on tie-rich graphs — 'unit' distances (rand 0, 3) and the
+    evaluation loops' default path (np.random.seed(0), olson measure, 'same', rand=0,
+    utils/common.py:51-58) — against the reference driver's own output around the pyamg-order
+    lloyd_cluster (tests/golden/reference_callers.npz): seeds, roots and AggOp bitwise."""
     A = golden_csr(golden, k)
-    C = sp.csr_matrix((np.ones_like(A.data), A.indices, A.indptr), A.shape)
-    AggOp, roots, _ = ml.graph.lloyd_aggregation(C, ratio=0.1, distance='unit', rand=3)
-    AggC, rootsC, _ = oracle.lloyd_aggregation(C, ratio=0.1, distance='unit', rand=3, canon=True)
-    assert np.array_equal(roots, rootsC)
-    assert np.array_equal(AggOp.indices, AggC.indices)
+    if case == "olson":
+        np.random.seed(0)
+        C = ml.strength.strength_measure_funcs["olson"](A)
+        AggOp, roots, seeds = ml.graph.lloyd_aggregation(C, ratio=0.1, distance='same', rand=0)
+    else:
+        C = _weights(A, "unit")
+        AggOp, roots, seeds = ml.graph.lloyd_aggregation(C, ratio=0.1, distance='unit',
+                                                         rand=int(case[-1]))
+    assert np.array_equal(seeds, callers[f"{k}_{case}_seeds"])
+    assert np.array_equal(roots, callers[f"{k}_{case}_roots"])
+    assert np.array_equal(AggOp.indptr, callers[f"{k}_{case}_agg_indptr"])
+    assert np.array_equal(AggOp.indices, callers[f"{k}_{case}_agg_indices"])
+
+
+@pytest.mark.parametrize("k", ("p2d", "lap3d"))
+@pytest.mark.parametrize("rand", (1, 7))
+@pytest.mark.parametrize("distance", ("unit", "abs"))
+def test_lloyd_tie_rich_matches_oracle(golden, ml, oracle, k, rand, distance):
+    """More tie-rich draws against the oracle's pyamg-order restatement (canon=False), and the
+    hierarchy's order-independent variant against the oracle's restatement of its rule."""
+    from mlamg.sparse import DeviceCSR
+    import torch
+    A = golden_csr(golden, k)
+    C = abs(A).tocsr()
+    AggOp, roots, _ = ml.graph.lloyd_aggregation(C, ratio=0.1, distance=distance, rand=rand)
+    AggR, rootsR, _ = oracle.lloyd_aggregation(C, ratio=0.1, distance=distance, rand=rand)
+    assert np.array_equal(roots, rootsR)
+    assert np.array_equal(AggOp.indices, AggR.indices)
+    G = ml.graph.distance_data(C, distance)
+    G = sp.csr_matrix((G, C.indices, C.indptr), shape=C.shape)
+    seeds = np.random.RandomState(rand).permutation(A.shape[0])[:int(np.ceil(0.1 * A.shape[0]))]
+    _, cc, sc = oracle.lloyd_cluster(G, seeds.copy(), maxiter=10, canon=True)
+    _, c, s, _ = ml.graph.lloyd_cluster_device(DeviceCSR.from_scipy(G),
+                                               torch.as_tensor(seeds.astype(np.int32)).cuda(),
+                                               10, exact=False)
+    assert np.array_equal(c.cpu().numpy(), cc) and np.array_equal(s.cpu().numpy(), sc)
 
 
 # ---------------------------------------------------------------- smoothers / coarse solve

@@ -128,6 +128,9 @@ def test_multilevel_pc_apply_semantics(ml, gmres):
     assert M.H.n_levels >= 3 and M.amg_precon_gmres is gmres and M.amg_rtol == 1e-6
     b = 1e3 * np.random.RandomState(1).randn(n)
     Y = _Vec(n=n)
+    calls = []
+    real = M.H.gmres
+    M.H.gmres = lambda *a, **kw: calls.append(kw) or real(*a, **kw)
     np.random.seed(5)
     st = np.random.get_state()
     M.apply(pc, _Vec(b), Y)
@@ -135,6 +138,8 @@ def test_multilevel_pc_apply_semantics(ml, gmres):
     r = np.linalg.norm(b - A @ Y.out)
     assert r <= 1e-6 * np.linalg.norm(b)
     assert r > 1e-9 * np.linalg.norm(b)  # relative, not absolute: no over-solving to 1e-6 abs
+    # pyamg's budget: krylov.gmres without a restart value = one outer cycle of <= 100 steps
+    assert calls == ([{"rtol": 1e-6, "restart": 100, "maxiter": 1}] if gmres else [])
     # zero right-hand side: zero solution
     M.apply(pc, _Vec(np.zeros(n)), Y)
     assert not np.any(Y.out)

@@ -98,8 +98,7 @@ def test_default_path_reproduces_reference_call(oracle, torch_cuda, name, mode):
     np.random.seed(0)
     C_ref = sp.csr_matrix(oracle.strength_measure(A, mode))
     st_ref = np.random.get_state()
-    Agg_ref, roots_ref, seeds_ref = oracle.lloyd_aggregation(C_ref, ratio=0.1, distance="same",
-                                                             canon=True)
+    Agg_ref, roots_ref, seeds_ref = oracle.lloyd_aggregation(C_ref, ratio=0.1, distance="same")
     st_ref_after = np.random.get_state()
 
     np.random.seed(0)

@@ -1,5 +1,7 @@
 """CPU: pin the oracle (oracle/) against golden vectors produced by the reference itself
 (tests/golden/make_golden.py). Bitwise wherever the reference is deterministic scipy/driver code."""
+import os
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -215,3 +217,24 @@ def test_oracle_pyamg_bellman_ford(oracle, kind):
     assert np.array_equal(d[reach], dc[reach])
     if kind == "disconnected":
         assert not reach.all() and np.all(d[~reach] == np.finfo(np.float32).max)
+
+
+@pytest.mark.parametrize("k", ("p2d", "lap3d"))
+@pytest.mark.parametrize("case", ("unit0", "unit3", "olson"))
+def test_lloyd_tie_rich_driver(golden, oracle, k, case):
+    """The oracle's pyamg-order lloyd_cluster inside its restated driver against the reference
+    driver's own output on tie-rich graphs (tests/golden/reference_callers.npz)."""
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "reference_callers.npz")))
+    A = golden_csr(golden, k)
+    if case == "olson":
+        np.random.seed(0)
+        C = oracle.strength_measure(A, "olson")
+        AggOp, roots, seeds = oracle.lloyd_aggregation(C, ratio=0.1, distance='same', rand=0)
+    else:
+        C = sp.csr_matrix((np.ones_like(A.data), A.indices, A.indptr), A.shape)
+        AggOp, roots, seeds = oracle.lloyd_aggregation(C, ratio=0.1, distance='unit',
+                                                       rand=int(case[-1]))
+    assert np.array_equal(seeds, g[f"{k}_{case}_seeds"])
+    assert np.array_equal(roots, g[f"{k}_{case}_roots"])
+    assert np.array_equal(AggOp.indptr, g[f"{k}_{case}_agg_indptr"])
+    assert np.array_equal(AggOp.indices, g[f"{k}_{case}_agg_indices"])
