@@ -102,6 +102,22 @@ struct RpWin {
           base[kRpWinMax] = {0, 0, 0, 0};
 };
 
+// Uniform row-pair stencils (spmv.hip k_rowpat_uni): every pattern entry is one of k <= 8
+// column offsets with one value per (offset, row parity); offsets within +-halo rows read x from
+// an LDS window of the workgroup's rows, the rest (at most kRpUniFar) are global loads
+constexpr int kRpUniMax = 8;
+constexpr int kRpUniFar = 2;
+constexpr int kRpUniMaxHalo = 512;  // rows staged on each side of a workgroup's rows, at most
+struct RpUni {
+  int32_t k = 0;     // slots (0: not uniform)
+  int32_t halo = 0;  // staged rows on each side (even)
+  int32_t off[kRpUniMax] = {0, 0, 0, 0, 0, 0, 0, 0};   // slot column offsets, ascending
+  int32_t kind[kRpUniMax] = {0, 0, 0, 0, 0, 0, 0, 0};  // 0 even window offset, 1 offset -1,
+                                                       // 2 offset +1, 3 global (far)
+  double v0[kRpUniMax] = {0, 0, 0, 0, 0, 0, 0, 0};     // row 2i's value at each slot
+  double v1[kRpUniMax] = {0, 0, 0, 0, 0, 0, 0, 0};     // row 2i+1's
+};
+
 // Tolerance arguments: tol >= 0 arms the device stop flag with ||.|| <= tol (the reference's
 // `e <= tol`, ns/lib/multigrid.py:197, MLAMG.py:194 — tol = 0 included: an exactly zero norm
 // stops); a negative tol means "no tolerance" (run every requested cycle).
@@ -177,6 +193,8 @@ struct mlamg_csr {
   uint16_t* rp_slot = nullptr;         // its slot order: pattern | local pair << 8, per workgroup
                                        // sorted by pattern
   std::vector<int32_t> rp_rep;         // representative pair of each pattern (host)
+  mlamg::RpUni rp_uni;                 // uniform-stencil form (k_rowpat_uni; k == 0: none)
+  uint16_t* rp_msk = nullptr;          // its per-pattern slot masks (row 2i | row 2i+1 << 8)
   // attached Jacobi weights (mlamg_csr_attach_dinv): an epilogue whose dinv pointer equals
   // rp_dinv_att reads the per-pattern values rp_dinv[2p], rp_dinv[2p+1] instead of memory
   const double* rp_dinv_att = nullptr;
@@ -198,6 +216,32 @@ struct mlamg_dense {
                    // (lower) with X^T (strict upper) applied as two triangular passes (dense.hip)
   double* y = nullptr;  // method 2: the intermediate X b
 };
+
+namespace mlamg {
+// Correctly rounded a / b off a dependency chain's critical path. Gauss-Seidel's x_i =
+// (b_i - rsum) / a_ii sits on the sweep's level-to-level chain, and the IEEE division is ~11
+// dependent operations (div_scale, rcp, 4 refinement fmas, mul, fma, div_fmas, div_fixup). The
+// reciprocal y = RN(1 / a_ii) does not depend on the chain, so it is computed when the row's
+// data is loaded (mk_recip), and the chain keeps 3 operations (mk_div): q = RN(a y), the exact
+// remainder r = a - b q (one fma), q' = RN(q + r y). Markstein's theorem: with y the correctly
+// rounded reciprocal and q within one ulp of a / b, q' = RN(a / b) — the IEEE quotient — barring
+// overflow and underflow, which are excluded by range checks on |b| (at recip time), |a| and |q|;
+// outside them, and for a = 0 (the sign of a zero quotient), the plain division is taken.
+// Checked against the IEEE division on 2e8 random operand pairs and the special values
+// (tests/test_markstein.py, oracle/markstein_check.c): no mismatch.
+__device__ __forceinline__ double mk_recip(double b) {
+  const double ab = __builtin_fabs(b);
+  return (ab >= 0x1p-1000 && ab <= 0x1p1000) ? 1.0 / b : __builtin_nan("");
+}
+__device__ __forceinline__ double mk_div(double a, double b, double y) {
+  const double q = a * y;
+  const double r = __builtin_fma(-b, q, a);
+  const double aq = __builtin_fabs(q), aa = __builtin_fabs(a);
+  if (aq >= 0x1p-960 && aq <= 0x1p960 && aa >= 0x1p-960 && aa <= 0x1p960)
+    return __builtin_fma(r, y, q);
+  return a / b;
+}
+}  // namespace mlamg
 
 namespace mlamg {
 // s = p[start] + p[start+step] + ... in that order (bitwise a plain strided loop), with the loads

@@ -241,6 +241,8 @@ void csr_free(mlamg_csr* A) {
   if (A->rp_off) (void)hipFree(A->rp_off);
   if (A->rp_val) (void)hipFree(A->rp_val);
   if (A->rp_dinv) (void)hipFree(A->rp_dinv);
+  if (A->rp_slot) (void)hipFree(A->rp_slot);
+  if (A->rp_msk) (void)hipFree(A->rp_msk);
   if (A->lg_tile) (void)hipFree(A->lg_tile);
   delete A;
 }

@@ -639,6 +639,171 @@ void k_rowpair(const uint8_t* __restrict__ pid,
   }
 }
 
+// ---------------------------------------------------------------- uniform row-pair stencils
+// k_rowpat_uni: the row-pair pattern format for operators whose pattern entries all come from
+// ONE list of <= 8 column offsets with one value per (offset, row parity) — constant-coefficient
+// stencils, where the patterns only differ in which neighbours a boundary row lacks (C4 A_0: 27
+// patterns over the 7 offsets -n^2 -n -1 0 1 n n^2). A pattern is then a 16-bit mask (the slots
+// row 2i and row 2i+1 have) in a 512-byte LDS table and the values are kernel arguments. Same pid
+// bytes and the same lane -> pair map as k_rowpair (chunk c of workgroup lb: pairs
+// lb*CH*256 + c*256 + lane), so the products, their order and the norm partials are k_rowpair's,
+// i.e. scipy's (an entry a row lacks is a +0.0 operand: a sum started at +0.0 is never -0.0, so
+// adding it changes no bit). The x operands within +-halo rows come from an LDS window of the
+// workgroup's 2 CH 256 rows plus the halo, staged once with 16-byte loads (k_rowpair issues 7
+// 16-byte texture loads per pair; tools/stencil_lab.hip k_pair_tile: 24.4 us for the C4 stencil
+// against 32.6 us with every neighbour a global load, 23.2 us for a copy of x into y): even
+// offsets are one aligned 16-byte LDS read, -1 / +1 take the neighbouring pairs' reads. The far
+// offsets (C4: +-n^2) are 16-byte global loads, chunk c + 1's issued while chunk c sums. An
+// epilogue operand equal to x (Jacobi's xin, the fused sweep's copy_from) comes from the window.
+template <int OP, bool NORM, int CH>
+__global__ __launch_bounds__(kThreads)
+__attribute__((amdgpu_waves_per_eu(MLAMG_RP_WAVES > 0 ? MLAMG_RP_WAVES : 1, 8)))
+void k_rowpat_uni(const uint8_t* __restrict__ pid, const uint16_t* __restrict__ pat_msk,
+                  int n_pat, int64_t n_rows, int64_t n_cols, const double* __restrict__ dinv_att,
+                  const dbl2* __restrict__ pat_dinv, RpUni U, const double* __restrict__ x,
+                  Epi ep) {
+  // LDS: window[CH 256 + halo] (dbl2) | dinv[n_pat] (dbl2) | mask[256] (uint16)
+  extern __shared__ dbl2 uni_lds[];
+  __shared__ double red[kThreads / 64];
+  if (ep.done && *ep.done) return;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const int hw = U.halo >> 1;  // halo in pairs
+  const int nwin = CH * kThreads + 2 * hw;
+  dbl2* win = uni_lds;
+  dbl2* dt = win + nwin;
+  uint16_t* msk = reinterpret_cast<uint16_t*>(dt + n_pat);
+  const bool tab_dinv = ep.dinv != nullptr && ep.dinv == dinv_att;
+  bool x_op = false;
+  if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) x_op = ep.xin == x;
+  if constexpr (OP == EPI_RESID) x_op = ep.copy_to != nullptr && ep.copy_from == x;
+  const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t p0 = lb * CH * kThreads;  // the workgroup's first pair
+  const int64_t T0 = 2 * p0 - U.halo;     // its first window row (even)
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(n_cols * 8), 0x00020000);
+  // x[g], x[g + 1] as one 16-byte load when both are in range, else per element (zeros outside)
+  auto ld16 = [&](int64_t g) -> dbl2 {
+    if (g >= 0 && g + 1 < n_cols) {
+      const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(g * 8), 0, 0);
+      return dbl2{__builtin_bit_cast(double, (uint64_t)t.x | ((uint64_t)t.y << 32)),
+                  __builtin_bit_cast(double, (uint64_t)t.z | ((uint64_t)t.w << 32))};
+    }
+    return dbl2{(g >= 0 && g < n_cols) ? x[g] : 0.0, (g + 1 >= 0 && g + 1 < n_cols) ? x[g + 1] : 0.0};
+  };
+  // the far slots (kind 3), at most kRpUniFar, in slot order
+  int fq[kRpUniFar], fo[kRpUniFar], nf = 0;
+#pragma unroll
+  for (int t = 0; t < kRpUniFar; ++t) {
+    fq[t] = -1;
+    fo[t] = 0;
+  }
+#pragma unroll
+  for (int q = 0; q < kRpUniMax; ++q)
+    if (q < U.k && U.kind[q] == 3) {
+#pragma unroll
+      for (int t = 0; t < kRpUniFar; ++t)
+        if (t == nf) {
+          fq[t] = q;
+          fo[t] = U.off[q];
+        }
+      ++nf;
+    }
+  // chunk 0's pattern ids and far operands, then the window
+  const int64_t pa = p0 + threadIdx.x;
+  int pcur = 2 * pa < n_rows ? (int)pid[pa] : 0;
+  dbl2 fcur[kRpUniFar];
+#pragma unroll
+  for (int t = 0; t < kRpUniFar; ++t)
+    fcur[t] = (fq[t] >= 0 && 2 * pa < n_rows) ? ld16(2 * pa + fo[t]) : dbl2{0.0, 0.0};
+  constexpr int WQ = CH + 2;  // window slots per thread in registers (halo <= 256 pairs a side)
+  dbl2 wv[WQ];
+#pragma unroll
+  for (int q = 0; q < WQ; ++q) {
+    const int i = threadIdx.x + q * kThreads;
+    wv[q] = i < nwin ? ld16(T0 + 2 * (int64_t)i) : dbl2{0.0, 0.0};
+  }
+#pragma unroll
+  for (int q = 0; q < WQ; ++q) {
+    const int i = threadIdx.x + q * kThreads;
+    if (i < nwin) win[i] = wv[q];
+  }
+  for (int i = threadIdx.x; i < 256; i += kThreads) msk[i] = i < n_pat ? pat_msk[i] : 0;
+  if (tab_dinv)
+    for (int i = threadIdx.x; i < n_pat; i += kThreads) dt[i] = pat_dinv[i];
+  __syncthreads();
+  double sq = 0.0;
+#pragma unroll 1
+  for (int c = 0; c < CH; ++c) {
+    const int64_t pr = pa + (int64_t)c * kThreads;
+    const bool ok0 = 2 * pr < n_rows;
+    const bool both = 2 * pr + 1 < n_rows;
+    const int r = ok0 ? (int)(2 * pr) : 0;
+    EpiIn u, w;
+    if (ok0) epi_load2<OP>(r, both, ep, u, w, tab_dinv, x_op);
+    // the next chunk's id and far operands, in flight while this one sums
+    const int64_t prn = pr + kThreads;
+    const bool okn = c + 1 < CH && 2 * prn < n_rows;
+    const int pnext = okn ? (int)pid[prn] : 0;
+    dbl2 fnext[kRpUniFar];
+#pragma unroll
+    for (int t = 0; t < kRpUniFar; ++t)
+      fnext[t] = (fq[t] >= 0 && okn) ? ld16(2 * prn + fo[t]) : dbl2{0.0, 0.0};
+    const int pl = c * kThreads + (int)threadIdx.x + hw;  // this pair's window slot
+    const dbl2 xc = win[pl];
+    const dbl2 xl = win[pl - 1];
+    const dbl2 xr = win[pl + 1];
+    const int m = msk[pcur];
+    if (tab_dinv) {
+      const dbl2 d = dt[pcur];
+      u.c = d.x;
+      w.c = d.y;
+    }
+    if (x_op) {
+      u.b = xc.x;
+      w.b = xc.y;
+    }
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < kRpUniMax; ++q) {
+      if (q >= U.k) break;
+      const int kd = U.kind[q];
+      double t0, t1;
+      if (kd == 0) {
+        const dbl2 v = win[pl + (U.off[q] >> 1)];
+        t0 = v.x;
+        t1 = v.y;
+      } else if (kd == 1) {
+        t0 = xl.y;
+        t1 = xc.x;
+      } else if (kd == 2) {
+        t0 = xc.y;
+        t1 = xr.x;
+      } else {
+        t0 = fq[0] == q ? fcur[0].x : fcur[kRpUniFar - 1].x;
+        t1 = fq[0] == q ? fcur[0].y : fcur[kRpUniFar - 1].y;
+      }
+      const double y0 = (m >> q) & 1 ? t0 : 0.0;
+      const double y1 = (m >> (q + 8)) & 1 ? t1 : 0.0;
+      s0 += U.v0[q] * y0;
+      s1 += U.v1[q] * y1;
+    }
+    if (ok0) sq += epi_store2<OP>(r, both, s0, s1, u, w, ep);
+    pcur = pnext;
+#pragma unroll
+    for (int t = 0; t < kRpUniFar; ++t) fcur[t] = fnext[t];
+  }
+  if constexpr (NORM) {
+    double v = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+      ep.partial[lb] = t;
+    }
+  }
+}
+
 // Row-pair patterns with LDS row windows (C4 A_0: the x gathers, not HBM, bound k_rowpair —
 // 7 16-byte loads per pair through the texture path, 36-38 us; tools/stencil_lab.hip: a 216^3
 // 7-point stencil 32.6 us with every neighbour a global load, 24.4 us with x staged per
@@ -1584,6 +1749,18 @@ static int launch_rowpair_ch(const mlamg_csr* A, const double* x, const Epi& ep,
 
 template <int OP, bool NORM>
 static int launch_rowpair(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  if (A->rp_uni.k > 0 && A->rp_msk) {
+    const int64_t n_pairs = (A->n_rows + 1) / 2;
+    constexpr int CH = kRpChunks;
+    const unsigned nb = (unsigned)((n_pairs + CH * kThreads - 1) / (CH * kThreads));
+    const size_t lds = sizeof(dbl2) * (size_t)(CH * kThreads + A->rp_uni.halo + A->rp_n_pat) +
+                       sizeof(uint16_t) * 256;
+    hipLaunchKernelGGL((k_rowpat_uni<OP, NORM, CH>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid,
+                       A->rp_msk, A->rp_n_pat, A->n_rows, A->n_cols, A->rp_dinv_att,
+                       reinterpret_cast<const dbl2*>(A->rp_dinv), A->rp_uni, x, ep);
+    MLAMG_HIP(hipGetLastError());
+    return MLAMG_OK;
+  }
   if (A->rp_win.rows >= 0 && A->rp_slot) {
     const int64_t n_pairs = (A->n_rows + 1) / 2;
     const unsigned nb = (unsigned)((n_pairs + kRpWinNT - 1) / kRpWinNT);
@@ -2448,8 +2625,10 @@ __global__ void k_rp_assign(const int32_t* __restrict__ ip, const int32_t* __res
 
 static void drop_rowpat(mlamg_csr* A) {
   for (void* p : {(void*)A->rp_pid, (void*)A->rp_ptr, (void*)A->rp_off, (void*)A->rp_val,
-                  (void*)A->rp_dinv, (void*)A->rp_slot})
+                  (void*)A->rp_dinv, (void*)A->rp_slot, (void*)A->rp_msk})
     if (p) (void)hipFree(p);
+  A->rp_msk = nullptr;
+  A->rp_uni = RpUni{};
   A->rp_slot = nullptr;
   A->rp_dinv = nullptr;
   A->rp_dinv_att = nullptr;
@@ -2516,6 +2695,8 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
     fail(MLAMG_EUNSUPPORTED, "more than 255 distinct row-pair patterns");
   std::vector<int32_t> hptr(257, 0), hoff, reps;
   RpWin win{};
+  RpUni uni{};
+  std::vector<uint16_t> hmsk;
   int kstep = 8;
   std::vector<double> hv0, hv1;
   std::vector<uint8_t> hfl;
@@ -2556,6 +2737,7 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
     };
     std::vector<std::vector<Ent>> pent(pats.size());
     std::vector<bool> pwide(pats.size(), false);
+    bool all_sorted = true;
     size_t maxlen = 0;
     for (size_t k = 0; k < pats.size() && rc == MLAMG_OK; ++k) {
       hslot[pats[k].second] = (int32_t)k;
@@ -2567,6 +2749,7 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
       bool sorted_rows = true;
       for (auto* o : {&o0, &o1})
         for (size_t e = 1; e < o->size(); ++e) sorted_rows = sorted_rows && (*o)[e] > (*o)[e - 1];
+      all_sorted = all_sorted && sorted_rows;
       // wide (see rp_pair_wide): the same rule on the representative pair
       bool wide = r0 + 1 < n;
       for (int32_t o : o0) wide = wide && r0 + o <= A->n_cols - 2;
@@ -2612,6 +2795,61 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
       }
       pwide[k] = wide;
       maxlen = std::max(maxlen, pe.size());
+    }
+    // uniform form (k_rowpat_uni): every entry one of <= kRpUniMax offsets with one value per
+    // (offset, row parity), rows in ascending column order (then each row sums in slot order)
+    {
+      const char* ev = std::getenv("MLAMG_RP_UNI");
+      bool ok = all_sorted && !(ev && ev[0] == '0') && n_pat <= 255;
+      std::vector<int32_t> offs;
+      for (auto& pe : pent)
+        for (auto& en : pe)
+          if (en.fl & 3) offs.push_back(en.off);
+      std::sort(offs.begin(), offs.end());
+      offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
+      ok = ok && !offs.empty() && offs.size() <= (size_t)kRpUniMax;
+      bool set0[kRpUniMax] = {}, set1[kRpUniMax] = {};
+      hmsk.assign(pent.size(), 0);
+      for (size_t k = 0; ok && k < pent.size(); ++k)
+        for (auto& en : pent[k]) {
+          if (!(en.fl & 3)) continue;
+          const int q = (int)(std::lower_bound(offs.begin(), offs.end(), en.off) - offs.begin());
+          auto same = [](double a, double b) {
+            return __builtin_bit_cast(uint64_t, a) == __builtin_bit_cast(uint64_t, b);
+          };
+          if (en.fl & 1) {
+            if (!set0[q]) uni.v0[q] = en.v0;
+            ok = ok && same(uni.v0[q], en.v0);
+            set0[q] = true;
+            hmsk[k] |= (uint16_t)(1u << q);
+          }
+          if (en.fl & 2) {
+            if (!set1[q]) uni.v1[q] = en.v1;
+            ok = ok && same(uni.v1[q], en.v1);
+            set1[q] = true;
+            hmsk[k] |= (uint16_t)(1u << (q + 8));
+          }
+        }
+      int halo = 2, nfar = 0;
+      for (size_t q = 0; ok && q < offs.size(); ++q) {
+        const int32_t o = offs[q];
+        int kd;
+        if (o == -1) kd = 1;
+        else if (o == 1) kd = 2;
+        else if ((o & 1) == 0 && std::abs(o) <= kRpUniMaxHalo) kd = 0;
+        else kd = 3;
+        if (kd == 0) halo = std::max(halo, std::abs(o));
+        if (kd == 3) ++nfar;
+        uni.off[q] = o;
+        uni.kind[q] = kd;
+      }
+      ok = ok && nfar <= kRpUniFar;
+      uni.k = ok ? (int32_t)offs.size() : 0;
+      uni.halo = ok ? halo : 0;
+      if (!ok) {
+        uni = RpUni{};
+        hmsk.clear();
+      }
     }
     // the kernel's step: the longest pattern when it fits one step of 5..8 entries, else 8;
     // every pattern is padded with null entries to whole steps
@@ -2768,7 +3006,19 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
       win = RpWin{};
     }
   }
+  uint16_t* pmsk = nullptr;
+  if (uni.k > 0) {
+    hmsk.resize(256, 0);
+    if (hipMalloc(&pmsk, sizeof(uint16_t) * 256) != hipSuccess ||
+        hipMemcpy(pmsk, hmsk.data(), sizeof(uint16_t) * 256, hipMemcpyHostToDevice) != hipSuccess) {
+      if (pmsk) (void)hipFree(pmsk);
+      pmsk = nullptr;
+      uni = RpUni{};
+    }
+  }
   drop_rowpat(A);
+  A->rp_uni = uni;
+  A->rp_msk = pmsk;
   A->rp_win = win;
   A->rp_slot = pslot;
   A->rp_pid = pid;
@@ -3054,6 +3304,8 @@ int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
     b += (A->vec_idx16 ? 10.0 : 12.0) * A->nnz + 4.0 * (n + 1);
   } else if (A->lg_tile) {
     b += 12.0 * A->nnz + 4.0 * (n + 1) + 4.0 * (A->lg_nt + 1);
+  } else if (A->rp_pid && A->rp_uni.k > 0) {
+    b += 1.0 * ((A->n_rows + 1) / 2) + 2.0 * 256;  // pair ids + the mask table
   } else if (A->rp_pid) {
     b += 1.0 * ((A->n_rows + 1) / 2) + 4.0 * 257 + 32.0 * A->rp_n_ent;  // pair ids + tables
   } else if (A->srt_pk) {

@@ -184,7 +184,8 @@ def _pyamg_bf_literal(G, seeds, dt=np.float32):
 @pytest.mark.parametrize("kind", ("random", "unit_ties", "disconnected"))
 def test_oracle_pyamg_bellman_ford(oracle, kind):
     """oracle.pyamg_bellman_ford (the restatement of the aggregation step FullAggNet runs,
-    ns/model/agg_interp.py:475) against a literal transcription of pyamg 4.x: distances, nearest
+    ns/model/agg_interp.py:475) against a second, independent Python restatement of pyamg 4.x
+    (a self-consistency check of two restatements — parity unpinned, pyamg absent): distances, nearest
     seeds (first strictly better in sweep order — ties included) and the sweep count; its
     distances are the order-independent fixed point the device's own Bellman-Ford computes."""
     import scipy.sparse as sp
