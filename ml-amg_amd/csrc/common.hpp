@@ -109,8 +109,10 @@ constexpr int kRpUniMax = 8;
 constexpr int kRpUniFar = 2;
 constexpr int kRpUniMaxHalo = 512;  // rows staged on each side of a workgroup's rows, at most
 struct RpUni {
-  int32_t k = 0;     // slots (0: not uniform)
-  int32_t halo = 0;  // staged rows on each side (even)
+  int32_t k = 0;       // slots (0: not uniform)
+  int32_t halo = 0;    // staged rows on each side (even)
+  int32_t layout = 0;  // compile-time slot layout of k_rowpat_uni (0: run-time kinds)
+  int32_t ch = 4;      // 256-pair chunks per workgroup (1, 2 or 4)
   int32_t off[kRpUniMax] = {0, 0, 0, 0, 0, 0, 0, 0};   // slot column offsets, ascending
   int32_t kind[kRpUniMax] = {0, 0, 0, 0, 0, 0, 0, 0};  // 0 even window offset, 1 offset -1,
                                                        // 2 offset +1, 3 global (far)

@@ -645,28 +645,53 @@ void k_rowpair(const uint8_t* __restrict__ pid,
 // stencils, where the patterns only differ in which neighbours a boundary row lacks (C4 A_0: 27
 // patterns over the 7 offsets -n^2 -n -1 0 1 n n^2). A pattern is then a 16-bit mask (the slots
 // row 2i and row 2i+1 have) in a 512-byte LDS table and the values are kernel arguments. Same pid
-// bytes and the same lane -> pair map as k_rowpair (chunk c of workgroup lb: pairs
-// lb*CH*256 + c*256 + lane), so the products, their order and the norm partials are k_rowpair's,
-// i.e. scipy's (an entry a row lacks is a +0.0 operand: a sum started at +0.0 is never -0.0, so
-// adding it changes no bit). The x operands within +-halo rows come from an LDS window of the
-// workgroup's 2 CH 256 rows plus the halo, staged once with 16-byte loads (k_rowpair issues 7
-// 16-byte texture loads per pair; tools/stencil_lab.hip k_pair_tile: 24.4 us for the C4 stencil
-// against 32.6 us with every neighbour a global load, 23.2 us for a copy of x into y): even
-// offsets are one aligned 16-byte LDS read, -1 / +1 take the neighbouring pairs' reads. The far
-// offsets (C4: +-n^2) are 16-byte global loads, chunk c + 1's issued while chunk c sums. An
-// epilogue operand equal to x (Jacobi's xin, the fused sweep's copy_from) comes from the window.
-template <int OP, bool NORM, int CH>
-__global__ __launch_bounds__(kThreads)
-__attribute__((amdgpu_waves_per_eu(MLAMG_RP_WAVES > 0 ? MLAMG_RP_WAVES : 1, 8)))
-void k_rowpat_uni(const uint8_t* __restrict__ pid, const uint16_t* __restrict__ pat_msk,
-                  int n_pat, int64_t n_rows, int64_t n_cols, const double* __restrict__ dinv_att,
-                  const dbl2* __restrict__ pat_dinv, RpUni U, const double* __restrict__ x,
-                  Epi ep) {
+// bytes as k_rowpair; chunk c of workgroup lb holds pairs lb*CH*256 + c*256 + lane, and with
+// CH = kRpChunks the lane -> pair map, the norm partials and every product and sum are
+// k_rowpair's, i.e. scipy's (an entry a row lacks is a +0.0 operand: a sum started at +0.0 is
+// never -0.0, so adding it changes no bit). The x operands within +-halo rows come from an LDS
+// window of the workgroup's 2 CH 256 rows plus the halo, staged once with 16-byte loads
+// (k_rowpair issues 7 16-byte texture loads per pair; tools/stencil_lab.hip k_pair_tile: 24.4 us
+// for the C4 stencil against 32.6 us with every neighbour a global load): even offsets are one
+// aligned 16-byte LDS read, -1 / +1 take the neighbouring pairs' reads. The far offsets (C4:
+// +-n^2) are 16-byte global loads, all issued before the staging. An epilogue operand equal to
+// x (Jacobi's xin, the fused sweep's copy_from) comes from the window. Every load is
+// branch-free: an address is clamped into x and the lanes it does not cover are selected to
+// zero (a branch join makes the compiler wait for every load in flight).
+// LY: slot layout (kinds in slot order; 0 even window offset, 1 offset -1, 2 offset +1, 3 far):
+// 1 = {3,0,1,0,2,0,3} (3-D 7-point), 2 = {0,1,0,2,0} (2-D 5-point, +-n staged),
+// 3 = {3,1,0,2,3} (2-D 5-point, +-n far), 0 = any (run-time kinds).
+__device__ __forceinline__ dbl2 x16(const double* __restrict__ x, int64_t g, int64_t n) {
+  const int64_t gc = g < 0 ? 0 : (g > n - 2 ? n - 2 : g);
+  const dbl2 t = *reinterpret_cast<const dbl2u*>(x + gc);
+  // g == gc: both in range; g == -1: (0, x[0]) = (0, t.x); g == n - 1: (x[n-1], 0) = (t.y, 0)
+  dbl2 o;
+  o.x = g == gc ? t.x : (g == n - 1 ? t.y : 0.0);
+  o.y = g == gc ? t.y : (g == -1 ? t.x : 0.0);
+  return o;
+}
+
+template <int LY>
+__device__ __forceinline__ int uni_kind(const RpUni& U, int q) {
+  constexpr int k1[7] = {3, 0, 1, 0, 2, 0, 3}, k2[5] = {0, 1, 0, 2, 0}, k3[5] = {3, 1, 0, 2, 3};
+  if constexpr (LY == 1) return k1[q < 7 ? q : 0];
+  if constexpr (LY == 2) return k2[q < 5 ? q : 0];
+  if constexpr (LY == 3) return k3[q < 5 ? q : 0];
+  return U.kind[q];
+}
+template <int LY>
+__device__ __forceinline__ int uni_k(const RpUni& U) {
+  return LY == 1 ? 7 : (LY == 2 || LY == 3) ? 5 : U.k;
+}
+
+template <int OP, bool NORM, int CH, int LY>
+__global__ __launch_bounds__(kThreads) void k_rowpat_uni(
+    const uint8_t* __restrict__ pid, const uint16_t* __restrict__ pat_msk, int n_pat,
+    int64_t n_rows, int64_t n_cols, const double* __restrict__ dinv_att,
+    const dbl2* __restrict__ pat_dinv, RpUni U, const double* __restrict__ x, Epi ep) {
   // LDS: window[CH 256 + halo] (dbl2) | dinv[n_pat] (dbl2) | mask[256] (uint16)
   extern __shared__ dbl2 uni_lds[];
   __shared__ double red[kThreads / 64];
   if (ep.done && *ep.done) return;
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const int hw = U.halo >> 1;  // halo in pairs
   const int nwin = CH * kThreads + 2 * hw;
   dbl2* win = uni_lds;
@@ -676,51 +701,39 @@ void k_rowpat_uni(const uint8_t* __restrict__ pid, const uint16_t* __restrict__ 
   bool x_op = false;
   if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) x_op = ep.xin == x;
   if constexpr (OP == EPI_RESID) x_op = ep.copy_to != nullptr && ep.copy_from == x;
+  const int K = uni_k<LY>(U);
   const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
   const int64_t p0 = lb * CH * kThreads;  // the workgroup's first pair
   const int64_t T0 = 2 * p0 - U.halo;     // its first window row (even)
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(n_cols * 8), 0x00020000);
-  // x[g], x[g + 1] as one 16-byte load when both are in range, else per element (zeros outside)
-  auto ld16 = [&](int64_t g) -> dbl2 {
-    if (g >= 0 && g + 1 < n_cols) {
-      const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(g * 8), 0, 0);
-      return dbl2{__builtin_bit_cast(double, (uint64_t)t.x | ((uint64_t)t.y << 32)),
-                  __builtin_bit_cast(double, (uint64_t)t.z | ((uint64_t)t.w << 32))};
-    }
-    return dbl2{(g >= 0 && g < n_cols) ? x[g] : 0.0, (g + 1 >= 0 && g + 1 < n_cols) ? x[g + 1] : 0.0};
-  };
-  // the far slots (kind 3), at most kRpUniFar, in slot order
-  int fq[kRpUniFar], fo[kRpUniFar], nf = 0;
-#pragma unroll
-  for (int t = 0; t < kRpUniFar; ++t) {
-    fq[t] = -1;
-    fo[t] = 0;
-  }
-#pragma unroll
-  for (int q = 0; q < kRpUniMax; ++q)
-    if (q < U.k && U.kind[q] == 3) {
-#pragma unroll
-      for (int t = 0; t < kRpUniFar; ++t)
-        if (t == nf) {
-          fq[t] = q;
-          fo[t] = U.off[q];
-        }
-      ++nf;
-    }
-  // chunk 0's pattern ids and far operands, then the window
   const int64_t pa = p0 + threadIdx.x;
-  int pcur = 2 * pa < n_rows ? (int)pid[pa] : 0;
-  dbl2 fcur[kRpUniFar];
+  // far offsets (slot order)
+  int fo[kRpUniFar];
+  {
+    int nf = 0;
 #pragma unroll
-  for (int t = 0; t < kRpUniFar; ++t)
-    fcur[t] = (fq[t] >= 0 && 2 * pa < n_rows) ? ld16(2 * pa + fo[t]) : dbl2{0.0, 0.0};
-  constexpr int WQ = CH + 2;  // window slots per thread in registers (halo <= 256 pairs a side)
+    for (int t = 0; t < kRpUniFar; ++t) fo[t] = 0;
+#pragma unroll
+    for (int q = 0; q < kRpUniMax; ++q)
+      if (q < K && uni_kind<LY>(U, q) == 3) {
+#pragma unroll
+        for (int t = 0; t < kRpUniFar; ++t)
+          if (t == nf) fo[t] = U.off[q];
+        ++nf;
+      }
+  }
+  constexpr int NF = LY == 1 || LY == 3 ? 2 : (LY == 2 ? 0 : kRpUniFar);
+  constexpr int NFR = NF > 0 ? NF : 1;
+  // chunk 0's id and far operands, then the window: all loads before the first LDS store
+  int pcur = pid[2 * pa < n_rows ? pa : 0];
+  dbl2 fcur[NFR];
+#pragma unroll
+  for (int t = 0; t < NF; ++t) fcur[t] = x16(x, 2 * pa + fo[t], n_cols);
+  constexpr int WQ = CH + 2;  // window slots per thread (halo <= 256 pairs a side)
   dbl2 wv[WQ];
 #pragma unroll
   for (int q = 0; q < WQ; ++q) {
     const int i = threadIdx.x + q * kThreads;
-    wv[q] = i < nwin ? ld16(T0 + 2 * (int64_t)i) : dbl2{0.0, 0.0};
+    wv[q] = x16(x, T0 + 2 * (int64_t)(i < nwin ? i : 0), n_cols);
   }
 #pragma unroll
   for (int q = 0; q < WQ; ++q) {
@@ -742,12 +755,10 @@ void k_rowpat_uni(const uint8_t* __restrict__ pid, const uint16_t* __restrict__ 
     if (ok0) epi_load2<OP>(r, both, ep, u, w, tab_dinv, x_op);
     // the next chunk's id and far operands, in flight while this one sums
     const int64_t prn = pr + kThreads;
-    const bool okn = c + 1 < CH && 2 * prn < n_rows;
-    const int pnext = okn ? (int)pid[prn] : 0;
-    dbl2 fnext[kRpUniFar];
+    const int pnext = pid[c + 1 < CH && 2 * prn < n_rows ? prn : 0];
+    dbl2 fnext[NFR];
 #pragma unroll
-    for (int t = 0; t < kRpUniFar; ++t)
-      fnext[t] = (fq[t] >= 0 && okn) ? ld16(2 * prn + fo[t]) : dbl2{0.0, 0.0};
+    for (int t = 0; t < NF; ++t) fnext[t] = x16(x, 2 * prn + fo[t], n_cols);
     const int pl = c * kThreads + (int)threadIdx.x + hw;  // this pair's window slot
     const dbl2 xc = win[pl];
     const dbl2 xl = win[pl - 1];
@@ -763,34 +774,38 @@ void k_rowpat_uni(const uint8_t* __restrict__ pid, const uint16_t* __restrict__ 
       w.b = xc.y;
     }
     double s0 = 0.0, s1 = 0.0;
+    int tf = 0;
 #pragma unroll
     for (int q = 0; q < kRpUniMax; ++q) {
-      if (q >= U.k) break;
-      const int kd = U.kind[q];
-      double t0, t1;
-      if (kd == 0) {
-        const dbl2 v = win[pl + (U.off[q] >> 1)];
-        t0 = v.x;
-        t1 = v.y;
-      } else if (kd == 1) {
-        t0 = xl.y;
-        t1 = xc.x;
-      } else if (kd == 2) {
-        t0 = xc.y;
-        t1 = xr.x;
-      } else {
-        t0 = fq[0] == q ? fcur[0].x : fcur[kRpUniFar - 1].x;
-        t1 = fq[0] == q ? fcur[0].y : fcur[kRpUniFar - 1].y;
+      if (q < K) {
+        const int kd = uni_kind<LY>(U, q);
+        double t0, t1;
+        if (kd == 0) {
+          const dbl2 v = win[pl + (U.off[q] >> 1)];
+          t0 = v.x;
+          t1 = v.y;
+        } else if (kd == 1) {
+          t0 = xl.y;
+          t1 = xc.x;
+        } else if (kd == 2) {
+          t0 = xc.y;
+          t1 = xr.x;
+        } else {
+          const dbl2 f = NF > 1 && tf == 1 ? fcur[NFR - 1] : fcur[0];
+          t0 = f.x;
+          t1 = f.y;
+          ++tf;
+        }
+        const double y0 = (m >> q) & 1 ? t0 : 0.0;
+        const double y1 = (m >> (q + 8)) & 1 ? t1 : 0.0;
+        s0 += U.v0[q] * y0;
+        s1 += U.v1[q] * y1;
       }
-      const double y0 = (m >> q) & 1 ? t0 : 0.0;
-      const double y1 = (m >> (q + 8)) & 1 ? t1 : 0.0;
-      s0 += U.v0[q] * y0;
-      s1 += U.v1[q] * y1;
     }
     if (ok0) sq += epi_store2<OP>(r, both, s0, s1, u, w, ep);
     pcur = pnext;
 #pragma unroll
-    for (int t = 0; t < kRpUniFar; ++t) fcur[t] = fnext[t];
+    for (int t = 0; t < NF; ++t) fcur[t] = fnext[t];
   }
   if constexpr (NORM) {
     double v = wave_sum(sq);
@@ -1747,19 +1762,35 @@ static int launch_rowpair_ch(const mlamg_csr* A, const double* x, const Epi& ep,
   }
 }
 
+template <int OP, bool NORM, int CH>
+static int launch_rowpat_uni(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  const int64_t n_pairs = (A->n_rows + 1) / 2;
+  const unsigned nb = (unsigned)((n_pairs + CH * kThreads - 1) / (CH * kThreads));
+  const size_t lds = sizeof(dbl2) * (size_t)(CH * kThreads + A->rp_uni.halo + A->rp_n_pat) +
+                     sizeof(uint16_t) * 256;
+#define MLAMG_RPU(LYV)                                                                           \
+  hipLaunchKernelGGL((k_rowpat_uni<OP, NORM, CH, LYV>), dim3(nb), dim3(kThreads), lds, s,        \
+                     A->rp_pid, A->rp_msk, A->rp_n_pat, A->n_rows, A->n_cols, A->rp_dinv_att,    \
+                     reinterpret_cast<const dbl2*>(A->rp_dinv), A->rp_uni, x, ep)
+  switch (A->rp_uni.layout) {
+    case 1: MLAMG_RPU(1); break;
+    case 2: MLAMG_RPU(2); break;
+    case 3: MLAMG_RPU(3); break;
+    default: MLAMG_RPU(0); break;
+  }
+#undef MLAMG_RPU
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
 template <int OP, bool NORM>
 static int launch_rowpair(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   if (A->rp_uni.k > 0 && A->rp_msk) {
-    const int64_t n_pairs = (A->n_rows + 1) / 2;
-    constexpr int CH = kRpChunks;
-    const unsigned nb = (unsigned)((n_pairs + CH * kThreads - 1) / (CH * kThreads));
-    const size_t lds = sizeof(dbl2) * (size_t)(CH * kThreads + A->rp_uni.halo + A->rp_n_pat) +
-                       sizeof(uint16_t) * 256;
-    hipLaunchKernelGGL((k_rowpat_uni<OP, NORM, CH>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid,
-                       A->rp_msk, A->rp_n_pat, A->n_rows, A->n_cols, A->rp_dinv_att,
-                       reinterpret_cast<const dbl2*>(A->rp_dinv), A->rp_uni, x, ep);
-    MLAMG_HIP(hipGetLastError());
-    return MLAMG_OK;
+    switch (A->rp_uni.ch) {
+      case 1: return launch_rowpat_uni<OP, NORM, 1>(A, x, ep, s);
+      case 2: return launch_rowpat_uni<OP, NORM, 2>(A, x, ep, s);
+      default: return launch_rowpat_uni<OP, NORM, 4>(A, x, ep, s);
+    }
   }
   if (A->rp_win.rows >= 0 && A->rp_slot) {
     const int64_t n_pairs = (A->n_rows + 1) / 2;
@@ -2843,8 +2874,24 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
         uni.off[q] = o;
         uni.kind[q] = kd;
       }
-      ok = ok && nfar <= kRpUniFar;
+      ok = ok && nfar <= kRpUniFar && A->n_cols >= 2;
       uni.k = ok ? (int32_t)offs.size() : 0;
+      auto kinds_are = [&](std::initializer_list<int> ks) {
+        if ((size_t)uni.k != ks.size()) return false;
+        int q = 0;
+        for (int kd : ks)
+          if (uni.kind[q++] != kd) return false;
+        return true;
+      };
+      {
+        const char* ec = std::getenv("MLAMG_RPU_CH");  // A/B knob
+        const int chv = ec ? std::atoi(ec) : 4;
+        uni.ch = (chv == 1 || chv == 2) ? chv : 4;
+      }
+      uni.layout = kinds_are({3, 0, 1, 0, 2, 0, 3}) ? 1
+                   : kinds_are({0, 1, 0, 2, 0})     ? 2
+                   : kinds_are({3, 1, 0, 2, 3})     ? 3
+                                                    : 0;
       uni.halo = ok ? halo : 0;
       if (!ok) {
         uni = RpUni{};
@@ -3046,8 +3093,9 @@ __global__ void k_rp_dinv_check(const uint8_t* __restrict__ pid, const double* _
 
 static int32_t rowpat_parts(const mlamg_csr* A) {
   const int64_t n_pairs = (A->n_rows + 1) / 2,
-                per = (A->rp_win.rows >= 0 && A->rp_slot) ? (int64_t)kRpWinNT
-                                                           : (int64_t)kRpChunks * kThreads;
+                per = (A->rp_uni.k > 0 && A->rp_msk) ? (int64_t)A->rp_uni.ch * kThreads
+                      : (A->rp_win.rows >= 0 && A->rp_slot) ? (int64_t)kRpWinNT
+                                                             : (int64_t)kRpChunks * kThreads;
   return (int32_t)std::max<int64_t>(1, (n_pairs + per - 1) / per);
 }
 

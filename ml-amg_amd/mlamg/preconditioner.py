@@ -153,11 +153,12 @@ class MultilevelPC(MLAMG):
     else None)`: zero initial guess and a tolerance relative to ||b|| (pyamg's solve scales tol
     by ||b||, and its default maxiter is 100).
       * with GMRES (the default, :54): device GMRES preconditioned by one V-cycle
-        (Hierarchy.gmres), with pyamg's iteration budget: pyamg.krylov.gmres called without a
-        restart value runs ONE outer cycle of at most maxiter = 100 inner steps (each one
-        V-cycle), so this is one cycle of restart min(100, n). Stop test ||b - A x|| <= amg_rtol
-        ||b|| on the true residual; pyamg's Householder GMRES tests the preconditioned one
-        (parity unpinned: pyamg absent);
+        (Hierarchy.gmres), with pyamg's iteration budget and stop test: pyamg.krylov.gmres
+        called without a restart value runs ONE outer cycle of at most maxiter = 100 inner steps
+        (each one V-cycle) and stops when the preconditioned residual ||M r|| <= tol ||M b||;
+        this is one cycle of restart min(100, n) whose inner stop (scipy's first-cycle ptol =
+        tol ||M b||) is that same test. The true residual lands near tol ||b|| (pyamg's
+        Householder orthogonalisation vs MGS here: parity unpinned, pyamg absent);
       * without: stationary V-cycles from x = 0 until ||b - A x|| <= amg_rtol ||b||, at most 100.
     """
 

@@ -71,7 +71,7 @@ def main():
                 "resid+norm": lambda: call("mlamg_residual", M.handle, ptr(b), ptr(x), ptr(r),
                                            ptr(nrm), s),
                 "jacobi(xin=x)": lambda: call("mlamg_jacobi", M.handle, ptr(d), ptr(b), ptr(xj),
-                                              ptr(xt), 2.0 / 3.0, 1, s),
+                                              ptr(xt), 1, s),
             }
             res = {}
             for op, fn in ops.items():
