@@ -1351,18 +1351,15 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
     const int lane = tid & 63;
     const double* sv = stg;
     const double* sd = sv + (int64_t)(cap + 1) * KM;
-    const double* sy = sd + (cap + 1);  // mk_recip(diagonal), computed by the staging
-    const double* sb = sy + (cap + 1);
+    const double* sb = sd + (cap + 1);
     const int32_t* sc = reinterpret_cast<const int32_t*>(sb + (cap + 1));
     const int32_t* sr = sc + (int64_t)(cap + 1) * KM;
     const int32_t* slp = sr + (cap + 1);
     int c[RW][KM], row[RW];
-    double v[RW][KM], d[RW], bv[RW], y[RW];
-    // a level's rows: slots [a, z) of the staging area (the level starts come one level ahead,
-    // so the next level's loads wait on no LDS read of this one); y = RN(1 / diagonal), staged
-    // with the row, keeps the division's dependent part to three operations (mk_div)
-    auto load_level = [&](int a, int z, int (&cc)[RW][KM], double (&vv)[RW][KM], double* dd,
-                          double* bb, int* rr, double* yy) {
+    double v[RW][KM], d[RW], bv[RW];
+    auto load_level = [&](int l, int (&cc)[RW][KM], double (&vv)[RW][KM], double* dd,
+                          double* bb, int* rr) {
+      const int a = slp[l], z = slp[l + 1];
 #pragma unroll
       for (int u = 0; u < RW; ++u) {
         const int p = a + lane + 64 * u < z ? a + lane + 64 * u : cnt;
@@ -1383,12 +1380,9 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
         dd[u] = sd[p];
         bb[u] = sb[p];
         rr[u] = sr[p];
-        yy[u] = sy[p];
       }
     };
-    auto lstart = [&](int l) { return slp[l < nl ? l : nl]; };
-    load_level(lstart(0), lstart(1), c, v, d, bv, row, y);
-    int a1 = lstart(1), z1 = lstart(2);
+    load_level(0, c, v, d, bv, row);
     #pragma unroll 1
     for (int l = 0; l < nl; ++l) {
       double g[RW][KM];
@@ -1397,35 +1391,29 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
 #pragma unroll
         for (int k = 0; k < KM; ++k) g[u][k] = xs[c[u][k]];
       int c2[RW][KM], row2[RW];
-      double v2[RW][KM], d2[RW], bv2[RW], y2[RW];
-      const int z2 = lstart(l + 3);  // the level after next's end, for the next iteration
-      if (l + 1 < nl) load_level(a1, z1, c2, v2, d2, bv2, row2, y2);
+      double v2[RW][KM], d2[RW], bv2[RW];
+      load_level(l + 1 < nl ? l + 1 : l, c2, v2, d2, bv2, row2);
 #pragma unroll
       for (int u = 0; u < RW; ++u) {
-        double t = 0.0;
+        double y = 0.0;
 #pragma unroll
-        for (int k = 0; k < KM; ++k) t += v[u][k] * g[u][k];
-        xs[row[u]] = mk_div(bv[u] - t, d[u], y[u]);
+        for (int k = 0; k < KM; ++k) y += v[u][k] * g[u][k];
+        xs[row[u]] = (bv[u] - y) / d[u];
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (l + 1 < nl) {
 #pragma unroll
-        for (int u = 0; u < RW; ++u) {
+      for (int u = 0; u < RW; ++u) {
 #pragma unroll
-          for (int k = 0; k < KM; ++k) {
-            c[u][k] = c2[u][k];
-            v[u][k] = v2[u][k];
-          }
-          d[u] = d2[u];
-          bv[u] = bv2[u];
-          row[u] = row2[u];
-          y[u] = y2[u];
+        for (int k = 0; k < KM; ++k) {
+          c[u][k] = c2[u][k];
+          v[u][k] = v2[u][k];
         }
+        d[u] = d2[u];
+        bv[u] = bv2[u];
+        row[u] = row2[u];
       }
-      a1 = z1;
-      z1 = z2;
     }
   };
 
@@ -1437,11 +1425,10 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
       // chunk ch + 1 into the other, so a chunk's global round trip hides behind the previous
       // sweep (when the LDS left holds two buffers of >= 3 levels; else one buffer, restaged
       // by the whole workgroup between chunks)
-      const int64_t buf_doubles = (((int64_t)(cap + 1) * (3 * K + 8) + 1) / 2 + 1) & ~int64_t(1);
+      const int64_t buf_doubles = (((int64_t)(cap + 1) * (3 * K + 6) + 1) / 2 + 1) & ~int64_t(1);
       auto stage_chunk = [&](int ch, double* wv, int t0, int nt) {
         double* wd = wv + (int64_t)(cap + 1) * K;
-        double* wy = wd + (cap + 1);
-        double* wb = wy + (cap + 1);
+        double* wb = wd + (cap + 1);
         int32_t* wc = reinterpret_cast<int32_t*>(wb + (cap + 1));
         int32_t* wr = wc + (int64_t)(cap + 1) * K;
         int32_t* wl = wr + (cap + 1);
@@ -1452,9 +1439,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
           wv[q] = pkv[(int64_t)P0 * K + q];
         }
         for (int q = t0; q < cnt; q += nt) {
-          const double dg = pkd[P0 + q];
-          wd[q] = dg;
-          wy[q] = mk_recip(dg);
+          wd[q] = pkd[P0 + q];
           wb[q] = bl[P0 + q];
           wr[q] = pkr[P0 + q];
         }
@@ -1464,7 +1449,6 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
         }
         if (t0 == 0) {
           wd[cnt] = 1.0;
-          wy[cnt] = 1.0;
           wb[cnt] = 0.0;
           wr[cnt] = n + 1;
         }
@@ -1476,7 +1460,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
       // ch + 1 into registers while wave 0 sweeps ch, and write it into the buffer after the
       // sweep's barrier, so only an LDS copy separates two sweeps
       int rg_c[2] = {0, 0}, rg_r = 0, rg_l = 0;
-      double rg_v[2] = {0.0, 0.0}, rg_d = 0.0, rg_y = 0.0, rg_b = 0.0;
+      double rg_v[2] = {0.0, 0.0}, rg_d = 0.0, rg_b = 0.0;
       // half-steps h = 2 ch - 1 (staging of chunk 0), 2 ch (wave 0 sweeps ch; with db, waves
       // 1-15 stage ch + 1 meanwhile; with rp they load it), 2 ch + 1 (without db: waves 1-15
       // stage ch + 1, with rp from their registers)
@@ -1513,7 +1497,6 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
             }
             if (t0 < cnt) {
               rg_d = pkd[P0 + t0];
-              rg_y = mk_recip(rg_d);
               rg_b = bl[P0 + t0];
               rg_r = pkr[P0 + t0];
             }
@@ -1521,8 +1504,7 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
           } else {  // registers -> the buffer (the sweep of ch is done)
             double* wv = stage;
             double* wd = wv + (int64_t)(cap + 1) * K;
-            double* wy = wd + (cap + 1);
-            double* wb = wy + (cap + 1);
+            double* wb = wd + (cap + 1);
             int32_t* wc = reinterpret_cast<int32_t*>(wb + (cap + 1));
             int32_t* wr = wc + (int64_t)(cap + 1) * K;
             int32_t* wl = wr + (cap + 1);
@@ -1536,7 +1518,6 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
             }
             if (t0 < cnt) {
               wd[t0] = rg_d;
-              wy[t0] = rg_y;
               wb[t0] = rg_b;
               wr[t0] = rg_r;
             }
@@ -1547,7 +1528,6 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
             }
             if (t0 == 0) {
               wd[cnt] = 1.0;
-              wy[cnt] = 1.0;
               wb[cnt] = 0.0;
               wr[cnt] = n + 1;
             }
@@ -2218,11 +2198,11 @@ std::shared_ptr<Shape> analyse_shape(const mlamg_amg2v_problem& P,
     const int km = maxoff <= 4 ? 4 : maxoff <= 8 ? 8 : 0;
     if (km == 4 && wmax <= 128) gs_rw = wmax <= 64 ? 1 : 2;
     if (km == 8 && wmax <= 64) gs_rw = 1;
-    if (gs_rw && (int)std::min<size_t>(4096, room / (12 * km + 32)) - 1 < wmax) gs_rw = 0;
+    if (gs_rw && (int)std::min<size_t>(4096, room / (12 * km + 24)) - 1 < wmax) gs_rw = 0;
     // two staging buffers when each still holds >= 3 of the widest levels
     static const bool no_db = std::getenv("MLAMG_BATCH_NO_DB") != nullptr;  // A/B knob
     if (gs_rw && !no_db &&
-        (int)std::min<size_t>(4096, room / (2 * (12 * km + 32) + 16)) - 1 >= 3 * wmax)
+        (int)std::min<size_t>(4096, room / (2 * (12 * km + 24) + 16)) - 1 >= 3 * wmax)
       L.gs_db = 1;
     L.K = gs_rw ? km : std::max(maxoff, 1);
     const int64_t K = L.K;
@@ -2262,7 +2242,7 @@ std::shared_ptr<Shape> analyse_shape(const mlamg_amg2v_problem& P,
   // after the cycle vectors, one position kept for the one-wave sweep's dummy (a level wider
   // than cap is swept by the workgroup straight from the arena)
   if (smoother == 0) {
-    const size_t per_pos = (12 * (size_t)L.K + 32) * (L.gs_db ? 2 : 1);
+    const size_t per_pos = (12 * (size_t)L.K + 24) * (L.gs_db ? 2 : 1);
     const size_t slack = L.gs_db ? 32 : 0;
     L.cap = (int)std::min<size_t>(4096, (room > slack ? room - slack : 0) / per_pos) - 1;
     L.clev.push_back(0);
@@ -2282,7 +2262,7 @@ std::shared_ptr<Shape> analyse_shape(const mlamg_amg2v_problem& P,
       L.cap * L.K <= 2 * (kBT - 64))
     L.gs_rp = 1;
   L.lds_base = gj_lds(pb, nc);
-  L.lds_cycles = vec_lds + 16 + (size_t)(L.cap + 1) * (12 * L.K + 32) * (L.gs_db ? 2 : 1) + 40;
+  L.lds_cycles = vec_lds + 16 + (size_t)(L.cap + 1) * (12 * L.K + 24) * (L.gs_db ? 2 : 1) + 40;
   L.gs_rw = gs_rw;
   return Sp;
 }

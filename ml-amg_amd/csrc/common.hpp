@@ -220,32 +220,6 @@ struct mlamg_dense {
 };
 
 namespace mlamg {
-// Correctly rounded a / b off a dependency chain's critical path. Gauss-Seidel's x_i =
-// (b_i - rsum) / a_ii sits on the sweep's level-to-level chain, and the IEEE division is ~11
-// dependent operations (div_scale, rcp, 4 refinement fmas, mul, fma, div_fmas, div_fixup). The
-// reciprocal y = RN(1 / a_ii) does not depend on the chain, so it is computed when the row's
-// data is loaded (mk_recip), and the chain keeps 3 operations (mk_div): q = RN(a y), the exact
-// remainder r = a - b q (one fma), q' = RN(q + r y). Markstein's theorem: with y the correctly
-// rounded reciprocal and q within one ulp of a / b, q' = RN(a / b) — the IEEE quotient — barring
-// overflow and underflow, which are excluded by range checks on |b| (at recip time), |a| and |q|;
-// outside them, and for a = 0 (the sign of a zero quotient), the plain division is taken.
-// Checked against the IEEE division on 2e8 random operand pairs and the special values
-// (tests/test_markstein.py, oracle/markstein_check.c): no mismatch.
-__device__ __forceinline__ double mk_recip(double b) {
-  const double ab = __builtin_fabs(b);
-  return (ab >= 0x1p-1000 && ab <= 0x1p1000) ? 1.0 / b : __builtin_nan("");
-}
-__device__ __forceinline__ double mk_div(double a, double b, double y) {
-  const double q = a * y;
-  const double r = __builtin_fma(-b, q, a);
-  const double aq = __builtin_fabs(q), aa = __builtin_fabs(a);
-  if (aq >= 0x1p-960 && aq <= 0x1p960 && aa >= 0x1p-960 && aa <= 0x1p960)
-    return __builtin_fma(r, y, q);
-  return a / b;
-}
-}  // namespace mlamg
-
-namespace mlamg {
 // s = p[start] + p[start+step] + ... in that order (bitwise a plain strided loop), with the loads
 // issued 8 at a time: a one-workgroup reduction over tens of thousands of partials is otherwise
 // a chain of dependent memory round trips.

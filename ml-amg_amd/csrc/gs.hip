@@ -232,12 +232,12 @@ constexpr int kGsWinBlock = 512;
 constexpr int kGsWinStageU = 4;  // positions per staging thread with all loads in flight
 
 // one staging buffer of cap + 1 positions (the last: the dummy of lanes past a level's end),
-// 16-byte aligned sections: vals (cap+1) x KM | diag | mk_recip(diag) | b (doubles) | level starts
+// 16-byte aligned sections: vals (cap+1) x KM | diag | b (doubles) | level starts
 // (cap + 2 int32) | columns (cap+1) x KM (uint16 ring slots), after a 16-byte header (levels,
 // first position, positions)
 __host__ __device__ constexpr int64_t win_a16(int64_t b) { return (b + 15) & ~int64_t(15); }
 __host__ __device__ constexpr int64_t win_buf_bytes(int64_t cap, int KM) {
-  return 16 + win_a16(8 * (cap + 1) * KM) + 3 * win_a16(8 * (cap + 1)) + win_a16(4 * (cap + 2)) +
+  return 16 + win_a16(8 * (cap + 1) * KM) + 2 * win_a16(8 * (cap + 1)) + win_a16(4 * (cap + 2)) +
          win_a16(2 * (cap + 1) * KM);
 }
 
@@ -245,7 +245,6 @@ template <int KM>
 struct WinBuf {
   double* v;
   double* d;
-  double* y;  // RN(1 / diag) (mk_recip): the sweep's division keeps 3 dependent operations
   double* b;
   int32_t* l;
   uint16_t* c;
@@ -256,8 +255,6 @@ struct WinBuf {
     v = reinterpret_cast<double*>(p);
     p += win_a16(8 * (int64_t)(cap + 1) * KM);
     d = reinterpret_cast<double*>(p);
-    p += win_a16(8 * (int64_t)(cap + 1));
-    y = reinterpret_cast<double*>(p);
     p += win_a16(8 * (int64_t)(cap + 1));
     b = reinterpret_cast<double*>(p);
     p += win_a16(8 * (int64_t)(cap + 1));
@@ -356,7 +353,6 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int4* __restrict__
             *reinterpret_cast<double2*>(w.v + (int64_t)q * KM + k) = v2;
           }
           w.d[q] = dummy ? 0.0 : d[u];
-          w.y[q] = dummy ? 0.0 : mk_recip(d[u]);
           w.b[q] = dummy ? 0.0 : bv[u];
         }
         if (q < xcnt) ring[(X0 + q) & RM] = xo[u];
@@ -373,9 +369,9 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int4* __restrict__
         const WinBuf<KM> w(cur, cap);
         const int nl = w.h[0], P0 = w.h[1], cnt = w.h[2];
         int c[RW][KM], p[RW];
-        double v[RW][KM], d[RW], yr[RW], bv[RW];
-        auto load = [&](int l, int (&cc)[RW][KM], double (&vv)[RW][KM], double* dd, double* yq,
-                        double* bq, int* pq) {
+        double v[RW][KM], d[RW], bv[RW];
+        auto load = [&](int l, int (&cc)[RW][KM], double (&vv)[RW][KM], double* dd, double* bq,
+                        int* pq) {
           const int a = w.l[l], z = w.l[l + 1];
 #pragma unroll
           for (int u = 0; u < RW; ++u) {
@@ -392,12 +388,11 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int4* __restrict__
               vv[u][k + 1] = v2.y;
             }
             dd[u] = w.d[q];
-            yq[u] = w.y[q];
             bq[u] = w.b[q];
             pq[u] = q;
           }
         };
-        load(0, c, v, d, yr, bv, p);
+        load(0, c, v, d, bv, p);
         #pragma unroll 1
         for (int l = 0; l < nl; ++l) {
           double g[RW][KM];
@@ -406,8 +401,8 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int4* __restrict__
 #pragma unroll
             for (int k = 0; k < KM; ++k) g[u][k] = ring[c[u][k]];
           int c2[RW][KM], p2[RW];
-          double v2[RW][KM], d2[RW], y2[RW], bv2[RW];
-          load(l + 1 < nl ? l + 1 : l, c2, v2, d2, y2, bv2, p2);
+          double v2[RW][KM], d2[RW], bv2[RW];
+          load(l + 1 < nl ? l + 1 : l, c2, v2, d2, bv2, p2);
           // the RW rows' sums and divisions first, as one block (their dependency chains
           // interleave), then the stores
           double xi[RW];
@@ -416,7 +411,7 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int4* __restrict__
             double y = 0.0;
 #pragma unroll
             for (int k = 0; k < KM; ++k) y += v[u][k] * g[u][k];
-            xi[u] = mk_div(bv[u] - y, d[u], yr[u]);
+            xi[u] = (bv[u] - y) / d[u];
           }
 #pragma unroll
           for (int u = 0; u < RW; ++u)  // zero diagonal (and the dummy): left alone
@@ -451,7 +446,6 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int4* __restrict__
               v[u][k] = v2[u][k];
             }
             d[u] = d2[u];
-            yr[u] = y2[u];
             bv[u] = bv2[u];
             p[u] = p2[u];
           }

@@ -12,3 +12,7 @@ T=$(find gpurun_out/prof_c2 -name "*kernel_trace.csv" | head -1)
 python3 tools/cycle_trace.py "$T" 15 > gpurun_out/r04/cycle_trace_c2.txt 2>&1
 rm -rf gpurun_out/prof_c2
 tail -2 gpurun_out/r04/cycle_trace_c2.txt
+# the multi-GPU compute floor (timing-only communicator) on this tree, world 1/2/4/8, with the
+# default and a deeper partition
+timeout -k 10 600 python3 tools/dist_rank_timing.py --worlds 1,2,4,8 --steps 40 --min-rows 50000,5000 > gpurun_out/r04/dist_rank_timing.log 2>&1 || { echo "dist timing failed rc=$?"; tail -5 gpurun_out/r04/dist_rank_timing.log; exit 1; }
+tail -3 gpurun_out/r04/dist_rank_timing.log

@@ -22,7 +22,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out", "pmc")
 KERNELS = {"csr_stream": "k_csr_stream", "sell": "k_sell<", "sorted": "k_sorted",
-           "sell_dict": "k_sell_dict", "rowpat": "k_rowpair"}
+           "sell_dict": "k_sell_dict", "rowpat": "k_rowpa"}
 
 
 def run_pass(counter, fmt):
