@@ -144,29 +144,46 @@ _FLUSH = None
 
 
 def time_kernel_cold(fn, reps=20):
-    """Device time of fn() (one kernel launch on torch's current stream) from a cold cache: each
-    launch follows a read of a 512 MB buffer (twice the 256 MB MALL, so no operand survives in
-    any cache level — what the autotune does before its timings, mlamg/hierarchy.py) and is
-    bracketed by its own pair of HIP events on that stream. Returns (mean, median, list) in s;
-    the mean is what rocprofv3's kernel trace averages over the same launches
-    (tools/rocprof_roofline.py)."""
+    """Device time of fn() (one SpMV-family kernel launch on torch's current stream) from a cold
+    cache: each launch follows a read of a 512 MB buffer (twice the 256 MB MALL, so no operand
+    survives in any cache level — what the autotune does before its timings,
+    mlamg/hierarchy.py). The kernel is timed by the events of its own dispatch packet
+    (mlamg_timer_*, hipExtLaunchKernel): its execution alone, which is what rocprofv3's kernel
+    trace reports for the same launches (tools/rocprof_roofline.py). A second round brackets each
+    call with a pair of stream events instead (event packet + dispatch + kernel), reported beside
+    it. Returns (mean, median, stream-event mean) in s."""
+    import ctypes
+    from mlamg._lib import call
     global _FLUSH
     if _FLUSH is None:
         _FLUSH = torch.ones(64 << 20, dtype=torch.float64, device="cuda")
     s = torch.cuda.current_stream()
     fn()
     torch.cuda.synchronize()
+    sink = torch.empty((), dtype=torch.float64, device="cuda")
+    tm = ctypes.c_void_p()
+    call("mlamg_timer_create", ctypes.byref(tm))
+    ts = []
+    try:
+        ms = ctypes.c_float()
+        for _ in range(reps):
+            torch.sum(_FLUSH, dim=0, out=sink)
+            call("mlamg_timer_arm", tm)
+            fn()
+            call("mlamg_timer_elapsed_ms", tm, ctypes.byref(ms))
+            ts.append(ms.value / 1000.0)
+    finally:
+        call("mlamg_timer_destroy", tm)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(reps)]
-    sink = torch.empty((), dtype=torch.float64, device="cuda")
     for e0, e1 in ev:
         torch.sum(_FLUSH, dim=0, out=sink)
         e0.record(s)
         fn()
         e1.record(s)
     torch.cuda.synchronize()
-    ts = [e0.elapsed_time(e1) / 1000.0 for e0, e1 in ev]
-    return float(np.mean(ts)), float(np.median(ts)), ts
+    te = [e0.elapsed_time(e1) / 1000.0 for e0, e1 in ev]
+    return float(np.mean(ts)), float(np.median(ts)), float(np.mean(te))
 
 
 def load_traffic(name):
@@ -308,7 +325,7 @@ def main():
     xs = torch.randn(n, dtype=torch.float64, device="cuda")
     ys = torch.empty_like(xs)
     # cold launches (every operand from HBM), then back to back (x/y may stay in the MALL)
-    t_spmv, t_spmv_med, _ = time_kernel_cold(lambda: A0.matvec(xs, out=ys), reps=20)
+    t_spmv, t_spmv_med, t_spmv_ev = time_kernel_cold(lambda: A0.matvec(xs, out=ys), reps=20)
     t_warm = time_kernel(lambda: A0.matvec(xs, out=ys), reps=50)
     B = spmv_bytes(n, n, A0.nnz)          # SURVEY.md §8(d) CSR bytes (format independent)
     B_fmt = A0.format_bytes()             # bytes the chosen storage format actually streams
@@ -364,9 +381,10 @@ def main():
             "csr_algorithmic_bytes_per_launch": B,
             "csr_equivalent_GBps": round(B / t_spmv / 1e9, 1),
             "avg_launch_us": round(t_spmv * 1e6, 2),
-            "timing": "mean of 20 cold launches (a 512 MB read before each, HIP events around "
-                      "each launch on its stream)",
+            "timing": "mean of 20 cold launches (a 512 MB read before each), each timed by the "
+                      "events of its own dispatch packet (hipExtLaunchKernel)",
             "median_launch_us": round(t_spmv_med * 1e6, 2),
+            "stream_event_avg_launch_us": round(t_spmv_ev * 1e6, 2),
             "warm_avg_launch_us": round(t_warm * 1e6, 2),
             "warm_frac": round(B_fmt / t_warm / 1e9 / HBM_PEAK_GBPS, 4),
         },

@@ -52,6 +52,16 @@ const char* mlamg_last_error(void);
 int mlamg_set_device(int dev);
 int mlamg_get_device(int* dev);
 int mlamg_stream_sync(void* stream);
+/* Dispatch-packet kernel timing (no reference counterpart: bench.py's roofline measurement).
+ * Arm a timer on the calling thread; the next SpMV-family kernel launch (mlamg_spmv,
+ * mlamg_residual, the smoother sweeps and their fused epilogues) records the timer's events in
+ * its own dispatch packet and disarms it; elapsed_ms then waits for it and returns that kernel's
+ * execution time, as a profiler's kernel trace reports it. */
+typedef struct mlamg_timer mlamg_timer;
+int mlamg_timer_create(mlamg_timer** out);
+int mlamg_timer_destroy(mlamg_timer* t);
+int mlamg_timer_arm(mlamg_timer* t);
+int mlamg_timer_elapsed_ms(mlamg_timer* t, float* ms);
 
 /* ---------------------------------------------------------------- CSR handles
  * Replaces the scipy.sparse.csr_matrix objects the reference passes around

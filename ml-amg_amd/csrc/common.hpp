@@ -7,6 +7,7 @@
 // CPU path (ns/lib/multigrid.py:44,181,191; ns/preconditioner/MLAMG.py:145,191,194).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -197,6 +198,7 @@ struct mlamg_csr {
   std::vector<int32_t> rp_rep;         // representative pair of each pattern (host)
   mlamg::RpUni rp_uni;                 // uniform-stencil form (k_rowpat_uni; k == 0: none)
   uint16_t* rp_msk = nullptr;          // its per-pattern slot masks (row 2i | row 2i+1 << 8)
+  int32_t rp_lds_pad = 0;              // extra LDS bytes per workgroup (occupancy cap, A/B knob)
   // attached Jacobi weights (mlamg_csr_attach_dinv): an epilogue whose dinv pointer equals
   // rp_dinv_att reads the per-pattern values rp_dinv[2p], rp_dinv[2p+1] instead of memory
   const double* rp_dinv_att = nullptr;
@@ -264,6 +266,23 @@ void* scratch(size_t bytes, int slot);
 // arrays in, so graph caches compare it and re-capture after a change.
 uint64_t format_epoch();
 void bump_format_epoch();
+
+// Dispatch-packet kernel timing (mlamg_timer_*, runtime.cpp): while a timer is armed on this
+// thread, the next SpMV-family launch (MLAMG_LAUNCH) carries the timer's two events in its own
+// dispatch packet (hipExtLaunchKernel) and disarms it. Their interval is then the kernel's
+// execution alone — what rocprofv3's kernel trace reports — instead of event packet + dispatch
+// + kernel, which is what a pair of stream events around the call measures.
+struct LaunchTimer {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchTimer* take_armed_timer();
+#define MLAMG_LAUNCH(K, G, B, L, S, ...)                                             \
+  do {                                                                               \
+    if (::mlamg::LaunchTimer* lt_ = ::mlamg::take_armed_timer())                     \
+      hipExtLaunchKernelGGL(K, G, B, L, S, lt_->start, lt_->stop, 0, __VA_ARGS__);   \
+    else                                                                             \
+      hipLaunchKernelGGL(K, G, B, L, S, __VA_ARGS__);                                \
+  } while (0)
 
 // generic kernels shared across translation units
 int launch_spmv_plain(const mlamg_csr* A, const double* x, double* y, hipStream_t s);

@@ -421,6 +421,59 @@ int mlamg_csr_copy_device(const mlamg_csr* A, int32_t* indptr, int32_t* indices,
 
 }  // extern "C"
 
+struct mlamg_timer {
+  mlamg::LaunchTimer ev;
+  bool used = false;
+};
+
+namespace mlamg {
+static thread_local LaunchTimer* g_armed = nullptr;
+LaunchTimer* take_armed_timer() {
+  LaunchTimer* t = g_armed;
+  g_armed = nullptr;
+  return t;
+}
+}  // namespace mlamg
+
+extern "C" {
+int mlamg_timer_create(mlamg_timer** out) {
+  MLAMG_REQUIRE(out, "out is NULL");
+  auto* t = new mlamg_timer();
+  hipError_t e = hipEventCreate(&t->ev.start);
+  if (e == hipSuccess) e = hipEventCreate(&t->ev.stop);
+  if (e != hipSuccess) {
+    if (t->ev.start) (void)hipEventDestroy(t->ev.start);
+    delete t;
+    set_error(std::string("mlamg_timer_create: ") + hipGetErrorString(e));
+    return MLAMG_EHIP;
+  }
+  *out = t;
+  return MLAMG_OK;
+}
+int mlamg_timer_destroy(mlamg_timer* t) {
+  if (!t) return MLAMG_OK;
+  if (g_armed == &t->ev) g_armed = nullptr;
+  (void)hipEventDestroy(t->ev.start);
+  (void)hipEventDestroy(t->ev.stop);
+  delete t;
+  return MLAMG_OK;
+}
+int mlamg_timer_arm(mlamg_timer* t) {
+  MLAMG_REQUIRE(t, "t is NULL");
+  t->used = true;
+  g_armed = &t->ev;
+  return MLAMG_OK;
+}
+int mlamg_timer_elapsed_ms(mlamg_timer* t, float* ms) {
+  MLAMG_REQUIRE(t && ms, "t / ms is NULL");
+  MLAMG_REQUIRE(t->used && g_armed != &t->ev,
+                "the timer was not armed, or no SpMV-family launch has consumed it");
+  MLAMG_HIP(hipEventSynchronize(t->ev.stop));
+  MLAMG_HIP(hipEventElapsedTime(ms, t->ev.start, t->ev.stop));
+  return MLAMG_OK;
+}
+}  // extern "C"
+
 namespace mlamg {
 static std::atomic<uint64_t> g_format_epoch{0};
 uint64_t format_epoch() { return g_format_epoch.load(); }

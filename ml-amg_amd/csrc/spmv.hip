@@ -428,12 +428,18 @@ __device__ __forceinline__ void ld2(const double* p, int i, bool both, double& v
   }
 }
 
+#ifndef MLAMG_ST_NT
+#define MLAMG_ST_NT 0
+#endif
 __device__ __forceinline__ void st2(double* p, int i, bool both, double v0, double v1) {
   if (both && al16(p)) {
     dbl2 t;
     t.x = v0;
     t.y = v1;
-    *reinterpret_cast<dbl2*>(p + i) = t;
+    if constexpr (MLAMG_ST_NT)
+      __builtin_nontemporal_store(t, reinterpret_cast<dbl2*>(p + i));
+    else
+      *reinterpret_cast<dbl2*>(p + i) = t;
   } else {
     p[i] = v0;
     if (both) p[i + 1] = v1;
@@ -1131,10 +1137,10 @@ static int launch_vcan(const mlamg_csr* A, const double* x, const Epi& ep, hipSt
   constexpr int RPB = 8 / Q;
   const unsigned nb = (unsigned)std::max<int64_t>(1, (A->n_rows + RPB - 1) / RPB);
   if (A->vec_idx16)
-    hipLaunchKernelGGL((k_csr_vcan<Q, OP, NORM, uint16_t>), dim3(nb), dim3(512), 0, s, A->indptr,
+    MLAMG_LAUNCH((k_csr_vcan<Q, OP, NORM, uint16_t>), dim3(nb), dim3(512), 0, s, A->indptr,
                        A->vec_idx16, A->data, A->n_rows, x, ep);
   else
-    hipLaunchKernelGGL((k_csr_vcan<Q, OP, NORM, int32_t>), dim3(nb), dim3(512), 0, s, A->indptr,
+    MLAMG_LAUNCH((k_csr_vcan<Q, OP, NORM, int32_t>), dim3(nb), dim3(512), 0, s, A->indptr,
                        A->indices, A->data, A->n_rows, x, ep);
   MLAMG_HIP(hipGetLastError());
   return MLAMG_OK;
@@ -1322,10 +1328,10 @@ static void launch_vcan_wave_nt(const mlamg_csr* A, const IT* idx, const double*
                                 const Epi& ep, hipStream_t s, unsigned nb, size_t lds,
                                 int64_t rpb) {
   if (ep.cached)
-    hipLaunchKernelGGL((k_vcan_wave<OP, NORM, IT, XL, false>), dim3(nb), dim3(kVwThreads), lds, s,
+    MLAMG_LAUNCH((k_vcan_wave<OP, NORM, IT, XL, false>), dim3(nb), dim3(kVwThreads), lds, s,
                        A->indptr, idx, A->data, A->n_rows, A->n_cols, A->nnz, rpb, x, ep);
   else
-    hipLaunchKernelGGL((k_vcan_wave<OP, NORM, IT, XL, true>), dim3(nb), dim3(kVwThreads), lds, s,
+    MLAMG_LAUNCH((k_vcan_wave<OP, NORM, IT, XL, true>), dim3(nb), dim3(kVwThreads), lds, s,
                        A->indptr, idx, A->data, A->n_rows, A->n_cols, A->nnz, rpb, x, ep);
 }
 
@@ -1743,7 +1749,7 @@ static int launch_rowpair_ck(const mlamg_csr* A, const double* x, const Epi& ep,
   const int64_t n_pairs = (A->n_rows + 1) / 2;
   const unsigned nb = (unsigned)((n_pairs + CH * kThreads - 1) / (CH * kThreads));
   const size_t lds = (size_t)A->rp_n_ent * 32 + (size_t)A->rp_n_pat * 16 + 257 * 4;
-  hipLaunchKernelGGL((k_rowpair<OP, NORM, CH, K>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid,
+  MLAMG_LAUNCH((k_rowpair<OP, NORM, CH, K>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid,
                      A->rp_ptr, reinterpret_cast<const int4*>(A->rp_off),
                      reinterpret_cast<const dbl2*>(A->rp_val), A->rp_n_ent, A->n_rows,
                      A->n_cols, A->rp_dinv_att, reinterpret_cast<const dbl2*>(A->rp_dinv),
@@ -1767,9 +1773,9 @@ static int launch_rowpat_uni(const mlamg_csr* A, const double* x, const Epi& ep,
   const int64_t n_pairs = (A->n_rows + 1) / 2;
   const unsigned nb = (unsigned)((n_pairs + CH * kThreads - 1) / (CH * kThreads));
   const size_t lds = sizeof(dbl2) * (size_t)(CH * kThreads + A->rp_uni.halo + A->rp_n_pat) +
-                     sizeof(uint16_t) * 256;
+                     sizeof(uint16_t) * 256 + (size_t)A->rp_lds_pad;
 #define MLAMG_RPU(LYV)                                                                           \
-  hipLaunchKernelGGL((k_rowpat_uni<OP, NORM, CH, LYV>), dim3(nb), dim3(kThreads), lds, s,        \
+  MLAMG_LAUNCH((k_rowpat_uni<OP, NORM, CH, LYV>), dim3(nb), dim3(kThreads), lds, s,        \
                      A->rp_pid, A->rp_msk, A->rp_n_pat, A->n_rows, A->n_cols, A->rp_dinv_att,    \
                      reinterpret_cast<const dbl2*>(A->rp_dinv), A->rp_uni, x, ep)
   switch (A->rp_uni.layout) {
@@ -1797,7 +1803,7 @@ static int launch_rowpair(const mlamg_csr* A, const double* x, const Epi& ep, hi
     const unsigned nb = (unsigned)((n_pairs + kRpWinNT - 1) / kRpWinNT);
     const size_t lds = sizeof(double) * (size_t)A->rp_win.rows;
 #define MLAMG_RPW(KV)                                                                           \
-  hipLaunchKernelGGL((k_rowpair_win<OP, NORM, KV>), dim3(nb), dim3(kRpWinNT), lds, s,            \
+  MLAMG_LAUNCH((k_rowpair_win<OP, NORM, KV>), dim3(nb), dim3(kRpWinNT), lds, s,            \
                      A->rp_slot, A->rp_ptr, reinterpret_cast<const int4*>(A->rp_off),           \
                      reinterpret_cast<const dbl2*>(A->rp_val), A->n_rows, A->n_cols,            \
                      A->rp_dinv_att, reinterpret_cast<const dbl2*>(A->rp_dinv), A->rp_win, x,   \
@@ -1829,7 +1835,7 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep_in, hipStre
   if (A->vec_width) return launch_vec<OP, NORM>(A, x, ep, s);
   if (A->lg_tile) {
     if (A->lg_nt == 0) return MLAMG_OK;
-    hipLaunchKernelGGL((k_csr_long<OP, NORM>), dim3(A->lg_nt), dim3(kThreads), 0, s, A->indptr,
+    MLAMG_LAUNCH((k_csr_long<OP, NORM>), dim3(A->lg_nt), dim3(kThreads), 0, s, A->indptr,
                        A->indices, A->data, A->lg_tile, x, ep);
     MLAMG_HIP(hipGetLastError());
     return MLAMG_OK;
@@ -1842,7 +1848,7 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep_in, hipStre
     if (A->srt_nb == 0) return MLAMG_OK;
     const bool lr = A->avg_row_len >= kSrtLongRow;
 #define MLAMG_SRT_LAUNCH(VDV, LRV)                                                              \
-  hipLaunchKernelGGL((k_sorted<OP, NORM, VDV, LRV>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s, \
+  MLAMG_LAUNCH((k_sorted<OP, NORM, VDV, LRV>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s, \
                      A->indptr, A->srt_pk, A->srt_val, A->srt_vi, A->srt_vtab, A->srt_blk,     \
                      A->srt_base, x, ep)
     if (A->srt_vi) {
@@ -1866,15 +1872,15 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep_in, hipStre
     const int64_t per_block = (kThreads / 64) * spw;
     const unsigned nb = (unsigned)((A->n_slices + per_block - 1) / per_block);
     if (spw == 1)
-      hipLaunchKernelGGL((k_sell_dict<OP, NORM, 1>), dim3(nb), dim3(kThreads), 0, s, A->dict_ptr,
+      MLAMG_LAUNCH((k_sell_dict<OP, NORM, 1>), dim3(nb), dim3(kThreads), 0, s, A->dict_ptr,
                          A->dict_code, A->dict_off, A->dict_val, A->sell_perm, A->n_rows,
                          A->n_slices, x, ep);
     else if (spw == 2)
-      hipLaunchKernelGGL((k_sell_dict<OP, NORM, 2>), dim3(nb), dim3(kThreads), 0, s, A->dict_ptr,
+      MLAMG_LAUNCH((k_sell_dict<OP, NORM, 2>), dim3(nb), dim3(kThreads), 0, s, A->dict_ptr,
                          A->dict_code, A->dict_off, A->dict_val, A->sell_perm, A->n_rows,
                          A->n_slices, x, ep);
     else
-      hipLaunchKernelGGL((k_sell_dict<OP, NORM, 4>), dim3(nb), dim3(kThreads), 0, s, A->dict_ptr,
+      MLAMG_LAUNCH((k_sell_dict<OP, NORM, 4>), dim3(nb), dim3(kThreads), 0, s, A->dict_ptr,
                          A->dict_code, A->dict_off, A->dict_val, A->sell_perm, A->n_rows,
                          A->n_slices, x, ep);
     MLAMG_HIP(hipGetLastError());
@@ -1883,13 +1889,13 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep_in, hipStre
   if (A->sell_ptr) {
     if (A->n_slices == 0) return MLAMG_OK;
     const unsigned nb = (unsigned)((A->n_slices + kThreads / 64 - 1) / (kThreads / 64));
-    hipLaunchKernelGGL((k_sell<OP, NORM>), dim3(nb), dim3(kThreads), 0, s, A->sell_ptr,
+    MLAMG_LAUNCH((k_sell<OP, NORM>), dim3(nb), dim3(kThreads), 0, s, A->sell_ptr,
                        A->sell_col, A->sell_val, A->sell_perm, A->n_rows, A->n_slices, x, ep);
     MLAMG_HIP(hipGetLastError());
     return MLAMG_OK;
   }
   if (A->n_blocks == 0) return MLAMG_OK;
-  hipLaunchKernelGGL((k_csr_stream<OP, NORM>), dim3(A->n_blocks), dim3(kThreads), 0, s,
+  MLAMG_LAUNCH((k_csr_stream<OP, NORM>), dim3(A->n_blocks), dim3(kThreads), 0, s,
                      A->indptr, A->indices, A->data, A->blk, x, ep);
   MLAMG_HIP(hipGetLastError());
   return MLAMG_OK;
@@ -2887,6 +2893,8 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
         const char* ec = std::getenv("MLAMG_RPU_CH");  // A/B knob
         const int chv = ec ? std::atoi(ec) : 4;
         uni.ch = (chv == 1 || chv == 2) ? chv : 4;
+        const char* ep = std::getenv("MLAMG_RPU_LDSPAD");  // A/B knob: caps workgroups per CU
+        A->rp_lds_pad = ep ? std::max(0, std::min(std::atoi(ep), 96 << 10)) : 0;
       }
       uni.layout = kinds_are({3, 0, 1, 0, 2, 0, 3}) ? 1
                    : kinds_are({0, 1, 0, 2, 0})     ? 2

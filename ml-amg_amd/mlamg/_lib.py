@@ -74,6 +74,10 @@ SIGNATURES = {
     "mlamg_set_device": (c_int, [c_int]),
     "mlamg_get_device": (c_int, [P_int]),
     "mlamg_stream_sync": (c_int, [c_vp]),
+    "mlamg_timer_create": (c_int, [c_vpp]),
+    "mlamg_timer_destroy": (c_int, [c_vp]),
+    "mlamg_timer_arm": (c_int, [c_vp]),
+    "mlamg_timer_elapsed_ms": (c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),
     "mlamg_csr_create": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vpp]),
     "mlamg_csr_destroy": (c_int, [c_vp]),
     "mlamg_csr_shape": (c_int, [c_vp, P_i64, P_i64, P_i64]),

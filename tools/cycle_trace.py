@@ -1,11 +1,12 @@
 """Per-kernel breakdown of the V-cycle from a rocprofv3 kernel trace (host-side analysis).
 
-  python tools/cycle_trace.py gpurun_out/prof/bench_kernel_trace.csv [n_cycles]
+  python tools/cycle_trace.py gpurun_out/prof/bench_kernel_trace.csv [n_cycles] [must_contain]
 
 Cycles are delimited by the end-of-cycle norm kernel (k_finalize_norm). Over the last n_cycles
 cycles (default 10) that launch the same kernel sequence as the last one, prints each
 position's median duration and median idle gap before it, then the median span and busy time
-(a single cycle's numbers scatter by a few microseconds per kernel).
+(a single cycle's numbers scatter by a few microseconds per kernel). must_contain: only cycles
+launching a kernel whose name contains it (bench.py also runs a variable-coefficient cycle).
 """
 import csv
 import statistics
@@ -22,6 +23,8 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     cyc = cycles(rows)
+    if len(sys.argv) > 3:
+        cyc = [c for c in cyc if any(sys.argv[3] in r["Kernel_Name"] for r in c)]
     names = [r["Kernel_Name"] for r in cyc[-1]]
     same = [c for c in cyc if [r["Kernel_Name"] for r in c] == names][-n:]
     durs, gaps, spans, busys = [], [], [], []

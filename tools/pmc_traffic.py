@@ -25,14 +25,14 @@ KERNELS = {"csr_stream": "k_csr_stream", "sell": "k_sell<", "sorted": "k_sorted"
            "sell_dict": "k_sell_dict", "rowpat": "k_rowpa"}
 
 
-def run_pass(counter, fmt):
-    d = os.path.join(OUT, f"{counter}_{fmt}")
+def run_pass(counter, fmt, tag=""):
+    d = os.path.join(OUT, f"{counter.replace(' ', '+')}_{fmt}{tag}")
     shutil.rmtree(d, ignore_errors=True)
     os.makedirs(d, exist_ok=True)
-    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
+    cmd = ["rocprofv3", "--pmc", *counter.split(), "--output-format", "csv", "-d", d, "-o", "run", "--",
            sys.executable, os.path.join(ROOT, "tools", "spmv_driver.py")]
     env = dict(os.environ, MLAMG_FMT=fmt)
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     if r.returncode != 0:
         raise RuntimeError(f"rocprofv3 failed:\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}")
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
@@ -44,6 +44,9 @@ def run_pass(counter, fmt):
             for row in csv.DictReader(fh):
                 if KERNELS[fmt] in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
+                elif (" " in counter and KERNELS[fmt] in row.get("Kernel_Name", "")
+                      and row.get("Counter_Name") in counter.split()):
+                    vals.append((row["Counter_Name"], float(row["Counter_Value"])))
     drv = [ln for ln in r.stdout.splitlines() if ln.startswith("spmv_driver:")]
     return vals, files, (drv[-1] if drv else "")
 
@@ -51,8 +54,18 @@ def run_pass(counter, fmt):
 def main():
     round_tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     fmt = sys.argv[2] if len(sys.argv) > 2 else "sell"
-    fetch, f1, drv = run_pass("FETCH_SIZE", fmt)
-    write, f2, _ = run_pass("WRITE_SIZE", fmt)
+    # PMC_TAG names a variant run (e.g. MLAMG_RP_UNI=0 in the environment: the general row-pair
+    # kernel); PMC_L2=1 adds a third pass with the L2 hit / miss counts
+    tag = os.environ.get("PMC_TAG", "")
+    fetch, f1, drv = run_pass("FETCH_SIZE", fmt, tag)
+    write, f2, _ = run_pass("WRITE_SIZE", fmt, tag)
+    l2 = {}
+    if os.environ.get("PMC_L2") == "1":
+        v, _, _ = run_pass("TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum", fmt, tag)
+        for name in ("TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_sum"):
+            xs = sorted(x for nm, x in v if nm == name)
+            if xs:
+                l2[name + "_median"] = xs[len(xs) // 2]
     if not fetch or not write:
         raise RuntimeError("no dispatches of the SpMV kernel found in the counter CSVs")
     # skip the first (cold) dispatch
@@ -80,11 +93,12 @@ def main():
         "driver": drv,
         "traffic_over_algorithmic": (read_bytes + write_bytes) / algo,
         "dispatches": len(fetch),
+        **l2,
     }
-    with open(os.path.join(OUT, f"spmv_c4_pmc_{fmt}.json"), "w") as fh:
+    with open(os.path.join(OUT, f"spmv_c4_pmc_{fmt}{tag}.json"), "w") as fh:
         json.dump(res, fh, indent=1)
-    for f, tag in ((f1[0], "FETCH_SIZE"), (f2[0], "WRITE_SIZE")):
-        shutil.copy(f, os.path.join(OUT, f"spmv_c4_pmc_{fmt}_{tag}_{round_tag}.csv"))
+    for f, ctr in ((f1[0], "FETCH_SIZE"), (f2[0], "WRITE_SIZE")):
+        shutil.copy(f, os.path.join(OUT, f"spmv_c4_pmc_{fmt}{tag}_{ctr}_{round_tag}.csv"))
     print(json.dumps(res, indent=1))
 
 

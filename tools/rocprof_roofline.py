@@ -4,7 +4,7 @@ HIP-event figure (host-side analysis).
   python tools/rocprof_roofline.py <kernel_trace.csv> <bench.json line file> [out_stats.csv]
 
 bench.py times the fine-level SpMV cold: 20 launches, each right after a 512 MB torch.sum (the
-cache flush). Those launches are found in the trace as the kernels that start right after a
+cache flush) and timed by its own dispatch packet's events, then 20 more between stream events. Those launches are found in the trace as the kernels that start right after a
 torch reduce kernel and whose name is the roofline kernel's (the first one launched after a
 flush); their mean duration is what bench.py's avg_launch_us measures. Writes a rocprofv3-style
 stats row for exactly those launches and prints the agreement.
@@ -25,9 +25,18 @@ def main():
         if "reduce_kernel" in a["Kernel_Name"] and "mlamg::" in b["Kernel_Name"]:
             picked.append(b)
     names = {r["Kernel_Name"] for r in picked}
-    # the roofline window is the last 20 flush-preceded launches (the autotune flushes too)
-    name = picked[-1]["Kernel_Name"]
-    same = [r for r in picked if r["Kernel_Name"] == name][-20:]
+    # the roofline window: the last 20 flush-preceded launches of the fine level's plain SpMV
+    # (y = A x: epilogue 0, no norm) in the bench's format — the autotune flushes before its
+    # timings too, earlier, and the variable-coefficient line after it uses other formats
+    fam = {"rowpat": ("k_rowpat_uni<0, false", "k_rowpair<0, false"), "sell": ("k_sell<0, false",),
+           "sell_dict": ("k_sell_dict<0, false",), "sorted": ("k_sorted<0, false",),
+           "csr_stream": ("k_csr_stream<0, false",)}
+    fmt = bench["kernel"].split("(")[1].split()[0]
+    keys = fam.get(fmt, ("<0, false",))
+    cand = [r for r in picked if any(k in r["Kernel_Name"] for k in keys)]
+    name = cand[-1]["Kernel_Name"]
+    # bench.py times 20 launches by their dispatch packets, then 20 between stream events
+    same = [r for r in cand if r["Kernel_Name"] == name][-40:-20]
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in same]
     mean_us = statistics.mean(d) / 1e3
     med_us = statistics.median(d) / 1e3
