@@ -199,6 +199,10 @@ struct mlamg_csr {
   mlamg::RpUni rp_uni;                 // uniform-stencil form (k_rowpat_uni; k == 0: none)
   uint16_t* rp_msk = nullptr;          // its per-pattern slot masks (row 2i | row 2i+1 << 8)
   int32_t rp_lds_pad = 0;              // extra LDS bytes per workgroup (occupancy cap, A/B knob)
+  // plane-marching form of a uniform 3-D 7-point stencil (k_rowpat_march; rp_mF == 0: none):
+  // far offset +-rp_mF (one grid plane), chunks per tile, planes per z segment
+  int64_t rp_mF = 0;
+  int32_t rp_mch = 4, rp_mseg = 0;
   // attached Jacobi weights (mlamg_csr_attach_dinv): an epilogue whose dinv pointer equals
   // rp_dinv_att reads the per-pattern values rp_dinv[2p], rp_dinv[2p+1] instead of memory
   const double* rp_dinv_att = nullptr;

@@ -689,6 +689,9 @@ __device__ __forceinline__ int uni_k(const RpUni& U) {
   return LY == 1 ? 7 : (LY == 2 || LY == 3) ? 5 : U.k;
 }
 
+#ifndef MLAMG_UNI_DBG
+#define MLAMG_UNI_DBG 0  // timing-only builds (tools/build_variant.sh): 1 no masks, 2 no id
+#endif                   // loads, 4 no far loads, 8 no stores — results are then wrong
 template <int OP, bool NORM, int CH, int LY>
 __global__ __launch_bounds__(kThreads) void k_rowpat_uni(
     const uint8_t* __restrict__ pid, const uint16_t* __restrict__ pat_msk, int n_pat,
@@ -730,10 +733,11 @@ __global__ __launch_bounds__(kThreads) void k_rowpat_uni(
   constexpr int NF = LY == 1 || LY == 3 ? 2 : (LY == 2 ? 0 : kRpUniFar);
   constexpr int NFR = NF > 0 ? NF : 1;
   // chunk 0's id and far operands, then the window: all loads before the first LDS store
-  int pcur = pid[2 * pa < n_rows ? pa : 0];
+  int pcur = (MLAMG_UNI_DBG & 2) ? 13 : pid[2 * pa < n_rows ? pa : 0];
   dbl2 fcur[NFR];
 #pragma unroll
-  for (int t = 0; t < NF; ++t) fcur[t] = x16(x, 2 * pa + fo[t], n_cols);
+  for (int t = 0; t < NF; ++t)
+    fcur[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0} : x16(x, 2 * pa + fo[t], n_cols);
   constexpr int WQ = CH + 2;  // window slots per thread (halo <= 256 pairs a side)
   dbl2 wv[WQ];
 #pragma unroll
@@ -761,10 +765,11 @@ __global__ __launch_bounds__(kThreads) void k_rowpat_uni(
     if (ok0) epi_load2<OP>(r, both, ep, u, w, tab_dinv, x_op);
     // the next chunk's id and far operands, in flight while this one sums
     const int64_t prn = pr + kThreads;
-    const int pnext = pid[c + 1 < CH && 2 * prn < n_rows ? prn : 0];
+    const int pnext = (MLAMG_UNI_DBG & 2) ? 13 : pid[c + 1 < CH && 2 * prn < n_rows ? prn : 0];
     dbl2 fnext[NFR];
 #pragma unroll
-    for (int t = 0; t < NF; ++t) fnext[t] = x16(x, 2 * prn + fo[t], n_cols);
+    for (int t = 0; t < NF; ++t)
+      fnext[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0} : x16(x, 2 * prn + fo[t], n_cols);
     const int pl = c * kThreads + (int)threadIdx.x + hw;  // this pair's window slot
     const dbl2 xc = win[pl];
     const dbl2 xl = win[pl - 1];
@@ -802,13 +807,17 @@ __global__ __launch_bounds__(kThreads) void k_rowpat_uni(
           t1 = f.y;
           ++tf;
         }
-        const double y0 = (m >> q) & 1 ? t0 : 0.0;
-        const double y1 = (m >> (q + 8)) & 1 ? t1 : 0.0;
+        const double y0 = (MLAMG_UNI_DBG & 1) || ((m >> q) & 1) ? t0 : 0.0;
+        const double y1 = (MLAMG_UNI_DBG & 1) || ((m >> (q + 8)) & 1) ? t1 : 0.0;
         s0 += U.v0[q] * y0;
         s1 += U.v1[q] * y1;
       }
     }
-    if (ok0) sq += epi_store2<OP>(r, both, s0, s1, u, w, ep);
+    if (MLAMG_UNI_DBG & 8) {
+      if (s0 == 1.2345 && s1 == 5.4321 && ok0) sq += epi_store2<OP>(r, both, s0, s1, u, w, ep);
+    } else if (ok0) {
+      sq += epi_store2<OP>(r, both, s0, s1, u, w, ep);
+    }
     pcur = pnext;
 #pragma unroll
     for (int t = 0; t < NF; ++t) fcur[t] = fnext[t];
@@ -822,6 +831,149 @@ __global__ __launch_bounds__(kThreads) void k_rowpat_uni(
       for (int i = 0; i < kThreads / 64; ++i) t += red[i];
       ep.partial[lb] = t;
     }
+  }
+}
+
+// ---------------------------------------------------------------- plane-marching stencil form
+// k_rowpat_march: k_rowpat_uni for the 3-D 7-point layout (slots -F -n -1 0 1 n F, F = one grid
+// plane of rows, even) with the far operands from LDS as well. A workgroup owns a tile of
+// T = 2 CH 256 consecutive rows of a plane (rows j T .. j T + T - 1 of every plane, the last
+// tile of a plane partial) and marches it through a segment of planes k0 .. k1 - 1 (2.5-D
+// blocking): a ring of three LDS windows holds x around the tile in planes k - 1, k, k + 1
+// (each T rows + the in-plane halo), so x[r -+ F] is the same slot of the neighbouring window
+// and each row of x comes from HBM about once (plus the halo, shared with the neighbouring
+// tiles that march beside it in the same XCD's L2, and two extra planes per segment), where
+// k_rowpat_uni loads every far operand again (C4 A_0: 1.4x the algorithmic bytes through the
+// fabric, rocprofv3 PMC). The window of plane k + 2 is loaded into registers while plane k is
+// summed (plain loads survive the barrier). Per row pair: the same pattern id, mask, values,
+// products and order as k_rowpat_uni — the same bits. No NORM form: the norm partials follow
+// the 2048-row blocks of the other row-pair kernels, which plane tiles do not align with.
+template <int OP, int CH>
+__global__ __launch_bounds__(kThreads) void k_rowpat_march(
+    const uint8_t* __restrict__ pid, const uint16_t* __restrict__ pat_msk, int n_pat,
+    int64_t n_rows, const double* __restrict__ dinv_att, const dbl2* __restrict__ pat_dinv,
+    RpUni U, const double* __restrict__ x, Epi ep, int64_t F, int nt, int seg,
+    int64_t n_planes) {
+  // LDS: ring[3][W] (dbl2) | dinv[n_pat] (dbl2) | mask[256] (uint16)
+  extern __shared__ dbl2 uni_lds[];
+  if (ep.done && *ep.done) return;
+  constexpr int T = 2 * CH * kThreads;  // rows per tile
+  const int hw = U.halo >> 1;           // halo in pairs
+  const int W = CH * kThreads + 2 * hw;  // window slots
+  dbl2* ring = uni_lds;
+  dbl2* dt = ring + 3 * W;
+  uint16_t* msk = reinterpret_cast<uint16_t*>(dt + n_pat);
+  const bool tab_dinv = ep.dinv != nullptr && ep.dinv == dinv_att;
+  bool x_op = false;
+  if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) x_op = ep.xin == x;
+  if constexpr (OP == EPI_RESID) x_op = ep.copy_to != nullptr && ep.copy_from == x;
+  const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const int j = (int)(lb % nt);
+  const int64_t k0 = (lb / nt) * seg;
+  const int64_t k1 = k0 + seg < n_planes ? k0 + seg : n_planes;
+  if (k0 >= k1) return;  // uniform per workgroup, before any barrier
+  const int64_t tile0 = (int64_t)j * T;
+  const int64_t lim = F - tile0;  // rows of the tile inside its plane (even)
+  constexpr int WQ = CH + 2;      // window slots per thread (halo <= 256 pairs a side)
+  dbl2 wv[WQ];
+  auto wload = [&](int64_t k) {
+    const int64_t w0 = k * F + tile0 - U.halo;
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+      const int i = threadIdx.x + q * kThreads;
+      wv[q] = x16(x, w0 + 2 * (int64_t)(i < W ? i : 0), n_rows);
+    }
+  };
+  auto wstore = [&](int slot) {
+    dbl2* w = ring + slot * W;
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+      const int i = threadIdx.x + q * kThreads;
+      if (i < W) w[i] = wv[q];
+    }
+  };
+  // prologue: planes k0 - 1 and k0 staged, k0 + 1 in flight
+  wload(k0 - 1);
+  wstore(0);
+  wload(k0);
+  wstore(1);
+  wload(k0 + 1);
+  for (int i = threadIdx.x; i < 256; i += kThreads) msk[i] = i < n_pat ? pat_msk[i] : 0;
+  if (tab_dinv)
+    for (int i = threadIdx.x; i < n_pat; i += kThreads) dt[i] = pat_dinv[i];
+  int sm = 0;  // ring slot of plane k - 1 (k, k + 1 follow cyclically)
+#pragma unroll 1
+  for (int64_t k = k0; k < k1; ++k) {
+    const int sc = sm == 2 ? 0 : sm + 1, sp = sc == 2 ? 0 : sc + 1;
+    wstore(sp);  // plane k + 1 (its slot held plane k - 2, last read before the previous barrier)
+    // this plane's pattern ids and epilogue operands, in flight across the barrier
+    const int64_t rb = k * F + tile0;
+    int pc[CH];
+    EpiIn u[CH], w[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int lp = 2 * (c * kThreads + (int)threadIdx.x);
+      const int64_t r = rb + lp;
+      const bool ok0 = lp < lim && r < n_rows;
+      pc[c] = ok0 ? pid[r >> 1] : 0;
+      if (ok0) epi_load2<OP>((int)r, r + 1 < n_rows, ep, u[c], w[c], tab_dinv, x_op);
+    }
+    __syncthreads();
+    if (k + 2 <= k1) wload(k + 2);  // the next plane's window, in flight while this one sums
+    const dbl2* wm = ring + sm * W;
+    const dbl2* wc = ring + sc * W;
+    const dbl2* wp = ring + sp * W;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int lp = 2 * (c * kThreads + (int)threadIdx.x);
+      const int64_t r = rb + lp;
+      if (!(lp < lim && r < n_rows)) continue;
+      const bool both = r + 1 < n_rows;
+      const int pl = c * kThreads + (int)threadIdx.x + hw;
+      const dbl2 xc = wc[pl];
+      const dbl2 xl = wc[pl - 1];
+      const dbl2 xr = wc[pl + 1];
+      const dbl2 fm = wm[pl];
+      const dbl2 fp = wp[pl];
+      const int m = msk[pc[c]];
+      if (tab_dinv) {
+        const dbl2 d = dt[pc[c]];
+        u[c].c = d.x;
+        w[c].c = d.y;
+      }
+      if (x_op) {
+        u[c].b = xc.x;
+        w[c].b = xc.y;
+      }
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int q = 0; q < 7; ++q) {
+        const int kd = uni_kind<1>(U, q);
+        double t0, t1;
+        if (kd == 0) {
+          const dbl2 v = wc[pl + (U.off[q] >> 1)];
+          t0 = v.x;
+          t1 = v.y;
+        } else if (kd == 1) {
+          t0 = xl.y;
+          t1 = xc.x;
+        } else if (kd == 2) {
+          t0 = xc.y;
+          t1 = xr.x;
+        } else {
+          const dbl2 f = q == 0 ? fm : fp;
+          t0 = f.x;
+          t1 = f.y;
+        }
+        const double y0 = (m >> q) & 1 ? t0 : 0.0;
+        const double y1 = (m >> (q + 8)) & 1 ? t1 : 0.0;
+        s0 += U.v0[q] * y0;
+        s1 += U.v1[q] * y1;
+      }
+      epi_store2<OP>((int)r, both, s0, s1, u[c], w[c], ep);
+    }
+    __syncthreads();  // plane k - 1's slot is refilled next
+    sm = sc;
   }
 }
 
@@ -1789,8 +1941,32 @@ static int launch_rowpat_uni(const mlamg_csr* A, const double* x, const Epi& ep,
   return MLAMG_OK;
 }
 
+template <int OP, int CH>
+static int launch_rowpat_march(const mlamg_csr* A, const double* x, const Epi& ep,
+                               hipStream_t s) {
+  constexpr int64_t T = 2 * CH * kThreads;
+  const int64_t F = A->rp_mF;
+  const int nt = (int)((F + T - 1) / T);
+  const int64_t n_planes = (A->n_rows + F - 1) / F;
+  const int seg = A->rp_mseg;
+  const unsigned nb = (unsigned)(nt * ((n_planes + seg - 1) / seg));
+  const size_t lds = sizeof(dbl2) * (size_t)(3 * (CH * kThreads + A->rp_uni.halo) + A->rp_n_pat) +
+                     sizeof(uint16_t) * 256;
+  MLAMG_LAUNCH((k_rowpat_march<OP, CH>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid, A->rp_msk,
+               A->rp_n_pat, A->n_rows, A->rp_dinv_att, reinterpret_cast<const dbl2*>(A->rp_dinv),
+               A->rp_uni, x, ep, F, nt, seg, n_planes);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
 template <int OP, bool NORM>
 static int launch_rowpair(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
+  if constexpr (!NORM) {
+    if (A->rp_mF > 0 && A->rp_msk)
+      return A->rp_mch == 1   ? launch_rowpat_march<OP, 1>(A, x, ep, s)
+             : A->rp_mch == 2 ? launch_rowpat_march<OP, 2>(A, x, ep, s)
+                              : launch_rowpat_march<OP, 4>(A, x, ep, s);
+  }
   if (A->rp_uni.k > 0 && A->rp_msk) {
     switch (A->rp_uni.ch) {
       case 1: return launch_rowpat_uni<OP, NORM, 1>(A, x, ep, s);
@@ -2666,6 +2842,7 @@ static void drop_rowpat(mlamg_csr* A) {
     if (p) (void)hipFree(p);
   A->rp_msk = nullptr;
   A->rp_uni = RpUni{};
+  A->rp_mF = 0;
   A->rp_slot = nullptr;
   A->rp_dinv = nullptr;
   A->rp_dinv_att = nullptr;
@@ -3073,6 +3250,28 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
   }
   drop_rowpat(A);
   A->rp_uni = uni;
+  // plane-marching form (k_rowpat_march): the 3-D 7-point layout with its far offsets one even
+  // plane of rows F apart. MLAMG_RPM=0 turns it off; MLAMG_RPM_CH (2 | 4) and MLAMG_RPM_SEG
+  // (planes per segment; 0 = enough workgroups for two (CH 4) / four (CH 2) per CU) are A/B knobs
+  if (uni.k == 7 && uni.layout == 1 && A->n_rows == A->n_cols && uni.off[6] > 0 &&
+      uni.off[0] == -uni.off[6] && (uni.off[6] & 1) == 0 && uni.off[6] >= 2048 &&
+      A->n_rows >= 3 * (int64_t)uni.off[6]) {
+    const char* e0 = std::getenv("MLAMG_RPM");
+    const char* e1 = std::getenv("MLAMG_RPM_CH");
+    const char* e2 = std::getenv("MLAMG_RPM_SEG");
+    if (!(e0 && std::atoi(e0) == 0)) {
+      const int64_t F = uni.off[6];
+      const int ch = e1 && (std::atoi(e1) == 1 || std::atoi(e1) == 2) ? std::atoi(e1) : 4;
+      const int64_t T = 2 * ch * kThreads;
+      const int64_t nt = (F + T - 1) / T, n_planes = (A->n_rows + F - 1) / F;
+      const int64_t target = 256 * (ch == 4 ? 2 : ch == 2 ? 4 : 6);
+      int64_t seg = e2 ? std::atoi(e2) : 0;
+      if (seg <= 0) seg = std::max<int64_t>(2, (n_planes * nt + target - 1) / target);
+      A->rp_mF = F;
+      A->rp_mch = ch;
+      A->rp_mseg = (int32_t)std::min<int64_t>(seg, n_planes);
+    }
+  }
   A->rp_msk = pmsk;
   A->rp_win = win;
   A->rp_slot = pslot;

@@ -672,6 +672,73 @@ def test_rowpat_window(ml, torch_cuda, monkeypatch, win):
         assert np.allclose(h1, h2, rtol=1e-14, atol=0)
 
 
+@pytest.mark.parametrize("rpm,ch,seg", [("1", "4", "0"), ("1", "4", "1"), ("1", "2", "0"),
+                                        ("1", "2", "3"), ("1", "4", "7"), ("1", "1", "0"), ("0", "4", "0")])
+def test_rowpat_march(ml, torch_cuda, monkeypatch, rpm, ch, seg):
+    """Plane-marching form of the uniform 3-D stencil kernel (k_rowpat_march, csrc/spmv.hip;
+    MLAMG_RPM=0: k_rowpat_uni): every non-norm epilogue bitwise scipy — y = A x, y = 2 A x -
+    y/2, the residual, Jacobi (xin == x, window operand; nu = 2; attached weights), the explicit
+    form, x += A e — on planes that are a whole number of tiles (64^3), a partial last tile
+    (48^3, 46^3), an odd plane (47^3: not marched) and segments of 1, 3, 7 planes or the
+    automatic length; the norm form (k_rowpat_uni) alongside; the cycle equals the
+    CSR-stream cycle bit for bit, eager and from the captured graph."""
+    torch = torch_cuda
+    from mlamg._lib import call, ptr, stream_ptr
+    monkeypatch.setenv("MLAMG_RPM", rpm)
+    monkeypatch.setenv("MLAMG_RPM_CH", ch)
+    monkeypatch.setenv("MLAMG_RPM_SEG", seg)
+    rs = np.random.RandomState(13)
+    s = stream_ptr()
+    for m in (64, 48, 46, 47):
+        A = ml.problems.poisson_3d_7pt(m)
+        n = A.shape[0]
+        x, b, d, y0 = rs.randn(n), rs.randn(n), rs.rand(n) + 0.5, rs.randn(n)
+        xd, bd, dd = dev(torch, x), dev(torch, b), dev(torch, d)
+        Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("rowpat")
+        y = A @ x
+        assert np.array_equal(Ad.matvec(xd).cpu().numpy(), y)
+        yd = dev(torch, y0)
+        call("mlamg_spmv", Ad.handle, ptr(xd), ptr(yd), 2.0, -0.5, s)
+        assert np.array_equal(yd.cpu().numpy(), 2.0 * y + (-0.5) * y0)
+        r = torch.empty(n, dtype=torch.float64, device="cuda")
+        call("mlamg_residual", Ad.handle, ptr(bd), ptr(xd), ptr(r), None, s)
+        assert np.array_equal(r.cpu().numpy(), b - y)
+        nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
+        r.zero_()
+        call("mlamg_residual", Ad.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), s)
+        assert np.array_equal(r.cpu().numpy(), b - y)
+        assert abs(nrm.item() - np.linalg.norm(b - y)) <= 1e-13 * np.linalg.norm(b - y)
+        xs, t = dev(torch, x), torch.empty(n, dtype=torch.float64, device="cuda")
+        call("mlamg_jacobi", Ad.handle, ptr(dd), ptr(bd), ptr(xs), ptr(t), 2, s)
+        x1 = x + d * (b - y)
+        assert np.array_equal(xs.cpu().numpy(), x1 + d * (b - A @ x1))
+        xs = dev(torch, x)
+        call("mlamg_jacobi_explicit", Ad.handle, ptr(dd), ptr(bd), ptr(xs), ptr(t), 1, s)
+        assert np.array_equal(xs.cpu().numpy(), x + (d * b - y))
+        xs = dev(torch, y0)
+        call("mlamg_prolong_add", Ad.handle, ptr(xd), ptr(xs), s)
+        assert np.array_equal(xs.cpu().numpy(), y0 + y)
+        # attached weights (the per-pattern table) give the same bits
+        dw = dev(torch, np.full(n, 1.0 / 9.0))
+        assert Ad.attach_dinv(dw)
+        xs = dev(torch, x)
+        call("mlamg_jacobi", Ad.handle, ptr(dw), ptr(bd), ptr(xs), ptr(t), 1, s)
+        assert np.array_equal(xs.cpu().numpy(), x + np.full(n, 1.0 / 9.0) * (b - y))
+    A = ml.problems.poisson_3d_7pt(48)
+    bd = dev(torch, rs.randn(A.shape[0]))
+    x0 = rs.randn(A.shape[0])
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=500, fine_format="csr_stream")
+    H2 = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=500, fine_format="csr_stream")
+    H2.levels[0].A.set_format("rowpat")
+    assert H2.levels[0].A.attach_dinv(H2.levels[0].dinv)
+    for use_graph in (False, True):
+        x1, x2 = dev(torch, x0), dev(torch, x0)
+        h1 = H.cycle(bd, x1, 4, use_graph=use_graph)
+        h2 = H2.cycle(bd, x2, 4, use_graph=use_graph)
+        assert torch.equal(x1, x2)
+        assert np.allclose(h1, h2, rtol=1e-14, atol=0)
+
+
 def test_supplied_aggregates_and_prolongator(ml, oracle, torch_cuda):
     """Hierarchy.build with supplied level-0 aggregates (C5: learned/supplied aggregates on the
     jump-coefficient problem) and with a supplied P (the MLAMG PC's learned P,

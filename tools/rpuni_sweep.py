@@ -1,6 +1,7 @@
 """Launch-shape sweep of the uniform stencil kernel (k_rowpat_uni) on the C4 fine operator:
 chunks per workgroup (MLAMG_RPU_CH) and an LDS pad that caps workgroups per CU
-(MLAMG_RPU_LDSPAD), y = A x timed cold by its dispatch packet (mlamg_timer_*, a 512 MB read
+(MLAMG_RPU_LDSPAD), and the plane-marching form (rpm=0|1, mch=2|4 chunks, seg planes per
+segment; MLAMG_RPM*), y = A x timed cold by its dispatch packet (mlamg_timer_*, a 512 MB read
 before each launch) and back to back; outputs compared bitwise with the first configuration.
 
   python tools/rpuni_sweep.py [n3=216] ch=4,pad=0 ch=2,pad=0 ...
@@ -38,6 +39,9 @@ def main():
         kv = dict(t.split("=") for t in cfg.split(","))
         os.environ["MLAMG_RPU_CH"] = kv.get("ch", "4")
         os.environ["MLAMG_RPU_LDSPAD"] = kv.get("pad", "0")
+        os.environ["MLAMG_RPM"] = kv.get("rpm", "1")        # plane-marching form
+        os.environ["MLAMG_RPM_CH"] = kv.get("mch", "4")
+        os.environ["MLAMG_RPM_SEG"] = kv.get("seg", "0")
         M = DeviceCSR.from_scipy(A, check=False).set_format("rowpat")
         M.matvec(x, out=y)
         torch.cuda.synchronize()
