@@ -3251,7 +3251,8 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
   drop_rowpat(A);
   A->rp_uni = uni;
   // plane-marching form (k_rowpat_march): the 3-D 7-point layout with its far offsets one even
-  // plane of rows F apart. MLAMG_RPM=0 turns it off; MLAMG_RPM_CH (2 | 4) and MLAMG_RPM_SEG
+  // plane of rows F apart. Opt-in (MLAMG_RPM=1: slower than k_rowpat_uni so far, DESIGN.md
+  // §13); MLAMG_RPM_CH (1 | 2 | 4) and MLAMG_RPM_SEG
   // (planes per segment; 0 = enough workgroups for two (CH 4) / four (CH 2) per CU) are A/B knobs
   if (uni.k == 7 && uni.layout == 1 && A->n_rows == A->n_cols && uni.off[6] > 0 &&
       uni.off[0] == -uni.off[6] && (uni.off[6] & 1) == 0 && uni.off[6] >= 2048 &&
@@ -3259,7 +3260,7 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
     const char* e0 = std::getenv("MLAMG_RPM");
     const char* e1 = std::getenv("MLAMG_RPM_CH");
     const char* e2 = std::getenv("MLAMG_RPM_SEG");
-    if (!(e0 && std::atoi(e0) == 0)) {
+    if (e0 && std::atoi(e0) == 1) {
       const int64_t F = uni.off[6];
       const int ch = e1 && (std::atoi(e1) == 1 || std::atoi(e1) == 2) ? std::atoi(e1) : 4;
       const int64_t T = 2 * ch * kThreads;
