@@ -202,7 +202,7 @@ struct mlamg_csr {
   // plane-marching form of a uniform 3-D 7-point stencil (k_rowpat_march; rp_mF == 0: none):
   // far offset +-rp_mF (one grid plane), chunks per tile, planes per z segment
   int64_t rp_mF = 0;
-  int32_t rp_mch = 4, rp_mseg = 0;
+  int32_t rp_mch = 4, rp_mseg = 0, rp_mpf = 1;
   // attached Jacobi weights (mlamg_csr_attach_dinv): an epilogue whose dinv pointer equals
   // rp_dinv_att reads the per-pattern values rp_dinv[2p], rp_dinv[2p+1] instead of memory
   const double* rp_dinv_att = nullptr;

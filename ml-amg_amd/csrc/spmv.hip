@@ -692,8 +692,13 @@ __device__ __forceinline__ int uni_k(const RpUni& U) {
 #ifndef MLAMG_UNI_DBG
 #define MLAMG_UNI_DBG 0  // timing-only builds (tools/build_variant.sh): 1 no masks, 2 no id
 #endif                   // loads, 4 no far loads, 8 no stores — results are then wrong
+#ifndef MLAMG_UNI_WPE  // build-time A/B knob: minimum waves per SIMD for k_rowpat_uni (0: free)
+#define MLAMG_UNI_WPE 0
+#endif
 template <int OP, bool NORM, int CH, int LY>
-__global__ __launch_bounds__(kThreads) void k_rowpat_uni(
+__global__ __launch_bounds__(kThreads)
+__attribute__((amdgpu_waves_per_eu(MLAMG_UNI_WPE > 0 ? MLAMG_UNI_WPE : 1, 8)))
+void k_rowpat_uni(
     const uint8_t* __restrict__ pid, const uint16_t* __restrict__ pat_msk, int n_pat,
     int64_t n_rows, int64_t n_cols, const double* __restrict__ dinv_att,
     const dbl2* __restrict__ pat_dinv, RpUni U, const double* __restrict__ x, Epi ep) {
@@ -848,7 +853,7 @@ __global__ __launch_bounds__(kThreads) void k_rowpat_uni(
 // summed (plain loads survive the barrier). Per row pair: the same pattern id, mask, values,
 // products and order as k_rowpat_uni — the same bits. No NORM form: the norm partials follow
 // the 2048-row blocks of the other row-pair kernels, which plane tiles do not align with.
-template <int OP, int CH>
+template <int OP, int CH, int PF>
 __global__ __launch_bounds__(kThreads) void k_rowpat_march(
     const uint8_t* __restrict__ pid, const uint16_t* __restrict__ pat_msk, int n_pat,
     int64_t n_rows, const double* __restrict__ dinv_att, const dbl2* __restrict__ pat_dinv,
@@ -875,37 +880,39 @@ __global__ __launch_bounds__(kThreads) void k_rowpat_march(
   const int64_t tile0 = (int64_t)j * T;
   const int64_t lim = F - tile0;  // rows of the tile inside its plane (even)
   constexpr int WQ = CH + 2;      // window slots per thread (halo <= 256 pairs a side)
-  dbl2 wv[WQ];
-  auto wload = [&](int64_t k) {
+  auto wload = [&](dbl2 (&v)[WQ], int64_t k) {
     const int64_t w0 = k * F + tile0 - U.halo;
 #pragma unroll
     for (int q = 0; q < WQ; ++q) {
       const int i = threadIdx.x + q * kThreads;
-      wv[q] = x16(x, w0 + 2 * (int64_t)(i < W ? i : 0), n_rows);
+      v[q] = x16(x, w0 + 2 * (int64_t)(i < W ? i : 0), n_rows);
     }
   };
-  auto wstore = [&](int slot) {
+  auto wstore = [&](const dbl2 (&v)[WQ], int slot) {
     dbl2* w = ring + slot * W;
 #pragma unroll
     for (int q = 0; q < WQ; ++q) {
       const int i = threadIdx.x + q * kThreads;
-      if (i < W) w[i] = wv[q];
+      if (i < W) w[i] = v[q];
     }
   };
-  // prologue: planes k0 - 1 and k0 staged, k0 + 1 in flight
-  wload(k0 - 1);
-  wstore(0);
-  wload(k0);
-  wstore(1);
-  wload(k0 + 1);
+  // PF planes ahead in registers: set A holds plane k + 1 at step k (k - k0 even), set B at the
+  // odd steps (PF = 1: one set, reloaded every step)
+  dbl2 wa[WQ], wb[WQ];
+  // prologue: planes k0 - 1 and k0 staged, k0 + 1 (and k0 + 2) in flight
+  wload(wa, k0 - 1);
+  wstore(wa, 0);
+  wload(wa, k0);
+  wstore(wa, 1);
+  wload(wa, k0 + 1);
+  if (PF == 2 && k0 + 2 <= k1) wload(wb, k0 + 2);
   for (int i = threadIdx.x; i < 256; i += kThreads) msk[i] = i < n_pat ? pat_msk[i] : 0;
   if (tab_dinv)
     for (int i = threadIdx.x; i < n_pat; i += kThreads) dt[i] = pat_dinv[i];
   int sm = 0;  // ring slot of plane k - 1 (k, k + 1 follow cyclically)
-#pragma unroll 1
-  for (int64_t k = k0; k < k1; ++k) {
+  auto step = [&](int64_t k, dbl2 (&cur)[WQ]) {
     const int sc = sm == 2 ? 0 : sm + 1, sp = sc == 2 ? 0 : sc + 1;
-    wstore(sp);  // plane k + 1 (its slot held plane k - 2, last read before the previous barrier)
+    wstore(cur, sp);  // plane k + 1 (its slot held plane k - 2, last read before the last barrier)
     // this plane's pattern ids and epilogue operands, in flight across the barrier
     const int64_t rb = k * F + tile0;
     int pc[CH];
@@ -919,7 +926,8 @@ __global__ __launch_bounds__(kThreads) void k_rowpat_march(
       if (ok0) epi_load2<OP>((int)r, r + 1 < n_rows, ep, u[c], w[c], tab_dinv, x_op);
     }
     __syncthreads();
-    if (k + 2 <= k1) wload(k + 2);  // the next plane's window, in flight while this one sums
+    // plane k + 1 + PF's window into the set just stored, in flight while PF planes sum
+    if (k + 1 + PF <= k1) wload(cur, k + 1 + PF);
     const dbl2* wm = ring + sm * W;
     const dbl2* wc = ring + sc * W;
     const dbl2* wp = ring + sp * W;
@@ -974,6 +982,16 @@ __global__ __launch_bounds__(kThreads) void k_rowpat_march(
     }
     __syncthreads();  // plane k - 1's slot is refilled next
     sm = sc;
+  };
+  if constexpr (PF == 1) {
+#pragma unroll 1
+    for (int64_t k = k0; k < k1; ++k) step(k, wa);
+  } else {
+#pragma unroll 1
+    for (int64_t k = k0; k < k1; k += 2) {
+      step(k, wa);
+      if (k + 1 < k1) step(k + 1, wb);
+    }
   }
 }
 
@@ -1941,7 +1959,7 @@ static int launch_rowpat_uni(const mlamg_csr* A, const double* x, const Epi& ep,
   return MLAMG_OK;
 }
 
-template <int OP, int CH>
+template <int OP, int CH, int PF>
 static int launch_rowpat_march(const mlamg_csr* A, const double* x, const Epi& ep,
                                hipStream_t s) {
   constexpr int64_t T = 2 * CH * kThreads;
@@ -1952,7 +1970,7 @@ static int launch_rowpat_march(const mlamg_csr* A, const double* x, const Epi& e
   const unsigned nb = (unsigned)(nt * ((n_planes + seg - 1) / seg));
   const size_t lds = sizeof(dbl2) * (size_t)(3 * (CH * kThreads + A->rp_uni.halo) + A->rp_n_pat) +
                      sizeof(uint16_t) * 256;
-  MLAMG_LAUNCH((k_rowpat_march<OP, CH>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid, A->rp_msk,
+  MLAMG_LAUNCH((k_rowpat_march<OP, CH, PF>), dim3(nb), dim3(kThreads), lds, s, A->rp_pid, A->rp_msk,
                A->rp_n_pat, A->n_rows, A->rp_dinv_att, reinterpret_cast<const dbl2*>(A->rp_dinv),
                A->rp_uni, x, ep, F, nt, seg, n_planes);
   MLAMG_HIP(hipGetLastError());
@@ -1963,9 +1981,13 @@ template <int OP, bool NORM>
 static int launch_rowpair(const mlamg_csr* A, const double* x, const Epi& ep, hipStream_t s) {
   if constexpr (!NORM) {
     if (A->rp_mF > 0 && A->rp_msk)
-      return A->rp_mch == 1   ? launch_rowpat_march<OP, 1>(A, x, ep, s)
-             : A->rp_mch == 2 ? launch_rowpat_march<OP, 2>(A, x, ep, s)
-                              : launch_rowpat_march<OP, 4>(A, x, ep, s);
+      switch (A->rp_mch + 8 * A->rp_mpf) {
+        case 1 + 8: return launch_rowpat_march<OP, 1, 1>(A, x, ep, s);
+        case 2 + 8: return launch_rowpat_march<OP, 2, 1>(A, x, ep, s);
+        case 4 + 8: return launch_rowpat_march<OP, 4, 1>(A, x, ep, s);
+        case 1 + 16: return launch_rowpat_march<OP, 1, 2>(A, x, ep, s);
+        default: return launch_rowpat_march<OP, 2, 2>(A, x, ep, s);
+      }
   }
   if (A->rp_uni.k > 0 && A->rp_msk) {
     switch (A->rp_uni.ch) {
@@ -3268,8 +3290,10 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
       const int64_t target = 256 * (ch == 4 ? 2 : ch == 2 ? 4 : 6);
       int64_t seg = e2 ? std::atoi(e2) : 0;
       if (seg <= 0) seg = std::max<int64_t>(2, (n_planes * nt + target - 1) / target);
+      const char* e3 = std::getenv("MLAMG_RPM_PF");  // planes prefetched ahead (1 | 2)
       A->rp_mF = F;
       A->rp_mch = ch;
+      A->rp_mpf = (e3 && std::atoi(e3) == 2 && ch <= 2) ? 2 : 1;
       A->rp_mseg = (int32_t)std::min<int64_t>(seg, n_planes);
     }
   }

@@ -672,21 +672,24 @@ def test_rowpat_window(ml, torch_cuda, monkeypatch, win):
         assert np.allclose(h1, h2, rtol=1e-14, atol=0)
 
 
-@pytest.mark.parametrize("rpm,ch,seg", [("1", "4", "0"), ("1", "4", "1"), ("1", "2", "0"),
-                                        ("1", "2", "3"), ("1", "4", "7"), ("1", "1", "0"), ("0", "4", "0")])
-def test_rowpat_march(ml, torch_cuda, monkeypatch, rpm, ch, seg):
+@pytest.mark.parametrize("rpm,ch,seg,pf", [
+    ("1", "4", "0", "1"), ("1", "4", "1", "1"), ("1", "2", "0", "1"), ("1", "2", "3", "1"),
+    ("1", "4", "7", "1"), ("1", "1", "0", "1"), ("1", "2", "0", "2"), ("1", "1", "3", "2"),
+    ("1", "2", "1", "2"), ("0", "4", "0", "1")])
+def test_rowpat_march(ml, torch_cuda, monkeypatch, rpm, ch, seg, pf):
     """Plane-marching form of the uniform 3-D stencil kernel (k_rowpat_march, csrc/spmv.hip;
     MLAMG_RPM=0: k_rowpat_uni): every non-norm epilogue bitwise scipy — y = A x, y = 2 A x -
     y/2, the residual, Jacobi (xin == x, window operand; nu = 2; attached weights), the explicit
     form, x += A e — on planes that are a whole number of tiles (64^3), a partial last tile
-    (48^3, 46^3), an odd plane (47^3: not marched) and segments of 1, 3, 7 planes or the
-    automatic length; the norm form (k_rowpat_uni) alongside; the cycle equals the
+    (48^3, 46^3), an odd plane (47^3: not marched), segments of 1, 3, 7 planes or the
+    automatic length, and one or two planes prefetched; the norm form (k_rowpat_uni) alongside; the cycle equals the
     CSR-stream cycle bit for bit, eager and from the captured graph."""
     torch = torch_cuda
     from mlamg._lib import call, ptr, stream_ptr
     monkeypatch.setenv("MLAMG_RPM", rpm)
     monkeypatch.setenv("MLAMG_RPM_CH", ch)
     monkeypatch.setenv("MLAMG_RPM_SEG", seg)
+    monkeypatch.setenv("MLAMG_RPM_PF", pf)
     rs = np.random.RandomState(13)
     s = stream_ptr()
     for m in (64, 48, 46, 47):

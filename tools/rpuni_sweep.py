@@ -42,6 +42,7 @@ def main():
         os.environ["MLAMG_RPM"] = kv.get("rpm", "1")        # plane-marching form
         os.environ["MLAMG_RPM_CH"] = kv.get("mch", "4")
         os.environ["MLAMG_RPM_SEG"] = kv.get("seg", "0")
+        os.environ["MLAMG_RPM_PF"] = kv.get("pf", "1")
         M = DeviceCSR.from_scipy(A, check=False).set_format("rowpat")
         M.matvec(x, out=y)
         torch.cuda.synchronize()
