@@ -651,10 +651,10 @@ void k_rowpair(const uint8_t* __restrict__ pid,
 // stencils, where the patterns only differ in which neighbours a boundary row lacks (C4 A_0: 27
 // patterns over the 7 offsets -n^2 -n -1 0 1 n n^2). A pattern is then a 16-bit mask (the slots
 // row 2i and row 2i+1 have) in a 512-byte LDS table and the values are kernel arguments. Same pid
-// bytes as k_rowpair; chunk c of workgroup lb holds pairs lb*CH*256 + c*256 + lane, and with
-// CH = kRpChunks the lane -> pair map, the norm partials and every product and sum are
-// k_rowpair's, i.e. scipy's (an entry a row lacks is a +0.0 operand: a sum started at +0.0 is
-// never -0.0, so adding it changes no bit). The x operands within +-halo rows come from an LDS
+// bytes as k_rowpair; chunk c of workgroup lb holds pairs lb*CH*256 + c*256 + lane (CH = 2 by
+// default; with CH = kRpChunks the norm partials are k_rowpair's too), and every product and
+// sum is k_rowpair's, i.e. scipy's (an entry a row lacks is a +0.0 operand: a sum started at
+// +0.0 is never -0.0, so adding it changes no bit). The x operands within +-halo rows come from an LDS
 // window of the workgroup's 2 CH 256 rows plus the halo, staged once with 16-byte loads
 // (k_rowpair issues 7 16-byte texture loads per pair; tools/stencil_lab.hip k_pair_tile: 24.4 us
 // for the C4 stencil against 32.6 us with every neighbour a global load): even offsets are one
@@ -3089,9 +3089,12 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
         return true;
       };
       {
-        const char* ec = std::getenv("MLAMG_RPU_CH");  // A/B knob
-        const int chv = ec ? std::atoi(ec) : 4;
-        uni.ch = (chv == 1 || chv == 2) ? chv : 4;
+        // chunks of 256 pairs per workgroup: 2 (round 4: the C4 bench 1,292-1,318 -> 1,328-1,331
+        // V-cycles/s against 4 on one box, same cold SpMV time; profiles/r04/uni_lab/wpe_ab.log);
+        // MLAMG_RPU_CH = 1 | 2 | 4 is the A/B knob
+        const char* ec = std::getenv("MLAMG_RPU_CH");
+        const int chv = ec ? std::atoi(ec) : 2;
+        uni.ch = (chv == 1 || chv == 4) ? chv : 2;
         const char* ep = std::getenv("MLAMG_RPU_LDSPAD");  // A/B knob: caps workgroups per CU
         A->rp_lds_pad = ep ? std::max(0, std::min(std::atoi(ep), 96 << 10)) : 0;
       }

@@ -18,4 +18,5 @@ for i in 1 2; do
   MLAMG_RPU_CH=2 timeout -k 10 300 $B > gpurun_out/r04/wb_b.log 2>&1 || exit 1; echo "default ch2 $(val gpurun_out/r04/wb_b.log)"
   MLAMG_LIB=$PWD/tools/abv/libmlamg_wpe8.so MLAMG_RPU_CH=2 timeout -k 10 300 $B > gpurun_out/r04/wb_c.log 2>&1 || exit 1; echo "wpe8 ch2 $(val gpurun_out/r04/wb_c.log)"
   MLAMG_LIB=$PWD/tools/abv/libmlamg_wpe7.so timeout -k 10 300 $B > gpurun_out/r04/wb_d.log 2>&1 || exit 1; echo "wpe7 ch4 $(val gpurun_out/r04/wb_d.log)"
+  MLAMG_LIB=$PWD/tools/abv/libmlamg_nt.so timeout -k 10 300 $B > gpurun_out/r04/wb_e.log 2>&1 || exit 1; echo "nt ch4 $(val gpurun_out/r04/wb_e.log)"
 done
