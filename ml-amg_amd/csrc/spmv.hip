@@ -692,6 +692,9 @@ __device__ __forceinline__ int uni_k(const RpUni& U) {
 #ifndef MLAMG_UNI_DBG
 #define MLAMG_UNI_DBG 0  // timing-only builds (tools/build_variant.sh): 1 no masks, 2 no id
 #endif                   // loads, 4 no far loads, 8 no stores — results are then wrong
+#ifndef MLAMG_UNI_EPF  // build-time A/B knob: epilogue operands prefetched one chunk ahead
+#define MLAMG_UNI_EPF 2  // 0 never, 1 always, 2 in the NORM form (the end-of-cycle pass: traced
+#endif                   // 66.7 -> 58.6 us; the other passes got slower: 51.8 -> 55.3 us)
 #ifndef MLAMG_UNI_WPE  // build-time A/B knob: minimum waves per SIMD for k_rowpat_uni (0: free)
 #define MLAMG_UNI_WPE 0
 #endif
@@ -743,6 +746,13 @@ void k_rowpat_uni(
 #pragma unroll
   for (int t = 0; t < NF; ++t)
     fcur[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0} : x16(x, 2 * pa + fo[t], n_cols);
+  // EPF: the epilogue's row operands (b, ...) of chunk 0 go out here too, and chunk c + 1's
+  // with its id and far operands, so no chunk waits for its own epilogue loads
+  constexpr bool EPF = MLAMG_UNI_EPF == 1 || (MLAMG_UNI_EPF == 2 && NORM);
+  EpiIn unx, wnx;
+  if constexpr (EPF) {
+    if (2 * pa < n_rows) epi_load2<OP>((int)(2 * pa), 2 * pa + 1 < n_rows, ep, unx, wnx, tab_dinv, x_op);
+  }
   constexpr int WQ = CH + 2;  // window slots per thread (halo <= 256 pairs a side)
   dbl2 wv[WQ];
 #pragma unroll
@@ -767,9 +777,16 @@ void k_rowpat_uni(
     const bool both = 2 * pr + 1 < n_rows;
     const int r = ok0 ? (int)(2 * pr) : 0;
     EpiIn u, w;
-    if (ok0) epi_load2<OP>(r, both, ep, u, w, tab_dinv, x_op);
-    // the next chunk's id and far operands, in flight while this one sums
     const int64_t prn = pr + kThreads;
+    if constexpr (EPF) {
+      u = unx;
+      w = wnx;
+      if (c + 1 < CH && 2 * prn < n_rows)
+        epi_load2<OP>((int)(2 * prn), 2 * prn + 1 < n_rows, ep, unx, wnx, tab_dinv, x_op);
+    } else {
+      if (ok0) epi_load2<OP>(r, both, ep, u, w, tab_dinv, x_op);
+    }
+    // the next chunk's id and far operands, in flight while this one sums
     const int pnext = (MLAMG_UNI_DBG & 2) ? 13 : pid[c + 1 < CH && 2 * prn < n_rows ? prn : 0];
     dbl2 fnext[NFR];
 #pragma unroll
