@@ -95,3 +95,39 @@ def test_comm_init_and_partitioned_operator(ml):
         call("mlamg_comm_finalize")
     c = ctypes.c_void_p()
     assert _lib.lib.mlamg_comm_default(ctypes.byref(c)) == _lib.MLAMG_EINVAL
+
+
+def test_dispatch_packet_timer(ml):
+    """mlamg_timer_* (bench.py's roofline timing): an armed timer is consumed by the next
+    SpMV-family launch, which still computes scipy's bits; elapsed_ms returns that kernel's time
+    (positive, below the host-measured wall time of the call); reading a timer that no launch
+    consumed is an error, and a timer armed then destroyed leaves later launches untimed."""
+    import time
+
+    import torch
+    from mlamg._lib import MlamgError, call, ptr, stream_ptr
+    A = ml.problems.poisson_3d_7pt(64)
+    n = A.shape[0]
+    x = np.random.RandomState(3).randn(n)
+    Ad = ml.sparse.DeviceCSR.from_scipy(A).set_format("rowpat")
+    xd = torch.as_tensor(x).cuda()
+    yd = torch.empty_like(xd)
+    tm = ctypes.c_void_p()
+    call("mlamg_timer_create", ctypes.byref(tm))
+    ms = ctypes.c_float()
+    with pytest.raises(MlamgError):
+        call("mlamg_timer_elapsed_ms", tm, ctypes.byref(ms))  # never armed
+    torch.cuda.synchronize()
+    for _ in range(3):
+        t0 = time.perf_counter()
+        call("mlamg_timer_arm", tm)
+        call("mlamg_spmv", Ad.handle, ptr(xd), ptr(yd), 1.0, 0.0, stream_ptr())
+        call("mlamg_timer_elapsed_ms", tm, ctypes.byref(ms))
+        wall_ms = (time.perf_counter() - t0) * 1e3
+        assert 0.0 < ms.value < wall_ms
+        assert np.array_equal(yd.cpu().numpy(), A @ x)
+    call("mlamg_timer_arm", tm)
+    call("mlamg_timer_destroy", tm)  # disarms: the next launch must not touch the freed events
+    call("mlamg_spmv", Ad.handle, ptr(xd), ptr(yd), 1.0, 0.0, stream_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(yd.cpu().numpy(), A @ x)
