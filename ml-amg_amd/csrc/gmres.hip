@@ -14,8 +14,9 @@
 // preconditioner (hier_coarse_cycle: one V-cycle from a zero guess, replayed from a captured
 // graph), and the Gram-Schmidt dots / updates (fixed-order reductions finished by the
 // last-arriving workgroup, so a solve is deterministic). The (restart+1)-sized Hessenberg work —
-// rotations, the triangular solve, the tolerance logic — is done on the host from the column the
-// device computed (one read-back per inner iteration), as scipy does in numpy.
+// rotations and the inner stop test — runs on the device in one thread (k_gm_arnoldi, the same
+// operations as scipy's numpy code), so an inner iteration costs one status read; the
+// triangular solve and the restart logic stay on the host, once per restart cycle.
 #include "common.hpp"
 
 #include <cmath>
@@ -36,9 +37,10 @@ __device__ __forceinline__ double gm_wave_sum(double v) {
 __global__ __launch_bounds__(kGmThreads) void k_gm_dot(const double* __restrict__ a,
                                                       const double* __restrict__ b, int64_t n,
                                                       double* __restrict__ partial, int32_t* ctr,
-                                                      double* out) {
+                                                      double* out, const int32_t* done) {
   __shared__ double red[kGmThreads / 64];
   __shared__ int last;
+  if (done && *done) return;  // uniform: no workgroup arrives, the counter stays 0
   double s = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kGmThreads)
@@ -67,7 +69,8 @@ __global__ __launch_bounds__(kGmThreads) void k_gm_dot(const double* __restrict_
 // w -= (*coef) * v   (numpy's `w -= tmp * v[k, :]`: one product, one subtraction per entry)
 __global__ __launch_bounds__(kGmThreads) void k_gm_axmy(double* __restrict__ w,
                                                        const double* __restrict__ v, int64_t n,
-                                                       const double* coef) {
+                                                       const double* coef, const int32_t* done) {
+  if (done && *done) return;
   const double c = *coef;
   for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kGmThreads)
@@ -79,6 +82,18 @@ __global__ __launch_bounds__(kGmThreads) void k_gm_scale(double* __restrict__ y,
                                                         const double* __restrict__ x, int64_t n,
                                                         double d) {
   const double inv = 1.0 / d;
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads)
+    y[i] = x[i] * inv;
+}
+
+// y = x * (1 / d) with d read on the device (the Arnoldi step's h1), skipped once done
+__global__ __launch_bounds__(kGmThreads) void k_gm_scale_dev(double* __restrict__ y,
+                                                            const double* __restrict__ x,
+                                                            int64_t n, const double* d,
+                                                            const int32_t* done) {
+  if (*done) return;
+  const double inv = 1.0 / *d;
   for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kGmThreads)
     y[i] = x[i] * inv;
@@ -104,7 +119,7 @@ static int gm_grid(int64_t n) {
 
 // LAPACK dlartg (3.10+, the safe-scaling version scipy's get_lapack_funcs('lartg') binds):
 // c f + s g = r, -s f + c g = 0
-static void lartg(double f, double g, double* c, double* s, double* r) {
+__host__ __device__ static void lartg(double f, double g, double* c, double* s, double* r) {
   if (g == 0.0) {
     *c = 1.0;
     *s = 0.0;
@@ -112,13 +127,63 @@ static void lartg(double f, double g, double* c, double* s, double* r) {
   } else if (f == 0.0) {
     *c = 0.0;
     *s = g > 0 ? 1.0 : -1.0;
-    *r = std::fabs(g);
+    *r = fabs(g);
   } else {
-    const double d = std::sqrt(f * f + g * g);
-    *c = std::fabs(f) / d;
+    const double d = sqrt(f * f + g * g);
+    *c = fabs(f) / d;
     *r = f > 0 ? d : -d;
     *s = g / *r;
   }
+}
+
+// One Arnoldi step's small-matrix work on the device, by one thread — what the host did with
+// the read-back column, the same operations in the same order (so the same bits): Hessenberg
+// column from the MGS coefficients and norms, exact-solution test, the past rotations, a new
+// rotation (lartg), the rotated right-hand side and the preconditioned residual estimate; then
+// the inner stop (presid <= ptol or breakdown) raises `done`, which the next iteration's kernels
+// and V-cycle (the hierarchy's own flag) read, so the host needs one status read per iteration.
+// st: [0] presid, [1] h1 (the scale of v_{col+1}), [2] breakdown, [3] last column, [4] steps,
+// [5] ||w||^2 before the projections (h0^2).
+__global__ void k_gm_arnoldi(int col, int ldh, const double* __restrict__ scal, int norm_slot,
+                             double* __restrict__ Hd, double* __restrict__ giv,
+                             double* __restrict__ S, double* __restrict__ st, double eps,
+                             double ptol, double bnrm2, double* __restrict__ hist, int hist_cap,
+                             int32_t* done) {
+  if (threadIdx.x != 0 || blockIdx.x != 0 || *done) return;
+  auto H = [&](int c, int k) -> double& { return Hd[(size_t)c * ldh + k]; };
+  const double h0 = sqrt(st[5]);
+  for (int k = 0; k <= col; ++k) H(col, k) = scal[k];
+  const double h1 = sqrt(scal[norm_slot]);
+  H(col, col + 1) = h1;
+  bool breakdown = false;
+  if (h1 <= eps * h0) {  // exact solution indicator
+    H(col, col + 1) = 0.0;
+    breakdown = true;
+  }
+  st[1] = h1;
+  for (int k = 0; k < col; ++k) {  // past rotations
+    const double c = giv[2 * k], sn = giv[2 * k + 1];
+    const double n0 = H(col, k), n1 = H(col, k + 1);
+    H(col, k) = c * n0 + sn * n1;
+    H(col, k + 1) = -sn * n0 + c * n1;
+  }
+  double c, sn, mag;
+  lartg(H(col, col), H(col, col + 1), &c, &sn, &mag);
+  giv[2 * col] = c;
+  giv[2 * col + 1] = sn;
+  H(col, col) = mag;
+  H(col, col + 1) = 0.0;
+  const double t2 = -sn * S[col];
+  S[col] = c * S[col];
+  S[col + 1] = t2;
+  const double presid = fabs(t2);
+  const int steps = (int)st[4];
+  if (hist && steps < hist_cap) hist[steps] = presid / bnrm2;
+  st[0] = presid;
+  st[2] = breakdown ? 1.0 : 0.0;
+  st[3] = (double)col;
+  st[4] = (double)(steps + 1);
+  if (presid <= ptol || breakdown) *done = 1;
 }
 
 struct GmWork {
@@ -130,6 +195,11 @@ struct GmWork {
   double* scal = nullptr;  // dot results: [0..restart+1) MGS coefficients, [restart+1] norm^2
   double* y = nullptr;     // solution of the small triangular system
   int32_t* ctr = nullptr;
+  double* Hd = nullptr;    // restart x (restart + 1) Hessenberg columns (device copy)
+  double* giv = nullptr;   // 2 restart Givens coefficients
+  double* S = nullptr;     // restart + 1 rotated right-hand side
+  double* st = nullptr;    // Arnoldi status (k_gm_arnoldi)
+  double* hist = nullptr;  // presid / ||b|| per inner step
   void* mem = nullptr;
   int64_t ld = 0;
 };
@@ -144,8 +214,10 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   GmWork W;
   W.ld = ((std::max<int64_t>(n, 1) + 31) / 32) * 32;
   const size_t vec = sizeof(double) * W.ld;
+  const size_t small = sizeof(double) * ((size_t)restart * (restart + 1) + 2 * restart +
+                                         (restart + 1) + 8 + std::max(hist_cap, 1));
   const size_t total = vec * (restart + 1) + 3 * vec + sizeof(double) * kGmMaxBlocks +
-                       sizeof(double) * (2 * restart + 4) + 256;
+                       sizeof(double) * (2 * restart + 6) + 256 + small;
   MLAMG_HIP(hipMalloc(&W.mem, total));
   char* p = static_cast<char*>(W.mem);
   W.V = reinterpret_cast<double*>(p);
@@ -161,6 +233,11 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   W.scal = reinterpret_cast<double*>(p);
   W.y = W.scal + restart + 2;
   W.ctr = reinterpret_cast<int32_t*>(W.y + restart + 2);
+  W.Hd = reinterpret_cast<double*>(reinterpret_cast<char*>(W.ctr) + 64);
+  W.giv = W.Hd + (size_t)restart * (restart + 1);
+  W.S = W.giv + 2 * restart;
+  W.st = W.S + restart + 1;
+  W.hist = W.st + 8;
   struct Free {
     void* m;
     ~Free() { (void)hipFree(m); }
@@ -171,11 +248,14 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   const int nb = gm_grid(n);
   const int norm_slot = restart + 1;
 
-  auto dot = [&](const double* a, const double* c, int slot) -> int {
+  auto dot_to = [&](const double* a, const double* c, double* out, const int32_t* dn) -> int {
     hipLaunchKernelGGL(k_gm_dot, dim3(nb), dim3(kGmThreads), 0, s, a, c, n, W.partial, W.ctr,
-                       W.scal + slot);
+                       out, dn);
     MLAMG_HIP(hipGetLastError());
     return MLAMG_OK;
+  };
+  auto dot = [&](const double* a, const double* c, int slot) -> int {
+    return dot_to(a, c, W.scal + slot, nullptr);
   };
   auto read = [&](int slot, int count, double* dst) -> int {
     MLAMG_HIP(hipMemcpyAsync(dst, W.scal + slot, sizeof(double) * count, hipMemcpyDeviceToHost,
@@ -219,8 +299,8 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   double ptol_max_factor = 1.0;
   double ptol = Mb_nrm2 * std::min(ptol_max_factor, atol / bnrm2);
   double presid = 0.0, rnorm = 0.0;
-  std::vector<double> h((size_t)restart * (restart + 1), 0.0), giv(2 * (size_t)restart, 0.0),
-      S(restart + 1, 0.0), y(restart + 1, 0.0), col_h(restart + 2, 0.0);
+  std::vector<double> h((size_t)restart * (restart + 1), 0.0), S(restart + 1, 0.0),
+      y(restart + 1, 0.0);
   auto H = [&](int c, int k) -> double& { return h[(size_t)c * (restart + 1) + k]; };
   double* V0 = W.V;
   auto Vk = [&](int k) { return W.V + (int64_t)k * W.ld; };
@@ -242,54 +322,49 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
     MLAMG_HIP(hipGetLastError());
     std::fill(S.begin(), S.end(), 0.0);
     S[0] = tmp;
+    // the cycle's small state on the device: rotated right-hand side, step count; the inner
+    // stop is the hierarchy's done flag (k_gm_arnoldi raises it; the V-cycle and the Krylov
+    // kernels of later steps then do nothing), one status read per step
+    int32_t* done = hier_done_flag(M);
+    double st_h[8] = {0.0, 0.0, 0.0, 0.0, (double)iters, 0.0, 0.0, 0.0};
+    MLAMG_HIP(hipMemcpyAsync(W.S, S.data(), sizeof(double) * (restart + 1),
+                             hipMemcpyHostToDevice, s));
+    MLAMG_HIP(hipMemcpyAsync(W.st, st_h, sizeof(st_h), hipMemcpyHostToDevice, s));
     bool breakdown = false;
     int col = 0;
     for (col = 0; col < restart; ++col) {
-      MLAMG_TRY(spmv_set(A, Vk(col), W.r, nullptr, s));  // av (W.r is free until the update)
-      MLAMG_TRY(psolve(W.r, W.w));                       // w = M av
-      double h0 = 0.0;
-      MLAMG_TRY(norm(W.w, &h0));
+      MLAMG_TRY(spmv_set(A, Vk(col), W.r, done, s));  // av (W.r is free until the update)
+      MLAMG_TRY(psolve(W.r, W.w));                    // w = M av
+      MLAMG_TRY(dot_to(W.w, W.w, W.st + 5, done));    // h0^2
       for (int k = 0; k <= col; ++k) {  // modified Gram-Schmidt, coefficient on the device
-        MLAMG_TRY(dot(Vk(k), W.w, k));
+        MLAMG_TRY(dot_to(Vk(k), W.w, W.scal + k, done));
         hipLaunchKernelGGL(k_gm_axmy, dim3(nb), dim3(kGmThreads), 0, s, W.w, Vk(k), n,
-                           W.scal + k);
+                           W.scal + k, done);
         MLAMG_HIP(hipGetLastError());
       }
-      MLAMG_TRY(dot(W.w, W.w, norm_slot));
-      MLAMG_TRY(read(0, restart + 2, col_h.data()));
-      for (int k = 0; k <= col; ++k) H(col, k) = col_h[k];
-      const double h1 = std::sqrt(col_h[norm_slot]);
-      H(col, col + 1) = h1;
-      if (h1 <= eps * h0) {  // exact solution indicator
-        H(col, col + 1) = 0.0;
-        breakdown = true;
-        MLAMG_HIP(hipMemcpyAsync(Vk(col + 1), W.w, sizeof(double) * n, hipMemcpyDeviceToDevice,
-                                 s));
-      } else {
-        hipLaunchKernelGGL(k_gm_scale, dim3(nb), dim3(kGmThreads), 0, s, Vk(col + 1), W.w, n,
-                           h1);
-        MLAMG_HIP(hipGetLastError());
-      }
-      for (int k = 0; k < col; ++k) {  // past rotations
-        const double c = giv[2 * k], sn = giv[2 * k + 1];
-        const double n0 = H(col, k), n1 = H(col, k + 1);
-        H(col, k) = c * n0 + sn * n1;
-        H(col, k + 1) = -sn * n0 + c * n1;
-      }
-      double c, sn, mag;
-      lartg(H(col, col), H(col, col + 1), &c, &sn, &mag);
-      giv[2 * col] = c;
-      giv[2 * col + 1] = sn;
-      H(col, col) = mag;
-      H(col, col + 1) = 0.0;
-      const double t2 = -sn * S[col];
-      S[col] = c * S[col];
-      S[col + 1] = t2;
-      presid = std::fabs(t2);
-      if (presid_hist && iters < hist_cap) presid_hist[iters] = presid / bnrm2;
-      ++iters;
-      if (presid <= ptol || breakdown) break;
+      MLAMG_TRY(dot_to(W.w, W.w, W.scal + norm_slot, done));
+      hipLaunchKernelGGL(k_gm_arnoldi, dim3(1), dim3(64), 0, s, col, restart + 1, W.scal,
+                         norm_slot, W.Hd, W.giv, W.S, W.st, eps, ptol, bnrm2,
+                         presid_hist ? W.hist : nullptr, hist_cap, done);
+      MLAMG_HIP(hipGetLastError());
+      hipLaunchKernelGGL(k_gm_scale_dev, dim3(nb), dim3(kGmThreads), 0, s, Vk(col + 1), W.w, n,
+                         W.st + 1, done);
+      MLAMG_HIP(hipGetLastError());
+      int32_t dn = 0;
+      MLAMG_HIP(hipMemcpyAsync(&dn, done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      MLAMG_HIP(hipStreamSynchronize(s));
+      if (dn) break;
     }
+    MLAMG_HIP(hipMemcpyAsync(st_h, W.st, sizeof(st_h), hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipMemcpyAsync(h.data(), W.Hd, sizeof(double) * h.size(), hipMemcpyDeviceToHost,
+                             s));
+    MLAMG_HIP(hipMemcpyAsync(S.data(), W.S, sizeof(double) * (restart + 1),
+                             hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipMemsetAsync(done, 0, sizeof(int32_t), s));  // the update's V-cycles run again
+    MLAMG_HIP(hipStreamSynchronize(s));
+    presid = st_h[0];
+    breakdown = st_h[2] != 0.0;
+    iters = (int)st_h[4];
     if (col == restart) col = restart - 1;
     if (H(col, col) == 0.0) S[col] = 0.0;
     for (int k = 0; k <= col; ++k) y[k] = S[k];
@@ -317,6 +392,9 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   }
   *info_out = rnorm <= atol ? 0 : maxiter;
   *iters_out = iters;
+  if (presid_hist && iters > 0)
+    MLAMG_HIP(hipMemcpyAsync(presid_hist, W.hist, sizeof(double) * std::min(iters, hist_cap),
+                             hipMemcpyDeviceToHost, s));
   MLAMG_HIP(hipStreamSynchronize(s));
   return MLAMG_OK;
 }
