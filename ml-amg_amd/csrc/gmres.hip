@@ -66,6 +66,52 @@ __global__ __launch_bounds__(kGmThreads) void k_gm_dot(const double* __restrict_
   if (threadIdx.x == 0) *out = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
+// The inner loop's dots without the arrival counter: k_gm_part writes k_gm_dot's per-workgroup
+// partials, and the consumer sums them with gm_total — k_gm_dot's last-workgroup sum, the same
+// order — so no workgroup needs the agent-scope fence before arriving (on MI355X that fence
+// writes back the XCD's L2, once per workgroup).
+__global__ __launch_bounds__(kGmThreads) void k_gm_part(const double* __restrict__ a,
+                                                       const double* __restrict__ b, int64_t n,
+                                                       double* __restrict__ partial,
+                                                       const int32_t* done) {
+  __shared__ double red[kGmThreads / 64];
+  if (done && *done) return;
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads)
+    s += a[i] * b[i];
+  s = gm_wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// sum of np partials by a whole workgroup of kGmThreads, k_gm_dot's order; every thread gets it
+__device__ double gm_total(const double* __restrict__ partial, int np, double* red) {
+  double t = strided_sum(partial, np, threadIdx.x, kGmThreads);
+  t = gm_wave_sum(t);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  return ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// w -= c v with c = the dot k_gm_part left in partial (every workgroup sums it; workgroup 0
+// also stores it, the Hessenberg entry)
+__global__ __launch_bounds__(kGmThreads) void k_gm_axmy_p(double* __restrict__ w,
+                                                         const double* __restrict__ v, int64_t n,
+                                                         const double* __restrict__ partial,
+                                                         int np, double* coef,
+                                                         const int32_t* done) {
+  __shared__ double red[kGmThreads / 64];
+  if (done && *done) return;
+  const double c = gm_total(partial, np, red);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *coef = c;
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads)
+    w[i] = w[i] - c * v[i];
+}
+
 // w -= (*coef) * v   (numpy's `w -= tmp * v[k, :]`: one product, one subtraction per entry)
 __global__ __launch_bounds__(kGmThreads) void k_gm_axmy(double* __restrict__ w,
                                                        const double* __restrict__ v, int64_t n,
@@ -144,16 +190,23 @@ __host__ __device__ static void lartg(double f, double g, double* c, double* s, 
 // and V-cycle (the hierarchy's own flag) read, so the host needs one status read per iteration.
 // st: [0] presid, [1] h1 (the scale of v_{col+1}), [2] breakdown, [3] last column, [4] steps,
 // [5] ||w||^2 before the projections (h0^2).
-__global__ void k_gm_arnoldi(int col, int ldh, const double* __restrict__ scal, int norm_slot,
-                             double* __restrict__ Hd, double* __restrict__ giv,
-                             double* __restrict__ S, double* __restrict__ st, double eps,
-                             double ptol, double bnrm2, double* __restrict__ hist, int hist_cap,
-                             int32_t* done) {
-  if (threadIdx.x != 0 || blockIdx.x != 0 || *done) return;
+__global__ __launch_bounds__(kGmThreads) void k_gm_arnoldi(
+    int col, int ldh, const double* __restrict__ scal, const double* __restrict__ p_h0,
+    const double* __restrict__ p_h1, int np, double* __restrict__ Hd, double* __restrict__ giv,
+    double* __restrict__ S, double* __restrict__ st, double eps, double ptol, double bnrm2,
+    double* __restrict__ hist, int hist_cap, int32_t* done) {
+  __shared__ double red[kGmThreads / 64];
+  if (*done) return;
+  // ||w||^2 before and after the projections, from k_gm_part's partials (k_gm_dot's sums)
+  const double w0 = gm_total(p_h0, np, red);
+  __syncthreads();
+  const double w1 = gm_total(p_h1, np, red);
+  if (threadIdx.x != 0) return;
+  st[5] = w0;
   auto H = [&](int c, int k) -> double& { return Hd[(size_t)c * ldh + k]; };
-  const double h0 = sqrt(st[5]);
+  const double h0 = sqrt(w0);
   for (int k = 0; k <= col; ++k) H(col, k) = scal[k];
-  const double h1 = sqrt(scal[norm_slot]);
+  const double h1 = sqrt(w1);
   H(col, col + 1) = h1;
   bool breakdown = false;
   if (h1 <= eps * h0) {  // exact solution indicator
@@ -192,6 +245,8 @@ struct GmWork {
   double* r = nullptr;
   double* pb = nullptr;   // staging right-hand side of the preconditioner (fixed address)
   double* partial = nullptr;
+  double* p_h0 = nullptr;  // k_gm_part partials of ||w||^2 before / after the projections
+  double* p_h1 = nullptr;
   double* scal = nullptr;  // dot results: [0..restart+1) MGS coefficients, [restart+1] norm^2
   double* y = nullptr;     // solution of the small triangular system
   int32_t* ctr = nullptr;
@@ -216,7 +271,7 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   const size_t vec = sizeof(double) * W.ld;
   const size_t small = sizeof(double) * ((size_t)restart * (restart + 1) + 2 * restart +
                                          (restart + 1) + 8 + std::max(hist_cap, 1));
-  const size_t total = vec * (restart + 1) + 3 * vec + sizeof(double) * kGmMaxBlocks +
+  const size_t total = vec * (restart + 1) + 3 * vec + 3 * sizeof(double) * kGmMaxBlocks +
                        sizeof(double) * (2 * restart + 6) + 256 + small;
   MLAMG_HIP(hipMalloc(&W.mem, total));
   char* p = static_cast<char*>(W.mem);
@@ -229,6 +284,10 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   W.pb = reinterpret_cast<double*>(p);
   p += vec;
   W.partial = reinterpret_cast<double*>(p);
+  p += sizeof(double) * kGmMaxBlocks;
+  W.p_h0 = reinterpret_cast<double*>(p);
+  p += sizeof(double) * kGmMaxBlocks;
+  W.p_h1 = reinterpret_cast<double*>(p);
   p += sizeof(double) * kGmMaxBlocks;
   W.scal = reinterpret_cast<double*>(p);
   W.y = W.scal + restart + 2;
@@ -248,14 +307,11 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   const int nb = gm_grid(n);
   const int norm_slot = restart + 1;
 
-  auto dot_to = [&](const double* a, const double* c, double* out, const int32_t* dn) -> int {
+  auto dot = [&](const double* a, const double* c, int slot) -> int {
     hipLaunchKernelGGL(k_gm_dot, dim3(nb), dim3(kGmThreads), 0, s, a, c, n, W.partial, W.ctr,
-                       out, dn);
+                       W.scal + slot, nullptr);
     MLAMG_HIP(hipGetLastError());
     return MLAMG_OK;
-  };
-  auto dot = [&](const double* a, const double* c, int slot) -> int {
-    return dot_to(a, c, W.scal + slot, nullptr);
   };
   auto read = [&](int slot, int count, double* dst) -> int {
     MLAMG_HIP(hipMemcpyAsync(dst, W.scal + slot, sizeof(double) * count, hipMemcpyDeviceToHost,
@@ -335,16 +391,18 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
     for (col = 0; col < restart; ++col) {
       MLAMG_TRY(spmv_set(A, Vk(col), W.r, done, s));  // av (W.r is free until the update)
       MLAMG_TRY(psolve(W.r, W.w));                    // w = M av
-      MLAMG_TRY(dot_to(W.w, W.w, W.st + 5, done));    // h0^2
+      hipLaunchKernelGGL(k_gm_part, dim3(nb), dim3(kGmThreads), 0, s, W.w, W.w, n, W.p_h0,
+                         done);  // h0^2
       for (int k = 0; k <= col; ++k) {  // modified Gram-Schmidt, coefficient on the device
-        MLAMG_TRY(dot_to(Vk(k), W.w, W.scal + k, done));
-        hipLaunchKernelGGL(k_gm_axmy, dim3(nb), dim3(kGmThreads), 0, s, W.w, Vk(k), n,
-                           W.scal + k, done);
+        hipLaunchKernelGGL(k_gm_part, dim3(nb), dim3(kGmThreads), 0, s, Vk(k), W.w, n,
+                           W.partial, done);
+        hipLaunchKernelGGL(k_gm_axmy_p, dim3(nb), dim3(kGmThreads), 0, s, W.w, Vk(k), n,
+                           W.partial, nb, W.scal + k, done);
         MLAMG_HIP(hipGetLastError());
       }
-      MLAMG_TRY(dot_to(W.w, W.w, W.scal + norm_slot, done));
-      hipLaunchKernelGGL(k_gm_arnoldi, dim3(1), dim3(64), 0, s, col, restart + 1, W.scal,
-                         norm_slot, W.Hd, W.giv, W.S, W.st, eps, ptol, bnrm2,
+      hipLaunchKernelGGL(k_gm_part, dim3(nb), dim3(kGmThreads), 0, s, W.w, W.w, n, W.p_h1, done);
+      hipLaunchKernelGGL(k_gm_arnoldi, dim3(1), dim3(kGmThreads), 0, s, col, restart + 1,
+                         W.scal, W.p_h0, W.p_h1, nb, W.Hd, W.giv, W.S, W.st, eps, ptol, bnrm2,
                          presid_hist ? W.hist : nullptr, hist_cap, done);
       MLAMG_HIP(hipGetLastError());
       hipLaunchKernelGGL(k_gm_scale_dev, dim3(nb), dim3(kGmThreads), 0, s, Vk(col + 1), W.w, n,
