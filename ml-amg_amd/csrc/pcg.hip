@@ -15,7 +15,8 @@
 // once. Eagerly launched solves poll the flag every few iterations and stop launching; inside a
 // stream capture every iteration up to maxit is recorded (the V-cycle executor therefore runs
 // hierarchies with a PCG coarse solver eagerly). Reductions are fixed-order (partials over a
-// fixed grid, summed in order by the last-arriving workgroup), so a solve is deterministic.
+// fixed grid, summed in order by the kernel that consumes the scalar), so a solve is
+// deterministic.
 #include "common.hpp"
 
 #include <cmath>
@@ -30,7 +31,8 @@ struct mlamg_pcg {
   void* mem = nullptr;
   double *r = nullptr, *p = nullptr, *q = nullptr, *partial = nullptr;
   double* scal = nullptr;     // [0] rho, [1] alpha, [2] beta, [3] ||b||^2, [4] ||r||^2 (last),
-                              // [5] largest final ||r||/||b|| over solves
+                              // [5] largest final ||r||/||b|| over solves, [6], [7] rho by
+                              // iteration parity
   int32_t* flags = nullptr;   // [0] iterations of the last solve, [1] solves not converged,
                               // [2] total iterations, [3] solves ended by a breakdown
                               // (p.Ap <= 0, r.z <= 0 or a NaN: A_c or the preconditioner
@@ -129,72 +131,44 @@ __device__ __forceinline__ void breakdown(int32_t* done, int32_t* flags) {
   flags[3] += 1;
 }
 
-// alpha = rho / (p.q)
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_alpha(const double* __restrict__ p,
-                                                           const double* __restrict__ q, int64_t n,
-                                                           double* __restrict__ partial,
-                                                           int32_t* ctr, double* scal,
-                                                           int32_t* done, int32_t* flags) {
+// The iteration's dot products without the arrival counter: a reduction kernel only writes
+// its per-workgroup partials, and the kernel that consumes the scalar sums them itself (every
+// workgroup, last_total's fixed order, so every workgroup gets the same bits). An arrival counter
+// needs an agent-scope release fence in every workgroup, and on MI355X that fence writes back the
+// XCD's L2 (GMRES, the same change: 1.6-2.7x per solve). rho alternates between scal[6] and
+// scal[7] by iteration parity, so no workgroup overwrites a value another one still reads.
+
+// partials of p.q (the alpha step's denominator)
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_pq(const double* __restrict__ p,
+                                                        const double* __restrict__ q, int64_t n,
+                                                        double* __restrict__ partial,
+                                                        const int32_t* done) {
   if (*done) return;
   double s = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kPcgThreads)
     s += p[i] * q[i];
   block_partial(s, partial);
-  if (!arrive_last(ctr)) return;
-  const double t = last_total(partial, gridDim.x);
-  if (threadIdx.x == 0) {
-    scal[1] = scal[0] / t;
-    if (!(t > 0.0)) breakdown(done, flags);  // p.Ap <= 0 or NaN: A_c not positive definite
-  }
 }
 
-// rho = r.z, beta = rho / rho_old (first: beta = 0, so k_pcg_p sets p = z)
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_rho(const double* __restrict__ r,
-                                                         const double* __restrict__ z, int64_t n,
-                                                         double* __restrict__ partial,
-                                                         int32_t* ctr, double* scal,
-                                                         int32_t* done, int32_t* flags,
-                                                         int first) {
-  if (*done) return;
-  double s = 0.0;
-  for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kPcgThreads)
-    s += r[i] * z[i];
-  block_partial(s, partial);
-  if (!arrive_last(ctr)) return;
-  const double t = last_total(partial, gridDim.x);
-  if (threadIdx.x == 0) {
-    scal[2] = first ? 0.0 : t / scal[0];
-    scal[0] = t;
-    // r != 0 here (a zero residual ended the solve), so r.z <= 0 means the preconditioner is
-    // not positive definite
-    if (!(t > 0.0)) breakdown(done, flags);
-  }
-}
-
-// p = z + beta p
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_p(const double* __restrict__ z,
-                                                       double* __restrict__ p, int64_t n,
-                                                       const double* scal, const int32_t* done) {
-  if (*done) return;
-  const double beta = scal[2];
-  for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kPcgThreads)
-    p[i] = z[i] + beta * p[i];
-}
-
-// x += alpha p, r -= alpha q; ||r||^2 <= rtol^2 ||b||^2 -> done; iteration count
+// alpha = rho / (p.q); x += alpha p, r -= alpha q; partials of r.r
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(double* __restrict__ x,
                                                             double* __restrict__ r,
                                                             const double* __restrict__ p,
                                                             const double* __restrict__ q,
                                                             int64_t n, double* scal,
+                                                            const double* __restrict__ pq,
                                                             double* __restrict__ partial,
-                                                            int32_t* ctr, int32_t* done,
-                                                            int32_t* flags, double rtol) {
+                                                            int np, int32_t* done,
+                                                            int32_t* flags, int it) {
   if (*done) return;
-  const double alpha = scal[1];
+  const double t = last_total(pq, np);
+  const double alpha = scal[6 + (it & 1)] / t;
+  if (!(t > 0.0)) {  // p.Ap <= 0 or NaN: A_c not positive definite
+    if (blockIdx.x == 0 && threadIdx.x == 0) breakdown(done, flags);
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) scal[1] = alpha;
   double s = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kPcgThreads) {
@@ -204,8 +178,15 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(double* __restrict__
     s += v * v;
   }
   block_partial(s, partial);
-  if (!arrive_last(ctr)) return;
-  const double t = last_total(partial, gridDim.x);
+}
+
+// ||r||^2 <= rtol^2 ||b||^2 -> done (before the V-cycle, which then does nothing); iteration
+// count; one workgroup
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_check(const double* __restrict__ partial,
+                                                           int np, double* scal, int32_t* done,
+                                                           int32_t* flags, double rtol) {
+  if (*done) return;
+  const double t = last_total(partial, np);
   if (threadIdx.x == 0) {
     scal[4] = t;
     flags[0] += 1;
@@ -218,6 +199,45 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(double* __restrict__
       breakdown(done, flags);  // NaN residual
     }
   }
+}
+
+// partials of r.z
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_rz(const double* __restrict__ r,
+                                                        const double* __restrict__ z, int64_t n,
+                                                        double* __restrict__ partial,
+                                                        const int32_t* done) {
+  if (*done) return;
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kPcgThreads)
+    s += r[i] * z[i];
+  block_partial(s, partial);
+}
+
+// rho = r.z (into scal[6 + (it + 1) % 2], the next iteration's), beta = rho / rho_old (first:
+// beta = 0, so p = z); p = z + beta p
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_p(const double* __restrict__ z,
+                                                       double* __restrict__ p, int64_t n,
+                                                       const double* __restrict__ rz, int np,
+                                                       double* scal, int32_t* done,
+                                                       int32_t* flags, int first, int it) {
+  if (*done) return;
+  const double t = last_total(rz, np);
+  // r != 0 here (a zero residual ended the solve), so r.z <= 0 means the preconditioner is not
+  // positive definite
+  if (!(t > 0.0)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) breakdown(done, flags);
+    return;
+  }
+  const double beta = first ? 0.0 : t / scal[6 + (it & 1)];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    scal[6 + ((it + 1) & 1)] = t;
+    scal[0] = t;
+    scal[2] = beta;
+  }
+  for (int64_t i = blockIdx.x * (int64_t)kPcgThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kPcgThreads)
+    p[i] = z[i] + beta * p[i];
 }
 
 // after the last launched iteration: a solve that did not reach the tolerance is counted
@@ -234,19 +254,22 @@ static int pcg_grid(int64_t n) {
                                                                         kPcgThreads));
 }
 
-static int pcg_iteration(mlamg_pcg* C, double* x, int32_t* done, hipStream_t s) {
+static int pcg_iteration(mlamg_pcg* C, double* x, int32_t* done, int it, hipStream_t s) {
   const int nb = C->nb;
   const int64_t n = C->n;
+  double* pa = C->partial;             // p.q partials
+  double* pb = C->partial + kPcgMaxBlocks;  // r.r, then r.z partials
   MLAMG_TRY(spmv_set(C->A, C->p, C->q, done, s));
-  hipLaunchKernelGGL(k_pcg_alpha, dim3(nb), dim3(kPcgThreads), 0, s, C->p, C->q, n, C->partial,
-                     C->ctr, C->scal, done, C->flags);
+  hipLaunchKernelGGL(k_pcg_pq, dim3(nb), dim3(kPcgThreads), 0, s, C->p, C->q, n, pa, done);
   hipLaunchKernelGGL(k_pcg_update, dim3(nb), dim3(kPcgThreads), 0, s, x, C->r, C->p, C->q, n,
-                     C->scal, C->partial, C->ctr, done, C->flags, C->rtol);
+                     C->scal, pa, pb, nb, done, C->flags, it);
+  hipLaunchKernelGGL(k_pcg_check, dim3(1), dim3(kPcgThreads), 0, s, pb, nb, C->scal, done,
+                     C->flags, C->rtol);
   double* z = nullptr;
   MLAMG_TRY(hier_coarse_cycle(C->M, C->r, &z, 0, s));
-  hipLaunchKernelGGL(k_pcg_rho, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, n, C->partial,
-                     C->ctr, C->scal, done, C->flags, 0);
-  hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(kPcgThreads), 0, s, z, C->p, n, C->scal, done);
+  hipLaunchKernelGGL(k_pcg_rz, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, n, pa, done);
+  hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(kPcgThreads), 0, s, z, C->p, n, pa, nb, C->scal,
+                     done, C->flags, 0, it);
   MLAMG_HIP(hipGetLastError());
   return MLAMG_OK;
 }
@@ -264,15 +287,17 @@ int pcg_solve_impl(mlamg_pcg* C, const double* b, double* x, const int32_t* oute
                      C->ctr, C->scal, done, outer_done, C->flags);
   double* z = nullptr;
   MLAMG_TRY(hier_coarse_cycle(C->M, C->r, &z, 0, s));
-  hipLaunchKernelGGL(k_pcg_rho, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, C->n, C->partial,
-                     C->ctr, C->scal, done, C->flags, 1);
-  hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(kPcgThreads), 0, s, z, C->p, C->n, C->scal, done);
+  // rho_0 = r.z into scal[6] (iteration 0 reads it), p = z
+  hipLaunchKernelGGL(k_pcg_rz, dim3(nb), dim3(kPcgThreads), 0, s, C->r, z, C->n, C->partial,
+                     done);
+  hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(kPcgThreads), 0, s, z, C->p, C->n, C->partial, nb,
+                     C->scal, done, C->flags, 1, -1);
   // The host polls the done flag without draining the queue: after queueing group g of `poll`
   // iterations it copies the flag into pinned slot g % 2 and then waits for group g - 1's copy,
   // so the device always has the next group queued while the host reads the previous one.
   int g = 0;
   for (int it = 0; it < C->maxit; ++it) {
-    MLAMG_TRY(pcg_iteration(C, x, done, s));
+    MLAMG_TRY(pcg_iteration(C, x, done, it, s));
     if (poll && (it + 1) % C->poll == 0 && it + 1 < C->maxit) {
       const int slot = g & 1;
       MLAMG_HIP(hipMemcpyAsync(C->done_host + slot, done, sizeof(int32_t), hipMemcpyDeviceToHost,
@@ -343,7 +368,7 @@ int mlamg_pcg_create(const mlamg_csr* A, mlamg_hier* M, double rtol, int maxit,
   C->maxit = maxit;
   C->nb = pcg_grid(C->n);
   const size_t vec = ((sizeof(double) * (size_t)std::max<int64_t>(C->n, 1)) + 255) & ~size_t(255);
-  const size_t total = 3 * vec + sizeof(double) * kPcgMaxBlocks + 256 + 256;
+  const size_t total = 3 * vec + 2 * sizeof(double) * kPcgMaxBlocks + 256 + 256;
   if (hipMalloc(&C->mem, total) != hipSuccess) {
     delete C;
     set_error("pcg_create: hipMalloc failed");
@@ -354,8 +379,8 @@ int mlamg_pcg_create(const mlamg_csr* A, mlamg_hier* M, double rtol, int maxit,
   C->p = reinterpret_cast<double*>(p + vec);
   C->q = reinterpret_cast<double*>(p + 2 * vec);
   C->partial = reinterpret_cast<double*>(p + 3 * vec);
-  C->scal = reinterpret_cast<double*>(p + 3 * vec + sizeof(double) * kPcgMaxBlocks);
-  C->flags = reinterpret_cast<int32_t*>(p + 3 * vec + sizeof(double) * kPcgMaxBlocks + 256);
+  C->scal = reinterpret_cast<double*>(p + 3 * vec + 2 * sizeof(double) * kPcgMaxBlocks);
+  C->flags = reinterpret_cast<int32_t*>(p + 3 * vec + 2 * sizeof(double) * kPcgMaxBlocks + 256);
   C->ctr = C->flags + 8;
   if (hipMemset(C->mem, 0, total) != hipSuccess ||
       hipHostMalloc(&C->done_host, 2 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess ||
