@@ -225,8 +225,12 @@ def test_sync_formats_makes_replicas_bitwise():
     from mlamg.hierarchy import Hierarchy
     A = problems.poisson_3d_7pt(40)
     H0 = Hierarchy.build(A, alpha=0.1, max_coarse=100)
-    H1 = Hierarchy.build(A, alpha=0.1, max_coarse=100, coarse_format="exact")  # other choices
-    assert H0.formats() != H1.formats()
+    H1 = Hierarchy.build(A, alpha=0.1, max_coarse=100, coarse_format="exact")
+    # a replica whose timings went another way on every operator (the autotune alone may or may
+    # not pick differently on a given box)
+    H1.set_formats([{k: (("sell", 1) if v[0] != "sell" else ("csr_stream", 0)) for k, v in lv.items()}
+                    for lv in H0.formats()])
+    assert all(a[k][0] != b[k][0] for a, b in zip(H0.formats(), H1.formats()) for k in a)
     H1.set_formats(H0.formats())
     assert H1.formats() == H0.formats()
     n = A.shape[0]
