@@ -60,6 +60,14 @@ def main():
     fetch, f1, drv = run_pass("FETCH_SIZE", fmt, tag)
     write, f2, _ = run_pass("WRITE_SIZE", fmt, tag)
     l2 = {}
+    if os.environ.get("PMC_SQ") == "1":  # where the waves' time goes (quad-cycle units)
+        names = ("SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY "
+                 "SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS")
+        v, _, _ = run_pass(names, fmt, tag)
+        for name in names.split():
+            xs = sorted(x for nm, x in v if nm == name)
+            if xs:
+                l2[name + "_median"] = xs[len(xs) // 2]
     if os.environ.get("PMC_L2") == "1":
         v, _, _ = run_pass("TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum", fmt, tag)
         for name in ("TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_sum"):
