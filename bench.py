@@ -125,65 +125,27 @@ def spmv_bytes(n_rows, n_cols, nnz):
     return 12.0 * nnz + 4.0 * (n_rows + 1) + 8.0 * n_cols + 8.0 * n_rows
 
 
+def aggregation_rule(args):
+    """The aggregation rule a bench line used, in words (config.workload)."""
+    if args.aggregation == "reference":
+        order = ("columns relabelled in ascending seed order" if args.coarse_order == "sorted"
+                 else "nearest_center_to_agg column order")
+        return ("level 0: the reference's push-order modified_bellman_ford from unsorted "
+                f"RandomState(0) seeds, graph.py:40-51, {order}; coarser levels: "
+                "order-independent rule, sorted seeds")
+    return "every level: order-independent rule (smallest tight seed), sorted seeds"
+
+
 def time_kernel(fn, reps=50):
-    """Average device time of fn() (one kernel launch on torch's current stream) via HIP events."""
-    s = torch.cuda.current_stream()
-    fn()
-    torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(reps):
-        fn()
-    e1.record(s)
-    e1.synchronize()
-    return e0.elapsed_time(e1) / 1000.0 / reps
-
-
-_FLUSH = None
+    """mlamg.timing.time_kernel (imported lazily: the self-launching parent never loads HIP)."""
+    from mlamg.timing import time_kernel as tk
+    return tk(fn, reps)
 
 
 def time_kernel_cold(fn, reps=20):
-    """Device time of fn() (one SpMV-family kernel launch on torch's current stream) from a cold
-    cache: each launch follows a read of a 512 MB buffer (twice the 256 MB MALL, so no operand
-    survives in any cache level — what the autotune does before its timings,
-    mlamg/hierarchy.py). The kernel is timed by the events of its own dispatch packet
-    (mlamg_timer_*, hipExtLaunchKernel): its execution alone, which is what rocprofv3's kernel
-    trace reports for the same launches (tools/rocprof_roofline.py). A second round brackets each
-    call with a pair of stream events instead (event packet + dispatch + kernel), reported beside
-    it. Returns (mean, median, stream-event mean) in s."""
-    import ctypes
-    from mlamg._lib import call
-    global _FLUSH
-    if _FLUSH is None:
-        _FLUSH = torch.ones(64 << 20, dtype=torch.float64, device="cuda")
-    s = torch.cuda.current_stream()
-    fn()
-    torch.cuda.synchronize()
-    sink = torch.empty((), dtype=torch.float64, device="cuda")
-    tm = ctypes.c_void_p()
-    call("mlamg_timer_create", ctypes.byref(tm))
-    ts = []
-    try:
-        ms = ctypes.c_float()
-        for _ in range(reps):
-            torch.sum(_FLUSH, dim=0, out=sink)
-            call("mlamg_timer_arm", tm)
-            fn()
-            call("mlamg_timer_elapsed_ms", tm, ctypes.byref(ms))
-            ts.append(ms.value / 1000.0)
-    finally:
-        call("mlamg_timer_destroy", tm)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(reps)]
-    for e0, e1 in ev:
-        torch.sum(_FLUSH, dim=0, out=sink)
-        e0.record(s)
-        fn()
-        e1.record(s)
-    torch.cuda.synchronize()
-    te = [e0.elapsed_time(e1) / 1000.0 for e0, e1 in ev]
-    return float(np.mean(ts)), float(np.median(ts)), float(np.mean(te))
+    """mlamg.timing.time_kernel_cold: cold launches timed by their own dispatch packet."""
+    from mlamg.timing import time_kernel_cold as tkc
+    return tkc(fn, reps)
 
 
 def load_traffic(name):
@@ -245,6 +207,13 @@ def main():
                     help="grid points per dimension (C4: 216); use --grid under torchrun")
     ap.add_argument("--alpha", type=float, default=0.1)
     ap.add_argument("--max-coarse", type=int, default=2000)
+    ap.add_argument("--aggregation", choices=("reference", "bellman_ford"), default="reference",
+                    help="level-0 aggregates: 'reference' = the reference's push-order seeded "
+                         "Bellman-Ford (ns/lib/graph.py:40-51, utils/evaluate_dataset.py:80-90); "
+                         "'bellman_ford' = the order-independent rule on every level")
+    ap.add_argument("--coarse-order", choices=("sorted", "seed"), default="sorted",
+                    help="aggregation='reference': level-0 coarse unknowns in ascending seed "
+                         "order (same aggregates, relabelled) or nearest_center_to_agg's order")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cycles", type=int, default=20)
     ap.add_argument("--cpu-par-cycles", type=int, default=10)
@@ -264,6 +233,9 @@ def main():
                     help="skip the variable-coefficient 216^3 cycle beside the headline")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="launch the ranks, rendezvous over gloo and report them; no GPU work")
+    ap.add_argument("--phase-selftest", action="store_true",
+                    help="run the distributed phase sequence over gloo with its watchdog (a "
+                         "stall injected by MLAMG_STALL_RANK_PHASE=rank:phase); no GPU work")
     ap.add_argument("--verify-selftest", action="store_true",
                     help="run the distributed verification chain over gloo (mismatch injected "
                          "by MLAMG_INJECT_MISMATCH_RANK); no GPU work")
@@ -281,6 +253,9 @@ def main():
         return launch_selftest(world, rank)
     if args.verify_selftest:
         return verify_selftest(world, rank)
+    if args.phase_selftest:
+        from mlamg import distributed
+        return distributed.phase_selftest(world, rank)
     if os.environ.get("MLAMG_ONE_DEVICE") == "1":
         local_rank = 0  # rehearsal only: every rank on GPU 0 (checks the RCCL code path on 1 GPU)
     torch.cuda.set_device(local_rank)
@@ -295,7 +270,8 @@ def main():
     A = problems.poisson_3d_7pt(n1)
     log(f"C4 matrix {A.shape[0]} rows, {A.nnz} nnz built in {time.perf_counter() - t0:.1f}s")
     H = Hierarchy.build(A, alpha=args.alpha, strength_mode="invabs", max_coarse=args.max_coarse,
-                        verbose=args.verbose)
+                        verbose=args.verbose, aggregation=args.aggregation,
+                        coarse_order=args.coarse_order)
     setup_s = H.timings["total"]
     for row in H.describe():
         log(row)
@@ -364,7 +340,9 @@ def main():
         "config": {
             "workload": f"C4: 3D 7-point Laplace {n1}^3 ({n} DoF, nnz {A0.nnz}), SA-AMG "
                         f"V(1,1) weighted Jacobi w=2/3, seeded Bellman-Ford aggregates "
-                        f"alpha={args.alpha}, {H.n_levels} levels, dense coarse n={H.Ac.shape[0]}",
+                        f"alpha={args.alpha} ({aggregation_rule(args)}), {H.n_levels} levels, "
+                        f"dense coarse n={H.Ac.shape[0]}",
+                "aggregation": args.aggregation, "coarse_order": args.coarse_order,
             "n": n, "nnz": A0.nnz, "levels": H.n_levels,
             "operator_complexity": round(H.operator_complexity(), 4),
             "parallelism": "single GPU",
@@ -469,7 +447,8 @@ def varcoef_c4(args, use_graph):
     t0 = time.perf_counter()
     A = problems.random_coeff_3d_7pt(args.n, seed=0)
     t_mat = time.perf_counter() - t0
-    H = Hierarchy.build(A, alpha=args.alpha, strength_mode="invabs", max_coarse=args.max_coarse)
+    H = Hierarchy.build(A, alpha=args.alpha, strength_mode="invabs", max_coarse=args.max_coarse,
+                        aggregation=args.aggregation, coarse_order=args.coarse_order)
     n = A.shape[0]
     x0 = np.random.RandomState(0).randn(n)
     x0 /= np.linalg.norm(x0)
@@ -492,8 +471,8 @@ def varcoef_c4(args, use_graph):
     cyc_fmt = H.cycle_bytes(stored=True)
     res = {
         "workload": f"3D 7-point diffusion {args.n}^3 ({n} DoF, nnz {A.nnz}), random face "
-                    f"coefficients 10^U(-1,1) (all values distinct), same SA-AMG V(1,1) recipe, "
-                    f"{H.n_levels} levels",
+                    f"coefficients 10^U(-1,1) (all values distinct), same SA-AMG V(1,1) recipe "
+                    f"({aggregation_rule(args)}), {H.n_levels} levels",
         "value": round(steps / dt, 3), "unit": "V-cycles/s", "ms_per_step": round(dt / steps * 1e3, 4),
         "conv_factor_10cycles": round(conv, 5),
         "fine_spmv": {"format": "/".join(map(str, A0.get_format()[:2])),
@@ -586,23 +565,28 @@ def verify_selftest(world, rank):
 
 def run_distributed(args, world, rank, local_rank):
     from mlamg import distributed
+    ph = distributed.PhaseLog(rank, world)
     try:
         out, H, x0, teardown = distributed.bench_main(args, world, rank, local_rank, METRIC,
-                                                      HBM_PEAK_GBPS)
+                                                      HBM_PEAK_GBPS, phases=ph)
+        if rank == 0:
+            if not args.no_cpu_baseline:
+                # rank 0 only, on the same (replicated) hierarchy; the others wait in teardown
+                n = x0.shape[0]
+                v, dtc, hcpu = cpu_baseline(H, np.zeros(n), x0, args.cpu_cycles)
+                out["cpu_baseline"] = {
+                    "value": round(v, 5), "unit": "V-cycles/s", "cores": 1, "kind": "port",
+                    "sample": f"{args.cpu_cycles} V-cycles of the same C4 hierarchy with the "
+                              f"scipy oracle (oracle/restated.py vcycle_solve), 1 thread, "
+                              f"{dtc:.1f}s, rank 0's host; host: {host_cores()[1]}"}
+            print(json.dumps(out), flush=True)
+        teardown()
     except distributed.DistributedMismatch as e:
         refuse_mismatch(e)
-    if rank == 0:
-        if not args.no_cpu_baseline:
-            # rank 0 only, on the same (replicated) hierarchy; the other ranks wait in teardown
-            n = x0.shape[0]
-            v, dtc, hcpu = cpu_baseline(H, np.zeros(n), x0, args.cpu_cycles)
-            out["cpu_baseline"] = {
-                "value": round(v, 5), "unit": "V-cycles/s", "cores": 1, "kind": "port",
-                "sample": f"{args.cpu_cycles} V-cycles of the same C4 hierarchy with the scipy "
-                          f"oracle (oracle/restated.py vcycle_solve), 1 thread, {dtc:.1f}s, "
-                          f"rank 0's host; host: {host_cores()[1]}"}
-        print(json.dumps(out), flush=True)
-    teardown()
+    except Exception as e:  # noqa: BLE001 — name the phase, exit non-zero, never hang
+        import traceback
+        traceback.print_exc()
+        ph.fail(f"{type(e).__name__}: {e}")
 
 
 if __name__ == "__main__":

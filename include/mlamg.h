@@ -56,11 +56,14 @@ int mlamg_stream_sync(void* stream);
  * Arm a timer on the calling thread; the next SpMV-family kernel launch (mlamg_spmv,
  * mlamg_residual, the smoother sweeps and their fused epilogues) records the timer's events in
  * its own dispatch packet and disarms it; elapsed_ms then waits for it and returns that kernel's
- * execution time, as a profiler's kernel trace reports it. */
+ * execution time, as a profiler's kernel trace reports it. A launch recorded into a stream
+ * capture never takes the timer. disarm drops an armed timer no launch took (call it after the
+ * timed entry point returns: a later, unrelated launch must not take it). */
 typedef struct mlamg_timer mlamg_timer;
 int mlamg_timer_create(mlamg_timer** out);
 int mlamg_timer_destroy(mlamg_timer* t);
 int mlamg_timer_arm(mlamg_timer* t);
+int mlamg_timer_disarm(void);
 int mlamg_timer_elapsed_ms(mlamg_timer* t, float* ms);
 
 /* ---------------------------------------------------------------- CSR handles
@@ -304,8 +307,9 @@ int mlamg_labels_to_columns(const int32_t* label, int64_t n, const int32_t* seed
 /* pyamg 4.x lloyd_cluster (called at ns/lib/graph.py:232 and behind
  * pyamg.aggregation.lloyd_aggregation, utils/common.py:91): up to maxiter rounds of {outward
  * Bellman-Ford, boundary detection, inward Bellman-Ford, recentre}, fp64 distances, the outward
- * pass in amg_core's sequential sweep order, so clusters and new seeds are bitwise pyamg's,
- * ties included. seeds (DEVICE, k) updated in place; dist[n], cluster[n] (aggregate index,
+ * pass in amg_core's sequential sweep order (as restated from pyamg 4.x's published source:
+ * pyamg is absent here, so agreement with amg_core itself, ties included, is parity unpinned;
+ * the device is bitwise the oracle's restatement, oracle/oracle.c lloyd_cluster). seeds (DEVICE, k) updated in place; dist[n], cluster[n] (aggregate index,
  * -1 none); *iters_host = rounds run (stops early when no seed moves). Syncs. */
 int mlamg_lloyd_cluster(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxiter, double* dist,
                         int32_t* cluster, int32_t* iters_host, void* stream);

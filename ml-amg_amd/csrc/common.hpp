@@ -278,11 +278,12 @@ void bump_format_epoch();
 // + kernel, which is what a pair of stream events around the call measures.
 struct LaunchTimer {
   hipEvent_t start = nullptr, stop = nullptr;
+  bool taken = false;  // a launch recorded the events since the last arm
 };
-LaunchTimer* take_armed_timer();
+LaunchTimer* take_armed_timer(hipStream_t s);
 #define MLAMG_LAUNCH(K, G, B, L, S, ...)                                             \
   do {                                                                               \
-    if (::mlamg::LaunchTimer* lt_ = ::mlamg::take_armed_timer())                     \
+    if (::mlamg::LaunchTimer* lt_ = ::mlamg::take_armed_timer(S))                    \
       hipExtLaunchKernelGGL(K, G, B, L, S, lt_->start, lt_->stop, 0, __VA_ARGS__);   \
     else                                                                             \
       hipLaunchKernelGGL(K, G, B, L, S, __VA_ARGS__);                                \

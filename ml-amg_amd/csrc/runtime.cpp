@@ -428,9 +428,15 @@ struct mlamg_timer {
 
 namespace mlamg {
 static thread_local LaunchTimer* g_armed = nullptr;
-LaunchTimer* take_armed_timer() {
+LaunchTimer* take_armed_timer(hipStream_t s) {
   LaunchTimer* t = g_armed;
+  if (!t) return nullptr;
+  // a launch being captured into a graph must not carry the events
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone)
+    return nullptr;
   g_armed = nullptr;
+  t->taken = true;
   return t;
 }
 }  // namespace mlamg
@@ -461,12 +467,17 @@ int mlamg_timer_destroy(mlamg_timer* t) {
 int mlamg_timer_arm(mlamg_timer* t) {
   MLAMG_REQUIRE(t, "t is NULL");
   t->used = true;
+  t->ev.taken = false;
   g_armed = &t->ev;
+  return MLAMG_OK;
+}
+int mlamg_timer_disarm(void) {
+  g_armed = nullptr;
   return MLAMG_OK;
 }
 int mlamg_timer_elapsed_ms(mlamg_timer* t, float* ms) {
   MLAMG_REQUIRE(t && ms, "t / ms is NULL");
-  MLAMG_REQUIRE(t->used && g_armed != &t->ev,
+  MLAMG_REQUIRE(t->used && t->ev.taken && g_armed != &t->ev,
                 "the timer was not armed, or no SpMV-family launch has consumed it");
   MLAMG_HIP(hipEventSynchronize(t->ev.stop));
   MLAMG_HIP(hipEventElapsedTime(ms, t->ev.start, t->ev.stop));

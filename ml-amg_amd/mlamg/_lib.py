@@ -77,6 +77,7 @@ SIGNATURES = {
     "mlamg_timer_create": (c_int, [c_vpp]),
     "mlamg_timer_destroy": (c_int, [c_vp]),
     "mlamg_timer_arm": (c_int, [c_vp]),
+    "mlamg_timer_disarm": (c_int, []),
     "mlamg_timer_elapsed_ms": (c_int, [c_vp, ctypes.POINTER(ctypes.c_float)]),
     "mlamg_csr_create": (c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vpp]),
     "mlamg_csr_destroy": (c_int, [c_vp]),

@@ -9,6 +9,7 @@ one problem across GPUs is new here. Bootstrap: torch.distributed (gloo, CPU) ca
 from __future__ import annotations
 
 import ctypes
+import io
 import json
 import os
 import sys
@@ -26,8 +27,10 @@ from .sparse import DeviceCSR
 class Comm:
     """RCCL communicator created from a unique id broadcast over torch.distributed (gloo)."""
 
-    def __init__(self, world, rank):
+    def __init__(self, world, rank, phases=None):
         self.world, self.rank = world, rank
+        if phases is not None:
+            phases.enter("uid_broadcast")
         buf = ctypes.create_string_buffer(128)
         if rank == 0:
             call("mlamg_comm_unique_id", buf)
@@ -35,6 +38,8 @@ class Comm:
         if world > 1:
             dist.broadcast_object_list(obj, src=0)
         uid = ctypes.create_string_buffer(obj[0], 128)
+        if phases is not None:
+            phases.enter("comm_create")
         h = ctypes.c_void_p()
         call("mlamg_comm_create", uid, int(world), int(rank), ctypes.byref(h))
         self.handle = h
@@ -175,6 +180,11 @@ class DistributedHierarchy:
         if max_partitioned is not None:
             K = max(1, min(K, int(max_partitioned)))
         self.K = K
+        if any(np.any(np.diff(H.levels[l].seeds) <= 0) for l in range(K)):
+            # coarse rows follow their seed's owner: contiguous only with ascending seeds
+            raise ValueError("the distributed cycle needs each partitioned level's coarse "
+                             "unknowns in ascending seed order (Hierarchy.build with sorted "
+                             "seeds; aggregation='reference' with coarse_order='sorted')")
         As = [A_host if (l == 0 and A_host is not None) else H.levels[l].A.to_scipy()
               for l in range(K)]
         Ps = [H.levels[l].P.to_scipy() for l in range(K)]
@@ -348,10 +358,104 @@ def sync_formats(H, world):
         H.set_formats(obj[0])
 
 
+EXIT_DIST_TIMEOUT = 5
+EXIT_DIST_FAILED = 6
+
+# the phases of a distributed bench run, in order, with their wall-time budgets (s) — generous
+# multiples of what C4 takes (the replicated build ~5 s, partition ~20 s, verify ~2 s); a phase
+# that overruns is a hang (e.g. a peer that never joined an RCCL call) and ends the rank
+DIST_PHASES = (("init", 300), ("build", 900), ("sync_formats", 300), ("uid_broadcast", 300),
+               ("comm_create", 600), ("partition", 900), ("verify", 600), ("warmup", 300),
+               ("timed", 600), ("roofline", 300), ("gather", 300), ("report", 900),
+               ("teardown", 300))
+
+
+def dist_timeout_s():
+    """Timeout of every gloo collective (init, barriers, object broadcasts): the environment's
+    MLAMG_DIST_TIMEOUT_S, default 600 s (torch's own default is 30 min)."""
+    return float(os.environ.get("MLAMG_DIST_TIMEOUT_S", "600"))
+
+
+class PhaseLog:
+    """Rank-tagged phase markers on stderr and a watchdog (VERDICT r04 Weak #5).
+
+    enter(name) prints `[mlamg rank r/w] phase <name> t=<s>` on every rank and starts that
+    phase's budget (DIST_PHASES x MLAMG_PHASE_TIMEOUT_SCALE). A watchdog thread ends the process
+    with EXIT_DIST_TIMEOUT, after printing the phase it was in, when a phase overruns its budget
+    — e.g. a rank blocked in an RCCL call whose peer never arrives (ctypes and torch release the
+    GIL while they wait, so the thread runs). fail() is the same exit for an error caught in the
+    main thread (a gloo collective that timed out). The rank exits; it never re-executes or
+    restarts itself, and a launcher (torch.distributed.run, bench.py's self-launch) then stops
+    the other ranks."""
+
+    def __init__(self, rank, world, scale=None, stream=None):
+        import threading
+        self.rank, self.world = rank, world
+        self.scale = (float(os.environ.get("MLAMG_PHASE_TIMEOUT_SCALE", "1"))
+                      if scale is None else float(scale))
+        self.budgets = dict(DIST_PHASES)
+        self.stream = stream if stream is not None else sys.stderr
+        self.t0 = time.monotonic()
+        self.name, self.started, self.deadline = "start", self.t0, None
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._watch, daemon=True, name="mlamg-phase-watchdog")
+        self._th.start()
+        try:  # a launcher's SIGTERM (another rank failed): dump where every thread is, then die
+            import faulthandler
+            import signal
+            faulthandler.register(signal.SIGTERM, file=self.stream, all_threads=True, chain=True)
+        except (AttributeError, ValueError, OSError, io.UnsupportedOperation):
+            pass
+
+    def _say(self, msg):
+        print(f"[mlamg rank {self.rank}/{self.world}] {msg}", file=self.stream, flush=True)
+
+    def enter(self, name):
+        now = time.monotonic()
+        budget = self.budgets.get(name, 600) * self.scale
+        with self._lock:
+            prev, self.name, self.started, self.deadline = self.name, name, now, now + budget
+        self._say(f"phase {name} t={now - self.t0:.1f}s (previous {prev}; budget {budget:.0f}s)")
+
+    def selftest_stall_point(self):
+        """phase_selftest only: MLAMG_SELFTEST_STALL=rank:phase makes that rank hang here."""
+        stall = os.environ.get("MLAMG_SELFTEST_STALL")
+        if stall and stall == f"{self.rank}:{self.name}":
+            self._say(f"test hook: stalling in phase {self.name}")
+            while True:
+                time.sleep(1.0)
+
+    def done(self):
+        self._stop.set()
+        self._say(f"done t={time.monotonic() - self.t0:.1f}s")
+
+    def fail(self, why, code=EXIT_DIST_FAILED):
+        with self._lock:
+            name, started = self.name, self.started
+        self._say(f"FAILED in phase {name} after {time.monotonic() - started:.1f}s "
+                  f"(t={time.monotonic() - self.t0:.1f}s): {why}; exiting {code}")
+        try:
+            sys.stdout.flush()
+        finally:
+            os._exit(code)
+
+    def _watch(self):
+        while not self._stop.wait(0.1):
+            with self._lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                name = self.name
+            if late:
+                self.fail(f"phase {name} exceeded its budget of "
+                          f"{self.budgets.get(name, 600) * self.scale:.0f}s", EXIT_DIST_TIMEOUT)
+
+
 def init_process_group(world, rank):
     if world > 1 and not dist.is_initialized():
+        import datetime
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", world_size=world, rank=rank)
+        dist.init_process_group("gloo", world_size=world, rank=rank,
+                                timeout=datetime.timedelta(seconds=dist_timeout_s()))
 
 
 def _barrier(world):
@@ -365,6 +469,31 @@ def _max(v, world):
     t = torch.tensor([v], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def phase_selftest(world, rank):
+    """bench.py --phase-selftest (CPU, gloo; no GPU work): every phase of a distributed bench
+    run in order, each opened by a barrier, under the same PhaseLog — with
+    MLAMG_SELFTEST_STALL=r:name rank r hangs in that phase (after its barrier, as a rank whose
+    work in the phase never returns) and must exit non-zero naming it; its peer waits in the
+    next phase's barrier (tests/test_bench_launch.py)."""
+    ph = PhaseLog(rank, world)
+    try:
+        for name, _ in DIST_PHASES:
+            ph.enter(name)
+            if name == "init":
+                init_process_group(world, rank)
+            elif world > 1:
+                dist.barrier()
+            ph.selftest_stall_point()
+        ph.done()
+    except Exception as e:  # a gloo collective that timed out or lost its peer
+        ph.fail(f"{type(e).__name__}: {e}")
+    if rank == 0:
+        print(json.dumps({"phase_selftest": True, "n_gpus": world,
+                          "phases": [n for n, _ in DIST_PHASES]}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 class DistributedMismatch(RuntimeError):
@@ -393,30 +522,41 @@ def verify_paths(check, D, graph_on, overlap_on):
     return graph_on, overlap_on
 
 
-def bench_main(args, world, rank, local_rank, metric, hbm_peak):
+def bench_main(args, world, rank, local_rank, metric, hbm_peak, phases=None):
     """bench.py for N > 1: strong scaling of one C4 problem over N GPUs. Returns
     (out, H, x0, teardown): `out` is the JSON dict on rank 0 (None elsewhere), H the replicated
     single-GPU hierarchy (rank 0's CPU baseline runs on it), teardown() ends the run (barrier,
-    process group). Every rank reports its own fine-level SpMV roofline and its communicator's
-    rank count as RCCL itself reports it (ncclCommCount); rank 0 gathers them."""
+    process group). Every rank reports its own fine-level SpMV roofline (cold launches timed by
+    their dispatch packet, as the N = 1 line) and its communicator's rank count as RCCL itself
+    reports it (ncclCommCount); rank 0 gathers them. `phases` (PhaseLog): every rank marks each
+    phase on stderr and a phase that overruns its budget ends the rank (DIST_PHASES)."""
     from . import problems
     from .hierarchy import Hierarchy
+    from .timing import time_kernel, time_kernel_cold
+
+    ph = phases if phases is not None else PhaseLog(rank, world)
 
     def log(*a):
         if rank == 0:
             print("[bench]", *a, file=sys.stderr, flush=True)
 
+    ph.enter("init")
     init_process_group(world, rank)
     torch.cuda.set_device(local_rank)
+    ph.enter("build")
     n1 = args.n
     A = problems.poisson_3d_7pt(n1)
     n = A.shape[0]
     t0 = time.perf_counter()
-    H = Hierarchy.build(A, alpha=args.alpha, strength_mode="invabs", max_coarse=args.max_coarse)
+    H = Hierarchy.build(A, alpha=args.alpha, strength_mode="invabs", max_coarse=args.max_coarse,
+                        aggregation=getattr(args, "aggregation", "bellman_ford"),
+                        coarse_order=getattr(args, "coarse_order", "sorted"))
     setup_s = time.perf_counter() - t0
+    ph.enter("sync_formats")
     sync_formats(H, world)
-    comm = Comm(world, rank)
+    comm = Comm(world, rank, phases=ph)
     cinfo = comm.info()
+    ph.enter("partition")
     t1 = time.perf_counter()
     omr = getattr(args, "overlap_min_rows", 2_000_000)
     D = DistributedHierarchy(H, comm, min_rows=args.dist_min_rows, A_host=A,
@@ -425,6 +565,7 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
     log(f"setup {setup_s:.1f}s (replicated), partition+upload {part_s:.1f}s; {D.K} of "
         f"{len(H.levels)} levels partitioned; rank rows {D.lo}..{D.hi}; ghosts (x, r, p) per "
         f"level {D.ghosts}; communicator {cinfo}")
+    ph.enter("verify")
     x0 = np.random.RandomState(0).randn(n)
     x0 /= np.linalg.norm(x0)
     b_own = torch.zeros(D.n_own, dtype=torch.float64, device="cuda")
@@ -458,36 +599,37 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
     ok_all = True
     del x_full, b_full
     # timing
+    ph.enter("warmup")
     x_ext = D.new_x(torch.as_tensor(x0[D.lo:D.hi]))
     D.cycle(b_own, x_ext, args.warmup, history=False)
     torch.cuda.synchronize()
     _barrier(world)
+    ph.enter("timed")
     torch.cuda.synchronize()
     ta = time.perf_counter()
     D.cycle(b_own, x_ext, args.steps, history=False)
     torch.cuda.synchronize()
     _barrier(world)
     dt = _max(time.perf_counter() - ta, world)
-    # per-rank fine-level SpMV (local rows) for the roofline
+    # per-rank fine-level SpMV (local rows) for the roofline: cold launches (a 512 MB read
+    # before each), each timed by its own dispatch packet — the N = 1 line's method; warm
+    # back-to-back launches beside it (the local operator can sit in the MALL at world 8)
+    ph.enter("roofline")
     xs = torch.randn(D.n_ext, dtype=torch.float64, device="cuda")
     ys = torch.empty(D.n_own, dtype=torch.float64, device="cuda")
-    s = torch.cuda.current_stream()
-    D.A_loc.matvec(xs, out=ys)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(50):
-        D.A_loc.matvec(xs, out=ys)
-    e1.record(s)
-    e1.synchronize()
-    t_spmv = e0.elapsed_time(e1) / 1000.0 / 50
+    t_spmv, t_med, t_ev = time_kernel_cold(lambda: D.A_loc.matvec(xs, out=ys), reps=20)
+    t_warm = time_kernel(lambda: D.A_loc.matvec(xs, out=ys), reps=50)
     B = D.A_loc.format_bytes()  # bytes the chosen storage format streams for y = A_loc x_ext
     B_csr = 12.0 * D.A_loc.nnz + 4.0 * (D.n_own + 1) + 8.0 * D.n_ext + 8.0 * D.n_own
     mine = {"rank": rank, "rccl_nranks": cinfo["nranks"], "rccl_rank": cinfo["rank"],
             "device": cinfo["device"], "transport": cinfo["transport"],
             "rows": [int(D.lo), int(D.hi)], "format": D.A_loc.get_format()[0],
             "format_bytes": B, "us": round(t_spmv * 1e6, 2),
-            "GBps": round(B / t_spmv / 1e9, 1), "frac": round(B / t_spmv / 1e9 / hbm_peak, 4)}
+            "median_us": round(t_med * 1e6, 2), "stream_event_us": round(t_ev * 1e6, 2),
+            "warm_us": round(t_warm * 1e6, 2),
+            "GBps": round(B / t_spmv / 1e9, 1), "frac": round(B / t_spmv / 1e9 / hbm_peak, 4),
+            "warm_frac": round(B / t_warm / 1e9 / hbm_peak, 4)}
+    ph.enter("gather")
     per_rank = [None] * world
     if world > 1:
         dist.all_gather_object(per_rank, mine)
@@ -513,7 +655,10 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
             "config": {
                 "workload": f"C4: 3D 7-point Laplace {n1}^3 ({n} DoF), SA-AMG V(1,1) weighted "
                             f"Jacobi, {D.K} finest levels row-split over {world} GPUs + RCCL "
-                            f"halos, {H.n_levels - D.K} coarser levels replicated",
+                            f"halos, {H.n_levels - D.K} coarser levels replicated; aggregation "
+                            f"{getattr(H, 'aggregation', 'bellman_ford')} (coarse order "
+                            f"{getattr(H, 'coarse_order', 'sorted')})",
+                "aggregation": getattr(H, "aggregation", "bellman_ford"),
                 "partitioned_levels": D.K,
                 "overlap_splits": [(s["level"], s["op"]) for s in D.splits] if overlap_on else [],
                 "n": n, "levels": H.n_levels, "parallelism": f"rowsplit{world}",
@@ -534,17 +679,24 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak):
                 "algorithmic_bytes_per_launch": slow["format_bytes"],
                 "csr_algorithmic_bytes_per_launch": B_csr,
                 "avg_launch_us": slow["us"],
+                "timing": "per rank: mean of 20 cold launches (a 512 MB read before each), each "
+                          "timed by the events of its own dispatch packet (hipExtLaunchKernel); "
+                          "the slowest rank's",
+                "warm_avg_launch_us": slow["warm_us"],
             },
             "per_rank_spmv": per_rank,
             "setup_s": {"replicated_build": round(setup_s, 3), "partition": round(part_s, 3)},
         }
+    ph.enter("report")
 
     def teardown():
         nonlocal D
+        ph.enter("teardown")
         _barrier(world)
         D = None
         if world > 1:
             dist.destroy_process_group()
+        ph.done()
 
     return out, H, x0, teardown
 

@@ -160,7 +160,8 @@ def nearest_center_to_agg(top_k, nearest_center):
 
 def lloyd_cluster_device(G, seeds_dev, maxiter=10, exact=True):
     """pyamg 4.x lloyd_cluster on the device (seeds_dev updated in place). exact=True runs the
-    outward pass in amg_core's sweep order (pyamg's clusters, ties included); exact=False the
+    outward pass in amg_core's sweep order as restated from pyamg 4.x (bitwise the oracle's
+    restatement, ties included; pyamg itself is absent: parity unpinned); exact=False the
     order-independent rule (the hierarchy's option). Returns (distances, clusters, seeds,
     iters)."""
     n = G.shape[0]
@@ -243,7 +244,8 @@ def lloyd_cluster(G, seeds, maxiter=10):
 
     seeds: an int (that many seeds drawn as np.random.permutation(N)[:seeds] from numpy's
     GLOBAL generator, like pyamg) or an array of seed nodes. Returns (distances float64,
-    clusters intc, seeds intc) like pyamg; clusters and seeds bitwise amg_core's, ties included.
+    clusters intc, seeds intc) like pyamg; clusters and seeds bitwise the oracle's restatement of
+    amg_core's sweep order, ties included (pyamg absent: parity with amg_core unpinned).
     Weights are used in float64 (the reference's graphs are float64)."""
     G = _asgraph(G)
     N = G.shape[0]

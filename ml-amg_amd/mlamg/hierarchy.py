@@ -28,7 +28,8 @@ import torch
 
 from . import _lib
 from ._lib import MLAMG_EUNSUPPORTED, MlamgError, _tol_arg, call, ptr, stream_ptr
-from .graph import aggregate_op_device, bellman_ford_device, labels_to_columns, lloyd_cluster_device
+from .graph import (aggregate_op_device, bellman_ford_device, labels_to_columns,
+                    lloyd_cluster_device, modified_bellman_ford_device)
 from .multigrid import lambda_max_dinv_a
 from .sparse import DeviceCSR, _device, as_device, galerkin, to_device_vec
 
@@ -62,7 +63,7 @@ def csr_symmetric(M, rtol=0.0):
 
 class Level:
     __slots__ = ("A", "dinv", "P", "R", "Agg", "omega", "lam", "lanczos_iters", "n_seeds",
-                 "bf_sweeps", "seeds", "gs")
+                 "bf_sweeps", "seeds", "gs", "labels")
 
     def __init__(self, A):
         self.A = A
@@ -74,6 +75,7 @@ class Level:
         self.bf_sweeps = 0
         self.seeds = None
         self.gs = None
+        self.labels = None  # per-node aggregate seed (node id, -1 none) when built by BF
 
 
 _PHASES = ("count", "alloc", "expand", "sort", "runsum", "emit", "finalize", "free")
@@ -328,12 +330,26 @@ class Hierarchy:
               max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, seed=0, sort_seeds=True,
               lanczos_tol=1e-15, lanczos_iter=20000, lloyd_maxiter=10, nu_pre=1, nu_post=1,
               fine_format="autotune", coarse_format="auto", verbose=False, finalize=True,
-              aggregates=None, prolongators=None):
+              aggregates=None, prolongators=None, coarse_order="seed"):
         """Smoothed-aggregation hierarchy built on the GPU.
 
         Per level: strength -> seeds RandomState(seed).permutation(n)[:ceil(alpha n)] ->
         seeded Bellman-Ford (or Lloyd) aggregates -> SA prolongator P = (I - w D^-1 A) Agg with
         w = (4/3)/lambda_max(D^-1 A) (ns/lib/multigrid.py:102-108) -> A_c = P^T A P (:165).
+
+        aggregation:
+          'bellman_ford' (default): every level the order-independent seeded Bellman-Ford
+              (label = smallest seed among tight predecessors), seeds sorted (sort_seeds);
+          'reference': level 0 is the reference's "dumb" recipe of
+              utils/evaluate_dataset.py:80-90 exactly — unsorted RandomState(seed) seeds, the
+              in-place row-major push sweeps of ns/lib/graph.py:40-51 in fp32
+              (mlamg_bellman_ford) and nearest_center_to_agg's columns (graph.py:56-86: column t
+              = seeds[t]); coarser levels (no reference counterpart) as 'bellman_ford'.
+              coarse_order='sorted' relabels the level-0 aggregates in ascending seed order
+              (the same aggregates — each column is the same node set — permuted so coarse
+              unknowns follow the fine ordering: locality, and the contiguous coarse ownership
+              the distributed executor needs); 'seed' keeps the reference's column order;
+          'lloyd': pyamg lloyd_cluster with the order-independent rule.
 
         aggregates / prolongators: supplied instead of computed, for the first levels — e.g. the
         learned aggregates of C5 or the learned P of the MLAMG PC
@@ -342,8 +358,14 @@ class Hierarchy:
         or an n x k 0/1 matrix (scipy or DeviceCSR), and is smoothed into P as above; a
         prolongator item is used as P as given (no smoothing). jacobi_weight="sa" smooths every
         level with its SA weight w instead of a fixed one."""
+        if aggregation not in ("bellman_ford", "reference", "lloyd"):
+            raise ValueError(f"unknown aggregation {aggregation!r}")
+        if coarse_order not in ("seed", "sorted"):
+            raise ValueError(f"coarse_order must be 'seed' or 'sorted', got {coarse_order!r}")
         H = cls()
         H.jacobi_weight = jacobi_weight
+        H.aggregation = aggregation
+        H.coarse_order = coarse_order
         t_all = time.perf_counter()
         A_dev = as_device(A)
         tm = {"aggregation": 0.0, "lambda_max": 0.0, "prolongator": 0.0, "galerkin": 0.0,
@@ -364,18 +386,27 @@ class Hierarchy:
                 C = strength(A_dev, strength_mode)
                 k = int(math.ceil(alpha * n))
                 seeds = np.random.RandomState(seed).permutation(n)[:k]
-                if sort_seeds:
-                    seeds = np.sort(seeds)
-                L.seeds = seeds
-                seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
-                if aggregation == "bellman_ford":
-                    _, lab, L.bf_sweeps = bellman_ford_device(C, seeds_dev)
+                if aggregation == "reference" and lvl == 0:
+                    # evaluate_dataset.py:80-90: push-order sweeps from the unsorted seeds
+                    seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
+                    _, lab, L.bf_sweeps = modified_bellman_ford_device(C, seeds_dev)
+                    if coarse_order == "sorted":
+                        seeds = np.sort(seeds)
+                        seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
                     col = labels_to_columns(lab, seeds_dev)
-                elif aggregation == "lloyd":
-                    _, col, _, L.bf_sweeps = lloyd_cluster_device(C, seeds_dev, lloyd_maxiter,
-                                                                  exact=False)
+                    L.labels = lab
                 else:
-                    raise ValueError(f"unknown aggregation {aggregation!r}")
+                    if sort_seeds:
+                        seeds = np.sort(seeds)
+                    seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
+                    if aggregation == "lloyd":
+                        _, col, _, L.bf_sweeps = lloyd_cluster_device(C, seeds_dev,
+                                                                      lloyd_maxiter, exact=False)
+                    else:
+                        _, lab, L.bf_sweeps = bellman_ford_device(C, seeds_dev)
+                        col = labels_to_columns(lab, seeds_dev)
+                        L.labels = lab
+                L.seeds = seeds
                 L.Agg = aggregate_op_device(col, k)
                 L.n_seeds = k
                 del C

@@ -444,9 +444,13 @@ def amg_2_v(A, P, b, x,
     # The PCG coarse solve broke down: A_H is not positive definite. SuperLU (the reference's
     # factorisation) solves any nonsingular A_H, so the coarse operator is inverted densely
     # instead (Gauss-Jordan with partial pivoting when it is not SPD) and the solve rerun; the
-    # reference's failure return only when that factorisation fails too.
+    # reference's failure return when that factorisation fails too, or when A_H is beyond the
+    # dense solver's size (the run("dense") CoarseSolveError must not escape — a
+    # dataset loop over amg_2_v expects the (x, 1.0, zeros, 0) tuple, not an exception)
     try:
         return run("dense")
+    except CoarseSolveError:
+        return failed
     except _lib.MlamgError as e:
         if e.code == _lib.MLAMG_EINVAL and "singular" in str(e):
             return failed

@@ -365,10 +365,29 @@ STRENGTH = {
 }
 
 
+def reference_aggregates(C, n, alpha, seed=0):
+    """utils/evaluate_dataset.py:80-90 ("dumb" method): seeds = RandomState(seed).permutation(N)
+    [:ceil(alpha N)] (unsorted), modified_bellman_ford on C in fp32 (graph.py:7-53), Agg =
+    nearest_center_to_agg(seeds, nearest_center) (graph.py:56-86: column t = seeds[t]).
+    Returns (seeds, nearest_center int64, Agg CSR n x k)."""
+    k = int(math.ceil(alpha * n))
+    seeds = np.random.RandomState(seed).permutation(n)[:k]
+    _, near, _ = modified_bellman_ford(C, seeds)
+    pos = np.full(n, -1, dtype=np.int64)
+    pos[seeds] = np.arange(k)
+    col = pos[near]
+    if (col < 0).any():  # the reference's dict lookup (graph.py:80-82) raises
+        raise KeyError(int(near[col < 0][0]))
+    Agg = sp.csr_matrix((np.ones(n), (np.arange(n), col)), shape=(n, k))
+    return seeds, near, Agg
+
+
 def build_hierarchy(A, alpha=0.1, strength_mode="invabs", seed=0, sort_seeds=True,
                     max_coarse=1000, max_levels=10, jacobi_weight=2.0 / 3.0, omegas=None,
-                    rhos=None):
-    """CPU restatement of mlamg.hierarchy.Hierarchy.build (aggregation='bellman_ford').
+                    rhos=None, aggregation="bellman_ford", coarse_order="seed"):
+    """CPU restatement of mlamg.hierarchy.Hierarchy.build (aggregation='bellman_ford' or
+    'reference': level 0 by reference_aggregates, columns in seed order or, with
+    coarse_order='sorted', relabelled in ascending seed order).
 
     omegas: per-level SA weights to use (e.g. the device's); None -> ARPACK (multigrid.py:105).
     rhos: per-level rho(D^-1 A) for the evolution measures ('evolution', 'olson').
@@ -383,14 +402,23 @@ def build_hierarchy(A, alpha=0.1, strength_mode="invabs", seed=0, sort_seeds=Tru
         else:
             C = STRENGTH[strength_mode](A)
         k = int(math.ceil(alpha * n))
-        seeds = np.random.RandomState(seed).permutation(n)[:k]
-        if sort_seeds:
-            seeds = np.sort(seeds)
-        _, lab = canon_bellman_ford(C, seeds)
-        pos = {int(s): t for t, s in enumerate(seeds)}
-        col = np.array([pos.get(int(l), -1) if l >= 0 else -1 for l in lab])
-        rows = np.nonzero(col >= 0)[0]
-        Agg = sp.csr_matrix((np.ones(len(rows)), (rows, col[rows])), shape=(n, k))
+        if aggregation == "reference" and not levels:
+            seeds, lab, Agg = reference_aggregates(C, n, alpha, seed)
+            if coarse_order == "sorted":
+                order = np.argsort(seeds)
+                seeds = seeds[order]
+                Agg = Agg[:, order].tocsr()
+                Agg.sort_indices()
+        else:
+            seeds = np.random.RandomState(seed).permutation(n)[:k]
+            if sort_seeds:
+                seeds = np.sort(seeds)
+            _, lab = canon_bellman_ford(C, seeds)
+            pos = np.full(n, -1, dtype=np.int64)
+            pos[seeds] = np.arange(k)
+            col = np.where(lab >= 0, pos[np.maximum(lab, 0)], -1)
+            rows = np.nonzero(col >= 0)[0]
+            Agg = sp.csr_matrix((np.ones(len(rows)), (rows, col[rows])), shape=(n, k))
         om = None if omegas is None else omegas[len(levels)]
         P, om = smoothed_aggregation_jacobi(A, Agg, omega=om)
         P = P.tocsr()

@@ -72,3 +72,45 @@ def test_failing_rank_fails_the_launch():
     would otherwise wait in the rendezvous)."""
     r = _run(["--gpus", "3", "--launch-selftest"], env_extra={"MLAMG_SELFTEST_FAIL_RANK": "1"})
     assert r.returncode == 3
+
+
+def test_phase_sequence_completes():
+    """Every rank walks the distributed bench's phases (mlamg.distributed.DIST_PHASES) under the
+    watchdog and marks each on stderr, rank-tagged."""
+    r = _run(["--gpus", "2", "--phase-selftest"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["phase_selftest"] and out["phases"][0] == "init"
+    for rank in (0, 1):
+        for ph in out["phases"]:
+            assert f"[mlamg rank {rank}/2] phase {ph} " in r.stderr, (rank, ph)
+        assert f"[mlamg rank {rank}/2] done" in r.stderr
+
+
+@pytest.mark.parametrize("phase", ("uid_broadcast", "warmup"))
+def test_stalled_rank_exits_nonzero_naming_its_phase(phase):
+    """VERDICT r04 Next #2: a rank that hangs (test hook MLAMG_SELFTEST_STALL=1:<phase>) is
+    ended by its watchdog when the phase overruns its budget: it prints the phase it was in and
+    exits non-zero (EXIT_DIST_TIMEOUT); the launcher then stops the other rank, which is waiting
+    in the next phase's barrier (a phase with twice the budget, so the stalled rank's watchdog
+    fires first). Nothing re-executes or restarts."""
+    r = _run(["--gpus", "2", "--phase-selftest"],
+             env_extra={"MLAMG_SELFTEST_STALL": f"1:{phase}",
+                        "MLAMG_PHASE_TIMEOUT_SCALE": "0.01", "MLAMG_DIST_TIMEOUT_S": "60"})
+    assert r.returncode == 5, (r.returncode, r.stderr[-3000:])
+    assert f"[mlamg rank 1/2] FAILED in phase {phase}" in r.stderr, r.stderr[-3000:]
+    assert "exceeded its budget" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_gloo_timeout_names_the_waiting_phase():
+    """The peer side: with the watchdog budgets long, the rank waiting for a stalled peer hits
+    the gloo collective timeout (MLAMG_DIST_TIMEOUT_S) in the next phase's barrier and exits
+    non-zero naming that phase; the launcher's SIGTERM then makes the stalled rank dump its
+    threads' stacks (faulthandler) before it dies — its last marker names the phase it hung in."""
+    r = _run(["--gpus", "2", "--phase-selftest"],
+             env_extra={"MLAMG_SELFTEST_STALL": "1:timed", "MLAMG_DIST_TIMEOUT_S": "5"})
+    assert r.returncode == 6, (r.returncode, r.stderr[-3000:])
+    assert "[mlamg rank 0/2] FAILED in phase roofline" in r.stderr, r.stderr[-3000:]
+    assert "[mlamg rank 1/2] test hook: stalling in phase timed" in r.stderr
+    assert "selftest_stall_point" in r.stderr  # rank 1's stack dump on SIGTERM

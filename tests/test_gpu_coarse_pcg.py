@@ -186,3 +186,9 @@ def test_pcg_breakdown_is_reported(ml, oracle, torch_cuda, monkeypatch):
     assert it >= 1 and x is not x0
     assert np.linalg.norm(bb - A @ x) <= 1e-10 and e[-1] <= 1e-10
     assert np.linalg.norm(x - xr) <= 1e-10 * np.linalg.norm(xr)
+    # A_H beyond the dense solver's size: the dense retry cannot run, and amg_2_v returns the
+    # reference's failure tuple (ns/lib/multigrid.py:167-170) instead of raising
+    monkeypatch.setattr(H_, "DENSE_LIMIT", 1000)
+    x, c, e, it = ml.multigrid.amg_2_v(A, P, bb, x0, res_tol=1e-10, max_iter=7,
+                                       engine="hierarchy")
+    assert x is x0 and c == 1.0 and it == 0 and np.array_equal(e, np.zeros(7))

@@ -122,3 +122,56 @@ def test_varcoef_refuses_stencil_encodings(ml, torch_cuda):
         with pytest.raises(MlamgError) as e:
             Ad.set_format(fmt)
         assert e.value.code == MLAMG_EUNSUPPORTED
+
+
+@pytest.mark.parametrize("coarse_order", ("seed", "sorted"))
+def test_c2_reference_aggregation_parity(ml, oracle, torch_cuda, coarse_order):
+    """aggregation='reference' on C2 (2D 5-point 1024^2, full size): the level-0 aggregate
+    operator is bitwise the reference's "dumb" recipe (utils/evaluate_dataset.py:80-90:
+    unsorted RandomState(0) seeds, modified_bellman_ford's fp32 push sweeps, graph.py:40-51,
+    nearest_center_to_agg's columns, graph.py:56-86) as the oracle restates it (its Bellman-Ford
+    is pinned to the reference's own output, test_oracle_golden.py); coarse_order='sorted' is
+    the same aggregates with the columns in ascending seed order. Then every level, the coarsest
+    operator and six V-cycles against the oracle's hierarchy of the same recipe."""
+    torch = torch_cuda
+    A = _matrix("c2_1024")
+    n = A.shape[0]
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=2000, aggregation="reference",
+                                     coarse_order=coarse_order)
+    C = sp.csr_matrix((1.0 / np.abs(A.data), A.indices, A.indptr), A.shape)
+    seeds, near, Agg = oracle.reference_aggregates(C, n, 0.1, 0)
+    assert np.array_equal(H.levels[0].labels.cpu().numpy().astype(np.int64), near)
+    if coarse_order == "sorted":
+        order = np.argsort(seeds)
+        seeds, Agg = seeds[order], Agg[:, order].tocsr()
+        Agg.sort_indices()
+    assert np.array_equal(H.levels[0].seeds, seeds)
+    Aggd = H.levels[0].Agg.to_scipy()
+    for arr in ("indptr", "indices", "data"):
+        assert np.array_equal(getattr(Aggd, arr), getattr(Agg, arr)), arr
+    levels, Ac = oracle.build_hierarchy(A, alpha=0.1, max_coarse=2000,
+                                        omegas=[L.omega for L in H.levels],
+                                        aggregation="reference", coarse_order=coarse_order)
+    assert len(levels) == len(H.levels)
+    for Lo, Ld in zip(levels, H.levels):
+        assert np.array_equal(Ld.seeds, Lo["seeds"])
+        for key, M in (("P", Ld.P), ("A", Ld.A)):
+            Md = M.to_scipy()
+            for arr in ("indptr", "indices", "data"):
+                assert np.array_equal(getattr(Md, arr), getattr(Lo[key], arr)), (key, arr)
+    Acd = H.Ac.to_scipy()
+    assert np.array_equal(Acd.indices, Ac.indices) and np.array_equal(Acd.data, Ac.data)
+    lv = []
+    for L in H.levels:
+        f = {k: M.get_format() for k, M in (("A", L.A), ("P", L.P), ("R", L.R))}
+        vw = {k: (v[1] if v[0] == "vector" else 0) for k, v in f.items()}
+        lv.append({"A": L.A.to_scipy(), "P": L.P.to_scipy(), "R": L.R.to_scipy(),
+                   "Dw": sp.diags(L.dinv.cpu().numpy()),
+                   "A_vw": vw["A"], "P_vw": vw["P"], "R_vw": vw["R"]})
+    x0 = np.random.RandomState(0).randn(n)
+    b = np.random.RandomState(1).randn(n)
+    xo, ho = oracle.vcycle_solve(lv, Acd, b, x0, 6)
+    xd = torch.as_tensor(x0).cuda()
+    hd = H.cycle(torch.as_tensor(b).cuda(), xd, 6)
+    assert np.allclose(hd, ho, rtol=1e-11, atol=0), (hd, ho)
+    assert np.allclose(xd.cpu().numpy(), xo, rtol=1e-9, atol=1e-11 * np.abs(xo).max())

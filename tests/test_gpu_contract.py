@@ -126,6 +126,25 @@ def test_dispatch_packet_timer(ml):
         wall_ms = (time.perf_counter() - t0) * 1e3
         assert 0.0 < ms.value < wall_ms
         assert np.array_equal(yd.cpu().numpy(), A @ x)
+    # disarm drops a timer no launch took
+    call("mlamg_timer_arm", tm)
+    call("mlamg_timer_disarm")
+    call("mlamg_spmv", Ad.handle, ptr(xd), ptr(yd), 1.0, 0.0, stream_ptr())
+    with pytest.raises(MlamgError):
+        call("mlamg_timer_elapsed_ms", tm, ctypes.byref(ms))
+    # a launch recorded into a stream capture never takes the timer
+    g = torch.cuda.CUDAGraph()
+    yd.zero_()
+    torch.cuda.synchronize()
+    call("mlamg_timer_arm", tm)
+    with torch.cuda.graph(g):
+        call("mlamg_spmv", Ad.handle, ptr(xd), ptr(yd), 1.0, 0.0, stream_ptr())
+    with pytest.raises(MlamgError):
+        call("mlamg_timer_elapsed_ms", tm, ctypes.byref(ms))
+    call("mlamg_timer_disarm")
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(yd.cpu().numpy(), A @ x)
     call("mlamg_timer_arm", tm)
     call("mlamg_timer_destroy", tm)  # disarms: the next launch must not touch the freed events
     call("mlamg_spmv", Ad.handle, ptr(xd), ptr(yd), 1.0, 0.0, stream_ptr())

@@ -337,8 +337,11 @@ def test_lloyd_aggregation(golden, ml, oracle):
 def test_lloyd_tie_rich_matches_reference(golden, callers, ml, oracle, k, case):
     """ns.lib.graph.lloyd_aggregation on tie-rich graphs — 'unit' distances (rand 0, 3) and the
     evaluation loops' default path (np.random.seed(0), olson measure, 'same', rand=0,
-    utils/common.py:51-58) — against the reference driver's own output around the pyamg-order
-    lloyd_cluster (tests/golden/reference_callers.npz): seeds, roots and AggOp bitwise."""
+    utils/common.py:51-58) — against the reference driver's output with the ORACLE's
+    pyamg-order lloyd_cluster standing in for pyamg (tests/golden/reference_callers.npz): seeds,
+    roots and AggOp bitwise. A SELF-CONSISTENCY check of the cluster kernel against its
+    restatement inside the reference driver (seeding, distance transform, AggOp assembly are
+    the reference's own code); parity with pyamg's amg_core tie-breaking is unpinned (absent)."""
     A = golden_csr(golden, k)
     if case == "olson":
         np.random.seed(0)

@@ -224,7 +224,9 @@ def test_oracle_pyamg_bellman_ford(oracle, kind):
 @pytest.mark.parametrize("case", ("unit0", "unit3", "olson"))
 def test_lloyd_tie_rich_driver(golden, oracle, k, case):
     """The oracle's pyamg-order lloyd_cluster inside its restated driver against the reference
-    driver's own output on tie-rich graphs (tests/golden/reference_callers.npz)."""
+    driver run around that same restated lloyd_cluster on tie-rich graphs
+    (tests/golden/reference_callers.npz): pins the restated DRIVER (seeding, distances, AggOp)
+    to the reference's; the cluster kernel is self-consistent only (pyamg absent: unpinned)."""
     g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "reference_callers.npz")))
     A = golden_csr(golden, k)
     if case == "olson":
