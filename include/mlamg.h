@@ -82,6 +82,9 @@ int mlamg_csr_copy_device(const mlamg_csr* A, int32_t* indptr, int32_t* indices,
                           void* stream);
 int mlamg_csr_download(const mlamg_csr* A, int32_t* indptr_host, int32_t* indices_host,
                        double* data_host);
+/* 64-bit fingerprint of the operator's rows, columns and value bits (order-independent sum of
+ * per-entry hashes; keys the format autotune's cache, no reference counterpart); syncs */
+int mlamg_csr_fingerprint(const mlamg_csr* A, uint64_t* fp_host, void* stream);
 
 /* SpMV storage/kernel of a handle (the CSR arrays always stay; formats add a device copy):
  *   CSR_STREAM  LDS-staged row blocks, lane-per-row sums in stored order (scipy's bits)
@@ -371,6 +374,10 @@ int mlamg_hier_add_level(mlamg_hier* H, const mlamg_csr* A, const double* dinv_w
                          const mlamg_csr* P, const mlamg_csr* R);
 int mlamg_hier_set_coarse(mlamg_hier* H, const mlamg_csr* A_coarse, const mlamg_dense* D);
 int mlamg_hier_set_smoothing(mlamg_hier* H, int nu_pre, int nu_post);
+/* Stop-flag test of the cycle kernels (no reference counterpart; an A/B switch): 0 (default) =
+ * tested only when mlamg_hier_vcycle has a tolerance (tol >= 0; without one nothing can raise
+ * it, so the fixed-count cycles skip the per-kernel load); 1 = tested by every launch. */
+int mlamg_hier_set_done_check(mlamg_hier* H, int always);
 /* smoother of one level: a Gauss-Seidel handle built on that level's operator (pyamg forward
  * sweep, in place; ns/lib/multigrid.py:175,184 — the reference amg_2_v), or NULL for weighted
  * Jacobi (default) */

@@ -180,6 +180,15 @@ struct mlamg_csr {
   // constant-coefficient stencils): srt_vi[e] indexes srt_vtab and srt_val is dropped
   uint8_t* srt_vi = nullptr;
   double* srt_vtab = nullptr;
+  // value codes of the sorted copy (set_format(SORTED, 2): operators with more than 256 but
+  // few distinct values, e.g. the Galerkin A_1 of a constant stencil): srt_vc[e] < srt_vck
+  // indexes srt_vtab (the srt_vck most frequent values, most frequent first); srt_vc[e] >=
+  // srt_vck is the (srt_vc[e] - srt_vck)-th of the block's exceptions in srt_vcx, which start at
+  // srt_base[8 b + 7]. srt_val is dropped.
+  uint16_t* srt_vc = nullptr;
+  double* srt_vcx = nullptr;
+  int32_t srt_vck = 0;
+  int64_t srt_vcx_n = 0;
   // optional row-pair pattern copy ("rowpat" format): every pair of rows (2i, 2i+1) is one of
   // <= 255 distinct pair patterns (the merge by column offset of the two rows' (col - row,
   // value) sequences), kept in LDS tables; the matrix stream is one byte per pair.
@@ -330,6 +339,8 @@ int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_gr
                       hipStream_t s);
 int32_t* hier_done_flag(mlamg_hier* H);
 int64_t hier_fine_rows(const mlamg_hier* H);
+// H's Krylov workspace of at least `bytes` (kept across calls, freed with H)
+int hier_workspace(mlamg_hier* H, size_t bytes, void** out);
 // coarsest solve by inner-hierarchy PCG (pcg.hip)
 int pcg_solve_impl(mlamg_pcg* C, const double* b, double* x, const int32_t* outer_done,
                    hipStream_t s);

@@ -273,7 +273,9 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
                                          (restart + 1) + 8 + std::max(hist_cap, 1));
   const size_t total = vec * (restart + 1) + 3 * vec + 3 * sizeof(double) * kGmMaxBlocks +
                        sizeof(double) * (2 * restart + 6) + 256 + small;
-  MLAMG_HIP(hipMalloc(&W.mem, total));
+  // the preconditioner hierarchy keeps the workspace across calls (a restart-100
+  // solve on a 10M-row grid would map and unmap 8 GB per call)
+  MLAMG_TRY(hier_workspace(M, total, &W.mem));
   char* p = static_cast<char*>(W.mem);
   W.V = reinterpret_cast<double*>(p);
   p += vec * (restart + 1);
@@ -297,10 +299,6 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   W.S = W.giv + 2 * restart;
   W.st = W.S + restart + 1;
   W.hist = W.st + 8;
-  struct Free {
-    void* m;
-    ~Free() { (void)hipFree(m); }
-  } guard{W.mem};
   MLAMG_HIP(hipMemsetAsync(W.ctr, 0, 64, s));
   MLAMG_TRY(hier_prepare_ext(M));  // allocates the hierarchy's flags and work buffers
   MLAMG_HIP(hipMemsetAsync(hier_done_flag(M), 0, sizeof(int32_t), s));

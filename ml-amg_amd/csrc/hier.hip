@@ -61,6 +61,15 @@ struct mlamg_hier {
   uint64_t g_epoch = 0, cg_epoch = 0;
   double* cg_res = nullptr;
   int32_t* done_host = nullptr;  // pinned copy of flags[1], polled between batches of cycles
+  // the stop flag the cycle's kernels test: flags + 1, or nullptr while a no-tolerance
+  // mlamg_hier_vcycle runs (nothing can raise it, and every kernel would otherwise start with a
+  // dependent load of it). done_check = 1 keeps it on every launch (A/B, mlamg_hier_set_done_check)
+  int32_t* cur_done = nullptr;
+  int done_check = 0;
+  // a Krylov solver's workspace (gmres.hip), kept across calls and grown on demand: at C4 a
+  // restart-100 GMRES needs 101 fine vectors (8 GB), too large for the allocation cache
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
 };
 
 
@@ -133,6 +142,7 @@ static int hier_prepare(mlamg_hier* H) {
   H->bc = take(nc);
   H->partial = take(maxblk);
   H->flags = reinterpret_cast<int32_t*>(p);
+  H->cur_done = H->flags + 1;
   MLAMG_HIP(hipMemset(H->mem, 0, total));
   // hipMemset runs on the null stream and may return before it completes: a caller on a
   // non-blocking stream (one thread per rank, csrc/comm.hip's loopback) must not race it
@@ -156,7 +166,7 @@ static int smooth(const Level& L, const double* b, double*& cur, double* other, 
 // caller's restriction kernel already wrote the first zero-guess sweep x = Dinv_w b into L.x.
 static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, hipStream_t s,
                         bool presmoothed = false) {
-  const int32_t* done = H->flags + 1;
+  const int32_t* done = H->cur_done;
   if (l == H->lv.size()) {
     MLAMG_TRY(coarse_solve(H, b, H->xc, done, s));
     *res = H->xc;
@@ -212,7 +222,7 @@ static bool fused_presmooth(const mlamg_hier* H) {
 static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, double tol,
                      hipStream_t s) {
   int32_t* counter = H->flags;
-  int32_t* done = H->flags + 1;
+  int32_t* done = H->cur_done;
   if (H->lv.empty()) {  // coarse-only hierarchy: x = A^-1 b
     MLAMG_TRY(coarse_solve(H, b, x, done, s));
     return MLAMG_OK;
@@ -263,6 +273,17 @@ namespace mlamg {
 int hier_prepare_ext(mlamg_hier* H) { return hier_prepare(H); }
 // the device flag every kernel of a cycle checks (a PCG using H as preconditioner shares it)
 int32_t* hier_done_flag(mlamg_hier* H) { return H->flags + 1; }
+int hier_workspace(mlamg_hier* H, size_t bytes, void** out) {
+  if (H->ws_bytes < bytes) {
+    if (H->ws) (void)hipFree(H->ws);  // ordered after every earlier use (cache semantics)
+    H->ws = nullptr;
+    H->ws_bytes = 0;
+    MLAMG_HIP(hipMalloc(&H->ws, bytes));
+    H->ws_bytes = bytes;
+  }
+  *out = H->ws;
+  return MLAMG_OK;
+}
 int64_t hier_fine_rows(const mlamg_hier* H) {
   return H->lv.empty() ? coarse_rows(H) : H->lv[0].n;
 }
@@ -315,6 +336,7 @@ int mlamg_hier_destroy(mlamg_hier* H) {
   if (H->cap_stream) (void)hipStreamDestroy(H->cap_stream);
   if (H->mem) (void)hipFree(H->mem);
   if (H->done_host) (void)hipHostFree(H->done_host);
+  if (H->ws) (void)hipFree(H->ws);
   delete H;
   return MLAMG_OK;
 }
@@ -376,6 +398,13 @@ int mlamg_hier_set_norm(mlamg_hier* H, int mode) {
   return MLAMG_OK;
 }
 
+int mlamg_hier_set_done_check(mlamg_hier* H, int always) {
+  MLAMG_REQUIRE(H && (always == 0 || always == 1), "always must be 0 or 1");
+  H->done_check = always;
+  hier_free_graph(H);
+  return MLAMG_OK;
+}
+
 int mlamg_hier_set_smoothing(mlamg_hier* H, int nu_pre, int nu_post) {
   MLAMG_REQUIRE(H && nu_pre >= 0 && nu_post >= 0, "invalid argument");
   H->nu_pre = nu_pre;
@@ -394,6 +423,13 @@ int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, d
   // a PCG coarse solve polls its convergence flag between iterations: cycles run eagerly
   if (H->pcg) use_graph = 0;
   MLAMG_HIP(hipMemsetAsync(H->flags, 0, 2 * sizeof(int32_t), s));
+  // no tolerance: no kernel can raise the stop flag, so none tests it (restored on return: a
+  // PCG that uses H as its preconditioner shares the flag, hier_done_flag)
+  struct DoneScope {
+    mlamg_hier* H;
+    ~DoneScope() { H->cur_done = H->flags + 1; }
+  } done_scope{H};
+  H->cur_done = (tol >= 0.0 || H->done_check || H->pcg) ? H->flags + 1 : nullptr;
   const bool fused = fused_presmooth(H) && n_cycles > 0;
   if (!H->lv.empty()) {
     Level& L = H->lv[0];

@@ -1632,11 +1632,16 @@ __device__ __forceinline__ void sum_two_rows(const double* __restrict__ p, int a
 // cache lines instead of one per row neighbourhood (the x gather, not HBM, bounds long-row
 // operators: Galerkin A_l, R = P^T). Products are written to LDS at their CSR slot and phase 2
 // sums every row in stored order, so the result is bitwise k_csr_stream's (scipy's).
-// VD: values come from a <= 256-entry dictionary (one byte per nonzero instead of eight)
+// VM: how the values are stored — 0 fp64 (8 B per nonzero); 1 a <= 256-entry dictionary (one
+// byte per nonzero, the table staged in LDS); 2 value codes (two bytes per nonzero): code c < K
+// is entry c of a global table of the operator's K most frequent values (frequency order, so the
+// hot entries share a few cache lines), c >= K the (c - K)-th exception of the block, an fp64
+// stream of the values outside the table (block b's at srt_base[8b + 7]). The products and
+// their order are those of the fp64 form, so every mode computes the same bits.
 #ifndef MLAMG_SRT_WAVES  // minimum waves per SIMD the register allocation must allow (0: free)
 #define MLAMG_SRT_WAVES 0
 #endif
-template <int OP, bool NORM, bool VD, bool LR>
+template <int OP, bool NORM, int VM, bool LR>
 __global__ __launch_bounds__(kSrtThreads)
 __attribute__((amdgpu_waves_per_eu(MLAMG_SRT_WAVES > 0 ? MLAMG_SRT_WAVES : 1, 8)))
 void k_sorted(const int32_t* __restrict__ indptr,
@@ -1644,9 +1649,13 @@ void k_sorted(const int32_t* __restrict__ indptr,
                                                         const double* __restrict__ av,
                                                         const uint8_t* __restrict__ vi,
                                                         const double* __restrict__ vtab,
+                                                        const uint16_t* __restrict__ vc,
+                                                        const double* __restrict__ vcx,
+                                                        int vck,
                                                         const int32_t* __restrict__ blk,
                                                         const int32_t* __restrict__ base,
                                                         const double* __restrict__ x, Epi ep) {
+  constexpr bool VD = VM == 1;
   __shared__ double prod[kSrtNnz];
   __shared__ int32_t rp[kSrtRows + 1];
   __shared__ double red[kSrtThreads / 64];
@@ -1670,13 +1679,16 @@ void k_sorted(const int32_t* __restrict__ indptr,
   constexpr uint32_t kNone = 0xffffffffu, kSlot = (1u << kSrtPosBits) - 1;
   uint32_t w[U];
   double vv[U], xv[U];
+  int cv[VM == 2 ? U : 1];
   {
     const size_t eb = (size_t)b * kSrtNnz + tid;
     if (ep.cached) {  // uniform: one unrolled load sequence or the other
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         w[u] = pk[eb + u * kSrtThreads];
-        if constexpr (VD)
+        if constexpr (VM == 2)
+          cv[u] = vc[eb + u * kSrtThreads];
+        else if constexpr (VD)
           vv[u] = (double)vi[eb + u * kSrtThreads];  // index for now
         else
           vv[u] = av[eb + u * kSrtThreads];
@@ -1685,18 +1697,31 @@ void k_sorted(const int32_t* __restrict__ indptr,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         w[u] = __builtin_nontemporal_load(pk + eb + u * kSrtThreads);
-        if constexpr (VD)
+        if constexpr (VM == 2)
+          cv[u] = __builtin_nontemporal_load(vc + eb + u * kSrtThreads);
+        else if constexpr (VD)
           vv[u] = (double)__builtin_nontemporal_load(vi + eb + u * kSrtThreads);  // index for now
         else
           vv[u] = __builtin_nontemporal_load(av + eb + u * kSrtThreads);
       }
     }
   }
+  if constexpr (VM == 2) {
+    // table values (cached: hot codes share lines) now; exceptions once the record is in
+#pragma unroll
+    for (int u = 0; u < U; ++u) vv[u] = (w[u] != kNone && cv[u] < vck) ? vtab[cv[u]] : 0.0;
+  }
   const int r0 = m0.x, r1 = m0.y, nr = r1 - r0;
   const int e0 = m0.z;
   // two column windows per block: sorted entries [0, split) are offsets from lo, the rest from
   // hi (a halo-extended local matrix has its ghost columns far from the owned ones)
   const int lo = m1.x, hi = m1.y, split = m1.z;
+  if constexpr (VM == 2) {
+    const int xb = m1.w - vck;  // the block's exceptions, indexed by code - K
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (w[u] != kNone && cv[u] >= vck) vv[u] = vcx[xb + cv[u]];
+  }
   constexpr int RPQ = kSrtRows / kSrtThreads + 1;  // row pointers per thread (nr + 1 <= kSrtRows + 1)
   int rpv[RPQ];
 #pragma unroll
@@ -2062,20 +2087,25 @@ static int launch(const mlamg_csr* A, const double* x, const Epi& ep_in, hipStre
   if (A->srt_pk) {
     if (A->srt_nb == 0) return MLAMG_OK;
     const bool lr = A->avg_row_len >= kSrtLongRow;
-#define MLAMG_SRT_LAUNCH(VDV, LRV)                                                              \
-  MLAMG_LAUNCH((k_sorted<OP, NORM, VDV, LRV>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s, \
-                     A->indptr, A->srt_pk, A->srt_val, A->srt_vi, A->srt_vtab, A->srt_blk,     \
-                     A->srt_base, x, ep)
+#define MLAMG_SRT_LAUNCH(VMV, LRV)                                                              \
+  MLAMG_LAUNCH((k_sorted<OP, NORM, VMV, LRV>), dim3(A->srt_nb), dim3(kSrtThreads), 0, s, \
+                     A->indptr, A->srt_pk, A->srt_val, A->srt_vi, A->srt_vtab, A->srt_vc,      \
+                     A->srt_vcx, A->srt_vck, A->srt_blk, A->srt_base, x, ep)
     if (A->srt_vi) {
       if (lr)
-        MLAMG_SRT_LAUNCH(true, true);
+        MLAMG_SRT_LAUNCH(1, true);
       else
-        MLAMG_SRT_LAUNCH(true, false);
+        MLAMG_SRT_LAUNCH(1, false);
+    } else if (A->srt_vc) {
+      if (lr)
+        MLAMG_SRT_LAUNCH(2, true);
+      else
+        MLAMG_SRT_LAUNCH(2, false);
     } else {
       if (lr)
-        MLAMG_SRT_LAUNCH(false, true);
+        MLAMG_SRT_LAUNCH(0, true);
       else
-        MLAMG_SRT_LAUNCH(false, false);
+        MLAMG_SRT_LAUNCH(0, false);
     }
 #undef MLAMG_SRT_LAUNCH
     MLAMG_HIP(hipGetLastError());
@@ -2552,6 +2582,12 @@ static void drop_sorted(mlamg_csr* A) {
   if (A->srt_val) (void)hipFree(A->srt_val);
   if (A->srt_vi) (void)hipFree(A->srt_vi);
   if (A->srt_vtab) (void)hipFree(A->srt_vtab);
+  if (A->srt_vc) (void)hipFree(A->srt_vc);
+  if (A->srt_vcx) (void)hipFree(A->srt_vcx);
+  A->srt_vc = nullptr;
+  A->srt_vcx = nullptr;
+  A->srt_vck = 0;
+  A->srt_vcx_n = 0;
   A->srt_vi = nullptr;
   A->srt_vtab = nullptr;
   A->srt_blk = nullptr;
@@ -2629,6 +2665,213 @@ static int sorted_value_dict(mlamg_csr* A, hipStream_t s) {
   return MLAMG_OK;
 }
 
+// ---------------------------------------------------------------- sorted-format value codes
+// Two-byte codes: at most kVcMaxK table entries, so that a code >= K can index any of a block's
+// (<= kSrtNnz) exceptions.
+constexpr int kVcMaxK = 65536 - kSrtNnz;
+
+__global__ void k_vc_bits(const double* __restrict__ v, int64_t n, uint64_t* __restrict__ k) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) k[i] = __double_as_longlong(v[i]);
+}
+// frequency order: key = ~count (ascending = most frequent first), payload = unique index
+__global__ void k_vc_freq_keys(const uint32_t* __restrict__ cnt, int64_t u,
+                               uint32_t* __restrict__ key, int32_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < u) {
+    key[i] = ~cnt[i];
+    idx[i] = (int32_t)i;
+  }
+}
+__global__ void k_vc_rank(const int32_t* __restrict__ order, const uint64_t* __restrict__ uniq,
+                          int64_t u, int k, int32_t* __restrict__ rank, double* __restrict__ tab) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p < u) {
+    rank[order[p]] = (int32_t)p;
+    if (p < k) tab[p] = __longlong_as_double(uniq[order[p]]);
+  }
+}
+__device__ __forceinline__ int32_t vc_rank_of(double v, const uint64_t* __restrict__ uniq,
+                                              int64_t u, const int32_t* __restrict__ rank) {
+  const uint64_t key = __double_as_longlong(v);
+  int64_t lo = 0, hi = u - 1;  // the value is present: binary search of its bit pattern
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (uniq[mid] < key)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return rank[lo];
+}
+// per block: the number of its entries outside the table
+__global__ __launch_bounds__(256) void k_vc_count(const double* __restrict__ v,
+                                                  const int32_t* __restrict__ meta,
+                                                  const uint64_t* __restrict__ uniq, int64_t u,
+                                                  const int32_t* __restrict__ rank, int k,
+                                                  int32_t* __restrict__ cnt) {
+  __shared__ int32_t c;
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) c = 0;
+  __syncthreads();
+  const int e0 = meta[8 * b + 2], ne = meta[8 * b + 3];
+  int mine = 0;
+  for (int e = threadIdx.x; e < ne; e += 256) mine += vc_rank_of(v[e0 + e], uniq, u, rank) >= k;
+  if (mine) atomicAdd(&c, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[b] = c;
+}
+// per block, entries in stored order: code = rank (< k) or k + the entry's exception index in
+// the block (a block-wide exclusive count, so the layout is deterministic); exceptions to
+// x[xbase[b] + index]; meta[8 b + 7] = xbase[b]
+__global__ __launch_bounds__(256) void k_vc_encode(const double* __restrict__ v,
+                                                   int32_t* __restrict__ meta,
+                                                   const uint64_t* __restrict__ uniq, int64_t u,
+                                                   const int32_t* __restrict__ rank, int k,
+                                                   const int32_t* __restrict__ xbase,
+                                                   uint16_t* __restrict__ code,
+                                                   double* __restrict__ xv) {
+  __shared__ int32_t wsum[4];
+  const int b = blockIdx.x;
+  const int e0 = meta[8 * b + 2], ne = meta[8 * b + 3];
+  const int xb = xbase[b];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int run = 0;  // exceptions before this chunk
+  for (int c0 = 0; c0 < ne; c0 += 256) {
+    const int e = c0 + (int)threadIdx.x;
+    double val = 0.0;
+    int32_t r = 0;
+    if (e < ne) {
+      val = v[e0 + e];
+      r = vc_rank_of(val, uniq, u, rank);
+    }
+    const bool exc = e < ne && r >= k;
+    const uint64_t m = __ballot(exc);
+    const int before_in_wave = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wv] = __popcll(m);
+    __syncthreads();
+    int before = run + before_in_wave;
+    for (int q = 0; q < wv; ++q) before += wsum[q];
+    if (e < ne) {
+      if (exc) {
+        code[e0 + e] = (uint16_t)(k + before);
+        xv[xb + before] = val;
+      } else {
+        code[e0 + e] = (uint16_t)r;
+      }
+    }
+    run += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) meta[8 * b + 7] = xb;
+}
+
+// Replace the sorted copy's fp64 values by two-byte value codes (layout above). EUNSUPPORTED
+// (nothing changed) when the operator has <= 256 distinct values (the dictionary is smaller) or
+// when the codes would not pay: more than a quarter of the entries outside the table.
+static int sorted_value_codes(mlamg_csr* A, hipStream_t s) {
+  const int64_t nnz = A->nnz;
+  const int nb = A->srt_nb;
+  if (!A->srt_val || nnz == 0 || nb == 0) return MLAMG_EUNSUPPORTED;
+  if (nnz >= (int64_t(1) << 31)) return MLAMG_EUNSUPPORTED;
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  uint32_t *cnt = nullptr, *fk0 = nullptr, *fk1 = nullptr;
+  int32_t *fi0 = nullptr, *fi1 = nullptr, *rank = nullptr, *bcnt = nullptr, *xbase = nullptr;
+  uint32_t* nruns = nullptr;
+  void* tmp = nullptr;
+  uint16_t* code = nullptr;
+  double *tab = nullptr, *xv = nullptr;
+  int rc = MLAMG_OK;
+  const unsigned g = (unsigned)((nnz + 255) / 256);
+  auto ok = [&](hipError_t e) {
+    if (e != hipSuccess && rc == MLAMG_OK) {
+      set_error(std::string("sorted value codes: ") + hipGetErrorString(e));
+      rc = MLAMG_EHIP;
+    }
+    return rc == MLAMG_OK;
+  };
+  size_t tb = 0, tb2 = 0;
+  uint32_t u32 = 0;
+  int64_t u = 0;
+  if (ok(hipMalloc(&k0, sizeof(uint64_t) * nnz)) && ok(hipMalloc(&k1, sizeof(uint64_t) * nnz)) &&
+      ok(hipMalloc(&cnt, sizeof(uint32_t) * nnz)) && ok(hipMalloc(&nruns, sizeof(uint32_t)))) {
+    hipLaunchKernelGGL(k_vc_bits, dim3(g), dim3(256), 0, s, A->srt_val, nnz, k0);
+    ok(hipGetLastError());
+    ok(rocprim::radix_sort_keys(nullptr, tb, k0, k1, (size_t)nnz, 0, 64, s));
+    ok(rocprim::run_length_encode(nullptr, tb2, k1, (unsigned)nnz, k0, cnt, nruns, s));
+    if (ok(hipMalloc(&tmp, std::max(tb, tb2) + 16))) {
+      ok(rocprim::radix_sort_keys(tmp, tb, k0, k1, (size_t)nnz, 0, 64, s));  // k1 sorted
+      ok(rocprim::run_length_encode(tmp, tb2, k1, (unsigned)nnz, k0, cnt, nruns, s));  // k0 uniq
+      ok(hipMemcpyAsync(&u32, nruns, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      ok(hipStreamSynchronize(s));
+    }
+  }
+  u = u32;
+  if (rc == MLAMG_OK && u <= 256) rc = MLAMG_EUNSUPPORTED;  // the dictionary applies
+  const int k = (int)std::min<int64_t>(u, kVcMaxK);
+  if (rc == MLAMG_OK) {
+    const unsigned gu = (unsigned)((u + 255) / 256);
+    if (ok(hipMalloc(&fk0, sizeof(uint32_t) * u)) && ok(hipMalloc(&fk1, sizeof(uint32_t) * u)) &&
+        ok(hipMalloc(&fi0, sizeof(int32_t) * u)) && ok(hipMalloc(&fi1, sizeof(int32_t) * u)) &&
+        ok(hipMalloc(&rank, sizeof(int32_t) * u)) && ok(hipMalloc(&tab, sizeof(double) * k))) {
+      hipLaunchKernelGGL(k_vc_freq_keys, dim3(gu), dim3(256), 0, s, cnt, u, fk0, fi0);
+      ok(hipGetLastError());
+      size_t tb3 = 0;
+      ok(rocprim::radix_sort_pairs(nullptr, tb3, fk0, fk1, fi0, fi1, (size_t)u, 0, 32, s));
+      if (tb3 > std::max(tb, tb2) + 16) {
+        (void)hipFree(tmp);
+        tmp = nullptr;
+        ok(hipMalloc(&tmp, tb3 + 16));
+      }
+      if (rc == MLAMG_OK) {
+        ok(rocprim::radix_sort_pairs(tmp, tb3, fk0, fk1, fi0, fi1, (size_t)u, 0, 32, s));
+        hipLaunchKernelGGL(k_vc_rank, dim3(gu), dim3(256), 0, s, fi1, k0, u, k, rank, tab);
+        ok(hipGetLastError());
+      }
+    }
+  }
+  int32_t n_exc = 0;
+  if (rc == MLAMG_OK && ok(hipMalloc(&bcnt, sizeof(int32_t) * (nb + 1))) &&
+      ok(hipMalloc(&xbase, sizeof(int32_t) * (nb + 1)))) {
+    hipLaunchKernelGGL(k_vc_count, dim3(nb), dim3(256), 0, s, A->srt_val, A->srt_base, k0, u,
+                       rank, k, bcnt);
+    ok(hipGetLastError());
+    if (rc == MLAMG_OK) rc = exclusive_scan_i32(bcnt, xbase, nb, s);
+    if (rc == MLAMG_OK) {
+      ok(hipMemcpyAsync(&n_exc, xbase + nb, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      ok(hipStreamSynchronize(s));
+    }
+  }
+  if (rc == MLAMG_OK && 4 * (int64_t)n_exc > nnz) {
+    set_error("sorted value codes: more than a quarter of the entries outside the table");
+    rc = MLAMG_EUNSUPPORTED;
+  }
+  if (rc == MLAMG_OK && ok(hipMalloc(&code, sizeof(uint16_t) * nnz)) &&
+      ok(hipMalloc(&xv, sizeof(double) * std::max<int32_t>(n_exc, 1)))) {
+    hipLaunchKernelGGL(k_vc_encode, dim3(nb), dim3(256), 0, s, A->srt_val, A->srt_base, k0, u,
+                       rank, k, xbase, code, xv);
+    ok(hipGetLastError());
+    ok(hipStreamSynchronize(s));
+  }
+  for (void* p : {(void*)k0, (void*)k1, (void*)cnt, (void*)fk0, (void*)fk1, (void*)fi0,
+                  (void*)fi1, (void*)rank, (void*)bcnt, (void*)xbase, (void*)nruns, tmp})
+    if (p) (void)hipFree(p);
+  if (rc != MLAMG_OK) {
+    if (code) (void)hipFree(code);
+    if (tab) (void)hipFree(tab);
+    if (xv) (void)hipFree(xv);
+    return rc;
+  }
+  (void)hipFree(A->srt_val);
+  A->srt_val = nullptr;
+  A->srt_vc = code;
+  A->srt_vtab = tab;
+  A->srt_vcx = xv;
+  A->srt_vck = k;
+  A->srt_vcx_n = n_exc;
+  return MLAMG_OK;
+}
+
 // Fixed-stride layout of the sorted copy: block b's entries at [b * kSrtNnz, (b + 1) * kSrtNnz),
 // padded with `pad` (kNone codes, zero values): the kernel's entry loads then need no block
 // record (e0, ne) and issue at launch, in parallel with the record load, instead of one memory
@@ -2663,7 +2906,7 @@ static int pad_stream(T** arr, int nb, const int32_t* meta, T pad, hipStream_t s
 // (block, column) (stable, so equal columns keep CSR order; any order would give the same bits).
 // EUNSUPPORTED (A unchanged) if a row is longer than kSrtNnz or a block's columns do not fit
 // two windows of 2^20.
-static int build_sorted(mlamg_csr* A, hipStream_t s) {
+static int build_sorted(mlamg_csr* A, hipStream_t s, int value_mode = 0) {
   drop_sorted(A);
   const int64_t n = A->n_rows, nnz = A->nnz;
   std::vector<int32_t> ip(n + 1);
@@ -2755,10 +2998,19 @@ static int build_sorted(mlamg_csr* A, hipStream_t s) {
   A->srt_nb = nb;
   A->n_part = nb;
   (void)sorted_value_dict(A, s);  // optional: keeps the fp64 values when it does not apply
+  if (value_mode == 2 && !A->srt_vi) {
+    // value codes asked for: refused (EUNSUPPORTED, the format dropped) where they do not apply
+    rc = sorted_value_codes(A, s);
+    if (rc != MLAMG_OK) {
+      drop_sorted(A);
+      return rc;
+    }
+  }
   rc = pad_stream<uint32_t>(&A->srt_pk, nb, A->srt_base, 0xffffffffu, s);
   if (rc == MLAMG_OK)
-    rc = A->srt_vi ? pad_stream<uint8_t>(&A->srt_vi, nb, A->srt_base, (uint8_t)0, s)
-                   : pad_stream<double>(&A->srt_val, nb, A->srt_base, 0.0, s);
+    rc = A->srt_vi   ? pad_stream<uint8_t>(&A->srt_vi, nb, A->srt_base, (uint8_t)0, s)
+         : A->srt_vc ? pad_stream<uint16_t>(&A->srt_vc, nb, A->srt_base, (uint16_t)0, s)
+                     : pad_stream<double>(&A->srt_val, nb, A->srt_base, 0.0, s);
   if (rc != MLAMG_OK) drop_sorted(A);
   return rc;
 }
@@ -3523,8 +3775,11 @@ int mlamg_csr_set_format(mlamg_csr* A, int fmt, int vec_width, void* stream) {
       drop_long(A);
       return build_sell_dict(A, s, vec_width > 1 ? vec_width : 1);
     case MLAMG_FMT_SORTED: {
-      // built first, so an unsupported matrix keeps its current format
-      MLAMG_TRY(build_sorted(A, s));
+      // built first, so an unsupported matrix keeps its current format (vec_width 2: fp64
+      // values replaced by two-byte value codes, EUNSUPPORTED where they do not apply)
+      MLAMG_REQUIRE(vec_width == 0 || vec_width == 1 || vec_width == 2,
+                    "sorted: vec_width must be 0/1 (values or dictionary) or 2 (value codes)");
+      MLAMG_TRY(build_sorted(A, s, vec_width));
       drop_rowpat(A);
       drop_sell(A);
       drop_long(A);
@@ -3609,8 +3864,9 @@ int mlamg_csr_format_bytes(const mlamg_csr* A, double* bytes) {
   } else if (A->rp_pid) {
     b += 1.0 * ((A->n_rows + 1) / 2) + 4.0 * 257 + 32.0 * A->rp_n_ent;  // pair ids + tables
   } else if (A->srt_pk) {
-    b += (A->srt_vi ? 5.0 : 12.0) * (double)kSrtNnz * A->srt_nb + 4.0 * (n + 1) +
-         32.0 * A->srt_nb;  // the padded fixed-stride stream
+    b += (A->srt_vi ? 5.0 : A->srt_vc ? 6.0 : 12.0) * (double)kSrtNnz * A->srt_nb +
+         4.0 * (n + 1) + 32.0 * A->srt_nb;  // the padded fixed-stride stream
+    if (A->srt_vc) b += 8.0 * (double)A->srt_vcx_n + 8.0 * A->srt_vck;  // exceptions + table
   } else if (A->dict_code) {
     int64_t n_codes = 0;
     MLAMG_HIP(hipMemcpy(&n_codes, A->dict_ptr + A->n_slices, sizeof(int64_t), hipMemcpyDeviceToHost));
@@ -3693,7 +3949,7 @@ int mlamg_csr_get_format(const mlamg_csr* A, int* fmt, int* vec_width, int64_t* 
   if (vec_width)
     *vec_width = A->vec_width ? A->vec_width
                  : A->rp_pid  ? A->rp_n_pat
-                 : A->srt_pk  ? (A->srt_vi ? 1 : 0)
+                 : A->srt_pk  ? (A->srt_vi ? 1 : A->srt_vc ? 2 : 0)
                               : A->sell_sigma;
   if (stored) *stored = A->sell_ptr ? A->sell_elems : A->nnz;
   return MLAMG_OK;

@@ -227,3 +227,55 @@ int count_out_of_range(const int32_t* a, int64_t n, int64_t lo, int64_t hi, hipS
   return MLAMG_OK;
 }
 }  // namespace mlamg
+
+// ---------------------------------------------------------------- operator fingerprint
+// 64-bit fingerprint of a CSR operator (rows, columns, value bits, per-entry position): the sum
+// mod 2^64 of a splitmix64 mix of every (row, row length) and (entry, column, value bits) —
+// addition commutes, so the result does not depend on the launch geometry. Keys the format
+// autotune's cache (mlamg/hierarchy.py): an operator rebuilt with the same entries reuses its
+// timing decision.
+namespace mlamg {
+__device__ __forceinline__ uint64_t fp_mix(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void k_csr_fp(const int32_t* __restrict__ ip,
+                                                const int32_t* __restrict__ ij,
+                                                const double* __restrict__ v, int64_t n,
+                                                int64_t nnz, unsigned long long* __restrict__ out) {
+  uint64_t h = 0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+    h += fp_mix(((uint64_t)i << 32) ^ (uint64_t)(uint32_t)(ip[i + 1] - ip[i]) ^ 0x5555ull);
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nnz; e += stride)
+    h += fp_mix(fp_mix(((uint64_t)e << 32) ^ (uint64_t)(uint32_t)ij[e]) ^
+                (uint64_t)__double_as_longlong(v[e]));
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)h);
+}
+}  // namespace mlamg
+
+extern "C" int mlamg_csr_fingerprint(const mlamg_csr* A, uint64_t* fp_host, void* stream) {
+  using namespace mlamg;
+  MLAMG_REQUIRE(A && fp_host, "NULL argument");
+  hipStream_t s = S(stream);
+  unsigned long long* d = nullptr;
+  MLAMG_HIP(hipMalloc(&d, sizeof(unsigned long long)));
+  unsigned long long h = 0;
+  hipError_t e = hipMemsetAsync(d, 0, sizeof(unsigned long long), s);
+  if (e == hipSuccess) {
+    const int64_t m = std::max<int64_t>(A->n_rows, A->nnz);
+    const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>((m + 255) / 256, 1), 4096);
+    hipLaunchKernelGGL(k_csr_fp, dim3(g), dim3(256), 0, s, A->indptr, A->indices, A->data,
+                       A->n_rows, A->nnz, d);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(d);
+  MLAMG_HIP(e);
+  *fp_host = (uint64_t)h ^ ((uint64_t)A->n_cols * 0x9e3779b97f4a7c15ull);
+  return MLAMG_OK;
+}

@@ -83,6 +83,7 @@ SIGNATURES = {
     "mlamg_csr_destroy": (c_int, [c_vp]),
     "mlamg_csr_shape": (c_int, [c_vp, P_i64, P_i64, P_i64]),
     "mlamg_csr_device_arrays": (c_int, [c_vp, c_vpp, c_vpp, c_vpp]),
+    "mlamg_csr_fingerprint": (c_int, [c_vp, ctypes.POINTER(ctypes.c_uint64), c_vp]),
     "mlamg_csr_download": (c_int, [c_vp, c_vp, c_vp, c_vp]),
     "mlamg_csr_copy_device": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mlamg_csr_set_format": (c_int, [c_vp, c_int, c_int, c_vp]),
@@ -159,6 +160,7 @@ SIGNATURES = {
                             c_vp, c_int, c_vp]),
     "mlamg_csr_symmetric": (c_int, [c_vp, c_dbl, P_int, c_vp]),
     "mlamg_hier_set_smoothing": (c_int, [c_vp, c_int, c_int]),
+    "mlamg_hier_set_done_check": (c_int, [c_vp, c_int]),
     "mlamg_hier_set_level_smoother": (c_int, [c_vp, c_int, c_vp]),
     "mlamg_hier_set_norm": (c_int, [c_vp, c_int]),
     "mlamg_hier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_int, c_vp]),

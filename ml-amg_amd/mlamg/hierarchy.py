@@ -175,7 +175,7 @@ class Hierarchy:
         return H
 
     EXACT_CANDIDATES = (("csr_stream", 0), ("sell", 1), ("sell", 512), ("sorted", 0),
-                        ("sell_dict", 1), ("sell_dict", 512), ("rowpat", 0))
+                        ("sorted", 2), ("sell_dict", 1), ("sell_dict", 512), ("rowpat", 0))
     LONG_CANDIDATES = (("long", 0),)
     VECTOR_CANDIDATES = (("vector", 64), ("vector", 128), ("vector", 256), ("vector", 512))
 
@@ -242,6 +242,19 @@ class Hierarchy:
     # 34 us) up and lose below (A_2, 187 per row: 79 vs 54 us).
     VEC_MIN_MEAN_ROW = 256
 
+    # autotune decisions per operator signature (kind, shape, nnz, fingerprint of rows, columns
+    # and value bits, candidate family): a hierarchy rebuilt on the same operator (a dataset loop
+    # re-solving one grid, a distributed rank rebuilding rank 0's hierarchy) takes the same
+    # kernel without re-timing (VERDICT r04 Next #7). The choice is a timing decision only —
+    # every candidate of a family computes the same bits — so a stale entry costs speed, never
+    # a result. Bounded; cleared by clear_tune_cache().
+    _TUNE_CACHE = {}
+    TUNE_CACHE_MAX = 256
+
+    @classmethod
+    def clear_tune_cache(cls):
+        cls._TUNE_CACHE.clear()
+
     def apply_formats(self, fine_format="autotune", coarse_format="auto", vec_min_row=None):
         """Choose the SpMV kernel of every operator.
 
@@ -277,6 +290,13 @@ class Hierarchy:
                     M.set_format(fine_format if fine_format != "vector" else "auto_exact")
                     row[name] = {"chosen": M.get_format()[:2]}
                     continue
+                key = (name, M.shape, M.nnz, M.fingerprint(), tuple(cands))
+                hit = self._TUNE_CACHE.get(key)
+                if hit is not None:
+                    fmt, arg = hit["chosen"].split("/")
+                    M.set_format(fmt, int(arg))
+                    row[name] = dict(hit, cached=True)
+                    continue
                 x = torch.randn(M.shape[1], dtype=torch.float64, device=dev)
                 y = torch.zeros(M.shape[0], dtype=torch.float64, device=dev)
                 times = {}
@@ -301,6 +321,9 @@ class Hierarchy:
                 M.set_format(fmt, int(arg))
                 row[name] = {"chosen": best, "us": {k: round(v, 2) for k, v in times.items()},
                              "pruned": pruned}
+                if len(self._TUNE_CACHE) >= self.TUNE_CACHE_MAX:
+                    self._TUNE_CACHE.pop(next(iter(self._TUNE_CACHE)))
+                self._TUNE_CACHE[key] = row[name]
             self.tuning.append(row)
         self.attach_dinvs()
 

@@ -178,6 +178,12 @@ class DeviceCSR:
         name = {v: k for k, v in self.FORMATS.items()}[f.value]
         return name, int(vw.value), int(st.value)
 
+    def fingerprint(self):
+        """64-bit fingerprint of the rows, columns and value bits (mlamg_csr_fingerprint)."""
+        v = ctypes.c_uint64()
+        call("mlamg_csr_fingerprint", self.handle, ctypes.byref(v), stream_ptr())
+        return int(v.value)
+
     def format_bytes(self):
         """Algorithmic HBM bytes of one y = A@x in the active storage format."""
         b = ctypes.c_double()

@@ -315,6 +315,70 @@ def test_sorted_value_dictionary(ml, torch_cuda):
     assert np.array_equal(Qd.matvec(dev(torch, q)).cpu().numpy(), Q @ q)
 
 
+def test_sorted_value_codes(ml, torch_cuda):
+    """sorted format with two-byte value codes (set_format('sorted', 2)): a Galerkin A_1 of a
+    constant stencil (more than 256 but few distinct values, all in the table) and a skewed
+    operator with more distinct values than the table holds (the tail stored as per-block
+    exceptions; 80k distinct values, 15 % of the entries outside the table) — every epilogue
+    bitwise the fp64 form (scipy's order); refused (EUNSUPPORTED, plain fp64 kept out of the
+    autotune's way) where the table would miss more than a quarter of the entries or a
+    dictionary applies."""
+    torch = torch_cuda
+    from mlamg._lib import MLAMG_EUNSUPPORTED, MlamgError, call, ptr, stream_ptr
+    rs = np.random.RandomState(12)
+    A = ml.problems.poisson_3d_7pt(40)
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=500, fine_format="csr_stream",
+                                     finalize=False)
+    A1 = H.levels[1].A.to_scipy()
+    assert 256 < len(np.unique(A1.data)) < 61440
+    # skewed: 85 % of the entries from 300 values, the rest (~80k) all distinct
+    n = 40000
+    Q = sp.random(n, n, density=2.5e-3, random_state=rs, format="csr") + sp.eye(n, format="csr")
+    Q = Q.tocsr()
+    Q.sort_indices()
+    common = rs.randn(300)
+    pick = rs.rand(Q.nnz) < 0.85
+    Q.data[pick] = common[rs.randint(0, 300, pick.sum())]
+    Q.data[~pick] = rs.randn((~pick).sum())
+    assert len(np.unique(Q.data)) > 61440
+    for M in (A1, Q):
+        Md = ml.sparse.DeviceCSR.from_scipy(M).set_format("sorted", 2)
+        assert Md.get_format()[:2] == ("sorted", 2)
+        Mf = ml.sparse.DeviceCSR.from_scipy(M).set_format("sorted", 0)
+        assert Md.format_bytes() < Mf.format_bytes()
+        m = M.shape[0]
+        x, b, e = rs.randn(m), rs.randn(m), rs.randn(m)
+        xd, bd = dev(torch, x), dev(torch, b)
+        assert np.array_equal(Md.matvec(xd).cpu().numpy(), M @ x)
+        r = torch.empty_like(bd)
+        nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
+        call("mlamg_residual", Md.handle, ptr(bd), ptr(xd), ptr(r), ptr(nrm), stream_ptr())
+        assert np.array_equal(r.cpu().numpy(), b - M @ x)
+        y = dev(torch, e)
+        call("mlamg_prolong_add", Md.handle, ptr(xd), ptr(y), stream_ptr())
+        assert np.array_equal(y.cpu().numpy(), e + M @ x)
+    # too many values outside any 61,440-entry table: refused
+    W = sp.random(3000, 3000, density=0.02, random_state=rs, format="csr")
+    with pytest.raises(MlamgError) as ex:
+        ml.sparse.DeviceCSR.from_scipy(W).set_format("sorted", 2)
+    assert ex.value.code == MLAMG_EUNSUPPORTED
+    # <= 256 values: the one-byte dictionary, as format 'sorted'
+    P = H.levels[0].P.to_scipy()
+    with pytest.raises(MlamgError):
+        ml.sparse.DeviceCSR.from_scipy(P).set_format("sorted", 2)
+    # in a hierarchy: the autotune may pick it; the cycle is the fp64 format's bit for bit
+    H2 = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=500, fine_format="csr_stream",
+                                      coarse_format="exact")
+    x0 = rs.randn(A.shape[0])
+    b0 = rs.randn(A.shape[0])
+    x1 = dev(torch, x0)
+    h1 = H2.cycle(dev(torch, b0), x1, 3)
+    H2.levels[1].A.set_format("sorted", 2)
+    x2 = dev(torch, x0)
+    h2 = H2.cycle(dev(torch, b0), x2, 3)
+    assert np.array_equal(h1, h2) and torch.equal(x1, x2)
+
+
 def test_graph_recaptured_after_format_change(ml, torch_cuda):
     """A captured cycle graph bakes in kernels and format arrays: changing an operator's format
     must force a re-capture (format epoch), and the iterate stays bitwise the same."""
@@ -476,8 +540,8 @@ def test_c4_full_size_properties(ml, oracle, torch_cuda):
 
 @pytest.mark.slow
 def test_c4_full_size_hierarchy_parity(ml, oracle, torch_cuda):
-    """C4 (216^3, the bench configuration) at full size: the device hierarchy vs the oracle's
-    build_hierarchy given the device's omegas — every level's seeds, P and A, and the coarsest
+    """C4 (216^3, the bench configuration, aggregation='reference' as bench.py) at full size: the
+    device hierarchy vs the oracle's build_hierarchy given the device's omegas — every level's seeds, P and A, and the coarsest
     matrix bitwise (the SpGEMM / SA / Bellman-Ford kernels reproduce scipy's results at 70 M
     nonzeros) — then 4 V-cycles of the device executor vs the oracle's cycle on the ORACLE's
     operators (each operator summed in the device kernel's order: scipy order for every exact
@@ -488,10 +552,14 @@ def test_c4_full_size_hierarchy_parity(ml, oracle, torch_cuda):
     import gc
     torch = torch_cuda
     A = ml.problems.poisson_3d_7pt(216)
-    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, strength_mode="invabs", max_coarse=2000)
+    # the bench's aggregation (bench.py defaults): level 0 by the reference's push-order
+    # Bellman-Ford from unsorted seeds (ns/lib/graph.py:40-51), relabelled in seed order
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, strength_mode="invabs", max_coarse=2000,
+                                     aggregation="reference", coarse_order="sorted")
     assert H.n_levels == 5
     levels, Ac = oracle.build_hierarchy(A, alpha=0.1, strength_mode="invabs", max_coarse=2000,
-                                        omegas=[L.omega for L in H.levels])
+                                        omegas=[L.omega for L in H.levels],
+                                        aggregation="reference", coarse_order="sorted")
     assert len(levels) == len(H.levels)
     for l, (Lo, Ld) in enumerate(zip(levels, H.levels)):
         assert np.array_equal(Ld.seeds, Lo["seeds"]), l
@@ -773,3 +841,31 @@ def test_supplied_aggregates_and_prolongator(ml, oracle, torch_cuda):
     assert np.array_equal(P2.data, P_ref.data) and np.array_equal(P2.indices, P_ref.indices)
     with pytest.raises(ValueError):
         ml.hierarchy.Hierarchy.build(A, aggregates=labels[:-1])
+
+
+def test_autotune_cache_reuses_decisions(ml, torch_cuda):
+    """The format autotune keeps its decision per operator fingerprint (rows, columns, value
+    bits): a hierarchy rebuilt on the same operator takes the same kernels without re-timing
+    (VERDICT r04 Next #7), and an operator with one value changed is timed afresh."""
+    torch = torch_cuda
+    H_ = ml.hierarchy.Hierarchy
+    H_.clear_tune_cache()
+    A = ml.problems.poisson_2d_5pt(200)
+    H1 = H_.build(A, alpha=0.1, max_coarse=300)
+    assert not any(r.get("cached") for row in H1.tuning for r in row.values())
+    H2 = H_.build(A, alpha=0.1, max_coarse=300)
+    assert all(r.get("cached") for row in H2.tuning for r in row.values())
+    assert H1.formats() == H2.formats()
+    assert H2.timings["formats"] < H1.timings["formats"]
+    b = torch.zeros(A.shape[0], dtype=torch.float64, device="cuda")
+    x0 = np.random.RandomState(0).randn(A.shape[0])
+    h1 = H1.cycle(b, dev(torch, x0), 4)
+    h2 = H2.cycle(b, dev(torch, x0), 4)
+    assert np.array_equal(h1, h2)
+    A2 = A.copy()
+    A2.data[0] *= 1.0 + 2.0 ** -40
+    H3 = H_.build(A2, alpha=0.1, max_coarse=300)
+    assert not H3.tuning[0]["A"].get("cached")
+    Ad = ml.sparse.DeviceCSR.from_scipy(A)
+    assert Ad.fingerprint() == ml.sparse.DeviceCSR.from_scipy(A).fingerprint()
+    assert Ad.fingerprint() != ml.sparse.DeviceCSR.from_scipy(A2).fingerprint()

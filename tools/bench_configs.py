@@ -39,6 +39,11 @@ def main():
     ap.add_argument("--cpu-cycles", type=int, default=5)
     ap.add_argument("--only", default="")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "configs.json"))
+    ap.add_argument("--aggregation", default="reference", choices=("reference", "bellman_ford"))
+    ap.add_argument("--done-ab", action="store_true",
+                    help="also time every config with the per-kernel stop-flag test forced on "
+                         "(mlamg_hier_set_done_check 1; interleaved with the default)")
+    ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
     from mlamg.hierarchy import Hierarchy
     from bench import cpu_baseline
@@ -48,7 +53,8 @@ def main():
             continue
         A = make()
         n = A.shape[0]
-        H = Hierarchy.build(A, alpha=0.1, max_coarse=max_coarse)
+        H = Hierarchy.build(A, alpha=0.1, max_coarse=max_coarse, aggregation=args.aggregation,
+                            coarse_order="sorted")
         x0 = np.random.RandomState(0).randn(n)
         x0 /= np.linalg.norm(x0)
         b = torch.zeros(n, dtype=torch.float64, device="cuda")
@@ -56,11 +62,32 @@ def main():
         hist = H.cycle(b, x, 10)
         H.cycle_async(b, x, 5)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        H.cycle_async(b, x, args.steps)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / args.steps
-        cps, _, _ = cpu_baseline(H, np.zeros(n), x0, args.cpu_cycles)
+        from mlamg._lib import call
+
+        def timed():
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            H.cycle_async(b, x, args.steps)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / args.steps
+
+        ab = {}
+        if args.done_ab:
+            # interleaved A/B, best of 3 each (same hierarchy, same graph shape)
+            ts = {0: [], 1: []}
+            for _ in range(3):
+                for mode in (1, 0):
+                    call("mlamg_hier_set_done_check", H.handle, mode)
+                    H.cycle_async(b, x, 3)
+                    ts[mode].append(timed())
+            call("mlamg_hier_set_done_check", H.handle, 0)
+            ab = {"done_check_always_ms": round(min(ts[1]) * 1e3, 4),
+                  "done_check_notol_ms": round(min(ts[0]) * 1e3, 4)}
+            dt = min(ts[0])
+        else:
+            dt = timed()
+        cps = (float("nan") if args.no_cpu
+               else cpu_baseline(H, np.zeros(n), x0, args.cpu_cycles)[0])
         row = {"config": key, "workload": desc, "n": n, "nnz": int(A.nnz),
                "levels": H.n_levels, "operator_complexity": round(H.operator_complexity(), 3),
                "setup_s": round(H.timings["total"], 3), "gpu_vcycles_per_s": round(1 / dt, 2),
@@ -70,7 +97,8 @@ def main():
                "conv_factor_10cycles": round(float((hist[-1] / hist[-4]) ** (1 / 3)), 5),
                "cpu_vcycles_per_s_1thread": round(cps, 3),
                "gpu_over_cpu": round((1 / dt) / cps, 1),
-               "formats": [{k: v[0] for k, v in f.items()} for f in H.formats()]}
+               "formats": [{k: v[0] for k, v in f.items()} for f in H.formats()],
+               "aggregation": args.aggregation, **ab}
         print(json.dumps(row), flush=True)
         rows.append(row)
         del H
