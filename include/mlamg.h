@@ -378,6 +378,14 @@ int mlamg_hier_set_smoothing(mlamg_hier* H, int nu_pre, int nu_post);
  * tested only when mlamg_hier_vcycle has a tolerance (tol >= 0; without one nothing can raise
  * it, so the fixed-count cycles skip the per-kernel load); 1 = tested by every launch. */
 int mlamg_hier_set_done_check(mlamg_hier* H, int always);
+/* Opt-in factored prolongation at `level` (VERDICT r04 Next #5; not bitwise the explicit P):
+ * x += t - dinv_w .* (A t), t = Agg e (t_i = e[agg[i]], 0 where agg[i] < 0), i.e. x += P e for
+ * the SA prolongator P = (I - w D^-1 A) Agg without streaming P. A_uni: the level's operator in
+ * the uniform row-pair format (EUNSUPPORTED otherwise; dinv_w = w / a_ii may be attached to it
+ * with mlamg_csr_attach_dinv); agg (DEVICE, n) the aggregate column of each row; NULL A_uni
+ * restores x += P e. */
+int mlamg_hier_set_factored_prolong(mlamg_hier* H, int level, const mlamg_csr* A_uni,
+                                    const int32_t* agg, const double* dinv_w);
 /* smoother of one level: a Gauss-Seidel handle built on that level's operator (pyamg forward
  * sweep, in place; ns/lib/multigrid.py:175,184 — the reference amg_2_v), or NULL for weighted
  * Jacobi (default) */
@@ -452,6 +460,8 @@ int mlamg_hier_set_norm(mlamg_hier* H, int mode);
  * first cycle with ||r|| <= tol (MLAMG.py:194; tol = 0 stops on an exactly zero norm, like the
  * reference's `e <= tol`); tol < 0 = no tolerance. *cycles_done_host (nullable) receives the count and
  * the call syncs. use_graph != 0 replays one captured hipGraph per cycle. */
+/* b may be NULL: a zero right-hand side (every fine-level kernel takes b = +0.0 instead of
+ * reading a vector of zeros; the same bits as an all-zero b). */
 int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, double tol,
                       double* res_hist, int32_t* cycles_done_host, int use_graph, void* stream);
 /* bytes of one V-cycle with every operator priced as CSR (SURVEY.md §8(d) model): a

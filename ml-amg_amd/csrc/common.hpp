@@ -314,6 +314,8 @@ int residual_partials(const mlamg_csr* A, const double* b, const double* x, doub
 int jacobi_sweep(const mlamg_csr* A, const double* dinv, const double* b, const double* xin,
                  double* xout, bool explicit_form, const int32_t* done, hipStream_t s);
 int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s);
+int spmv_fadd(const mlamg_csr* A, const int32_t* agg, const double* e, double* y,
+              const double* dinv_w, const int32_t* done, hipStream_t s);
 int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s,
              double* smooth_x = nullptr, const double* smooth_dinv = nullptr);
 int jacobi_from_residual(double* x, const double* dinv, const double* r, int64_t n,

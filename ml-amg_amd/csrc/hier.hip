@@ -29,7 +29,18 @@ struct Level {
   double* r = nullptr;    // residual
   double* tmp = nullptr;  // ping-pong partner of x
   const mlamg_gs* gs = nullptr;  // Gauss-Seidel smoother (in place) instead of weighted Jacobi
+  // factored prolongation (opt-in, mlamg_hier_set_factored_prolong): x += t - (w D^-1) A t with
+  // t = Agg e, through fac_A (this level's A in the uniform row-pair format), instead of x += P e
+  const mlamg_csr* fac_A = nullptr;
+  const int32_t* fac_agg = nullptr;
+  const double* fac_dinv = nullptr;
 };
+
+static int prolong_add(const Level& L, const double* e, double* x, const int32_t* done,
+                       hipStream_t s) {
+  if (L.fac_A) return mlamg::spmv_fadd(L.fac_A, L.fac_agg, e, x, L.fac_dinv, done, s);
+  return mlamg::spmv_add(L.P, e, x, done, s);
+}
 }  // namespace
 
 struct mlamg_hier {
@@ -70,6 +81,9 @@ struct mlamg_hier {
   // restart-100 GMRES needs 101 fine vectors (8 GB), too large for the allocation cache
   void* ws = nullptr;
   size_t ws_bytes = 0;
+  // zero right-hand side for the paths that read b as a vector (Gauss-Seidel, coarse-only)
+  double* zero_b = nullptr;
+  bool zero_rhs = false;  // the last mlamg_hier_vcycle had b = NULL (cycle_bytes prices that)
 };
 
 
@@ -198,7 +212,7 @@ static int cycle_coarse(mlamg_hier* H, size_t l, const double* b, double** res, 
   }
   double* xn = nullptr;
   MLAMG_TRY(cycle_coarse(H, l + 1, bn, &xn, s, fuse_next));
-  MLAMG_TRY(spmv_add(L.P, xn, cur, done, s));
+  MLAMG_TRY(prolong_add(L, xn, cur, done, s));
   other = (cur == L.x) ? L.tmp : L.x;
   MLAMG_TRY(smooth(L, b, cur, other, H->nu_post, done, s));
   *res = cur;
@@ -250,7 +264,7 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
   }
   double* xn = nullptr;
   MLAMG_TRY(cycle_coarse(H, 1, bn, &xn, s, fuse_next));
-  MLAMG_TRY(spmv_add(L.P, xn, cur, done, s));
+  MLAMG_TRY(prolong_add(L, xn, cur, done, s));
   other = (cur == x) ? L.tmp : x;
   MLAMG_TRY(smooth(L, b, cur, other, H->nu_post, done, s));
   // end-of-cycle residual + norm (+ copy the iterate back into x when it sits in tmp)
@@ -337,6 +351,7 @@ int mlamg_hier_destroy(mlamg_hier* H) {
   if (H->mem) (void)hipFree(H->mem);
   if (H->done_host) (void)hipHostFree(H->done_host);
   if (H->ws) (void)hipFree(H->ws);
+  if (H->zero_b) (void)hipFree(H->zero_b);
   delete H;
   return MLAMG_OK;
 }
@@ -398,6 +413,30 @@ int mlamg_hier_set_norm(mlamg_hier* H, int mode) {
   return MLAMG_OK;
 }
 
+int mlamg_hier_set_factored_prolong(mlamg_hier* H, int level, const mlamg_csr* A_uni,
+                                    const int32_t* agg, const double* dinv_w) {
+  MLAMG_REQUIRE(H && level >= 0 && (size_t)level < H->lv.size(), "invalid level");
+  Level& L = H->lv[level];
+  if (!A_uni) {
+    L.fac_A = nullptr;
+    L.fac_agg = nullptr;
+    L.fac_dinv = nullptr;
+    hier_free_graph(H);
+    return MLAMG_OK;
+  }
+  MLAMG_REQUIRE(agg && dinv_w, "agg and dinv_w are required");
+  MLAMG_REQUIRE(A_uni->n_rows == L.n && A_uni->n_cols == L.n, "A_uni is not this level's size");
+  if (!(A_uni->rp_pid && A_uni->rp_uni.k > 0 && A_uni->rp_msk)) {
+    set_error("factored prolongation: A_uni is not in the uniform row-pair format");
+    return MLAMG_EUNSUPPORTED;
+  }
+  L.fac_A = A_uni;
+  L.fac_agg = agg;
+  L.fac_dinv = dinv_w;
+  hier_free_graph(H);
+  return MLAMG_OK;
+}
+
 int mlamg_hier_set_done_check(mlamg_hier* H, int always) {
   MLAMG_REQUIRE(H && (always == 0 || always == 1), "always must be 0 or 1");
   H->done_check = always;
@@ -415,11 +454,23 @@ int mlamg_hier_set_smoothing(mlamg_hier* H, int nu_pre, int nu_post) {
 
 int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, double tol,
                       double* res_hist, int32_t* cycles_done_host, int use_graph, void* stream) {
-  MLAMG_REQUIRE(H && b && x, "NULL argument");
+  MLAMG_REQUIRE(H && x, "NULL argument");
   MLAMG_REQUIRE(b != x, "b and x must differ");
   MLAMG_REQUIRE(n_cycles >= 0, "n_cycles < 0");
   MLAMG_TRY(hier_prepare(H));
   hipStream_t s = S(stream);
+  // b NULL: a zero right-hand side (the reference's convergence-factor problems, b = 0). The
+  // fine-level kernels then take b = +0.0 without reading a vector of zeros (the same bits:
+  // 0.0 - A x); the paths that read b as a vector get a zero buffer
+  H->zero_rhs = !b;
+  if (!b && (H->lv.empty() || H->lv[0].gs)) {
+    const int64_t n0 = hier_fine_rows(H);
+    if (!H->zero_b) {
+      MLAMG_HIP(hipMalloc(&H->zero_b, sizeof(double) * std::max<int64_t>(n0, 1)));
+      MLAMG_HIP(hipMemsetAsync(H->zero_b, 0, sizeof(double) * std::max<int64_t>(n0, 1), s));
+    }
+    b = H->zero_b;
+  }
   // a PCG coarse solve polls its convergence flag between iterations: cycles run eagerly
   if (H->pcg) use_graph = 0;
   MLAMG_HIP(hipMemsetAsync(H->flags, 0, 2 * sizeof(int32_t), s));
@@ -508,9 +559,16 @@ static int cycle_bytes(const mlamg_hier* H, bool stored, double* bytes) {
     MLAMG_TRY(op(L.A, &a));
     MLAMG_TRY(op(L.R, &r));
     MLAMG_TRY(op(L.P, &p));
+    if (L.fac_A) {  // the factored form streams agg (4 B/row) and gathers e instead of P
+      double fa = 0.0;
+      MLAMG_TRY(op(L.fac_A, &fa));
+      p = fa - 8.0 * n + 4.0 * n + 8.0 * (double)L.P->n_cols;
+    }
     const double dv = (stored && L.A->rp_dinv_att) ? 0.0 : 8.0 * n;
-    const double jac = a + 8.0 * n + dv;  // + b, dinv
-    const double res = a + 8.0 * n;       // + b
+    // + b (not read at the finest level when the right-hand side is zero), dinv
+    const double bb = (l == 0 && H->zero_rhs && !L.gs) ? 0.0 : 8.0 * n;
+    const double jac = a + bb + dv;
+    const double res = a + bb;
     const bool fused = l == 0 && fused_presmooth(H);
     if (H->nu_pre > 0) {
       // first sweep: elementwise at the top (unless fused into the cycle end); below, fused

@@ -23,7 +23,8 @@
 
 namespace mlamg {
 
-enum EpiOp : int { EPI_AXPBY = 0, EPI_RESID = 1, EPI_JACOBI = 2, EPI_JACEXP = 3, EPI_ADD = 4 };
+enum EpiOp : int { EPI_AXPBY = 0, EPI_RESID = 1, EPI_JACOBI = 2, EPI_JACEXP = 3, EPI_ADD = 4,
+                   EPI_FADD = 5 };
 
 struct Epi {
   double alpha, beta;
@@ -36,6 +37,9 @@ struct Epi {
   double* partial;     // RESID: per-block sum of r^2 (nullable)
   const int32_t* done; // nullable: device flag; nonzero -> kernel is a no-op
   int cached;          // set by launch(): 1 = cached loads of the nonzero stream (see kCachedNnz)
+  // FADD (factored SA prolongation, k_rowpat_uni only): the kernel's x operand is the virtual
+  // vector t = Agg e (t_i = e[agg[i]], 0 where agg[i] < 0) and y += t - dinv * (A t)
+  const int32_t* agg;
 };
 
 // A level operator (square) of at most kCachedNnz entries (~100 MB in CSR) is read with ordinary
@@ -62,14 +66,17 @@ __device__ __forceinline__ EpiIn epi_load(int row, const Epi& e) {
     if (e.beta != 0.0) v.a = e.y[row];
     if (e.copy_to) v.c = e.dinv[row];
   } else if constexpr (OP == EPI_RESID) {
-    v.a = e.b[row];
+    v.a = e.b ? e.b[row] : 0.0;  // b NULL: a zero right-hand side (+0.0: the same bits)
     if (e.copy_to) {
       v.b = e.copy_from[row];
       if (e.dinv) v.c = e.dinv[row];
     }
   } else if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) {
-    v.a = e.b[row];
+    v.a = e.b ? e.b[row] : 0.0;
     v.b = e.xin[row];
+    v.c = e.dinv[row];
+  } else if constexpr (OP == EPI_FADD) {
+    v.a = e.y[row];
     v.c = e.dinv[row];
   } else {  // EPI_ADD
     v.a = e.y[row];
@@ -104,6 +111,9 @@ __device__ __forceinline__ double epi_store(int row, double s, const EpiIn& v, c
   } else if constexpr (OP == EPI_JACEXP) {
     const double t1 = v.c * v.a;
     e.y[row] = v.b + (t1 - s);
+    return 0.0;
+  } else if constexpr (OP == EPI_FADD) {
+    e.y[row] = v.a + (v.b - v.c * s);
     return 0.0;
   } else {  // EPI_ADD
     e.y[row] = v.a + s;
@@ -457,15 +467,18 @@ __device__ __forceinline__ void epi_load2(int r, bool both, const Epi& e, EpiIn&
     if (e.beta != 0.0) ld2(e.y, r, both, u.a, w.a);
     if (e.copy_to && !no_dinv) ld2(e.dinv, r, both, u.c, w.c);
   } else if constexpr (OP == EPI_RESID) {
-    ld2(e.b, r, both, u.a, w.a);
+    if (e.b) ld2(e.b, r, both, u.a, w.a);  // b NULL: zero right-hand side (u.a = w.a = +0.0)
     if (e.copy_to) {
       if (!no_x) ld2(e.copy_from, r, both, u.b, w.b);
       if (e.dinv && !no_dinv) ld2(e.dinv, r, both, u.c, w.c);
     }
   } else if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) {
-    ld2(e.b, r, both, u.a, w.a);
+    if (e.b) ld2(e.b, r, both, u.a, w.a);
     if (!no_x) ld2(e.xin, r, both, u.b, w.b);
     if (!no_dinv) ld2(e.dinv, r, both, u.c, w.c);
+  } else if constexpr (OP == EPI_FADD) {
+    ld2(e.y, r, both, u.a, w.a);
+    if (!no_dinv) ld2(e.dinv, r, both, u.c, w.c);  // t (u.b, w.b) comes from the x window
   } else {  // EPI_ADD
     ld2(e.y, r, both, u.a, w.a);
   }
@@ -492,6 +505,8 @@ __device__ __forceinline__ double epi_value(double s, const EpiIn& v, const Epi&
   } else if constexpr (OP == EPI_JACEXP) {
     const double t1 = v.c * v.a;
     return v.b + (t1 - s);
+  } else if constexpr (OP == EPI_FADD) {
+    return v.a + (v.b - v.c * s);  // x + (t - (w / a_ii) (A t)): x + P e, P = (I - w D^-1 A) Agg
   } else {  // EPI_ADD
     return v.a + s;
   }
@@ -676,6 +691,28 @@ __device__ __forceinline__ dbl2 x16(const double* __restrict__ x, int64_t g, int
   return o;
 }
 
+// x16 for the virtual operand t = Agg e of the factored prolongation (EPI_FADD): t_g =
+// e[agg[g]] (0 where agg[g] < 0 or g outside [0, n)), branch-free like x16
+__device__ __forceinline__ dbl2 t16(const int32_t* __restrict__ agg, const double* __restrict__ e,
+                                    int64_t g, int64_t n) {
+  const int64_t gc = g < 0 ? 0 : (g > n - 2 ? n - 2 : g);
+  const int a0 = agg[gc], a1 = agg[gc + 1];
+  const double v0 = e[a0 < 0 ? 0 : a0], v1 = e[a1 < 0 ? 0 : a1];
+  const double t0 = a0 < 0 ? 0.0 : v0, t1 = a1 < 0 ? 0.0 : v1;
+  dbl2 o;
+  o.x = g == gc ? t0 : (g == n - 1 ? t1 : 0.0);
+  o.y = g == gc ? t1 : (g == -1 ? t0 : 0.0);
+  return o;
+}
+template <int OP>
+__device__ __forceinline__ dbl2 uni_x16(const double* __restrict__ x, int64_t g, int64_t n,
+                                        const Epi& ep) {
+  if constexpr (OP == EPI_FADD)
+    return t16(ep.agg, x, g, n);
+  else
+    return x16(x, g, n);
+}
+
 template <int LY>
 __device__ __forceinline__ int uni_kind(const RpUni& U, int q) {
   constexpr int k1[7] = {3, 0, 1, 0, 2, 0, 3}, k2[5] = {0, 1, 0, 2, 0}, k3[5] = {3, 1, 0, 2, 3};
@@ -718,6 +755,7 @@ void k_rowpat_uni(
   bool x_op = false;
   if constexpr (OP == EPI_JACOBI || OP == EPI_JACEXP) x_op = ep.xin == x;
   if constexpr (OP == EPI_RESID) x_op = ep.copy_to != nullptr && ep.copy_from == x;
+  if constexpr (OP == EPI_FADD) x_op = true;  // t_i, t_i+1: the window's own pair
   const int K = uni_k<LY>(U);
   const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
   const int64_t p0 = lb * CH * kThreads;  // the workgroup's first pair
@@ -745,7 +783,7 @@ void k_rowpat_uni(
   dbl2 fcur[NFR];
 #pragma unroll
   for (int t = 0; t < NF; ++t)
-    fcur[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0} : x16(x, 2 * pa + fo[t], n_cols);
+    fcur[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0} : uni_x16<OP>(x, 2 * pa + fo[t], n_cols, ep);
   // EPF: the epilogue's row operands (b, ...) of chunk 0 go out here too, and chunk c + 1's
   // with its id and far operands, so no chunk waits for its own epilogue loads
   constexpr bool EPF = MLAMG_UNI_EPF == 1 || (MLAMG_UNI_EPF == 2 && NORM);
@@ -758,7 +796,7 @@ void k_rowpat_uni(
 #pragma unroll
   for (int q = 0; q < WQ; ++q) {
     const int i = threadIdx.x + q * kThreads;
-    wv[q] = x16(x, T0 + 2 * (int64_t)(i < nwin ? i : 0), n_cols);
+    wv[q] = uni_x16<OP>(x, T0 + 2 * (int64_t)(i < nwin ? i : 0), n_cols, ep);
   }
 #pragma unroll
   for (int q = 0; q < WQ; ++q) {
@@ -791,7 +829,7 @@ void k_rowpat_uni(
     dbl2 fnext[NFR];
 #pragma unroll
     for (int t = 0; t < NF; ++t)
-      fnext[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0} : x16(x, 2 * prn + fo[t], n_cols);
+      fnext[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0} : uni_x16<OP>(x, 2 * prn + fo[t], n_cols, ep);
     const int pl = c * kThreads + (int)threadIdx.x + hw;  // this pair's window slot
     const dbl2 xc = win[pl];
     const dbl2 xl = win[pl - 1];
@@ -3671,6 +3709,28 @@ int spmv_add(const mlamg_csr* A, const double* x, double* y, const int32_t* done
   ep.y = y;
   ep.done = done;
   return launch<EPI_ADD, false>(A, x, ep, s);
+}
+
+// y += P e with P = (I - w D^-1 A) Agg applied factored (VERDICT r04 Next #5, opt-in): t = Agg e
+// gathered into k_rowpat_uni's x window, y += t - (w / a_ii) (A t); dinv_w = w / a_ii (attached
+// to A as its pattern table, else read per row). A in the uniform row-pair format only.
+int spmv_fadd(const mlamg_csr* A, const int32_t* agg, const double* e, double* y,
+              const double* dinv_w, const int32_t* done, hipStream_t s) {
+  if (!(A->rp_pid && A->rp_uni.k > 0 && A->rp_msk) || A->n_rows != A->n_cols) {
+    set_error("factored prolongation: the operator is not in the uniform row-pair format");
+    return MLAMG_EUNSUPPORTED;
+  }
+  if (A->n_rows == 0) return MLAMG_OK;
+  Epi ep{};
+  ep.y = y;
+  ep.dinv = dinv_w;
+  ep.done = done;
+  ep.agg = agg;
+  switch (A->rp_uni.ch) {
+    case 1: return launch_rowpat_uni<EPI_FADD, false, 1>(A, e, ep, s);
+    case 2: return launch_rowpat_uni<EPI_FADD, false, 2>(A, e, ep, s);
+    default: return launch_rowpat_uni<EPI_FADD, false, 4>(A, e, ep, s);
+  }
 }
 
 int spmv_set(const mlamg_csr* A, const double* x, double* y, const int32_t* done, hipStream_t s,

@@ -161,6 +161,7 @@ SIGNATURES = {
     "mlamg_csr_symmetric": (c_int, [c_vp, c_dbl, P_int, c_vp]),
     "mlamg_hier_set_smoothing": (c_int, [c_vp, c_int, c_int]),
     "mlamg_hier_set_done_check": (c_int, [c_vp, c_int]),
+    "mlamg_hier_set_factored_prolong": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp]),
     "mlamg_hier_set_level_smoother": (c_int, [c_vp, c_int, c_vp]),
     "mlamg_hier_set_norm": (c_int, [c_vp, c_int]),
     "mlamg_hier_vcycle": (c_int, [c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, P_i32, c_int, c_vp]),

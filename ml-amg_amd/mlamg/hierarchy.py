@@ -63,7 +63,7 @@ def csr_symmetric(M, rtol=0.0):
 
 class Level:
     __slots__ = ("A", "dinv", "P", "R", "Agg", "omega", "lam", "lanczos_iters", "n_seeds",
-                 "bf_sweeps", "seeds", "gs", "labels")
+                 "bf_sweeps", "seeds", "gs", "labels", "agg_col")
 
     def __init__(self, A):
         self.A = A
@@ -76,6 +76,7 @@ class Level:
         self.seeds = None
         self.gs = None
         self.labels = None  # per-node aggregate seed (node id, -1 none) when built by BF
+        self.agg_col = None  # per-node aggregate column (int32 device tensor, -1 none)
 
 
 _PHASES = ("count", "alloc", "expand", "sort", "runsum", "emit", "finalize", "free")
@@ -115,6 +116,19 @@ def _aggregate_operator(agg, n):
     return aggregate_op_device(torch.as_tensor(lab.astype(np.int32)).to(_device()), k)
 
 
+def rhs_arg(b):
+    """The right-hand side handed to mlamg_hier_vcycle: None when every entry of b is +0.0
+    (bit pattern 0, so -0.0 does not count) — the reference's convergence-factor problems
+    (utils/common.py:74, utils/evaluate_dataset.py:92: b = zeros). The fine-level kernels then
+    take b = +0.0 instead of streaming a vector of zeros; the results are the same bits. One
+    reduction over b per call (no per-cycle cost)."""
+    if b is None:
+        return None
+    if b.numel() and bool(torch.count_nonzero(b.reshape(-1).contiguous().view(torch.int64))):
+        return b
+    return None
+
+
 class Hierarchy:
     """A multilevel (or two-level) smoothed-aggregation hierarchy resident on the GPU."""
 
@@ -130,6 +144,7 @@ class Hierarchy:
         self.pcg = None
         self.inner = None
         self._breakdowns_seen = 0
+        self._factored = {}
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -333,6 +348,34 @@ class Hierarchy:
             if L.A.get_format()[0] == "rowpat":
                 L.A.attach_dinv(L.dinv)
 
+    def set_factored_prolong(self, level=0, on=True):
+        """Opt-in (VERDICT r04 Next #5): apply level `level`'s prolongation factored, x += t -
+        (w / a_ii) (A t) with t = Agg e (P = (I - w D^-1 A) Agg, ns/lib/multigrid.py:102-108),
+        through the level operator's uniform row-pair kernel (csrc/spmv.hip spmv_fadd) instead
+        of streaming the explicit P. Same operator, different rounding: NOT bitwise the explicit
+        P @ e (tests hold it to the oracle cycle at rtol 1e-11). Needs the level's aggregates
+        (built here, not supplied as P) and a constant-stencil operator; raises MlamgError
+        (EUNSUPPORTED) otherwise. on=False restores x += P e."""
+        L = self.levels[level]
+        if not on:
+            call("mlamg_hier_set_factored_prolong", self.handle, int(level), None, None, None)
+            self._factored.pop(level, None)
+            return
+        if L.agg_col is None or L.omega is None:
+            raise ValueError("factored prolongation needs the level's aggregates and SA weight")
+        ip, ij, ax = L.A.arrays()
+        h = ctypes.c_void_p()
+        n = L.A.shape[0]
+        call("mlamg_csr_create", n, n, L.A.nnz, ctypes.c_void_p(ip), ctypes.c_void_p(ij),
+             ctypes.c_void_p(ax), _lib.MLAMG_WRAP_DEVICE, ctypes.byref(h))
+        A_uni = DeviceCSR(h, keep=(L.A,))  # wraps L.A's arrays: keep L.A alive
+        A_uni.set_format("rowpat")
+        c = L.A.diag_inv(L.omega)  # w / a_ii
+        A_uni.attach_dinv(c)
+        call("mlamg_hier_set_factored_prolong", self.handle, int(level), A_uni.handle,
+             ptr(L.agg_col), ptr(c))
+        self._factored[level] = (A_uni, c)
+
     def formats(self):
         return [{"A": L.A.get_format(), "P": L.P.get_format(), "R": L.R.get_format()}
                 for L in self.levels]
@@ -431,6 +474,7 @@ class Hierarchy:
                         L.labels = lab
                 L.seeds = seeds
                 L.Agg = aggregate_op_device(col, k)
+                L.agg_col = col
                 L.n_seeds = k
                 del C
             elif P_given is None:
@@ -601,17 +645,25 @@ class Hierarchy:
         dev = x.device
         hist = torch.zeros(max(n_cycles, 1), dtype=torch.float64, device=dev) if history else None
         done = ctypes.c_int32()
-        call("mlamg_hier_vcycle", self.handle, ptr(b), ptr(x), int(n_cycles), _tol_arg(tol),
-             ptr(hist), ctypes.byref(done), int(bool(use_graph)), stream_ptr())
+        call("mlamg_hier_vcycle", self.handle, ptr(rhs_arg(b)), ptr(x), int(n_cycles),
+             _tol_arg(tol), ptr(hist), ctypes.byref(done), int(bool(use_graph)), stream_ptr())
         if self.pcg is not None:
             self.check_coarse()
         if not history:
             return None
         return hist[: int(done.value)].cpu().numpy()
 
-    def cycle_async(self, b, x, n_cycles, use_graph=True):
-        """Launch n_cycles V-cycles without reading anything back (for timing)."""
-        call("mlamg_hier_vcycle", self.handle, ptr(b), ptr(x), int(n_cycles), _tol_arg(None),
+    def cycle_async(self, b, x, n_cycles, use_graph=True, zero_rhs=None):
+        """Launch n_cycles V-cycles without reading anything back (for timing). zero_rhs: None
+        = detect an all-zero b (rhs_arg: one reduction and a sync), True / False = as given
+        (False streams b even when it is zero: the general-b kernels)."""
+        if zero_rhs is None:
+            bb = rhs_arg(b)
+        else:
+            bb = None if zero_rhs else b
+            if zero_rhs and b is not None and bool(torch.count_nonzero(b.view(torch.int64))):
+                raise ValueError("zero_rhs=True with a nonzero b")
+        call("mlamg_hier_vcycle", self.handle, ptr(bb), ptr(x), int(n_cycles), _tol_arg(None),
              None, None, int(bool(use_graph)), stream_ptr())
 
     def solve(self, b, x0=None, tol=1e-8, maxiter=500, return_history=False):

@@ -23,7 +23,8 @@ def main():
         if k != key:
             continue
         A = make()
-        H = Hierarchy.build(A, alpha=0.1, max_coarse=max_coarse)
+        H = Hierarchy.build(A, alpha=0.1, max_coarse=max_coarse, aggregation="reference",
+                            coarse_order="sorted")
         n = A.shape[0]
         x0 = np.random.RandomState(0).randn(n)
         x0 /= np.linalg.norm(x0)

@@ -1,4 +1,4 @@
 set -o pipefail
 O=gpurun_out/r05d; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_hierarchy.py -k "sorted or exact_formats" > $O/pytest.log 2>&1 && \
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_hierarchy.py -k "sorted or exact_formats or zero_rhs or autotune_cache or factored" > $O/pytest.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-c3 --no-varcoef > $O/bench.json 2> $O/bench.err
