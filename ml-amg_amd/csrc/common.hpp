@@ -180,15 +180,13 @@ struct mlamg_csr {
   // constant-coefficient stencils): srt_vi[e] indexes srt_vtab and srt_val is dropped
   uint8_t* srt_vi = nullptr;
   double* srt_vtab = nullptr;
-  // value codes of the sorted copy (set_format(SORTED, 2): operators with more than 256 but
-  // few distinct values, e.g. the Galerkin A_1 of a constant stencil): srt_vc[e] < srt_vck
-  // indexes srt_vtab (the srt_vck most frequent values, most frequent first); srt_vc[e] >=
-  // srt_vck is the (srt_vc[e] - srt_vck)-th of the block's exceptions in srt_vcx, which start at
-  // srt_base[8 b + 7]. srt_val is dropped.
+  // block value dictionaries of the sorted copy (set_format(SORTED, 2): operators whose row
+  // blocks repeat values, e.g. the Galerkin A_1 of a constant stencil, ~1,700 distinct values
+  // per 4,096-entry block): block b's distinct values are srt_vtab[srt_vblk[2b] ..
+  // + srt_vblk[2b+1]) and srt_vc[e] indexes them. srt_val is dropped.
   uint16_t* srt_vc = nullptr;
-  double* srt_vcx = nullptr;
-  int32_t srt_vck = 0;
-  int64_t srt_vcx_n = 0;
+  int32_t* srt_vblk = nullptr;
+  int64_t srt_vtab_n = 0;
   // optional row-pair pattern copy ("rowpat" format): every pair of rows (2i, 2i+1) is one of
   // <= 255 distinct pair patterns (the merge by column offset of the two rows' (col - row,
   // value) sequences), kept in LDS tables; the matrix stream is one byte per pair.

@@ -236,7 +236,7 @@ void csr_free(mlamg_csr* A) {
   if (A->srt_vi) (void)hipFree(A->srt_vi);
   if (A->srt_vtab) (void)hipFree(A->srt_vtab);
   if (A->srt_vc) (void)hipFree(A->srt_vc);
-  if (A->srt_vcx) (void)hipFree(A->srt_vcx);
+  if (A->srt_vblk) (void)hipFree(A->srt_vblk);
   if (A->vec_idx16) (void)hipFree(A->vec_idx16);
   if (A->rp_pid) (void)hipFree(A->rp_pid);
   if (A->rp_ptr) (void)hipFree(A->rp_ptr);

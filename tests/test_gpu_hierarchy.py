@@ -318,13 +318,12 @@ def test_sorted_value_dictionary(ml, torch_cuda):
 
 
 def test_sorted_value_codes(ml, torch_cuda):
-    """sorted format with two-byte value codes (set_format('sorted', 2)): a Galerkin A_1 of a
-    constant stencil (more than 256 but few distinct values, all in the table) and a skewed
-    operator with more distinct values than the table holds (the tail stored as per-block
-    exceptions; 80k distinct values, 15 % of the entries outside the table) — every epilogue
-    bitwise the fp64 form (scipy's order); refused (EUNSUPPORTED, plain fp64 kept out of the
-    autotune's way) where the table would miss more than a quarter of the entries or a
-    dictionary applies."""
+    """sorted format with per-block value dictionaries (set_format('sorted', 2): two-byte codes
+    into each 4,096-entry block's own list of distinct values): a Galerkin A_1 of a constant
+    stencil (few distinct values per block) and a skewed operator (85 % of the entries from 300
+    values, the rest ~600 k distinct) — every epilogue bitwise the fp64 form (scipy's order);
+    refused (EUNSUPPORTED) where more than half of a block's entries are distinct or a
+    one-byte dictionary applies."""
     torch = torch_cuda
     from mlamg._lib import MLAMG_EUNSUPPORTED, MlamgError, call, ptr, stream_ptr
     rs = np.random.RandomState(12)
@@ -359,7 +358,7 @@ def test_sorted_value_codes(ml, torch_cuda):
         y = dev(torch, e)
         call("mlamg_prolong_add", Md.handle, ptr(xd), ptr(y), stream_ptr())
         assert np.array_equal(y.cpu().numpy(), e + M @ x)
-    # too many values outside any 61,440-entry table: refused
+    # all values distinct: refused
     W = sp.random(3000, 3000, density=0.02, random_state=rs, format="csr")
     with pytest.raises(MlamgError) as ex:
         ml.sparse.DeviceCSR.from_scipy(W).set_format("sorted", 2)
@@ -928,16 +927,16 @@ def test_zero_rhs_same_bits(ml, torch_cuda):
     assert float(xc.abs().max()) == 0.0
 
 
-@pytest.mark.parametrize("n1", (40, 41))
-def test_factored_prolongation_within_tolerance(ml, oracle, torch_cuda, n1):
+@pytest.mark.parametrize("dim,n1", ((3, 40), (2, 201)))
+def test_factored_prolongation_within_tolerance(ml, oracle, torch_cuda, dim, n1):
     """Opt-in factored level-0 prolongation (VERDICT r04 Next #5): x += t - (w/a_ii) A t with
     t = Agg e instead of x += P e (ns/lib/multigrid.py:102-108's P = (I - w D^-1 A) Agg,
     applied without streaming P). Not bitwise the explicit P: the residual history stays
     within rtol 1e-11 of the oracle's cycle on the explicit operators, and the iterate within
-    1e-10 of its max; off again, the cycle is the explicit one bit for bit. Even and odd grid
-    sizes (the row-pair window's last pair single)."""
+    1e-10 of its max; off again, the cycle is the explicit one bit for bit. The 3-D 7-point and
+    an odd 2-D grid (an odd row count: the row-pair window's last pair single)."""
     torch = torch_cuda
-    A = ml.problems.poisson_3d_7pt(n1)
+    A = ml.problems.poisson_3d_7pt(n1) if dim == 3 else ml.problems.poisson_2d_5pt(n1)
     n = A.shape[0]
     H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=500, aggregation="reference",
                                      coarse_order="sorted")
