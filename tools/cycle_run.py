@@ -25,6 +25,8 @@ def main():
         A = make()
         H = Hierarchy.build(A, alpha=0.1, max_coarse=max_coarse, aggregation="reference",
                             coarse_order="sorted")
+        if os.environ.get("MLAMG_FACTORED_P0") == "1":
+            H.set_factored_prolong(0)  # opt-in factored level-0 prolongation
         n = A.shape[0]
         x0 = np.random.RandomState(0).randn(n)
         x0 /= np.linalg.norm(x0)
