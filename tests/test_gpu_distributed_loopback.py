@@ -149,14 +149,16 @@ def test_loopback_refuses_graph_capture(setup):
 
 @pytest.mark.slow
 def test_loopback_c4_world8_bench_partition():
-    """The bench's own configuration at world 8 (C4 216^3, levels with >= 50,000 rows
-    partitioned, per-rank autotuned local kernels), eager loopback cycles: every rank's
-    iterate bitwise the single-GPU iterate after 3 cycles."""
+    """The bench's own configuration at world 8 (C4 216^3, level 0 aggregated in the reference's
+    push order and relabelled in seed order, levels with >= 50,000 rows partitioned, per-rank
+    autotuned local kernels), eager loopback cycles: every rank's iterate bitwise the
+    single-GPU iterate after 3 cycles."""
     import torch
     from mlamg import problems
     from mlamg.hierarchy import Hierarchy
     A = problems.poisson_3d_7pt(216)
-    H = Hierarchy.build(A, alpha=0.1, strength_mode="invabs", max_coarse=2000)
+    H = Hierarchy.build(A, alpha=0.1, strength_mode="invabs", max_coarse=2000,
+                        aggregation="reference", coarse_order="sorted")
     n = A.shape[0]
     x0 = np.random.RandomState(0).randn(n)
     x0 /= np.linalg.norm(x0)
@@ -189,6 +191,38 @@ def test_loopback_c4_world8_bench_partition():
     for D, (x_own, h) in zip(Ds, out):
         assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank}"
         np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("world", (3, 8))
+def test_loopback_reference_aggregation(world):
+    """The distributed executor on a hierarchy whose level 0 is the reference's push-order
+    aggregation relabelled in seed order (bench.py's setting): bitwise the single-GPU iterate;
+    with the reference's own column order (seeds unsorted) the partition is refused."""
+    import torch
+    from mlamg import problems
+    from mlamg.distributed import DistributedHierarchy, LoopbackGroup
+    from mlamg.hierarchy import Hierarchy
+    A = problems.poisson_3d_7pt(30)
+    n = A.shape[0]
+    H = Hierarchy.build(A, alpha=0.1, max_coarse=200, aggregation="reference",
+                        coarse_order="sorted")
+    x0 = np.random.RandomState(3).randn(n)
+    b = np.random.RandomState(4).randn(n)
+    xd = torch.as_tensor(x0).cuda()
+    h_ref = H.cycle(torch.as_tensor(b).cuda(), xd, 5, use_graph=False)
+    x_ref = xd.cpu().numpy()
+    Ds, out = _run(A, H, world, 0, ncyc=5, b=b, x0=x0)
+    for D, (x_own, h) in zip(Ds, out):
+        assert np.array_equal(x_own, x_ref[D.lo:D.hi]), f"rank {D.comm.rank} of {world}"
+        np.testing.assert_allclose(h, h_ref, rtol=1e-12, atol=0)
+    Hs = Hierarchy.build(A, alpha=0.1, max_coarse=200, aggregation="reference",
+                         coarse_order="seed")
+    group = LoopbackGroup(2)
+    try:
+        with pytest.raises(ValueError):
+            DistributedHierarchy(Hs, group.comms[0], min_rows=0, A_host=A)
+    finally:
+        group.close()
 
 
 @pytest.mark.parametrize("world", (6, 8))
