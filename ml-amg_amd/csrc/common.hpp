@@ -269,6 +269,7 @@ int csr_alloc(int64_t n_rows, int64_t n_cols, int64_t nnz, mlamg_csr** out);
 // Build the CSR-stream row-block partition from the device indptr (syncs `stream`).
 int csr_finalize(mlamg_csr* A, hipStream_t stream);
 void csr_free(mlamg_csr* A);
+int transpose_impl(const mlamg_csr* A, mlamg_csr** out, hipStream_t s);
 
 // scratch buffer cache (per device); grows monotonically, freed at destroy/exit.
 void* scratch(size_t bytes, int slot);
