@@ -241,3 +241,24 @@ def test_lloyd_tie_rich_driver(golden, oracle, k, case):
     assert np.array_equal(roots, g[f"{k}_{case}_roots"])
     assert np.array_equal(AggOp.indptr, g[f"{k}_{case}_agg_indptr"])
     assert np.array_equal(AggOp.indices, g[f"{k}_{case}_agg_indices"])
+
+
+def test_reference_aggregates_match_dumb_driver(oracle):
+    """oracle.reference_aggregates (the recipe of Hierarchy.build(aggregation='reference'),
+    the bench's level-0 aggregation) against the reference's own utils/evaluate_dataset.py
+    'dumb' method (:80-90) run here on the caller dataset (tests/golden/reference_callers.npz,
+    ed_dumb*): unsorted RandomState(0) seeds, modified_bellman_ford, nearest_center_to_agg —
+    the aggregate operator bitwise (indptr, indices). The strength is the loop's olson measure
+    (pyamg's evolution restated, global RNG re-seeded as the loop does: parity of that measure
+    is unpinned; the aggregation recipe around it is what this pins)."""
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "reference_callers.npz")))
+    i = 0
+    while f"ds{i}_indptr" in g:
+        A = sp.csr_matrix((g[f"ds{i}_data"], g[f"ds{i}_indices"], g[f"ds{i}_indptr"]))
+        np.random.seed(0)  # utils/evaluate_dataset.py:70
+        C = oracle.strength_measure(A, "olson")
+        _, _, Agg = oracle.reference_aggregates(C, A.shape[0], 0.1, 0)
+        assert np.array_equal(Agg.indptr, g[f"ed_dumb{i}_agg_indptr"]), i
+        assert np.array_equal(Agg.indices, g[f"ed_dumb{i}_agg_indices"]), i
+        i += 1
+    assert i >= 4
