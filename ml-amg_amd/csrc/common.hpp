@@ -85,7 +85,10 @@ constexpr int kSrtNnz = 8 * MLAMG_SRT_THREADS;
 constexpr int kSrtPosBits = 12;
 // operators averaging at least this many entries per row take the sorted kernel's long-row
 // instantiation (two rows summed side by side per thread)
-constexpr double kSrtLongRow = 48.0;
+#ifndef MLAMG_SRT_LONG_ROW  // build-time A/B knob
+#define MLAMG_SRT_LONG_ROW 32.0
+#endif
+constexpr double kSrtLongRow = MLAMG_SRT_LONG_ROW;
 // "long" format tiles (long-row coarse operators: Galerkin A_l, R = P^T): 256-thread
 // workgroups, <= kLongNnz fp64 products in LDS, <= kLongRows rows per tile (one lane each)
 constexpr int kLongNnz = 4096;
