@@ -577,10 +577,10 @@ static int build_push_plan(const mlamg_csr* G, hipStream_t s, SeqPlan& P) {
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipMemcpyAsync(&hbad, bad, sizeof(int32_t), hipMemcpyDeviceToHost, s);
-  // the transpose runs on the device while the host computes the levels below
+  // the in-edge lists: G's transpose on the device (it syncs s, so hbad is in too)
   mlamg_csr* T = nullptr;
   int rc = e == hipSuccess ? MLAMG_OK : MLAMG_EHIP;
-  if (rc == MLAMG_OK) rc = transpose_impl(G, &T, s);  // syncs s (hbad is in)
+  if (rc == MLAMG_OK) rc = transpose_impl(G, &T, s);
   (void)hipFree(bad);
   if (rc != MLAMG_OK) {
     if (e != hipSuccess) set_error(std::string("bellman_ford plan: ") + hipGetErrorString(e));
