@@ -57,3 +57,27 @@ def test_distributed_tolerance_stop(setup):
         h = D.cycle(b, xe, 50, tol=1e-6 * float(torch.linalg.norm(b)))
         assert len(h) == len(h_ref) < 50
         assert torch.equal(xe[:n], x)
+
+
+def test_finalize_replicated_matches_full_build():
+    """bench.py's N > 1 setup: every rank builds with finalize=False, rank 0 autotunes and
+    broadcasts the formats, every rank then builds its coarse solver (finalize_replicated) —
+    the cycle is bitwise that of a hierarchy built in one call (world 1 here; the broadcast is
+    the same object list sync_formats used)."""
+    from mlamg import problems
+    from mlamg.distributed import finalize_replicated
+    from mlamg.hierarchy import Hierarchy
+    A = problems.poisson_3d_7pt(24)
+    n = A.shape[0]
+    H1 = Hierarchy.build(A, alpha=0.1, max_coarse=60, aggregation="reference",
+                         coarse_order="sorted")
+    H2 = Hierarchy.build(A, alpha=0.1, max_coarse=60, aggregation="reference",
+                         coarse_order="sorted", finalize=False)
+    assert H2.handle is None
+    finalize_replicated(H2, 1, 0)
+    x0 = np.random.RandomState(0).randn(n)
+    b = torch.as_tensor(np.random.RandomState(1).randn(n)).cuda()
+    x1, x2 = torch.as_tensor(x0).cuda(), torch.as_tensor(x0).cuda()
+    h1 = H1.cycle(b, x1, 5)
+    h2 = H2.cycle(b, x2, 5)
+    assert np.array_equal(h1, h2) and torch.equal(x1, x2)
