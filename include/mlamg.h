@@ -536,6 +536,7 @@ int mlamg_dhier_set_coarse_graph(mlamg_dhier* D, int use_graph);
 /* capture one whole distributed cycle (kernels and RCCL send/recv/all-reduce) into a hipGraph
  * and replay it (default off); re-captured when b, x, res_hist, tol or a kernel format change */
 int mlamg_dhier_set_cycle_graph(mlamg_dhier* D, int use_graph);
+/* b may be NULL: this rank's part of the right-hand side is zero (as mlamg_hier_vcycle) */
 int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cycles, double tol,
                        double* res_hist, int32_t* cycles_done_host, void* stream);
 

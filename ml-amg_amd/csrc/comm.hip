@@ -846,8 +846,8 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
   const mlamg_csr* A = L.A;
   D->ev_next = 0;
   MLAMG_TRY(exchange_then(D, L.hx, x_ext, A, L.sA, s, [&](const mlamg_csr* M, int64_t r0, int) {
-    return residual_impl(M, b + r0, x_ext, L.r_ext + r0, nullptr, nullptr, nullptr, done, kNoTol,
-                         nullptr, nullptr, nullptr, s);
+    return residual_impl(M, b ? b + r0 : nullptr, x_ext, L.r_ext + r0, nullptr, nullptr, nullptr,
+                         done, kNoTol, nullptr, nullptr, nullptr, s);
   }));
   MLAMG_TRY(correct(D, 0, x_ext, done, s));
   MLAMG_TRY(jacobi_sweep(A, L.dinv, b, x_ext, L.t_ext, false, done, s));
@@ -868,7 +868,8 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
   }
   MLAMG_TRY(exchange_then(D, L.hx, L.t_ext, A, L.sA, s,
                           [&](const mlamg_csr* M, int64_t r0, int part) {
-                            return residual_partials(M, b + r0, L.t_ext, nullptr, x_ext + r0,
+                            return residual_partials(M, b ? b + r0 : nullptr, L.t_ext, nullptr,
+                                                     x_ext + r0,
                                                      L.t_ext + r0,
                                                      D->partial + (part < 0 ? 0 : poff[part]),
                                                      done, s, L.dinv + r0);
@@ -884,7 +885,9 @@ static int dcycle(mlamg_dhier* D, const double* b, double* x_ext, double* hist, 
 
 int mlamg_dhier_vcycle(mlamg_dhier* D, const double* b, double* x_ext, int n_cycles, double tol,
                        double* res_hist, int32_t* cycles_done_host, void* stream) {
-  MLAMG_REQUIRE(D && b && x_ext, "NULL argument");
+  // b NULL: this rank's part of the right-hand side is zero (as mlamg_hier_vcycle: the
+  // fine-level kernels take +0.0 instead of reading b; same bits)
+  MLAMG_REQUIRE(D && x_ext, "NULL argument");
   MLAMG_REQUIRE(n_cycles >= 0, "n_cycles < 0");
   MLAMG_TRY(dprepare(D));
   hipStream_t s = S(stream);

@@ -292,7 +292,9 @@ class DistributedHierarchy:
     def cycle(self, b_own, x_ext, n_cycles, tol=None, history=True):
         hist = torch.zeros(max(n_cycles, 1), dtype=torch.float64, device="cuda") if history else None
         done = ctypes.c_int32()
-        call("mlamg_dhier_vcycle", self.handle, ptr(b_own), ptr(x_ext), int(n_cycles), _tol_arg(tol),
+        from .hierarchy import rhs_arg
+        call("mlamg_dhier_vcycle", self.handle, ptr(rhs_arg(b_own)), ptr(x_ext), int(n_cycles),
+             _tol_arg(tol),
              ptr(hist), ctypes.byref(done) if history else None, stream_ptr())
         if not history:
             return None
