@@ -322,11 +322,44 @@ int mlamg_lloyd_cluster(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxit
 int mlamg_lloyd_cluster_canon(const mlamg_csr* G, int32_t* seeds, int32_t k, int maxiter,
                               double* dist, int32_t* cluster, int32_t* iters_host, void* stream);
 
+/* ---------------------------------------------------------------- pyamg smoothed aggregation
+ * Setup kernels of pyamg.aggregation.smoothed_aggregation_solver with its defaults, the
+ * hierarchy the reference's PyAMG preconditioner builds (ns/preconditioner/PyAMG.py:94). pyamg is
+ * absent: restated from its published algorithm (amg_core), parity unpinned; bitwise the
+ * oracle's restatement (oracle/oracle.c pyamg_*). csrc/sa.hip.
+ * symmetric_strength_of_connection(A, theta): row i keeps its diagonal and a_ij with
+ * a_ij^2 >= theta^2 |a_ii| |a_jj| (stored order), values |a_ij| / (row max). */
+int mlamg_symmetric_strength(const mlamg_csr* A, double theta, mlamg_csr** out, void* stream);
+/* standard_aggregation(C) (amg_core, three greedy passes in row order; pass 1 decided in
+ * parallel rounds, bitwise the sequential result): agg[n] (DEVICE) = aggregate of each row, -1
+ * unaggregated; cpts (DEVICE, n, may be NULL) = the root of each aggregate; *n_agg = aggregates;
+ * *rounds_host = pass-1 rounds. Syncs. */
+int mlamg_standard_aggregation(const mlamg_csr* C, int32_t* agg, int32_t* cpts, int64_t* n_agg,
+                               int32_t* rounds_host, void* stream);
+/* fit_candidates(AggOp, B, tol) with one candidate: per aggregate (rows ascending)
+ * norm = sqrt(sum B_i^2), T_i = B_i * (1 / norm) (0 if norm <= tol * norm), Bc = norm; T has
+ * AggOp's pattern. B (DEVICE, n), Bc (DEVICE, n_agg). */
+int mlamg_fit_candidates(const mlamg_csr* AggOp, const double* B, double tol, mlamg_csr** T_out,
+                         double* Bc, void* stream);
+/* C = A - B with scipy's csr binop rules (a - b, a - 0, 0 - b; zero results not stored), columns
+ * ascending (jacobi_prolongation_smoother's P = T - D^-1 A T). */
+int mlamg_csr_sub(const mlamg_csr* A, const mlamg_csr* B, mlamg_csr** out, void* stream);
+/* pyamg get_diagonal(A, inv=True): dinv_i = 1 / (sum of row i's diagonal entries), 0 where that
+ * sum is 0 (DEVICE, n). */
+int mlamg_diag_pinv(const mlamg_csr* A, double* dinv, void* stream);
+
 /* ---------------------------------------------------------------- Gauss-Seidel
  * pyamg relaxation.gauss_seidel (forward lexicographic, in place) used by the reference driver
  * (ns/lib/multigrid.py:175,184). Exact lexicographic order via level scheduling of the row
  * dependency DAG: bitwise identical to the sequential sweep. */
 int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream);
+/* the same with a sweep direction (0 forward, 1 backward, 2 symmetric: forward then backward per
+ * iteration) and block = 1 for pyamg relaxation.block_gauss_seidel's arithmetic with 1 x 1 blocks
+ * (rsum = b_i - (0 + a_ij x_j) ..., x_i = 0 + Dinv_i rsum, Dinv_i = 1/a_ii or 0): the smoother and
+ * the candidate improvement of pyamg.aggregation.smoothed_aggregation_solver
+ * (ns/preconditioner/PyAMG.py:94; pyamg absent: parity unpinned, bitwise the oracle's
+ * restatement, oracle/oracle.c pyamg_block_gauss_seidel) */
+int mlamg_gs_create_ex(const mlamg_csr* A, int sweep, int block, mlamg_gs** out, void* stream);
 int mlamg_gs_destroy(mlamg_gs* G);
 int mlamg_gs_levels(const mlamg_gs* G, int32_t* n_levels);
 int mlamg_gs_sweep(const mlamg_gs* G, double* x, const double* b, int iterations, void* stream);
@@ -337,6 +370,10 @@ int mlamg_gs_sweep(const mlamg_gs* G, double* x, const double* b, int iterations
  * dense GEMV. Returns MLAMG_EINVAL if the matrix is numerically singular. */
 int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream);
 int mlamg_dense_destroy(mlamg_dense* D);
+/* a given n x n row-major matrix M (host) applied as x = M b: the 'pinv' coarse solver of
+ * pyamg's multilevel solver (M = scipy.linalg.pinv(A_c), formed by the caller as pyamg does;
+ * ns/preconditioner/PyAMG.py:94). Syncs. */
+int mlamg_dense_create_matrix(const double* M_host, int64_t n, mlamg_dense** out, void* stream);
 /* which inverse was built: 1 = inverse Cholesky factor X = L^-1 with A^-1 = X^T X formed
  * (symmetric positive definite), 2 = the same factor kept and applied as X^T (X b), two
  * triangular passes (SPD operators of >= 2048 rows: no O(n^3) product), 0 = Gauss-Jordan with

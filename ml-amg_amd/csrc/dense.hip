@@ -721,6 +721,31 @@ int mlamg_dense_create(const mlamg_csr* A, mlamg_dense** out, void* stream) {
   return MLAMG_OK;
 }
 
+int mlamg_dense_create_matrix(const double* M_host, int64_t n, mlamg_dense** out, void* stream) {
+  MLAMG_REQUIRE(out && (n == 0 || M_host), "NULL argument");
+  MLAMG_REQUIRE(n >= 0 && n <= 32768, "matrix too large for the dense solver");
+  hipStream_t s = S(stream);
+  auto* D = new mlamg_dense();
+  D->n = n;
+  if (hipMalloc(&D->inv, sizeof(double) * std::max<int64_t>(n * n, 1)) != hipSuccess) {
+    delete D;
+    set_error("dense_create_matrix: hipMalloc failed");
+    return MLAMG_ENOMEM;
+  }
+  hipError_t e = hipSuccess;
+  if (n) e = hipMemcpyAsync(D->inv, M_host, sizeof(double) * n * n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    (void)hipFree(D->inv);
+    delete D;
+    set_error(std::string("dense_create_matrix: ") + hipGetErrorString(e));
+    return MLAMG_EHIP;
+  }
+  D->method = 0;  // applied as x = M b (k_gemv)
+  *out = D;
+  return MLAMG_OK;
+}
+
 int mlamg_dense_info(const mlamg_dense* D, int* method, int64_t* n) {
   MLAMG_REQUIRE(D, "NULL argument");
   if (method) *method = D->method;

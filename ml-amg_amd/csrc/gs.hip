@@ -1,12 +1,19 @@
-// Forward lexicographic Gauss-Seidel, pyamg relaxation.gauss_seidel semantics (the smoother of
-// the reference driver, ns/lib/multigrid.py:175,184):
+// Lexicographic Gauss-Seidel sweeps, pyamg semantics:
+//   gauss_seidel (the smoother of the reference driver, ns/lib/multigrid.py:175,184):
 //     for i in 0..n-1: rsum = sum_{j != i} A_ij x_j (stored order); diag = A_ii (last one);
 //                      if diag != 0: x_i = (b_i - rsum) / diag
-// Row i reads x_j (j < i) after their update and x_j (j > i) before theirs. Level scheduling
-// keeps exactly that order on the GPU: level(i) = 1 + max level(j) over j < i coupled to i in
-// either direction (a_ij or a_ji nonzero), so every row of a level sees final values of all
-// earlier-coupled rows and old values of all later-coupled rows; rows inside a level are
-// independent. Results are therefore bit for bit those of the sequential sweep.
+//   block_gauss_seidel with 1 x 1 blocks (the pre/post smoother and the candidate improvement of
+//   pyamg's smoothed_aggregation_solver, which ns/preconditioner/PyAMG.py:94 builds; amg_core
+//   block_gauss_seidel): rsum = b_i; rsum -= (0 + A_ij x_j) for j != i in stored order;
+//     x_i = 0 + Dinv_i rsum, Dinv_i = pinv(A_ii) = 1 / A_ii (0 when A_ii = 0)
+//   sweep 'forward' (rows 0..n-1), 'backward' (n-1..0) or 'symmetric' (forward, then backward,
+//   per iteration).
+// Row i reads x_j of rows swept before it after their update and the others before theirs.
+// Level scheduling keeps exactly that order on the GPU: level(i) = 1 + max level(j) over rows j
+// swept before i and coupled to i in either direction (a_ij or a_ji nonzero), so every row of a
+// level sees final values of all earlier-coupled rows and old values of all later-coupled rows;
+// rows inside a level are independent. Results are therefore bit for bit those of the sequential
+// sweep.
 #include "common.hpp"
 
 #include <chrono>
@@ -15,6 +22,9 @@
 
 struct mlamg_gs {
   const mlamg_csr* A = nullptr;
+  bool block = false;        // block_gauss_seidel arithmetic (pk_diag then holds Dinv)
+  bool backward = false;     // rows swept n-1..0
+  mlamg_gs* bwd = nullptr;   // symmetric sweep: the backward schedule of the same operator
   int32_t n_levels = 0;
   int32_t max_level_rows = 0;
   std::vector<int32_t> level_ptr;  // host
@@ -44,19 +54,40 @@ struct mlamg_gs {
 
 namespace mlamg {
 
+// the two row updates: gauss_seidel (BLK false) sums the off-diagonal products from +0.0 and
+// divides b_i minus the sum by the diagonal; block_gauss_seidel (BLK true) subtracts each product
+// (gemm's 0 + a x) from b_i and multiplies by Dinv_i (gemm's 0 + d r)
+template <bool BLK>
+__device__ __forceinline__ double gs_init(double bi) { return BLK ? bi : 0.0; }
+template <bool BLK>
+__device__ __forceinline__ double gs_acc(double s, double a, double xj) {
+  return BLK ? s - (0.0 + a * xj) : s + a * xj;
+}
+// d: the diagonal (gauss_seidel) or Dinv (block)
+template <bool BLK>
+__device__ __forceinline__ double gs_fin(double s, double bi, double d) {
+  return BLK ? 0.0 + d * s : (bi - s) / d;
+}
+// gauss_seidel leaves a zero-diagonal row alone; block_gauss_seidel updates every row
+template <bool BLK>
+__device__ __forceinline__ bool gs_upd(double d) { return BLK || d != 0.0; }
+
+template <bool BLK>
 __device__ __forceinline__ void gs_row(const int32_t* __restrict__ ip,
                                        const int32_t* __restrict__ ij,
                                        const double* __restrict__ ax, int32_t i, double* x,
                                        const double* __restrict__ b) {
-  double rsum = 0.0, diag = 0.0;
+  double s = gs_init<BLK>(b[i]), diag = 0.0;
   for (int k = ip[i]; k < ip[i + 1]; ++k) {
     const int32_t j = ij[k];
     if (j == i) diag = ax[k];
-    else rsum += ax[k] * x[j];
+    else s = gs_acc<BLK>(s, ax[k], x[j]);
   }
-  if (diag != 0.0) x[i] = (b[i] - rsum) / diag;
+  if (BLK) diag = diag != 0.0 ? 1.0 / diag : 0.0;
+  if (gs_upd<BLK>(diag)) x[i] = gs_fin<BLK>(s, b[i], diag);
 }
 
+template <bool BLK>
 __global__ __launch_bounds__(256) void k_gs_level(const int32_t* __restrict__ ip,
                                                   const int32_t* __restrict__ ij,
                                                   const double* __restrict__ ax,
@@ -66,7 +97,7 @@ __global__ __launch_bounds__(256) void k_gs_level(const int32_t* __restrict__ ip
   if (done && *done) return;
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t >= cnt) return;
-  gs_row(ip, ij, ax, rows[t], x, b);
+  gs_row<BLK>(ip, ij, ax, rows[t], x, b);
 }
 
 // The whole sweep in one workgroup: levels in order, a barrier between consecutive levels
@@ -75,6 +106,7 @@ __global__ __launch_bounds__(256) void k_gs_level(const int32_t* __restrict__ ip
 constexpr int kGsBlock = 1024;
 constexpr int kGsBlockMaxLevelRows = 8 * kGsBlock;
 
+template <bool BLK>
 __global__ __launch_bounds__(kGsBlock) void k_gs_block(const int32_t* __restrict__ ip,
                                                        const int32_t* __restrict__ ij,
                                                        const double* __restrict__ ax,
@@ -87,7 +119,7 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_block(const int32_t* __restrict
   for (int it = 0; it < iterations; ++it) {
     for (int32_t l = 0; l < n_levels; ++l) {
       const int32_t a = lptr[l], z = lptr[l + 1];
-      for (int32_t t = a + (int32_t)threadIdx.x; t < z; t += kGsBlock) gs_row(ip, ij, ax, rows[t], x, b);
+      for (int32_t t = a + (int32_t)threadIdx.x; t < z; t += kGsBlock) gs_row<BLK>(ip, ij, ax, rows[t], x, b);
       __syncthreads();
     }
   }
@@ -129,7 +161,7 @@ __device__ __forceinline__ void gs_pipe_load(GsRows<R, K>& q, int32_t a, int32_t
   }
 }
 
-template <int R, int K>
+template <int R, int K, bool BLK>
 __global__ __launch_bounds__(kGsBlock) void k_gs_pipe(const int32_t* __restrict__ rows,
                                                       const int32_t* __restrict__ lptr,
                                                       int32_t n_levels,
@@ -157,11 +189,12 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_pipe(const int32_t* __restrict_
 #pragma unroll
       for (int u = 0; u < R; ++u) {
         if (cur.row[u] < 0) continue;
-        double rsum = 0.0;
+        double rsum = gs_init<BLK>(cur.bi[u]);
 #pragma unroll
         for (int k = 0; k < K; ++k)
-          if (cur.col[u][k] >= 0) rsum += cur.val[u][k] * xv[u][k];
-        if (cur.diag[u] != 0.0) x[cur.row[u]] = (cur.bi[u] - rsum) / cur.diag[u];
+          if (cur.col[u][k] >= 0) rsum = gs_acc<BLK>(rsum, cur.val[u][k], xv[u][k]);
+        if (gs_upd<BLK>(cur.diag[u]))
+          x[cur.row[u]] = gs_fin<BLK>(rsum, cur.bi[u], cur.diag[u]);
       }
       __syncthreads();
       if (l + 1 < n_levels) cur = nxt;
@@ -174,7 +207,7 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_pipe(const int32_t* __restrict_
 // level costs an LDS round trip and a barrier instead of a global-memory round trip.
 constexpr int kGsLdsMax = 8192;  // 64 KB of x: within the default dynamic-LDS limit
 
-template <int K>
+template <int K, bool BLK>
 __global__ __launch_bounds__(kGsBlock) void k_gs_lds(const int32_t* __restrict__ rows,
                                                      const int32_t* __restrict__ lptr,
                                                      int32_t n_levels, int64_t n,
@@ -199,11 +232,11 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_lds(const int32_t* __restrict__
         double xv[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) xv[k] = cur.col[0][k] >= 0 ? xs[cur.col[0][k]] : 0.0;
-        double rsum = 0.0;
+        double rsum = gs_init<BLK>(cur.bi[0]);
 #pragma unroll
         for (int k = 0; k < K; ++k)
-          if (cur.col[0][k] >= 0) rsum += cur.val[0][k] * xv[k];
-        if (cur.diag[0] != 0.0) xs[cur.row[0]] = (cur.bi[0] - rsum) / cur.diag[0];
+          if (cur.col[0][k] >= 0) rsum = gs_acc<BLK>(rsum, cur.val[0][k], xv[k]);
+        if (gs_upd<BLK>(cur.diag[0])) xs[cur.row[0]] = gs_fin<BLK>(rsum, cur.bi[0], cur.diag[0]);
       }
       __syncthreads();
       if (l + 1 < n_levels) cur = nxt;
@@ -269,7 +302,7 @@ struct WinCols {  // KM uint16 slots: one 8-byte (KM 4) or 16-byte (KM 8) LDS ac
   typedef typename std::conditional<KM == 4, uint2, uint4>::type T;
 };
 
-template <int KM, int RW, int CW>
+template <int KM, int RW, int CW, bool BLK>
 __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int4* __restrict__ cdesc,
                                                      const int32_t* __restrict__ wlev,
                                                      int32_t nchunks,
@@ -408,17 +441,20 @@ __global__ __launch_bounds__(kGsWinBlock) void k_gs_win(const int4* __restrict__
           double xi[RW];
 #pragma unroll
           for (int u = 0; u < RW; ++u) {
-            double y = 0.0;
+            double y = gs_init<BLK>(bv[u]);
 #pragma unroll
-            for (int k = 0; k < KM; ++k) y += v[u][k] * g[u][k];
-            xi[u] = (bv[u] - y) / d[u];
+            for (int k = 0; k < KM; ++k) y = gs_acc<BLK>(y, v[u][k], g[u][k]);
+            xi[u] = gs_fin<BLK>(y, bv[u], d[u]);
           }
+          // the dummy, and a zero-diagonal row of gauss_seidel: left alone (the sink slot)
+          bool up[RW];
 #pragma unroll
-          for (int u = 0; u < RW; ++u)  // zero diagonal (and the dummy): left alone
-            ring[d[u] != 0.0 ? ((P0 + p[u]) & RM) : RS + 1] = xi[u];
+          for (int u = 0; u < RW; ++u) up[u] = p[u] != cnt && gs_upd<BLK>(d[u]);
+#pragma unroll
+          for (int u = 0; u < RW; ++u) ring[up[u] ? ((P0 + p[u]) & RM) : RS + 1] = xi[u];
 #pragma unroll
           for (int u = 0; u < RW; ++u)
-            if (d[u] != 0.0) xl[P0 + p[u]] = xi[u];
+            if (up[u]) xl[P0 + p[u]] = xi[u];
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -474,19 +510,19 @@ static bool gs_lds_disabled() {
   return e && e[0] == '1';
 }
 
-template <int R, int K>
+template <int R, int K, bool BLK>
 static void launch_gs_pipe(const mlamg_gs* G, double* x, const double* b, int iterations,
                            const int32_t* done, hipStream_t s) {
   const int64_t n = G->A->n_rows;
   hipLaunchKernelGGL(k_gs_b_level, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
                      n, b, G->b_lvl, done);
   if (R == 1 && n <= kGsLdsMax && !gs_lds_disabled()) {
-    hipLaunchKernelGGL((k_gs_lds<K>), dim3(1), dim3(kGsBlock), sizeof(double) * n, s, G->rows,
+    hipLaunchKernelGGL((k_gs_lds<K, BLK>), dim3(1), dim3(kGsBlock), sizeof(double) * n, s, G->rows,
                        G->d_level_ptr, G->n_levels, n, G->pk_col, G->pk_val, G->pk_diag,
                        G->b_lvl, iterations, x, done);
     return;
   }
-  hipLaunchKernelGGL((k_gs_pipe<R, K>), dim3(1), dim3(kGsBlock), 0, s, G->rows, G->d_level_ptr,
+  hipLaunchKernelGGL((k_gs_pipe<R, K, BLK>), dim3(1), dim3(kGsBlock), 0, s, G->rows, G->d_level_ptr,
                      G->n_levels, G->pk_col, G->pk_val, G->pk_diag, G->b_lvl, iterations, x,
                      done);
 }
@@ -519,13 +555,13 @@ static bool gs_win_disabled() {  // MLAMG_GS_NO_WIN=1: A/B runs, tests
   return e && e[0] == '1';
 }
 
-template <int KM, int RW, int CW>
+template <int KM, int RW, int CW, bool BLK>
 static void launch_gs_win(const mlamg_gs* G, double* x, const double* b, int iterations,
                           const int32_t* done, hipStream_t s) {
   const int64_t n = G->A->n_rows;
   hipLaunchKernelGGL(k_gs_win_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
                      n, b, G->b_lvl, x, G->win_xl, done);
-  hipLaunchKernelGGL((k_gs_win<KM, RW, CW>), dim3(1), dim3(kGsWinBlock), G->win_lds, s,
+  hipLaunchKernelGGL((k_gs_win<KM, RW, CW, BLK>), dim3(1), dim3(kGsWinBlock), G->win_lds, s,
                      reinterpret_cast<const int4*>(G->d_clev), G->d_clev + 8 * G->n_chunks,
                      G->n_chunks, G->wcol, G->pk_val, G->pk_diag, G->b_lvl, G->ring_log2,
                      G->win_cap, iterations, G->win_xl, done);
@@ -535,8 +571,9 @@ static void launch_gs_win(const mlamg_gs* G, double* x, const double* b, int ite
 
 int64_t gs_rows(const mlamg_gs* G) { return G->A->n_rows; }
 
-int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
-                  const int32_t* done, hipStream_t s) {
+template <bool BLK>
+static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int iterations,
+                        const int32_t* done, hipStream_t s) {
   const mlamg_csr* A = G->A;
   if (A->n_rows == 0 || iterations <= 0) return MLAMG_OK;
   const bool pipe = G->pk_k > 0 && G->n_levels > 4;
@@ -544,43 +581,58 @@ int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
     // win_rw = 64-row slots per level: up to 4 sweeping waves, then 2 rows per lane
     if (G->pk_k == 4) {
       switch (G->win_rw) {
-        case 1: launch_gs_win<4, 1, 1>(G, x, b, iterations, done, s); break;
-        case 2: launch_gs_win<4, 1, 2>(G, x, b, iterations, done, s); break;
-        case 3: launch_gs_win<4, 1, 3>(G, x, b, iterations, done, s); break;
-        case 4: launch_gs_win<4, 1, 4>(G, x, b, iterations, done, s); break;
-        default: launch_gs_win<4, 2, 4>(G, x, b, iterations, done, s); break;
+        case 1: launch_gs_win<4, 1, 1, BLK>(G, x, b, iterations, done, s); break;
+        case 2: launch_gs_win<4, 1, 2, BLK>(G, x, b, iterations, done, s); break;
+        case 3: launch_gs_win<4, 1, 3, BLK>(G, x, b, iterations, done, s); break;
+        case 4: launch_gs_win<4, 1, 4, BLK>(G, x, b, iterations, done, s); break;
+        default: launch_gs_win<4, 2, 4, BLK>(G, x, b, iterations, done, s); break;
       }
     } else {
       switch (G->win_rw) {
-        case 1: launch_gs_win<8, 1, 1>(G, x, b, iterations, done, s); break;
-        case 2: launch_gs_win<8, 1, 2>(G, x, b, iterations, done, s); break;
-        case 3: launch_gs_win<8, 1, 3>(G, x, b, iterations, done, s); break;
-        case 4: launch_gs_win<8, 1, 4>(G, x, b, iterations, done, s); break;
-        default: launch_gs_win<8, 2, 4>(G, x, b, iterations, done, s); break;
+        case 1: launch_gs_win<8, 1, 1, BLK>(G, x, b, iterations, done, s); break;
+        case 2: launch_gs_win<8, 1, 2, BLK>(G, x, b, iterations, done, s); break;
+        case 3: launch_gs_win<8, 1, 3, BLK>(G, x, b, iterations, done, s); break;
+        case 4: launch_gs_win<8, 1, 4, BLK>(G, x, b, iterations, done, s); break;
+        default: launch_gs_win<8, 2, 4, BLK>(G, x, b, iterations, done, s); break;
       }
     }
   } else if (pipe && G->max_level_rows <= 2 * kGsBlock) {
     const bool one = G->max_level_rows <= kGsBlock;
     if (G->pk_k == 4) {
-      if (one) launch_gs_pipe<1, 4>(G, x, b, iterations, done, s);
-      else launch_gs_pipe<2, 4>(G, x, b, iterations, done, s);
+      if (one) launch_gs_pipe<1, 4, BLK>(G, x, b, iterations, done, s);
+      else launch_gs_pipe<2, 4, BLK>(G, x, b, iterations, done, s);
     } else {
-      if (one) launch_gs_pipe<1, 8>(G, x, b, iterations, done, s);
-      else launch_gs_pipe<2, 8>(G, x, b, iterations, done, s);
+      if (one) launch_gs_pipe<1, 8, BLK>(G, x, b, iterations, done, s);
+      else launch_gs_pipe<2, 8, BLK>(G, x, b, iterations, done, s);
     }
   } else if (G->max_level_rows <= kGsBlockMaxLevelRows && G->n_levels > 4) {
-    hipLaunchKernelGGL(k_gs_block, dim3(1), dim3(kGsBlock), 0, s, A->indptr, A->indices, A->data,
+    hipLaunchKernelGGL(k_gs_block<BLK>, dim3(1), dim3(kGsBlock), 0, s, A->indptr, A->indices, A->data,
                        G->rows, G->d_level_ptr, G->n_levels, iterations, x, b, done);
   } else {
     for (int it = 0; it < iterations; ++it) {
       for (int32_t l = 0; l < G->n_levels; ++l) {
         const int32_t a = G->level_ptr[l], cnt = G->level_ptr[l + 1] - a;
-        hipLaunchKernelGGL(k_gs_level, dim3((cnt + 255) / 256), dim3(256), 0, s, A->indptr,
+        hipLaunchKernelGGL(k_gs_level<BLK>, dim3((cnt + 255) / 256), dim3(256), 0, s, A->indptr,
                            A->indices, A->data, G->rows + a, cnt, x, b, done);
       }
     }
   }
   MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+// one iteration of a symmetric sweep = the forward schedule, then the backward one
+int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
+                  const int32_t* done, hipStream_t s) {
+  auto one = [&](const mlamg_gs* H, int it) {
+    return H->block ? gs_sweep_one<true>(H, x, b, it, done, s)
+                    : gs_sweep_one<false>(H, x, b, it, done, s);
+  };
+  if (!G->bwd) return one(G, iterations);
+  for (int it = 0; it < iterations; ++it) {
+    MLAMG_TRY(one(G, 1));
+    MLAMG_TRY(one(G->bwd, 1));
+  }
   return MLAMG_OK;
 }
 
@@ -666,12 +718,9 @@ static void setup_window(mlamg_gs* G, const std::vector<int32_t>& ip,
   }
 }
 
-extern "C" {
-
-int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
-  MLAMG_REQUIRE(A && out, "NULL argument");
-  MLAMG_REQUIRE(A->n_rows == A->n_cols, "square matrix required");
-  hipStream_t s = S(stream);
+// one sweep direction's schedule and packed copies
+static int gs_build(const mlamg_csr* A, bool backward, bool block, mlamg_gs** out,
+                    hipStream_t s) {
   const int64_t n = A->n_rows;
   // MLAMG_TIMING=1: host phase times of the schedule analysis on stderr
   static const bool timing = std::getenv("MLAMG_TIMING") != nullptr;
@@ -691,21 +740,26 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
   phase("copy_in");
   std::vector<int32_t> level(n, 0), req(n, 0);
   int32_t nlev = 0;
-  for (int64_t i = 0; i < n; ++i) {
+  // rows in sweep order; `before(j, i)`: row j is swept before row i
+  auto before = [backward](int64_t j, int64_t i) { return backward ? j > i : j < i; };
+  for (int64_t t = 0; t < n; ++t) {
+    const int64_t i = backward ? n - 1 - t : t;
     int32_t L = req[i];
     for (int k = ip[i]; k < ip[i + 1]; ++k) {
       const int32_t j = ij[k];
-      if (j < i) L = std::max(L, level[j] + 1);
+      if (j != i && before(j, i)) L = std::max(L, level[j] + 1);
     }
     level[i] = L;
     for (int k = ip[i]; k < ip[i + 1]; ++k) {
       const int32_t j = ij[k];
-      if (j > i) req[j] = std::max(req[j], L + 1);
+      if (j != i && before(i, j)) req[j] = std::max(req[j], L + 1);
     }
     nlev = std::max(nlev, L + 1);
   }
   auto* G = new mlamg_gs();
   G->A = A;
+  G->block = block;
+  G->backward = backward;
   G->n_levels = nlev;
   G->level_ptr.assign(nlev + 1, 0);
   for (int64_t i = 0; i < n; ++i) G->level_ptr[level[i] + 1]++;
@@ -757,6 +811,7 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
             ++c;
           }
         }
+        if (block) pdiag[p] = pdiag[p] != 0.0 ? 1.0 / pdiag[p] : 0.0;  // Dinv = pinv(A_ii)
       }
       phase("pack");
       const size_t m = std::max<size_t>((size_t)n * K, 1), nn = std::max<int64_t>(n, 1);
@@ -785,8 +840,34 @@ int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
   return MLAMG_OK;
 }
 
+extern "C" {
+
+int mlamg_gs_create_ex(const mlamg_csr* A, int sweep, int block, mlamg_gs** out, void* stream) {
+  MLAMG_REQUIRE(A && out, "NULL argument");
+  MLAMG_REQUIRE(A->n_rows == A->n_cols, "square matrix required");
+  MLAMG_REQUIRE(sweep >= 0 && sweep <= 2, "sweep must be 0 forward, 1 backward, 2 symmetric");
+  MLAMG_REQUIRE(block == 0 || block == 1, "block must be 0 or 1");
+  hipStream_t s = S(stream);
+  mlamg_gs* G = nullptr;
+  MLAMG_TRY(gs_build(A, sweep == 1, block == 1, &G, s));
+  if (sweep == 2) {
+    int rc = gs_build(A, true, block == 1, &G->bwd, s);
+    if (rc != MLAMG_OK) {
+      mlamg_gs_destroy(G);
+      return rc;
+    }
+  }
+  *out = G;
+  return MLAMG_OK;
+}
+
+int mlamg_gs_create(const mlamg_csr* A, mlamg_gs** out, void* stream) {
+  return mlamg_gs_create_ex(A, 0, 0, out, stream);
+}
+
 int mlamg_gs_destroy(mlamg_gs* G) {
   if (G) {
+    if (G->bwd) mlamg_gs_destroy(G->bwd);
     for (void* q : {(void*)G->rows, (void*)G->d_level_ptr, (void*)G->pk_col, (void*)G->pk_val,
                     (void*)G->pk_diag, (void*)G->b_lvl, (void*)G->wcol, (void*)G->d_clev,
                     (void*)G->win_xl})

@@ -136,6 +136,13 @@ SIGNATURES = {
     "mlamg_lloyd_cluster": (c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp, P_i32, c_vp]),
     "mlamg_lloyd_cluster_canon": (c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp, P_i32, c_vp]),
     "mlamg_gs_create": (c_int, [c_vp, c_vpp, c_vp]),
+    "mlamg_gs_create_ex": (c_int, [c_vp, c_int, c_int, c_vpp, c_vp]),
+    "mlamg_symmetric_strength": (c_int, [c_vp, c_dbl, c_vpp, c_vp]),
+    "mlamg_standard_aggregation": (c_int, [c_vp, c_vp, c_vp, P_i64, P_i32, c_vp]),
+    "mlamg_fit_candidates": (c_int, [c_vp, c_vp, c_dbl, c_vpp, c_vp, c_vp]),
+    "mlamg_csr_sub": (c_int, [c_vp, c_vp, c_vpp, c_vp]),
+    "mlamg_diag_pinv": (c_int, [c_vp, c_vp, c_vp]),
+    "mlamg_dense_create_matrix": (c_int, [c_vp, c_i64, c_vpp, c_vp]),
     "mlamg_gs_destroy": (c_int, [c_vp]),
     "mlamg_gs_levels": (c_int, [c_vp, P_i32]),
     "mlamg_gs_sweep": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp]),

@@ -63,7 +63,7 @@ def csr_symmetric(M, rtol=0.0):
 
 class Level:
     __slots__ = ("A", "dinv", "P", "R", "Agg", "omega", "lam", "lanczos_iters", "n_seeds",
-                 "bf_sweeps", "seeds", "gs", "labels", "agg_col")
+                 "bf_sweeps", "seeds", "gs", "labels", "agg_col", "B")
 
     def __init__(self, A):
         self.A = A
@@ -77,6 +77,7 @@ class Level:
         self.gs = None
         self.labels = None  # per-node aggregate seed (node id, -1 none) when built by BF
         self.agg_col = None  # per-node aggregate column (int32 device tensor, -1 none)
+        self.B = None  # near-nullspace candidate fitted at this level (pyamg_sa)
 
 
 _PHASES = ("count", "alloc", "expand", "sort", "runsum", "emit", "finalize", "free")
@@ -549,6 +550,178 @@ class Hierarchy:
         tm["total"] = time.perf_counter() - t_all
         H.timings = tm
         return H
+
+    @classmethod
+    def pyamg_sa(cls, A, *, max_levels=10, max_coarse=10, theta=0.0, omega=4.0 / 3.0,
+                 improve_iterations=4, rho="lanczos", B=None, fine_format="csr_stream",
+                 coarse_format="exact", verbose=False):
+        """pyamg.aggregation.smoothed_aggregation_solver(A, max_levels=max_levels) with pyamg's
+        defaults — the multilevel solver of the reference's PyAMG preconditioner
+        (ns/preconditioner/PyAMG.py:94) — built on the GPU. Per level, while n > max_coarse
+        and fewer than max_levels levels:
+          C = symmetric_strength_of_connection(A, theta)          mlamg_symmetric_strength
+          AggOp = standard_aggregation(C)                          mlamg_standard_aggregation
+          level 0: B <- 4 symmetric block Gauss-Seidel sweeps on A B = 0 from B = ones
+                   (improve_candidates, level 0 only)              mlamg_gs_create_ex
+          T, B_c = fit_candidates(AggOp, B)                        mlamg_fit_candidates
+          P = T - (omega / rho) (D^-1 A) T  (jacobi_prolongation_smoother: D^-1 A by row
+              scaling with get_diagonal(inv=True), scaled by omega / rho, times T, subtracted)
+          R = P^T;  A_c = (R A) P
+        Coarsest level: scipy.linalg.pinv(A_c) applied as a dense product (pyamg's 'pinv'
+        coarse solver; the same scipy call). Smoother: symmetric block Gauss-Seidel, one
+        iteration before and after the coarse correction (pyamg's presmoother/postsmoother).
+        rho: rho(D^-1 A); 'lanczos' (default) the converged device Lanczos value, 'arnoldi'
+        pyamg's approximate_spectral_radius estimate (15-step Arnoldi from np.random.rand: draws
+        from numpy's global generator, as pyamg does), or a number / per-level list.
+        pyamg is absent here: parity unpinned; every setup kernel is bitwise the oracle's
+        restatement (oracle/oracle.c pyamg_*). Summation orders of pyamg's BSR products are not
+        restated (the Galerkin product sums over k ascending, as scipy's CSR/CSC kernels do)."""
+        from .multigrid import GaussSeidel
+        if max_levels < 1:
+            raise ValueError("max_levels must be >= 1")
+        H = cls()
+        H.recipe = "pyamg_sa"
+        H.jacobi_weight = None
+        t_all = time.perf_counter()
+        A_dev = as_device(A)
+        dev = _device()
+        n0 = A_dev.shape[0]
+        if B is None:
+            Bv = torch.ones(n0, dtype=torch.float64, device=dev)
+        else:
+            Bn = np.asarray(B, dtype=np.float64)
+            if Bn.size != n0:
+                raise NotImplementedError("one near-nullspace candidate (B of shape (n, 1))")
+            Bv = to_device_vec(Bn.reshape(-1)).clone()
+        tm = {"strength": 0.0, "aggregation": 0.0, "candidates": 0.0, "rho": 0.0,
+              "prolongator": 0.0, "galerkin": 0.0}
+        H.galerkin_s = []
+        while A_dev.shape[0] > max_coarse and len(H.levels) + 1 < max_levels:
+            n = A_dev.shape[0]
+            lvl = len(H.levels)
+            L = Level(A_dev)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            h = ctypes.c_void_p()
+            call("mlamg_symmetric_strength", A_dev.handle, float(theta), ctypes.byref(h),
+                 stream_ptr())
+            C = DeviceCSR(h)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            agg = torch.empty(n, dtype=torch.int32, device=dev)
+            cpts = torch.empty(n, dtype=torch.int32, device=dev)
+            k, rounds = ctypes.c_int64(), ctypes.c_int32()
+            call("mlamg_standard_aggregation", C.handle, ptr(agg), ptr(cpts), ctypes.byref(k),
+                 ctypes.byref(rounds), stream_ptr())
+            del C
+            k = int(k.value)
+            if k == 0:
+                raise ValueError(f"level {lvl}: standard aggregation found no aggregate")
+            L.Agg = aggregate_op_device(agg, k)
+            L.agg_col = agg
+            L.seeds = cpts[:k]
+            L.n_seeds = k
+            L.bf_sweeps = int(rounds.value)
+            t2 = time.perf_counter()
+            if lvl == 0 and improve_iterations > 0:
+                gsi = GaussSeidel(A_dev, "symmetric", block=True)
+                gsi.sweep(Bv, torch.zeros_like(Bv), int(improve_iterations))
+                del gsi
+            L.B = Bv
+            h = ctypes.c_void_p()
+            Bc = torch.empty(k, dtype=torch.float64, device=dev)
+            call("mlamg_fit_candidates", L.Agg.handle, ptr(Bv), 1e-10, ctypes.byref(h), ptr(Bc),
+                 stream_ptr())
+            T = DeviceCSR(h)
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            dinv = torch.empty(n, dtype=torch.float64, device=dev)
+            call("mlamg_diag_pinv", A_dev.handle, ptr(dinv), stream_ptr())
+            h = ctypes.c_void_p()
+            call("mlamg_csr_scale_rows", A_dev.handle, ptr(dinv), 0, ctypes.byref(h),
+                 stream_ptr())
+            DinvA = DeviceCSR(h)
+            if rho == "lanczos":
+                lam, L.lanczos_iters = lambda_max_dinv_a(A_dev)
+                L.lam = abs(lam)
+            elif rho == "arnoldi":
+                from .strength import approximate_spectral_radius
+                L.lam = approximate_spectral_radius(DinvA)
+            else:
+                r = _level_item(rho, lvl) if isinstance(rho, (list, tuple)) else rho
+                if r is None:
+                    raise ValueError(f"no rho given for level {lvl}")
+                L.lam = float(r)
+            t4 = time.perf_counter()
+            L.omega = omega / L.lam
+            h = ctypes.c_void_p()
+            cvec = torch.full((n,), L.omega, dtype=torch.float64, device=dev)
+            call("mlamg_csr_scale_rows", DinvA.handle, ptr(cvec), 0, ctypes.byref(h),
+                 stream_ptr())
+            DinvA = DeviceCSR(h)
+            M = DinvA @ T
+            del DinvA
+            h = ctypes.c_void_p()
+            call("mlamg_csr_sub", T.handle, M.handle, ctypes.byref(h), stream_ptr())
+            L.P = DeviceCSR(h)
+            del M, T
+            L.R = L.P.transpose()
+            L.dinv = dinv
+            torch.cuda.synchronize()
+            t5 = time.perf_counter()
+            A_next = galerkin(L.R, A_dev, L.P)
+            torch.cuda.synchronize()
+            t6 = time.perf_counter()
+            for key, dt in (("strength", t1 - t0), ("aggregation", t2 - t1),
+                            ("candidates", t3 - t2), ("rho", t4 - t3),
+                            ("prolongator", t5 - t4), ("galerkin", t6 - t5)):
+                tm[key] += dt
+            H.galerkin_s.append(round(t6 - t5, 4))
+            H.levels.append(L)
+            if verbose:
+                print(f"[mlamg pyamg_sa] level {lvl}: n={n} nnz={A_dev.nnz} aggregates={k} "
+                      f"rounds={L.bf_sweeps} rho={L.lam:.6g} P nnz={L.P.nnz} -> "
+                      f"n_c={A_next.shape[0]} nnz_c={A_next.nnz}", flush=True)
+            A_dev = A_next
+            Bv = Bc
+        H.Ac = A_dev
+        H.B_coarse = Bv
+        call("mlamg_scratch_trim", None)
+        t7 = time.perf_counter()
+        if H.levels:
+            H.apply_formats(fine_format, coarse_format)
+        t8 = time.perf_counter()
+        H._finalize_pinv()
+        torch.cuda.synchronize()
+        tm["formats"] = t8 - t7
+        tm["coarse_and_smoothers"] = time.perf_counter() - t8
+        tm["total"] = time.perf_counter() - t_all
+        H.timings = tm
+        return H
+
+    def _finalize_pinv(self):
+        """pyamg's default coarse solver ('pinv': scipy.linalg.pinv of the dense A_c, applied as
+        a product) and symmetric block Gauss-Seidel V(1,1) smoothing on every level."""
+        import scipy.linalg
+        from .multigrid import GaussSeidel
+        self.nu_pre = self.nu_post = 1
+        Ad = self.Ac.to_scipy().toarray()
+        Pinv = np.ascontiguousarray(scipy.linalg.pinv(Ad), dtype=np.float64)
+        self.coarse_pinv = Pinv
+        h = ctypes.c_void_p()
+        call("mlamg_dense_create_matrix", Pinv.ctypes.data_as(ctypes.c_void_p),
+             int(Pinv.shape[0]), ctypes.byref(h), stream_ptr())
+        self.dense = h
+        hh = ctypes.c_void_p()
+        call("mlamg_hier_create", ctypes.byref(hh))
+        self.handle = hh
+        for L in self.levels:
+            call("mlamg_hier_add_level", hh, L.A.handle, ptr(L.dinv), L.P.handle, L.R.handle)
+        call("mlamg_hier_set_coarse", hh, self.Ac.handle, self.dense)
+        call("mlamg_hier_set_smoothing", hh, 1, 1)
+        for i, L in enumerate(self.levels):
+            L.gs = GaussSeidel(L.A, "symmetric", block=True)
+            call("mlamg_hier_set_level_smoother", hh, i, L.gs.handle)
 
     # coarsest solve: a dense inverse up to this many rows (its setup is O(n_c^3)), above it
     # PCG preconditioned by an inner hierarchy of the coarse operator (csrc/pcg.hip)

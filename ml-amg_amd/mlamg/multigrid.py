@@ -74,12 +74,22 @@ def jacobi(A, b, x, Dinv=None, omega=0.666, nu=2):
 
 
 class GaussSeidel:
-    """Level-scheduled forward Gauss-Seidel with pyamg relaxation.gauss_seidel semantics."""
+    """Level-scheduled Gauss-Seidel: pyamg relaxation.gauss_seidel semantics (block=False, the
+    reference driver's forward sweep), or relaxation.block_gauss_seidel with 1 x 1 blocks
+    (block=True: pyamg's smoothed-aggregation smoother). sweep: 'forward', 'backward' or
+    'symmetric' (forward then backward, per iteration)."""
 
-    def __init__(self, A_dev):
+    SWEEPS = {"forward": 0, "backward": 1, "symmetric": 2}
+
+    def __init__(self, A_dev, sweep="forward", block=False):
+        if sweep not in self.SWEEPS:
+            raise ValueError("valid sweep directions are 'forward', 'backward', and 'symmetric'")
         self.A = A_dev
+        self.sweep_dir = sweep
+        self.block = bool(block)
         h = ctypes.c_void_p()
-        call("mlamg_gs_create", A_dev.handle, ctypes.byref(h), stream_ptr())
+        call("mlamg_gs_create_ex", A_dev.handle, self.SWEEPS[sweep], int(self.block),
+             ctypes.byref(h), stream_ptr())
         self.handle = h
         n = ctypes.c_int32()
         call("mlamg_gs_levels", h, ctypes.byref(n))

@@ -48,6 +48,11 @@ class _Options:
             return self._petsc.getInt(key, default)
         return int(self.store.get(key, default))
 
+    def getString(self, key, default):
+        if self._petsc is not None:  # pragma: no cover
+            return self._petsc.getString(key, default)
+        return str(self.store.get(key, default))
+
     def getBool(self, key, default):
         if self._petsc is not None:  # pragma: no cover
             return self._petsc.getBool(key, default)
@@ -145,10 +150,14 @@ class MLAMG:
 class MultilevelPC(MLAMG):
     """The PyAMG PC (ns/preconditioner/PyAMG.py:13-130) on the MI355X.
 
-    Setup (:79-100): a multilevel smoothed-aggregation hierarchy of the operator, at most
-    '<prefix>pyamg_amg_max_levels' levels (default 10, :53) — built on the device (seeded
-    Bellman-Ford aggregates, SA prolongators, dense coarsest level) in place of pyamg's
-    smoothed_aggregation_solver (absent here).
+    Setup (:79-100): `pyamg.aggregation.smoothed_aggregation_solver(P, max_levels=...)` (:94)
+    with at most '<prefix>pyamg_amg_max_levels' levels (default 10, :53), built on the device
+    with pyamg's default recipe (Hierarchy.pyamg_sa: symmetric strength, standard aggregation,
+    candidate improvement by symmetric block Gauss-Seidel, fit_candidates, Jacobi-smoothed P
+    with omega 4/3 / rho(D^-1 A), max_coarse 10, pinv coarse solve, symmetric block Gauss-Seidel
+    V(1,1)); pyamg itself is absent, so parity is unpinned (bitwise the oracle's restatement).
+    Option '<prefix>pyamg_amg_recipe' = 'mlamg_sa' selects this package's own SA hierarchy
+    instead (seeded Bellman-Ford aggregates, Jacobi smoothing, dense coarsest level).
     Apply (:118-120), `Amg.solve(b, tol=amg_rtol, accel='gmres' if amg_precondition_with_gmres
     else None)`: zero initial guess and a tolerance relative to ||b|| (pyamg's solve scales tol
     by ||b||, and its default maxiter is 100).
@@ -178,8 +187,14 @@ class MultilevelPC(MLAMG):
         opts = _Options()
         prefix = ((pc.getOptionsPrefix() if hasattr(pc, "getOptionsPrefix") else "") or "")
         levels = opts.getInt(f"{prefix}{self._prefix}amg_max_levels", 10)
-        self.H = Hierarchy.build(A, alpha=self.alpha, max_levels=levels,
-                                 jacobi_weight=self.jacobi_weight)
+        recipe = opts.getString(f"{prefix}{self._prefix}amg_recipe", "pyamg_sa")
+        if recipe == "pyamg_sa":
+            self.H = Hierarchy.pyamg_sa(A, max_levels=levels)
+        elif recipe == "mlamg_sa":
+            self.H = Hierarchy.build(A, alpha=self.alpha, max_levels=levels,
+                                     jacobi_weight=self.jacobi_weight)
+        else:
+            raise ValueError(f"unknown amg_recipe {recipe!r} (pyamg_sa, mlamg_sa)")
 
     def _apply(self, pc, X, Y):
         b = X.array_r if hasattr(X, "array_r") else np.asarray(X)

@@ -18,6 +18,13 @@
  *                           (called at ns/lib/graph.py:232), sequential
  *   canon_lloyd_cluster     same with the device's label rule (min cluster index over tight
  *                           pull neighbours)
+ *   pyamg_symmetric_strength, pyamg_standard_aggregation, pyamg_block_gauss_seidel,
+ *   pyamg_fit_candidates    pyamg 4.x/5.x amg_core symmetric_strength_of_connection,
+ *                           standard_aggregation, block_gauss_seidel (1 x 1 blocks) and
+ *                           fit_candidates_common (one candidate): the setup and smoother of
+ *                           pyamg.aggregation.smoothed_aggregation_solver, which the reference's
+ *                           PyAMG preconditioner builds (ns/preconditioner/PyAMG.py:94). pyamg is
+ *                           absent: restated from its published algorithm, parity unpinned.
  */
 #include <float.h>
 #include <math.h>
@@ -296,3 +303,152 @@ int lloyd_cluster(int64_t n, const int32_t* ip, const int32_t* ij, const double*
   }
 PYAMG_BF(pyamg_bellman_ford, float, FLT_MAX)
 PYAMG_BF(pyamg_bellman_ford_f64, double, DBL_MAX)
+
+/* ---------------------------------------------------------------- pyamg smoothed aggregation */
+/* amg_core symmetric_strength_of_connection + pyamg's |.| and scale_rows_by_largest_entry.
+ * sp (n+1), sj/sx (capacity nnz); returns nnz kept. */
+int64_t pyamg_symmetric_strength(int64_t n, const int32_t* ip, const int32_t* ij,
+                                 const double* ax, double theta, int32_t* sp, int32_t* sj,
+                                 double* sx) {
+  double* dg = (double*)malloc(sizeof(double) * (n ? n : 1));
+  for (int64_t i = 0; i < n; ++i) {
+    double d = 0.0;
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k)
+      if (ij[k] == i) d += ax[k];
+    dg[i] = fabs(d);
+  }
+  int64_t nnz = 0;
+  sp[0] = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const double eps = theta * theta * dg[i];
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
+      const int32_t j = ij[k];
+      const double a = ax[k];
+      if (j == i || a * a >= eps * dg[j]) {
+        sj[nnz] = j;
+        sx[nnz] = a;
+        ++nnz;
+      }
+    }
+    sp[i + 1] = (int32_t)nnz;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    double mx = 0.0;
+    for (int32_t k = sp[i]; k < sp[i + 1]; ++k) mx = fmax(mx, fabs(sx[k]));
+    const double inv = mx != 0.0 ? 1.0 / mx : 0.0;
+    for (int32_t k = sp[i]; k < sp[i + 1]; ++k) sx[k] = fabs(sx[k]) * inv;
+  }
+  free(dg);
+  return nnz;
+}
+
+/* amg_core standard_aggregation, literally: x[n] aggregate (-1 none), y[n] Cpts; returns the
+ * number of aggregates */
+int64_t pyamg_standard_aggregation(int64_t n, const int32_t* ip, const int32_t* ij, int32_t* x,
+                                   int32_t* y) {
+  for (int64_t i = 0; i < n; ++i) x[i] = 0;
+  int32_t next = 1;
+  for (int64_t i = 0; i < n; ++i) { /* pass 1 */
+    if (x[i]) continue;
+    int has_agg = 0, has_nb = 0;
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
+      const int32_t j = ij[k];
+      if (j != i) {
+        has_nb = 1;
+        if (x[j]) {
+          has_agg = 1;
+          break;
+        }
+      }
+    }
+    if (!has_nb) {
+      x[i] = -(int32_t)n;
+    } else if (!has_agg) {
+      x[i] = next;
+      y[next - 1] = (int32_t)i;
+      for (int32_t k = ip[i]; k < ip[i + 1]; ++k) x[ij[k]] = next;
+      ++next;
+    }
+  }
+  for (int64_t i = 0; i < n; ++i) { /* pass 2 */
+    if (x[i]) continue;
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
+      const int32_t xj = x[ij[k]];
+      if (xj > 0) {
+        x[i] = -xj;
+        break;
+      }
+    }
+  }
+  --next;
+  for (int64_t i = 0; i < n; ++i) { /* pass 3 */
+    const int32_t xi = x[i];
+    if (xi != 0) {
+      if (xi > 0) x[i] = xi - 1;
+      else if (xi == -(int32_t)n) x[i] = -1;
+      else x[i] = -xi - 1;
+      continue;
+    }
+    x[i] = next;
+    y[next] = (int32_t)i;
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k)
+      if (x[ij[k]] == 0) x[ij[k]] = next;
+    ++next;
+  }
+  return next;
+}
+
+/* pyamg relaxation.block_gauss_seidel with blocksize 1 (amg_core block_gauss_seidel; Dinv from
+ * get_block_diag + pinv_array: 1 / a_ii, 0 for a zero or missing diagonal). sweep 0 forward,
+ * 1 backward, 2 symmetric (forward then backward, per iteration). */
+static void bgs_once(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
+                     const double* dinv, double* x, const double* b, int backward) {
+  for (int64_t t = 0; t < n; ++t) {
+    const int64_t i = backward ? n - 1 - t : t;
+    double rsum = b[i];
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
+      const int32_t j = ij[k];
+      if (j == i) continue;
+      const double axl = 0.0 + ax[k] * x[j];
+      rsum -= axl;
+    }
+    x[i] = 0.0 + dinv[i] * rsum;
+  }
+}
+
+void pyamg_block_gauss_seidel(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
+                              double* x, const double* b, int iterations, int sweep) {
+  double* dinv = (double*)malloc(sizeof(double) * (n ? n : 1));
+  for (int64_t i = 0; i < n; ++i) {
+    double d = 0.0;
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k)
+      if (ij[k] == i) d = ax[k]; /* the stored diagonal (the last one, as the sweeps read it) */
+    dinv[i] = d != 0.0 ? 1.0 / d : 0.0;
+  }
+  for (int it = 0; it < iterations; ++it) {
+    if (sweep == 0 || sweep == 2) bgs_once(n, ip, ij, ax, dinv, x, b, 0);
+    if (sweep == 1 || sweep == 2) bgs_once(n, ip, ij, ax, dinv, x, b, 1);
+  }
+  free(dinv);
+}
+
+/* fit_candidates_common with K1 = K2 = 1: agg[n] (-1 none), k aggregates; T values (per row
+ * with an aggregate, row order) into tx, Bc[k] */
+void pyamg_fit_candidates(int64_t n, const int32_t* agg, int64_t k, const double* B, double tol,
+                          double* tx, double* Bc) {
+  double* s = (double*)calloc(k ? k : 1, sizeof(double));
+  double* scale = (double*)malloc(sizeof(double) * (k ? k : 1));
+  for (int64_t i = 0; i < n; ++i) /* AggOp.tocsc(): every column's rows ascending */
+    if (agg[i] >= 0) s[agg[i]] += B[i] * B[i];
+  for (int64_t j = 0; j < k; ++j) {
+    const double nrm = sqrt(s[j]);
+    const double thr = tol * nrm;
+    scale[j] = nrm > thr ? 1.0 / nrm : 0.0;
+    Bc[j] = nrm > thr ? nrm : 0.0;
+  }
+  int64_t o = 0;
+  for (int64_t i = 0; i < n; ++i)
+    if (agg[i] >= 0) tx[o++] = B[i] * scale[agg[i]];
+  free(s);
+  free(scale);
+}

@@ -41,6 +41,13 @@ def lib():
         L.lloyd_cluster.argtypes = [i64, vp, vp, vp, ctypes.c_int32, vp, ctypes.c_int, vp, vp,
                                     ctypes.c_int]
         L.lloyd_cluster.restype = ctypes.c_int
+        L.pyamg_symmetric_strength.argtypes = [i64, vp, vp, vp, ctypes.c_double, vp, vp, vp]
+        L.pyamg_symmetric_strength.restype = i64
+        L.pyamg_standard_aggregation.argtypes = [i64, vp, vp, vp, vp]
+        L.pyamg_standard_aggregation.restype = i64
+        L.pyamg_block_gauss_seidel.argtypes = [i64, vp, vp, vp, vp, vp, ctypes.c_int,
+                                               ctypes.c_int]
+        L.pyamg_fit_candidates.argtypes = [i64, vp, i64, vp, ctypes.c_double, vp, vp]
         _LIB = L
     return _LIB
 
@@ -714,3 +721,143 @@ def strength_measure(A, name, rho=None):
     if name == "olson":
         return ev + sp.csr_matrix((1. / np.abs(A.data), A.indices, A.indptr), A.shape)
     raise KeyError(name)
+
+
+# --------------------------------------------------------------------------------------------
+# pyamg.aggregation.smoothed_aggregation_solver with its defaults (pyamg 4.x/5.x, absent here:
+# restated from its published algorithm; parity unpinned), the multilevel solver the reference's
+# PyAMG preconditioner builds (ns/preconditioner/PyAMG.py:94) and applies (:119). The amg_core
+# loops are in oracle/oracle.c; the scipy steps are pyamg's own scipy calls.
+
+_SWEEPS = {"forward": 0, "backward": 1, "symmetric": 2}
+
+
+def pyamg_symmetric_strength(A, theta=0.0):
+    """pyamg.strength.symmetric_strength_of_connection(A, theta) on a CSR matrix."""
+    ip, ij, ax = _csr_arrays(A)
+    n = A.shape[0]
+    sp_ = np.empty(n + 1, dtype=np.int32)
+    sj = np.empty(max(len(ij), 1), dtype=np.int32)
+    sx = np.empty(max(len(ij), 1), dtype=np.float64)
+    nnz = lib().pyamg_symmetric_strength(n, _p(ip), _p(ij), _p(ax), float(theta), _p(sp_),
+                                         _p(sj), _p(sx))
+    return sp.csr_matrix((sx[:nnz], sj[:nnz], sp_), shape=A.shape)
+
+
+def pyamg_standard_aggregation(C):
+    """pyamg.aggregation.standard_aggregation(C): (per-row aggregate, -1 none; Cpts; count)."""
+    ip, ij, _ = _csr_arrays(C)
+    n = C.shape[0]
+    x = np.empty(max(n, 1), dtype=np.int32)
+    y = np.empty(max(n, 1), dtype=np.int32)
+    k = lib().pyamg_standard_aggregation(n, _p(ip), _p(ij), _p(x), _p(y))
+    return x[:n], y[:k].copy(), int(k)
+
+
+def pyamg_aggop(agg, k):
+    """AggOp as standard_aggregation returns it (rows with agg == -1 empty)."""
+    agg = np.asarray(agg)
+    rows = np.nonzero(agg >= 0)[0]
+    return sp.csr_matrix((np.ones(len(rows)), (rows, agg[rows])), shape=(len(agg), k))
+
+
+def pyamg_block_gauss_seidel(A, x, b, iterations=1, sweep="forward"):
+    """pyamg.relaxation.relaxation.block_gauss_seidel(A, x, b, iterations, sweep) with 1 x 1
+    blocks, in place on x (float64, contiguous)."""
+    ip, ij, ax = _csr_arrays(A)
+    assert x.dtype == np.float64 and x.flags.c_contiguous
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    lib().pyamg_block_gauss_seidel(A.shape[0], _p(ip), _p(ij), _p(ax), _p(x), _p(b),
+                                   int(iterations), _SWEEPS[sweep])
+    return x
+
+
+def pyamg_fit_candidates(agg, k, B, tol=1e-10):
+    """pyamg.aggregation.fit_candidates(AggOp, B[:, None], tol): (T as CSR, B_c)."""
+    agg = np.ascontiguousarray(agg, dtype=np.int32)
+    B = np.ascontiguousarray(B, dtype=np.float64).reshape(-1)
+    n = agg.shape[0]
+    rows = np.nonzero(agg >= 0)[0]
+    tx = np.empty(max(len(rows), 1))
+    Bc = np.empty(max(k, 1))
+    lib().pyamg_fit_candidates(n, _p(agg), int(k), _p(B), float(tol), _p(tx), _p(Bc))
+    T = sp.csr_matrix((tx[:len(rows)], (rows, agg[rows])), shape=(n, k))
+    return T, Bc[:k].copy()
+
+
+def pyamg_dinv(A):
+    """pyamg.util.utils.get_diagonal(A, inv=True): 1 / diag, 0 where diag == 0."""
+    D = A.diagonal()
+    Dinv = np.zeros_like(D, dtype=np.float64)
+    mask = D != 0.0
+    Dinv[mask] = 1.0 / D[mask]
+    return Dinv
+
+
+def pyamg_jacobi_prolongation(A, T, rho, omega=4.0 / 3.0):
+    """pyamg jacobi_prolongation_smoother(A, T, C, B, omega, degree=1, filter=False,
+    weighting='diagonal') with the spectral radius given: D_inv_S = scale_rows(A, D_inv)
+    (csr_scale_rows: a_ij * d_i, pattern and order kept), times (omega / rho) (data * c),
+    P = T - D_inv_S @ T (scipy csr_matmat, then the csr binop; zeros dropped). Columns sorted."""
+    A = sp.csr_matrix(A)
+    d = pyamg_dinv(A)
+    row = np.repeat(np.arange(A.shape[0]), np.diff(A.indptr))
+    S = sp.csr_matrix((A.data * d[row], A.indices.copy(), A.indptr.copy()), shape=A.shape)
+    c = omega / rho
+    S = sp.csr_matrix((S.data * c, S.indices, S.indptr), shape=A.shape)
+    P = sp.csr_matrix(T - S @ T)
+    P.sort_indices()
+    return P
+
+
+def pyamg_sa_setup(A, rhos=None, max_levels=10, max_coarse=10, theta=0.0, omega=4.0 / 3.0,
+                   improve_iterations=4, B=None):
+    """The levels of smoothed_aggregation_solver(A, max_levels=...): a list of dicts (A, C,
+    agg, k, B, T, P, R, rho) and the coarsest operator. rhos: per-level rho(D^-1 A) (default:
+    scipy eigs of D^-1 A, largest magnitude). A_c = (P^T A) P in scipy."""
+    A = canonical(sp.csr_matrix(A, dtype=np.float64))
+    Bv = np.ones(A.shape[0]) if B is None else np.asarray(B, dtype=np.float64).reshape(-1).copy()
+    levels = []
+    while A.shape[0] > max_coarse and len(levels) + 1 < max_levels:
+        lvl = len(levels)
+        C = pyamg_symmetric_strength(A, theta)
+        agg, cpts, k = pyamg_standard_aggregation(C)
+        if lvl == 0 and improve_iterations > 0:
+            pyamg_block_gauss_seidel(A, Bv, np.zeros(A.shape[0]), improve_iterations,
+                                     "symmetric")
+        T, Bc = pyamg_fit_candidates(agg, k, Bv)
+        if rhos is None:
+            Dinv_A = sp.diags(pyamg_dinv(A)) @ A
+            rho = float(np.abs(spla.eigs(Dinv_A, k=1, which="LM",
+                                         return_eigenvectors=False)[0]))
+        else:
+            rho = float(rhos[lvl])
+        P = pyamg_jacobi_prolongation(A, T, rho, omega)
+        R = sp.csr_matrix(P.T)
+        R.sort_indices()
+        levels.append({"A": A, "C": C, "agg": agg, "cpts": cpts, "k": k, "B": Bv.copy(),
+                       "T": T, "P": P, "R": R, "rho": rho})
+        A = canonical((P.T @ A) @ P)
+        Bv = Bc
+    return levels, A
+
+
+def pyamg_sa_vcycle(levels, Ac_pinv, b, x, lvl=0):
+    """pyamg MultilevelSolver.__solve(lvl, x, b, 'V') with block Gauss-Seidel symmetric pre/post
+    smoothing and the 'pinv' coarse solve (np.dot(pinv, b)); x updated in place."""
+    if not levels:
+        x[:] = Ac_pinv @ b
+        return x
+    L = levels[lvl]
+    A = L["A"]
+    pyamg_block_gauss_seidel(A, x, b, 1, "symmetric")
+    r = b - A @ x
+    bc = L["R"] @ r
+    xc = np.zeros_like(bc)
+    if lvl == len(levels) - 1:
+        xc[:] = Ac_pinv @ bc
+    else:
+        pyamg_sa_vcycle(levels, Ac_pinv, bc, xc, lvl + 1)
+    x += L["P"] @ xc
+    pyamg_block_gauss_seidel(A, x, b, 1, "symmetric")
+    return x
