@@ -41,6 +41,10 @@ struct mlamg_gs {
   double* pk_diag = nullptr;
   double* b_lvl = nullptr;
   int32_t max_off = 0;  // longest off-diagonal count
+  // level-ordered (row, first entry, length, 0) per position for the wave-cooperative sweep
+  // (rows with more than 8 off-diagonals, at most 128 entries per row; nullptr: none)
+  int32_t* wpos = nullptr;
+  int32_t max_len = 0;
   // windowed one-wave sweep (k_gs_win): x by level-order position in an LDS ring of 2^ring_log2
   // slots; wcol = the packed columns as positions (pads -1); chunks of levels staged into two
   // LDS buffers of win_cap + 1 positions; win_w = the widest level distance of a coupling
@@ -121,6 +125,124 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_block(const int32_t* __restrict
       const int32_t a = lptr[l], z = lptr[l + 1];
       for (int32_t t = a + (int32_t)threadIdx.x; t < z; t += kGsBlock) gs_row<BLK>(ip, ij, ax, rows[t], x, b);
       __syncthreads();
+    }
+  }
+}
+
+// One workgroup, rows with many off-diagonals (coarse Galerkin operators: 10-120 entries): 16
+// lanes per row, EPL entries per lane, 64 rows per pass. A row's lanes gather their entries'
+// x values in parallel and leave the products (and the diagonal) in LDS in stored order; the
+// row's first lane then folds them in that order — the same products, in the same order, as
+// gs_row — and stores x_i. The next level's first pass (position info from the level-ordered
+// `wpos` = (row, first entry, length), then its columns and values: none of it depends on x) is
+// loaded while this level computes, so a level's critical path is its x gathers, the fold and
+// the barrier.
+constexpr int kGsWaveBlock = 1024;
+constexpr int kGsWaveLPR = 16;
+constexpr int kGsWaveRows = kGsWaveBlock / kGsWaveLPR;
+
+template <int EPL>
+struct GsWaveRow {
+  int32_t row, len;
+  double bi;
+  int32_t col[EPL];
+  double val[EPL];
+};
+
+template <int EPL>
+__device__ __forceinline__ void gs_wave_load(GsWaveRow<EPL>& r, int32_t t, int32_t z, int lane,
+                                             const int4* __restrict__ wpos,
+                                             const int32_t* __restrict__ ij,
+                                             const double* __restrict__ ax,
+                                             const double* __restrict__ b) {
+  const bool live = t < z;
+  const int4 w = live ? wpos[t] : make_int4(0, 0, 0, 0);
+  r.row = live ? w.x : -1;  // an empty row still updates (block_gauss_seidel: x_i = 0 + 0 b_i)
+  r.len = w.z;
+  r.bi = live ? b[w.x] : 0.0;
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int k = lane + e * kGsWaveLPR;
+    const bool ok = k < w.z;
+    r.col[e] = ok ? ij[w.y + k] : -1;
+    r.val[e] = ok ? ax[w.y + k] : 0.0;
+  }
+}
+
+template <int EPL, bool BLK>
+__global__ __launch_bounds__(kGsWaveBlock) void k_gs_wave(const int4* __restrict__ wpos,
+                                                         const int32_t* __restrict__ ij,
+                                                         const double* __restrict__ ax,
+                                                         const int32_t* __restrict__ lptr,
+                                                         int32_t n_levels, int iterations,
+                                                         double* x, const double* __restrict__ b,
+                                                         const int32_t* done) {
+  constexpr int SPAN = kGsWaveLPR * EPL;  // LDS slots per row
+  __shared__ double pv[kGsWaveRows * SPAN];
+  __shared__ int32_t pc[kGsWaveRows * SPAN];
+  if (done && *done) return;
+  const int tid = threadIdx.x;
+  const int g = tid / kGsWaveLPR, lane = tid % kGsWaveLPR;
+  double* gv = pv + g * SPAN;
+  int32_t* gc = pc + g * SPAN;
+  for (int it = 0; it < iterations; ++it) {
+    GsWaveRow<EPL> cur, nxt;
+    gs_wave_load<EPL>(cur, lptr[0] + g, lptr[1], lane, wpos, ij, ax, b);
+    for (int32_t l = 0; l < n_levels; ++l) {
+      const int32_t a = lptr[l], z = lptr[l + 1];
+      // passes over the level's rows (uniform for the workgroup: the LDS fences are per wave)
+      for (int32_t t0 = a; t0 < z; t0 += kGsWaveRows) {
+        if (t0 > a) gs_wave_load<EPL>(cur, t0 + g, z, lane, wpos, ij, ax, b);
+        double p[EPL];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const int32_t j = cur.col[e];
+          const double xj = (j >= 0 && j != cur.row) ? x[j] : 0.0;
+          p[e] = j == cur.row ? cur.val[e] : (BLK ? 0.0 + cur.val[e] * xj : cur.val[e] * xj);
+        }
+        if (t0 == a && l + 1 < n_levels)
+          gs_wave_load<EPL>(nxt, lptr[l + 1] + g, lptr[l + 2], lane, wpos, ij, ax, b);
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const int k = lane + e * kGsWaveLPR;
+          gv[k] = p[e];
+          gc[k] = cur.col[e];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0 && cur.row >= 0) {
+          double s = gs_init<BLK>(cur.bi), diag = 0.0;
+          int k = 0;
+          // 8 LDS reads in flight, then the 8 ordered steps
+          for (; k + 8 <= cur.len; k += 8) {
+            double v[8];
+            int32_t c[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              v[u] = gv[k + u];
+              c[u] = gc[k + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              if (c[u] == cur.row) diag = v[u];
+              else s = BLK ? s - v[u] : s + v[u];
+            }
+          }
+          for (; k < cur.len; ++k) {
+            const double v = gv[k];
+            if (gc[k] == cur.row) diag = v;
+            else s = BLK ? s - v : s + v;
+          }
+          if (BLK) diag = diag != 0.0 ? 1.0 / diag : 0.0;
+          if (gs_upd<BLK>(diag)) x[cur.row] = gs_fin<BLK>(s, cur.bi, diag);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      __syncthreads();
+      cur = nxt;
     }
   }
 }
@@ -550,6 +672,11 @@ __global__ void k_gs_win_prep(const int32_t* __restrict__ rows, int64_t n,
   }
 }
 
+static bool gs_wave_disabled() {  // MLAMG_GS_NO_WAVE=1: A/B runs, tests
+  const char* e = std::getenv("MLAMG_GS_NO_WAVE");
+  return e && e[0] == '1';
+}
+
 static bool gs_win_disabled() {  // MLAMG_GS_NO_WIN=1: A/B runs, tests
   const char* e = std::getenv("MLAMG_GS_NO_WIN");
   return e && e[0] == '1';
@@ -605,7 +732,20 @@ static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int itera
       if (one) launch_gs_pipe<1, 8, BLK>(G, x, b, iterations, done, s);
       else launch_gs_pipe<2, 8, BLK>(G, x, b, iterations, done, s);
     }
-  } else if (G->max_level_rows <= kGsBlockMaxLevelRows && G->n_levels > 4) {
+  } else if (G->wpos && G->max_level_rows <= kGsBlockMaxLevelRows && G->n_levels > 4 &&
+             !gs_wave_disabled()) {
+    const int epl = (G->max_len + kGsWaveLPR - 1) / kGsWaveLPR;  // entries per lane
+    auto go = [&](auto e) {
+      hipLaunchKernelGGL((k_gs_wave<decltype(e)::value, BLK>), dim3(1), dim3(kGsWaveBlock), 0, s,
+                         reinterpret_cast<const int4*>(G->wpos), A->indices, A->data,
+                         G->d_level_ptr, G->n_levels, iterations, x, b, done);
+    };
+    if (epl <= 1) go(std::integral_constant<int, 1>());
+    else if (epl <= 2) go(std::integral_constant<int, 2>());
+    else if (epl <= 4) go(std::integral_constant<int, 4>());
+    else go(std::integral_constant<int, 8>());
+  } else if (G->max_level_rows <= kGsBlock && G->n_levels > 4) {
+    // one row per thread per level; wider levels go one launch per level over the whole chip
     hipLaunchKernelGGL(k_gs_block<BLK>, dim3(1), dim3(kGsBlock), 0, s, A->indptr, A->indices, A->data,
                        G->rows, G->d_level_ptr, G->n_levels, iterations, x, b, done);
   } else {
@@ -793,6 +933,24 @@ static int gs_build(const mlamg_csr* A, bool backward, bool block, mlamg_gs** ou
     }
     G->max_off = mo;
     const int K = mo <= 4 ? 4 : (mo <= 8 ? 8 : 0);
+    int32_t ml = 0;
+    for (int64_t i = 0; i < n; ++i) ml = std::max(ml, ip[i + 1] - ip[i]);
+    G->max_len = ml;
+    if (!K && ml <= 8 * kGsWaveLPR) {
+      std::vector<int32_t> wp((size_t)n * 4);
+      for (int64_t p = 0; p < n; ++p) {
+        const int32_t i = rows[p];
+        wp[4 * p] = i;
+        wp[4 * p + 1] = ip[i];
+        wp[4 * p + 2] = ip[i + 1] - ip[i];
+        wp[4 * p + 3] = 0;
+      }
+      if (hipMalloc(&G->wpos, sizeof(int32_t) * std::max<size_t>(wp.size(), 4)) == hipSuccess) {
+        if (n) (void)hipMemcpy(G->wpos, wp.data(), sizeof(int32_t) * wp.size(), hipMemcpyHostToDevice);
+      } else {
+        G->wpos = nullptr;  // optional: the plain one-workgroup kernel takes these rows
+      }
+    }
     if (K) {
       std::vector<double> ax(A->nnz);
       if (A->nnz)
@@ -870,7 +1028,7 @@ int mlamg_gs_destroy(mlamg_gs* G) {
     if (G->bwd) mlamg_gs_destroy(G->bwd);
     for (void* q : {(void*)G->rows, (void*)G->d_level_ptr, (void*)G->pk_col, (void*)G->pk_val,
                     (void*)G->pk_diag, (void*)G->b_lvl, (void*)G->wcol, (void*)G->d_clev,
-                    (void*)G->win_xl})
+                    (void*)G->win_xl, (void*)G->wpos})
       if (q) (void)hipFree(q);
     delete G;
   }

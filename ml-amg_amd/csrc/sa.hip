@@ -80,8 +80,15 @@ __global__ void k_ss_fill(const int32_t* __restrict__ ip, const int32_t* __restr
 // first independent set of that conflict relation, decided here in rounds: a row becomes a
 // non-root as soon as one such r is a root, a root once all of them are decided non-roots. The
 // smallest undecided row always decides, so rounds terminate; each thread walks a run of
-// consecutive rows in order, so a chain of decisions inside a run resolves in one round.
-constexpr int kSaRun = 32;
+// consecutive rows in order, so a chain of decisions inside a run resolves in one round, and a
+// row that must wait re-reads only the row it waits on until that row is decided.
+// rows per thread: long runs resolve chains of short-row operators in one round; an operator
+// with long rows (coarse Galerkin levels: ~30 entries, ~900 markers per decision) gets short
+// runs so that one round's work is spread over enough threads
+static int sa_run_len(const mlamg_csr* C) {
+  const double m = C->n_rows ? (double)C->nnz / (double)C->n_rows : 1.0;
+  return (int)std::max(1.0, std::min(32.0, 512.0 / (m * m)));
+}
 enum : int8_t { kSaUndecided = 0, kSaRoot = 1, kSaNonRoot = 2 };
 
 __global__ void k_sa_iso(const int32_t* __restrict__ ip, const int32_t* __restrict__ ij,
@@ -94,30 +101,32 @@ __global__ void k_sa_iso(const int32_t* __restrict__ ip, const int32_t* __restri
   iso[i] = f;
 }
 
-// 0 pending, else the decision; `st` entries only ever go from undecided to final
+// the decision of row i, or kSaUndecided with *blocker = the smallest undecided row among its
+// markers (decisions mostly arrive in row order, so it is usually the last one i waits for);
+// `st` entries only ever go from undecided to final
 __device__ int8_t sa_decide(int64_t i, const int32_t* __restrict__ ip,
                             const int32_t* __restrict__ ij, const int32_t* __restrict__ tp,
                             const int32_t* __restrict__ tj, const int8_t* __restrict__ iso,
-                            const int8_t* st) {
+                            const int8_t* st, int32_t* blocker) {
   if (iso[i]) return kSaNonRoot;
   for (int k = ip[i]; k < ip[i + 1]; ++k) {
     const int32_t j = ij[k];
     if (j < i && iso[j]) return kSaNonRoot;
   }
-  bool pending = false;
-  // markers of v: rows r < i with v a column of row r, and v itself
-  auto check = [&](int32_t v) -> bool {  // true: a root marks v
+  int32_t blk = INT32_MAX;
+  // markers of v: rows r < i with v a column of row r, and v itself; true: a root marks v
+  auto check = [&](int32_t v) -> bool {
     if (v < i) {
-      const int8_t s = __hip_atomic_load(st + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int8_t s = st[v];
       if (s == kSaRoot) return true;
-      pending |= s == kSaUndecided;
+      if (s == kSaUndecided) blk = min(blk, v);
     }
     for (int q = tp[v]; q < tp[v + 1]; ++q) {
       const int32_t r = tj[q];
       if (r >= i || r == v) continue;
-      const int8_t s = __hip_atomic_load(st + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int8_t s = st[r];
       if (s == kSaRoot) return true;
-      pending |= s == kSaUndecided;
+      if (s == kSaUndecided) blk = min(blk, r);
     }
     return false;
   };
@@ -126,29 +135,56 @@ __device__ int8_t sa_decide(int64_t i, const int32_t* __restrict__ ip,
     const int32_t j = ij[k];
     if (j != (int32_t)i && check(j)) return kSaNonRoot;
   }
-  return pending ? kSaUndecided : kSaRoot;
+  if (blk == INT32_MAX) return kSaRoot;
+  *blocker = blk;
+  return kSaUndecided;
 }
 
+// one round: a thread walks its run of rows in order (a chain of decisions inside the run
+// resolves in one round); an undecided row remembers the row it waits on and is re-examined only
+// once that row is decided (two byte reads per round until then). Reads of other threads'
+// decisions may be stale within a launch — they can only read as undecided: a delay, never a
+// wrong decision; the launch boundary makes every decision visible to the next round.
 __global__ void k_sa_round(const int32_t* __restrict__ ip, const int32_t* __restrict__ ij,
                            const int32_t* __restrict__ tp, const int32_t* __restrict__ tj,
                            const int8_t* __restrict__ iso, int64_t n, int8_t* st,
-                           int8_t* __restrict__ run_done, int32_t* __restrict__ pending) {
+                           int32_t* __restrict__ wait, int32_t* __restrict__ run_pos,
+                           int run_len, int32_t* __restrict__ pending) {
   const int64_t r = blockIdx.x * 256ll + threadIdx.x;
-  const int64_t a = r * kSaRun;
-  if (a >= n || run_done[r]) return;
-  const int64_t z = std::min<int64_t>(a + kSaRun, n);
+  if (r * run_len >= n) return;
+  const int64_t z = std::min<int64_t>((r + 1) * run_len, n);
+  int64_t first = run_pos[r];
+  if (first >= z) return;
   bool all = true;
-  for (int64_t i = a; i < z; ++i) {
-    if (st[i] != kSaUndecided) continue;
-    const int8_t d = sa_decide(i, ip, ij, tp, tj, iso, st);
+  for (int64_t i = first; i < z; ++i) {
+    if (st[i] != kSaUndecided) {
+      if (all) first = i + 1;
+      continue;
+    }
+    const int32_t w = wait[i];
+    if (w >= 0 && st[w] == kSaUndecided) {
+      all = false;
+      continue;
+    }
+    int32_t blk = -1;
+    const int8_t d = sa_decide(i, ip, ij, tp, tj, iso, st, &blk);
     if (d == kSaUndecided) {
+      wait[i] = blk;
       all = false;
     } else {
-      __hip_atomic_store(st + i, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st[i] = d;
+      if (all) first = i + 1;
     }
   }
-  if (all) run_done[r] = 1;
-  else atomicAdd(pending, 1);
+  run_pos[r] = (int32_t)first;
+  if (!all) atomicAdd(pending, 1);
+}
+
+__global__ void k_sa_runs_init(int64_t runs, int64_t n, int run_len,
+                               int32_t* __restrict__ run_pos, int32_t* __restrict__ wait) {
+  const int64_t r = blockIdx.x * 256ll + threadIdx.x;
+  if (r < runs) run_pos[r] = (int32_t)(r * run_len);
+  if (r < n) wait[r] = -1;
 }
 
 __global__ void k_sa_root_flag(const int8_t* __restrict__ st, int64_t n, int32_t* __restrict__ f) {
@@ -393,17 +429,20 @@ int mlamg_standard_aggregation(const mlamg_csr* C, int32_t* agg, int32_t* cpts, 
   if (n == 0) return MLAMG_OK;
   mlamg_csr* T = nullptr;
   MLAMG_TRY(transpose_impl(C, &T, s));
-  const int64_t runs = (n + kSaRun - 1) / kSaRun;
+  const int run_len = sa_run_len(C);
+  const int64_t runs = (n + run_len - 1) / run_len;
   constexpr int kBatch = 8;
-  int8_t *st = nullptr, *iso = nullptr, *run_done = nullptr;
-  int32_t *flag = nullptr, *id = nullptr, *ctr = nullptr;
+  int8_t *st = nullptr, *iso = nullptr;
+  int32_t *flag = nullptr, *id = nullptr, *ctr = nullptr, *run_pos = nullptr, *run_wait = nullptr;
   auto cleanup = [&]() {
-    for (void* q : {(void*)st, (void*)iso, (void*)run_done, (void*)flag, (void*)id, (void*)ctr})
+    for (void* q : {(void*)st, (void*)iso, (void*)run_pos, (void*)run_wait, (void*)flag,
+                    (void*)id, (void*)ctr})
       if (q) (void)hipFree(q);
     csr_free(T);
   };
   if (hipMalloc(&st, n) != hipSuccess || hipMalloc(&iso, n) != hipSuccess ||
-      hipMalloc(&run_done, runs) != hipSuccess ||
+      hipMalloc(&run_pos, sizeof(int32_t) * runs) != hipSuccess ||
+      hipMalloc(&run_wait, sizeof(int32_t) * n) != hipSuccess ||
       hipMalloc(&flag, sizeof(int32_t) * n) != hipSuccess ||
       hipMalloc(&id, sizeof(int32_t) * (n + 1)) != hipSuccess ||
       hipMalloc(&ctr, sizeof(int32_t) * (kBatch + 2)) != hipSuccess) {
@@ -412,7 +451,8 @@ int mlamg_standard_aggregation(const mlamg_csr* C, int32_t* agg, int32_t* cpts, 
     return MLAMG_ENOMEM;
   }
   (void)hipMemsetAsync(st, 0, n, s);
-  (void)hipMemsetAsync(run_done, 0, runs, s);
+  hipLaunchKernelGGL(k_sa_runs_init, gsa(n), dim3(256), 0, s, runs, n, run_len, run_pos,
+                     run_wait);
   hipLaunchKernelGGL(k_sa_iso, gsa(n), dim3(256), 0, s, C->indptr, C->indices, n, iso);
   // pass 1 in rounds, kBatch launches between host checks; the smallest undecided row decides
   // every round, so n + 1 rounds always suffice
@@ -427,7 +467,8 @@ int mlamg_standard_aggregation(const mlamg_csr* C, int32_t* agg, int32_t* cpts, 
     (void)hipMemsetAsync(ctr, 0, sizeof(int32_t) * kBatch, s);
     for (int b = 0; b < kBatch; ++b)
       hipLaunchKernelGGL(k_sa_round, gsa(runs), dim3(256), 0, s, C->indptr, C->indices,
-                         T->indptr, T->indices, iso, n, st, run_done, ctr + b);
+                         T->indptr, T->indices, iso, n, st, run_wait, run_pos, run_len,
+                         ctr + b);
     int32_t h[kBatch];
     (void)hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, s);
     hipError_t e = hipStreamSynchronize(s);

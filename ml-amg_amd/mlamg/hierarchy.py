@@ -624,9 +624,9 @@ class Hierarchy:
             L.bf_sweeps = int(rounds.value)
             t2 = time.perf_counter()
             if lvl == 0 and improve_iterations > 0:
-                gsi = GaussSeidel(A_dev, "symmetric", block=True)
-                gsi.sweep(Bv, torch.zeros_like(Bv), int(improve_iterations))
-                del gsi
+                # the same symmetric block sweep later smooths this level: one handle
+                L.gs = GaussSeidel(A_dev, "symmetric", block=True)
+                L.gs.sweep(Bv, torch.zeros_like(Bv), int(improve_iterations))
             L.B = Bv
             h = ctypes.c_void_p()
             Bc = torch.empty(k, dtype=torch.float64, device=dev)
@@ -720,7 +720,8 @@ class Hierarchy:
         call("mlamg_hier_set_coarse", hh, self.Ac.handle, self.dense)
         call("mlamg_hier_set_smoothing", hh, 1, 1)
         for i, L in enumerate(self.levels):
-            L.gs = GaussSeidel(L.A, "symmetric", block=True)
+            if L.gs is None:
+                L.gs = GaussSeidel(L.A, "symmetric", block=True)
             call("mlamg_hier_set_level_smoother", hh, i, L.gs.handle)
 
     # coarsest solve: a dense inverse up to this many rows (its setup is O(n_c^3)), above it

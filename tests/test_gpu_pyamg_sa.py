@@ -48,9 +48,23 @@ def _nonsym_pattern(n, seed):
     return M
 
 
+def _long_rows(n, per_row, seed):
+    """Symmetric, diagonally dominant, ~per_row entries per row (coarse-Galerkin-like rows; the
+    wave-cooperative Gauss-Seidel kernel and its chunk loop past 64 entries)."""
+    rng = np.random.default_rng(seed)
+    M = sp.random(n, n, density=per_row / (2.0 * n), random_state=rng, format="csr")
+    M.data[:] = -rng.uniform(0.1, 1.0, M.nnz)
+    M = sp.csr_matrix(M + M.T)
+    M = sp.csr_matrix(M + sp.diags(1.0 + np.asarray(abs(M).sum(axis=1)).ravel()))
+    M.sort_indices()
+    return M
+
+
 def _matrices(ml):
     P = ml.problems
     return {
+        "long_30": _long_rows(2500, 30, 4),
+        "long_90": _long_rows(1500, 90, 6),
         "chain_2000": P.poisson_1d(2000),
         "poisson_64": P.poisson_2d_5pt(64),
         "poisson3d_18": P.poisson_3d_7pt(18),
