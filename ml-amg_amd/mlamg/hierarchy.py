@@ -642,7 +642,8 @@ class Hierarchy:
                  stream_ptr())
             DinvA = DeviceCSR(h)
             if rho == "lanczos":
-                lam, L.lanczos_iters = lambda_max_dinv_a(A_dev)
+                # pyamg's own estimate is a 15-step Arnoldi value; 1e-10 is far tighter
+                lam, L.lanczos_iters = lambda_max_dinv_a(A_dev, tol=1e-10)
                 L.lam = abs(lam)
             elif rho == "arnoldi":
                 from .strength import approximate_spectral_radius
