@@ -45,6 +45,9 @@ struct mlamg_gs {
   // (rows with more than 8 off-diagonals, at most 128 entries per row; nullptr: none)
   int32_t* wpos = nullptr;
   int32_t max_len = 0;
+  // ring sweep (k_gs_ring): slot columns classified earlier (ring position) / later (-(c + 2))
+  int32_t* rcol = nullptr;
+  int32_t ring_log2_r = 0;
   // windowed one-wave sweep (k_gs_win): x by level-order position in an LDS ring of 2^ring_log2
   // slots; wcol = the packed columns as positions (pads -1); chunks of levels staged into two
   // LDS buffers of win_cap + 1 positions; win_w = the widest level distance of a coupling
@@ -321,6 +324,90 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_pipe(const int32_t* __restrict_
       __syncthreads();
       if (l + 1 < n_levels) cur = nxt;
     }
+  }
+}
+
+// Levels of 513..1024 rows with <= 4 off-diagonals (2-D five-point grids up to 1024^2): the
+// pipelined walk with the x values of the last W levels in an LDS ring indexed by level-order
+// position, W = the widest level distance of a coupling to an earlier level. A slot's column is
+// host-classified: a row swept earlier (its updated value: the ring) or later (its old value: read
+// from x while the structure is prefetched, two levels ahead, since nothing writes it before its
+// own level). A level's critical path is then LDS gathers, the ordered sum, the stores and the
+// barrier. Same products, same order, same division as gs_row.
+constexpr int kGsRingK = 4;
+struct GsRingRow {
+  int32_t row, pos;
+  double diag, bi;
+  int32_t col[kGsRingK];  // >= 0 ring position, -1 pad, <= -2 global column -(c + 2)
+  double val[kGsRingK], xo[kGsRingK];
+};
+
+__device__ __forceinline__ void gs_ring_struct(GsRingRow& q, int32_t a, int32_t z,
+                                               const int32_t* __restrict__ rows,
+                                               const int32_t* __restrict__ rcol,
+                                               const double* __restrict__ pval,
+                                               const double* __restrict__ pdiag,
+                                               const double* __restrict__ blvl) {
+  const int32_t p = a + (int32_t)threadIdx.x;
+  const bool ok = p < z;
+  q.row = ok ? rows[p] : -1;
+  q.pos = p;
+  q.diag = ok ? pdiag[p] : 0.0;
+  q.bi = ok ? blvl[p] : 0.0;
+#pragma unroll
+  for (int k = 0; k < kGsRingK; ++k) {
+    q.col[k] = ok ? rcol[(int64_t)p * kGsRingK + k] : -1;
+    q.val[k] = ok ? pval[(int64_t)p * kGsRingK + k] : 0.0;
+  }
+}
+
+// the old values of the later-swept columns (needs the columns: the second round trip)
+__device__ __forceinline__ void gs_ring_old(GsRingRow& q, const double* x) {
+#pragma unroll
+  for (int k = 0; k < kGsRingK; ++k) q.xo[k] = q.col[k] <= -2 ? x[-(q.col[k] + 2)] : 0.0;
+}
+
+template <bool BLK>
+__global__ __launch_bounds__(kGsBlock) void k_gs_ring(const int32_t* __restrict__ rows,
+                                                      const int32_t* __restrict__ lptr,
+                                                      int32_t n_levels,
+                                                      const int32_t* __restrict__ rcol,
+                                                      const double* __restrict__ pval,
+                                                      const double* __restrict__ pdiag,
+                                                      const double* __restrict__ blvl,
+                                                      int ring_log2, int iterations, double* x,
+                                                      const int32_t* done) {
+  extern __shared__ double ring[];
+  if (done && *done) return;
+  const int32_t RM = (1 << ring_log2) - 1;
+  for (int it = 0; it < iterations; ++it) {
+    GsRingRow cur, n1, n2;
+    gs_ring_struct(cur, lptr[0], lptr[1], rows, rcol, pval, pdiag, blvl);
+    gs_ring_old(cur, x);
+    if (n_levels > 1) gs_ring_struct(n1, lptr[1], lptr[2], rows, rcol, pval, pdiag, blvl);
+    for (int32_t l = 0; l < n_levels; ++l) {
+      // in flight during this level: level l+1's old values, level l+2's structure
+      if (l + 1 < n_levels) gs_ring_old(n1, x);
+      if (l + 2 < n_levels) gs_ring_struct(n2, lptr[l + 2], lptr[l + 3], rows, rcol, pval, pdiag, blvl);
+      if (cur.row >= 0) {
+        double xv[kGsRingK];
+#pragma unroll
+        for (int k = 0; k < kGsRingK; ++k)
+          xv[k] = cur.col[k] >= 0 ? ring[cur.col[k] & RM] : cur.xo[k];
+        double rsum = gs_init<BLK>(cur.bi);
+#pragma unroll
+        for (int k = 0; k < kGsRingK; ++k)
+          if (cur.col[k] != -1) rsum = gs_acc<BLK>(rsum, cur.val[k], xv[k]);
+        // a row left alone (zero diagonal of gauss_seidel) keeps its old value in the ring
+        const double xi = gs_upd<BLK>(cur.diag) ? gs_fin<BLK>(rsum, cur.bi, cur.diag) : x[cur.row];
+        ring[cur.pos & RM] = xi;
+        if (gs_upd<BLK>(cur.diag)) x[cur.row] = xi;
+      }
+      __syncthreads();
+      cur = n1;
+      n1 = n2;
+    }
+    __syncthreads();
   }
 }
 
@@ -672,6 +759,11 @@ __global__ void k_gs_win_prep(const int32_t* __restrict__ rows, int64_t n,
   }
 }
 
+static bool gs_ring_disabled() {  // MLAMG_GS_NO_RING=1: A/B runs, tests
+  const char* e = std::getenv("MLAMG_GS_NO_RING");
+  return e && e[0] == '1';
+}
+
 static bool gs_wave_disabled() {  // MLAMG_GS_NO_WAVE=1: A/B runs, tests
   const char* e = std::getenv("MLAMG_GS_NO_WAVE");
   return e && e[0] == '1';
@@ -723,6 +815,14 @@ static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int itera
         default: launch_gs_win<8, 2, 4, BLK>(G, x, b, iterations, done, s); break;
       }
     }
+  } else if (pipe && G->rcol && !gs_ring_disabled()) {
+    const int64_t n = A->n_rows;
+    hipLaunchKernelGGL(k_gs_b_level, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
+                       n, b, G->b_lvl, done);
+    hipLaunchKernelGGL((k_gs_ring<BLK>), dim3(1), dim3(kGsBlock),
+                       sizeof(double) << G->ring_log2_r, s, G->rows, G->d_level_ptr, G->n_levels,
+                       G->rcol, G->pk_val, G->pk_diag, G->b_lvl, G->ring_log2_r, iterations, x,
+                       done);
   } else if (pipe && G->max_level_rows <= 2 * kGsBlock) {
     const bool one = G->max_level_rows <= kGsBlock;
     if (G->pk_k == 4) {
@@ -779,6 +879,43 @@ int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
 }  // namespace mlamg
 
 using namespace mlamg;
+
+// The ring sweep's plan (levels of <= 1024 rows, K = 4 slots): W = the widest level distance from
+// a row to an earlier-swept column; positions of levels [l - W, l] must fit the ring
+// (<= 8,192 doubles). Optional: rcol stays nullptr otherwise.
+static void setup_ring(mlamg_gs* G, const std::vector<int32_t>& level,
+                       const std::vector<int32_t>& rows, const std::vector<int32_t>& pcol) {
+  const int64_t n = G->A->n_rows;
+  const int K = kGsRingK;
+  if (G->max_level_rows > kGsBlock || G->n_levels <= 4 || n == 0) return;
+  std::vector<int32_t> pos(n);
+  for (int64_t p = 0; p < n; ++p) pos[rows[p]] = (int32_t)p;
+  int W = 0;
+  for (int64_t p = 0; p < n; ++p)
+    for (int k = 0; k < K; ++k) {
+      const int32_t c = pcol[(size_t)p * K + k];
+      if (c >= 0 && level[c] < level[rows[p]]) W = std::max(W, level[rows[p]] - level[c]);
+    }
+  const std::vector<int32_t>& lp = G->level_ptr;
+  int64_t span = 0;
+  for (int l = 0; l < G->n_levels; ++l)
+    span = std::max<int64_t>(span, lp[l + 1] - lp[std::max(0, l - W)]);
+  int lg = 0;
+  while ((int64_t(1) << lg) < span) ++lg;
+  if (lg > 13) return;
+  std::vector<int32_t> rc((size_t)n * K);
+  for (int64_t p = 0; p < n; ++p)
+    for (int k = 0; k < K; ++k) {
+      const int32_t c = pcol[(size_t)p * K + k];
+      rc[(size_t)p * K + k] = c < 0 ? -1 : (level[c] < level[rows[p]] ? pos[c] : -(c + 2));
+    }
+  if (hipMalloc(&G->rcol, sizeof(int32_t) * rc.size()) != hipSuccess) {
+    G->rcol = nullptr;
+    return;
+  }
+  (void)hipMemcpy(G->rcol, rc.data(), sizeof(int32_t) * rc.size(), hipMemcpyHostToDevice);
+  G->ring_log2_r = lg;
+}
 
 // The windowed one-wave sweep's plan: W = the widest level distance of a coupling, chunks of
 // levels that fit a staging buffer, and the ring that holds every position a step and the
@@ -986,6 +1123,7 @@ static int gs_build(const mlamg_csr* A, bool backward, bool block, mlamg_gs** ou
         phase("pack_upload");
         setup_window(G, ip, ij, level, rows, pcol, K);
         phase("window");
+        if (K == kGsRingK && G->win_rw == 0) setup_ring(G, level, rows, pcol);
       } else {  // optional: the sweep falls back to the plain kernels
         for (void* q : {(void*)G->pk_col, (void*)G->pk_val, (void*)G->pk_diag, (void*)G->b_lvl})
           if (q) (void)hipFree(q);
@@ -1028,7 +1166,7 @@ int mlamg_gs_destroy(mlamg_gs* G) {
     if (G->bwd) mlamg_gs_destroy(G->bwd);
     for (void* q : {(void*)G->rows, (void*)G->d_level_ptr, (void*)G->pk_col, (void*)G->pk_val,
                     (void*)G->pk_diag, (void*)G->b_lvl, (void*)G->wcol, (void*)G->d_clev,
-                    (void*)G->win_xl, (void*)G->wpos})
+                    (void*)G->win_xl, (void*)G->wpos, (void*)G->rcol})
       if (q) (void)hipFree(q);
     delete G;
   }

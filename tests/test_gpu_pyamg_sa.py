@@ -141,7 +141,9 @@ def test_gauss_seidel_directions_bitwise(ml, oracle, torch_cuda, sweep, block):
     torch = torch_cuda
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(5)
-    for name, A in _matrices(ml).items():
+    mats = dict(_matrices(ml))
+    mats["poisson_600"] = ml.problems.poisson_2d_5pt(600)  # 600-row levels: the LDS-ring sweep
+    for name, A in mats.items():
         if name == "doc_isolated":
             continue
         n = A.shape[0]
