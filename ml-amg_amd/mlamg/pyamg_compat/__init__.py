@@ -7,11 +7,13 @@ mlamg.compat.install() when the real package is missing (or on request):
   pyamg.graph.bellman_ford              ns/model/agg_interp.py:475
   pyamg.strength.evolution_strength_of_connection   utils/common.py:27,30
   pyamg.relaxation.relaxation.gauss_seidel          ns/lib/multigrid.py:175,184
+  pyamg.aggregation.smoothed_aggregation_solver     ns/preconditioner/PyAMG.py:94 (its default
+      recipe: symmetric_strength_of_connection, standard_aggregation, fit_candidates,
+      block_gauss_seidel, and the MultilevelSolver's solve / aspreconditioner / repr, :119,129)
 
-Everything else of pyamg (gallery, smoothed_aggregation_solver, krylov) is not provided: those
-are the reference's input generators and the PyAMG PC, which mlamg.mesh / mlamg.preconditioner
-cover under their own names.
+Everything else of pyamg (gallery, krylov, other solvers) is not provided: the gallery is the
+reference's input generator, which mlamg.mesh covers under its own names.
 """
-from . import aggregation, graph, relaxation, strength  # noqa: F401
+from . import aggregation, graph, multilevel, relaxation, strength  # noqa: F401
 
 __version__ = "4.2.3+mlamg"

@@ -59,6 +59,18 @@ def test_alias_table(compat):
     assert (pyamg.strength.evolution_strength_of_connection
             is mlamg.strength.evolution_strength_of_connection)
     assert callable(pyamg.relaxation.relaxation.gauss_seidel)
+    # the PyAMG PC's solver (ns/preconditioner/PyAMG.py:94) and its pieces
+    import mlamg.pyamg_compat.aggregation as agg
+    assert pyamg.aggregation.smoothed_aggregation_solver is agg.smoothed_aggregation_solver
+    assert callable(pyamg.aggregation.standard_aggregation)
+    assert callable(pyamg.aggregation.fit_candidates)
+    assert callable(pyamg.strength.symmetric_strength_of_connection)
+    assert callable(pyamg.relaxation.relaxation.block_gauss_seidel)
+    A = sp.identity(4, format="csr")
+    for bad in ({"aggregate": "lloyd"}, {"smooth": "energy"}, {"strength": "classical"},
+                {"coarse_solver": "splu"}, {"keep": True}):
+        with pytest.raises(NotImplementedError):  # before any device call
+            pyamg.aggregation.smoothed_aggregation_solver(A, **bad)
 
 
 def test_sparse_tensor_mirror():
@@ -157,3 +169,36 @@ def test_reference_callers_resolve(compat, monkeypatch):
     }.items():
         assert _resolve(ns2, dotted) is fn_, dotted
     assert {"ns", "np", "torch", "pyamg", "common", "la"} <= _names(code)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present (GPU box)")
+def test_reference_pyamg_pc_resolves(compat, monkeypatch):
+    """ns/preconditioner/PyAMG.py exec'd from the reference file with Firedrake / PETSc /
+    matplotlib stubs: its `pyamg.aggregation.smoothed_aggregation_solver` (:94) is this package's
+    (tests/test_gpu_pyamg_sa.py runs that solver's :119 / :129 calls on the device)."""
+    import mlamg.pyamg_compat.aggregation as agg
+    fd = types.ModuleType("firedrake")
+
+    class PCBase:  # the python-PC base class the PC derives from
+        pass
+
+    fd.PCBase = PCBase
+    fd.__all__ = ["PCBase"]
+    petsc = types.ModuleType("firedrake.petsc")
+    petsc.PETSc = types.SimpleNamespace()
+    asm = types.ModuleType("firedrake.assemble")
+    asm.allocate_matrix = asm.assemble = None
+    mpl = types.ModuleType("matplotlib")
+    mpl.__path__ = []
+    for name, mod in (("firedrake", fd), ("firedrake.petsc", petsc), ("firedrake.assemble", asm),
+                      ("matplotlib", mpl), ("matplotlib.pyplot", types.ModuleType("pyplot"))):
+        monkeypatch.setitem(sys.modules, name, mod)
+    path = os.path.join(REF, "ns", "preconditioner", "PyAMG.py")
+    mod = types.ModuleType("PyAMG_ref")
+    with open(path) as fh:
+        exec(compile(fh.read(), path, "exec"), mod.__dict__)
+    g = mod.__dict__
+    assert _resolve(g, ("pyamg", "aggregation", "smoothed_aggregation_solver")) is \
+        agg.smoothed_aggregation_solver
+    assert "pyamg" in _names(mod.PyAMG._createAmgSolver.__code__)
+    assert "solve" in _names(mod.PyAMG._apply.__code__)

@@ -256,3 +256,47 @@ def test_multilevel_pc_uses_pyamg_recipe(ml, torch_cuda):
         assert getattr(pc2.H, "recipe", None) != "pyamg_sa"
     finally:
         ml.preconditioner._Options.store.pop("pyamg_amg_recipe", None)
+
+
+def test_pyamg_compat_solver_api(ml, oracle, torch_cuda):
+    """`pyamg.aggregation.smoothed_aggregation_solver(P, max_levels=10)` under the compat alias
+    (what ns/preconditioner/PyAMG.py:94 calls) and the MultilevelSolver calls of :119 and :129:
+    solve with accel='gmres' and None, residuals, repr; the pieces under pyamg's names."""
+    import scipy.sparse.linalg as spla
+    from mlamg.pyamg_compat import aggregation, relaxation, strength
+    A = ml.problems.poisson_2d_5pt(80)
+    ml_solver = aggregation.smoothed_aggregation_solver(A, max_levels=10)
+    text = repr(ml_solver)
+    assert "MultilevelSolver" in text and "Number of Levels" in text
+    assert len(ml_solver.levels) == ml_solver.H.n_levels and ml_solver.levels[-1].A.shape[0] <= 10
+    assert 1.0 < ml_solver.operator_complexity() < 2.0
+    b = np.random.default_rng(3).standard_normal(A.shape[0])
+    res = []
+    x = ml_solver.solve(b, tol=1e-8, accel="gmres", residuals=res)
+    assert np.linalg.norm(b - A @ x) <= 1e-6 * np.linalg.norm(b) and len(res) >= 2
+    res = []
+    x, info = ml_solver.solve(b, tol=1e-8, residuals=res, return_info=True)
+    assert info == 0 and res[-1] <= 1e-8 * np.linalg.norm(b) and res[0] == pytest.approx(
+        np.linalg.norm(b))
+    assert np.linalg.norm(b - A @ x) <= 1.01e-8 * np.linalg.norm(b)
+    M = ml_solver.aspreconditioner()
+    xs, code = spla.cg(A, b, rtol=1e-8, M=M)
+    assert code == 0
+    # the pieces
+    C = strength.symmetric_strength_of_connection(A, 0.25)
+    Co = oracle.pyamg_symmetric_strength(A, 0.25)
+    assert np.array_equal(C.indices, Co.indices) and np.array_equal(C.data, Co.data)
+    AggOp, Cpts = aggregation.standard_aggregation(C)
+    agg_o, cpts_o, k_o = oracle.pyamg_standard_aggregation(Co)
+    assert AggOp.shape == (A.shape[0], k_o) and np.array_equal(Cpts, cpts_o)
+    assert np.array_equal(AggOp.indices, agg_o[agg_o >= 0])
+    Q, R = aggregation.fit_candidates(AggOp, np.ones((A.shape[0], 1)))
+    To, Bco = oracle.pyamg_fit_candidates(agg_o, k_o, np.ones(A.shape[0]))
+    assert np.array_equal(Q.data, To.data) and np.array_equal(R.ravel(), Bco)
+    xr = np.random.default_rng(4).standard_normal(A.shape[0])
+    xo = xr.copy()
+    relaxation.relaxation.block_gauss_seidel(A, xr, b, iterations=2, sweep="symmetric")
+    oracle.pyamg_block_gauss_seidel(A, xo, b, 2, "symmetric")
+    assert np.array_equal(xr, xo)
+    with pytest.raises(NotImplementedError):
+        aggregation.smoothed_aggregation_solver(A, aggregate="lloyd")
