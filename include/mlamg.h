@@ -299,6 +299,12 @@ int mlamg_bellman_ford_canon(const mlamg_csr* G, const int32_t* seeds, int32_t k
 int mlamg_bellman_ford_pyamg(const mlamg_csr* G, const int32_t* seeds, int32_t k, int fp64,
                              void* dist, int32_t* nearest, int32_t* sweeps_host, void* stream);
 
+/* out[0..k) (DEVICE int32) = np.random.RandomState(seed).permutation(n)[:k] bit for bit (numpy's
+ * legacy MT19937 + Fisher-Yates; the seeds of ns/lib/graph.py:230-231 and
+ * utils/evaluate_dataset.py:80-85): the draws on the host, the first k positions followed
+ * through the swaps on the device (csrc/seeds.hip). Syncs. */
+int mlamg_legacy_permutation(uint32_t seed, int64_t n, int64_t k, int32_t* out, void* stream);
+
 /* Agg (n x k, values 1.0) from a per-node column assignment col[n] (-1 = no aggregate):
  * graph.py:56-86 nearest_center_to_agg and graph.py:234-238 AggOp. */
 int mlamg_aggregate_op(const int32_t* col, int64_t n, int64_t k, mlamg_csr** out, void* stream);

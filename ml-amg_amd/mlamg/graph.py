@@ -122,6 +122,24 @@ def modified_bellman_ford(S_T, centers):
     return dist.to(dev), nearest.to(dev)
 
 
+def legacy_permutation(seed, n, k):
+    """np.random.RandomState(seed).permutation(n)[:k] (int seed in [0, 2^32)), bit for bit, as
+    an int32 device tensor: numpy's MT19937 draws on the host, the Fisher-Yates swaps resolved
+    for the first k positions on the device (csrc/seeds.hip) — instead of n random-address swaps
+    of an 8n-byte array on the host (~1 s at the C4 size). Seeds of graph.py:230-231 and
+    utils/evaluate_dataset.py:80-85. numpy's global generator is not touched (the caller's
+    RandomState(seed) was a fresh generator too)."""
+    seed = int(seed)
+    if not 0 <= seed < 2 ** 32:
+        raise ValueError("Seed must be between 0 and 2**32 - 1")
+    if not 0 <= k <= n:
+        raise ValueError("need 0 <= k <= n")
+    out = torch.empty(max(int(k), 1), dtype=torch.int32, device=_device())
+    call("mlamg_legacy_permutation", ctypes.c_uint32(seed), int(n), int(k), ptr(out),
+         stream_ptr())
+    return out[:k]
+
+
 def aggregate_op_device(col_dev, k):
     """Agg (n x k, ones) from per-node aggregate columns (-1 = none) on the device."""
     h = ctypes.c_void_p()

@@ -11,8 +11,9 @@ Setup per level follows the reference's aggregation-based SA recipe, all on the 
 until n <= max_coarse; the last operator is inverted densely (multigrid.py:168 factorized).
 The cycle is the Jacobi V(1,1) of ns/preconditioner/MLAMG.py:143-197 applied recursively.
 
-Seeds are drawn on the host with numpy's RandomState for bit-exact reproducibility against the
-reference seeding; with sort_seeds=True (default for the multilevel solver) they are sorted so that
+Seeds are RandomState(seed).permutation(n)[:k] bit for bit, the reference seeding (numpy's
+MT19937 draws on the host, the shuffle's first k positions resolved on the device: graph.
+legacy_permutation); with sort_seeds=True (default for the multilevel solver) they are sorted so that
 coarse unknowns follow the fine ordering (better locality, contiguous ownership per GPU).
 """
 from __future__ import annotations
@@ -29,7 +30,7 @@ import torch
 from . import _lib
 from ._lib import MLAMG_EUNSUPPORTED, MlamgError, _tol_arg, call, ptr, stream_ptr
 from .graph import (aggregate_op_device, bellman_ford_device, labels_to_columns,
-                    lloyd_cluster_device, modified_bellman_ford_device)
+                    legacy_permutation, lloyd_cluster_device, modified_bellman_ford_device)
 from .multigrid import lambda_max_dinv_a
 from .sparse import DeviceCSR, _device, as_device, galerkin, to_device_vec
 
@@ -452,7 +453,8 @@ class Hierarchy:
             if P_given is None and Agg_given is None:
                 C = strength(A_dev, strength_mode)
                 k = int(math.ceil(alpha * n))
-                seeds = np.random.RandomState(seed).permutation(n)[:k]
+                # RandomState(seed).permutation(n)[:k], bit for bit (device, csrc/seeds.hip)
+                seeds = legacy_permutation(seed, n, k).cpu().numpy().astype(np.int64)
                 if aggregation == "reference" and lvl == 0:
                     # evaluate_dataset.py:80-90: push-order sweeps from the unsorted seeds
                     seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
