@@ -300,3 +300,35 @@ def test_pyamg_compat_solver_api(ml, oracle, torch_cuda):
     assert np.array_equal(xr, xo)
     with pytest.raises(NotImplementedError):
         aggregation.smoothed_aggregation_solver(A, aggregate="lloyd")
+
+
+def test_pyamg_sa_edge_cases(ml, torch_cuda):
+    """n <= max_coarse: no level, the solve is the pinv product (pyamg: len(levels) == 1), also
+    for a singular (pure Neumann) operator (the minimum-norm solution); x0 given; max_levels=1
+    and 2."""
+    from mlamg.pyamg_compat import aggregation
+    A = ml.problems.poisson_1d(8)
+    s = aggregation.smoothed_aggregation_solver(A)
+    assert s.H.n_levels == 1
+    b = np.arange(1.0, 9.0)
+    x = s.solve(b, tol=1e-12)
+    np.testing.assert_allclose(A @ x, b, rtol=0, atol=1e-12 * np.abs(b).max() * 100)
+    # singular (Neumann) coarse operator: the pinv coarse solve gives the minimum-norm solution
+    n = 8
+    N = sp.diags([-np.ones(n - 1), 2 * np.ones(n), -np.ones(n - 1)], [-1, 0, 1]).tolil()
+    N[0, 0] = N[n - 1, n - 1] = 1.0
+    N = sp.csr_matrix(N)
+    rhs = np.sin(np.linspace(0, 2 * np.pi, n))
+    rhs -= rhs.mean()
+    xn = aggregation.smoothed_aggregation_solver(N).solve(rhs, tol=1e-12)
+    np.testing.assert_allclose(N @ xn, rhs, atol=1e-12)
+    assert abs(xn.sum()) < 1e-12
+    for lv in (1, 2):
+        s2 = aggregation.smoothed_aggregation_solver(ml.problems.poisson_2d_5pt(12), max_levels=lv)
+        assert s2.H.n_levels == lv
+    P = ml.problems.poisson_2d_5pt(40)
+    s3 = aggregation.smoothed_aggregation_solver(P)
+    b3 = np.ones(P.shape[0])
+    x1 = s3.solve(b3, tol=1e-6, maxiter=3)
+    x2 = s3.solve(b3, x0=x1, tol=1e-10, maxiter=50)
+    assert np.linalg.norm(b3 - P @ x2) <= 1e-10 * np.linalg.norm(b3)
