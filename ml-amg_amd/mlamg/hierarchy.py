@@ -323,16 +323,30 @@ class Hierarchy:
                 lbs = {c: self._lower_bound_us(M, name, c[0]) for c in cands}
                 cands.sort(key=lambda c: lbs[c])
                 pruned = []
+                value_dict = False
+                refused = set()
                 for fmt, arg in cands:
                     if times and lbs[(fmt, arg)] >= min(times.values()):
+                        pruned.append(f"{fmt}/{arg}")
+                        continue
+                    if fmt in refused or ((fmt, arg) == ("sorted", 2) and value_dict):
+                        # builds that would be refused: a dictionary-SELL or sorted limit of
+                        # one variant (too many column offsets or values, a row over a block)
+                        # holds for the others, and block dictionaries are refused when the
+                        # <= 256-value table applies (known from sorted/0). At C4 these
+                        # refused builds were half the autotune (0.46 of 0.99 s).
                         pruned.append(f"{fmt}/{arg}")
                         continue
                     try:
                         times[f"{fmt}/{arg}"] = self._time_format(M, fmt, arg, x, y,
                                                                   kind=name, flush=flush)
+                        if (fmt, arg) == ("sorted", 0):
+                            value_dict = M.get_format()[1] == 1
                     except MlamgError as e:  # format limits (e.g. sorted: row > 4096 nnz)
                         if e.code != MLAMG_EUNSUPPORTED:
                             raise
+                        if fmt in ("sell_dict", "sell") or (fmt, arg) == ("sorted", 0):
+                            refused.add(fmt)
                 best = min(times, key=times.get)
                 fmt, arg = best.split("/")
                 M.set_format(fmt, int(arg))
