@@ -245,6 +245,9 @@ class Hierarchy:
     FORMAT_MIN_BYTES_PER_NNZ = {"csr_stream": 12.0, "sell": 12.0, "sorted": 5.0, "sell_dict": 2.0,
                                 "rowpat": 0.0, "long": 12.0, "vector": 10.0}
     LB_PEAK_BPS = 7e12
+    # a SELL / dictionary-SELL timed at more than this many times the best format so far skips
+    # its sigma-sorted (row-length-ordered) variant
+    SIGMA_SKIP_RATIO = 1.5
 
     @classmethod
     def _lower_bound_us(cls, M, kind, fmt):
@@ -338,10 +341,16 @@ class Hierarchy:
                         pruned.append(f"{fmt}/{arg}")
                         continue
                     try:
-                        times[f"{fmt}/{arg}"] = self._time_format(M, fmt, arg, x, y,
-                                                                  kind=name, flush=flush)
+                        t = self._time_format(M, fmt, arg, x, y, kind=name, flush=flush)
+                        times[f"{fmt}/{arg}"] = t
                         if (fmt, arg) == ("sorted", 0):
                             value_dict = M.get_format()[1] == 1
+                        if fmt in ("sell", "sell_dict") and arg == 1 and \
+                                t > self.SIGMA_SKIP_RATIO * min(times.values()):
+                            # the sigma-sorted variant only reorders rows by length: it does not
+                            # close a gap this large to the best format (C4 A_0: its build
+                            # alone took 0.18 s, and it ran at 106 against rowpat's 56 us)
+                            refused.add(fmt)
                     except MlamgError as e:  # format limits (e.g. sorted: row > 4096 nnz)
                         if e.code != MLAMG_EUNSUPPORTED:
                             raise
