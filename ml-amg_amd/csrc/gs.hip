@@ -331,8 +331,7 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_pipe(const int32_t* __restrict_
 // pipelined walk with the x values of the last W levels in an LDS ring indexed by level-order
 // position, W = the widest level distance of a coupling to an earlier level. A slot's column is
 // host-classified: a row swept earlier (its updated value: the ring) or later (its old value: read
-// from x while the structure is prefetched, two levels ahead, since nothing writes it before its
-// own level). A level's critical path is then LDS gathers, the ordered sum, the stores and the
+// from x two levels ahead, the structure three, since nothing writes it before its own level). A level's critical path is then LDS gathers, the ordered sum, the stores and the
 // barrier. Same products, same order, same division as gs_row.
 constexpr int kGsRingK = 4;
 struct GsRingRow {
@@ -381,14 +380,18 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_ring(const int32_t* __restrict_
   if (done && *done) return;
   const int32_t RM = (1 << ring_log2) - 1;
   for (int it = 0; it < iterations; ++it) {
-    GsRingRow cur, n1, n2;
+    GsRingRow cur, n1, n2, n3;
     gs_ring_struct(cur, lptr[0], lptr[1], rows, rcol, pval, pdiag, blvl);
     gs_ring_old(cur, x);
-    if (n_levels > 1) gs_ring_struct(n1, lptr[1], lptr[2], rows, rcol, pval, pdiag, blvl);
+    if (n_levels > 1) {
+      gs_ring_struct(n1, lptr[1], lptr[2], rows, rcol, pval, pdiag, blvl);
+      gs_ring_old(n1, x);
+    }
+    if (n_levels > 2) gs_ring_struct(n2, lptr[2], lptr[3], rows, rcol, pval, pdiag, blvl);
     for (int32_t l = 0; l < n_levels; ++l) {
-      // in flight during this level: level l+1's old values, level l+2's structure
-      if (l + 1 < n_levels) gs_ring_old(n1, x);
-      if (l + 2 < n_levels) gs_ring_struct(n2, lptr[l + 2], lptr[l + 3], rows, rcol, pval, pdiag, blvl);
+      // in flight during this level: level l+2's old values, level l+3's structure
+      if (l + 2 < n_levels) gs_ring_old(n2, x);
+      if (l + 3 < n_levels) gs_ring_struct(n3, lptr[l + 3], lptr[l + 4], rows, rcol, pval, pdiag, blvl);
       if (cur.row >= 0) {
         double xv[kGsRingK];
 #pragma unroll
@@ -406,6 +409,7 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_ring(const int32_t* __restrict_
       __syncthreads();
       cur = n1;
       n1 = n2;
+      n2 = n3;
     }
     __syncthreads();
   }
