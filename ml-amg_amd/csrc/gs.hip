@@ -152,15 +152,19 @@ struct GsWaveRow {
   double val[EPL];
 };
 
+// a position's (row, first entry, length): w.x < 0 marks no row
+__device__ __forceinline__ int4 gs_wave_pos(int32_t t, int32_t z, const int4* __restrict__ wpos) {
+  return t < z ? wpos[t] : make_int4(-1, 0, 0, 0);
+}
+
+// the row's b and entries from its position info
 template <int EPL>
-__device__ __forceinline__ void gs_wave_load(GsWaveRow<EPL>& r, int32_t t, int32_t z, int lane,
-                                             const int4* __restrict__ wpos,
-                                             const int32_t* __restrict__ ij,
-                                             const double* __restrict__ ax,
-                                             const double* __restrict__ b) {
-  const bool live = t < z;
-  const int4 w = live ? wpos[t] : make_int4(0, 0, 0, 0);
-  r.row = live ? w.x : -1;  // an empty row still updates (block_gauss_seidel: x_i = 0 + 0 b_i)
+__device__ __forceinline__ void gs_wave_entries(GsWaveRow<EPL>& r, int4 w, int lane,
+                                                const int32_t* __restrict__ ij,
+                                                const double* __restrict__ ax,
+                                                const double* __restrict__ b) {
+  const bool live = w.x >= 0;
+  r.row = w.x;  // an empty row still updates (block_gauss_seidel: x_i = 0 + 0 b_i)
   r.len = w.z;
   r.bi = live ? b[w.x] : 0.0;
 #pragma unroll
@@ -170,6 +174,15 @@ __device__ __forceinline__ void gs_wave_load(GsWaveRow<EPL>& r, int32_t t, int32
     r.col[e] = ok ? ij[w.y + k] : -1;
     r.val[e] = ok ? ax[w.y + k] : 0.0;
   }
+}
+
+template <int EPL>
+__device__ __forceinline__ void gs_wave_load(GsWaveRow<EPL>& r, int32_t t, int32_t z, int lane,
+                                             const int4* __restrict__ wpos,
+                                             const int32_t* __restrict__ ij,
+                                             const double* __restrict__ ax,
+                                             const double* __restrict__ b) {
+  gs_wave_entries<EPL>(r, gs_wave_pos(t, z, wpos), lane, ij, ax, b);
 }
 
 template <int EPL, bool BLK>
@@ -191,6 +204,9 @@ __global__ __launch_bounds__(kGsWaveBlock) void k_gs_wave(const int4* __restrict
   for (int it = 0; it < iterations; ++it) {
     GsWaveRow<EPL> cur, nxt;
     gs_wave_load<EPL>(cur, lptr[0] + g, lptr[1], lane, wpos, ij, ax, b);
+    // positions two levels ahead, entries one level ahead (the entries need the positions)
+    int4 w1 = n_levels > 1 ? gs_wave_pos(lptr[1] + g, lptr[2], wpos) : make_int4(-1, 0, 0, 0);
+    int4 w2 = make_int4(-1, 0, 0, 0);
     for (int32_t l = 0; l < n_levels; ++l) {
       const int32_t a = lptr[l], z = lptr[l + 1];
       // passes over the level's rows (uniform for the workgroup: the LDS fences are per wave)
@@ -203,8 +219,10 @@ __global__ __launch_bounds__(kGsWaveBlock) void k_gs_wave(const int4* __restrict
           const double xj = (j >= 0 && j != cur.row) ? x[j] : 0.0;
           p[e] = j == cur.row ? cur.val[e] : (BLK ? 0.0 + cur.val[e] * xj : cur.val[e] * xj);
         }
-        if (t0 == a && l + 1 < n_levels)
-          gs_wave_load<EPL>(nxt, lptr[l + 1] + g, lptr[l + 2], lane, wpos, ij, ax, b);
+        if (t0 == a) {
+          if (l + 1 < n_levels) gs_wave_entries<EPL>(nxt, w1, lane, ij, ax, b);
+          if (l + 2 < n_levels) w2 = gs_wave_pos(lptr[l + 2] + g, lptr[l + 3], wpos);
+        }
 #pragma unroll
         for (int e = 0; e < EPL; ++e) {
           const int k = lane + e * kGsWaveLPR;
@@ -246,6 +264,7 @@ __global__ __launch_bounds__(kGsWaveBlock) void k_gs_wave(const int4* __restrict
       }
       __syncthreads();
       cur = nxt;
+      w1 = w2;
     }
   }
 }
