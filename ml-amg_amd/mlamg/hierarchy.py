@@ -667,8 +667,9 @@ class Hierarchy:
                  stream_ptr())
             DinvA = DeviceCSR(h)
             if rho == "lanczos":
-                # pyamg's own estimate is a 15-step Arnoldi value; 1e-10 is far tighter
-                lam, L.lanczos_iters = lambda_max_dinv_a(A_dev, tol=1e-10)
+                # pyamg's own estimate is a 15-step Arnoldi value to a relative 1e-2
+                # (approximate_spectral_radius's tol); 1e-6 is far tighter
+                lam, L.lanczos_iters = lambda_max_dinv_a(A_dev, tol=1e-6)
                 L.lam = abs(lam)
             elif rho == "arnoldi":
                 from .strength import approximate_spectral_radius
