@@ -1096,7 +1096,10 @@ static int gs_build(const mlamg_csr* A, bool backward, bool block, mlamg_gs** ou
     int32_t ml = 0;
     for (int64_t i = 0; i < n; ++i) ml = std::max(ml, ip[i + 1] - ip[i]);
     G->max_len = ml;
-    if (!K && ml <= 8 * kGsWaveLPR) {
+    // the copies below serve one-workgroup sweeps only: levels wider than they take are swept
+    // one launch per level straight from the CSR arrays, so such schedules skip them (C4-size
+    // operators: ~1 GB of host packing and upload per sweep direction)
+    if (!K && ml <= 8 * kGsWaveLPR && G->max_level_rows <= kGsBlockMaxLevelRows) {
       std::vector<int32_t> wp((size_t)n * 4);
       for (int64_t p = 0; p < n; ++p) {
         const int32_t i = rows[p];
@@ -1111,7 +1114,7 @@ static int gs_build(const mlamg_csr* A, bool backward, bool block, mlamg_gs** ou
         G->wpos = nullptr;  // optional: the plain one-workgroup kernel takes these rows
       }
     }
-    if (K) {
+    if (K && G->max_level_rows <= 2 * kGsBlock) {
       std::vector<double> ax(A->nnz);
       if (A->nnz)
         MLAMG_HIP(hipMemcpy(ax.data(), A->data, sizeof(double) * A->nnz, hipMemcpyDeviceToHost));
