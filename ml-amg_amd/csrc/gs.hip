@@ -132,8 +132,8 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_block(const int32_t* __restrict
   }
 }
 
-// One workgroup, rows with many off-diagonals (coarse Galerkin operators: 10-120 entries): 16
-// lanes per row, EPL entries per lane, 64 rows per pass. A row's lanes gather their entries'
+// One workgroup, rows with many off-diagonals (coarse Galerkin operators: 10-120 entries): LPR
+// lanes per row (8, or 16 past 64 entries), EPL entries per lane, 1024 / LPR rows per pass. A row's lanes gather their entries'
 // x values in parallel and leave the products (and the diagonal) in LDS in stored order; the
 // row's first lane then folds them in that order — the same products, in the same order, as
 // gs_row — and stores x_i. The next level's first pass (position info from the level-ordered
@@ -141,8 +141,8 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_block(const int32_t* __restrict
 // loaded while this level computes, so a level's critical path is its x gathers, the fold and
 // the barrier.
 constexpr int kGsWaveBlock = 1024;
-constexpr int kGsWaveLPR = 16;
-constexpr int kGsWaveRows = kGsWaveBlock / kGsWaveLPR;
+constexpr int kGsWaveMaxLPR = 16;  // lanes per row: 8 for rows of <= 64 entries (128 rows per
+                                   // pass), 16 up to 128 entries
 
 template <int EPL>
 struct GsWaveRow {
@@ -158,7 +158,7 @@ __device__ __forceinline__ int4 gs_wave_pos(int32_t t, int32_t z, const int4* __
 }
 
 // the row's b and entries from its position info
-template <int EPL>
+template <int LPR, int EPL>
 __device__ __forceinline__ void gs_wave_entries(GsWaveRow<EPL>& r, int4 w, int lane,
                                                 const int32_t* __restrict__ ij,
                                                 const double* __restrict__ ax,
@@ -169,23 +169,23 @@ __device__ __forceinline__ void gs_wave_entries(GsWaveRow<EPL>& r, int4 w, int l
   r.bi = live ? b[w.x] : 0.0;
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
-    const int k = lane + e * kGsWaveLPR;
+    const int k = lane + e * LPR;
     const bool ok = k < w.z;
     r.col[e] = ok ? ij[w.y + k] : -1;
     r.val[e] = ok ? ax[w.y + k] : 0.0;
   }
 }
 
-template <int EPL>
+template <int LPR, int EPL>
 __device__ __forceinline__ void gs_wave_load(GsWaveRow<EPL>& r, int32_t t, int32_t z, int lane,
                                              const int4* __restrict__ wpos,
                                              const int32_t* __restrict__ ij,
                                              const double* __restrict__ ax,
                                              const double* __restrict__ b) {
-  gs_wave_entries<EPL>(r, gs_wave_pos(t, z, wpos), lane, ij, ax, b);
+  gs_wave_entries<LPR, EPL>(r, gs_wave_pos(t, z, wpos), lane, ij, ax, b);
 }
 
-template <int EPL, bool BLK>
+template <int LPR, int EPL, bool BLK>
 __global__ __launch_bounds__(kGsWaveBlock) void k_gs_wave(const int4* __restrict__ wpos,
                                                          const int32_t* __restrict__ ij,
                                                          const double* __restrict__ ax,
@@ -193,25 +193,26 @@ __global__ __launch_bounds__(kGsWaveBlock) void k_gs_wave(const int4* __restrict
                                                          int32_t n_levels, int iterations,
                                                          double* x, const double* __restrict__ b,
                                                          const int32_t* done) {
-  constexpr int SPAN = kGsWaveLPR * EPL;  // LDS slots per row
-  __shared__ double pv[kGsWaveRows * SPAN];
-  __shared__ int32_t pc[kGsWaveRows * SPAN];
+  constexpr int ROWS = kGsWaveBlock / LPR;  // rows per pass
+  constexpr int SPAN = LPR * EPL;             // LDS slots per row
+  __shared__ double pv[ROWS * SPAN];
+  __shared__ int32_t pc[ROWS * SPAN];
   if (done && *done) return;
   const int tid = threadIdx.x;
-  const int g = tid / kGsWaveLPR, lane = tid % kGsWaveLPR;
+  const int g = tid / LPR, lane = tid % LPR;
   double* gv = pv + g * SPAN;
   int32_t* gc = pc + g * SPAN;
   for (int it = 0; it < iterations; ++it) {
     GsWaveRow<EPL> cur, nxt;
-    gs_wave_load<EPL>(cur, lptr[0] + g, lptr[1], lane, wpos, ij, ax, b);
+    gs_wave_load<LPR, EPL>(cur, lptr[0] + g, lptr[1], lane, wpos, ij, ax, b);
     // positions two levels ahead, entries one level ahead (the entries need the positions)
     int4 w1 = n_levels > 1 ? gs_wave_pos(lptr[1] + g, lptr[2], wpos) : make_int4(-1, 0, 0, 0);
     int4 w2 = make_int4(-1, 0, 0, 0);
     for (int32_t l = 0; l < n_levels; ++l) {
       const int32_t a = lptr[l], z = lptr[l + 1];
       // passes over the level's rows (uniform for the workgroup: the LDS fences are per wave)
-      for (int32_t t0 = a; t0 < z; t0 += kGsWaveRows) {
-        if (t0 > a) gs_wave_load<EPL>(cur, t0 + g, z, lane, wpos, ij, ax, b);
+      for (int32_t t0 = a; t0 < z; t0 += ROWS) {
+        if (t0 > a) gs_wave_load<LPR, EPL>(cur, t0 + g, z, lane, wpos, ij, ax, b);
         double p[EPL];
 #pragma unroll
         for (int e = 0; e < EPL; ++e) {
@@ -220,12 +221,12 @@ __global__ __launch_bounds__(kGsWaveBlock) void k_gs_wave(const int4* __restrict
           p[e] = j == cur.row ? cur.val[e] : (BLK ? 0.0 + cur.val[e] * xj : cur.val[e] * xj);
         }
         if (t0 == a) {
-          if (l + 1 < n_levels) gs_wave_entries<EPL>(nxt, w1, lane, ij, ax, b);
+          if (l + 1 < n_levels) gs_wave_entries<LPR, EPL>(nxt, w1, lane, ij, ax, b);
           if (l + 2 < n_levels) w2 = gs_wave_pos(lptr[l + 2] + g, lptr[l + 3], wpos);
         }
 #pragma unroll
         for (int e = 0; e < EPL; ++e) {
-          const int k = lane + e * kGsWaveLPR;
+          const int k = lane + e * LPR;
           gv[k] = p[e];
           gc[k] = cur.col[e];
         }
@@ -857,16 +858,32 @@ static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int itera
     }
   } else if (G->wpos && G->max_level_rows <= kGsBlockMaxLevelRows && G->n_levels > 4 &&
              !gs_wave_disabled()) {
-    const int epl = (G->max_len + kGsWaveLPR - 1) / kGsWaveLPR;  // entries per lane
-    auto go = [&](auto e) {
-      hipLaunchKernelGGL((k_gs_wave<decltype(e)::value, BLK>), dim3(1), dim3(kGsWaveBlock), 0, s,
-                         reinterpret_cast<const int4*>(G->wpos), A->indices, A->data,
-                         G->d_level_ptr, G->n_levels, iterations, x, b, done);
+    auto go = [&](auto l, auto e) {
+      hipLaunchKernelGGL((k_gs_wave<decltype(l)::value, decltype(e)::value, BLK>), dim3(1),
+                         dim3(kGsWaveBlock), 0, s, reinterpret_cast<const int4*>(G->wpos),
+                         A->indices, A->data, G->d_level_ptr, G->n_levels, iterations, x, b,
+                         done);
     };
-    if (epl <= 1) go(std::integral_constant<int, 1>());
-    else if (epl <= 2) go(std::integral_constant<int, 2>());
-    else if (epl <= 4) go(std::integral_constant<int, 4>());
-    else go(std::integral_constant<int, 8>());
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, 4>;
+    using I8 = std::integral_constant<int, 8>;
+    using I16 = std::integral_constant<int, 16>;
+    const int ml = G->max_len;
+    // 8 lanes per row when the levels average more than 64 rows (128 rows per pass: fewer
+    // passes, each with its loads on the critical path), else 16 (fewer entries per lane)
+    const bool wide = A->n_rows > 64 * (int64_t)G->n_levels;
+    if (wide && ml <= 64) {
+      if (ml <= 8) go(I8(), I1());
+      else if (ml <= 16) go(I8(), I2());
+      else if (ml <= 32) go(I8(), I4());
+      else go(I8(), I8());
+    } else {
+      if (ml <= 16) go(I16(), I1());
+      else if (ml <= 32) go(I16(), I2());
+      else if (ml <= 64) go(I16(), I4());
+      else go(I16(), I8());
+    }
   } else if (G->max_level_rows <= kGsBlock && G->n_levels > 4) {
     // one row per thread per level; wider levels go one launch per level over the whole chip
     hipLaunchKernelGGL(k_gs_block<BLK>, dim3(1), dim3(kGsBlock), 0, s, A->indptr, A->indices, A->data,
@@ -1099,7 +1116,7 @@ static int gs_build(const mlamg_csr* A, bool backward, bool block, mlamg_gs** ou
     // the copies below serve one-workgroup sweeps only: levels wider than they take are swept
     // one launch per level straight from the CSR arrays, so such schedules skip them (C4-size
     // operators: ~1 GB of host packing and upload per sweep direction)
-    if (!K && ml <= 8 * kGsWaveLPR && G->max_level_rows <= kGsBlockMaxLevelRows) {
+    if (!K && ml <= 8 * kGsWaveMaxLPR && G->max_level_rows <= kGsBlockMaxLevelRows) {
       std::vector<int32_t> wp((size_t)n * 4);
       for (int64_t p = 0; p < n; ++p) {
         const int32_t i = rows[p];
