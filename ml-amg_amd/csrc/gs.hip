@@ -872,7 +872,8 @@ static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int itera
     const int ml = G->max_len;
     // 8 lanes per row when the levels average more than 64 rows (128 rows per pass: fewer
     // passes, each with its loads on the critical path), else 16 (fewer entries per lane)
-    const bool wide = A->n_rows > 64 * (int64_t)G->n_levels;
+    static const char* lpr_env = std::getenv("MLAMG_GS_WAVE_LPR");  // A/B knob: 8 or 16
+    const bool wide = lpr_env ? lpr_env[0] == '8' : A->n_rows > 64 * (int64_t)G->n_levels;
     if (wide && ml <= 64) {
       if (ml <= 8) go(I8(), I1());
       else if (ml <= 16) go(I8(), I2());
