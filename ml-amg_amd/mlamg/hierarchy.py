@@ -476,8 +476,11 @@ class Hierarchy:
             if P_given is None and Agg_given is None:
                 C = strength(A_dev, strength_mode)
                 k = int(math.ceil(alpha * n))
-                # RandomState(seed).permutation(n)[:k], bit for bit (device, csrc/seeds.hip)
-                seeds = legacy_permutation(seed, n, k).cpu().numpy().astype(np.int64)
+                if isinstance(seed, (int, np.integer)) and 0 <= int(seed) < 2 ** 32:
+                    # RandomState(seed).permutation(n)[:k], bit for bit (device, csrc/seeds.hip)
+                    seeds = legacy_permutation(seed, n, k).cpu().numpy().astype(np.int64)
+                else:  # a seed numpy takes otherwise (None, an array, a generator's state)
+                    seeds = np.random.RandomState(seed).permutation(n)[:k]
                 if aggregation == "reference" and lvl == 0:
                     # evaluate_dataset.py:80-90: push-order sweeps from the unsorted seeds
                     seeds_dev = torch.as_tensor(seeds.astype(np.int32)).to(_device())
