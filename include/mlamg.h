@@ -464,6 +464,16 @@ int mlamg_csr_symmetric(const mlamg_csr* A, double rtol, int* symmetric, void* s
 int mlamg_gmres(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, double rtol,
                 int restart, int maxiter, int x_is_zero, int* info, int* inner_iters,
                 double* presid_hist_host, int hist_cap, void* stream);
+/* pyamg.krylov.gmres with its default Householder orthogonalisation (pyamg 4.x
+ * _gmres_householder; the Krylov loop of ns/preconditioner/PyAMG.py:119, pyamg absent: parity
+ * unpinned): left-preconditioned by one V-cycle of M from a zero guess, returns at once if
+ * ||M(b - A x0)|| < tol ||b||, else one cycle of at most min(maxiter, n) steps (maxiter <= 0:
+ * min(n, 40)) until the rotated residual estimate < tol ||M(b - A x0)||. *info = 0 converged
+ * (final ||M(b - A x)|| below that), else the step count; resid_hist_host (may be NULL): the
+ * preconditioned residual norms, initial and per step, and the final one. Syncs per step. */
+int mlamg_gmres_householder(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x,
+                            double tol, int maxiter, int x_is_zero, int* info, int* inner_iters,
+                            double* resid_hist_host, int hist_cap, void* stream);
 /* use the PCG solver C (size = A_coarse rows) as H's coarsest solve instead of a dense inverse;
  * cycles of such a hierarchy run eagerly (use_graph is ignored) */
 int mlamg_hier_set_coarse_pcg(mlamg_hier* H, const mlamg_csr* A_coarse, mlamg_pcg* C);

@@ -455,11 +455,270 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   return MLAMG_OK;
 }
 
+// ---------------------------------------------------------------- Householder GMRES
+// pyamg.krylov.gmres with its default orthog='householder' (pyamg 4.x _gmres_householder; the
+// Krylov loop of `Amg.solve(b, accel='gmres')`, ns/preconditioner/PyAMG.py:119). pyamg is absent:
+// restated from its published algorithm, parity unpinned (bitwise nothing: the device dots are
+// fixed-order tree reductions where amg_core sums serially; oracle/restated.py
+// pyamg_gmres_householder is the same algorithm in numpy). Left preconditioned: r0 = M(b - A x0);
+// return at once if ||r0|| < tol ||b|| (||b|| = 0 counts as 1); else the inner stop is
+// |g_{k+1}| < tol ||r0||, one outer cycle of at most min(maxiter, n) steps (restrt=None).
+// Reflectors P_j = I - 2 w_j w_j^T, Krylov vector k = P_0 .. P_k e_k, new column
+// P_k .. P_0 M A v, next reflector from its tail, Givens rotations on the head (host, O(k)).
+
+// v = P_k e_k = e_k - 2 w_k[k] w_k
+__global__ __launch_bounds__(kGmThreads) void k_hh_unit(double* __restrict__ v,
+                                                       const double* __restrict__ w, int64_t n,
+                                                       int64_t k) {
+  const double c = -2.0 * w[k];
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads)
+    v[i] = c * w[i] + (i == k ? 1.0 : 0.0);
+}
+
+// v += (-2 (w . v)) w with the dot k_gm_part left in partial (amg_core apply_householders)
+__global__ __launch_bounds__(kGmThreads) void k_hh_apply(double* __restrict__ v,
+                                                        const double* __restrict__ w, int64_t n,
+                                                        const double* __restrict__ partial,
+                                                        int np) {
+  __shared__ double red[kGmThreads / 64];
+  const double a = -2.0 * gm_total(partial, np, red);
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads)
+    v[i] = v[i] + a * w[i];
+}
+
+// w = (0 .. 0, v[k1] + alpha, v[k1+1], ..) (the next reflector before its normalisation), and
+// v[k1] = -alpha, v[k1+1:] = 0
+__global__ __launch_bounds__(kGmThreads) void k_hh_next(double* __restrict__ w,
+                                                       double* __restrict__ v, int64_t n,
+                                                       int64_t k1, double alpha, int make_w) {
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads) {
+    const double vi = v[i];
+    if (make_w) w[i] = i < k1 ? 0.0 : (i == k1 ? vi + alpha : vi);
+    if (i == k1) v[i] = -alpha;
+    else if (i > k1) v[i] = 0.0;
+  }
+}
+
+// u[j] += y  (the Horner step's coefficient)
+__global__ void k_hh_addat(double* u, int64_t j, double y) { u[j] = u[j] + y; }
+
+// x = x + u
+__global__ __launch_bounds__(kGmThreads) void k_hh_axpy1(double* __restrict__ x,
+                                                        const double* __restrict__ u,
+                                                        int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)kGmThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGmThreads)
+    x[i] = x[i] + u[i];
+}
+
+static double hh_sign(double v) { return v == 0.0 ? 1.0 : (v > 0.0 ? 1.0 : -1.0); }
+
+int gmres_householder_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x,
+                           double tol, int maxiter, bool x_zero, int* info_out, int* iters_out,
+                           double* resid_hist, int hist_cap, hipStream_t s) {
+  const int64_t n = A->n_rows;
+  if (maxiter <= 0) maxiter = (int)std::min<int64_t>(n, 40);
+  const int max_inner = (int)std::min<int64_t>(maxiter, n);
+  const int64_t ld = ((std::max<int64_t>(n, 1) + 31) / 32) * 32;
+  const size_t vec = sizeof(double) * ld;
+  const size_t total = vec * (max_inner + 1) + 4 * vec + sizeof(double) * kGmMaxBlocks + 256;
+  void* mem = nullptr;
+  MLAMG_TRY(hier_workspace(M, total, &mem));
+  char* p = static_cast<char*>(mem);
+  double* Wv = reinterpret_cast<double*>(p);  // reflectors w_0 .. w_max_inner
+  p += vec * (max_inner + 1);
+  double* v = reinterpret_cast<double*>(p);
+  p += vec;
+  double* r = reinterpret_cast<double*>(p);
+  p += vec;
+  double* pb = reinterpret_cast<double*>(p);
+  p += vec;
+  double* u = reinterpret_cast<double*>(p);
+  p += vec;
+  double* partial = reinterpret_cast<double*>(p);
+  p += sizeof(double) * kGmMaxBlocks;
+  double* scal = reinterpret_cast<double*>(p);  // 16 doubles
+  int32_t* ctr = reinterpret_cast<int32_t*>(scal + 16);
+  MLAMG_HIP(hipMemsetAsync(ctr, 0, 64, s));
+  MLAMG_TRY(hier_prepare_ext(M));
+  MLAMG_HIP(hipMemsetAsync(hier_done_flag(M), 0, sizeof(int32_t), s));
+  const int nb = gm_grid(n);
+  auto Wk = [&](int k) { return Wv + (int64_t)k * ld; };
+  auto dotv = [&](const double* a, const double* c, int64_t len, double* out) -> int {
+    hipLaunchKernelGGL(k_gm_dot, dim3(gm_grid(len)), dim3(kGmThreads), 0, s, a, c, len, partial,
+                       ctr, scal, nullptr);
+    MLAMG_HIP(hipGetLastError());
+    MLAMG_HIP(hipMemcpyAsync(out, scal, sizeof(double), hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipStreamSynchronize(s));
+    return MLAMG_OK;
+  };
+  auto nrm = [&](const double* a, int64_t len, double* out) -> int {
+    double t = 0.0;
+    MLAMG_TRY(dotv(a, a, len, &t));
+    *out = std::sqrt(t);
+    return MLAMG_OK;
+  };
+  auto at = [&](const double* a, int64_t i, double* out) -> int {
+    MLAMG_HIP(hipMemcpyAsync(out, a + i, sizeof(double), hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipStreamSynchronize(s));
+    return MLAMG_OK;
+  };
+  auto apply = [&](double* z, int j) -> int {  // z = P_j z
+    hipLaunchKernelGGL(k_gm_part, dim3(nb), dim3(kGmThreads), 0, s, Wk(j), z, n, partial,
+                       nullptr);
+    hipLaunchKernelGGL(k_hh_apply, dim3(nb), dim3(kGmThreads), 0, s, z, Wk(j), n, partial, nb);
+    MLAMG_HIP(hipGetLastError());
+    return MLAMG_OK;
+  };
+  auto psolve = [&](const double* in, double* out) -> int {  // one V-cycle from x = 0
+    MLAMG_HIP(hipMemcpyAsync(pb, in, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    double* z = nullptr;
+    MLAMG_TRY(hier_coarse_cycle(M, pb, &z, 1, s));
+    MLAMG_HIP(hipMemcpyAsync(out, z, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    return MLAMG_OK;
+  };
+  auto pres = [&](double* out_norm) -> int {  // r = M (b - A x), ||r||
+    if (x_zero) {
+      MLAMG_HIP(hipMemcpyAsync(v, b, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    } else {
+      MLAMG_TRY(residual_impl(A, b, x, v, nullptr, nullptr, nullptr, nullptr, kNoTol, nullptr,
+                              nullptr, nullptr, s));
+    }
+    MLAMG_TRY(psolve(v, r));
+    return nrm(r, n, out_norm);
+  };
+  *info_out = 0;
+  *iters_out = 0;
+  int nh = 0;
+  double normr = 0.0, normb = 0.0;
+  MLAMG_TRY(pres(&normr));
+  x_zero = false;  // from here on x holds the iterate
+  if (resid_hist && nh < hist_cap) resid_hist[nh++] = normr;
+  MLAMG_TRY(nrm(b, n, &normb));
+  if (normb == 0.0) normb = 1.0;
+  if (normr < tol * normb) return MLAMG_OK;
+  if (normr != 0.0) tol = tol * normr;
+  // first reflector: w = r + sign(r_0) ||r|| e_0, normalised; g_0 = -sign(r_0) ||r||
+  double r0 = 0.0;
+  MLAMG_TRY(at(r, 0, &r0));
+  hipLaunchKernelGGL(k_hh_next, dim3(nb), dim3(kGmThreads), 0, s, Wk(0), r, n, (int64_t)0,
+                     hh_sign(r0) * normr, 1);
+  MLAMG_HIP(hipGetLastError());
+  double wn = 0.0;
+  MLAMG_TRY(nrm(Wk(0), n, &wn));
+  hipLaunchKernelGGL(k_gm_scale, dim3(nb), dim3(kGmThreads), 0, s, Wk(0), Wk(0), n, wn);
+  std::vector<double> g(max_inner + 1, 0.0), H((size_t)max_inner * max_inner, 0.0);
+  std::vector<double> Qc(max_inner, 1.0), Qs(max_inner, 0.0), head(max_inner + 2, 0.0);
+  g[0] = -hh_sign(r0) * normr;
+  int inner = 0, niter = 0;
+  for (inner = 0; inner < max_inner; ++inner) {
+    // v = P_0 .. P_inner e_inner
+    hipLaunchKernelGGL(k_hh_unit, dim3(nb), dim3(kGmThreads), 0, s, v, Wk(inner), n,
+                       (int64_t)inner);
+    for (int j = inner - 1; j >= 0; --j) MLAMG_TRY(apply(v, j));
+    // v = M A v
+    MLAMG_TRY(spmv_set(A, v, u, nullptr, s));
+    MLAMG_TRY(psolve(u, v));
+    for (int j = 0; j <= inner; ++j) MLAMG_TRY(apply(v, j));
+    if (inner != n - 1) {
+      double alpha = 0.0;
+      MLAMG_TRY(nrm(v + inner + 1, n - inner - 1, &alpha));
+      if (alpha == 0.0 && inner < max_inner - 1) {
+        // pyamg's reflector storage starts zeroed: an unused reflector is the identity
+        MLAMG_HIP(hipMemsetAsync(Wk(inner + 1), 0, sizeof(double) * n, s));
+      }
+      if (alpha != 0.0) {
+        double v1 = 0.0;
+        MLAMG_TRY(at(v, inner + 1, &v1));
+        alpha = hh_sign(v1) * alpha;
+        const int make_w = inner < max_inner - 1;
+        hipLaunchKernelGGL(k_hh_next, dim3(nb), dim3(kGmThreads), 0, s,
+                           make_w ? Wk(inner + 1) : u, v, n, (int64_t)(inner + 1), alpha,
+                           make_w);
+        MLAMG_HIP(hipGetLastError());
+        if (make_w) {
+          MLAMG_TRY(nrm(Wk(inner + 1), n, &wn));
+          hipLaunchKernelGGL(k_gm_scale, dim3(nb), dim3(kGmThreads), 0, s, Wk(inner + 1),
+                             Wk(inner + 1), n, wn);
+        }
+      }
+    }
+    const int hl = (int)std::min<int64_t>(inner + 2, n);
+    MLAMG_HIP(hipMemcpyAsync(head.data(), v, sizeof(double) * hl, hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipStreamSynchronize(s));
+    for (int j = 0; j < inner; ++j) {  // the previous rotations on the head
+      const double a0 = head[j], a1 = head[j + 1];
+      head[j] = Qc[j] * a0 + Qs[j] * a1;
+      head[j + 1] = -Qs[j] * a0 + Qc[j] * a1;
+    }
+    if (inner != n - 1 && head[inner + 1] != 0.0) {
+      double c = 1.0, sn = 0.0, rr = 0.0;
+      lartg(head[inner], head[inner + 1], &c, &sn, &rr);
+      Qc[inner] = c;
+      Qs[inner] = sn;
+      const double g0 = g[inner], g1 = g[inner + 1];
+      g[inner] = c * g0 + sn * g1;
+      g[inner + 1] = -sn * g0 + c * g1;
+      head[inner] = c * head[inner] + sn * head[inner + 1];
+      head[inner + 1] = 0.0;
+    }
+    for (int j = 0; j <= inner && j < max_inner; ++j) H[(size_t)inner * max_inner + j] = head[j];
+    ++niter;
+    if (inner < max_inner - 1) {
+      normr = std::fabs(g[inner + 1]);
+      if (resid_hist && nh < hist_cap) resid_hist[nh++] = normr;
+      if (normr < tol) break;
+    }
+  }
+  if (inner == max_inner) inner = max_inner - 1;
+  // y = R^-1 g (R upper triangular: column c of R is H[c][0 .. c])
+  std::vector<double> y(inner + 1, 0.0);
+  for (int k = inner; k >= 0; --k) {
+    double t = g[k];
+    for (int c = k + 1; c <= inner; ++c) t -= H[(size_t)c * max_inner + k] * y[c];
+    y[k] = t / H[(size_t)k * max_inner + k];
+  }
+  // update = P_0 (y_0 e_0 + P_1 (y_1 e_1 + .. P_inner (y_inner e_inner))) (Horner)
+  MLAMG_HIP(hipMemsetAsync(u, 0, sizeof(double) * n, s));
+  for (int j = inner; j >= 0; --j) {
+    hipLaunchKernelGGL(k_hh_addat, dim3(1), dim3(1), 0, s, u, (int64_t)j, y[j]);
+    MLAMG_TRY(apply(u, j));
+  }
+  hipLaunchKernelGGL(k_hh_axpy1, dim3(nb), dim3(kGmThreads), 0, s, x, u, n);
+  MLAMG_HIP(hipGetLastError());
+  MLAMG_TRY(pres(&normr));
+  if (resid_hist && nh < hist_cap) resid_hist[nh++] = normr;
+  *iters_out = niter;
+  *info_out = normr < tol ? 0 : niter;
+  return MLAMG_OK;
+}
+
 }  // namespace mlamg
 
 using namespace mlamg;
 
 extern "C" {
+
+int mlamg_gmres_householder(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x,
+                            double tol, int maxiter, int x_is_zero, int* info, int* inner_iters,
+                            double* resid_hist_host, int hist_cap, void* stream) {
+  MLAMG_REQUIRE(A && M && info && inner_iters, "NULL argument");
+  MLAMG_REQUIRE(A->n_rows == A->n_cols, "square matrix required");
+  MLAMG_REQUIRE(hier_fine_rows(M) == A->n_rows, "preconditioner hierarchy does not match A");
+  MLAMG_REQUIRE(A->n_rows == 0 || (b && x && b != x), "b and x must be distinct device vectors");
+  MLAMG_REQUIRE(tol >= 0.0, "tol >= 0 required");
+  if (A->n_rows == 0) {
+    *info = 0;
+    *inner_iters = 0;
+    return MLAMG_OK;
+  }
+  if (x_is_zero) MLAMG_HIP(hipMemsetAsync(x, 0, sizeof(double) * A->n_rows, S(stream)));
+  return gmres_householder_impl(A, M, b, x, tol, maxiter, x_is_zero != 0, info, inner_iters,
+                                resid_hist_host, resid_hist_host ? hist_cap : 0, S(stream));
+}
 
 int mlamg_gmres(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, double rtol,
                 int restart, int maxiter, int x_is_zero, int* info, int* inner_iters,

@@ -138,6 +138,8 @@ SIGNATURES = {
     "mlamg_gs_create": (c_int, [c_vp, c_vpp, c_vp]),
     "mlamg_gs_create_ex": (c_int, [c_vp, c_int, c_int, c_vpp, c_vp]),
     "mlamg_legacy_permutation": (c_int, [ctypes.c_uint32, c_i64, c_i64, c_vp, c_vp]),
+    "mlamg_gmres_householder": (c_int, [c_vp, c_vp, c_vp, c_vp, c_dbl, c_int, c_int, P_int,
+                                        P_int, c_vp, c_int, c_vp]),
     "mlamg_symmetric_strength": (c_int, [c_vp, c_dbl, c_vpp, c_vp]),
     "mlamg_standard_aggregation": (c_int, [c_vp, c_vp, c_vp, P_i64, P_i32, c_vp]),
     "mlamg_fit_candidates": (c_int, [c_vp, c_vp, c_dbl, c_vpp, c_vp, c_vp]),

@@ -905,6 +905,34 @@ class Hierarchy:
         return x, {"info": info.value, "inner_iters": inner.value,
                    "presid": np.array(hist[:k])}
 
+    def gmres_householder(self, b, x0=None, tol=1e-5, maxiter=None, return_info=False):
+        """pyamg.krylov.gmres(A, b, x0, tol, maxiter, M=one V-cycle) with its default
+        Householder orthogonalisation (mlamg_gmres_householder): what pyamg's
+        MultilevelSolver.solve(b, tol, accel='gmres') runs (ns/preconditioner/PyAMG.py:119).
+        Returns x (numpy in -> numpy out, tensor in -> tensor out), plus {"info", "iters",
+        "residuals"} (preconditioned residual norms: initial, per step, final) with
+        return_info=True."""
+        A = self.levels[0].A if self.levels else self.Ac
+        bd = to_device_vec(b)
+        xd = torch.zeros_like(bd) if x0 is None else to_device_vec(x0).clone()
+        cap = 4096
+        hist = (ctypes.c_double * cap)()
+        info, iters = ctypes.c_int(), ctypes.c_int()
+        call("mlamg_gmres_householder", A.handle, self.handle, ptr(bd), ptr(xd), float(tol),
+             int(maxiter or 0), int(x0 is None), ctypes.byref(info), ctypes.byref(iters), hist,
+             cap, stream_ptr())
+        if self.pcg is not None:
+            self.check_coarse()
+        x = xd if isinstance(b, torch.Tensor) else xd.cpu().numpy()
+        if not return_info:
+            return x
+        # recorded: the initial norm, one per step but the budget's last, the final norm
+        n = bd.numel()
+        max_inner = min(int(maxiter) if maxiter else min(n, 40), n)
+        it = iters.value
+        k = min(1 if it == 0 else it + (1 if it == max_inner else 2), cap)
+        return x, {"info": info.value, "iters": it, "residuals": np.array(hist[:k])}
+
     def precondition(self, b):
         """One V-cycle from a zero guess: the action of the preconditioner on b."""
         bd = to_device_vec(b)

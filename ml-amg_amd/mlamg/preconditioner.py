@@ -161,13 +161,12 @@ class MultilevelPC(MLAMG):
     Apply (:118-120), `Amg.solve(b, tol=amg_rtol, accel='gmres' if amg_precondition_with_gmres
     else None)`: zero initial guess and a tolerance relative to ||b|| (pyamg's solve scales tol
     by ||b||, and its default maxiter is 100).
-      * with GMRES (the default, :54): device GMRES preconditioned by one V-cycle
-        (Hierarchy.gmres), with pyamg's iteration budget and stop test: pyamg.krylov.gmres
-        called without a restart value runs ONE outer cycle of at most maxiter = 100 inner steps
-        (each one V-cycle) and stops when the preconditioned residual ||M r|| <= tol ||M b||;
-        this is one cycle of restart min(100, n) whose inner stop (scipy's first-cycle ptol =
-        tol ||M b||) is that same test. The true residual lands near tol ||b|| (pyamg's
-        Householder orthogonalisation vs MGS here: parity unpinned, pyamg absent);
+      * with GMRES (the default, :54): pyamg.krylov.gmres's default Householder GMRES on the
+        device, preconditioned by one V-cycle (Hierarchy.gmres_householder): ONE outer cycle
+        (no restart value) of at most maxiter = 100 inner steps, stopping when the
+        preconditioned residual ||M r|| < tol ||M b||. Option
+        '<prefix>pyamg_amg_gmres_orthog' = 'mgs' selects the restarted-MGS GMRES
+        (Hierarchy.gmres, scipy's algorithm) with the same budget and stop test instead;
       * without: stationary V-cycles from x = 0 until ||b - A x|| <= amg_rtol ||b||, at most 100.
     """
 
@@ -179,6 +178,11 @@ class MultilevelPC(MLAMG):
         opts = _Options()
         self.amg_precon_gmres = opts.getBool(
             f"{prefix}{self._prefix}amg_precondition_with_gmres", True)
+        self.gmres_orthog = opts.getString(
+            f"{prefix}{self._prefix}amg_gmres_orthog", "householder")
+        if self.gmres_orthog not in ("householder", "mgs"):
+            raise ValueError(f"unknown amg_gmres_orthog {self.gmres_orthog!r} "
+                             "(householder, mgs)")
         super()._initialize(pc)
 
     def _createAmgSolver(self, pc):
@@ -200,7 +204,10 @@ class MultilevelPC(MLAMG):
         b = X.array_r if hasattr(X, "array_r") else np.asarray(X)
         b = np.asarray(b, dtype=np.float64)
         if self.amg_precon_gmres:
-            out = self.H.gmres(b, rtol=self.amg_rtol, restart=self.PYAMG_MAXITER, maxiter=1)
+            if self.gmres_orthog == "householder":
+                out = self.H.gmres_householder(b, tol=self.amg_rtol, maxiter=self.PYAMG_MAXITER)
+            else:
+                out = self.H.gmres(b, rtol=self.amg_rtol, restart=self.PYAMG_MAXITER, maxiter=1)
         else:
             normb = float(np.linalg.norm(b))
             tol = self.amg_rtol * normb if normb != 0 else self.amg_rtol

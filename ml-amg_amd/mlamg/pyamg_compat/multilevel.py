@@ -75,10 +75,13 @@ class MultilevelSolver:
     def solve(self, b, x0=None, tol=1e-5, maxiter=100, cycle="V", accel=None, callback=None,
               residuals=None, return_info=False):
         """pyamg MultilevelSolver.solve: accel=None runs V-cycles from x0 (zeros) while the
-        residual exceeds tol * ||b|| (||b|| = 0: absolute) and fewer than maxiter cycles ran;
-        accel='gmres' runs GMRES preconditioned by one V-cycle, one cycle of at most maxiter
-        steps to a preconditioned residual of tol times its initial value. Returns x (and the
-        info code with return_info: 0 converged, maxiter otherwise)."""
+        residual exceeds tol * ||b|| (||b|| = 0: absolute) and fewer than maxiter cycles ran
+        (info: 0 converged, maxiter otherwise); accel='gmres' runs pyamg.krylov.gmres (its
+        default Householder orthogonalisation, Hierarchy.gmres_householder) preconditioned by
+        one V-cycle: one cycle of at most maxiter steps to a preconditioned residual below tol
+        times its initial value (info: 0 converged, else the steps taken; residuals: the
+        preconditioned residual norms, as pyamg records them). Returns x (and info with
+        return_info)."""
         import torch
         from ..sparse import to_device_vec
         if str(cycle).upper() != "V":
@@ -90,12 +93,11 @@ class MultilevelSolver:
         if accel is not None:
             if accel != "gmres":
                 raise NotImplementedError("accel must be None or 'gmres'")
-            x, info = H.gmres(b, x0=x0, rtol=tol, restart=int(maxiter), maxiter=1,
-                              return_info=True)
+            x, info = H.gmres_householder(b, x0=x0, tol=tol, maxiter=int(maxiter),
+                                          return_info=True)
             if residuals is not None:
-                residuals[:] = list(np.asarray(info["presid"]) * np.linalg.norm(b))
-            code = 0 if info["info"] == 0 else int(maxiter)
-            return (x, code) if return_info else x
+                residuals[:] = list(info["residuals"])
+            return (x, info["info"]) if return_info else x
         normb = float(np.linalg.norm(b))
         if normb == 0.0:
             normb = 1.0  # pyamg: an absolute tolerance

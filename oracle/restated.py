@@ -861,3 +861,93 @@ def pyamg_sa_vcycle(levels, Ac_pinv, b, x, lvl=0):
     x += L["P"] @ xc
     pyamg_block_gauss_seidel(A, x, b, 1, "symmetric")
     return x
+
+
+def _mysign(v):
+    return 1.0 if v == 0.0 else (1.0 if v > 0.0 else -1.0)
+
+
+def pyamg_gmres_householder(A, b, M, x0=None, tol=1e-5, maxiter=None):
+    """pyamg.krylov.gmres(A, b, x0, tol, restrt=None, maxiter, M) with orthog='householder'
+    (pyamg 4.x _gmres_householder, restated; pyamg absent: parity unpinned). M: callable, the
+    preconditioner. Returns (x, info, niter, residuals)."""
+    A = sp.csr_matrix(A)
+    n = A.shape[0]
+    b = np.asarray(b, dtype=np.float64)
+    x = np.zeros(n) if x0 is None else np.array(x0, dtype=np.float64)
+    if maxiter is None:
+        maxiter = min(n, 40)
+    max_inner = min(maxiter, n)
+    r = M(b - A @ x)
+    normr = np.linalg.norm(r)
+    res = [normr]
+    normb = np.linalg.norm(b)
+    if normb == 0.0:
+        normb = 1.0
+    if normr < tol * normb:
+        return x, 0, 0, res
+    if normr != 0.0:
+        tol = tol * normr
+    W = np.zeros((max_inner + 1, n))
+    w = r.copy()
+    w[0] = w[0] + _mysign(w[0]) * normr
+    W[0] = w / np.linalg.norm(w)
+    g = np.zeros(max_inner + 1)
+    g[0] = -_mysign(r[0]) * normr
+    H = np.zeros((max_inner, max_inner))
+    Q = []
+    niter = 0
+    inner = 0
+    for inner in range(max_inner):
+        v = -2.0 * W[inner, inner] * W[inner]
+        v[inner] = v[inner] + 1.0
+        for j in range(inner - 1, -1, -1):
+            v = v + (-2.0 * np.dot(W[j], v)) * W[j]
+        v = M(A @ v)
+        for j in range(inner + 1):
+            v = v + (-2.0 * np.dot(W[j], v)) * W[j]
+        if inner != n - 1:
+            alpha = np.linalg.norm(v[inner + 1:])
+            if alpha != 0.0:
+                alpha = _mysign(v[inner + 1]) * alpha
+                if inner < max_inner - 1:
+                    w = np.zeros(n)
+                    w[inner + 1:] = v[inner + 1:]
+                    w[inner + 1] = w[inner + 1] + alpha
+                    W[inner + 1] = w / np.linalg.norm(w)
+                v[inner + 1] = -alpha
+                v[inner + 2:] = 0.0
+        for j, (c, s) in enumerate(Q):
+            a0, a1 = v[j], v[j + 1]
+            v[j] = c * a0 + s * a1
+            v[j + 1] = -s * a0 + c * a1
+        if inner != n - 1 and v[inner + 1] != 0.0:
+            f, gg = v[inner], v[inner + 1]
+            d = np.sqrt(f * f + gg * gg)
+            c = abs(f) / d if f != 0.0 else 0.0
+            rr = (d if f > 0 else -d) if f != 0.0 else abs(gg)
+            s = gg / rr if f != 0.0 else (1.0 if gg > 0 else -1.0)
+            Q.append((c, s))
+            g0, g1 = g[inner], g[inner + 1]
+            g[inner] = c * g0 + s * g1
+            g[inner + 1] = -s * g0 + c * g1
+            v[inner] = c * v[inner] + s * v[inner + 1]
+            v[inner + 1] = 0.0
+        else:
+            Q.append((1.0, 0.0))
+        H[:inner + 1, inner] = v[:inner + 1]
+        niter += 1
+        if inner < max_inner - 1:
+            normr = abs(g[inner + 1])
+            res.append(normr)
+            if normr < tol:
+                break
+    y = np.linalg.solve(np.triu(H[:inner + 1, :inner + 1]), g[:inner + 1])
+    update = np.zeros(n)
+    for j in range(inner, -1, -1):
+        update[j] = update[j] + y[j]
+        update = update + (-2.0 * np.dot(W[j], update)) * W[j]
+    x = x + update
+    normr = np.linalg.norm(M(b - A @ x))
+    res.append(normr)
+    return x, (0 if normr < tol else niter), niter, res

@@ -116,3 +116,20 @@ def test_pyamg_sa_tiny_is_coarse_only(oracle, m):
     A = sp.csr_matrix(sp.diags([-np.ones(m - 1), 2 * np.ones(m), -np.ones(m - 1)], [-1, 0, 1]))
     levels, Ac = oracle.pyamg_sa_setup(A)
     assert levels == [] and Ac.shape == (m, m)
+
+
+def test_gmres_householder_docstring_example():
+    """pyamg.krylov.gmres's docstring example (orthog='householder'): poisson((10, 10)),
+    b = ones, maxiter=2, tol=1e-8 prints norm(b - A x) = 6.54282; the restatement's loop with
+    an identity preconditioner reproduces it, and with an exact one stops after one step."""
+    import mlamg.problems as P
+    from oracle import restated as R
+    A = P.poisson_2d_5pt(10)
+    b = np.ones(100)
+    x, info, it, res = R.pyamg_gmres_householder(A, b, lambda r: r, tol=1e-8, maxiter=2)
+    assert f"{np.linalg.norm(b - A @ x):.6}" == "6.54282"
+    assert it == 2 and info == 2 and len(res) == 3
+    Ainv = np.linalg.inv(A.toarray())
+    x, info, it, res = R.pyamg_gmres_householder(A, b, lambda r: Ainv @ r, tol=1e-10)
+    assert it == 1 and info == 0
+    np.testing.assert_allclose(A @ x, b, atol=1e-12)
