@@ -47,6 +47,7 @@ struct mlamg_gs {
   int32_t max_len = 0;
   // ring sweep (k_gs_ring): slot columns classified earlier (ring position) / later (-(c + 2))
   int32_t* rcol = nullptr;
+  double* rpv = nullptr;  // per slot: a, the later-swept product, or 0 (k_gs_ring_prep)
   int32_t ring_log2_r = 0;
   // windowed one-wave sweep (k_gs_win): x by level-order position in an LDS ring of 2^ring_log2
   // slots; wcol = the packed columns as positions (pads -1); chunks of levels staged into two
@@ -350,40 +351,96 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_pipe(const int32_t* __restrict_
 // Levels of 513..1024 rows with <= 4 off-diagonals (2-D five-point grids up to 1024^2): the
 // pipelined walk with the x values of the last W levels in an LDS ring indexed by level-order
 // position, W = the widest level distance of a coupling to an earlier level. A slot's column is
-// host-classified: a row swept earlier (its updated value: the ring) or later (its old value: read
-// from x two levels ahead, the structure three, since nothing writes it before its own level). A level's critical path is then LDS gathers, the ordered sum, the stores and the
-// barrier. Same products, same order, same division as gs_row.
+// host-classified: a row swept earlier (its updated value: the ring) or later (its old value,
+// which nothing writes before the slot's own row is swept). The later-swept slots' products
+// (0 + a x_old for block_gauss_seidel, a x_old for gauss_seidel: the very operation the sweep would
+// do, so the same bits) are formed before the sweep by a parallel pass (k_gs_ring_prep), which also
+// stores the old x of a zero-diagonal gauss_seidel row in place of its b. The sweep's loads thus
+// depend on nothing the sweep computes: each level's structure goes out kGsRingSets - 1 levels
+// ahead, all loads unconditional (positions past a level's end clamped to the last one and
+// selected away), the level starts in LDS, and the register sets rotate by unrolling, not by
+// copies (a copy of a register with a load in flight, or a branch join, makes the compiler wait
+// for every outstanding load: that had put one or two memory round trips on each level's critical
+// path, 2.5 us a level at 1024^2). Same products, same order, same division as gs_row.
 constexpr int kGsRingK = 4;
+constexpr int kGsRingSets = 6;                // levels in flight + 1
+constexpr size_t kGsRingLdsMax = 150 * 1024;  // the ring, its sink slot and the level starts
 struct GsRingRow {
-  int32_t row, pos;
+  int32_t row, pos;  // row: rows[clamped position]; pos: unclamped
+  bool ok;           // pos inside its level
   double diag, bi;
-  int32_t col[kGsRingK];  // >= 0 ring position, -1 pad, <= -2 global column -(c + 2)
-  double val[kGsRingK], xo[kGsRingK];
+  int4 col;  // >= 0 ring position, -1 pad, <= -2 a later-swept column (product in pv)
+  double pv[kGsRingK];
 };
 
-__device__ __forceinline__ void gs_ring_struct(GsRingRow& q, int32_t a, int32_t z,
-                                               const int32_t* __restrict__ rows,
-                                               const int32_t* __restrict__ rcol,
-                                               const double* __restrict__ pval,
-                                               const double* __restrict__ pdiag,
-                                               const double* __restrict__ blvl) {
-  const int32_t p = a + (int32_t)threadIdx.x;
-  const bool ok = p < z;
-  q.row = ok ? rows[p] : -1;
-  q.pos = p;
-  q.diag = ok ? pdiag[p] : 0.0;
-  q.bi = ok ? blvl[p] : 0.0;
+template <bool BLK>
+__device__ __forceinline__ double gs_prod(double a, double xj) {
+  return BLK ? 0.0 + a * xj : a * xj;
+}
+template <bool BLK>
+__device__ __forceinline__ double gs_acc_prod(double s, double t) {
+  return BLK ? s - t : s + t;
+}
+
+// pv[p, k] = a (earlier-swept column: multiplied in the sweep), the product with the old x
+// (later-swept), 0 (pad); blvl[p] = b[row], or x[row] for a zero-diagonal gauss_seidel row
+template <bool BLK>
+__global__ void k_gs_ring_prep(const int32_t* __restrict__ rows, int64_t n,
+                               const int32_t* __restrict__ rcol, const double* __restrict__ pval,
+                               const double* __restrict__ pdiag, const double* __restrict__ b,
+                               const double* __restrict__ x, double* __restrict__ pv,
+                               double* __restrict__ blvl, const int32_t* done) {
+  if (done && *done) return;
+  const int64_t p = blockIdx.x * 256ll + threadIdx.x;
+  if (p >= n) return;
+  const int32_t i = rows[p];
+  blvl[p] = (!BLK && pdiag[p] == 0.0) ? x[i] : b[i];
 #pragma unroll
   for (int k = 0; k < kGsRingK; ++k) {
-    q.col[k] = ok ? rcol[(int64_t)p * kGsRingK + k] : -1;
-    q.val[k] = ok ? pval[(int64_t)p * kGsRingK + k] : 0.0;
+    const int32_t c = rcol[p * kGsRingK + k];
+    const double a = pval[p * kGsRingK + k];
+    pv[p * kGsRingK + k] = c >= 0 ? a : (c == -1 ? 0.0 : gs_prod<BLK>(a, x[-(c + 2)]));
   }
 }
 
-// the old values of the later-swept columns (needs the columns: the second round trip)
-__device__ __forceinline__ void gs_ring_old(GsRingRow& q, const double* x) {
+__device__ __forceinline__ void gs_ring_struct(GsRingRow& q, int32_t a, int32_t z, int32_t last,
+                                               const int32_t* __restrict__ rows,
+                                               const int32_t* __restrict__ rcol,
+                                               const double* __restrict__ pv,
+                                               const double* __restrict__ pdiag,
+                                               const double* __restrict__ blvl) {
+  const int32_t p = a + (int32_t)threadIdx.x;
+  q.ok = p < z;
+  q.pos = p;
+  const int64_t pc = q.ok ? p : last;
+  q.row = rows[pc];
+  q.diag = pdiag[pc];
+  q.bi = blvl[pc];
+  q.col = *reinterpret_cast<const int4*>(rcol + pc * kGsRingK);
+  const double2 v01 = *reinterpret_cast<const double2*>(pv + pc * kGsRingK);
+  const double2 v23 = *reinterpret_cast<const double2*>(pv + pc * kGsRingK + 2);
+  q.pv[0] = v01.x;
+  q.pv[1] = v01.y;
+  q.pv[2] = v23.x;
+  q.pv[3] = v23.y;
+}
+
+template <bool BLK>
+__device__ __forceinline__ void gs_ring_row(const GsRingRow& q, double* ring, int32_t RM,
+                                            double* x) {
+  const int32_t c[4] = {q.col.x, q.col.y, q.col.z, q.col.w};
+  double rsum = gs_init<BLK>(q.bi);
 #pragma unroll
-  for (int k = 0; k < kGsRingK; ++k) q.xo[k] = q.col[k] <= -2 ? x[-(q.col[k] + 2)] : 0.0;
+  for (int k = 0; k < kGsRingK; ++k) {
+    const double r = ring[c[k] & RM];
+    const double t = c[k] >= 0 ? gs_prod<BLK>(q.pv[k], r) : q.pv[k];
+    const double u = gs_acc_prod<BLK>(rsum, t);
+    rsum = c[k] != -1 ? u : rsum;
+  }
+  const bool up = gs_upd<BLK>(q.diag);
+  const double xi = up ? gs_fin<BLK>(rsum, q.bi, q.diag) : q.bi;
+  ring[q.ok ? (q.pos & RM) : RM + 1] = xi;  // slot RM + 1: the sink of the clamped lanes
+  if (q.ok && up) x[q.row] = xi;
 }
 
 template <bool BLK>
@@ -391,47 +448,35 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_ring(const int32_t* __restrict_
                                                       const int32_t* __restrict__ lptr,
                                                       int32_t n_levels,
                                                       const int32_t* __restrict__ rcol,
-                                                      const double* __restrict__ pval,
+                                                      const double* __restrict__ pv,
                                                       const double* __restrict__ pdiag,
                                                       const double* __restrict__ blvl,
-                                                      int ring_log2, int iterations, double* x,
+                                                      int ring_log2, double* x,
                                                       const int32_t* done) {
-  extern __shared__ double ring[];
+  extern __shared__ double ring[];  // 2^ring_log2 slots, the sink slot, then the level starts
   if (done && *done) return;
   const int32_t RM = (1 << ring_log2) - 1;
-  for (int it = 0; it < iterations; ++it) {
-    GsRingRow cur, n1, n2, n3;
-    gs_ring_struct(cur, lptr[0], lptr[1], rows, rcol, pval, pdiag, blvl);
-    gs_ring_old(cur, x);
-    if (n_levels > 1) {
-      gs_ring_struct(n1, lptr[1], lptr[2], rows, rcol, pval, pdiag, blvl);
-      gs_ring_old(n1, x);
-    }
-    if (n_levels > 2) gs_ring_struct(n2, lptr[2], lptr[3], rows, rcol, pval, pdiag, blvl);
-    for (int32_t l = 0; l < n_levels; ++l) {
-      // in flight during this level: level l+2's old values, level l+3's structure
-      if (l + 2 < n_levels) gs_ring_old(n2, x);
-      if (l + 3 < n_levels) gs_ring_struct(n3, lptr[l + 3], lptr[l + 4], rows, rcol, pval, pdiag, blvl);
-      if (cur.row >= 0) {
-        double xv[kGsRingK];
+  int32_t* lp = reinterpret_cast<int32_t*>(ring + (RM + 2));
+  for (int i = threadIdx.x; i <= n_levels; i += kGsBlock) lp[i] = lptr[i];
+  __syncthreads();
+  const int32_t nl = n_levels, last = lp[nl] - 1;
+  auto lvl = [&](GsRingRow& q, int32_t l) {  // level l's structure (l >= nl: no row)
+    const int32_t a = lp[l < nl ? l : nl], z = lp[l + 1 < nl ? l + 1 : nl];
+    gs_ring_struct(q, a, z, last, rows, rcol, pv, pdiag, blvl);
+  };
+  constexpr int NS = kGsRingSets;
+  GsRingRow S[NS];
 #pragma unroll
-        for (int k = 0; k < kGsRingK; ++k)
-          xv[k] = cur.col[k] >= 0 ? ring[cur.col[k] & RM] : cur.xo[k];
-        double rsum = gs_init<BLK>(cur.bi);
+  for (int u = 0; u < NS - 1; ++u) lvl(S[u], u);
+  // step l: level l + NS - 1's structure goes out (into the set level l - 1 used), level l is
+  // swept; the steps past the last level sweep no row
+  for (int32_t l = 0; l < nl; l += NS) {
 #pragma unroll
-        for (int k = 0; k < kGsRingK; ++k)
-          if (cur.col[k] != -1) rsum = gs_acc<BLK>(rsum, cur.val[k], xv[k]);
-        // a row left alone (zero diagonal of gauss_seidel) keeps its old value in the ring
-        const double xi = gs_upd<BLK>(cur.diag) ? gs_fin<BLK>(rsum, cur.bi, cur.diag) : x[cur.row];
-        ring[cur.pos & RM] = xi;
-        if (gs_upd<BLK>(cur.diag)) x[cur.row] = xi;
-      }
+    for (int u = 0; u < NS; ++u) {
+      lvl(S[(u + NS - 1) % NS], l + u + NS - 1);
+      gs_ring_row<BLK>(S[u], ring, RM, x);
       __syncthreads();
-      cur = n1;
-      n1 = n2;
-      n2 = n3;
     }
-    __syncthreads();
   }
 }
 
@@ -814,6 +859,11 @@ static void launch_gs_win(const mlamg_gs* G, double* x, const double* b, int ite
 
 int64_t gs_rows(const mlamg_gs* G) { return G->A->n_rows; }
 
+static size_t gs_ring_lds(const mlamg_gs* G) {
+  return (sizeof(double) << G->ring_log2_r) + sizeof(double) +
+         sizeof(int32_t) * (G->n_levels + 1);
+}
+
 template <bool BLK>
 static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int iterations,
                         const int32_t* done, hipStream_t s) {
@@ -839,14 +889,18 @@ static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int itera
         default: launch_gs_win<8, 2, 4, BLK>(G, x, b, iterations, done, s); break;
       }
     }
-  } else if (pipe && G->rcol && !gs_ring_disabled()) {
+  } else if (pipe && G->rcol && G->rpv && !gs_ring_disabled() &&
+             gs_ring_lds(G) <= kGsRingLdsMax) {
     const int64_t n = A->n_rows;
-    hipLaunchKernelGGL(k_gs_b_level, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, G->rows,
-                       n, b, G->b_lvl, done);
-    hipLaunchKernelGGL((k_gs_ring<BLK>), dim3(1), dim3(kGsBlock),
-                       sizeof(double) << G->ring_log2_r, s, G->rows, G->d_level_ptr, G->n_levels,
-                       G->rcol, G->pk_val, G->pk_diag, G->b_lvl, G->ring_log2_r, iterations, x,
-                       done);
+    // one sweep per launch pair: the products of the old values are formed before each
+    for (int it = 0; it < iterations; ++it) {
+      hipLaunchKernelGGL((k_gs_ring_prep<BLK>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         G->rows, n, G->rcol, G->pk_val, G->pk_diag, b, x, G->rpv, G->b_lvl,
+                         done);
+      hipLaunchKernelGGL((k_gs_ring<BLK>), dim3(1), dim3(kGsBlock), gs_ring_lds(G), s, G->rows,
+                         G->d_level_ptr, G->n_levels, G->rcol, G->rpv, G->pk_diag, G->b_lvl,
+                         G->ring_log2_r, x, done);
+    }
   } else if (pipe && G->max_level_rows <= 2 * kGsBlock) {
     const bool one = G->max_level_rows <= kGsBlock;
     if (G->pk_k == 4) {
@@ -955,6 +1009,7 @@ static void setup_ring(mlamg_gs* G, const std::vector<int32_t>& level,
     return;
   }
   (void)hipMemcpy(G->rcol, rc.data(), sizeof(int32_t) * rc.size(), hipMemcpyHostToDevice);
+  if (hipMalloc(&G->rpv, sizeof(double) * rc.size()) != hipSuccess) G->rpv = nullptr;
   G->ring_log2_r = lg;
 }
 
@@ -1210,7 +1265,7 @@ int mlamg_gs_destroy(mlamg_gs* G) {
     if (G->bwd) mlamg_gs_destroy(G->bwd);
     for (void* q : {(void*)G->rows, (void*)G->d_level_ptr, (void*)G->pk_col, (void*)G->pk_val,
                     (void*)G->pk_diag, (void*)G->b_lvl, (void*)G->wcol, (void*)G->d_clev,
-                    (void*)G->win_xl, (void*)G->wpos, (void*)G->rcol})
+                    (void*)G->win_xl, (void*)G->wpos, (void*)G->rcol, (void*)G->rpv})
       if (q) (void)hipFree(q);
     delete G;
   }

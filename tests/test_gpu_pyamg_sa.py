@@ -143,6 +143,11 @@ def test_gauss_seidel_directions_bitwise(ml, oracle, torch_cuda, sweep, block):
     rng = np.random.default_rng(5)
     mats = dict(_matrices(ml))
     mats["poisson_600"] = ml.problems.poisson_2d_5pt(600)  # 600-row levels: the LDS-ring sweep
+    # the ring sweep with zero-diagonal rows (gauss_seidel leaves them alone): stored zeros
+    Z = sp.csr_matrix(mats["poisson_600"], copy=True)
+    for i in (0, 7, 1234, 180_000, 359_999):
+        Z.data[Z.indptr[i]:Z.indptr[i + 1]][Z.indices[Z.indptr[i]:Z.indptr[i + 1]] == i] = 0.0
+    mats["poisson_600_zero_diag"] = Z
     for name, A in mats.items():
         if name == "doc_isolated":
             continue
