@@ -48,6 +48,16 @@ struct mlamg_gs {
   // ring sweep (k_gs_ring): slot columns classified earlier (ring position) / later (-(c + 2))
   int32_t* rcol = nullptr;
   double* rpv = nullptr;  // per slot: a, the later-swept product, or 0 (k_gs_ring_prep)
+  uint16_t* rcode = nullptr;  // per slot: ring slot / kGsRingLater / kGsRingPad
+  // the long-row ring sweep (k_gs_wring): SPAN slots per position, step table, ring
+  int32_t wr_lpr = 0, wr_epl = 0, wr_steps = 0, wr_log2 = 0;
+  int32_t* wr_code = nullptr;
+  double* wr_pv = nullptr;
+  int32_t* wr_len = nullptr;
+  double* wr_d = nullptr;
+  int2* wr_st = nullptr;
+  size_t wr_lds = 0;
+  double* rxl = nullptr;      // the sweep's values in level order
   int32_t ring_log2_r = 0;
   // windowed one-wave sweep (k_gs_win): x by level-order position in an LDS ring of 2^ring_log2
   // slots; wcol = the packed columns as positions (pads -1); chunks of levels staged into two
@@ -365,11 +375,12 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_pipe(const int32_t* __restrict_
 constexpr int kGsRingK = 4;
 constexpr int kGsRingSets = 6;                // levels in flight + 1
 constexpr size_t kGsRingLdsMax = 150 * 1024;  // the ring, its sink slot and the level starts
+constexpr uint32_t kGsRingPad = 0xFFFF, kGsRingLater = 0xFFFE;  // the 16-bit slot codes
 struct GsRingRow {
-  int32_t row, pos;  // row: rows[clamped position]; pos: unclamped
-  bool ok;           // pos inside its level
+  int32_t pos;  // unclamped
+  bool ok;      // pos inside its level
   double diag, bi;
-  int4 col;  // >= 0 ring position, -1 pad, <= -2 a later-swept column (product in pv)
+  uint2 code;  // 4 x 16 bits: the ring slot of an earlier-swept column, kGsRingLater, kGsRingPad
   double pv[kGsRingK];
 };
 
@@ -404,8 +415,7 @@ __global__ void k_gs_ring_prep(const int32_t* __restrict__ rows, int64_t n,
 }
 
 __device__ __forceinline__ void gs_ring_struct(GsRingRow& q, int32_t a, int32_t z, int32_t last,
-                                               const int32_t* __restrict__ rows,
-                                               const int32_t* __restrict__ rcol,
+                                               const uint2* __restrict__ rcode,
                                                const double* __restrict__ pv,
                                                const double* __restrict__ pdiag,
                                                const double* __restrict__ blvl) {
@@ -413,10 +423,9 @@ __device__ __forceinline__ void gs_ring_struct(GsRingRow& q, int32_t a, int32_t 
   q.ok = p < z;
   q.pos = p;
   const int64_t pc = q.ok ? p : last;
-  q.row = rows[pc];
   q.diag = pdiag[pc];
   q.bi = blvl[pc];
-  q.col = *reinterpret_cast<const int4*>(rcol + pc * kGsRingK);
+  q.code = rcode[pc];
   const double2 v01 = *reinterpret_cast<const double2*>(pv + pc * kGsRingK);
   const double2 v23 = *reinterpret_cast<const double2*>(pv + pc * kGsRingK + 2);
   q.pv[0] = v01.x;
@@ -425,33 +434,33 @@ __device__ __forceinline__ void gs_ring_struct(GsRingRow& q, int32_t a, int32_t 
   q.pv[3] = v23.y;
 }
 
+// the row's new value into the ring and, in level order, into xl (a zero-diagonal gauss_seidel
+// row's bi holds its old x: that is its value)
 template <bool BLK>
 __device__ __forceinline__ void gs_ring_row(const GsRingRow& q, double* ring, int32_t RM,
-                                            double* x) {
-  const int32_t c[4] = {q.col.x, q.col.y, q.col.z, q.col.w};
+                                            double* __restrict__ xl) {
+  const uint32_t c[4] = {q.code.x & 0xFFFFu, q.code.x >> 16, q.code.y & 0xFFFFu, q.code.y >> 16};
   double rsum = gs_init<BLK>(q.bi);
 #pragma unroll
   for (int k = 0; k < kGsRingK; ++k) {
-    const double r = ring[c[k] & RM];
-    const double t = c[k] >= 0 ? gs_prod<BLK>(q.pv[k], r) : q.pv[k];
+    const double r = ring[c[k] & (uint32_t)RM];
+    const double t = c[k] < kGsRingLater ? gs_prod<BLK>(q.pv[k], r) : q.pv[k];
     const double u = gs_acc_prod<BLK>(rsum, t);
-    rsum = c[k] != -1 ? u : rsum;
+    rsum = c[k] != kGsRingPad ? u : rsum;
   }
-  const bool up = gs_upd<BLK>(q.diag);
-  const double xi = up ? gs_fin<BLK>(rsum, q.bi, q.diag) : q.bi;
+  const double xi = gs_upd<BLK>(q.diag) ? gs_fin<BLK>(rsum, q.bi, q.diag) : q.bi;
   ring[q.ok ? (q.pos & RM) : RM + 1] = xi;  // slot RM + 1: the sink of the clamped lanes
-  if (q.ok && up) x[q.row] = xi;
+  if (q.ok) xl[q.pos] = xi;
 }
 
 template <bool BLK>
-__global__ __launch_bounds__(kGsBlock) void k_gs_ring(const int32_t* __restrict__ rows,
-                                                      const int32_t* __restrict__ lptr,
+__global__ __launch_bounds__(kGsBlock) void k_gs_ring(const int32_t* __restrict__ lptr,
                                                       int32_t n_levels,
-                                                      const int32_t* __restrict__ rcol,
+                                                      const uint2* __restrict__ rcode,
                                                       const double* __restrict__ pv,
                                                       const double* __restrict__ pdiag,
                                                       const double* __restrict__ blvl,
-                                                      int ring_log2, double* x,
+                                                      int ring_log2, double* __restrict__ xl,
                                                       const int32_t* done) {
   extern __shared__ double ring[];  // 2^ring_log2 slots, the sink slot, then the level starts
   if (done && *done) return;
@@ -462,7 +471,7 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_ring(const int32_t* __restrict_
   const int32_t nl = n_levels, last = lp[nl] - 1;
   auto lvl = [&](GsRingRow& q, int32_t l) {  // level l's structure (l >= nl: no row)
     const int32_t a = lp[l < nl ? l : nl], z = lp[l + 1 < nl ? l + 1 : nl];
-    gs_ring_struct(q, a, z, last, rows, rcol, pv, pdiag, blvl);
+    gs_ring_struct(q, a, z, last, rcode, pv, pdiag, blvl);
   };
   constexpr int NS = kGsRingSets;
   GsRingRow S[NS];
@@ -474,8 +483,152 @@ __global__ __launch_bounds__(kGsBlock) void k_gs_ring(const int32_t* __restrict_
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
       lvl(S[(u + NS - 1) % NS], l + u + NS - 1);
-      gs_ring_row<BLK>(S[u], ring, RM, x);
+      gs_ring_row<BLK>(S[u], ring, RM, xl);
       __syncthreads();
+    }
+  }
+}
+
+// Rows longer than 8 off-diagonals (Galerkin levels; the wave-cooperative sweep's rows) with the
+// ring scheme of k_gs_ring: LPR lanes per row, each holding EPL slots of a level-ordered copy
+// padded to SPAN = LPR EPL slots per position (no pointer chasing: a step's loads depend on the
+// step index alone). Slot codes are fixed at setup: >= 0 the ring slot of an earlier-swept column
+// at most Wr levels back, <= kGsWringFar - p an earlier-swept column further back (its value is
+// read from xl at position p, two steps ahead: written at least Wr > NS levels before), or
+// later-swept / diagonal / pad. The slots' values are formed before each sweep by
+// k_gs_wring_prep (the later-swept products, the others' matrix values); the lanes form the
+// earlier-swept products and the row's first lane folds them in stored order, as k_gs_wave does.
+// A step is up to 1024 / LPR rows of one level (host table); the register sets of NS steps rotate
+// by unrolling. Values go to xl in level order (one scatter after the sweep).
+constexpr int32_t kGsWringPad = -1, kGsWringLater = -2, kGsWringDiag = -3, kGsWringFar = -16;
+constexpr size_t kGsWringLdsMax = 150 * 1024;
+template <int EPL>
+constexpr int gs_wring_sets() {
+  return 5;
+}
+
+template <bool BLK>
+__global__ void k_gs_wring_prep(const int32_t* __restrict__ rows, int64_t n,
+                                const int32_t* __restrict__ ip, const int32_t* __restrict__ ij,
+                                const double* __restrict__ ax, const int32_t* __restrict__ code,
+                                int span, const double* __restrict__ b,
+                                const double* __restrict__ x, double* __restrict__ pv,
+                                double* __restrict__ blvl, double* __restrict__ dlvl,
+                                const int32_t* done) {
+  if (done && *done) return;
+  const int64_t p = blockIdx.x * 256ll + threadIdx.x;
+  if (p >= n) return;
+  const int32_t i = rows[p], k0 = ip[i], len = ip[i + 1] - k0;
+  double diag = 0.0;
+  for (int k = 0; k < len; ++k) {
+    const int32_t c = code[p * span + k];
+    const double a = ax[k0 + k];
+    pv[p * span + k] = c == kGsWringLater ? gs_prod<BLK>(a, x[ij[k0 + k]]) : a;
+    if (c == kGsWringDiag) diag = a;  // the last stored diagonal entry counts
+  }
+  blvl[p] = (!BLK && diag == 0.0) ? x[i] : b[i];
+  dlvl[p] = BLK ? (diag != 0.0 ? 1.0 / diag : 0.0) : diag;
+}
+
+template <int EPL>
+struct GsWringRow {
+  int32_t pos, len;
+  bool ok;
+  double bi, dg;
+  int32_t code[EPL];
+  double pv[EPL], xf[EPL];
+};
+
+template <int LPR, int EPL, bool BLK>
+__global__ __launch_bounds__(1024) void k_gs_wring(const int2* __restrict__ steps, int32_t n_steps,
+                                                   int32_t last, const int32_t* __restrict__ code,
+                                                   const double* __restrict__ pv,
+                                                   const int32_t* __restrict__ plen,
+                                                   const double* __restrict__ blvl,
+                                                   const double* __restrict__ dlvl,
+                                                   int ring_log2, double* xl,
+                                                   const int32_t* done) {
+  constexpr int ROWS = 1024 / LPR, SPAN = LPR * EPL, NS = gs_wring_sets<EPL>();
+  extern __shared__ double lds[];  // ring (2^ring_log2 + 2) | products | diag flags | steps
+  if (done && *done) return;
+  const int32_t RM = (1 << ring_log2) - 1;
+  double* ring = lds;
+  double* gv = ring + (RM + 3);
+  uint16_t* gc = reinterpret_cast<uint16_t*>(gv + ROWS * SPAN);
+  int2* st = reinterpret_cast<int2*>(gc + ROWS * SPAN + 4);
+  for (int i = threadIdx.x; i < n_steps; i += 1024) st[i] = steps[i];
+  __syncthreads();
+  const int g = threadIdx.x / LPR, lane = threadIdx.x % LPR;
+  auto load = [&](GsWringRow<EPL>& q, int32_t t) {  // step t's structure (t >= n_steps: none)
+    const int2 d = st[t < n_steps ? t : n_steps - 1];
+    q.ok = t < n_steps && g < d.y;
+    q.pos = d.x + g;
+    const int64_t pc = q.ok ? q.pos : last;
+    q.len = plen[pc];
+    q.bi = blvl[pc];
+    q.dg = dlvl[pc];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      q.code[e] = code[pc * SPAN + lane + e * LPR];
+      q.pv[e] = pv[pc * SPAN + lane + e * LPR];
+    }
+  };
+  auto gather = [&](GsWringRow<EPL>& q) {  // the far columns' values (needs the codes)
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      const int32_t c = q.code[e];
+      q.xf[e] = xl[c <= kGsWringFar ? kGsWringFar - c : 0];
+    }
+  };
+  double* myv = gv + g * SPAN;
+  uint16_t* myc = gc + g * SPAN;
+  auto sweep = [&](const GsWringRow<EPL>& q) {
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      const int32_t c = q.code[e];
+      const double r = ring[c & RM];
+      const bool near = c >= 0, far = c <= kGsWringFar;
+      myv[lane + e * LPR] = (near || far) ? gs_prod<BLK>(q.pv[e], near ? r : q.xf[e]) : q.pv[e];
+      myc[lane + e * LPR] = (uint16_t)(c == kGsWringDiag);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0 && q.ok) {
+      double sum = gs_init<BLK>(q.bi);
+      int k = 0;
+      for (; k + 8 <= q.len; k += 8) {  // 8 LDS reads in flight, then the 8 ordered steps
+        double v[8];
+        uint32_t dflag[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          v[u] = myv[k + u];
+          dflag[u] = myc[k + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (!dflag[u]) sum = gs_acc_prod<BLK>(sum, v[u]);
+      }
+      for (; k < q.len; ++k)
+        if (!myc[k]) sum = gs_acc_prod<BLK>(sum, myv[k]);
+      const double xi = gs_upd<BLK>(q.dg) ? gs_fin<BLK>(sum, q.bi, q.dg) : q.bi;
+      ring[q.pos & RM] = xi;
+      xl[q.pos] = xi;
+    }
+    __syncthreads();
+  };
+  // step t: step t + NS - 1's structure and step t + NS - 3's far values go out, step t is swept
+  GsWringRow<EPL> S[NS];
+#pragma unroll
+  for (int u = 0; u < NS - 1; ++u) load(S[u], u);
+  gather(S[0]);
+  gather(S[1]);
+  for (int32_t t = 0; t < n_steps; t += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      load(S[(u + NS - 1) % NS], t + u + NS - 1);
+      gather(S[(u + 2) % NS]);
+      sweep(S[u]);
     }
   }
 }
@@ -838,6 +991,11 @@ static bool gs_wave_disabled() {  // MLAMG_GS_NO_WAVE=1: A/B runs, tests
   return e && e[0] == '1';
 }
 
+static bool gs_wring_disabled() {  // MLAMG_GS_NO_WRING=1: A/B runs, tests
+  const char* e = std::getenv("MLAMG_GS_NO_WRING");
+  return e && e[0] == '1';
+}
+
 static bool gs_win_disabled() {  // MLAMG_GS_NO_WIN=1: A/B runs, tests
   const char* e = std::getenv("MLAMG_GS_NO_WIN");
   return e && e[0] == '1';
@@ -889,7 +1047,7 @@ static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int itera
         default: launch_gs_win<8, 2, 4, BLK>(G, x, b, iterations, done, s); break;
       }
     }
-  } else if (pipe && G->rcol && G->rpv && !gs_ring_disabled() &&
+  } else if (pipe && G->rcol && G->rpv && G->rcode && G->rxl && !gs_ring_disabled() &&
              gs_ring_lds(G) <= kGsRingLdsMax) {
     const int64_t n = A->n_rows;
     // one sweep per launch pair: the products of the old values are formed before each
@@ -897,9 +1055,12 @@ static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int itera
       hipLaunchKernelGGL((k_gs_ring_prep<BLK>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                          G->rows, n, G->rcol, G->pk_val, G->pk_diag, b, x, G->rpv, G->b_lvl,
                          done);
-      hipLaunchKernelGGL((k_gs_ring<BLK>), dim3(1), dim3(kGsBlock), gs_ring_lds(G), s, G->rows,
-                         G->d_level_ptr, G->n_levels, G->rcol, G->rpv, G->pk_diag, G->b_lvl,
-                         G->ring_log2_r, x, done);
+      hipLaunchKernelGGL((k_gs_ring<BLK>), dim3(1), dim3(kGsBlock), gs_ring_lds(G), s,
+                         G->d_level_ptr, G->n_levels, reinterpret_cast<const uint2*>(G->rcode),
+                         G->rpv, G->pk_diag, G->b_lvl, G->ring_log2_r, G->rxl, done);
+      // the level-ordered values back to x (coalesced stores in the sweep, one scatter here)
+      hipLaunchKernelGGL(k_gs_win_post, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         G->rows, n, G->rxl, x, done);
     }
   } else if (pipe && G->max_level_rows <= 2 * kGsBlock) {
     const bool one = G->max_level_rows <= kGsBlock;
@@ -909,6 +1070,27 @@ static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int itera
     } else {
       if (one) launch_gs_pipe<1, 8, BLK>(G, x, b, iterations, done, s);
       else launch_gs_pipe<2, 8, BLK>(G, x, b, iterations, done, s);
+    }
+  } else if (G->wr_code && G->rxl && G->b_lvl && !gs_wring_disabled()) {
+    const int64_t n = A->n_rows;
+    const int span = G->wr_lpr * G->wr_epl;
+    auto go = [&](auto l, auto e) {
+      hipLaunchKernelGGL((k_gs_wring<decltype(l)::value, decltype(e)::value, BLK>), dim3(1),
+                         dim3(1024), G->wr_lds, s, G->wr_st, G->wr_steps, (int32_t)(n - 1),
+                         G->wr_code, G->wr_pv, G->wr_len, G->b_lvl, G->wr_d, G->wr_log2, G->rxl,
+                         done);
+    };
+    using I2 = std::integral_constant<int, 2>;
+    using I8 = std::integral_constant<int, 8>;
+    using I16 = std::integral_constant<int, 16>;
+    for (int it = 0; it < iterations; ++it) {
+      hipLaunchKernelGGL((k_gs_wring_prep<BLK>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                         s, G->rows, n, A->indptr, A->indices, A->data, G->wr_code, span, b, x,
+                         G->wr_pv, G->b_lvl, G->wr_d, done);
+      if (G->wr_lpr == 8) go(I8(), I2());
+      else go(I16(), I2());
+      hipLaunchKernelGGL(k_gs_win_post, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         G->rows, n, G->rxl, x, done);
     }
   } else if (G->wpos && G->max_level_rows <= kGsBlockMaxLevelRows && G->n_levels > 4 &&
              !gs_wave_disabled()) {
@@ -1009,8 +1191,106 @@ static void setup_ring(mlamg_gs* G, const std::vector<int32_t>& level,
     return;
   }
   (void)hipMemcpy(G->rcol, rc.data(), sizeof(int32_t) * rc.size(), hipMemcpyHostToDevice);
+  std::vector<uint16_t> code(rc.size());
+  const int32_t RM = (1 << lg) - 1;
+  for (size_t e = 0; e < rc.size(); ++e)
+    code[e] = (uint16_t)(rc[e] >= 0 ? (rc[e] & RM) : (rc[e] == -1 ? kGsRingPad : kGsRingLater));
   if (hipMalloc(&G->rpv, sizeof(double) * rc.size()) != hipSuccess) G->rpv = nullptr;
+  if (hipMalloc(&G->rxl, sizeof(double) * n) != hipSuccess) G->rxl = nullptr;
+  if (hipMalloc(&G->rcode, sizeof(uint16_t) * code.size()) != hipSuccess) G->rcode = nullptr;
+  else
+    (void)hipMemcpy(G->rcode, code.data(), sizeof(uint16_t) * code.size(), hipMemcpyHostToDevice);
   G->ring_log2_r = lg;
+}
+
+// The long-row ring sweep's plan (rows of 9..64 entries, levels swept in steps of 1024 / LPR
+// rows): the slot codes in the padded level order, the row lengths, the step table and the ring
+// (W levels of positions, <= 8,192 slots). Optional: wr_code stays nullptr otherwise.
+static void setup_wring(mlamg_gs* G, const std::vector<int32_t>& ip,
+                        const std::vector<int32_t>& ij, const std::vector<int32_t>& level,
+                        const std::vector<int32_t>& rows) {
+  const int64_t n = G->A->n_rows;
+  const int nlev = G->n_levels;
+  const int ml = G->max_len;
+  if (n == 0 || nlev <= 4 || ml > 64) return;
+  // 8 lanes per row when levels average more than 64 rows (a step covers 128), else 16; two
+  // slots per lane (rows of up to 32 entries): four would need register sets beyond the 128
+  // VGPRs of a 1024-thread workgroup (spilled: the 3-D 128^3 level-1 sweep ran 2x slower than
+  // k_gs_wave), so longer rows stay on k_gs_wave
+  const int lpr = (n > 64 * (int64_t)nlev && ml <= 16) ? 8 : 16;
+  const int epl = 2;
+  if (ml > lpr * epl) return;
+  const int span = lpr * epl, rows_per_step = 1024 / lpr;
+  std::vector<int32_t> pos(n);
+  for (int64_t p = 0; p < n; ++p) pos[rows[p]] = (int32_t)p;
+  int W = 0;
+  for (int64_t i = 0; i < n; ++i)
+    for (int k = ip[i]; k < ip[i + 1]; ++k)
+      if (ij[k] != i && level[ij[k]] < level[i]) W = std::max(W, level[i] - level[ij[k]]);
+  const std::vector<int32_t>& lp = G->level_ptr;
+  // the ring horizon Wr: the most levels back whose positions fit 8,192 slots; couplings further
+  // back are read from xl, which needs Wr >= NS + 1 levels
+  auto span_of = [&](int w) {
+    int64_t sp = 0;
+    for (int l = 0; l < nlev; ++l) sp = std::max<int64_t>(sp, lp[l + 1] - lp[std::max(0, l - w)]);
+    return sp;
+  };
+  int Wr = W;
+  while (Wr > 0 && span_of(Wr) > 8192) Wr = Wr * 7 / 8;
+  if (Wr < W && Wr < 8) return;
+  const int64_t spanp = span_of(Wr);
+  int lg = 0;
+  while ((int64_t(1) << lg) < spanp) ++lg;
+  if (lg > 13) return;
+  std::vector<int2> st;
+  for (int l = 0; l < nlev; ++l)
+    for (int32_t a = lp[l]; a < lp[l + 1]; a += rows_per_step)
+      st.push_back(make_int2(a, std::min<int32_t>(rows_per_step, lp[l + 1] - a)));
+  const size_t lds = sizeof(double) * (((size_t)1 << lg) + 3) +
+                     (sizeof(double) + sizeof(uint16_t)) * rows_per_step * span + 8 +
+                     sizeof(int2) * st.size() + 16;
+  if (lds > kGsWringLdsMax) return;
+  const int32_t RM = (1 << lg) - 1;
+  std::vector<int32_t> code((size_t)n * span, kGsWringPad);
+  std::vector<int32_t> len(n);
+  for (int64_t p = 0; p < n; ++p) {
+    const int32_t i = rows[p];
+    len[p] = ip[i + 1] - ip[i];
+    for (int k = ip[i]; k < ip[i + 1]; ++k) {
+      const int32_t j = ij[k];
+      int32_t c = kGsWringLater;
+      if (j == i) c = kGsWringDiag;
+      else if (level[j] < level[i]) c = level[i] - level[j] <= Wr ? (pos[j] & RM) : kGsWringFar - pos[j];
+      code[(size_t)p * span + (k - ip[i])] = c;
+    }
+  }
+  const size_t m = (size_t)n * span;
+  bool ok = hipMalloc(&G->wr_code, sizeof(int32_t) * m) == hipSuccess;
+  ok = ok && hipMalloc(&G->wr_pv, sizeof(double) * m) == hipSuccess;
+  ok = ok && hipMalloc(&G->wr_len, sizeof(int32_t) * n) == hipSuccess;
+  ok = ok && hipMalloc(&G->wr_d, sizeof(double) * n) == hipSuccess;
+  ok = ok && hipMalloc(&G->wr_st, sizeof(int2) * st.size()) == hipSuccess;
+  if (!G->rxl) ok = ok && hipMalloc(&G->rxl, sizeof(double) * n) == hipSuccess;
+  if (!G->b_lvl) ok = ok && hipMalloc(&G->b_lvl, sizeof(double) * n) == hipSuccess;
+  if (!ok) {
+    for (void* q : {(void*)G->wr_code, (void*)G->wr_pv, (void*)G->wr_len, (void*)G->wr_d,
+                    (void*)G->wr_st})
+      if (q) (void)hipFree(q);
+    G->wr_code = nullptr;
+    G->wr_pv = G->wr_d = nullptr;
+    G->wr_len = nullptr;
+    G->wr_st = nullptr;
+    return;
+  }
+  (void)hipMemcpy(G->wr_code, code.data(), sizeof(int32_t) * m, hipMemcpyHostToDevice);
+  (void)hipMemset(G->wr_pv, 0, sizeof(double) * m);
+  (void)hipMemcpy(G->wr_len, len.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice);
+  (void)hipMemcpy(G->wr_st, st.data(), sizeof(int2) * st.size(), hipMemcpyHostToDevice);
+  G->wr_lpr = lpr;
+  G->wr_epl = epl;
+  G->wr_steps = (int32_t)st.size();
+  G->wr_log2 = lg;
+  G->wr_lds = lds;
 }
 
 // The windowed one-wave sweep's plan: W = the widest level distance of a coupling, chunks of
@@ -1186,6 +1466,7 @@ static int gs_build(const mlamg_csr* A, bool backward, bool block, mlamg_gs** ou
       } else {
         G->wpos = nullptr;  // optional: the plain one-workgroup kernel takes these rows
       }
+      setup_wring(G, ip, ij, level, rows);
     }
     if (K && G->max_level_rows <= 2 * kGsBlock) {
       std::vector<double> ax(A->nnz);
@@ -1265,7 +1546,9 @@ int mlamg_gs_destroy(mlamg_gs* G) {
     if (G->bwd) mlamg_gs_destroy(G->bwd);
     for (void* q : {(void*)G->rows, (void*)G->d_level_ptr, (void*)G->pk_col, (void*)G->pk_val,
                     (void*)G->pk_diag, (void*)G->b_lvl, (void*)G->wcol, (void*)G->d_clev,
-                    (void*)G->win_xl, (void*)G->wpos, (void*)G->rcol, (void*)G->rpv})
+                    (void*)G->win_xl, (void*)G->wpos, (void*)G->rcol, (void*)G->rpv,
+                    (void*)G->rcode, (void*)G->rxl, (void*)G->wr_code, (void*)G->wr_pv,
+                    (void*)G->wr_len, (void*)G->wr_d, (void*)G->wr_st})
       if (q) (void)hipFree(q);
     delete G;
   }

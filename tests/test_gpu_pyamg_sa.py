@@ -148,6 +148,19 @@ def test_gauss_seidel_directions_bitwise(ml, oracle, torch_cuda, sweep, block):
     for i in (0, 7, 1234, 180_000, 359_999):
         Z.data[Z.indptr[i]:Z.indptr[i + 1]][Z.indices[Z.indptr[i]:Z.indptr[i + 1]] == i] = 0.0
     mats["poisson_600_zero_diag"] = Z
+    # 13 entries a row (12 off-diagonals), couplings up to 19,997 rows apart (6,667 levels of 3
+    # rows): the long-row ring sweep (k_gs_wring), with earlier-swept columns beyond its ring
+    # horizon (8,192 positions) read back from the level-ordered values
+    n = 20_000
+    offs = (3, 150, 1001, 3001, 6007, 9001, 15013, 19997)
+    O = sp.diags([np.full(n - o, -1.0 / (1 + k)) for k, o in enumerate(offs)], list(offs), (n, n))
+    W = sp.csr_matrix(O + O.T + sp.identity(n) * 13.0)
+    W.sort_indices()
+    mats["offsets_20k"] = W
+    W0 = W.copy()
+    for i in (5, 10_000, 19_999):
+        W0.data[W0.indptr[i]:W0.indptr[i + 1]][W0.indices[W0.indptr[i]:W0.indptr[i + 1]] == i] = 0.0
+    mats["offsets_20k_zero_diag"] = W0
     for name, A in mats.items():
         if name == "doc_isolated":
             continue
