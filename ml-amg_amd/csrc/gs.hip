@@ -506,6 +506,11 @@ template <int EPL>
 constexpr int gs_wring_sets() {
   return 5;
 }
+// four slots per lane: 512-thread workgroups (two waves per SIMD: 256 VGPRs for the five sets)
+template <int EPL>
+constexpr int gs_wring_threads() {
+  return EPL <= 2 ? 1024 : 512;
+}
 
 template <bool BLK>
 __global__ void k_gs_wring_prep(const int32_t* __restrict__ rows, int64_t n,
@@ -540,7 +545,7 @@ struct GsWringRow {
 };
 
 template <int LPR, int EPL, bool BLK>
-__global__ __launch_bounds__(1024) void k_gs_wring(const int2* __restrict__ steps, int32_t n_steps,
+__global__ __launch_bounds__(gs_wring_threads<EPL>()) void k_gs_wring(const int2* __restrict__ steps, int32_t n_steps,
                                                    int32_t last, const int32_t* __restrict__ code,
                                                    const double* __restrict__ pv,
                                                    const int32_t* __restrict__ plen,
@@ -548,7 +553,8 @@ __global__ __launch_bounds__(1024) void k_gs_wring(const int2* __restrict__ step
                                                    const double* __restrict__ dlvl,
                                                    int ring_log2, double* xl,
                                                    const int32_t* done) {
-  constexpr int ROWS = 1024 / LPR, SPAN = LPR * EPL, NS = gs_wring_sets<EPL>();
+  constexpr int TPB = gs_wring_threads<EPL>();
+  constexpr int ROWS = TPB / LPR, SPAN = LPR * EPL, NS = gs_wring_sets<EPL>();
   extern __shared__ double lds[];  // ring (2^ring_log2 + 2) | products | diag flags | steps
   if (done && *done) return;
   const int32_t RM = (1 << ring_log2) - 1;
@@ -556,7 +562,7 @@ __global__ __launch_bounds__(1024) void k_gs_wring(const int2* __restrict__ step
   double* gv = ring + (RM + 3);
   uint16_t* gc = reinterpret_cast<uint16_t*>(gv + ROWS * SPAN);
   int2* st = reinterpret_cast<int2*>(gc + ROWS * SPAN + 4);
-  for (int i = threadIdx.x; i < n_steps; i += 1024) st[i] = steps[i];
+  for (int i = threadIdx.x; i < n_steps; i += TPB) st[i] = steps[i];
   __syncthreads();
   const int g = threadIdx.x / LPR, lane = threadIdx.x % LPR;
   auto load = [&](GsWringRow<EPL>& q, int32_t t) {  // step t's structure (t >= n_steps: none)
@@ -1076,19 +1082,25 @@ static int gs_sweep_one(const mlamg_gs* G, double* x, const double* b, int itera
     const int span = G->wr_lpr * G->wr_epl;
     auto go = [&](auto l, auto e) {
       hipLaunchKernelGGL((k_gs_wring<decltype(l)::value, decltype(e)::value, BLK>), dim3(1),
-                         dim3(1024), G->wr_lds, s, G->wr_st, G->wr_steps, (int32_t)(n - 1),
+                         dim3(gs_wring_threads<decltype(e)::value>()), G->wr_lds, s, G->wr_st, G->wr_steps, (int32_t)(n - 1),
                          G->wr_code, G->wr_pv, G->wr_len, G->b_lvl, G->wr_d, G->wr_log2, G->rxl,
                          done);
     };
     using I2 = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, 4>;
     using I8 = std::integral_constant<int, 8>;
     using I16 = std::integral_constant<int, 16>;
     for (int it = 0; it < iterations; ++it) {
       hipLaunchKernelGGL((k_gs_wring_prep<BLK>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                          s, G->rows, n, A->indptr, A->indices, A->data, G->wr_code, span, b, x,
                          G->wr_pv, G->b_lvl, G->wr_d, done);
-      if (G->wr_lpr == 8) go(I8(), I2());
-      else go(I16(), I2());
+      if (G->wr_epl == 2) {
+        if (G->wr_lpr == 8) go(I8(), I2());
+        else go(I16(), I2());
+      } else {
+        if (G->wr_lpr == 8) go(I8(), I4());
+        else go(I16(), I4());
+      }
       hipLaunchKernelGGL(k_gs_win_post, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                          G->rows, n, G->rxl, x, done);
     }
@@ -1213,14 +1225,15 @@ static void setup_wring(mlamg_gs* G, const std::vector<int32_t>& ip,
   const int nlev = G->n_levels;
   const int ml = G->max_len;
   if (n == 0 || nlev <= 4 || ml > 64) return;
-  // 8 lanes per row when levels average more than 64 rows (a step covers 128), else 16; two
-  // slots per lane (rows of up to 32 entries): four would need register sets beyond the 128
-  // VGPRs of a 1024-thread workgroup (spilled: the 3-D 128^3 level-1 sweep ran 2x slower than
-  // k_gs_wave), so longer rows stay on k_gs_wave
-  const int lpr = (n > 64 * (int64_t)nlev && ml <= 16) ? 8 : 16;
-  const int epl = 2;
+  // 8 lanes per row when levels average more than 64 rows, else 16; two slots per lane in
+  // 1024-thread workgroups, four (rows of 33..64 entries, or 17..32 on wide levels) in 512-thread
+  // ones: five register sets of four slots exceed the 128 VGPRs a 1024-thread workgroup has
+  // (spilled, the 3-D 128^3 level-1 sweep ran 2x slower than k_gs_wave)
+  const bool wide = n > 64 * (int64_t)nlev;
+  const int lpr = (wide && ml <= 32) ? 8 : 16;
+  const int epl = ml <= 2 * lpr ? 2 : 4;
   if (ml > lpr * epl) return;
-  const int span = lpr * epl, rows_per_step = 1024 / lpr;
+  const int span = lpr * epl, rows_per_step = (epl == 2 ? 1024 : 512) / lpr;
   std::vector<int32_t> pos(n);
   for (int64_t p = 0; p < n; ++p) pos[rows[p]] = (int32_t)p;
   int W = 0;

@@ -161,6 +161,13 @@ def test_gauss_seidel_directions_bitwise(ml, oracle, torch_cuda, sweep, block):
     for i in (5, 10_000, 19_999):
         W0.data[W0.indptr[i]:W0.indptr[i + 1]][W0.indices[W0.indptr[i]:W0.indptr[i + 1]] == i] = 0.0
     mats["offsets_20k_zero_diag"] = W0
+    # 37 entries a row: four slots per lane (k_gs_wring in 512-thread workgroups)
+    offs2 = offs + (7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47)
+    O2 = sp.diags([np.full(n - o, -1.0 / (1 + k)) for k, o in enumerate(offs2)], list(offs2),
+                  (n, n))
+    W2 = sp.csr_matrix(O2 + O2.T + sp.identity(n) * 60.0)
+    W2.sort_indices()
+    mats["offsets_20k_long"] = W2
     for name, A in mats.items():
         if name == "doc_isolated":
             continue
