@@ -1241,28 +1241,34 @@ static void setup_wring(mlamg_gs* G, const std::vector<int32_t>& ip,
     for (int k = ip[i]; k < ip[i + 1]; ++k)
       if (ij[k] != i && level[ij[k]] < level[i]) W = std::max(W, level[i] - level[ij[k]]);
   const std::vector<int32_t>& lp = G->level_ptr;
-  // the ring horizon Wr: the most levels back whose positions fit 8,192 slots; couplings further
-  // back are read from xl, which needs Wr >= NS + 1 levels
+  std::vector<int2> st;
+  for (int l = 0; l < nlev; ++l)
+    for (int32_t a = lp[l]; a < lp[l + 1]; a += rows_per_step)
+      st.push_back(make_int2(a, std::min<int32_t>(rows_per_step, lp[l + 1] - a)));
+  // a step costs about what one of k_gs_wave's level passes does: levels much wider than a step
+  // stay there (3-D 128^3 level 1, 14 steps a level: V-cycle 63 -> 137 ms through this kernel)
+  if (st.size() > 2 * (size_t)nlev) return;
+  const size_t rest = sizeof(double) * 3 +
+                      (sizeof(double) + sizeof(uint16_t)) * rows_per_step * span + 8 +
+                      sizeof(int2) * st.size() + 16;
+  if (rest >= kGsWringLdsMax) return;
+  int64_t cap = 8192;  // ring slots: at most 8,192 and what the LDS budget leaves
+  while (cap > 1 && rest + sizeof(double) * cap > kGsWringLdsMax) cap >>= 1;
+  // the ring horizon Wr: the most levels back whose positions fit the ring; couplings further
+  // back are read from xl two steps ahead, which needs Wr >= 2 (a step advances <= 1 level)
   auto span_of = [&](int w) {
     int64_t sp = 0;
     for (int l = 0; l < nlev; ++l) sp = std::max<int64_t>(sp, lp[l + 1] - lp[std::max(0, l - w)]);
     return sp;
   };
   int Wr = W;
-  while (Wr > 0 && span_of(Wr) > 8192) Wr = Wr * 7 / 8;
-  if (Wr < W && Wr < 8) return;
+  while (Wr > 2 && span_of(Wr) > cap) Wr = std::max(2, Wr * 7 / 8);
+  if (span_of(Wr) > cap || (Wr < W && Wr < 2)) return;
   const int64_t spanp = span_of(Wr);
   int lg = 0;
   while ((int64_t(1) << lg) < spanp) ++lg;
-  if (lg > 13) return;
-  std::vector<int2> st;
-  for (int l = 0; l < nlev; ++l)
-    for (int32_t a = lp[l]; a < lp[l + 1]; a += rows_per_step)
-      st.push_back(make_int2(a, std::min<int32_t>(rows_per_step, lp[l + 1] - a)));
-  const size_t lds = sizeof(double) * (((size_t)1 << lg) + 3) +
-                     (sizeof(double) + sizeof(uint16_t)) * rows_per_step * span + 8 +
-                     sizeof(int2) * st.size() + 16;
-  if (lds > kGsWringLdsMax) return;
+  if (lg > 13 || (int64_t(1) << lg) > cap) return;
+  const size_t lds = rest + (sizeof(double) << lg);
   const int32_t RM = (1 << lg) - 1;
   std::vector<int32_t> code((size_t)n * span, kGsWringPad);
   std::vector<int32_t> len(n);
