@@ -1520,7 +1520,8 @@ static int gs_build(const mlamg_csr* A, bool backward, bool block, mlamg_gs** ou
         }
         G->pk_k = K;
         phase("pack_upload");
-        setup_window(G, ip, ij, level, rows, pcol, K);
+        static const char* prefer_ring = std::getenv("MLAMG_GS_PREFER_RING");  // A/B knob
+        if (!(prefer_ring && prefer_ring[0] == '1')) setup_window(G, ip, ij, level, rows, pcol, K);
         phase("window");
         if (K == kGsRingK && G->win_rw == 0) setup_ring(G, level, rows, pcol);
       } else {  // optional: the sweep falls back to the plain kernels
