@@ -477,6 +477,20 @@ int mlamg_gmres_householder(const mlamg_csr* A, mlamg_hier* M, const double* b, 
 /* use the PCG solver C (size = A_coarse rows) as H's coarsest solve instead of a dense inverse;
  * cycles of such a hierarchy run eagerly (use_graph is ignored) */
 int mlamg_hier_set_coarse_pcg(mlamg_hier* H, const mlamg_csr* A_coarse, mlamg_pcg* C);
+/* H's coarsest solve by restarted GMRES (mlamg_gmres's algorithm) on A_coarse, preconditioned by
+ * one V-cycle of `inner` (a hierarchy of A_coarse, kept alive by the caller), from a zero guess
+ * to ||b - A_c x|| <= rtol ||b|| (restart, maxiter restart cycles): for a coarse operator that is
+ * not SPD (PCG does not apply) and beyond the dense inverse's size — the reference factors any
+ * nonsingular A_H with SuperLU (ns/lib/multigrid.py:165-170). Cycles run eagerly. A solve that
+ * ends above fail_rtol makes the cycle call return MLAMG_EINVAL ("did not converge"), as a
+ * failed factorisation would. */
+int mlamg_hier_set_coarse_gmres(mlamg_hier* H, const mlamg_csr* A_coarse, mlamg_hier* inner,
+                                double rtol, double fail_rtol, int restart, int maxiter);
+/* GMRES coarse-solve statistics since H was built: solves, steps of the last one, total steps,
+ * solves that did not reach rtol, largest final relative residual (each nullable) */
+int mlamg_hier_coarse_gmres_stats(const mlamg_hier* H, int32_t* solves, int32_t* last_iters,
+                                  int32_t* total_iters, int32_t* not_converged,
+                                  double* worst_rel);
 /* ---------------------------------------------------------------- batched reference solves
  * The reference's own call pattern — two-level amg_2_v(A, P, b, x, ...) on small grids
  * (ns/lib/multigrid.py:111-210, called per grid by utils/common.py:77,106,

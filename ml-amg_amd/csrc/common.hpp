@@ -350,6 +350,11 @@ int pcg_solve_impl(mlamg_pcg* C, const double* b, double* x, const int32_t* oute
                    hipStream_t s);
 int64_t pcg_rows(const mlamg_pcg* C);
 mlamg_hier* pcg_inner(mlamg_pcg* C);
+// restarted left-preconditioned GMRES (scipy's algorithm) with one V-cycle of M as
+// preconditioner (gmres.hip); rel_out (optional): final ||b - A x|| / ||b||
+int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, double rtol,
+               int restart, int maxiter, bool x_zero, int* info_out, int* iters_out,
+               double* presid_hist, int hist_cap, hipStream_t s, double* rel_out = nullptr);
 int hier_prepare_ext(mlamg_hier* H);
 int gs_sweep_impl(const mlamg_gs* G, double* x, const double* b, int iterations,
                   const int32_t* done, hipStream_t s);

@@ -261,8 +261,9 @@ struct GmWork {
 
 int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, double rtol,
                int restart, int maxiter, bool x_zero, int* info_out, int* iters_out,
-               double* presid_hist, int hist_cap, hipStream_t s) {
+               double* presid_hist, int hist_cap, hipStream_t s, double* rel_out) {
   const int64_t n = A->n_rows;
+  if (rel_out) *rel_out = 0.0;
   if (restart <= 0) restart = 20;
   restart = (int)std::min<int64_t>(restart, std::max<int64_t>(n, 1));
   if (maxiter <= 0) maxiter = (int)std::min<int64_t>(INT32_MAX, 10 * std::max<int64_t>(n, 1));
@@ -367,7 +368,10 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
       }
       double r0 = 0.0;
       MLAMG_TRY(norm(W.r, &r0));
-      if (r0 < atol) break;
+      if (r0 < atol) {
+        rnorm = r0;
+        break;
+      }
     }
     MLAMG_TRY(psolve(W.r, V0));
     double tmp = 0.0;
@@ -448,6 +452,7 @@ int gmres_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, double* x, do
   }
   *info_out = rnorm <= atol ? 0 : maxiter;
   *iters_out = iters;
+  if (rel_out) *rel_out = rnorm / bnrm2;
   if (presid_hist && iters > 0)
     MLAMG_HIP(hipMemcpyAsync(presid_hist, W.hist, sizeof(double) * std::min(iters, hist_cap),
                              hipMemcpyDeviceToHost, s));
@@ -669,8 +674,8 @@ int gmres_householder_impl(const mlamg_csr* A, mlamg_hier* M, const double* b, d
     ++niter;
     if (inner < max_inner - 1) {
       normr = std::fabs(g[inner + 1]);
+      if (normr < tol) break;  // pyamg breaks before recording the estimate
       if (resid_hist && nh < hist_cap) resid_hist[nh++] = normr;
-      if (normr < tol) break;
     }
   }
   if (inner == max_inner) inner = max_inner - 1;

@@ -48,6 +48,14 @@ struct mlamg_hier {
   const mlamg_csr* Ac = nullptr;
   const mlamg_dense* D = nullptr;
   mlamg_pcg* pcg = nullptr;  // coarse solve by inner-hierarchy PCG instead of a dense inverse
+  // coarse solve by GMRES preconditioned by one V-cycle of an inner hierarchy of A_c (a coarse
+  // operator that is not SPD and beyond the dense inverse's size: the reference's SuperLU
+  // factors any nonsingular A_H, ns/lib/multigrid.py:165-170)
+  mlamg_hier* gm_inner = nullptr;
+  double gm_rtol = 1e-14, gm_fail_rtol = 1e-10;
+  int gm_restart = 50, gm_maxiter = 20;
+  int32_t gm_solves = 0, gm_last_iters = 0, gm_total_iters = 0, gm_not_converged = 0;
+  double gm_worst_rel = 0.0;
   double* xc = nullptr;
   double* bc = nullptr;
   int nu_pre = 1, nu_post = 1;
@@ -101,20 +109,60 @@ static void hier_free_graph(mlamg_hier* H) {
 }
 
 static int64_t coarse_rows(const mlamg_hier* H) {
-  return H->D ? H->D->n : pcg_rows(H->pcg);
+  if (H->D) return H->D->n;
+  if (H->gm_inner) return H->Ac->n_rows;
+  return pcg_rows(H->pcg);
 }
 
-// the coarsest solve: dense inverse GEMV, or inner-hierarchy PCG (pcg.hip)
+// a coarse solve that is driven from the host (PCG polls its flag, GMRES reads its status every
+// step): the cycle runs eagerly, never from a captured graph
+static bool host_driven_coarse(const mlamg_hier* H) { return H->pcg || H->gm_inner; }
+
+// x = A_c^-1 b by GMRES from a zero guess to ||b - A_c x|| <= gm_rtol ||b||; every solve's
+// outcome is counted (mlamg_hier_coarse_gmres_stats). Skipped once the outer tolerance flag is
+// up (later kernels of the cycle then do nothing either)
+static int gmres_coarse(mlamg_hier* H, const double* b, double* x, const int32_t* done,
+                        hipStream_t s) {
+  if (done) {
+    int32_t d = 0;
+    MLAMG_HIP(hipMemcpyAsync(&d, done, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    MLAMG_HIP(hipStreamSynchronize(s));
+    if (d) return MLAMG_OK;
+  }
+  const int64_t n = H->Ac->n_rows;
+  MLAMG_HIP(hipMemsetAsync(x, 0, sizeof(double) * n, s));
+  int info = 0, it = 0;
+  double rel = 0.0;
+  MLAMG_TRY(gmres_impl(H->Ac, H->gm_inner, b, x, H->gm_rtol, H->gm_restart, H->gm_maxiter, true,
+                       &info, &it, nullptr, 0, s, &rel));
+  H->gm_solves += 1;
+  H->gm_last_iters = it;
+  H->gm_total_iters += it;
+  if (info != 0) H->gm_not_converged += 1;
+  H->gm_worst_rel = std::max(H->gm_worst_rel, rel);
+  if (!(rel <= H->gm_fail_rtol)) {  // NaN included
+    char msg[160];
+    snprintf(msg, sizeof msg,
+             "GMRES coarse solve did not converge (final relative residual %.3e > %.1e): the "
+             "coarse operator may be singular", rel, H->gm_fail_rtol);
+    set_error(msg);
+    return MLAMG_EINVAL;
+  }
+  return MLAMG_OK;
+}
+
+// the coarsest solve: dense inverse GEMV, inner-hierarchy PCG (pcg.hip) or GMRES (gmres.hip)
 static int coarse_solve(mlamg_hier* H, const double* b, double* x, const int32_t* done,
                         hipStream_t s) {
   if (H->D) return dense_solve_impl(H->D, b, x, done, s);
+  if (H->gm_inner) return gmres_coarse(H, b, x, done, s);
   return pcg_solve_impl(H->pcg, b, x, done, s);
 }
 
 static int hier_prepare(mlamg_hier* H) {
   if (H->ready) return MLAMG_OK;
-  MLAMG_REQUIRE(H->D != nullptr || H->pcg != nullptr,
-                "coarse solver not set (mlamg_hier_set_coarse / mlamg_hier_set_coarse_pcg)");
+  MLAMG_REQUIRE(H->D != nullptr || H->pcg != nullptr || H->gm_inner != nullptr,
+                "coarse solver not set (mlamg_hier_set_coarse / _pcg / _gmres)");
   size_t total = 0;
   auto add = [&](int64_t n) {
     size_t b = sizeof(double) * (size_t)std::max<int64_t>(n, 1);
@@ -307,7 +355,7 @@ int64_t hier_fine_rows(const mlamg_hier* H) {
 int hier_coarse_cycle(mlamg_hier* H, const double* b, double** x_out, int use_graph,
                       hipStream_t s) {
   MLAMG_TRY(hier_prepare(H));
-  if (!use_graph || H->pcg) return cycle_coarse(H, 0, b, x_out, s);
+  if (!use_graph || host_driven_coarse(H)) return cycle_coarse(H, 0, b, x_out, s);
   if (!(H->cexec && H->cg_b == b && H->cg_epoch == format_epoch())) {
     if (H->cexec) (void)hipGraphExecDestroy(H->cexec);
     if (H->cgraph) (void)hipGraphDestroy(H->cgraph);
@@ -383,6 +431,8 @@ int mlamg_hier_set_coarse(mlamg_hier* H, const mlamg_csr* A_coarse, const mlamg_
     MLAMG_REQUIRE(H->lv.back().P->n_cols == D->n, "coarse size does not match last P");
   H->Ac = A_coarse;
   H->D = D;
+  H->pcg = nullptr;
+  H->gm_inner = nullptr;
   return MLAMG_OK;
 }
 
@@ -395,6 +445,43 @@ int mlamg_hier_set_coarse_pcg(mlamg_hier* H, const mlamg_csr* A_coarse, mlamg_pc
   H->Ac = A_coarse;
   H->D = nullptr;
   H->pcg = C;
+  H->gm_inner = nullptr;
+  return MLAMG_OK;
+}
+
+int mlamg_hier_set_coarse_gmres(mlamg_hier* H, const mlamg_csr* A_coarse, mlamg_hier* inner,
+                                double rtol, double fail_rtol, int restart, int maxiter) {
+  MLAMG_REQUIRE(H && A_coarse && inner, "NULL argument");
+  MLAMG_REQUIRE(inner != H, "the preconditioner hierarchy must be another hierarchy");
+  MLAMG_REQUIRE(!H->ready, "hierarchy already finalised");
+  MLAMG_REQUIRE(A_coarse->n_rows == A_coarse->n_cols, "A_coarse must be square");
+  MLAMG_REQUIRE(hier_fine_rows(inner) == A_coarse->n_rows,
+                "preconditioner hierarchy does not match A_coarse");
+  MLAMG_REQUIRE(rtol >= 0.0 && fail_rtol >= rtol && restart > 0 && maxiter > 0,
+                "invalid GMRES parameters");
+  if (!H->lv.empty())
+    MLAMG_REQUIRE(H->lv.back().P->n_cols == A_coarse->n_rows, "coarse size does not match last P");
+  H->Ac = A_coarse;
+  H->D = nullptr;
+  H->pcg = nullptr;
+  H->gm_inner = inner;
+  H->gm_rtol = rtol;
+  H->gm_fail_rtol = fail_rtol;
+  H->gm_restart = restart;
+  H->gm_maxiter = maxiter;
+  return MLAMG_OK;
+}
+
+int mlamg_hier_coarse_gmres_stats(const mlamg_hier* H, int32_t* solves, int32_t* last_iters,
+                                  int32_t* total_iters, int32_t* not_converged,
+                                  double* worst_rel) {
+  MLAMG_REQUIRE(H, "NULL argument");
+  MLAMG_REQUIRE(H->gm_inner, "the coarse solve is not GMRES");
+  if (solves) *solves = H->gm_solves;
+  if (last_iters) *last_iters = H->gm_last_iters;
+  if (total_iters) *total_iters = H->gm_total_iters;
+  if (not_converged) *not_converged = H->gm_not_converged;
+  if (worst_rel) *worst_rel = H->gm_worst_rel;
   return MLAMG_OK;
 }
 
@@ -471,8 +558,9 @@ int mlamg_hier_vcycle(mlamg_hier* H, const double* b, double* x, int n_cycles, d
     }
     b = H->zero_b;
   }
-  // a PCG coarse solve polls its convergence flag between iterations: cycles run eagerly
-  if (H->pcg) use_graph = 0;
+  // a PCG coarse solve polls its convergence flag between iterations, GMRES reads its status
+  // every step: cycles run eagerly
+  if (host_driven_coarse(H)) use_graph = 0;
   MLAMG_HIP(hipMemsetAsync(H->flags, 0, 2 * sizeof(int32_t), s));
   // no tolerance: no kernel can raise the stop flag, so none tests it (restored on return: a
   // PCG that uses H as its preconditioner shares the flag, hier_done_flag)
@@ -598,6 +686,14 @@ static int cycle_bytes(const mlamg_hier* H, bool stored, double* bytes) {
     MLAMG_TRY(stored ? mlamg_csr_format_bytes(H->Ac, &a) : (a = spmv_bytes(H->Ac), MLAMG_OK));
     MLAMG_TRY(cycle_bytes(pcg_inner(H->pcg), stored, &inner));
     t += (double)std::max(it, 1) * (a + 80.0 * (double)H->Ac->n_rows + inner);
+  }
+  if (H->gm_inner) {  // priced per GMRES step of the last solve: A_c x + one inner V-cycle +
+                      // ~2 (k + 1) Gram-Schmidt vector passes, k ~ restart / 2 on average
+    double a = 0.0, inner = 0.0;
+    MLAMG_TRY(stored ? mlamg_csr_format_bytes(H->Ac, &a) : (a = spmv_bytes(H->Ac), MLAMG_OK));
+    MLAMG_TRY(cycle_bytes(H->gm_inner, stored, &inner));
+    t += (double)std::max(H->gm_last_iters, 1) *
+         (a + inner + 8.0 * (double)(H->gm_restart + 2) * (double)H->Ac->n_rows);
   }
   *bytes = t;
   return MLAMG_OK;

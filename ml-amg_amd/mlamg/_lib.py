@@ -161,6 +161,8 @@ SIGNATURES = {
                                   c_vp]),
     "mlamg_amg2v_batch_limits": (c_int, [P_i64, P_i64, P_int]),
     "mlamg_hier_set_coarse_pcg": (c_int, [c_vp, c_vp, c_vp]),
+    "mlamg_hier_set_coarse_gmres": (c_int, [c_vp, c_vp, c_vp, c_dbl, c_dbl, c_int, c_int]),
+    "mlamg_hier_coarse_gmres_stats": (c_int, [c_vp, P_i32, P_i32, P_i32, P_i32, P_dbl]),
     "mlamg_pcg_create": (c_int, [c_vp, c_vp, c_dbl, c_int, c_vpp]),
     "mlamg_pcg_destroy": (c_int, [c_vp]),
     "mlamg_pcg_solve": (c_int, [c_vp, c_vp, c_vp, c_vp]),

@@ -62,9 +62,53 @@ def csr_symmetric(M, rtol=0.0):
     return bool(ok.value)
 
 
+def _pyamg_empty_level(H, L, A_dev, agg, cpts, rounds, Bv, lvl, improve_iterations, rho,
+                       omega):
+    """pyamg_sa's level when standard aggregation finds no aggregate: an n x 1 empty AggOp
+    (pyamg's standard_aggregation return), T = 0, B_c = [0], P = 0 (n x 1), R = P^T, A_c =
+    [[0]]. The level keeps its symmetric block Gauss-Seidel smoother (pyamg still smooths it;
+    for the operators this happens on — no off-diagonal couplings — the sweep is an exact
+    solve). Appends L to H and returns (A_c, B_c)."""
+    from .multigrid import GaussSeidel
+    n = A_dev.shape[0]
+    dev = _device()
+    L.Agg = DeviceCSR.from_scipy(sp.csr_matrix((n, 1)))
+    L.agg_col = agg
+    L.seeds = cpts[:0]
+    L.n_seeds = 1
+    L.bf_sweeps = int(rounds.value)
+    if lvl == 0 and improve_iterations > 0:
+        L.gs = GaussSeidel(A_dev, "symmetric", block=True)
+        L.gs.sweep(Bv, torch.zeros_like(Bv), int(improve_iterations))
+    L.B = Bv
+    dinv = torch.empty(n, dtype=torch.float64, device=dev)
+    call("mlamg_diag_pinv", A_dev.handle, ptr(dinv), stream_ptr())
+    if rho == "lanczos":
+        # rho(D^-1 A) of an operator without off-diagonal couplings: 1 where a_ii != 0
+        L.lam = 1.0 if bool((dinv != 0).any()) else 0.0
+    elif rho == "arnoldi":  # pyamg's estimate (draws from numpy's global generator)
+        from .strength import approximate_spectral_radius
+        h = ctypes.c_void_p()
+        call("mlamg_csr_scale_rows", A_dev.handle, ptr(dinv), 0, ctypes.byref(h), stream_ptr())
+        L.lam = approximate_spectral_radius(DeviceCSR(h))
+    else:
+        r = _level_item(rho, lvl) if isinstance(rho, (list, tuple)) else rho
+        if r is None:
+            raise ValueError(f"no rho given for level {lvl}")
+        L.lam = float(r)
+    L.omega = omega / L.lam if L.lam else 0.0
+    L.P = DeviceCSR.from_scipy(sp.csr_matrix((n, 1)))
+    L.R = DeviceCSR.from_scipy(sp.csr_matrix((1, n)))
+    L.dinv = dinv
+    H.galerkin_s.append(0.0)
+    H.levels.append(L)
+    return (DeviceCSR.from_scipy(sp.csr_matrix((1, 1))),
+            torch.zeros(1, dtype=torch.float64, device=dev))
+
+
 class Level:
     __slots__ = ("A", "dinv", "P", "R", "Agg", "omega", "lam", "lanczos_iters", "n_seeds",
-                 "bf_sweeps", "seeds", "gs", "labels", "agg_col", "B")
+                 "bf_sweeps", "seeds", "gs", "labels", "agg_col", "B", "sa_prolong")
 
     def __init__(self, A):
         self.A = A
@@ -79,6 +123,7 @@ class Level:
         self.labels = None  # per-node aggregate seed (node id, -1 none) when built by BF
         self.agg_col = None  # per-node aggregate column (int32 device tensor, -1 none)
         self.B = None  # near-nullspace candidate fitted at this level (pyamg_sa)
+        self.sa_prolong = False  # P = (I - omega D^-1 A) Agg formed here (mlamg_sa_smoother)
 
 
 _PHASES = ("count", "alloc", "expand", "sort", "runsum", "emit", "finalize", "free")
@@ -139,12 +184,14 @@ class Hierarchy:
         self.Ac = None
         self.dense = None
         self.handle = None
+        self.recipe = "mlamg_sa"  # Hierarchy.build / two_level; "pyamg_sa" from pyamg_sa()
         self.jacobi_weight = 2.0 / 3.0
         self.nu_pre = 1
         self.nu_post = 1
         self.timings = {}
         self.pcg = None
         self.inner = None
+        self.coarse_gmres = False  # coarsest solve by GMRES + inner hierarchy (_make_coarse_gmres)
         self._breakdowns_seen = 0
         self._factored = {}
 
@@ -155,7 +202,8 @@ class Hierarchy:
         """Two-level cycle with a given P: MLAMG.amg_2_v (ns/preconditioner/MLAMG.py:120-122,
         smoother='jacobi') or multigrid.amg_2_v (multigrid.py:111-210, smoother='gauss_seidel';
         norm='x' records ||x||_2 per cycle, the error_tol mode). coarse='dense' forces the
-        dense inverse (up to DENSE_LIMIT rows) where 'auto' would take PCG."""
+        dense inverse (up to DENSE_LIMIT rows) where 'auto' would take PCG; coarse='gmres'
+        the GMRES coarse solve (any A_c; Hierarchy._make_coarse_gmres)."""
         from .multigrid import GaussSeidel
         H = cls()
         H.jacobi_weight = omega
@@ -174,8 +222,11 @@ class Hierarchy:
         if coarse == "dense" and n_c > cls.DENSE_LIMIT:
             raise CoarseSolveError(f"coarse operator of {n_c} rows: the dense solver is limited "
                                    f"to {cls.DENSE_LIMIT} rows")
+        if coarse not in ("auto", "dense", "gmres"):
+            raise ValueError(f"unknown coarse solver {coarse!r}")
         H._finalize(nu_pre, nu_post,
-                    dense_max=n_c if coarse == "dense" else cls.TWO_LEVEL_DENSE_MAX)
+                    dense_max=n_c if coarse == "dense" else cls.TWO_LEVEL_DENSE_MAX,
+                    coarse="gmres" if coarse == "gmres" else None)
         torch.cuda.synchronize()
         tm["coarse_solver"], t0 = time.perf_counter() - t0, time.perf_counter()
         if smoother == "gauss_seidel":
@@ -386,6 +437,12 @@ class Hierarchy:
             call("mlamg_hier_set_factored_prolong", self.handle, int(level), None, None, None)
             self._factored.pop(level, None)
             return
+        if self.recipe != "mlamg_sa" or not L.sa_prolong:
+            # pyamg_sa's P = T - (w/rho) D^-1 A T smooths the normalised candidate T, not the
+            # 0/1 aggregate operator: the factored form would be a different prolongator
+            raise _lib.MlamgError(_lib.MLAMG_EUNSUPPORTED, "factored prolongation needs "
+                                  "P = (I - w D^-1 A) Agg built by Hierarchy.build "
+                                  f"(recipe {self.recipe!r}, level {level})")
         if L.agg_col is None or L.omega is None:
             raise ValueError("factored prolongation needs the level's aggregates and SA weight")
         ip, ij, ax = L.A.arrays()
@@ -530,6 +587,7 @@ class Hierarchy:
                      stream_ptr())
                 S = DeviceCSR(h)
                 L.P = S @ L.Agg
+                L.sa_prolong = True
                 del S
             else:
                 L.P = as_device(P_given)
@@ -644,7 +702,13 @@ class Hierarchy:
             del C
             k = int(k.value)
             if k == 0:
-                raise ValueError(f"level {lvl}: standard aggregation found no aggregate")
+                # no node has an off-diagonal strength entry (a diagonal or fully decoupled
+                # operator): pyamg's standard_aggregation returns an n x 1 empty AggOp, so
+                # T = 0, B_c = 0, P = 0 and A_c = [[0]], whose pinv is 0 (a zero coarse
+                # correction); the level keeps its smoother
+                A_dev, Bv = _pyamg_empty_level(H, L, A_dev, agg, cpts, rounds, Bv, lvl,
+                                               improve_iterations, rho, omega)
+                continue
             L.Agg = aggregate_op_device(agg, k)
             L.agg_col = agg
             L.seeds = cpts[:k]
@@ -771,19 +835,34 @@ class Hierarchy:
     DENSE_LIMIT = 32768
     SYMMETRY_RTOL = 1e-12  # dense.hip's "symmetric to rounding" test
 
-    def _finalize(self, nu_pre, nu_post, dense_max=None, coarse_rtol=None):
+    # coarsest solve of an operator that is not SPD and beyond DENSE_LIMIT rows: restarted GMRES
+    # (restart GMRES_RESTART, at most GMRES_MAXITER restart cycles) preconditioned by one V-cycle
+    # of an inner hierarchy, to ||r|| <= GMRES_RTOL ||b||; a solve whose final relative residual
+    # stays above GMRES_FAIL_RTOL is a failed coarse solve (CoarseSolveError, like a SuperLU
+    # factorisation failure)
+    GMRES_RTOL = 1e-14
+    GMRES_RESTART = 50
+    GMRES_MAXITER = 20
+    GMRES_FAIL_RTOL = 1e-10
+
+    def _finalize(self, nu_pre, nu_post, dense_max=None, coarse_rtol=None, coarse=None):
+        """coarse: None chooses (dense inverse up to dense_max rows; above, PCG for a symmetric
+        A_c, else the dense inverse up to DENSE_LIMIT rows, else GMRES); 'gmres' forces GMRES."""
         self.nu_pre, self.nu_post = nu_pre, nu_post
         dense_max = self.DENSE_MAX if dense_max is None else dense_max
         n_c = self.Ac.shape[0]
-        if n_c > dense_max and not csr_symmetric(self.Ac, self.SYMMETRY_RTOL):
+        use_gmres = coarse == "gmres"
+        if not use_gmres and n_c > dense_max and not csr_symmetric(self.Ac, self.SYMMETRY_RTOL):
             # PCG needs an SPD A_c (a Galerkin P^T A P of an SPD A is symmetric to rounding);
-            # SuperLU, which the reference uses, takes any nonsingular A_H
+            # SuperLU, which the reference uses, takes any nonsingular A_H: an exact dense
+            # inverse up to DENSE_LIMIT rows, GMRES beyond
             if n_c > self.DENSE_LIMIT:
-                raise CoarseSolveError(f"coarse operator of {n_c} rows is not symmetric: the "
-                                       "PCG coarse solve needs an SPD operator and the dense "
-                                       f"solver is limited to {self.DENSE_LIMIT} rows")
-            dense_max = n_c
-        if n_c <= dense_max:
+                use_gmres = True
+            else:
+                dense_max = n_c
+        if use_gmres:
+            self._make_coarse_gmres()
+        elif n_c <= dense_max:
             h = ctypes.c_void_p()
             call("mlamg_dense_create", self.Ac.handle, ctypes.byref(h), stream_ptr())
             self.dense = h
@@ -796,9 +875,25 @@ class Hierarchy:
             call("mlamg_hier_add_level", hh, L.A.handle, ptr(L.dinv), L.P.handle, L.R.handle)
         if self.dense is not None:
             call("mlamg_hier_set_coarse", hh, self.Ac.handle, self.dense)
-        else:
+        elif self.pcg is not None:
             call("mlamg_hier_set_coarse_pcg", hh, self.Ac.handle, self.pcg)
+        else:
+            call("mlamg_hier_set_coarse_gmres", hh, self.Ac.handle, self.inner.handle,
+                 float(self.GMRES_RTOL), float(self.GMRES_FAIL_RTOL), int(self.GMRES_RESTART),
+                 int(self.GMRES_MAXITER))
         call("mlamg_hier_set_smoothing", hh, int(nu_pre), int(nu_post))
+
+    def _make_coarse_gmres(self):
+        """Coarsest solve for a coarse operator that is not SPD (non-symmetric, or indefinite:
+        PCG broke down) and too large for the dense inverse: GMRES on A_c preconditioned by one
+        V(2,2) cycle of an inner smoothed-aggregation hierarchy of A_c (weighted Jacobi w = 2/3,
+        a dense coarsest inverse) — the reference factors any nonsingular A_H with SuperLU
+        (ns/lib/multigrid.py:165-170)."""
+        self.inner = Hierarchy.build(self.Ac, alpha=0.1, max_coarse=self.PCG_INNER_MAX_COARSE,
+                                     jacobi_weight=2.0 / 3.0, lanczos_tol=1e-8,
+                                     nu_pre=self.PCG_INNER_NU, nu_post=self.PCG_INNER_NU,
+                                     fine_format="csr_stream", coarse_format="exact")
+        self.coarse_gmres = True
 
     def _make_coarse_pcg(self, rtol, maxit=200):
         """Coarsest solve for an operator too large for the dense inverse (the reference
@@ -818,9 +913,17 @@ class Hierarchy:
         self.pcg = h
 
     def coarse_stats(self):
-        """PCG coarse solver statistics (None with a dense coarse inverse): iterations of the
-        last solve, solves that stopped at maxit, total iterations, largest final relative
-        residual."""
+        """PCG / GMRES coarse solver statistics (None with a dense coarse inverse): iterations
+        of the last solve, solves that stopped at maxit, total iterations, largest final
+        relative residual (GMRES: also the number of solves)."""
+        if getattr(self, "coarse_gmres", False) and self.handle:
+            sv, a, c, b = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+            d = ctypes.c_double()
+            call("mlamg_hier_coarse_gmres_stats", self.handle, ctypes.byref(sv), ctypes.byref(a),
+                 ctypes.byref(c), ctypes.byref(b), ctypes.byref(d))
+            return {"solver": "gmres", "solves": sv.value, "last_iters": a.value,
+                    "not_converged": b.value, "total_iters": c.value,
+                    "max_rel_residual": d.value, "breakdowns": 0}
         if getattr(self, "pcg", None) is None:
             return None
         a, b, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
@@ -835,13 +938,28 @@ class Hierarchy:
     def check_coarse(self):
         """Raise if a PCG coarse solve broke down (A_c or its preconditioner not positive
         definite: the iterate is not a solve of the coarse system). Syncs."""
+        if self.pcg is None and not self.coarse_gmres:
+            return
         st = self.coarse_stats()
+        if st.get("solver") == "gmres":  # a failed solve already ended its call (_gmres_call)
+            return
         if st is not None and st["breakdowns"] > self._breakdowns_seen:
             self._breakdowns_seen = st["breakdowns"]
             raise CoarseSolveError(f"PCG coarse solve broke down ({st['breakdowns']} solves): "
                                    "the coarse operator is not positive definite")
 
     # ------------------------------------------------------------------ cycling
+    def _solve_call(self, fn, *args):
+        """A C-ABI call that runs this hierarchy's cycles: a GMRES coarse solve that did not
+        converge ends it with EINVAL ("did not converge") -> CoarseSolveError (the reference's
+        factorisation failure, ns/lib/multigrid.py:167-170)."""
+        try:
+            return call(fn, *args)
+        except MlamgError as e:
+            if self.coarse_gmres and "did not converge" in str(e):
+                raise CoarseSolveError(str(e)) from None
+            raise
+
     def cycle(self, b, x, n_cycles, tol=None, use_graph=True, history=True):
         """Run up to n_cycles V-cycles in place on x (device tensors). Returns the residual
         history ||b - A x||_2 after each cycle (numpy, truncated at convergence). tol=None runs
@@ -849,10 +967,10 @@ class Hierarchy:
         dev = x.device
         hist = torch.zeros(max(n_cycles, 1), dtype=torch.float64, device=dev) if history else None
         done = ctypes.c_int32()
-        call("mlamg_hier_vcycle", self.handle, ptr(rhs_arg(b)), ptr(x), int(n_cycles),
-             _tol_arg(tol), ptr(hist), ctypes.byref(done), int(bool(use_graph)), stream_ptr())
-        if self.pcg is not None:
-            self.check_coarse()
+        self._solve_call("mlamg_hier_vcycle", self.handle, ptr(rhs_arg(b)), ptr(x),
+                         int(n_cycles), _tol_arg(tol), ptr(hist), ctypes.byref(done),
+                         int(bool(use_graph)), stream_ptr())
+        self.check_coarse()
         if not history:
             return None
         return hist[: int(done.value)].cpu().numpy()
@@ -867,8 +985,8 @@ class Hierarchy:
             bb = None if zero_rhs else b
             if zero_rhs and b is not None and bool(torch.count_nonzero(b.view(torch.int64))):
                 raise ValueError("zero_rhs=True with a nonzero b")
-        call("mlamg_hier_vcycle", self.handle, ptr(bb), ptr(x), int(n_cycles), _tol_arg(None),
-             None, None, int(bool(use_graph)), stream_ptr())
+        self._solve_call("mlamg_hier_vcycle", self.handle, ptr(bb), ptr(x), int(n_cycles),
+                         _tol_arg(None), None, None, int(bool(use_graph)), stream_ptr())
 
     def solve(self, b, x0=None, tol=1e-8, maxiter=500, return_history=False):
         """Stationary V-cycle iteration until ||b - A x||_2 <= tol (absolute, MLAMG.py:194);
@@ -893,11 +1011,10 @@ class Hierarchy:
         cap = 4096
         hist = (ctypes.c_double * cap)()
         info, inner = ctypes.c_int(), ctypes.c_int()
-        call("mlamg_gmres", A.handle, self.handle, ptr(bd), ptr(xd), float(rtol), int(restart),
-             int(maxiter or 0), int(x0 is None), ctypes.byref(info), ctypes.byref(inner), hist,
-             cap, stream_ptr())
-        if self.pcg is not None:
-            self.check_coarse()  # a broken-down coarse solve inside the preconditioner
+        self._solve_call("mlamg_gmres", A.handle, self.handle, ptr(bd), ptr(xd), float(rtol),
+                         int(restart), int(maxiter or 0), int(x0 is None), ctypes.byref(info),
+                         ctypes.byref(inner), hist, cap, stream_ptr())
+        self.check_coarse()  # a broken-down coarse solve inside the preconditioner
         x = xd if isinstance(b, torch.Tensor) else xd.cpu().numpy()
         if not return_info:
             return x
@@ -918,19 +1035,17 @@ class Hierarchy:
         cap = 4096
         hist = (ctypes.c_double * cap)()
         info, iters = ctypes.c_int(), ctypes.c_int()
-        call("mlamg_gmres_householder", A.handle, self.handle, ptr(bd), ptr(xd), float(tol),
-             int(maxiter or 0), int(x0 is None), ctypes.byref(info), ctypes.byref(iters), hist,
-             cap, stream_ptr())
-        if self.pcg is not None:
-            self.check_coarse()
+        self._solve_call("mlamg_gmres_householder", A.handle, self.handle, ptr(bd), ptr(xd),
+                         float(tol), int(maxiter or 0), int(x0 is None), ctypes.byref(info),
+                         ctypes.byref(iters), hist, cap, stream_ptr())
+        self.check_coarse()
         x = xd if isinstance(b, torch.Tensor) else xd.cpu().numpy()
         if not return_info:
             return x
-        # recorded: the initial norm, one per step but the budget's last, the final norm
-        n = bd.numel()
-        max_inner = min(int(maxiter) if maxiter else min(n, 40), n)
+        # recorded: the initial norm, one per step except the last (the budget's last step, or
+        # the step whose estimate met tol: pyamg breaks before appending it), the final norm
         it = iters.value
-        k = min(1 if it == 0 else it + (1 if it == max_inner else 2), cap)
+        k = min(1 if it == 0 else it + 1, cap)
         return x, {"info": info.value, "iters": it, "residuals": np.array(hist[:k])}
 
     def precondition(self, b):
@@ -965,7 +1080,8 @@ class Hierarchy:
                          "lanczos_iters": L.lanczos_iters, "bf_sweeps": L.bf_sweeps})
         rows.append({"level": len(self.levels), "n": self.Ac.shape[0], "nnz": self.Ac.nnz,
                      "coarse": "dense inverse" if self.dense is not None
-                     else "PCG, inner SA hierarchy"})
+                     else ("GMRES, inner SA hierarchy" if self.coarse_gmres
+                           else "PCG, inner SA hierarchy")})
         return rows
 
     def __del__(self):

@@ -453,18 +453,23 @@ def amg_2_v(A, P, b, x,
         pass
     # The PCG coarse solve broke down: A_H is not positive definite. SuperLU (the reference's
     # factorisation) solves any nonsingular A_H, so the coarse operator is inverted densely
-    # instead (Gauss-Jordan with partial pivoting when it is not SPD) and the solve rerun; the
-    # reference's failure return when that factorisation fails too, or when A_H is beyond the
-    # dense solver's size (the run("dense") CoarseSolveError must not escape — a
-    # dataset loop over amg_2_v expects the (x, 1.0, zeros, 0) tuple, not an exception)
+    # instead (Gauss-Jordan with partial pivoting when it is not SPD) and the solve rerun, or,
+    # beyond the dense solver's size, solved by GMRES with an inner hierarchy (to 1e-14
+    # relative). The reference's failure return when the factorisation fails or GMRES does not
+    # converge (no CoarseSolveError escapes — a dataset loop over amg_2_v expects the
+    # (x, 1.0, zeros, 0) tuple, not an exception)
     try:
         return run("dense")
     except CoarseSolveError:
-        return failed
+        pass
     except _lib.MlamgError as e:
         if e.code == _lib.MLAMG_EINVAL and "singular" in str(e):
             return failed
         raise
+    try:
+        return run("gmres")
+    except CoarseSolveError:
+        return failed
 
 
 def amg_2_v_batch(problems, workers=8, **kw):

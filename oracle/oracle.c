@@ -7,6 +7,7 @@
  *
  *   ref_csr_matvec          scipy sparsetools csr_matvec (A@x at ns/lib/multigrid.py:181,191)
  *   ref_gauss_seidel        pyamg 4.x amg_core gauss_seidel, forward sweep (multigrid.py:175,184)
+ *   pyamg_gauss_seidel      the same in pyamg's three sweep directions (relaxation.gauss_seidel)
  *   ref_bellman_ford_torch  ns/lib/graph.py:28-53 modified_bellman_ford (fp32, sequential push
  *                           over coalesced COO order, strict <)
  *   canon_bellman_ford      same distances (order-independent fixed point) with the device's
@@ -79,6 +80,32 @@ void ref_gauss_seidel(int64_t n, const int32_t* ip, const int32_t* ij, const dou
       }
       if (diag != 0.0) x[i] = (b[i] - rsum) / diag;
     }
+  }
+}
+
+/* pyamg relaxation.gauss_seidel(A, x, b, iterations, sweep): amg_core gauss_seidel over rows
+ * [row_start, row_stop) with row_step, the forward arithmetic above (a zero or missing diagonal
+ * leaves x_i alone); sweep 0 forward, 1 backward (n-1 .. 0), 2 symmetric (forward then backward,
+ * per iteration). */
+static void gs_once(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax, double* x,
+                    const double* b, int backward) {
+  for (int64_t t = 0; t < n; ++t) {
+    const int64_t i = backward ? n - 1 - t : t;
+    double rsum = 0.0, diag = 0.0;
+    for (int32_t k = ip[i]; k < ip[i + 1]; ++k) {
+      const int32_t j = ij[k];
+      if (j == i) diag = ax[k];
+      else rsum += ax[k] * x[j];
+    }
+    if (diag != 0.0) x[i] = (b[i] - rsum) / diag;
+  }
+}
+
+void pyamg_gauss_seidel(int64_t n, const int32_t* ip, const int32_t* ij, const double* ax,
+                        double* x, const double* b, int iterations, int sweep) {
+  for (int it = 0; it < iterations; ++it) {
+    if (sweep == 0 || sweep == 2) gs_once(n, ip, ij, ax, x, b, 0);
+    if (sweep == 1 || sweep == 2) gs_once(n, ip, ij, ax, x, b, 1);
   }
 }
 

@@ -47,6 +47,7 @@ def lib():
         L.pyamg_standard_aggregation.restype = i64
         L.pyamg_block_gauss_seidel.argtypes = [i64, vp, vp, vp, vp, vp, ctypes.c_int,
                                                ctypes.c_int]
+        L.pyamg_gauss_seidel.argtypes = [i64, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
         L.pyamg_fit_candidates.argtypes = [i64, vp, i64, vp, ctypes.c_double, vp, vp]
         _LIB = L
     return _LIB
@@ -97,6 +98,19 @@ def gauss_seidel(A, x, b, iterations=1):
     assert x.dtype == np.float64 and x.flags.c_contiguous
     b = np.ascontiguousarray(b, dtype=np.float64)
     lib().ref_gauss_seidel(A.shape[0], _p(ip), _p(ij), _p(ax), _p(x), _p(b), int(iterations))
+    return x
+
+
+def pyamg_gauss_seidel(A, x, b, iterations=1, sweep="forward"):
+    """pyamg.relaxation.relaxation.gauss_seidel(A, x, b, iterations, sweep) in place: the
+    forward arithmetic of gauss_seidel above, rows n-1..0 for 'backward', forward then backward
+    per iteration for 'symmetric' (amg_core gauss_seidel with row_step -1). Parity unpinned
+    (pyamg absent)."""
+    ip, ij, ax = _csr_arrays(A)
+    assert x.dtype == np.float64 and x.flags.c_contiguous
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    lib().pyamg_gauss_seidel(A.shape[0], _p(ip), _p(ij), _p(ax), _p(x), _p(b), int(iterations),
+                             _SWEEPS[sweep])
     return x
 
 
@@ -939,9 +953,9 @@ def pyamg_gmres_householder(A, b, M, x0=None, tol=1e-5, maxiter=None):
         niter += 1
         if inner < max_inner - 1:
             normr = abs(g[inner + 1])
-            res.append(normr)
-            if normr < tol:
+            if normr < tol:  # pyamg _gmres_householder: break, then callback / residuals
                 break
+            res.append(normr)
     y = np.linalg.solve(np.triu(H[:inner + 1, :inner + 1]), g[:inner + 1])
     update = np.zeros(n)
     for j in range(inner, -1, -1):

@@ -65,17 +65,32 @@ def _matrix(name):
     raise KeyError(name)
 
 
-@pytest.mark.parametrize("name", ("c2_1024", "c3", "c3_r2", "c5_grid", "c5_mesh", "lap3d_grid",
-                                  "aniso3d_48", "varcoef3d_64"))
-def test_config_hierarchy_and_cycle_parity(ml, oracle, torch_cuda, name):
+CONFIGS = ("c2_1024", "c3", "c3_r2", "c5_grid", "c5_mesh", "lap3d_grid", "aniso3d_48",
+           "varcoef3d_64")
+# (aggregation, coarse_order): the builder's canonical rule, and the mode tools/bench_configs.py
+# times (profiles/*/configs.json): the reference's "dumb" recipe on level 0
+# (utils/evaluate_dataset.py:80-90) with the coarse unknowns in ascending seed order.
+MODES = (("bellman_ford", "seed"), ("reference", "sorted"))
+
+
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: m[0])
+@pytest.mark.parametrize("name", CONFIGS)
+def test_config_hierarchy_and_cycle_parity(ml, oracle, torch_cuda, name, mode):
     torch = torch_cuda
+    aggregation, coarse_order = mode
+    if aggregation == "reference" and name == "c2_1024":
+        pytest.skip("C2 in reference mode: test_c2_reference_aggregation_parity (both orders)")
     A = _matrix(name)
     n = A.shape[0]
     max_coarse = 500 if n < 100000 else 2000
-    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=max_coarse)
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=max_coarse,
+                                     aggregation=aggregation, coarse_order=coarse_order)
     assert H.n_levels >= 2
+    if aggregation == "reference":
+        _assert_reference_level0(oracle, H, A, coarse_order)
     levels, Ac = oracle.build_hierarchy(A, alpha=0.1, max_coarse=max_coarse,
-                                        omegas=[L.omega for L in H.levels])
+                                        omegas=[L.omega for L in H.levels],
+                                        aggregation=aggregation, coarse_order=coarse_order)
     assert len(levels) == len(H.levels)
     for Lo, Ld in zip(levels, H.levels):
         assert np.array_equal(Ld.seeds, Lo["seeds"])
@@ -110,6 +125,25 @@ def test_config_hierarchy_and_cycle_parity(ml, oracle, torch_cuda, name):
     assert np.allclose(hd, ho, rtol=1e-11, atol=0), (hd, ho)
     assert np.allclose(xd.cpu().numpy(), xo, rtol=1e-9, atol=1e-11 * np.abs(xo).max())
     assert hd[-1] < hd[0]
+
+
+def _assert_reference_level0(oracle, H, A, coarse_order):
+    """Level 0 of aggregation='reference' is bitwise the reference's "dumb" recipe
+    (utils/evaluate_dataset.py:80-90; ns/lib/graph.py:7-86) as oracle.reference_aggregates
+    restates it on the invabs strength graph (utils/common.py:29): nearest-center labels,
+    seeds (relabelled ascending when coarse_order='sorted') and the aggregate operator."""
+    n = A.shape[0]
+    C = oracle.STRENGTH["invabs"](oracle.canonical(A))
+    seeds, near, Agg = oracle.reference_aggregates(C, n, 0.1, 0)
+    assert np.array_equal(H.levels[0].labels.cpu().numpy().astype(np.int64), near)
+    if coarse_order == "sorted":
+        order = np.argsort(seeds)
+        seeds, Agg = seeds[order], Agg[:, order].tocsr()
+        Agg.sort_indices()
+    assert np.array_equal(H.levels[0].seeds, seeds)
+    Aggd = H.levels[0].Agg.to_scipy()
+    for arr in ("indptr", "indices", "data"):
+        assert np.array_equal(getattr(Aggd, arr), getattr(Agg, arr)), arr
 
 
 def test_varcoef_refuses_stencil_encodings(ml, torch_cuda):

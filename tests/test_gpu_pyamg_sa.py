@@ -182,8 +182,8 @@ def test_gauss_seidel_directions_bitwise(ml, oracle, torch_cuda, sweep, block):
             oracle.pyamg_block_gauss_seidel(A, xo, b, 3, sweep)
         elif sweep == "forward":
             oracle.gauss_seidel(A, xo, b, 3)
-        else:
-            continue  # gauss_seidel arithmetic in other directions: covered by the block oracle
+        else:  # gauss_seidel arithmetic backward / symmetric (zero diagonals: x_i kept)
+            oracle.pyamg_gauss_seidel(A, xo, b, 3, sweep)
         assert np.array_equal(xd.cpu().numpy().view(np.int64), xo.view(np.int64)), (name, sweep)
 
 
@@ -362,6 +362,14 @@ def test_pyamg_sa_edge_cases(ml, torch_cuda):
     for lv in (1, 2):
         s2 = aggregation.smoothed_aggregation_solver(ml.problems.poisson_2d_5pt(12), max_levels=lv)
         assert s2.H.n_levels == lv
+    # no off-diagonal couplings (n > max_coarse): pyamg's n x 1 empty AggOp, a zero coarse
+    # correction; the symmetric sweep alone solves the diagonal system
+    d = np.linspace(1.0, 3.0, 50)
+    sd = aggregation.smoothed_aggregation_solver(sp.diags(d).tocsr())
+    assert sd.H.n_levels == 2 and sd.H.Ac.shape == (1, 1)
+    assert sd.H.levels[0].P.shape == (50, 1) and sd.H.levels[0].P.nnz == 0
+    bd = np.arange(1.0, 51.0)
+    np.testing.assert_allclose(sd.solve(bd, tol=1e-12), bd / d, rtol=1e-15)
     P = ml.problems.poisson_2d_5pt(40)
     s3 = aggregation.smoothed_aggregation_solver(P)
     b3 = np.ones(P.shape[0])
@@ -424,6 +432,8 @@ def test_gmres_householder_edge_cases(ml, oracle, torch_cuda):
     b1 = np.arange(1.0, 9.0)
     x1, info1 = H1.gmres_householder(b1, tol=1e-10, maxiter=100, return_info=True)
     assert info1["iters"] == 1 and info1["info"] == 0
+    # pyamg breaks before recording the converged step's estimate: initial and final norms only
+    assert len(info1["residuals"]) == 2
     np.testing.assert_allclose(A1 @ x1, b1, atol=1e-12 * 8)
     Minv = np.linalg.pinv(A1.toarray())
     xo, info_o, it_o, _ = oracle.pyamg_gmres_householder(A1, b1, lambda r: Minv @ r, tol=1e-10,
