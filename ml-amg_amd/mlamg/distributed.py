@@ -152,7 +152,7 @@ class DistributedHierarchy:
     coarse cycle. The iterate is bitwise the single-GPU Hierarchy.cycle iterate."""
 
     def __init__(self, H, comm, min_rows=50000, max_partitioned=None, A_host=None,
-                 local_autotune=True, overlap_min_rows=2_000_000):
+                 local_autotune=True, overlap_min_rows=2_000_000, partition_impl="torch"):
         """H: mlamg.hierarchy.Hierarchy built identically on every rank (sorted seeds, same
         kernel formats — see sync_formats). Levels with at least `min_rows` rows (at most
         `max_partitioned` of them) are row-partitioned; the rest are replicated.
@@ -164,7 +164,13 @@ class DistributedHierarchy:
         costs two more launches and a stream fork/join per exchange (measured with the null
         communicator at world 8, C4: +7 us per split operator), so it pays only where the
         interior rows take longer than that: the default splits local operators of >= 2 M rows
-        (C4 level 0 at world <= 4)."""
+        (C4 level 0 at world <= 4).
+        partition_impl: 'torch' (default) builds the partition maps with torch ops on the
+        operators' own device arrays (partition.build_levels_torch; the local operators never
+        leave the GPU); 'numpy' downloads every partitioned operator and runs the host build
+        (partition.build_levels, the reference implementation of the maps; A_host, if given,
+        replaces the download of level 0). Both give the same maps. Phase wall times are kept
+        in self.setup_times."""
         if not H.levels:
             raise ValueError("distributed cycle needs at least one level above the coarse solve")
         if (H.nu_pre, H.nu_post) != (1, 1):
@@ -185,20 +191,45 @@ class DistributedHierarchy:
             raise ValueError("the distributed cycle needs each partitioned level's coarse "
                              "unknowns in ascending seed order (Hierarchy.build with sorted "
                              "seeds; aggregation='reference' with coarse_order='sorted')")
-        As = [A_host if (l == 0 and A_host is not None) else H.levels[l].A.to_scipy()
-              for l in range(K)]
-        Ps = [H.levels[l].P.to_scipy() for l in range(K)]
-        self.parts = parts = partition.build_levels(As, Ps, [H.levels[l].seeds for l in range(K)],
-                                                    world, rank)
-        del As, Ps
+        self.setup_times = st = {}
+        t0 = time.perf_counter()
+        seeds = [H.levels[l].seeds for l in range(K)]
+        if partition_impl == "torch":
+            def tc(M):
+                crow, col, val = M.to_torch()
+                return partition.TCSR(crow, col, val, M.shape)
+            As = [tc(H.levels[l].A) for l in range(K)]
+            Ps = [tc(H.levels[l].P) for l in range(K)]
+            Rs = [tc(H.levels[l].R) for l in range(K)]
+            torch.cuda.synchronize()
+            st["download"] = time.perf_counter() - t0
+            self.parts = parts = partition.build_levels_torch(As, Ps, Rs, seeds, world, rank)
+            del As, Ps, Rs
+        elif partition_impl == "numpy":
+            As = [A_host if (l == 0 and A_host is not None) else H.levels[l].A.to_scipy()
+                  for l in range(K)]
+            Ps = [H.levels[l].P.to_scipy() for l in range(K)]
+            st["download"] = time.perf_counter() - t0
+            self.parts = parts = partition.build_levels(As, Ps, seeds, world, rank)
+            del As, Ps
+        else:
+            raise ValueError(f"unknown partition_impl {partition_impl!r}")
+        torch.cuda.synchronize()
+        st["partition"] = time.perf_counter() - t0 - st["download"]
+        t_ops = [0.0, 0.0]  # upload, local autotune
         p0 = parts[0]
         self.lo, self.hi = p0["lo"], p0["hi"]
         self.n_own = self.hi - self.lo
 
         self.tuning = []
 
-        def like(M_glob, M_loc, kind):
+        def like(M_glob, M_part, kind):
+            t1 = time.perf_counter()
+            M_loc = _device_csr(M_part)
+            t2 = time.perf_counter()
             M, t = tune_local(M_glob, M_loc, kind, autotune=local_autotune)
+            t_ops[0] += t2 - t1
+            t_ops[1] += time.perf_counter() - t2
             self.tuning.append(t)
             return M
 
@@ -223,9 +254,9 @@ class DistributedHierarchy:
         self.splits = []
         for l, p in enumerate(parts):
             Lg = H.levels[l]
-            A_loc = like(Lg.A, DeviceCSR.from_scipy(p["A_loc"], check=False), "A")
-            P_loc = like(Lg.P, DeviceCSR.from_scipy(p["P_loc"], check=False), "P")
-            R_own = like(Lg.R, DeviceCSR.from_scipy(p["R_own"], check=False), "R")
+            A_loc = like(Lg.A, p["A_loc"], "A")
+            P_loc = like(Lg.P, p["P_loc"], "P")
+            R_own = like(Lg.R, p["R_own"], "R")
             dinv = Lg.dinv[p["lo"]:p["hi"]].clone()
             if A_loc.get_format()[0] == "rowpat":
                 A_loc.attach_dinv(dinv)
@@ -248,9 +279,17 @@ class DistributedHierarchy:
                 self.A_loc = A_loc
                 self.hx = hx
         self.n_ext = self.n_own + self.hx.n_ghost
+        torch.cuda.synchronize()
+        st["upload"], st["local_autotune"] = t_ops
+        st["total"] = time.perf_counter() - t0
+        for p in parts:  # the maps' own copies of the local operators are not needed again
+            p["A_loc"] = p["R_own"] = p["P_loc"] = None
 
     def _split(self, l, which, M_glob, M_host, n_owned, dinv, like):
-        cut = partition.interior_split(M_host, n_owned)
+        if isinstance(M_host, partition.TCSR):
+            cut = partition.interior_split_torch(M_host, n_owned)
+        else:
+            cut = partition.interior_split(M_host, n_owned)
         if cut is None:
             return
         lo, hi = cut
@@ -259,7 +298,8 @@ class DistributedHierarchy:
             if b == a:
                 parts.append(None)
                 continue
-            M = like(M_glob, DeviceCSR.from_scipy(M_host[a:b], check=False), "APR"[which])
+            Mp = M_host.rows(a, b) if isinstance(M_host, partition.TCSR) else M_host[a:b]
+            M = like(M_glob, Mp, "APR"[which])
             self.tuning.pop()  # keep D.tuning = the whole operators' choices, 3 per level
             if dinv is not None and M.get_format()[0] == "rowpat":
                 # a view: the epilogues are handed dinv + a, the very pointer attached
@@ -309,6 +349,28 @@ class DistributedHierarchy:
                 except Exception:
                     pass
                 setattr(self, attr, None)
+
+
+def rank_memory():
+    """This rank's memory: device bytes in use (hipMemGetInfo: everything the process holds on
+    its GPU, the library's own allocations included), torch's peak allocation, and the host
+    process's peak resident set."""
+    import resource
+    free, total = torch.cuda.mem_get_info()
+    return {"device_used_GB": round((total - free) / 1e9, 3),
+            "torch_peak_GB": round(torch.cuda.max_memory_allocated() / 1e9, 3),
+            "host_peak_rss_GB": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, 3)}
+
+
+def _device_csr(M):
+    """A partition map's local operator (scipy CSR or partition.TCSR) as a DeviceCSR."""
+    if isinstance(M, partition.TCSR):
+        if M.col.is_cuda:
+            return DeviceCSR.from_torch(M.crow.to(torch.int32).contiguous(),
+                                        M.col.to(torch.int32).contiguous(),
+                                        M.val.contiguous(), M.shape)
+        M = M.to_scipy()
+    return DeviceCSR.from_scipy(M, check=False)
 
 
 def tune_local(M_glob, M_loc, kind, autotune=True):
@@ -583,6 +645,7 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak, phases=None):
     D = DistributedHierarchy(H, comm, min_rows=args.dist_min_rows, A_host=A,
                              overlap_min_rows=None if omr < 0 else omr)
     part_s = time.perf_counter() - t1
+    log("partition phases (s): " + json.dumps({k: round(v, 3) for k, v in D.setup_times.items()}))
     log(f"setup {setup_s:.1f}s (replicated), partition+upload {part_s:.1f}s; {D.K} of "
         f"{len(H.levels)} levels partitioned; rank rows {D.lo}..{D.hi}; ghosts (x, r, p) per "
         f"level {D.ghosts}; communicator {cinfo}")
@@ -649,7 +712,9 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak, phases=None):
             "median_us": round(t_med * 1e6, 2), "stream_event_us": round(t_ev * 1e6, 2),
             "warm_us": round(t_warm * 1e6, 2),
             "GBps": round(B / t_spmv / 1e9, 1), "frac": round(B / t_spmv / 1e9 / hbm_peak, 4),
-            "warm_frac": round(B / t_warm / 1e9 / hbm_peak, 4)}
+            "warm_frac": round(B / t_warm / 1e9 / hbm_peak, 4),
+            "partition_s": {k: round(v, 3) for k, v in D.setup_times.items()},
+            "memory": rank_memory()}
     ph.enter("gather")
     per_rank = [None] * world
     if world > 1:
@@ -706,7 +771,9 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak, phases=None):
                 "warm_avg_launch_us": slow["warm_us"],
             },
             "per_rank_spmv": per_rank,
-            "setup_s": {"replicated_build": round(setup_s, 3), "partition": round(part_s, 3)},
+            "setup_s": {"replicated_build": round(setup_s, 3), "partition": round(part_s, 3),
+                        "partition_phases_rank0": {k: round(v, 3)
+                                                   for k, v in D.setup_times.items()}},
         }
     ph.enter("report")
 

@@ -416,6 +416,18 @@ def amg_2_v(A, P, b, x,
         raise ValueError(f"unknown smoother {smoother!r}")
     if engine not in ("auto", "fused", "hierarchy"):
         raise ValueError(f"unknown engine {engine!r}")
+    from . import broker
+    if broker.enabled() and engine == "auto":
+        # MLAMG_BROKER=1: the call goes to this GPU's broker process, which coalesces the calls
+        # of concurrent worker processes into fused batch launches (mlamg/broker.py)
+        def num(v):
+            return None if v is None else float(v)
+        return broker.solve(A, P, b, x, {
+            "pre_smoothing_steps": int(pre_smoothing_steps),
+            "post_smoothing_steps": int(post_smoothing_steps),
+            "jacobi_weight": float(jacobi_weight), "res_tol": num(res_tol),
+            "error_tol": num(error_tol), "max_iter": int(max_iter), "singular": bool(singular),
+            "smoother": smoother})
     prep = None
     if engine != "hierarchy" and not singular:
         prep = _fused_arrays(A, P, b, x, None if engine == "fused" else FUSED_SINGLE_MAX_NC)

@@ -234,3 +234,192 @@ def interior_split(M, n_owned_cols, min_frac=0.5):
     if hi - lo < max(2, min_frac * n):
         return None
     return lo, hi
+
+
+# ---------------------------------------------------------------- vectorised (torch) build
+# The same partition maps computed with torch tensor ops on the operators' own device arrays
+# (VERDICT r05 Weak #6: the numpy build above took 5.1 s per rank at C4 — np.unique over every
+# rank's 70 M column indices — and needed host copies of every partitioned operator). Every
+# rank's ghost sets come from ONE pass over each operator: the entries whose column lies in
+# another rank's range, keyed (owner of the row, column) and made unique; the rank then cuts
+# only its own rows. Bitwise the same maps as build_levels (tests/test_partition_torch.py).
+
+class TCSR:
+    """A CSR matrix as three torch tensors (crow int64 or int32, col int32, val float64)."""
+
+    __slots__ = ("crow", "col", "val", "shape")
+
+    def __init__(self, crow, col, val, shape):
+        self.crow, self.col, self.val, self.shape = crow, col, val, (int(shape[0]), int(shape[1]))
+
+    @property
+    def nnz(self):
+        return int(self.col.numel())
+
+    def rows(self, a, b):
+        """Rows [a, b) (a view of col / val)."""
+        s, e = int(self.crow[a]), int(self.crow[b])
+        return TCSR(self.crow[a:b + 1] - s, self.col[s:e], self.val[s:e], (b - a, self.shape[1]))
+
+    def to_scipy(self):
+        return sp.csr_matrix((self.val.cpu().numpy(), self.col.cpu().numpy(),
+                              self.crow.cpu().numpy()), shape=self.shape)
+
+    @classmethod
+    def from_scipy(cls, M, device="cpu"):
+        import torch
+        M = M.tocsr()
+        return cls(torch.as_tensor(M.indptr.astype(np.int64), device=device),
+                   torch.as_tensor(M.indices.astype(np.int32), device=device),
+                   torch.as_tensor(M.data.astype(np.float64), device=device), M.shape)
+
+
+def _t_owner(idx, his_t):
+    import torch
+    return torch.searchsorted(his_t, idx, right=True)
+
+
+def _t_entry_owner(crow, bounds):
+    """Owner rank of every entry of a CSR whose rows are split at `bounds` (lo of each rank +
+    the end): entries are contiguous per rank."""
+    import torch
+    cuts = crow[torch.as_tensor(bounds, dtype=torch.int64, device=crow.device)].to(torch.int64)
+    counts = cuts[1:] - cuts[:-1]
+    return torch.repeat_interleave(torch.arange(len(bounds) - 1, device=crow.device), counts)
+
+
+def _t_split_keys(keys, n, world):
+    """Unique (rank, index) keys rank * n + index -> per-rank ascending index arrays."""
+    import torch
+    keys = torch.unique(keys)
+    q = torch.div(keys, n, rounding_mode="floor")
+    idx = keys - q * n
+    counts = torch.bincount(q, minlength=world).cpu().numpy()
+    parts = torch.split(idx, counts.tolist())
+    return [p for p in parts]
+
+
+def _t_cross_keys(M, row_bounds, col_his, n_cols):
+    """keys (owner of the entry's row) * n_cols + column for entries whose column another rank
+    owns."""
+    import torch
+    ro = _t_entry_owner(M.crow, row_bounds)
+    col = M.col.to(torch.int64)
+    co = _t_owner(col, col_his)
+    cross = co != ro
+    return ro[cross] * n_cols + col[cross]
+
+
+def _t_gather_rows(M, rows):
+    """The rows `rows` (int64 tensor, any order) of M, in that order."""
+    import torch
+    crow = M.crow.to(torch.int64)
+    starts = crow[rows]
+    lens = crow[rows + 1] - starts
+    new_crow = torch.zeros(len(rows) + 1, dtype=torch.int64, device=crow.device)
+    new_crow[1:] = torch.cumsum(lens, 0)
+    total = int(new_crow[-1])
+    pos = torch.arange(total, device=crow.device) - torch.repeat_interleave(new_crow[:-1], lens)
+    src = torch.repeat_interleave(starts, lens) + pos
+    return TCSR(new_crow, M.col[src], M.val[src], (len(rows), M.shape[1])), src, lens
+
+
+def _t_remap(M, lo, hi, ghosts):
+    """_remap on a TCSR: owned j -> j - lo, ghost g -> n_own + position(g); stored order kept."""
+    import torch
+    n_own = hi - lo
+    col = M.col.to(torch.int64)
+    own = (col >= lo) & (col < hi)
+    out = torch.where(own, col - lo, n_own + torch.searchsorted(ghosts, col))
+    return TCSR(M.crow, out.to(torch.int32), M.val, (M.shape[0], n_own + len(ghosts)))
+
+
+def _t_halos(ghosts_all, ranges, r):
+    """_halos from per-rank ghost tensors (moved to the host: they are small)."""
+    g = [t.cpu().numpy().astype(np.int64) for t in ghosts_all]
+    return _halos(g, ranges, r)
+
+
+def build_levels_torch(As, Ps, Rs, seeds_list, world, rank):
+    """build_levels for `rank` from TCSR operators (any torch device): As[l] n x n, Ps[l] n x nc,
+    Rs[l] = P_l^T with ascending columns in every row (the device transpose's order, scipy's
+    P.T.tocsr()). Returns the same per-level dicts, with TCSR matrices for A_loc / R_own / P_loc
+    (on the operators' device)."""
+    import torch
+    K = len(As)
+    ranges = row_ranges(As[0].shape[0], world)
+    out = []
+    for l in range(K):
+        A, P, R = As[l], Ps[l], Rs[l]
+        dev = A.col.device
+        n, nc = A.shape[0], P.shape[1]
+        c_ranges = _seed_ranges(seeds_list[l], ranges, nc)
+        rb = [lo for lo, _ in ranges] + [n]
+        cb = [lo for lo, _ in c_ranges] + [nc]
+        his = torch.as_tensor([h for _, h in ranges], dtype=torch.int64, device=dev)
+        chis = torch.as_tensor([h for _, h in c_ranges], dtype=torch.int64, device=dev)
+        # x ghosts: columns of A outside the row owner's range; r ghosts: fine columns of R
+        # (rows split by coarse ranges) outside the fine range of the row's owner
+        xg = _t_split_keys(_t_cross_keys(A, rb, his, n), n, world)
+        rg = _t_split_keys(_t_cross_keys(R, cb, his, n), n, world)
+        # P rows of rank q: its owned rows, then its x-ghost rows; P ghosts = coarse columns of
+        # those rows outside q's coarse range
+        last = l == K - 1
+        pg = None
+        if not last:
+            keys = [_t_cross_keys(P, rb, chis, nc)]
+            for q in range(world):
+                if len(xg[q]):
+                    Pq, _, _ = _t_gather_rows(P, xg[q])
+                    c = Pq.col.to(torch.int64)
+                    keys.append(q * nc + c[(c < c_ranges[q][0]) | (c >= c_ranges[q][1])])
+            pg = _t_split_keys(torch.cat(keys), nc, world)
+        lo, hi = ranges[rank]
+        clo, chi = c_ranges[rank]
+        d = {
+            "level": l, "rank": rank, "world": world, "lo": lo, "hi": hi, "n": n, "nc": nc,
+            "c_lo": clo, "c_hi": chi, "c_ranges": c_ranges, "ranges": ranges,
+            "A_loc": _t_remap(A.rows(lo, hi), lo, hi, xg[rank]),
+            "R_own": _t_remap(R.rows(clo, chi), lo, hi, rg[rank]),
+            "halo_x": _t_halos(xg, ranges, rank),
+            "halo_r": _t_halos(rg, ranges, rank),
+        }
+        prow = torch.cat([torch.arange(lo, hi, device=dev, dtype=torch.int64), xg[rank]])
+        P_ext, _, _ = _t_gather_rows(P, prow)
+        if last:
+            d["P_loc"] = P_ext
+            d["halo_p"] = None
+        else:
+            d["P_loc"] = _t_remap(P_ext, clo, chi, pg[rank])
+            d["halo_p"] = _t_halos(pg, c_ranges, rank)
+        out.append(d)
+        ranges = c_ranges
+    return out
+
+
+def interior_split_torch(M, n_owned_cols, min_frac=0.5):
+    """interior_split on a TCSR (the per-row ghost test on M's device, the run search on the
+    host)."""
+    import torch
+    n = M.shape[0]
+    if n == 0:
+        return None
+    lens = (M.crow[1:] - M.crow[:-1]).to(torch.int64)
+    rows = torch.repeat_interleave(torch.arange(n, device=M.col.device), lens)
+    ghost = torch.zeros(n, dtype=torch.bool, device=M.col.device)
+    ghost[rows[M.col.to(torch.int64) >= n_owned_cols]] = True
+    ghost = ghost.cpu().numpy()
+    if not ghost.any():
+        return None
+    interior = ~ghost
+    edges = np.flatnonzero(np.diff(np.concatenate(([0], interior.astype(np.int8), [0]))))
+    starts, ends = edges[0::2], edges[1::2]
+    if len(starts) == 0:
+        return None
+    k = int(np.argmax(ends - starts))
+    lo, hi = int(starts[k]), int(ends[k])
+    lo += lo & 1
+    hi -= hi & 1
+    if hi - lo < max(2, min_frac * n):
+        return None
+    return lo, hi

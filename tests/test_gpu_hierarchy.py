@@ -977,3 +977,50 @@ def test_factored_prolongation_within_tolerance(ml, oracle, torch_cuda, dim, n1)
     from mlamg._lib import MlamgError
     with pytest.raises(MlamgError):
         Hv.set_factored_prolong(0)
+
+
+@pytest.mark.parametrize("case,fmt", [("p3d", ("rowpat", 0)), ("p3d", ("sorted", 0)),
+                                      ("p3d", ("sell", 1)), ("p3d", ("sell_dict", 1)),
+                                      ("p3d", ("csr_stream", 0)), ("p2d_1536", ("csr_stream", 0)),
+                                      ("varcoef", ("sell", 512)), ("varcoef", ("sorted", 2))])
+def test_end_of_cycle_norm_in_pass_same_bits(ml, torch_cuda, case, fmt):
+    """The end-of-cycle norm finished inside the norm pass by its last-arriving workgroup
+    (csrc/spmv.hip norm_fin: sc1 partials, one arrival counter, no k_finalize_norm launch) has
+    k_finalize_norm's bits: after one fused cycle x holds t and hist[0] = ||b - A t||, and
+    mlamg_residual (partials + the separate finalize launch) on that x gives the same double.
+    Fine-level formats with one partial per workgroup, up to 9,216 partials (the finalize's
+    unrolled strided loop); then a tolerance stop on the same cycle count as the separate
+    finalize's cycle."""
+    torch = torch_cuda
+    from mlamg._lib import call, ptr, stream_ptr
+    if case == "p3d":
+        A = ml.problems.poisson_3d_7pt(40)
+    elif case == "p2d_1536":
+        A = ml.problems.poisson_2d_5pt(1536)
+    else:
+        A = ml.problems.random_coeff_3d_7pt(40, seed=1)
+    n = A.shape[0]
+    H = ml.hierarchy.Hierarchy.build(A, alpha=0.1, max_coarse=2000)
+    try:
+        H.levels[0].A.set_format(*fmt)
+    except ml._lib.MlamgError as e:
+        if e.code == ml._lib.MLAMG_EUNSUPPORTED:
+            pytest.skip(f"{fmt} does not apply to {case}")
+        raise
+    H.attach_dinvs()
+    rng = np.random.RandomState(3)
+    b = dev(torch, rng.randn(n))
+    x = dev(torch, rng.randn(n))
+    for k in range(3):
+        h = H.cycle(b, x, 1)
+        r = torch.empty_like(x)
+        nrm = torch.zeros(1, dtype=torch.float64, device="cuda")
+        call("mlamg_residual", H.levels[0].A.handle, ptr(b), ptr(x), ptr(r), ptr(nrm),
+             stream_ptr())
+        assert h[0] == float(nrm[0]), (k, h[0], float(nrm[0]))
+    x1 = dev(torch, rng.randn(n))
+    x2 = x1.clone()
+    h_all = H.cycle(b, x1, 12)
+    tol = float(h_all[6])  # met first by cycle 7
+    h_tol = H.cycle(b, x2, 12, tol=tol)
+    assert len(h_tol) == 7 and np.array_equal(h_tol, h_all[:7])

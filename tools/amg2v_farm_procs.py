@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "ml-amg_amd")]
 
 SIZES = (32, 48, 64, 96, 128)
+BROKER_DIR = os.path.join(ROOT, "gpurun_out", "broker")
 
 
 def make_problem(i):
@@ -35,33 +36,41 @@ def make_problem(i):
     return A, P, np.zeros(A.shape[0]), np.random.RandomState(i).randn(A.shape[0])
 
 
-def worker(rank, nprocs, ngrids, device):
+def worker(rank, nprocs, ngrids, device, kw):
     """One pool worker: its cyclic share of the grids, one amg_2_v call per grid."""
     mine = [make_problem(i) for i in range(rank, ngrids, nprocs)]
-    if device == "gpu":
+    if device == "broker":  # unchanged single calls, MLAMG_BROKER=1: this process never
+        from mlamg import multigrid  # touches the GPU, the shared broker runs the solves
+        solve = multigrid.amg_2_v
+        solve(*make_problem(rank), **kw)  # connects (the first worker starts it)
+    elif device == "gpu":
         import torch
         torch.cuda.set_device(0)
         from mlamg import multigrid
         solve = multigrid.amg_2_v
-        solve(*make_problem(rank), res_tol=1e-10)  # context, library, caches
+        solve(*make_problem(rank), **kw)  # context, library, caches
     else:
         from threadpoolctl import threadpool_limits
         threadpool_limits(1)
         from oracle import restated as orc
         solve = orc.amg_2_v
-        solve(*make_problem(rank), res_tol=1e-10)
+        solve(*make_problem(rank), **kw)
     print("READY", flush=True)
     sys.stdin.readline()
     t0 = time.perf_counter()
-    its = [int(solve(*p, res_tol=1e-10)[3]) for p in mine]
+    its = [int(solve(*p, **kw)[3]) for p in mine]
     dt = time.perf_counter() - t0
     print(json.dumps({"rank": rank, "s": dt, "iters": its}), flush=True)
 
 
-def run_farm(nprocs, ngrids, device):
+def run_farm(nprocs, ngrids, device, mode):
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    if device == "broker":
+        env["MLAMG_BROKER"] = "1"
+        env["MLAMG_BROKER_DIR"] = BROKER_DIR
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--worker", str(r),
-                               "--procs", str(nprocs), "--grids", str(ngrids), "--device", device],
+                               "--procs", str(nprocs), "--grids", str(ngrids), "--device", device,
+                              "--mode", mode],
                               stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
              for r in range(nprocs)]
     try:
@@ -89,16 +98,25 @@ def main():
     ap.add_argument("--procs", default="1,4,8,16")
     ap.add_argument("--grids", type=int, default=80)
     ap.add_argument("--device", default="both")
+    ap.add_argument("--mode", default="res", choices=("res", "err"),
+                    help="res: res_tol=1e-10 (utils/evaluate_dataset.py:96); err: error_tol=1e-6 "
+                         "(utils/train_dataset.py:114)")
     ap.add_argument("--worker", type=int, default=-1)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "amg2v_farm_procs.json"))
     args = ap.parse_args()
     if args.worker >= 0:
-        return worker(args.worker, int(args.procs), args.grids, args.device)
+        kw = {"res_tol": 1e-10} if args.mode == "res" else {"error_tol": 1e-6}
+        return worker(args.worker, int(args.procs), args.grids, args.device, kw)
     rows = []
+    devices = {"both": ("cpu", "gpu"), "all": ("cpu", "gpu", "broker")}.get(args.device,
+                                                                            (args.device,))
+    os.makedirs(BROKER_DIR, exist_ok=True)
     for pn in [int(p) for p in args.procs.split(",")]:
-        row = {"procs": pn, "grids": args.grids, "sizes": [f"{m}^2" for m in SIZES]}
-        for device in (("cpu", "gpu") if args.device == "both" else (args.device,)):
-            wall, outs = run_farm(pn, args.grids, device)
+        row = {"procs": pn, "grids": args.grids, "sizes": [f"{m}^2" for m in SIZES],
+               "call": "amg_2_v(..., res_tol=1e-10)" if args.mode == "res"
+               else "amg_2_v(..., error_tol=1e-6)"}
+        for device in devices:
+            wall, outs = run_farm(pn, args.grids, device, args.mode)
             row[f"{device}_wall_s"] = round(wall, 3)
             row[f"{device}_grids_per_s"] = round(args.grids / wall, 2)
             row[f"{device}_iters"] = [it for o in sorted(outs, key=lambda o: o["rank"])
@@ -106,10 +124,17 @@ def main():
         if "gpu_wall_s" in row and "cpu_wall_s" in row:
             row["gpu_over_cpu"] = round(row["cpu_wall_s"] / row["gpu_wall_s"], 2)
             row["iters_match"] = row["cpu_iters"] == row["gpu_iters"]
-        for d in ("cpu", "gpu"):
+        if "broker_wall_s" in row and "cpu_wall_s" in row:
+            row["broker_over_cpu"] = round(row["cpu_wall_s"] / row["broker_wall_s"], 2)
+            row["broker_iters_match"] = row["cpu_iters"] == row["broker_iters"]
+        for d in ("cpu", "gpu", "broker"):
             row.pop(f"{d}_iters", None)
         print(json.dumps(row), flush=True)
         rows.append(row)
+    if "broker" in devices:
+        os.environ["MLAMG_BROKER_DIR"] = BROKER_DIR
+        from mlamg import broker
+        broker.shutdown()  # the parent never touched the GPU; this is a socket message
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as fh:
         json.dump({"note": "P processes, each single amg_2_v(res_tol=1e-10) calls on its cyclic "

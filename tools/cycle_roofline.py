@@ -99,9 +99,20 @@ def run(args):
           flush=True)
 
 
+def is_cycle_end(name, fused):
+    """The cycle's last launch: k_finalize_norm, or — with the norm finished inside the pass
+    (no finalize launch) — the end-of-cycle residual pass, the only RESID launch with NORM."""
+    return "k_finalize_norm" in name if not fused else "<1, true" in name
+
+
+def fused_norm(names):
+    return not any("k_finalize_norm" in n for n in names)
+
+
 def cycles_of(rows, key_start, key_end, key_name):
     rows = sorted(rows, key=lambda r: int(r[key_start]))
-    idx = [i for i, r in enumerate(rows) if "k_finalize_norm" in r[key_name]]
+    fused = fused_norm(r[key_name] for r in rows)
+    idx = [i for i, r in enumerate(rows) if is_cycle_end(r[key_name], fused)]
     return [rows[a + 1:b + 1] for a, b in zip(idx, idx[1:])]
 
 
@@ -109,7 +120,8 @@ def pmc_per_position(path, names, counter):
     """Median counter value per cycle position from a counter_collection CSV."""
     rows = [r for r in csv.DictReader(open(path)) if r.get("Counter_Name") == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    idx = [i for i, r in enumerate(rows) if "k_finalize_norm" in r["Kernel_Name"]]
+    fused = fused_norm(r["Kernel_Name"] for r in rows)
+    idx = [i for i, r in enumerate(rows) if is_cycle_end(r["Kernel_Name"], fused)]
     cyc = [rows[a + 1:b + 1] for a, b in zip(idx, idx[1:])]
     cyc = [c for c in cyc if len(c) == len(names)]
     if not cyc:
@@ -118,10 +130,34 @@ def pmc_per_position(path, names, counter):
             for i in range(len(names))]
 
 
+def counters(args):
+    """Per-position medians of every counter in the given counter_collection CSVs."""
+    meta = json.load(open(os.path.join(args.outdir, "launch_bytes.json")))
+    launches = meta["launches"]
+    res = {}
+    for path in args.csv:
+        rows = list(csv.DictReader(open(path)))
+        if fused_norm(r["Kernel_Name"] for r in rows):
+            launches = [L for L in meta["launches"] if L["op"] != "norm finalize"]
+        for name in sorted({r["Counter_Name"] for r in rows}):
+            v = pmc_per_position(path, launches, name)
+            if v is not None:
+                res[name] = v
+    names = sorted(res)
+    print("| # | launch | " + " | ".join(names) + " |")
+    print("|---|---|" + "---|" * len(names))
+    for i, L in enumerate(launches):
+        print(f"| {i} | {L['op']} | " + " | ".join(f"{res[k][i]:.4g}" for k in names) + " |")
+    with open(os.path.join(args.outdir, "cycle_counters.json"), "w") as fh:
+        json.dump({"positions": [L["op"] for L in launches], "counters": res}, fh, indent=1)
+
+
 def table(args):
     meta = json.load(open(os.path.join(args.outdir, "launch_bytes.json")))
     launches = meta["launches"]
     rows = list(csv.DictReader(open(args.trace)))
+    if fused_norm(r["Kernel_Name"] for r in rows):  # the norm is finished inside its pass
+        launches = [L for L in launches if L["op"] != "norm finalize"]
     cyc = cycles_of(rows, "Start_Timestamp", "End_Timestamp", "Kernel_Name")
     cyc = [c for c in cyc if len(c) == len(launches)][-15:]
     if not cyc:
@@ -180,8 +216,11 @@ def main():
     t.add_argument("trace")
     t.add_argument("--fetch")
     t.add_argument("--write")
+    c = sub.add_parser("counters")
+    c.add_argument("outdir")
+    c.add_argument("csv", nargs="+")
     args = ap.parse_args()
-    run(args) if args.cmd == "run" else table(args)
+    {"run": run, "table": table, "counters": counters}[args.cmd](args)
 
 
 if __name__ == "__main__":

@@ -15,7 +15,11 @@ import sys
 
 def cycles(rows):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "k_finalize_norm" in r["Kernel_Name"]]
+    fused = not any("k_finalize_norm" in r["Kernel_Name"] for r in rows)
+    # the cycle ends with k_finalize_norm, or, with the norm finished inside its pass, with the
+    # end-of-cycle residual pass (the only RESID launch with NORM: "<1, true")
+    idx = [i for i, r in enumerate(rows)
+           if ("<1, true" in r["Kernel_Name"] if fused else "k_finalize_norm" in r["Kernel_Name"])]
     return [rows[a + 1:b + 1] for a, b in zip(idx, idx[1:])]
 
 
