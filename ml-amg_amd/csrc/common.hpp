@@ -309,7 +309,7 @@ int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, hipStream_t s
 int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
                   double* hist, int32_t* counter, int32_t* done, double tol, double* copy_to,
                   const double* copy_from, double* partial, hipStream_t s,
-                  const double* smooth_dinv = nullptr, uint32_t* fin_arrive = nullptr);
+                  const double* smooth_dinv = nullptr);
 int residual_partials(const mlamg_csr* A, const double* b, const double* x, double* r,
                       double* copy_to, const double* copy_from, double* partial,
                       const int32_t* done, hipStream_t s, const double* smooth_dinv = nullptr);

@@ -63,7 +63,7 @@ struct mlamg_hier {
   void* mem = nullptr;
   size_t mem_bytes = 0;
   double* partial = nullptr;
-  int32_t* flags = nullptr;  // [0] counter, [1] done, [2] norm-pass arrival counter
+  int32_t* flags = nullptr;  // [0] counter, [1] done
   bool ready = false;
   // captured single cycle
   hipGraph_t graph = nullptr;
@@ -324,11 +324,9 @@ static int cycle_top(mlamg_hier* H, const double* b, double* x, double* hist, do
   }
   // fused: nothing reads this r (the next cycle starts with its own residual), so it is not
   // stored — the kernel still forms it for the norm and the fused sweep x = t + Dinv_w r
-  // the norm is finished by the pass's last workgroup where the kernel supports it (no
-  // k_finalize_norm launch; arrival counter flags[2], zeroed at prepare and after each pass)
   MLAMG_TRY(residual_impl(L.A, b, cur, fused ? nullptr : L.r, nullptr, hist, counter, done, tol,
                           cur != x ? x : nullptr, cur != x ? cur : nullptr, H->partial, s,
-                          fused ? L.dinv : nullptr, reinterpret_cast<uint32_t*>(H->flags + 2)));
+                          fused ? L.dinv : nullptr));
   return MLAMG_OK;
 }
 

@@ -40,16 +40,6 @@ struct Epi {
   // FADD (factored SA prolongation, k_rowpat_uni only): the kernel's x operand is the virtual
   // vector t = Agg e (t_i = e[agg[i]], 0 where agg[i] < 0) and y += t - dinv * (A t)
   const int32_t* agg;
-  // end-of-cycle norm finished in the norm pass itself (NORM kernels of one partial per
-  // workgroup; norm_fin below): arrival counter (zero between launches; nullptr = write the
-  // partials only), partial count, and k_finalize_norm's outputs
-  uint32_t* fin_arrive;
-  int fin_n;
-  double* fin_out;
-  double* fin_hist;
-  int32_t* fin_counter;
-  int32_t* fin_done;
-  double fin_tol;
 };
 
 // A level operator (square) of at most kCachedNnz entries (~100 MB in CSR) is read with ordinary
@@ -150,77 +140,6 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
   return (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + i;
 }
 
-// ---------------------------------------------------------------- norm finished in the pass
-// The end-of-cycle residual norm without a k_finalize_norm launch (VERDICT r05 Next #2a). Every
-// workgroup publishes its partial with a write-through store (relaxed agent-scope atomic store:
-// `global_store ... sc1`), waits for it (vmcnt(0)) and adds 1 to an arrival counter (agent scope,
-// relaxed); the workgroup whose add returns gridDim - 1 reads every partial with sc1 loads and
-// finishes the norm. No release / acquire fence: the round-4 variant fenced every workgroup
-// (an agent release writes back the XCD's L2, dirty with the pass's own output) and lost 30 %
-// (DESIGN §13). The hand-off is the first row of the measured sc1 table in
-// /opt/skills/guides/MI355X_MICROARCH.md (§ Workgroup dispatch: one lane per storing workgroup,
-// drained, one unsharded counter, the last adder loads after its add returned, the other waves
-// after a barrier). The last workgroup sums the partials in k_finalize_norm's order — 1024
-// virtual threads with strided sums, xor butterflies per 64 lanes, 16 wave sums in order — so
-// the norm has the same bits as the launch it replaces.
-__device__ __forceinline__ void norm_put(const Epi& ep, int64_t slot, double t) {
-  if (ep.fin_arrive)
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(ep.partial + slot),
-                       (unsigned long long)__double_as_longlong(t), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  else
-    ep.partial[slot] = t;
-}
-
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __longlong_as_double((long long)__hip_atomic_load(
-      reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-template <int BS>
-__device__ __forceinline__ void norm_fin(const Epi& ep) {
-  static_assert(BS % 64 == 0 && 1024 % BS == 0, "workgroup of whole waves dividing 1024");
-  __shared__ int fin_last;
-  __shared__ double fin_red[16];
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial's sc1 store has landed
-    const uint32_t prev =
-        __hip_atomic_fetch_add(ep.fin_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    fin_last = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!fin_last) return;
-  const int n = ep.fin_n;
-#pragma unroll
-  for (int k = 0; k < 1024 / BS; ++k) {
-    const int vt = (int)threadIdx.x + k * BS;  // virtual thread of the 1024-thread finalize
-    double s = 0.0;                            // strided_sum's order
-    int i = vt;
-    for (; i + 7 * 1024 < n; i += 8 * 1024) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = ld_sc1(ep.partial + i + u * 1024);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    for (; i < n; i += 1024) s += ld_sc1(ep.partial + i);
-    s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) fin_red[vt >> 6] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int i = 0; i < 16; ++i) t += fin_red[i];
-    const double nrm = sqrt(t);
-    if (ep.fin_out) *ep.fin_out = nrm;
-    const int c = ep.fin_counter ? *ep.fin_counter : 0;
-    if (ep.fin_hist) ep.fin_hist[c] = nrm;
-    if (ep.fin_counter) *ep.fin_counter = c + 1;
-    if (ep.fin_done && ep.fin_tol >= 0.0 && nrm <= ep.fin_tol) *ep.fin_done = 1;
-    __hip_atomic_store(ep.fin_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 template <int OP, bool NORM>
 __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restrict__ indptr,
                                                          const int32_t* __restrict__ indices,
@@ -313,9 +232,8 @@ __global__ __launch_bounds__(kThreads) void k_csr_stream(const int32_t* __restri
     if (tid == 0) {
       double t = 0.0;
       for (int i = 0; i < kThreads / 64; ++i) t += red[i];
-      norm_put(ep, b, t);
+      ep.partial[b] = t;
     }
-    if (ep.fin_arrive) norm_fin<kThreads>(ep);
   }
 }
 
@@ -398,9 +316,8 @@ __global__ __launch_bounds__(kThreads) void k_sell(const int64_t* __restrict__ s
     if (threadIdx.x == 0) {
       double t = 0.0;
       for (int i = 0; i < kThreads / 64; ++i) t += red[i];
-      norm_put(ep, lb, t);
+      ep.partial[lb] = t;
     }
-    if (ep.fin_arrive) norm_fin<kThreads>(ep);
   }
 }
 
@@ -487,9 +404,8 @@ __global__ __launch_bounds__(kThreads) void k_sell_dict(const int64_t* __restric
     if (threadIdx.x == 0) {
       double t = 0.0;
       for (int i = 0; i < kThreads / 64; ++i) t += red[i];
-      norm_put(ep, lb, t);
+      ep.partial[lb] = t;
     }
-    if (ep.fin_arrive) norm_fin<kThreads>(ep);
   }
 }
 
@@ -739,9 +655,8 @@ void k_rowpair(const uint8_t* __restrict__ pid,
     if (threadIdx.x == 0) {
       double t = 0.0;
       for (int i = 0; i < kThreads / 64; ++i) t += red[i];
-      norm_put(ep, lb, t);
+      ep.partial[lb] = t;
     }
-    if (ep.fin_arrive) norm_fin<kThreads>(ep);
   }
 }
 
@@ -974,9 +889,8 @@ void k_rowpat_uni(
     if (threadIdx.x == 0) {
       double t = 0.0;
       for (int i = 0; i < kThreads / 64; ++i) t += red[i];
-      norm_put(ep, lb, t);
+      ep.partial[lb] = t;
     }
-    if (ep.fin_arrive) norm_fin<kThreads>(ep);
   }
 }
 
@@ -1347,9 +1261,8 @@ __global__ __launch_bounds__(kRpWinNT) void k_rowpair_win(const uint16_t* __rest
     if (threadIdx.x == 0) {
       double t = 0.0;
       for (int i = 0; i < NT / 64; ++i) t += red[i];
-      norm_put(ep, lb, t);
+      ep.partial[lb] = t;
     }
-    if (ep.fin_arrive) norm_fin<NT>(ep);
   }
 }
 
@@ -1991,9 +1904,8 @@ void k_sorted(const int32_t* __restrict__ indptr,
     if (tid == 0) {
       double t = 0.0;
       for (int i = 0; i < kSrtThreads / 64; ++i) t += red[i];
-      norm_put(ep, b, t);
+      ep.partial[b] = t;
     }
-    if (ep.fin_arrive) norm_fin<kSrtThreads>(ep);
   }
 }
 
@@ -2076,8 +1988,7 @@ __global__ __launch_bounds__(kThreads) void k_csr_long(const int32_t* __restrict
     double w = wave_sum(sq);
     if ((tid & 63) == 0) red[tid >> 6] = w;
     __syncthreads();
-    if (tid == 0) norm_put(ep, b, ((red[0] + red[1]) + red[2]) + red[3]);
-    if (ep.fin_arrive) norm_fin<kThreads>(ep);
+    if (tid == 0) ep.partial[b] = ((red[0] + red[1]) + red[2]) + red[3];
   }
 }
 
@@ -3680,42 +3591,10 @@ static double* partial_buf(const mlamg_csr* A) {
   return static_cast<double*>(scratch(sizeof(double) * part_capacity(A), 0));
 }
 
-// The NORM launch of A writes one partial per workgroup and its grid has exactly n_part
-// workgroups: then the norm can be finished by the last-arriving workgroup (norm_fin)
-static bool norm_fin_ok(const mlamg_csr* A) {
-  static const bool off = [] {
-    const char* e = std::getenv("MLAMG_FUSED_NORM");  // A/B knob: 0 = separate finalize launch
-    return e && e[0] == '0';
-  }();
-  if (off || A->vec_width || A->n_part <= 0) return false;
-  const int64_t n_pairs = (A->n_rows + 1) / 2;
-  int64_t nb = -1;
-  if (A->lg_tile) {
-    nb = A->lg_nt;
-  } else if (A->rp_pid) {
-    if (A->rp_uni.k > 0 && A->rp_msk) {
-      const int64_t ch = A->rp_uni.ch == 1 ? 1 : A->rp_uni.ch == 2 ? 2 : 4;
-      nb = (n_pairs + ch * kThreads - 1) / (ch * kThreads);
-    } else if (A->rp_win.rows >= 0 && A->rp_slot) {
-      nb = (n_pairs + kRpWinNT - 1) / kRpWinNT;
-    }
-  } else if (A->srt_pk) {
-    nb = A->srt_nb;
-  } else if (A->dict_code) {
-    const int64_t per_block = (kThreads / 64) * dict_slices_per_wave();
-    nb = (A->n_slices + per_block - 1) / per_block;
-  } else if (A->sell_ptr) {
-    nb = (A->n_slices + kThreads / 64 - 1) / (kThreads / 64);
-  } else {
-    nb = A->n_blocks;
-  }
-  return nb > 0 && nb == A->n_part;
-}
-
 int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* r, double* norm2,
                   double* hist, int32_t* counter, int32_t* done, double tol, double* copy_to,
                   const double* copy_from, double* partial, hipStream_t s,
-                  const double* smooth_dinv, uint32_t* fin_arrive) {
+                  const double* smooth_dinv) {
   Epi ep{};
   ep.b = b;
   ep.y = r;
@@ -3727,16 +3606,6 @@ int residual_impl(const mlamg_csr* A, const double* b, const double* x, double* 
   if (!want) return launch<EPI_RESID, false>(A, x, ep, s);
   ep.partial = partial ? partial : partial_buf(A);
   MLAMG_REQUIRE(ep.partial, "scratch allocation failed");
-  if (fin_arrive && norm_fin_ok(A)) {  // finished by the pass's last workgroup: no launch
-    ep.fin_arrive = fin_arrive;
-    ep.fin_n = A->n_part;
-    ep.fin_out = norm2;
-    ep.fin_hist = hist;
-    ep.fin_counter = counter;
-    ep.fin_done = done;
-    ep.fin_tol = tol;
-    return launch<EPI_RESID, true>(A, x, ep, s);
-  }
   MLAMG_TRY((launch<EPI_RESID, true>(A, x, ep, s)));
   hipLaunchKernelGGL(k_finalize_norm, dim3(1), dim3(1024), 0, s, ep.partial, A->n_part, norm2,
                      hist, counter, done, tol);

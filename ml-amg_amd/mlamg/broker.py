@@ -18,8 +18,9 @@ per problem: mlamg_amg2v_batch) — no caller edits.
 * Transfer. A request is a length-prefixed JSON header (parameters, array dtypes and shapes)
   followed by the raw bytes of A (indptr, indices, data), P (same), b and x over the socket; the
   answer carries x and the residual history the same way, and conv / iterations in the header.
-* Batching. The broker's batcher thread takes every request queued at that moment, groups them
-  by their keyword arguments and runs each group: problems within the fused batch kernel's
+* Batching. Each of the broker's batcher threads (MLAMG_BROKER_STREAMS, default 4, each with a
+  HIP stream of its own, so a batch queued behind a slow one does not wait for it) takes every
+  request queued at that moment, groups them by their keyword arguments and runs each group: problems within the fused batch kernel's
   limits (n_c <= FUSED_BATCH_MAX_NC) in one mlamg_amg2v_batch launch — each result is bitwise
   its own single call (tests/test_gpu_batch.py, test_batch_equals_sequential) — and the others
   through the same amg_2_v a worker would call, one after another.
@@ -251,6 +252,18 @@ class _Server:
             conn.close()
 
     def _batcher(self):
+        ctx = None
+        if self.backend is _gpu_backend:  # each batcher launches on a stream of its own, so a
+            import torch                  # batch behind a slow one does not wait for it
+            torch.cuda.set_device(self.device)
+            ctx = torch.cuda.stream(torch.cuda.Stream(device=self.device))
+        if ctx is not None:
+            with ctx:
+                self._batch_loop()
+        else:
+            self._batch_loop()
+
+    def _batch_loop(self):
         while not self.stop.is_set():
             try:
                 first = self.q.get(timeout=0.2)
@@ -262,8 +275,9 @@ class _Server:
                     items.append(self.q.get_nowait())
                 except queue.Empty:
                     break
-            self.stats["batches"] += 1
-            self.stats["requests"] += len(items)
+            with self.lock:
+                self.stats["batches"] += 1
+                self.stats["requests"] += len(items)
             try:
                 self.backend(self, items)
             except Exception as e:  # every waiting worker gets the error, none hangs
@@ -286,7 +300,9 @@ class _Server:
         with open(self.path + ".pid", "w") as fh:
             fh.write(str(os.getpid()))
         srv.settimeout(0.5)
-        threading.Thread(target=self._batcher, daemon=True, name="mlamg-broker-batch").start()
+        for i in range(max(1, int(os.environ.get("MLAMG_BROKER_STREAMS", "4")))):
+            threading.Thread(target=self._batcher, daemon=True,
+                             name=f"mlamg-broker-batch{i}").start()
         idle = float(os.environ.get("MLAMG_BROKER_IDLE", "120"))
         try:
             while not self.stop.is_set():
@@ -302,10 +318,11 @@ class _Server:
                 threading.Thread(target=self._serve_conn, args=(conn,), daemon=True).start()
         finally:
             srv.close()
-            try:
-                os.unlink(self.path)
-            except FileNotFoundError:
-                pass
+            for f in (self.path, self.path + ".pid"):
+                try:
+                    os.unlink(f)
+                except FileNotFoundError:
+                    pass
 
 
 def _unpack(item):

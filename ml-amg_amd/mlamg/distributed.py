@@ -383,6 +383,12 @@ def tune_local(M_glob, M_loc, kind, autotune=True):
     (M_loc, {"chosen": ..., "us": {...}})."""
     from .hierarchy import Hierarchy
     fmt, arg, _ = M_glob.get_format()
+    if (autotune and M_loc.shape == M_glob.shape and M_loc.nnz == M_glob.nnz
+            and M_loc.fingerprint() == M_glob.fingerprint()):
+        # the rank's operator IS the global one (world 1, or a level a rank owns whole, e.g. the
+        # whole coarse index space): the global autotune's choice, nothing to time
+        M_loc.set_format(fmt, arg)
+        return M_loc, {"chosen": "/".join(map(str, M_loc.get_format()[:2])), "reused": True}
     if not autotune:
         try:
             M_loc.set_format(fmt, arg)
@@ -402,16 +408,27 @@ def tune_local(M_glob, M_loc, kind, autotune=True):
         cands = list(Hierarchy.EXACT_CANDIDATES)
         if M_loc.nnz >= 16 * max(M_loc.shape[0], 1):
             cands += list(Hierarchy.LONG_CANDIDATES)
+    # as Hierarchy.apply_formats: the global choice first, then the rest in order of their byte
+    # lower bound; a candidate that could not beat the best time even at LB_PEAK_BPS is skipped
+    # (a timing rule only: every candidate of the family computes the same bits)
+    lbs = {c: Hierarchy._lower_bound_us(M_loc, kind, c[0]) for c in cands}
+    cands.sort(key=lambda c: (c != (fmt, arg), lbs[c]))
+    pruned, refused = [], set()
     for f, a in cands:
+        if (times and lbs[(f, a)] >= min(times.values())) or f in refused:
+            pruned.append(f"{f}/{a}")
+            continue
         try:
             times[f"{f}/{a}"] = Hierarchy._time_format(M_loc, f, a, x, y, kind=kind)
         except _lib.MlamgError as e:
             if e.code != _lib.MLAMG_EUNSUPPORTED:
                 raise
+            refused.add(f)
     best = min(times, key=times.get)
     f, a = best.split("/")
     M_loc.set_format(f, int(a))
-    return M_loc, {"chosen": best, "us": {k: round(v, 2) for k, v in times.items()}}
+    return M_loc, {"chosen": best, "us": {k: round(v, 2) for k, v in times.items()},
+                   "pruned": pruned}
 
 
 def sync_formats(H, world):

@@ -983,14 +983,12 @@ def test_factored_prolongation_within_tolerance(ml, oracle, torch_cuda, dim, n1)
                                       ("p3d", ("sell", 1)), ("p3d", ("sell_dict", 1)),
                                       ("p3d", ("csr_stream", 0)), ("p2d_1536", ("csr_stream", 0)),
                                       ("varcoef", ("sell", 512)), ("varcoef", ("sorted", 2))])
-def test_end_of_cycle_norm_in_pass_same_bits(ml, torch_cuda, case, fmt):
-    """The end-of-cycle norm finished inside the norm pass by its last-arriving workgroup
-    (csrc/spmv.hip norm_fin: sc1 partials, one arrival counter, no k_finalize_norm launch) has
-    k_finalize_norm's bits: after one fused cycle x holds t and hist[0] = ||b - A t||, and
-    mlamg_residual (partials + the separate finalize launch) on that x gives the same double.
-    Fine-level formats with one partial per workgroup, up to 9,216 partials (the finalize's
-    unrolled strided loop); then a tolerance stop on the same cycle count as the separate
-    finalize's cycle."""
+def test_end_of_cycle_norm_same_bits(ml, torch_cuda, case, fmt):
+    """The end-of-cycle norm of the fused cycle (the residual pass of t that also writes the next
+    cycle's first sweep, MLAMG.py:194) is the norm mlamg_residual computes on the same iterate:
+    after one cycle x holds t and hist[0] = ||b - A t|| bit for bit. Every fine-level format, up
+    to 9,216 norm partials (k_finalize_norm's unrolled strided loop); then a tolerance stop on
+    the cycle whose norm met it."""
     torch = torch_cuda
     from mlamg._lib import call, ptr, stream_ptr
     if case == "p3d":

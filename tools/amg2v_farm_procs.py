@@ -63,6 +63,19 @@ def worker(rank, nprocs, ngrids, device, kw):
     print(json.dumps({"rank": rank, "s": dt, "iters": its}), flush=True)
 
 
+def stop_broker():
+    """Shut the farm's broker down (a socket message: this parent never touches the GPU) and
+    wait until it has exited."""
+    os.environ["MLAMG_BROKER_DIR"] = BROKER_DIR
+    from mlamg import broker
+    broker.shutdown()
+    for _ in range(600):
+        if not os.path.exists(broker.socket_path()):
+            break
+        time.sleep(0.05)
+    time.sleep(0.5)  # the process releases the GPU after it removed its socket
+
+
 def run_farm(nprocs, ngrids, device, mode):
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     if device == "broker":
@@ -117,6 +130,8 @@ def main():
                else "amg_2_v(..., error_tol=1e-6)"}
         for device in devices:
             wall, outs = run_farm(pn, args.grids, device, args.mode)
+            if device == "broker":  # stop it now: the next GPU farm's P processes plus a live
+                stop_broker()       # broker would exceed the box's 16 GPU processes
             row[f"{device}_wall_s"] = round(wall, 3)
             row[f"{device}_grids_per_s"] = round(args.grids / wall, 2)
             row[f"{device}_iters"] = [it for o in sorted(outs, key=lambda o: o["rank"])
@@ -131,10 +146,6 @@ def main():
             row.pop(f"{d}_iters", None)
         print(json.dumps(row), flush=True)
         rows.append(row)
-    if "broker" in devices:
-        os.environ["MLAMG_BROKER_DIR"] = BROKER_DIR
-        from mlamg import broker
-        broker.shutdown()  # the parent never touched the GPU; this is a socket message
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as fh:
         json.dump({"note": "P processes, each single amg_2_v(res_tol=1e-10) calls on its cyclic "
