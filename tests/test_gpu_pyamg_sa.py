@@ -255,6 +255,32 @@ def test_pyamg_sa_hierarchy_and_cycle(ml, oracle, torch_cuda, case):
     assert hist[-1] < (1e-3 if case.startswith("poisson") else 0.1) * np.linalg.norm(b)
 
 
+def test_factored_prolong_refused_on_pyamg_recipe(ml, torch_cuda):
+    """pyamg's P = T - (omega/rho) D^-1 A T smooths the normalised candidate T, not the 0/1
+    aggregate operator, so the factored form x += t - w D^-1 A t (t = Agg e) of
+    Hierarchy.set_factored_prolong would be another prolongator: the call is refused
+    (EUNSUPPORTED) and the cycle keeps pyamg's explicit P, bit for bit."""
+    torch = torch_cuda
+    from mlamg._lib import MLAMG_EUNSUPPORTED, MlamgError
+    A = sp.csr_matrix(_matrices(ml)["poisson3d_18"])
+    H = ml.hierarchy.Hierarchy.pyamg_sa(A)
+    assert H.recipe == "pyamg_sa" and H.levels[0].agg_col is not None
+    b = torch.as_tensor(np.random.default_rng(3).standard_normal(A.shape[0])).cuda()
+    x1 = torch.zeros_like(b)
+    h1 = H.cycle(b, x1, 3)
+    with pytest.raises(MlamgError) as e:
+        H.set_factored_prolong(0)
+    assert e.value.code == MLAMG_EUNSUPPORTED
+    x2 = torch.zeros_like(b)
+    h2 = H.cycle(b, x2, 3)
+    assert np.array_equal(h1, h2) and torch.equal(x1, x2)
+    # the Bellman-Ford SA recipe (P = (I - w D^-1 A) Agg) still takes it
+    Hb = ml.hierarchy.Hierarchy.build(ml.problems.poisson_3d_7pt(24), alpha=0.1, max_coarse=300)
+    assert Hb.recipe == "mlamg_sa" and Hb.levels[0].sa_prolong
+    Hb.set_factored_prolong(0)
+    Hb.set_factored_prolong(0, on=False)
+
+
 def test_multilevel_pc_uses_pyamg_recipe(ml, torch_cuda):
     """The PyAMG PC (PyAMG.py:13-130) builds pyamg's recipe by default and its GMRES apply meets
     the amg_rtol stop (1e-8 relative); 'mlamg_sa' selects the Bellman-Ford SA recipe."""

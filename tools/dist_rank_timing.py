@@ -31,7 +31,9 @@ def main():
     a = ap.parse_args()
     torch.cuda.set_device(0)
     A = problems.poisson_3d_7pt(a.n)
-    H = Hierarchy.build(A, alpha=0.1, strength_mode="invabs", max_coarse=2000)
+    # the bench's hierarchy (bench.py defaults): reference aggregation, coarse rows in seed order
+    H = Hierarchy.build(A, alpha=0.1, strength_mode="invabs", max_coarse=2000,
+                        aggregation="reference", coarse_order="sorted")
     n = A.shape[0]
     xd = torch.zeros(n, dtype=torch.float64, device="cuda")
     bd = torch.zeros(n, dtype=torch.float64, device="cuda")
@@ -63,7 +65,8 @@ def main():
                        "overlap": ov, "splits": [(s["level"], s["op"]) for s in D.splits],
                        "compute_ms_per_cycle": round(t * 1e3, 4),
                        "compute_bound_cycles_per_s": round(1.0 / t, 1),
-                       "local_formats": [x["chosen"] for x in D.tuning]}
+                       "local_formats": [x["chosen"] for x in D.tuning],
+                       "partition_s": {k: round(v, 3) for k, v in D.setup_times.items()}}
                 out["ranks"].append(row)
                 print(json.dumps(row), flush=True)
             del D

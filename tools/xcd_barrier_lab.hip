@@ -62,6 +62,20 @@ __global__ __launch_bounds__(256) void k_barriers(unsigned* ctr, int steps, int 
   if (threadIdx.x == 0) spin_out[me] = spins;
 }
 
+// streaming read of n doubles by the participating blocks (b % stride == 0), 16-B loads, one
+// partial sum per block (so nothing is optimised away)
+__global__ __launch_bounds__(256) void k_read(const double2* __restrict__ p, int64_t n2,
+                                              int stride, double* out) {
+  if (blockIdx.x % stride) return;
+  const int64_t nb = gridDim.x / stride, me = blockIdx.x / stride;
+  double s = 0.0;
+  for (int64_t i = me * 256 + threadIdx.x; i < n2; i += nb * 256) {
+    const double2 v = p[i];
+    s += v.x + v.y;
+  }
+  if (s == 1.2345) out[me] = s;
+}
+
 template <class F>
 static float time_ms(F f, int reps, hipStream_t st) {
   hipEvent_t a, b;
@@ -131,6 +145,28 @@ int main() {
     std::printf(", \"barrier_us_%s\": %.3f, \"one_xcd_%s\": %s", c.name, 1e3f * (t1 - t0) / S,
                 c.name, same ? "true" : "false");
     if (timeouts) std::printf(", \"timeouts_%s\": %d", c.name, timeouts);
+  }
+  // 3. what one XCD can stream: a coarse tail's working set (the C2 levels >= 2 + dense
+  // coarse inverse, ~18 MB, resident in the Infinity Cache across cycles) read by 32 blocks on
+  // one XCD vs 256 blocks on all eight, warm (back to back)
+  for (int mb : {4, 18, 64}) {
+    const int64_t n2 = (int64_t)mb * (1 << 20) / 16;
+    double2* buf;
+    CK(hipMalloc(&buf, n2 * 16));
+    CK(hipMemset(buf, 0, n2 * 16));
+    double* out;
+    CK(hipMalloc(&out, sizeof(double) * 256));
+    const float t_one = time_ms([&] {
+      hipLaunchKernelGGL(k_read, dim3(256), dim3(256), 0, st, buf, n2, 8, out);
+    }, 20, st);
+    const float t_all = time_ms([&] {
+      hipLaunchKernelGGL(k_read, dim3(256), dim3(256), 0, st, buf, n2, 1, out);
+    }, 20, st);
+    CK(hipGetLastError());
+    std::printf(", \"read_%dMB_one_xcd_GBps\": %.0f, \"read_%dMB_all_GBps\": %.0f", mb,
+                n2 * 16 / (t_one * 1e6), mb, n2 * 16 / (t_all * 1e6));
+    CK(hipFree(buf));
+    CK(hipFree(out));
   }
   std::printf("}\n");
   CK(hipGraphExecDestroy(ge));
