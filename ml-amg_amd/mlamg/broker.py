@@ -20,10 +20,11 @@ per problem: mlamg_amg2v_batch) — no caller edits.
   answer carries x and the residual history the same way, and conv / iterations in the header.
 * Batching. Each of the broker's batcher threads (MLAMG_BROKER_STREAMS, default 4, each with a
   HIP stream of its own, so a batch queued behind a slow one does not wait for it) takes every
-  request queued at that moment, groups them by their keyword arguments and runs each group: problems within the fused batch kernel's
-  limits (n_c <= FUSED_BATCH_MAX_NC) in one mlamg_amg2v_batch launch — each result is bitwise
-  its own single call (tests/test_gpu_batch.py, test_batch_equals_sequential) — and the others
-  through the same amg_2_v a worker would call, one after another.
+  request queued at that moment, groups them by their keyword arguments and runs each group: the
+  problems a single call would give the fused engine (n_c <= FUSED_SINGLE_MAX_NC) in one
+  mlamg_amg2v_batch launch — each problem's path in the kernel follows its own size, so each
+  result is bitwise its own single call (tests/test_gpu_batch.py, tests/test_gpu_broker.py) —
+  and the others through the same amg_2_v a worker would call, one after another.
 * Failure. A broker that dies (or closes the connection) makes the pending call raise
   BrokerError in the worker instead of hanging; the next call starts a new broker.
 """
@@ -296,6 +297,7 @@ class _Server:
             pass
         srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
         srv.bind(self.path)
+        os.chmod(self.path, 0o600)  # this user's workers only
         srv.listen(256)
         with open(self.path + ".pid", "w") as fh:
             fh.write(str(os.getpid()))
@@ -362,7 +364,10 @@ def _gpu_backend(server, items):
         fused, prepared, xs = [], [], []
         if not kw["singular"]:
             for m in members:
-                prep = mg._fused_arrays(m[1], m[2], m[3], m[4], mg.FUSED_BATCH_MAX_NC)
+                # every problem a single call would give the fused engine (n_c up to
+                # FUSED_SINGLE_MAX_NC): its path inside the kernel follows its own n_c, so the
+                # batch result is its single call's, bit for bit (tests/test_gpu_broker.py)
+                prep = mg._fused_arrays(m[1], m[2], m[3], m[4], mg.FUSED_SINGLE_MAX_NC)
                 if prep is not None:
                     fused.append(m)
                     prepared.append(prep)
