@@ -60,6 +60,9 @@ constexpr int kBMaxK = 32;          // off-diagonal entries per row of A
 constexpr int kBMaxKP = 32;         // entries per row of P
 constexpr int kBMaxKT = 256;        // entries per row of P^T
 constexpr int kBMaxPanel = 16;
+#ifndef MLAMG_GS_SCHED_FENCE  // build-time A/B knob: scheduling barrier after a level's stores
+#define MLAMG_GS_SCHED_FENCE 1
+#endif
 constexpr int kExtCoarseMin = 300;  // single calls above this n_c: device-wide coarse factor
 constexpr size_t kBLdsBytes = 156 * 1024;
 
@@ -1400,6 +1403,12 @@ __global__ __launch_bounds__(kBT) void k_amg2v_cycles(const BDesc* __restrict__ 
         for (int k = 0; k < KM; ++k) y += v[u][k] * g[u][k];
         xs[row[u]] = (bv[u] - y) / d[u];
       }
+#if MLAMG_GS_SCHED_FENCE
+      // keep the next level's register copies below the store: scheduled above it they made
+      // the store wait for the next level's structure reads (s_waitcnt lgkmcnt(0) before the
+      // division's last step), one LDS round trip on every level of the dependency chain
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
