@@ -286,6 +286,26 @@ int mlamg_bellman_ford(const mlamg_csr* G, const int32_t* seeds, int32_t k, floa
 int mlamg_bellman_ford_canon(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* dist_f32,
                              int32_t* cluster, int32_t* iters_host, void* stream);
 
+/* mlamg_bellman_ford_canon taken apart, for the distributed setup (a sweep,
+ * then the boundary (distance, label) exchange and an any-changed reduction, until no rank
+ * changes anything; mlamg/dsetup.py). G may be a "global-shaped" operator whose rows outside a
+ * rank's range are empty; every array is indexed by global node id.
+ *   begin: w_f32[nnz] = (float)G.data, dist = +inf, cluster = INT32_MAX, is_seed = 0 for all n,
+ *          then seeds[0..k): dist 0, cluster = itself, is_seed 1 (seeds may lie in any rank's
+ *          range: every rank marks the global seed list);
+ *   sweep: one push relaxation over G's rows (atomicMin; *changed = 1 if anything decreased —
+ *          ghost copies included; the caller zeroes it);
+ *   label: one min-label push along tight edges (dist final);
+ *   end:   cluster INT32_MAX -> -1.
+ * All asynchronous on `stream`. */
+int mlamg_bf_canon_begin(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* w_f32,
+                         float* dist_f32, int32_t* cluster, int32_t* is_seed, void* stream);
+int mlamg_bf_canon_sweep(const mlamg_csr* G, const float* w_f32, float* dist_f32, int32_t* changed,
+                         void* stream);
+int mlamg_bf_canon_label(const mlamg_csr* G, const float* w_f32, const float* dist_f32,
+                         const int32_t* is_seed, int32_t* cluster, int32_t* changed, void* stream);
+int mlamg_bf_canon_end(int32_t* cluster, int64_t n, void* stream);
+
 /* pyamg 4.x graph.bellman_ford(G, seeds) exactly (the aggregation step of FullAggNet.forward,
  * ns/model/agg_interp.py:475; replaces that call): sequential in-place pull sweeps
  * x_i <- min(x_i, G_ij + x_j) over rows 0..n-1 in stored order, strict <, nearest seed from the

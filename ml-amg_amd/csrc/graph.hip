@@ -719,6 +719,56 @@ int mlamg_bellman_ford_canon(const mlamg_csr* G, const int32_t* seeds, int32_t k
   return MLAMG_OK;
 }
 
+int mlamg_bf_canon_begin(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* w,
+                         float* dist, int32_t* cluster, int32_t* is_seed, void* stream) {
+  MLAMG_REQUIRE(G && w && dist && cluster && is_seed && (k == 0 || seeds), "NULL argument");
+  MLAMG_REQUIRE(G->n_rows == G->n_cols, "graph must be square");
+  MLAMG_REQUIRE(k >= 0 && k <= G->n_rows, "seed count out of range");
+  hipStream_t s = S(stream);
+  const int64_t n = G->n_rows;
+  int64_t bad = 0;
+  MLAMG_TRY(count_out_of_range(seeds, k, 0, n, s, &bad));
+  MLAMG_REQUIRE(bad == 0, "seed index out of range [0, n)");
+  if (G->nnz) hipLaunchKernelGGL(k_to_f32, g1(G->nnz), dim3(256), 0, s, G->data, G->nnz, w);
+  if (n) {
+    MLAMG_HIP(hipMemsetAsync(is_seed, 0, sizeof(int32_t) * n, s));
+    hipLaunchKernelGGL(k_bf_init, g1(n), dim3(256), 0, s, dist, cluster, n);
+  }
+  if (k) hipLaunchKernelGGL(k_bf_seeds, g1(k), dim3(256), 0, s, seeds, k, dist, cluster, is_seed);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+int mlamg_bf_canon_sweep(const mlamg_csr* G, const float* w, float* dist, int32_t* changed,
+                         void* stream) {
+  MLAMG_REQUIRE(G && w && dist && changed, "NULL argument");
+  MLAMG_REQUIRE(G->n_rows == G->n_cols, "graph must be square");
+  if (G->n_rows)
+    hipLaunchKernelGGL(k_bf_sweep, g1(G->n_rows), dim3(256), 0, S(stream), G->indptr, G->indices,
+                       w, G->n_rows, dist, changed);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+int mlamg_bf_canon_label(const mlamg_csr* G, const float* w, const float* dist,
+                         const int32_t* is_seed, int32_t* cluster, int32_t* changed,
+                         void* stream) {
+  MLAMG_REQUIRE(G && w && dist && is_seed && cluster && changed, "NULL argument");
+  MLAMG_REQUIRE(G->n_rows == G->n_cols, "graph must be square");
+  if (G->n_rows)
+    hipLaunchKernelGGL(k_bf_label, g1(G->n_rows), dim3(256), 0, S(stream), G->indptr, G->indices,
+                       w, G->n_rows, dist, is_seed, cluster, changed);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
+int mlamg_bf_canon_end(int32_t* cluster, int64_t n, void* stream) {
+  MLAMG_REQUIRE(n == 0 || cluster, "NULL argument");
+  if (n) hipLaunchKernelGGL(k_lab_finish, g1(n), dim3(256), 0, S(stream), cluster, n);
+  MLAMG_HIP(hipGetLastError());
+  return MLAMG_OK;
+}
+
 int mlamg_bellman_ford(const mlamg_csr* G, const int32_t* seeds, int32_t k, float* dist,
                        int32_t* nearest, int32_t* sweeps_host, void* stream) {
   MLAMG_REQUIRE(G && dist && nearest && (k == 0 || seeds), "NULL argument");

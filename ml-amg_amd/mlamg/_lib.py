@@ -131,6 +131,10 @@ SIGNATURES = {
     "mlamg_bellman_ford": (c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, P_i32, c_vp]),
     "mlamg_bellman_ford_canon": (c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, P_i32, c_vp]),
     "mlamg_bellman_ford_pyamg": (c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp, P_i32, c_vp]),
+    "mlamg_bf_canon_begin": (c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_bf_canon_sweep": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_bf_canon_label": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mlamg_bf_canon_end": (c_int, [c_vp, c_i64, c_vp]),
     "mlamg_aggregate_op": (c_int, [c_vp, c_i64, c_i64, c_vpp, c_vp]),
     "mlamg_labels_to_columns": (c_int, [c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "mlamg_lloyd_cluster": (c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp, P_i32, c_vp]),

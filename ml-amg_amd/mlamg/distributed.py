@@ -170,7 +170,8 @@ class DistributedHierarchy:
         leave the GPU); 'numpy' downloads every partitioned operator and runs the host build
         (partition.build_levels, the reference implementation of the maps; A_host, if given,
         replaces the download of level 0). Both give the same maps. Phase wall times are kept
-        in self.setup_times."""
+        in self.setup_times.
+        Without a replicated hierarchy: DistributedHierarchy.from_setup (mlamg.dsetup)."""
         if not H.levels:
             raise ValueError("distributed cycle needs at least one level above the coarse solve")
         if (H.nu_pre, H.nu_post) != (1, 1):
@@ -178,6 +179,7 @@ class DistributedHierarchy:
         if any(L.seeds is None for L in H.levels):
             raise ValueError("hierarchy was not built by Hierarchy.build (seeds unknown)")
         self.H = H
+        self.setup = None
         self.comm = comm
         world, rank = comm.world, comm.rank
         K = 1
@@ -216,6 +218,38 @@ class DistributedHierarchy:
             raise ValueError(f"unknown partition_impl {partition_impl!r}")
         torch.cuda.synchronize()
         st["partition"] = time.perf_counter() - t0 - st["download"]
+        globs = [{"A": H.levels[l].A, "P": H.levels[l].P, "R": H.levels[l].R, "family": None}
+                 for l in range(K)]
+        dinvs = [H.levels[l].dinv[p["lo"]:p["hi"]].clone() for l, p in enumerate(parts)]
+        self._assemble(parts, globs, dinvs, H.levels[K:], H, local_autotune, overlap_min_rows,
+                       t0)
+
+    @classmethod
+    def from_setup(cls, S, comm, local_autotune=True, overlap_min_rows=2_000_000):
+        """The executor over a distributed setup (mlamg.dsetup.build_distributed): the rank's
+        partition maps and Jacobi weights as built there, each local operator's kernel family
+        by Hierarchy.apply_formats's rule on the global operator (S.families), the replicated
+        tail S.tail. Without a replicated hierarchy there is no global operator to reuse a
+        format from: every local operator is tuned within its family."""
+        if (S.nu_pre, S.nu_post) != (1, 1):
+            raise NotImplementedError("the distributed cycle is V(1,1)")
+        self = cls.__new__(cls)
+        self.H = None
+        self.setup = S
+        self.comm = comm
+        self.K = len(S.parts)
+        self.setup_times = {"download": 0.0, "partition": 0.0}
+        self.parts = S.parts
+        globs = [{"A": None, "P": None, "R": None, "family": f} for f in S.families]
+        self._assemble(S.parts, globs, S.dinv, S.tail.levels, S.tail, local_autotune,
+                       overlap_min_rows, time.perf_counter())
+        return self
+
+    def _assemble(self, parts, globs, dinvs, tail_levels, tail, local_autotune,
+                  overlap_min_rows, t0):
+        """Local operators (tuned), halos, the replicated coarse hierarchy and the C executor."""
+        comm = self.comm
+        st = self.setup_times
         t_ops = [0.0, 0.0]  # upload, local autotune
         p0 = parts[0]
         self.lo, self.hi = p0["lo"], p0["hi"]
@@ -223,11 +257,11 @@ class DistributedHierarchy:
 
         self.tuning = []
 
-        def like(M_glob, M_part, kind):
+        def like(M_glob, M_part, kind, family=None):
             t1 = time.perf_counter()
             M_loc = _device_csr(M_part)
             t2 = time.perf_counter()
-            M, t = tune_local(M_glob, M_loc, kind, autotune=local_autotune)
+            M, t = tune_local(M_glob, M_loc, kind, autotune=local_autotune, family=family)
             t_ops[0] += t2 - t1
             t_ops[1] += time.perf_counter() - t2
             self.tuning.append(t)
@@ -235,14 +269,14 @@ class DistributedHierarchy:
 
         self._keep = []
         last = parts[-1]
-        # replicated coarse hierarchy: levels K..L + the dense coarse inverse of H
+        # replicated coarse hierarchy: the levels below the partitioned ones + the coarse solve
         hh = ctypes.c_void_p()
         call("mlamg_hier_create", ctypes.byref(hh))
         self.coarse = hh
-        for L in H.levels[K:]:
+        for L in tail_levels:
             call("mlamg_hier_add_level", hh, L.A.handle, ptr(L.dinv), L.P.handle, L.R.handle)
-        call("mlamg_hier_set_coarse", hh, H.Ac.handle, H.dense)
-        call("mlamg_hier_set_smoothing", hh, int(H.nu_pre), int(H.nu_post))
+        call("mlamg_hier_set_coarse", hh, tail.Ac.handle, tail.dense)
+        call("mlamg_hier_set_smoothing", hh, int(tail.nu_pre), int(tail.nu_post))
         self.c_lo = np.array([a for a, _ in last["c_ranges"]], dtype=np.int64)
         self.c_hi = np.array([b for _, b in last["c_ranges"]], dtype=np.int64)
         d = ctypes.c_void_p()
@@ -253,11 +287,12 @@ class DistributedHierarchy:
         self.ghosts = []
         self.splits = []
         for l, p in enumerate(parts):
-            Lg = H.levels[l]
-            A_loc = like(Lg.A, p["A_loc"], "A")
-            P_loc = like(Lg.P, p["P_loc"], "P")
-            R_own = like(Lg.R, p["R_own"], "R")
-            dinv = Lg.dinv[p["lo"]:p["hi"]].clone()
+            g = globs[l]
+            fam = g["family"]
+            A_loc = like(g["A"], p["A_loc"], "A", fam and fam["A"])
+            P_loc = like(g["P"], p["P_loc"], "P", fam and fam["P"])
+            R_own = like(g["R"], p["R_own"], "R", fam and fam["R"])
+            dinv = dinvs[l]
             if A_loc.get_format()[0] == "rowpat":
                 A_loc.attach_dinv(dinv)
             hx = Halo(comm, p["halo_x"])
@@ -269,12 +304,14 @@ class DistributedHierarchy:
                  hx.handle, hr.handle, hp.handle if hp else None)
             if overlap_min_rows is not None:
                 n_l = p["hi"] - p["lo"]
-                ops = [(0, Lg.A, p["A_loc"], n_l, dinv), (1, Lg.R, p["R_own"], n_l, None)]
+                ops = [(0, g["A"], p["A_loc"], n_l, dinv, fam and fam["A"]),
+                       (1, g["R"], p["R_own"], n_l, None, fam and fam["R"])]
                 if hp is not None:
-                    ops.append((2, Lg.P, p["P_loc"], p["c_hi"] - p["c_lo"], None))
-                for which, M_glob, M_host, n_owned, dv in ops:
+                    ops.append((2, g["P"], p["P_loc"], p["c_hi"] - p["c_lo"], None,
+                                fam and fam["P"]))
+                for which, M_glob, M_host, n_owned, dv, fm in ops:
                     if M_host.shape[0] >= overlap_min_rows:
-                        self._split(l, which, M_glob, M_host, n_owned, dv, like)
+                        self._split(l, which, M_glob, M_host, n_owned, dv, like, fm)
             if l == 0:
                 self.A_loc = A_loc
                 self.hx = hx
@@ -285,7 +322,7 @@ class DistributedHierarchy:
         for p in parts:  # the maps' own copies of the local operators are not needed again
             p["A_loc"] = p["R_own"] = p["P_loc"] = None
 
-    def _split(self, l, which, M_glob, M_host, n_owned, dinv, like):
+    def _split(self, l, which, M_glob, M_host, n_owned, dinv, like, family=None):
         if isinstance(M_host, partition.TCSR):
             cut = partition.interior_split_torch(M_host, n_owned)
         else:
@@ -299,7 +336,7 @@ class DistributedHierarchy:
                 parts.append(None)
                 continue
             Mp = M_host.rows(a, b) if isinstance(M_host, partition.TCSR) else M_host[a:b]
-            M = like(M_glob, Mp, "APR"[which])
+            M = like(M_glob, Mp, "APR"[which], family)
             self.tuning.pop()  # keep D.tuning = the whole operators' choices, 3 per level
             if dinv is not None and M.get_format()[0] == "rowpat":
                 # a view: the epilogues are handed dinv + a, the very pointer attached
@@ -373,17 +410,27 @@ def _device_csr(M):
     return DeviceCSR.from_scipy(M, check=False)
 
 
-def tune_local(M_glob, M_loc, kind, autotune=True):
+def tune_local(M_glob, M_loc, kind, autotune=True, family=None):
     """Kernel for one rank's local operator. The local operator keeps every row's stored
     entry order, so any kernel of the global operator's family reproduces its rows bit for bit:
     the exact-order family (CSR-stream, SELL, sorted, dictionary SELL, row-pair patterns,
     long-row tiles: scipy's order) or the CSR-vector family (one canonical order for every
     width). With autotune the fastest of the family on the local operator is kept (ghost
     columns change what the encoders accept and how well they pack). Returns
-    (M_loc, {"chosen": ..., "us": {...}})."""
+    (M_loc, {"chosen": ..., "us": {...}}).
+    M_glob None (a distributed setup: no global operator on the rank): `family` ('exact' or
+    'vector', Hierarchy.apply_formats's rule on the global operator) names the family; the
+    search starts from its first candidate."""
     from .hierarchy import Hierarchy
-    fmt, arg, _ = M_glob.get_format()
-    if (autotune and M_loc.shape == M_glob.shape and M_loc.nnz == M_glob.nnz
+    if M_glob is None:
+        if family not in ("exact", "vector"):
+            raise ValueError("tune_local without a global operator needs family='exact' or "
+                             "'vector'")
+        fmt, arg = ("vector", 64) if family == "vector" else ("csr_stream", 0)
+    else:
+        fmt, arg, _ = M_glob.get_format()
+    if (autotune and M_glob is not None and M_loc.shape == M_glob.shape
+            and M_loc.nnz == M_glob.nnz
             and M_loc.fingerprint() == M_glob.fingerprint()):
         # the rank's operator IS the global one (world 1, or a level a rank owns whole, e.g. the
         # whole coarse index space): the global autotune's choice, nothing to time

@@ -326,7 +326,8 @@ class Hierarchy:
     def clear_tune_cache(cls):
         cls._TUNE_CACHE.clear()
 
-    def apply_formats(self, fine_format="autotune", coarse_format="auto", vec_min_row=None):
+    def apply_formats(self, fine_format="autotune", coarse_format="auto", vec_min_row=None,
+                      first_level=0):
         """Choose the SpMV kernel of every operator.
 
         The candidates of one operator all compute the same bits, so the autotune — a timing
@@ -339,7 +340,10 @@ class Hierarchy:
             rows of coarse Galerkin operators where a one-lane chain is latency-bound.
         Which family applies is a rule on the matrix; coarse_format='exact' keeps every
         operator in the exact family. fine_format='autotune' times the family's kernels on each
-        operator once and keeps the fastest (self.tuning); any other value forces that format."""
+        operator once and keeps the fastest (self.tuning); any other value forces that format.
+        first_level: the global index of self.levels[0] (a hierarchy that continues another one,
+        e.g. the replicated tail of the distributed setup: the family rule uses the global
+        level index)."""
         if coarse_format not in ("auto", "exact", "vector"):
             raise ValueError(f"coarse_format must be 'auto' or 'exact', got {coarse_format!r}")
         vec_min_row = self.VEC_MIN_MEAN_ROW if vec_min_row is None else vec_min_row
@@ -350,7 +354,7 @@ class Hierarchy:
         for i, L in enumerate(self.levels):
             row = {}
             for name, M in (("A", L.A), ("P", L.P), ("R", L.R)):
-                if (i > 0 and coarse_format != "exact" and M.shape[0] <= (1 << 20)
+                if (i + first_level > 0 and coarse_format != "exact" and M.shape[0] <= (1 << 20)
                         and M.nnz >= vec_min_row * M.shape[0]):
                     cands = list(self.VECTOR_CANDIDATES)
                 else:
