@@ -224,6 +224,10 @@ def main():
     ap.add_argument("--dist-min-rows", type=int, default=50000,
                     help="distributed run: row-partition every level with at least this many "
                          "rows (the rest are replicated on each GPU)")
+    ap.add_argument("--dist-setup", action="store_true",
+                    help="distributed run: build the partitioned levels with the distributed "
+                         "setup (mlamg.dsetup: each rank its rows; SURVEY.md §8(e)) instead of "
+                         "replicating the whole hierarchy on every rank")
     ap.add_argument("--overlap-min-rows", type=int, default=2_000_000,
                     help="distributed run: split local operators of at least this many rows so "
                          "their halo exchange overlaps the interior rows (-1: never)")
@@ -625,7 +629,7 @@ def run_distributed(args, world, rank, local_rank):
         out, H, x0, teardown = distributed.bench_main(args, world, rank, local_rank, METRIC,
                                                       HBM_PEAK_GBPS, phases=ph)
         if rank == 0:
-            if not args.no_cpu_baseline:
+            if not args.no_cpu_baseline and H is not None:
                 # rank 0 only, on the same (replicated) hierarchy; the others wait in teardown
                 n = x0.shape[0]
                 v, dtc, hcpu = cpu_baseline(H, np.zeros(n), x0, args.cpu_cycles)

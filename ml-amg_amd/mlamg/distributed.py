@@ -695,33 +695,71 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak, phases=None):
     A = problems.poisson_3d_7pt(n1)
     n = A.shape[0]
     t0 = time.perf_counter()
-    H = Hierarchy.build(A, alpha=args.alpha, strength_mode="invabs", max_coarse=args.max_coarse,
-                        aggregation=getattr(args, "aggregation", "bellman_ford"),
-                        coarse_order=getattr(args, "coarse_order", "sorted"), finalize=False)
-    ph.enter("sync_formats")
-    finalize_replicated(H, world, rank)
-    setup_s = time.perf_counter() - t0
-    comm = Comm(world, rank, phases=ph)
-    cinfo = comm.info()
-    ph.enter("partition")
-    t1 = time.perf_counter()
     omr = getattr(args, "overlap_min_rows", 2_000_000)
-    D = DistributedHierarchy(H, comm, min_rows=args.dist_min_rows, A_host=A,
-                             overlap_min_rows=None if omr < 0 else omr)
+    aggregation = getattr(args, "aggregation", "bellman_ford")
+    dist_setup = bool(getattr(args, "dist_setup", False))
+    H = None
+    if dist_setup:
+        # SURVEY.md §8(e) setup: each rank builds its rows of the partitioned levels
+        # (mlamg.dsetup); only the tail below them is replicated
+        from . import dsetup
+        scomm = dsetup.setup_comm(world)
+        S = dsetup.build_distributed(
+            dsetup.split_rows(A, world, rank), n, scomm, alpha=args.alpha,
+            strength_mode="invabs", aggregation=aggregation,
+            A0_global=A if aggregation == "reference" else None, max_coarse=args.max_coarse,
+            min_rows=args.dist_min_rows)
+        setup_s = time.perf_counter() - t0
+        log("distributed setup phases (s, rank 0): " + json.dumps(S.times))
+        comm = Comm(world, rank, phases=ph)
+        cinfo = comm.info()
+        ph.enter("partition")
+        t1 = time.perf_counter()
+        D = DistributedHierarchy.from_setup(S, comm, overlap_min_rows=None if omr < 0 else omr)
+        n_levels = len(S.parts) + S.tail.n_levels
+    else:
+        H = Hierarchy.build(A, alpha=args.alpha, strength_mode="invabs",
+                            max_coarse=args.max_coarse, aggregation=aggregation,
+                            coarse_order=getattr(args, "coarse_order", "sorted"),
+                            finalize=False)
+        ph.enter("sync_formats")
+        finalize_replicated(H, world, rank)
+        setup_s = time.perf_counter() - t0
+        comm = Comm(world, rank, phases=ph)
+        cinfo = comm.info()
+        ph.enter("partition")
+        t1 = time.perf_counter()
+        D = DistributedHierarchy(H, comm, min_rows=args.dist_min_rows, A_host=A,
+                                 overlap_min_rows=None if omr < 0 else omr)
+        n_levels = H.n_levels
     part_s = time.perf_counter() - t1
     log("partition phases (s): " + json.dumps({k: round(v, 3) for k, v in D.setup_times.items()}))
-    log(f"setup {setup_s:.1f}s (replicated), partition+upload {part_s:.1f}s; {D.K} of "
-        f"{len(H.levels)} levels partitioned; rank rows {D.lo}..{D.hi}; ghosts (x, r, p) per "
-        f"level {D.ghosts}; communicator {cinfo}")
+    log(f"setup {setup_s:.1f}s ({'distributed' if dist_setup else 'replicated'}), "
+        f"partition+upload {part_s:.1f}s; {D.K} of {n_levels} levels partitioned; rank rows "
+        f"{D.lo}..{D.hi}; ghosts (x, r, p) per level {D.ghosts}; communicator {cinfo}")
     ph.enter("verify")
     x0 = np.random.RandomState(0).randn(n)
     x0 /= np.linalg.norm(x0)
     b_own = torch.zeros(D.n_own, dtype=torch.float64, device="cuda")
-    # correctness: the distributed iterate equals the single-GPU iterate (replicated here)
     ncheck = 5
-    b_full = torch.zeros(n, dtype=torch.float64, device="cuda")
-    x_full = torch.as_tensor(x0).cuda()
-    h_single = H.cycle(b_full, x_full, ncheck, use_graph=True)
+    if dist_setup:
+        # no replicated hierarchy to compare with: the timed path must reproduce the eager,
+        # overlap-free cycle of the same distributed hierarchy bit for bit (the setup itself is
+        # bitwise the replicated build given the same lambda_max: tests/test_gpu_dsetup.py)
+        D.set_cycle_graph(False)
+        D.set_overlap(False)
+        x_ref = D.new_x(torch.as_tensor(x0[D.lo:D.hi]))
+        h_single = D.cycle(b_own, x_ref, ncheck)
+        x_ref_own = x_ref[: D.n_own].clone()
+        D.set_overlap(True)
+        ref_name = "eager distributed"
+    else:
+        # correctness: the distributed iterate equals the single-GPU iterate (replicated here)
+        b_full = torch.zeros(n, dtype=torch.float64, device="cuda")
+        x_full = torch.as_tensor(x0).cuda()
+        h_single = H.cycle(b_full, x_full, ncheck, use_graph=True)
+        x_ref_own = x_full[D.lo:D.hi]
+        ref_name = "single-GPU"
 
     def check():
         x_ext = D.new_x(torch.as_tensor(x0[D.lo:D.hi]))
@@ -730,13 +768,13 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak, phases=None):
         except _lib.MlamgError as e:
             log(f"distributed cycle failed: {e}")
             h_dist = np.full(ncheck, np.nan)
-        same_x = bool(torch.equal(x_ext[: D.n_own], x_full[D.lo:D.hi]))
+        same_x = bool(torch.equal(x_ext[: D.n_own], x_ref_own))
         same_h = bool(len(h_dist) == len(h_single)
                       and np.allclose(h_dist, h_single, rtol=1e-10, atol=0))
         ok = torch.tensor([1.0 if (same_x and same_h) else 0.0])
         if world > 1:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        log(f"distributed vs single-GPU after {ncheck} cycles: x bitwise "
+        log(f"distributed vs {ref_name} after {ncheck} cycles: x bitwise "
             f"{same_x}, history {same_h} ({h_dist[-1]:.6e} vs {h_single[-1]:.6e})")
         return bool(ok.item() == 1.0)
 
@@ -745,7 +783,7 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak, phases=None):
     D.set_cycle_graph(graph_on)
     graph_on, overlap_on = verify_paths(check, D, graph_on, overlap_on)
     ok_all = True
-    del x_full, b_full
+    x_ref_own = None
     # timing
     ph.enter("warmup")
     x_ext = D.new_x(torch.as_tensor(x0[D.lo:D.hi]))
@@ -805,13 +843,14 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak, phases=None):
             "config": {
                 "workload": f"C4: 3D 7-point Laplace {n1}^3 ({n} DoF), SA-AMG V(1,1) weighted "
                             f"Jacobi, {D.K} finest levels row-split over {world} GPUs + RCCL "
-                            f"halos, {H.n_levels - D.K} coarser levels replicated; aggregation "
-                            f"{getattr(H, 'aggregation', 'bellman_ford')} (coarse order "
-                            f"{getattr(H, 'coarse_order', 'sorted')})",
-                "aggregation": getattr(H, "aggregation", "bellman_ford"),
+                            f"halos, {n_levels - D.K} coarser levels replicated; aggregation "
+                            f"{aggregation} (coarse order sorted); setup "
+                            f"{'distributed' if dist_setup else 'replicated'}",
+                "aggregation": aggregation,
+                "setup": "distributed" if dist_setup else "replicated",
                 "partitioned_levels": D.K,
                 "overlap_splits": [(s["level"], s["op"]) for s in D.splits] if overlap_on else [],
-                "n": n, "levels": H.n_levels, "parallelism": f"rowsplit{world}",
+                "n": n, "levels": n_levels, "parallelism": f"rowsplit{world}",
                 "dist_matches_single_gpu": bool(ok_all),
                 "cycle_graph": graph_on,
                 "rccl_nranks": sorted({r["rccl_nranks"] for r in per_rank}),
@@ -835,9 +874,11 @@ def bench_main(args, world, rank, local_rank, metric, hbm_peak, phases=None):
                 "warm_avg_launch_us": slow["warm_us"],
             },
             "per_rank_spmv": per_rank,
-            "setup_s": {"replicated_build": round(setup_s, 3), "partition": round(part_s, 3),
+            "setup_s": {("distributed_build" if dist_setup else "replicated_build"):
+                        round(setup_s, 3), "partition": round(part_s, 3),
                         "partition_phases_rank0": {k: round(v, 3)
-                                                   for k, v in D.setup_times.items()}},
+                                                   for k, v in D.setup_times.items()},
+                        **({"distributed_phases_rank0": S.times} if dist_setup else {})},
         }
     ph.enter("report")
 

@@ -84,13 +84,19 @@ class ThreadComm:
         self.g = group
         self.world, self.rank = group.world, rank
         self.device = device if device is not None else _default_device()
+        self.busy_s = 0.0  # time this rank held the device (its own work, without the waits)
+        self._t = time.perf_counter()
 
     def _sync(self):
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        self.busy_s += time.perf_counter() - self._t
         self.g.lock.release()
         try:
             self.g.barrier.wait()
         finally:
             self.g.lock.acquire()
+            self._t = time.perf_counter()
 
     def allgather_obj(self, obj):
         self.g.box[("ag", self.rank)] = obj
@@ -138,7 +144,11 @@ def run_threads(world, fn, device=None):
             torch.cuda.set_device(dev)
         g.lock.acquire()
         try:
-            out[r] = fn(ThreadComm(g, r, device))
+            comm = ThreadComm(g, r, device)
+            out[r] = fn(comm)
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            comm.busy_s += time.perf_counter() - comm._t
         except BaseException as e:  # noqa: BLE001 — reported to the caller below
             errs.append((r, e))
             g.barrier.abort()  # peers blocked in a collective raise BrokenBarrierError
@@ -193,6 +203,27 @@ class TorchComm:
             r.wait()
         return {q: (bufs[("r", q)].to(dev) if cnt else torch.empty(0, dtype=dt, device=dev))
                 for q, (cnt, dt) in recvs.items()}
+
+
+class SoloComm:
+    """World 1 (no process group needed)."""
+
+    world, rank = 1, 0
+
+    def __init__(self, device=None):
+        self.device = device if device is not None else _default_device()
+
+    def allgather_obj(self, obj):
+        return [obj]
+
+    def exchange(self, sends, recvs):
+        return {q: (sends[q] if cnt else torch.empty(0, dtype=dt, device=self.device))
+                for q, (cnt, dt) in recvs.items()}
+
+
+def setup_comm(world):
+    """The setup transport of a torch.distributed job (SoloComm at world 1)."""
+    return TorchComm() if world > 1 else SoloComm()
 
 
 def _any(comm, flag):
@@ -713,5 +744,5 @@ def split_rows(A, world, rank, device=None):
     return TCSR.from_scipy(A[lo:hi], device=device or _device())
 
 
-__all__ = ["ThreadComm", "TorchComm", "run_threads", "build_distributed", "DistSetup", "DeviceBF",
+__all__ = ["ThreadComm", "TorchComm", "SoloComm", "setup_comm", "run_threads", "build_distributed", "DistSetup", "DeviceBF",
            "bellman_ford_distributed", "lambda_max_distributed", "split_rows"]

@@ -226,3 +226,89 @@ def test_dsetup_refuses_bad_input(prob):
     with pytest.raises(ValueError):
         dsetup.run_threads(2, lambda c: dsetup.build_distributed(
             dsetup.split_rows(A, 1, 0), n, c))  # rows of a world-1 split at world 2
+
+
+def _mp_worker(rank, world, port, q):
+    """One process of a gloo job on the shared GPU: the distributed setup over TorchComm (host
+    copies through gloo), reporting digests of its maps."""
+    import os
+    import hashlib
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from mlamg import dsetup, problems
+        from mlamg.hierarchy import Hierarchy
+        A = problems.poisson_3d_7pt(24)
+        n = A.shape[0]
+        # the single-GPU lambda_max values, so that the maps compare bitwise (the distributed
+        # Lanczos alone is held to 1e-13 below and in test_distributed_lanczos_and_cycle)
+        lams = [L.lam for L in Hierarchy.build(A, alpha=0.1, max_coarse=100).levels]
+        comm = dsetup.setup_comm(world)
+        S = dsetup.build_distributed(dsetup.split_rows(A, world, rank), n, comm, alpha=0.1,
+                                     max_coarse=100, min_rows=0, lams=lams)
+        lam_d = [dsetup.lambda_max_distributed(
+            dsetup._gs_csr(torch.arange(d["lo"], d["hi"], device="cuda"), A_own, d["n"],
+                           d["n"]),
+            dsetup.GHalo(comm, dsetup._ghosts(A_own, d["lo"], d["hi"]), d["ranges"]),
+            d["lo"], d["hi"], comm)[0]
+            for d, (A_own, _) in zip(S.parts, S.own_rows)]
+        dig = []
+        for d in S.parts:
+            h = hashlib.sha256()
+            for key in ("A_loc", "R_own", "P_loc"):
+                T = d[key]
+                for t in (T.crow.to(torch.int64), T.col.to(torch.int64), T.val):
+                    h.update(t.cpu().numpy().tobytes())
+            dig.append(h.hexdigest())
+        q.put((rank, dig, lam_d, None))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 — reported to the parent
+        q.put((rank, None, None, repr(e)))
+
+
+def test_dsetup_torch_comm_gloo_processes():
+    """World 2 as two processes on the one GPU over torch.distributed (gloo): the same maps as
+    the thread-transport run and the replicated build."""
+    import hashlib
+    import socket
+    import torch
+    import torch.multiprocessing as mp
+    from mlamg import problems
+    from mlamg.hierarchy import Hierarchy
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_mp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(2):
+        r, dig, lams, err = q.get(timeout=240)
+        assert err is None, f"rank {r}: {err}"
+        got[r] = (dig, lams)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    A = problems.poisson_3d_7pt(24)
+    H = Hierarchy.build(A, alpha=0.1, max_coarse=100)
+    K = len(got[0][0])
+    for r in range(2):
+        ref = _replicated_maps(H, K, 2, r)
+        for l, e in enumerate(ref):
+            h = hashlib.sha256()
+            for key in ("A_loc", "R_own", "P_loc"):
+                T = e[key]
+                for t in (T.crow.to(torch.int64), T.col.to(torch.int64), T.val):
+                    h.update(t.cpu().numpy().tobytes())
+            assert got[r][0][l] == h.hexdigest(), f"rank {r} level {l}"
+        for l, lam in enumerate(got[r][1]):
+            assert abs(lam - H.levels[l].lam) <= 1e-13 * abs(H.levels[l].lam)
