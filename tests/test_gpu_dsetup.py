@@ -312,3 +312,45 @@ def test_dsetup_torch_comm_gloo_processes():
             assert got[r][0][l] == h.hexdigest(), f"rank {r} level {l}"
         for l, lam in enumerate(got[r][1]):
             assert abs(lam - H.levels[l].lam) <= 1e-13 * abs(H.levels[l].lam)
+
+
+def test_dsetup_c4_world8_bench_configuration():
+    """The bench's C4 configuration (216^3, reference aggregation, max_coarse 2000, levels of
+    >= 50,000 rows partitioned) at world 8: every rank's maps, labels and Jacobi weights are the
+    replicated build's, bitwise (single-GPU lambda_max supplied); the distributed Lanczos gives
+    the same lambda_max to 1e-13 on every partitioned level."""
+    import torch
+    from mlamg import problems
+    from mlamg.hierarchy import Hierarchy
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    A = problems.poisson_3d_7pt(216)
+    kw = dict(alpha=0.1, max_coarse=2000, aggregation="reference")
+    H = Hierarchy.build(A, coarse_order="sorted", **kw)
+    world = 8
+    Ss = _setups(A, world, min_rows=50000, A0_global=A, lams=[L.lam for L in H.levels], **kw)
+    K = len(Ss[0].parts)
+    assert K == 3
+    for r in (0, 3, 7):  # first, interior and last slab (the maps of all 8 cost ~2 s each)
+        ref = _replicated_maps(H, K, world, r)
+        for l, (d, e) in enumerate(zip(Ss[r].parts, ref)):
+            tag = f"C4 world 8 rank {r} level {l}"
+            for key in ("A_loc", "R_own", "P_loc"):
+                _tcsr_equal(d[key], e[key], f"{tag}: {key}")
+            for key in ("halo_x", "halo_r", "halo_p"):
+                _halo_equal(d[key], e[key], f"{tag}: {key}")
+            lo, hi = d["lo"], d["hi"]
+            assert torch.equal(Ss[r].dinv[l].cpu(), H.levels[l].dinv[lo:hi].cpu()), tag
+    del Ss
+    torch.cuda.empty_cache()
+    # the distributed Lanczos on the same operators, world 8
+    from mlamg import dsetup
+
+    def lam_fn(comm):
+        S = dsetup.build_distributed(dsetup.split_rows(A, world, comm.rank), A.shape[0], comm,
+                                     min_rows=50000, A0_global=A, **kw)
+        return S.lams
+    lams = dsetup.run_threads(world, lam_fn)
+    for l in range(K):
+        assert all(x[l] == lams[0][l] for x in lams)
+        assert abs(lams[0][l] - H.levels[l].lam) <= 1e-13 * abs(H.levels[l].lam)
