@@ -28,6 +28,10 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--min-rows", default="50000", help="comma list of dist_min_rows values")
     ap.add_argument("--overlap", default="1", help="comma list: halo/interior overlap off (0) / on (1)")
+    ap.add_argument("--overlap-min-rows", default="2000000",
+                    help="comma list of DistributedHierarchy overlap_min_rows values (-1: none)")
+    ap.add_argument("--ranks", default="", help="comma list of ranks (default: first, middle, "
+                                                "last)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     A = problems.poisson_3d_7pt(a.n)
@@ -45,11 +49,15 @@ def main():
     single = (time.perf_counter() - t0) / a.steps
     out = {"n": n, "single_gpu_ms_per_cycle": round(single * 1e3, 4), "ranks": []}
     print(json.dumps(out), flush=True)
-    for w, mr in [(w, mr) for w in map(int, a.worlds.split(","))
-                  for mr in map(int, a.min_rows.split(","))]:
-        for r in sorted({0, w // 2, w - 1}):
+    for w, mr, omr in [(w, mr, omr) for w in map(int, a.worlds.split(","))
+                       for mr in map(int, a.min_rows.split(","))
+                       for omr in map(int, a.overlap_min_rows.split(","))]:
+        ranks = ([int(x) for x in a.ranks.split(",") if int(x) < w] if a.ranks
+                 else sorted({0, w // 2, w - 1}))
+        for r in ranks:
             c = NullComm(w, r)
-            D = DistributedHierarchy(H, c, min_rows=mr, A_host=A)
+            D = DistributedHierarchy(H, c, min_rows=mr, A_host=A,
+                                     overlap_min_rows=None if omr < 0 else omr)
             for ov in map(int, a.overlap.split(",")):
                 D.set_overlap(ov)
                 D.set_cycle_graph(True)
@@ -61,7 +69,8 @@ def main():
                 D.cycle(b, x, a.steps, history=False)
                 torch.cuda.synchronize()
                 t = (time.perf_counter() - t0) / a.steps
-                row = {"world": w, "rank": r, "min_rows": mr, "K": D.K, "rows": D.n_own,
+                row = {"world": w, "rank": r, "min_rows": mr, "overlap_min_rows": omr,
+                       "K": D.K, "rows": D.n_own,
                        "overlap": ov, "splits": [(s["level"], s["op"]) for s in D.splits],
                        "compute_ms_per_cycle": round(t * 1e3, 4),
                        "compute_bound_cycles_per_s": round(1.0 / t, 1),
