@@ -122,6 +122,12 @@ struct RpUni {
                                                        // 2 offset +1, 3 global (far)
   double v0[kRpUniMax] = {0, 0, 0, 0, 0, 0, 0, 0};     // row 2i's value at each slot
   double v1[kRpUniMax] = {0, 0, 0, 0, 0, 0, 0, 0};     // row 2i+1's
+  // far slot t (in slot order) reads x at pair offset alt_off[t] instead of its own offset for
+  // the pairs [alt_lo[t], alt_hi[t]) — a row-partitioned slab's ghost plane (its x_ext position
+  // is not the plane's global offset; build_rowpat). Empty range: none.
+  int32_t alt_off[kRpUniFar] = {0, 0};
+  int32_t alt_lo[kRpUniFar] = {0, 0};
+  int32_t alt_hi[kRpUniFar] = {0, 0};
 };
 
 // Tolerance arguments: tol >= 0 arms the device stop flag with ||.|| <= tol (the reference's

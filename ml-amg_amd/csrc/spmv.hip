@@ -778,12 +778,17 @@ void k_rowpat_uni(
   }
   constexpr int NF = LY == 1 || LY == 3 ? 2 : (LY == 2 ? 0 : kRpUniFar);
   constexpr int NFR = NF > 0 ? NF : 1;
+  // far slot t's offset for pair p (an alternate one on the pairs [alt_lo, alt_hi))
+  auto far_off = [&](int t, int64_t p) {
+    return p >= U.alt_lo[t] && p < U.alt_hi[t] ? U.alt_off[t] : fo[t];
+  };
   // chunk 0's id and far operands, then the window: all loads before the first LDS store
   int pcur = (MLAMG_UNI_DBG & 2) ? 13 : pid[2 * pa < n_rows ? pa : 0];
   dbl2 fcur[NFR];
 #pragma unroll
   for (int t = 0; t < NF; ++t)
-    fcur[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0} : uni_x16<OP>(x, 2 * pa + fo[t], n_cols, ep);
+    fcur[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0}
+                                   : uni_x16<OP>(x, 2 * pa + far_off(t, pa), n_cols, ep);
   // EPF: the epilogue's row operands (b, ...) of chunk 0 go out here too, and chunk c + 1's
   // with its id and far operands, so no chunk waits for its own epilogue loads
   constexpr bool EPF = MLAMG_UNI_EPF == 1 || (MLAMG_UNI_EPF == 2 && NORM);
@@ -829,7 +834,8 @@ void k_rowpat_uni(
     dbl2 fnext[NFR];
 #pragma unroll
     for (int t = 0; t < NF; ++t)
-      fnext[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0} : uni_x16<OP>(x, 2 * prn + fo[t], n_cols, ep);
+      fnext[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0}
+                                     : uni_x16<OP>(x, 2 * prn + far_off(t, prn), n_cols, ep);
     const int pl = c * kThreads + (int)threadIdx.x + hw;  // this pair's window slot
     const dbl2 xc = win[pl];
     const dbl2 xl = win[pl - 1];
@@ -3277,36 +3283,38 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
     }
     // uniform form (k_rowpat_uni): every entry one of <= kRpUniMax offsets with one value per
     // (offset, row parity), rows in ascending column order (then each row sums in slot order)
-    {
-      const char* ev = std::getenv("MLAMG_RP_UNI");
-      bool ok = all_sorted && !(ev && ev[0] == '0') && n_pat <= 255;
+    const char* uni_ev = std::getenv("MLAMG_RP_UNI");
+    auto try_uni = [&](const std::vector<std::vector<Ent>>& P, bool sorted, RpUni& u,
+                       std::vector<uint16_t>& msk) {
+      u = RpUni{};
+      bool ok = sorted && !(uni_ev && uni_ev[0] == '0') && n_pat <= 255;
       std::vector<int32_t> offs;
-      for (auto& pe : pent)
+      for (auto& pe : P)
         for (auto& en : pe)
           if (en.fl & 3) offs.push_back(en.off);
       std::sort(offs.begin(), offs.end());
       offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
       ok = ok && !offs.empty() && offs.size() <= (size_t)kRpUniMax;
       bool set0[kRpUniMax] = {}, set1[kRpUniMax] = {};
-      hmsk.assign(pent.size(), 0);
-      for (size_t k = 0; ok && k < pent.size(); ++k)
-        for (auto& en : pent[k]) {
+      msk.assign(P.size(), 0);
+      for (size_t k = 0; ok && k < P.size(); ++k)
+        for (auto& en : P[k]) {
           if (!(en.fl & 3)) continue;
           const int q = (int)(std::lower_bound(offs.begin(), offs.end(), en.off) - offs.begin());
           auto same = [](double a, double b) {
             return __builtin_bit_cast(uint64_t, a) == __builtin_bit_cast(uint64_t, b);
           };
           if (en.fl & 1) {
-            if (!set0[q]) uni.v0[q] = en.v0;
-            ok = ok && same(uni.v0[q], en.v0);
+            if (!set0[q]) u.v0[q] = en.v0;
+            ok = ok && same(u.v0[q], en.v0);
             set0[q] = true;
-            hmsk[k] |= (uint16_t)(1u << q);
+            msk[k] |= (uint16_t)(1u << q);
           }
           if (en.fl & 2) {
-            if (!set1[q]) uni.v1[q] = en.v1;
-            ok = ok && same(uni.v1[q], en.v1);
+            if (!set1[q]) u.v1[q] = en.v1;
+            ok = ok && same(u.v1[q], en.v1);
             set1[q] = true;
-            hmsk[k] |= (uint16_t)(1u << (q + 8));
+            msk[k] |= (uint16_t)(1u << (q + 8));
           }
         }
       int halo = 2, nfar = 0;
@@ -3319,16 +3327,16 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
         else kd = 3;
         if (kd == 0) halo = std::max(halo, std::abs(o));
         if (kd == 3) ++nfar;
-        uni.off[q] = o;
-        uni.kind[q] = kd;
+        u.off[q] = o;
+        u.kind[q] = kd;
       }
       ok = ok && nfar <= kRpUniFar && A->n_cols >= 2;
-      uni.k = ok ? (int32_t)offs.size() : 0;
+      u.k = ok ? (int32_t)offs.size() : 0;
       auto kinds_are = [&](std::initializer_list<int> ks) {
-        if ((size_t)uni.k != ks.size()) return false;
+        if ((size_t)u.k != ks.size()) return false;
         int q = 0;
         for (int kd : ks)
-          if (uni.kind[q++] != kd) return false;
+          if (u.kind[q++] != kd) return false;
         return true;
       };
       {
@@ -3337,19 +3345,117 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
         // MLAMG_RPU_CH = 1 | 2 | 4 is the A/B knob
         const char* ec = std::getenv("MLAMG_RPU_CH");
         const int chv = ec ? std::atoi(ec) : 2;
-        uni.ch = (chv == 1 || chv == 4) ? chv : 2;
+        u.ch = (chv == 1 || chv == 4) ? chv : 2;
         const char* ep = std::getenv("MLAMG_RPU_LDSPAD");  // A/B knob: caps workgroups per CU
         A->rp_lds_pad = ep ? std::max(0, std::min(std::atoi(ep), 96 << 10)) : 0;
       }
-      uni.layout = kinds_are({3, 0, 1, 0, 2, 0, 3}) ? 1
-                   : kinds_are({0, 1, 0, 2, 0})     ? 2
-                   : kinds_are({3, 1, 0, 2, 3})     ? 3
-                                                    : 0;
-      uni.halo = ok ? halo : 0;
+      u.layout = kinds_are({3, 0, 1, 0, 2, 0, 3}) ? 1
+                 : kinds_are({0, 1, 0, 2, 0})     ? 2
+                 : kinds_are({3, 1, 0, 2, 3})     ? 3
+                                                  : 0;
+      u.halo = ok ? halo : 0;
       if (!ok) {
+        u = RpUni{};
+        msk.clear();
+      }
+      return ok;
+    };
+    // alternate far offsets (a row-partitioned slab, csrc/comm.hip's x_ext = [owned | ghosts]):
+    // a ghost plane's entries reach x at an offset of their own (+n_own for the plane below,
+    // +2F for the plane above when the plane below precedes it), unsorted in the row where the
+    // plane below comes first. An extra far offset e stands for one of the two far offsets
+    // nearest zero (s) when, in every pattern holding e, s is absent and the rows with e read
+    // as s are in ascending order; the kernel then loads slot s from offset e on the pairs that
+    // use e (a contiguous range, checked after the pairs are assigned below).
+    std::vector<std::pair<int32_t, int32_t>> uni_alts;  // (e, s)
+    if (!try_uni(pent, all_sorted, uni, hmsk) && !(uni_ev && uni_ev[0] == '0')) {
+      std::vector<int32_t> far;
+      for (auto& pe : pent)
+        for (auto& en : pe)
+          if ((en.fl & 3) && en.off != -1 && en.off != 1 &&
+              ((en.off & 1) || std::abs(en.off) > kRpUniMaxHalo))
+            far.push_back(en.off);
+      std::sort(far.begin(), far.end());
+      far.erase(std::unique(far.begin(), far.end()), far.end());
+      int32_t fneg = 0, fpos = 0;
+      for (int32_t o : far) {
+        if (o < 0) fneg = o;  // the largest negative
+        if (o > 0 && fpos == 0) fpos = o;  // the smallest positive
+      }
+      auto row_sorted = [](const std::vector<Ent>& pe, int bit) {
+        bool first = true;
+        int32_t prev = 0;
+        for (auto& en : pe) {
+          if (!(en.fl & bit)) continue;
+          if (!first && en.off <= prev) return false;
+          prev = en.off;
+          first = false;
+        }
+        return true;
+      };
+      std::vector<std::vector<Ent>> pv = pent;
+      bool okv = fneg != 0 && fpos != 0;
+      for (int32_t e : far) {
+        if (!okv || e == fneg || e == fpos) continue;
+        int32_t pick = 0;
+        for (int32_t s_cand : {fneg, fpos}) {
+          bool good = true, used = false;
+          for (auto& pe : pent) {
+            bool has_e = false, has_s = false;
+            for (auto& en : pe) {
+              has_e = has_e || ((en.fl & 3) && en.off == e);
+              has_s = has_s || ((en.fl & 3) && en.off == s_cand);
+            }
+            if (!has_e) continue;
+            used = true;
+            if (has_s) {
+              good = false;
+              break;
+            }
+            std::vector<Ent> t = pe;
+            for (auto& en : t)
+              if (en.off == e) en.off = s_cand;
+            good = good && row_sorted(t, 1) && row_sorted(t, 2);
+          }
+          if (good && used) {
+            okv = pick == 0;  // exactly one candidate
+            pick = s_cand;
+          }
+        }
+        okv = okv && pick != 0;
+        if (!okv) break;
+        for (auto& a : uni_alts) okv = okv && a.second != pick;  // one alternate per slot
+        uni_alts.push_back({e, pick});
+        for (auto& pe : pv)
+          for (auto& en : pe)
+            if (en.off == e) en.off = pick;
+      }
+      bool sorted_v = okv && !uni_alts.empty();
+      for (auto& pe : pv) sorted_v = sorted_v && row_sorted(pe, 1) && row_sorted(pe, 2);
+      if (!sorted_v || !try_uni(pv, true, uni, hmsk)) {
         uni = RpUni{};
         hmsk.clear();
+        uni_alts.clear();
       }
+      // the alternates' far ordinals (slot order) and their offsets; ranges follow the assign
+      for (auto& a : uni_alts) {
+        int t = 0;
+        for (int q = 0; q < uni.k && uni.off[q] != a.second; ++q) t += uni.kind[q] == 3;
+        uni.alt_off[t] = a.first;
+      }
+    }
+    // patterns holding each alternate offset / its slot's own offset (pattern ids = pent order)
+    std::vector<std::vector<bool>> alt_has_e, alt_has_s;
+    for (auto& a : uni_alts) {
+      std::vector<bool> he(pent.size(), false), hs(pent.size(), false);
+      for (size_t k = 0; k < pent.size(); ++k)
+        for (auto& en : pent[k]) {
+          if (!(en.fl & 3)) continue;
+          if (en.off == a.first) he[k] = true;
+          if (en.off == a.second) hs[k] = true;
+        }
+      alt_has_e.push_back(he);
+      alt_has_s.push_back(hs);
     }
     // the kernel's step: the longest pattern when it fits one step of 5..8 entries, else 8;
     // every pattern is padded with null entries to whole steps
@@ -3473,6 +3579,31 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
       fail(MLAMG_EHIP, "assign");
     if (rc == MLAMG_OK && hc[0] != 0)
       fail(MLAMG_EUNSUPPORTED, "row-pair pattern hash collision");
+    // the alternates' pair ranges: the pairs whose pattern holds e must form one run in which no
+    // pair's pattern holds the slot's own offset (the kernel switches the slot's offset by pair
+    // range); otherwise no uniform form (the general row-pair kernel reads actual offsets)
+    if (rc == MLAMG_OK && !uni_alts.empty()) {
+      std::vector<uint8_t> hp((size_t)n_pairs);
+      bool okr = hipMemcpy(hp.data(), pid, (size_t)n_pairs, hipMemcpyDeviceToHost) == hipSuccess;
+      for (size_t a = 0; okr && a < uni_alts.size(); ++a) {
+        int64_t lo = -1, hi = -1;
+        for (int64_t i = 0; i < n_pairs; ++i)
+          if (alt_has_e[a][hp[i]]) {
+            if (lo < 0) lo = i;
+            hi = i + 1;
+          }
+        okr = lo >= 0;
+        for (int64_t i = lo; okr && i < hi; ++i) okr = !alt_has_s[a][hp[i]];
+        int t = 0;
+        for (int q = 0; q < uni.k && uni.off[q] != uni_alts[a].second; ++q) t += uni.kind[q] == 3;
+        uni.alt_lo[t] = (int32_t)lo;
+        uni.alt_hi[t] = (int32_t)hi;
+      }
+      if (!okr) {
+        uni = RpUni{};
+        hmsk.clear();
+      }
+    }
   }
   for (void* p : {(void*)tab, (void*)rep, (void*)counts, (void*)slot_pid})
     if (p) (void)hipFree(p);
@@ -3523,6 +3654,7 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
   // §13); MLAMG_RPM_CH (1 | 2 | 4) and MLAMG_RPM_SEG
   // (planes per segment; 0 = enough workgroups for two (CH 4) / four (CH 2) per CU) are A/B knobs
   if (uni.k == 7 && uni.layout == 1 && A->n_rows == A->n_cols && uni.off[6] > 0 &&
+      uni.alt_hi[0] == uni.alt_lo[0] && uni.alt_hi[1] == uni.alt_lo[1] &&
       uni.off[0] == -uni.off[6] && (uni.off[6] & 1) == 0 && uni.off[6] >= 2048 &&
       A->n_rows >= 3 * (int64_t)uni.off[6]) {
     const char* e0 = std::getenv("MLAMG_RPM");

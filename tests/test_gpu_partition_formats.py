@@ -129,3 +129,31 @@ def test_rowpat_rows_in_stored_not_ascending_order(oracle, seed):
     x = rs.randn(A.shape[1])
     y = M.matvec(torch.as_tensor(x).cuda()).cpu().numpy()
     assert np.array_equal(y, oracle.csr_matvec(M_host, x))
+
+
+@pytest.mark.parametrize("m,world", [(48, 3), (216, 8)])
+def test_slab_local_operators_take_uniform_form(m, world):
+    """Row-partitioned 3-D 7-point slabs: a middle or last rank's local operator reaches its
+    ghost planes at offsets of their own (+n_own below, +2F above), so the uniform row-pair form
+    takes them as alternate offsets of the two far slots on the first / last plane's pairs
+    (build_rowpat). Every rank's operator must take the uniform form (its format
+    bytes: x, y, one id byte per pair and the mask table) and reproduce the CSR-stream rows
+    bitwise."""
+    import torch
+    from mlamg import partition, problems
+    from mlamg.sparse import DeviceCSR
+    A = problems.poisson_3d_7pt(m)
+    ranges = partition.row_ranges(A.shape[0], world)
+    for rank in sorted({0, world // 2, world - 1}):
+        lo, hi = ranges[rank]
+        blk = A[lo:hi]
+        cols = np.unique(blk.indices)
+        ghosts = cols[(cols < lo) | (cols >= hi)]
+        loc = partition._remap(blk, lo, hi, ghosts)
+        M = DeviceCSR.from_scipy(loc, check=False).set_format("rowpat")
+        n, mc = loc.shape
+        uni_bytes = 8.0 * mc + 8.0 * n + float((n + 1) // 2) + 512.0
+        assert M.format_bytes() == uni_bytes, f"rank {rank}: not the uniform form"
+        R = DeviceCSR.from_scipy(loc, check=False).set_format("csr_stream")
+        x = torch.as_tensor(np.random.RandomState(rank).randn(mc)).cuda()
+        assert torch.equal(M.matvec(x), R.matvec(x)), f"rank {rank}"
