@@ -680,7 +680,9 @@ void k_rowpair(const uint8_t* __restrict__ pid,
 // zero (a branch join makes the compiler wait for every load in flight).
 // LY: slot layout (kinds in slot order; 0 even window offset, 1 offset -1, 2 offset +1, 3 far):
 // 1 = {3,0,1,0,2,0,3} (3-D 7-point), 2 = {0,1,0,2,0} (2-D 5-point, +-n staged),
-// 3 = {3,1,0,2,3} (2-D 5-point, +-n far), 0 = any (run-time kinds).
+// 3 = {3,1,0,2,3} (2-D 5-point, +-n far), 4 = layout 1 with alternate far offsets (a
+// row-partitioned slab's ghost planes, RpUni::alt_*), 0 = any (run-time kinds, alternates too).
+// Only layouts 0 and 4 compare pair indices against the alternate ranges.
 __device__ __forceinline__ dbl2 x16(const double* __restrict__ x, int64_t g, int64_t n) {
   const int64_t gc = g < 0 ? 0 : (g > n - 2 ? n - 2 : g);
   const dbl2 t = *reinterpret_cast<const dbl2u*>(x + gc);
@@ -719,11 +721,12 @@ __device__ __forceinline__ int uni_kind(const RpUni& U, int q) {
   if constexpr (LY == 1) return k1[q < 7 ? q : 0];
   if constexpr (LY == 2) return k2[q < 5 ? q : 0];
   if constexpr (LY == 3) return k3[q < 5 ? q : 0];
+  if constexpr (LY == 4) return k1[q < 7 ? q : 0];
   return U.kind[q];
 }
 template <int LY>
 __device__ __forceinline__ int uni_k(const RpUni& U) {
-  return LY == 1 ? 7 : (LY == 2 || LY == 3) ? 5 : U.k;
+  return LY == 1 || LY == 4 ? 7 : (LY == 2 || LY == 3) ? 5 : U.k;
 }
 
 #ifndef MLAMG_UNI_DBG
@@ -734,6 +737,9 @@ __device__ __forceinline__ int uni_k(const RpUni& U) {
 #endif                   // 66.7 -> 58.6 us; the other passes got slower: 51.8 -> 55.3 us)
 #ifndef MLAMG_UNI_WPE  // build-time A/B knob: minimum waves per SIMD for k_rowpat_uni (0: free)
 #define MLAMG_UNI_WPE 0
+#endif
+#ifndef MLAMG_UNI_PFA  // build-time A/B knob: every chunk's id and far operands issued before the
+#define MLAMG_UNI_PFA 0  // window staging (1), instead of one chunk ahead (0)
 #endif
 template <int OP, bool NORM, int CH, int LY>
 __global__ __launch_bounds__(kThreads)
@@ -761,34 +767,45 @@ void k_rowpat_uni(
   const int64_t p0 = lb * CH * kThreads;  // the workgroup's first pair
   const int64_t T0 = 2 * p0 - U.halo;     // its first window row (even)
   const int64_t pa = p0 + threadIdx.x;
-  // far offsets (slot order)
-  int fo[kRpUniFar];
+  // far offsets (slot order), as two scalars: an array here ends up in scratch memory once a
+  // select picks between its element and an alternate offset (the select becomes one of
+  // addresses; 8-12 B per lane, the C4 A_0 pass 45 -> 57 us cold)
+  int fo0 = 0, fo1 = 0;
   {
     int nf = 0;
 #pragma unroll
-    for (int t = 0; t < kRpUniFar; ++t) fo[t] = 0;
-#pragma unroll
     for (int q = 0; q < kRpUniMax; ++q)
       if (q < K && uni_kind<LY>(U, q) == 3) {
-#pragma unroll
-        for (int t = 0; t < kRpUniFar; ++t)
-          if (t == nf) fo[t] = U.off[q];
+        if (nf == 0) fo0 = U.off[q];
+        if (nf == 1) fo1 = U.off[q];
         ++nf;
       }
   }
-  constexpr int NF = LY == 1 || LY == 3 ? 2 : (LY == 2 ? 0 : kRpUniFar);
+  static_assert(kRpUniFar == 2, "far slots: fo0, fo1");
+  constexpr int NF = LY == 1 || LY == 3 || LY == 4 ? 2 : (LY == 2 ? 0 : kRpUniFar);
   constexpr int NFR = NF > 0 ? NF : 1;
+  constexpr bool ALT = LY == 0 || LY == 4;
   // far slot t's offset for pair p (an alternate one on the pairs [alt_lo, alt_hi))
-  auto far_off = [&](int t, int64_t p) {
-    return p >= U.alt_lo[t] && p < U.alt_hi[t] ? U.alt_off[t] : fo[t];
-  };
+#define MLAMG_FAR_OFF(t, p)                                                          \
+  ((ALT && (p) >= U.alt_lo[t] && (p) < U.alt_hi[t]) ? U.alt_off[t] : ((t) == 0 ? fo0 : fo1))
   // chunk 0's id and far operands, then the window: all loads before the first LDS store
-  int pcur = (MLAMG_UNI_DBG & 2) ? 13 : pid[2 * pa < n_rows ? pa : 0];
+  constexpr bool PFA = MLAMG_UNI_PFA != 0;
+  constexpr int CHA = PFA ? CH : 1;  // chunks whose id and far operands go out up front
+  int pall[CHA];
+  dbl2 fall[CHA][NFR];
+#pragma unroll
+  for (int c = 0; c < CHA; ++c) {
+    const int64_t pc = pa + (int64_t)c * kThreads;
+    pall[c] = (MLAMG_UNI_DBG & 2) ? 13 : pid[2 * pc < n_rows ? pc : 0];
+#pragma unroll
+    for (int t = 0; t < NF; ++t)
+      fall[c][t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0}
+                                        : uni_x16<OP>(x, 2 * pc + MLAMG_FAR_OFF(t, pc), n_cols, ep);
+  }
+  int pcur = pall[0];
   dbl2 fcur[NFR];
 #pragma unroll
-  for (int t = 0; t < NF; ++t)
-    fcur[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0}
-                                   : uni_x16<OP>(x, 2 * pa + far_off(t, pa), n_cols, ep);
+  for (int t = 0; t < NF; ++t) fcur[t] = fall[0][t];
   // EPF: the epilogue's row operands (b, ...) of chunk 0 go out here too, and chunk c + 1's
   // with its id and far operands, so no chunk waits for its own epilogue loads
   constexpr bool EPF = MLAMG_UNI_EPF == 1 || (MLAMG_UNI_EPF == 2 && NORM);
@@ -813,7 +830,11 @@ void k_rowpat_uni(
     for (int i = threadIdx.x; i < n_pat; i += kThreads) dt[i] = pat_dinv[i];
   __syncthreads();
   double sq = 0.0;
+#if MLAMG_UNI_PFA
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
   for (int c = 0; c < CH; ++c) {
     const int64_t pr = pa + (int64_t)c * kThreads;
     const bool ok0 = 2 * pr < n_rows;
@@ -830,12 +851,20 @@ void k_rowpat_uni(
       if (ok0) epi_load2<OP>(r, both, ep, u, w, tab_dinv, x_op);
     }
     // the next chunk's id and far operands, in flight while this one sums
-    const int pnext = (MLAMG_UNI_DBG & 2) ? 13 : pid[c + 1 < CH && 2 * prn < n_rows ? prn : 0];
+    int pnext = 0;
     dbl2 fnext[NFR];
+    if constexpr (PFA) {
+      const int cn = c + 1 < CHA ? c + 1 : 0;
+      pnext = pall[cn];
 #pragma unroll
-    for (int t = 0; t < NF; ++t)
-      fnext[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0}
-                                     : uni_x16<OP>(x, 2 * prn + far_off(t, prn), n_cols, ep);
+      for (int t = 0; t < NF; ++t) fnext[t] = fall[cn][t];
+    } else {
+      pnext = (MLAMG_UNI_DBG & 2) ? 13 : pid[c + 1 < CH && 2 * prn < n_rows ? prn : 0];
+#pragma unroll
+      for (int t = 0; t < NF; ++t)
+        fnext[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0}
+                                       : uni_x16<OP>(x, 2 * prn + MLAMG_FAR_OFF(t, prn), n_cols, ep);
+    }
     const int pl = c * kThreads + (int)threadIdx.x + hw;  // this pair's window slot
     const dbl2 xc = win[pl];
     const dbl2 xl = win[pl - 1];
@@ -898,6 +927,7 @@ void k_rowpat_uni(
       ep.partial[lb] = t;
     }
   }
+#undef MLAMG_FAR_OFF
 }
 
 // ---------------------------------------------------------------- plane-marching stencil form
@@ -2049,6 +2079,7 @@ static int launch_rowpat_uni(const mlamg_csr* A, const double* x, const Epi& ep,
     case 1: MLAMG_RPU(1); break;
     case 2: MLAMG_RPU(2); break;
     case 3: MLAMG_RPU(3); break;
+    case 4: MLAMG_RPU(4); break;
     default: MLAMG_RPU(0); break;
   }
 #undef MLAMG_RPU
@@ -3602,6 +3633,9 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
       if (!okr) {
         uni = RpUni{};
         hmsk.clear();
+      } else {
+        // the compile-time layouts without alternates never compare pair ranges
+        uni.layout = uni.layout == 1 ? 4 : 0;
       }
     }
   }
