@@ -738,9 +738,9 @@ __device__ __forceinline__ int uni_k(const RpUni& U) {
 #ifndef MLAMG_UNI_WPE  // build-time A/B knob: minimum waves per SIMD for k_rowpat_uni (0: free)
 #define MLAMG_UNI_WPE 0
 #endif
-#ifndef MLAMG_UNI_PFA  // build-time A/B knob: every chunk's id and far operands issued before the
-#define MLAMG_UNI_PFA 0  // window staging (1), instead of one chunk ahead (0)
-#endif
+#ifndef MLAMG_UNI_PFA  // build-time A/B knob: with CH <= 2 chunks, every chunk's id and far
+#define MLAMG_UNI_PFA 1  // operands issued before the window staging (1), not one chunk ahead (0):
+#endif                   // C4 A_0 cold 45.0 -> 43.0 us, resid+norm 64 -> 52 us
 template <int OP, bool NORM, int CH, int LY>
 __global__ __launch_bounds__(kThreads)
 __attribute__((amdgpu_waves_per_eu(MLAMG_UNI_WPE > 0 ? MLAMG_UNI_WPE : 1, 8)))
@@ -790,7 +790,7 @@ void k_rowpat_uni(
   ((ALT && (p) >= U.alt_lo[t] && (p) < U.alt_hi[t]) ? U.alt_off[t] : ((t) == 0 ? fo0 : fo1))
   // chunk 0's id and far operands, then the window: all loads before the first LDS store
   constexpr bool PFA = MLAMG_UNI_PFA != 0;
-  constexpr int CHA = PFA ? CH : 1;  // chunks whose id and far operands go out up front
+  constexpr int CHA = PFA && CH <= 2 ? CH : 1;  // chunks whose id and far operands go out first
   int pall[CHA];
   dbl2 fall[CHA][NFR];
 #pragma unroll
@@ -854,11 +854,14 @@ void k_rowpat_uni(
     int pnext = 0;
     dbl2 fnext[NFR];
     if constexpr (PFA) {
-      const int cn = c + 1 < CHA ? c + 1 : 0;
-      pnext = pall[cn];
+      if constexpr (CHA == CH) {
+        const int cn = c + 1 < CHA ? c + 1 : 0;
+        pnext = pall[cn];
 #pragma unroll
-      for (int t = 0; t < NF; ++t) fnext[t] = fall[cn][t];
-    } else {
+        for (int t = 0; t < NF; ++t) fnext[t] = fall[cn][t];
+      }
+    }
+    if constexpr (!PFA || CHA != CH) {
       pnext = (MLAMG_UNI_DBG & 2) ? 13 : pid[c + 1 < CH && 2 * prn < n_rows ? prn : 0];
 #pragma unroll
       for (int t = 0; t < NF; ++t)
