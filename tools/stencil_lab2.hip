@@ -32,6 +32,18 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
   return (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + i;
 }
 
+// xcd_block, then each XCD's contiguous range dealt to SUB fronts: the XCD's i-th dispatched
+// workgroup takes block k = i / SUB of sub-range i % SUB, so its resident workgroups cover SUB
+// narrow fronts instead of one wide one (bijective; the remainder blocks come last)
+__device__ __forceinline__ int64_t xcd_block_sub(int64_t b, int64_t nb, int sub) {
+  const int64_t q = nb >> 3, r = nb & 7, g = b & 7, i = b >> 3;
+  const int64_t s0 = g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q;
+  const int64_t len = g < r ? q + 1 : q;
+  const int64_t ql = len / sub;
+  if (i < ql * sub) return s0 + (i % sub) * ql + i / sub;
+  return s0 + i;
+}
+
 __global__ __launch_bounds__(256) void k_copy(const double* __restrict__ x, double* __restrict__ y,
                                               int64_t N) {
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -56,6 +68,15 @@ __device__ __forceinline__ dbl2 x16c(const double* __restrict__ x, int64_t g, in
 __device__ __forceinline__ dbl2 x16g(const double* __restrict__ x, int64_t g, int64_t n) {
   return (g >= 0 && g + 1 < n) ? *reinterpret_cast<const dbl2u*>(x + g) : dbl2{0.0, 0.0};
 }
+__device__ __forceinline__ dbl2 x16n(const double* __restrict__ x, int64_t g, int64_t n) {
+  if (g >= 0 && g + 1 < n) {
+    dbl2 t;
+    t.x = __builtin_nontemporal_load(x + g);
+    t.y = __builtin_nontemporal_load(x + g + 1);
+    return t;
+  }
+  return dbl2{0.0, 0.0};
+}
 
 template <int NT, int CH, bool PID, bool CL, int FAR = 3, int PF = 0, int ORD = 0>
 __global__ __launch_bounds__(NT) void k_tile(const double* __restrict__ x, double* __restrict__ y,
@@ -63,7 +84,10 @@ __global__ __launch_bounds__(NT) void k_tile(const double* __restrict__ x, doubl
                                              const uint16_t* __restrict__ pmsk, int n, int64_t N) {
   extern __shared__ dbl2 win[];
   __shared__ uint16_t msk[256];
-  const int64_t lb = ORD == 0 ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int64_t lb = (ORD == 0 || ORD > 200) ? xcd_block(blockIdx.x, gridDim.x)
+                     : ORD > 100               ? xcd_block_sub(blockIdx.x, gridDim.x, ORD - 100)
+                                               : blockIdx.x;
+  constexpr bool FNT = ORD == 201 || ORD == 203, WNT = ORD == 202 || ORD == 203, YNT = ORD == 204;
   const int H = (n + 1) & ~1;  // halo rows (even)
   const int hw = H / 2;        // halo pairs
   const int64_t P0 = lb * CH * NT;  // first pair
@@ -77,8 +101,8 @@ __global__ __launch_bounds__(NT) void k_tile(const double* __restrict__ x, doubl
   for (int c = 0; c < CH; ++c) {
     const int64_t p = P0 + c * NT + threadIdx.x;
     pc[c] = PID ? pid[2 * p < N ? p : 0] : 0;
-    zm[c] = (FAR & 1) ? ld(2 * p - n2) : dbl2{0.0, 0.0};
-    zp[c] = (FAR & 2) ? ld(2 * p + n2) : dbl2{0.0, 0.0};
+    zm[c] = (FAR & 1) ? (FNT ? x16n(x, 2 * p - n2, N) : ld(2 * p - n2)) : dbl2{0.0, 0.0};
+    zp[c] = (FAR & 2) ? (FNT ? x16n(x, 2 * p + n2, N) : ld(2 * p + n2)) : dbl2{0.0, 0.0};
   }
   if (PF > 0) {  // touch the x lines PF workgroups ahead of this one's +n^2 operands
     const int64_t g = 2 * (P0 + (int64_t)PF * CH * NT + threadIdx.x * CH) + n2;
@@ -92,7 +116,8 @@ __global__ __launch_bounds__(NT) void k_tile(const double* __restrict__ x, doubl
 #pragma unroll
   for (int q = 0; q < WQ; ++q) {
     const int i = threadIdx.x + q * NT;
-    wv[q] = ld(T0 + 2 * (int64_t)(i < nwin ? i : 0));
+    wv[q] = WNT ? x16n(x, T0 + 2 * (int64_t)(i < nwin ? i : 0), N)
+                : ld(T0 + 2 * (int64_t)(i < nwin ? i : 0));
   }
 #pragma unroll
   for (int q = 0; q < WQ; ++q) {
@@ -124,7 +149,10 @@ __global__ __launch_bounds__(NT) void k_tile(const double* __restrict__ x, doubl
     dbl2 o;
     o.x = s0;
     o.y = s1;
-    *reinterpret_cast<dbl2*>(y + r) = o;
+    if (YNT)
+      __builtin_nontemporal_store(o, reinterpret_cast<dbl2*>(y + r));
+    else
+      *reinterpret_cast<dbl2*>(y + r) = o;
   }
 }
 
@@ -301,16 +329,10 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_copy, dim3((unsigned)((N / 2 + 255) / 256)), dim3(256), 0, 0, x, y, N);
   }, 16.0 * N / 1e6, reps);
   run_tile<256, 2, false, false>(T, x, y, pid, pm, n, N, reps);
-  run_tile<256, 2, false, false, 0>(T, x, y, pid, pm, n, N, reps);
-  run_march2<256, 2, 2>(T, x, y, n, N, reps);
-  run_march2<256, 2, 4>(T, x, y, n, N, reps);
-  run_march2<256, 2, 6>(T, x, y, n, N, reps);
-  run_march2<256, 2, 8>(T, x, y, n, N, reps);
-  run_march2<256, 2, 12>(T, x, y, n, N, reps);
-  run_march2<256, 1, 4>(T, x, y, n, N, reps);
-  run_march2<256, 1, 8>(T, x, y, n, N, reps);
-  run_march2<256, 4, 4>(T, x, y, n, N, reps);
-  run_march2<512, 1, 4>(T, x, y, n, N, reps);
-  run_march2<512, 1, 8>(T, x, y, n, N, reps);
+  run_tile<256, 2, false, false, 3, 0, 201>(T, x, y, pid, pm, n, N, reps);
+  run_tile<256, 2, false, false, 3, 0, 202>(T, x, y, pid, pm, n, N, reps);
+  run_tile<256, 2, false, false, 3, 0, 203>(T, x, y, pid, pm, n, N, reps);
+  run_tile<256, 2, false, false, 3, 0, 204>(T, x, y, pid, pm, n, N, reps);
+  run_tile<256, 2, false, false>(T, x, y, pid, pm, n, N, reps);
   return 0;
 }
