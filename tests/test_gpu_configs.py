@@ -73,13 +73,15 @@ CONFIGS = ("c2_1024", "c3", "c3_r2", "c5_grid", "c5_mesh", "lap3d_grid", "aniso3
 MODES = (("bellman_ford", "seed"), ("reference", "sorted"))
 
 
-@pytest.mark.parametrize("mode", MODES, ids=lambda m: m[0])
-@pytest.mark.parametrize("name", CONFIGS)
+# C2 in reference mode is test_c2_reference_aggregation_parity (both coarse orders)
+CASES = [pytest.param(name, mode, id=f"{name}-{mode[0]}") for mode in MODES for name in CONFIGS
+         if not (mode[0] == "reference" and name == "c2_1024")]
+
+
+@pytest.mark.parametrize("name,mode", CASES)
 def test_config_hierarchy_and_cycle_parity(ml, oracle, torch_cuda, name, mode):
     torch = torch_cuda
     aggregation, coarse_order = mode
-    if aggregation == "reference" and name == "c2_1024":
-        pytest.skip("C2 in reference mode: test_c2_reference_aggregation_parity (both orders)")
     A = _matrix(name)
     n = A.shape[0]
     max_coarse = 500 if n < 100000 else 2000
