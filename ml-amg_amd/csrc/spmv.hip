@@ -706,11 +706,26 @@ __device__ __forceinline__ dbl2 t16(const int32_t* __restrict__ agg, const doubl
   o.y = g == gc ? t1 : (g == -1 ? t0 : 0.0);
   return o;
 }
+// x16 through a buffer resource with 32-bit index arithmetic (n * 8 < 2^31, checked where the
+// uniform form is built): no 64-bit address registers per load
+__device__ __forceinline__ dbl2 x16r(__amdgpu_buffer_rsrc_t rs, int g, int n) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const int gc = g < 0 ? 0 : (g > n - 2 ? n - 2 : g);
+  const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, gc * 8, 0, 0);
+  const double t0 = __builtin_bit_cast(double, ((uint64_t)t.y << 32) | t.x);
+  const double t1 = __builtin_bit_cast(double, ((uint64_t)t.w << 32) | t.z);
+  dbl2 o;
+  o.x = g == gc ? t0 : (g == n - 1 ? t1 : 0.0);
+  o.y = g == gc ? t1 : (g == -1 ? t0 : 0.0);
+  return o;
+}
 template <int OP>
 __device__ __forceinline__ dbl2 uni_x16(const double* __restrict__ x, int64_t g, int64_t n,
-                                        const Epi& ep) {
+                                        const Epi& ep, __amdgpu_buffer_rsrc_t rs) {
   if constexpr (OP == EPI_FADD)
     return t16(ep.agg, x, g, n);
+  else if constexpr (MLAMG_UNI_BUF)
+    return x16r(rs, (int)g, (int)n);
   else
     return x16(x, g, n);
 }
@@ -738,6 +753,9 @@ __device__ __forceinline__ int uni_k(const RpUni& U) {
 #ifndef MLAMG_UNI_WPE  // build-time A/B knob: minimum waves per SIMD for k_rowpat_uni (0: free)
 #define MLAMG_UNI_WPE 0
 #endif
+#ifndef MLAMG_UNI_BUF  // build-time A/B knob: x operands through a buffer resource with 32-bit
+#define MLAMG_UNI_BUF 1  // offsets (1) or flat 64-bit addresses (0): 74 -> 62 VGPRs (6 -> 8
+#endif                   // waves per SIMD), C4 A_0 cold 43.1 -> 41.9 us
 #ifndef MLAMG_UNI_PFA  // build-time A/B knob: with CH <= 2 chunks, every chunk's id and far
 #define MLAMG_UNI_PFA 1  // operands issued before the window staging (1), not one chunk ahead (0):
 #endif                   // C4 A_0 cold 45.0 -> 43.0 us, resid+norm 64 -> 52 us
@@ -763,6 +781,8 @@ void k_rowpat_uni(
   if constexpr (OP == EPI_RESID) x_op = ep.copy_to != nullptr && ep.copy_from == x;
   if constexpr (OP == EPI_FADD) x_op = true;  // t_i, t_i+1: the window's own pair
   const int K = uni_k<LY>(U);
+  const __amdgpu_buffer_rsrc_t rsx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(n_cols * 8), 0x00020000);
   const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
   const int64_t p0 = lb * CH * kThreads;  // the workgroup's first pair
   const int64_t T0 = 2 * p0 - U.halo;     // its first window row (even)
@@ -800,7 +820,7 @@ void k_rowpat_uni(
 #pragma unroll
     for (int t = 0; t < NF; ++t)
       fall[c][t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0}
-                                        : uni_x16<OP>(x, 2 * pc + MLAMG_FAR_OFF(t, pc), n_cols, ep);
+                                        : uni_x16<OP>(x, 2 * pc + MLAMG_FAR_OFF(t, pc), n_cols, ep, rsx);
   }
   int pcur = pall[0];
   dbl2 fcur[NFR];
@@ -818,7 +838,7 @@ void k_rowpat_uni(
 #pragma unroll
   for (int q = 0; q < WQ; ++q) {
     const int i = threadIdx.x + q * kThreads;
-    wv[q] = uni_x16<OP>(x, T0 + 2 * (int64_t)(i < nwin ? i : 0), n_cols, ep);
+    wv[q] = uni_x16<OP>(x, T0 + 2 * (int64_t)(i < nwin ? i : 0), n_cols, ep, rsx);
   }
 #pragma unroll
   for (int q = 0; q < WQ; ++q) {
@@ -866,7 +886,7 @@ void k_rowpat_uni(
 #pragma unroll
       for (int t = 0; t < NF; ++t)
         fnext[t] = (MLAMG_UNI_DBG & 4) ? dbl2{0.0, 0.0}
-                                       : uni_x16<OP>(x, 2 * prn + MLAMG_FAR_OFF(t, prn), n_cols, ep);
+                                       : uni_x16<OP>(x, 2 * prn + MLAMG_FAR_OFF(t, prn), n_cols, ep, rsx);
     }
     const int pl = c * kThreads + (int)threadIdx.x + hw;  // this pair's window slot
     const dbl2 xc = win[pl];
@@ -3364,7 +3384,8 @@ static int build_rowpat(mlamg_csr* A, hipStream_t s) {
         u.off[q] = o;
         u.kind[q] = kd;
       }
-      ok = ok && nfar <= kRpUniFar && A->n_cols >= 2;
+      // (n_cols < 2^28: the kernel's x offsets are 32-bit byte offsets, x16r)
+      ok = ok && nfar <= kRpUniFar && A->n_cols >= 2 && A->n_cols < (int64_t(1) << 28);
       u.k = ok ? (int32_t)offs.size() : 0;
       auto kinds_are = [&](std::initializer_list<int> ks) {
         if ((size_t)u.k != ks.size()) return false;
