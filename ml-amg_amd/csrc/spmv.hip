@@ -706,6 +706,9 @@ __device__ __forceinline__ dbl2 t16(const int32_t* __restrict__ agg, const doubl
   o.y = g == gc ? t1 : (g == -1 ? t0 : 0.0);
   return o;
 }
+#ifndef MLAMG_UNI_BUF  // build-time A/B knob: x operands through a buffer resource with 32-bit
+#define MLAMG_UNI_BUF 1  // offsets (1) or flat 64-bit addresses (0): 74 -> 62 VGPRs (6 -> 8
+#endif                   // waves per SIMD), C4 A_0 cold 43.1 -> 41.9 us (DESIGN.md §16)
 // x16 through a buffer resource with 32-bit index arithmetic (n * 8 < 2^31, checked where the
 // uniform form is built): no 64-bit address registers per load
 __device__ __forceinline__ dbl2 x16r(__amdgpu_buffer_rsrc_t rs, int g, int n) {
@@ -753,9 +756,6 @@ __device__ __forceinline__ int uni_k(const RpUni& U) {
 #ifndef MLAMG_UNI_WPE  // build-time A/B knob: minimum waves per SIMD for k_rowpat_uni (0: free)
 #define MLAMG_UNI_WPE 0
 #endif
-#ifndef MLAMG_UNI_BUF  // build-time A/B knob: x operands through a buffer resource with 32-bit
-#define MLAMG_UNI_BUF 1  // offsets (1) or flat 64-bit addresses (0): 74 -> 62 VGPRs (6 -> 8
-#endif                   // waves per SIMD), C4 A_0 cold 43.1 -> 41.9 us (DESIGN.md §16)
 #ifndef MLAMG_UNI_PFA  // build-time A/B knob: with CH <= 2 chunks, every chunk's id and far
 #define MLAMG_UNI_PFA 1  // operands issued before the window staging (1), not one chunk ahead (0):
 #endif                   // C4 A_0 cold 45.0 -> 43.0 us, resid+norm 64 -> 52 us
