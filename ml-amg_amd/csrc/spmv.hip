@@ -1734,6 +1734,9 @@ __device__ __forceinline__ void sum_two_rows(const double* __restrict__ p, int a
 // plus the block's distinct values, read as one contiguous stream and staged in the LDS the
 // products use later). The products and their order are those of the fp64 form, so every
 // mode computes the same bits.
+#ifndef MLAMG_SRT_BUF  // build-time A/B knob: x gathers through a buffer resource with 32-bit
+#define MLAMG_SRT_BUF 1  // offsets (a padded entry reads out of range, i.e. 0) and the 2-byte value
+#endif                   // codes packed two to a register: P_0 72-74.5 -> 69-70 us
 #ifndef MLAMG_SRT_WAVES  // minimum waves per SIMD the register allocation must allow (0: free)
 #define MLAMG_SRT_WAVES 0
 #endif
@@ -1772,18 +1775,26 @@ void k_sorted(const int32_t* __restrict__ indptr,
   // loads that depend on the record then wait for it alone)
   const int4 m0 = reinterpret_cast<const int4*>(base)[2 * b];
   const int4 m1 = reinterpret_cast<const int4*>(base)[2 * b + 1];
+  // SB: every in-range offset is below 2^31 (n_cols < 2^28, checked at build), the padding
+  // offset ~7 is above the record count and reads 0
+  const __amdgpu_buffer_rsrc_t rsx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, 0x7ffffff8, 0x00020000);
   constexpr int U = kSrtNnz / kSrtThreads;
   constexpr uint32_t kNone = 0xffffffffu, kSlot = (1u << kSrtPosBits) - 1;
   uint32_t w[U];
   double vv[U], xv[U];
-  int cv[VM == 2 ? U : 1];
+  constexpr bool SB = MLAMG_SRT_BUF != 0;
+  uint32_t cv[VM == 2 ? (SB ? U / 2 : U) : 1];  // SB: codes u and u + 1 in one register
   {
     const size_t eb = (size_t)b * kSrtNnz + tid;
     if (ep.cached) {  // uniform: one unrolled load sequence or the other
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         w[u] = pk[eb + u * kSrtThreads];
-        if constexpr (VM == 2)
+        if constexpr (VM == 2 && SB)
+          cv[u >> 1] = (u & 1) ? cv[u >> 1] | ((uint32_t)vc[eb + u * kSrtThreads] << 16)
+                               : (uint32_t)vc[eb + u * kSrtThreads];
+        else if constexpr (VM == 2)
           cv[u] = vc[eb + u * kSrtThreads];
         else if constexpr (VD)
           vv[u] = (double)vi[eb + u * kSrtThreads];  // index for now
@@ -1794,7 +1805,11 @@ void k_sorted(const int32_t* __restrict__ indptr,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         w[u] = __builtin_nontemporal_load(pk + eb + u * kSrtThreads);
-        if constexpr (VM == 2)
+        if constexpr (VM == 2 && SB)
+          cv[u >> 1] = (u & 1) ? cv[u >> 1] | ((uint32_t)__builtin_nontemporal_load(
+                                                   vc + eb + u * kSrtThreads) << 16)
+                               : (uint32_t)__builtin_nontemporal_load(vc + eb + u * kSrtThreads);
+        else if constexpr (VM == 2)
           cv[u] = __builtin_nontemporal_load(vc + eb + u * kSrtThreads);
         else if constexpr (VD)
           vv[u] = (double)__builtin_nontemporal_load(vi + eb + u * kSrtThreads);  // index for now
@@ -1836,7 +1851,12 @@ void k_sorted(const int32_t* __restrict__ indptr,
 #ifdef MLAMG_SRT_LAB_NOGATHER  // timing variant only (tools/p0r0_time.py): no x gathers
     xv[u] = (double)(cb + (int)(w[u] >> kSrtPosBits));
 #else
-    xv[u] = w[u] != kNone ? x[cb + (int)(w[u] >> kSrtPosBits)] : 0.0;
+    if constexpr (SB) {
+      const uint32_t off = w[u] != kNone ? (uint32_t)(cb + (int)(w[u] >> kSrtPosBits)) * 8u : ~7u;
+      xv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsx, off, 0, 0));
+    } else {
+      xv[u] = w[u] != kNone ? x[cb + (int)(w[u] >> kSrtPosBits)] : 0.0;
+    }
 #endif
   }
 #pragma unroll
@@ -1860,7 +1880,10 @@ void k_sorted(const int32_t* __restrict__ indptr,
     }
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < U; ++u) vv[u] = w[u] != kNone ? prod[cv[u]] : 0.0;
+    for (int u = 0; u < U; ++u) {
+      const int c = SB ? (int)((cv[u >> 1] >> (16 * (u & 1))) & 0xffffu) : (int)cv[u];
+      vv[u] = w[u] != kNone ? prod[c] : 0.0;
+    }
     __syncthreads();
   }
 #pragma unroll
@@ -2942,6 +2965,10 @@ static int pad_stream(T** arr, int nb, const int32_t* meta, T pad, hipStream_t s
 static int build_sorted(mlamg_csr* A, hipStream_t s, int value_mode = 0) {
   drop_sorted(A);
   const int64_t n = A->n_rows, nnz = A->nnz;
+  if (A->n_cols >= (int64_t(1) << 28)) {  // k_sorted's x offsets are 32-bit byte offsets
+    set_error("sorted format: more than 2^28 columns");
+    return MLAMG_EUNSUPPORTED;
+  }
   std::vector<int32_t> ip(n + 1);
   MLAMG_HIP(hipMemcpyAsync(ip.data(), A->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost, s));
   MLAMG_HIP(hipStreamSynchronize(s));
