@@ -982,7 +982,8 @@ def test_factored_prolongation_within_tolerance(ml, oracle, torch_cuda, dim, n1)
 @pytest.mark.parametrize("case,fmt", [("p3d", ("rowpat", 0)), ("p3d", ("sorted", 0)),
                                       ("p3d", ("sell", 1)), ("p3d", ("sell_dict", 1)),
                                       ("p3d", ("csr_stream", 0)), ("p2d_1536", ("csr_stream", 0)),
-                                      ("varcoef", ("sell", 512)), ("varcoef", ("sorted", 2))])
+                                      ("varcoef", ("sell", 512)), ("varcoef", ("sorted", 0)),
+                                      ("varcoef", ("sorted", 2))])
 def test_end_of_cycle_norm_same_bits(ml, torch_cuda, case, fmt):
     """The end-of-cycle norm of the fused cycle (the residual pass of t that also writes the next
     cycle's first sweep, MLAMG.py:194) is the norm mlamg_residual computes on the same iterate:
@@ -1002,9 +1003,10 @@ def test_end_of_cycle_norm_same_bits(ml, torch_cuda, case, fmt):
     try:
         H.levels[0].A.set_format(*fmt)
     except ml._lib.MlamgError as e:
-        if e.code == ml._lib.MLAMG_EUNSUPPORTED:
-            pytest.skip(f"{fmt} does not apply to {case}")
-        raise
+        # the per-block dictionary refuses random coefficients (more than half of a block's
+        # values distinct): that refusal is the expected outcome, and the only one
+        assert e.code == ml._lib.MLAMG_EUNSUPPORTED and (case, fmt) == ("varcoef", ("sorted", 2)), e
+        return
     H.attach_dinvs()
     rng = np.random.RandomState(3)
     b = dev(torch, rng.randn(n))
